@@ -1,0 +1,276 @@
+/*
+ * orbx.h -- C ABI of the MI355X-native ORB-SLAM front end + local-BA kernels.
+ *
+ * Every entry point below replaces one reference interface on the hot path
+ * named by BASELINE.json's north_star.  The reference is
+ * a single C++ executable with no FFI layer, so the "binding" is a C++ adapter
+ * (orb_slam_amd/adapters/, shown in INTEGRATION.md) that keeps the reference
+ * class signatures and calls these functions.  Signatures use plain pointers
+ * and sizes only; all device memory is owned by an orbx_ctx.
+ *
+ * Conventions
+ *   - return 0 (ORBX_OK) on success, a negative ORBX_ERR_* code otherwise.
+ *     The reference has no error codes (it asserts or returns silently); the
+ *     adapter maps codes back to that behaviour.
+ *   - host pointers are caller-allocated; "cap" arguments bound outputs.
+ *   - an orbx_ctx owns one HIP stream and its buffers; it is NOT thread-safe
+ *     (mirrors ORBextractor, whose pyramid is member state:
+ *     include/ORBextractor.h:74).  Use one context per calling thread.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBX_OK               0
+#define ORBX_ERR_ARG         -1  /* invalid argument / shape                      */
+#define ORBX_ERR_HIP         -2  /* HIP runtime failure (device missing, launch)  */
+#define ORBX_ERR_CAPACITY    -3  /* caller buffer or context capacity too small   */
+#define ORBX_ERR_UNSUPPORTED -4  /* configuration outside the implemented subset  */
+#define ORBX_ERR_NOMEM       -5  /* device or host allocation failed              */
+#define ORBX_ERR_NOT_POSDEF  -6  /* reduced camera system not positive definite   */
+
+/* cv::KeyPoint layout (OpenCV 2.4 core/types.hpp): 28 bytes. */
+typedef struct {
+    float x, y;        /* pt                                 */
+    float size;        /* diameter of the meaningful region  */
+    float angle;       /* degrees in [0,360)                 */
+    float response;    /* FAST score                         */
+    int32_t octave;    /* pyramid level                      */
+    int32_t class_id;  /* always -1                          */
+} orbx_keypoint;
+
+typedef struct orbx_ctx orbx_ctx;
+
+/* ------------------------------------------------------------------------ */
+/* Context / extractor construction                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces ORBextractor::ORBextractor(int nfeatures, float scaleFactor,
+ * int nlevels, int scoreType, int fastTh)  (src/ORBextractor.cc:457-511,
+ * include/ORBextractor.h:37).  max_w/max_h/max_batch size the device
+ * buffers (frames larger than max_w x max_h are rejected); max_batch is the
+ * number of frames one batched launch may carry and also the number of
+ * device-resident frame slots available to orbx_dev_* (see below).
+ * score_type: 1 = FAST_SCORE (implemented), 0 = HARRIS_SCORE (unsupported). */
+int  orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor,
+                 int nlevels, int score_type, int fast_th,
+                 int max_w, int max_h, int max_batch);
+void orbx_destroy(orbx_ctx* ctx);
+
+/* ORBextractor::GetLevels / GetScaleFactor (include/ORBextractor.h:47-51). */
+int   orbx_get_levels(const orbx_ctx* ctx);
+float orbx_get_scale_factor(const orbx_ctx* ctx);
+/* mnFeaturesPerLevel (src/ORBextractor.cc:476-487) and mvScaleFactor. */
+int   orbx_get_features_per_level(const orbx_ctx* ctx, int32_t* out, int cap);
+int   orbx_get_scale_factors(const orbx_ctx* ctx, float* out, int cap);
+
+/* ------------------------------------------------------------------------ */
+/* A. Extraction                                                             */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces ORBextractor::operator()(image, mask=Mat(), keypoints, descriptors)
+ * (src/ORBextractor.cc:718-779).  img: w x h mono8 with row stride `stride`.
+ * Outputs keypoints in reference order (level-major, retainBest order within
+ * a level; coordinates scaled to level 0) and N x 32 descriptor bytes.
+ * An empty image (w==0 || h==0) returns ORBX_OK with *n_out = 0 -- the
+ * reference returns without touching its outputs (:721-722). */
+int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
+                 orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+
+/* Batched form: B frames of identical size, host in / host out.
+ * kps: B*cap records, desc: B*cap*32 bytes, n_out: B counts. */
+int orbx_extract_batch(orbx_ctx* ctx, int B, const uint8_t* const* imgs,
+                       int w, int h, size_t stride,
+                       orbx_keypoint* kps, uint8_t* desc, int cap, int32_t* n_out);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident pipeline (inputs already in HBM; used by bench/tests).     */
+/* A context owns `max_batch` frame slots.  Frames are uploaded once, then    */
+/* extracted and matched without host round-trips.                            */
+/* ------------------------------------------------------------------------ */
+
+/* Copy `count` host frames (w x h, contiguous rows of `stride` bytes, frame k
+ * at imgs + k*h*stride) into slots [first, first+count).  All slots of one
+ * context share one frame size (set by the first upload). */
+int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
+                    int w, int h, size_t stride);
+/* Extract slots [first, first+count) (async, on the context stream). */
+int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
+/* SearchForInitialization (B3) for slots [first, first+count): slot s is
+ * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
+ * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */
+int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len,
+                        int window, float nnratio, int check_ori);
+int orbx_dev_sync(orbx_ctx* ctx);
+/* Read back one slot's features / its match result (after sync). */
+int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps,
+                           uint8_t* desc, int cap, int* n_out);
+int orbx_dev_read_matches(orbx_ctx* ctx, int slot, int32_t* matches12, int cap,
+                          int* n_matches, int* n1);
+/* Timing of the dominant kernels over the launches issued since the last
+ * reset, measured with hipEvents on the context stream.  name: "fast",
+ * "retain", "pyramid", "blur", "describe", "match".  Returns the number of
+ * timed launches; *avg_ms receives the mean duration. */
+int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms,
+                         double* total_ms);
+int orbx_dev_kernel_time_enable(orbx_ctx* ctx, int enable);
+
+/* Debug / parity taps: padded pyramid level (raw or blurred) of a slot.
+ * Writes (w_l+32)*(h_l+32) bytes; *pw, *ph receive the padded size. */
+int orbx_dev_read_level(orbx_ctx* ctx, int slot, int level, int blurred,
+                        uint8_t* out, int cap, int* pw, int* ph);
+
+/* ------------------------------------------------------------------------ */
+/* B. Matching                                                               */
+/* ------------------------------------------------------------------------ */
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1794-1810), host side. */
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Frame view consumed by the matchers: mvKeysUn, mDescriptors, image bounds
+ * (Frame::ComputeImageBounds, src/Frame.cc:320-348) and the scale pyramid
+ * (mvScaleFactors, src/Frame.cc:94-102).  The 64x48 cell grid
+ * (src/Frame.cc:108-122) is rebuilt on the device from keys_un. */
+typedef struct {
+    const orbx_keypoint* keys_un;
+    const uint8_t* desc;          /* n x 32 */
+    int n;
+    float min_x, max_x, min_y, max_y;
+    int nlevels;
+    float scale_factor;
+} orbx_frame_view;
+
+/* All-pairs Hamming (B8 primitive): for every row a of dA, the first index of
+ * the smallest distance over dB, that distance and the second smallest value
+ * of the multiset of distances (reference best/second rule, ORBmatcher.cc:
+ * 640-649).  Distances are DescriptorDistance. */
+int orbx_hamming_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB,
+                    int nB, int32_t* best_idx, int32_t* best, int32_t* second);
+/* Brute-force matcher (C3): best/second rule + accept best <= th_low and
+ * best < nnratio*second.  m12[a] = matched b or -1. */
+int orbx_match_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB,
+                  int nB, int th_low, float nnratio, int32_t* m12, int* n_matches);
+
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:598-713).
+ * prev_matched: 2*F1->n floats (vbPrevMatched), updated in place.
+ * matches12: F1->n entries (vnMatches12). */
+int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1,
+                                   const orbx_frame_view* F2, float* prev_matched,
+                                   int32_t* matches12, int window, float nnratio,
+                                   int check_ori, int* n_matches);
+
+/* ORBmatcher::WindowSearch (src/ORBmatcher.cc:409-516).
+ * f1_mp: per F1 keypoint, 1 if F1.mvpMapPoints[i1] is set and not bad.
+ * matches21 (out, F2->n): i1 whose map point was assigned to F2 keypoint i2,
+ * or -1 (vpMapPointMatches2 / vnMatches21).  max_level < 0 means INT_MAX. */
+int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1,
+                       const orbx_frame_view* F2, const uint8_t* f1_mp,
+                       int window, int min_level, int max_level, float nnratio,
+                       int check_ori, int32_t* matches21, int* n_matches);
+
+/* ORBmatcher::SearchByProjection(Frame& F1, Frame& F2, int windowSize,
+ * vector<MapPoint*>&) (src/ORBmatcher.cc:519-594).
+ * f1_mp_xyz: 3 floats per F1 keypoint (world position of its map point);
+ * f1_mp_valid: 1 if the point exists, is not bad and is not already in F2
+ * (spMapPointsAlreadyFound).  f2_assigned (in): F2.mvpMapPoints non-null.
+ * Tcw2: F2 pose, 12 floats row-major [R|t].  cam: fx, fy, cx, cy.
+ * matches21 (out): F1 index assigned to each F2 keypoint or -1 (new only). */
+int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1,
+                                   const orbx_frame_view* F2,
+                                   const float* f1_mp_xyz, const uint8_t* f1_mp_valid,
+                                   const uint8_t* f2_assigned, const float* Tcw2,
+                                   const float* cam, int window, float nnratio,
+                                   int32_t* matches21, int* n_matches);
+
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame,
+ * float th) (src/ORBmatcher.cc:1507-1620), motion-model tracking.
+ * last_mp_xyz / last_mp_valid: per LastFrame keypoint (pMP && !mvbOutlier).
+ * cur_assigned (in): CurrentFrame.mvpMapPoints non-null.
+ * matches_cur (out, Cur->n): LastFrame index assigned to each current
+ * keypoint by this call, or -1. */
+int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur,
+                                     const orbx_frame_view* Last,
+                                     const float* last_mp_xyz,
+                                     const uint8_t* last_mp_valid,
+                                     const uint8_t* cur_assigned, const float* Tcw,
+                                     const float* cam, float th, int check_ori,
+                                     int32_t* matches_cur, int* n_matches);
+
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, float th)
+ * (src/ORBmatcher.cc:49-125), local-map tracking.  Per map point m (n_mp):
+ * in_view (mbTrackInView && !isBad), proj_xy (mTrackProjX/Y), pred_level
+ * (mnTrackScaleLevel), view_cos (mTrackViewCos), mp_desc (32 B).
+ * f_assigned (in): F.mvpMapPoints non-null.  matches_f (out, F->n): index of
+ * the map point assigned to each keypoint by this call, or -1. */
+int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F,
+                                    int n_mp, const uint8_t* in_view,
+                                    const float* proj_xy, const int32_t* pred_level,
+                                    const float* view_cos, const uint8_t* mp_desc,
+                                    const uint8_t* f_assigned, float th, float nnratio,
+                                    int32_t* matches_f, int* n_matches);
+
+/* ------------------------------------------------------------------------ */
+/* C. Local bundle adjustment                                                */
+/* ------------------------------------------------------------------------ */
+
+/* SoA local-BA problem (Optimizer::LocalBundleAdjustment, src/Optimizer.cc:
+ * 287-536).  Poses are SE3Quat (g2o se3quat.h) as unit quaternion (x,y,z,w)
+ * + translation; ids are the g2o vertex ids (KF mnId; points mnId+maxKFid+1)
+ * which fix the Hessian ordering (sparse_optimizer.cpp:166-190, 482-487).
+ * Edges are EdgeSE3ProjectXYZ in insertion order (points in local-list order,
+ * observations in the caller's map<KeyFrame*,size_t> order). */
+typedef struct {
+    int n_poses, n_points, n_edges;
+    double* pose_q;             /* [n_poses][4] x,y,z,w   (in/out)           */
+    double* pose_t;             /* [n_poses][3]           (in/out)           */
+    const uint8_t* pose_fixed;  /* [n_poses]                                  */
+    const int64_t* pose_id;     /* [n_poses] g2o vertex id                    */
+    const double* pose_cam;     /* [n_poses][4] fx, fy, cx, cy                */
+    double* points;             /* [n_points][3]          (in/out)           */
+    const int64_t* point_id;    /* [n_points]                                 */
+    const int32_t* point_nobs;  /* [n_points] MapPoint::Observations() at call*/
+    const int32_t* edge_point;  /* [n_edges] index into points                */
+    const int32_t* edge_pose;   /* [n_edges] index into poses                 */
+    const double* edge_obs;     /* [n_edges][2] undistorted keypoint          */
+    const double* edge_inv_sigma2; /* [n_edges] information = I * invSigma2   */
+    double huber_delta;         /* sqrt(5.991) as float, widened              */
+    double chi2_threshold;      /* 5.991                                      */
+} orbx_ba_problem;
+
+typedef struct {
+    int iterations[2];          /* LM iterations executed per optimize() call */
+    int levenberg_trials[2];    /* inner LM trials summed                     */
+    double chi2_initial[2];     /* robust chi2 at the first linearisation     */
+    double chi2_final[2];       /* robust chi2 of the accepted state          */
+    int n_outliers[2];          /* edges erased by each outlier pass          */
+    int not_posdef;             /* Cholesky failures (step rejected)          */
+} orbx_ba_stats;
+
+/* Runs optimize(iters0), the first outlier pass (edge erased and removed from
+ * the graph), optimize(iters1) and the second outlier pass.  edge_status
+ * (out, n_edges): 0 inlier, 1 erased in pass 1, 2 erased in pass 2.
+ * point_bad (out, n_points): MapPoint became bad through EraseObservation.
+ * abort: polled between LM iterations (mbAbortBA; may be NULL). */
+int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
+                   const volatile uint8_t* abort, uint8_t* edge_status,
+                   uint8_t* point_bad, orbx_ba_stats* stats);
+
+/* Batched throughput form: P independent problems, one workgroup each. */
+int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems,
+                         int iters0, int iters1, uint8_t* const* edge_status,
+                         uint8_t* const* point_bad, orbx_ba_stats* stats);
+
+/* Library identification. */
+const char* orbx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBX_H */

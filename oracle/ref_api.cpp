@@ -1,0 +1,247 @@
+// ORACLE -- TEST INFRASTRUCTURE ONLY (see ref_common.h).
+//
+// extern "C" surface of the CPU restatement, loaded by tests/ and bench.py
+// (cpu_baseline) through ctypes.  Mirrors include/orbx.h with an orbx_ref_
+// prefix; frame/keypoint structs are the public ABI ones.
+#include "ref_common.h"
+#include "../include/orbx.h"
+
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <memory>
+
+using namespace orbref;
+
+extern "C" {
+
+struct orbx_ref_extractor {
+    std::unique_ptr<ORBextractorRef> ex;
+};
+
+orbx_ref_extractor* orbx_ref_extractor_create(int nfeatures, float scale, int nlevels,
+                                              int score_type, int fast_th)
+{
+    if (nfeatures <= 0 || nlevels <= 0 || nlevels > 32 || !(scale > 1.0f) || score_type != 1)
+        return nullptr;
+    auto* r = new orbx_ref_extractor;
+    r->ex.reset(new ORBextractorRef(nfeatures, scale, nlevels, score_type, fast_th));
+    return r;
+}
+
+void orbx_ref_extractor_destroy(orbx_ref_extractor* r) { delete r; }
+
+int orbx_ref_extract(orbx_ref_extractor* r, const uint8_t* img, int w, int h, size_t stride,
+                     orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out)
+{
+    try {
+        std::vector<KeyPoint> k;
+        std::vector<uint8_t> d;
+        if (!r->ex->extract(img, w, h, stride, k, d)) {
+            *n_out = 0;
+            return ORBX_OK;
+        }
+        *n_out = (int)k.size();
+        if ((int)k.size() > cap) return ORBX_ERR_CAPACITY;
+        std::memcpy(kps, k.data(), k.size() * sizeof(KeyPoint));
+        std::memcpy(desc, d.data(), d.size());
+        return ORBX_OK;
+    } catch (const std::exception&) {
+        return ORBX_ERR_UNSUPPORTED;
+    }
+}
+
+// Debug tap: padded level (raw or blurred) of the last extract() call.
+int orbx_ref_level(orbx_ref_extractor* r, int level, int blurred, uint8_t* out, int cap,
+                   int* pw, int* ph)
+{
+    auto& v = blurred ? r->ex->blurred : r->ex->pyramid;
+    if (level < 0 || level >= (int)v.size()) return ORBX_ERR_ARG;
+    const PaddedImage& L = v[level];
+    *pw = L.pw;
+    *ph = L.ph;
+    if ((int)L.buf.size() > cap) return ORBX_ERR_CAPACITY;
+    std::memcpy(out, L.buf.data(), L.buf.size());
+    return ORBX_OK;
+}
+
+// Debug tap: level keypoints (level coordinates, pre-scaling) of the last call.
+int orbx_ref_level_keys(orbx_ref_extractor* r, int level, orbx_keypoint* out, int cap, int* n)
+{
+    if (level < 0 || level >= (int)r->ex->levelKeys.size()) return ORBX_ERR_ARG;
+    const auto& v = r->ex->levelKeys[level];
+    *n = (int)v.size();
+    if ((int)v.size() > cap) return ORBX_ERR_CAPACITY;
+    std::memcpy(out, v.data(), v.size() * sizeof(KeyPoint));
+    return ORBX_OK;
+}
+
+int orbx_ref_features_per_level(orbx_ref_extractor* r, int32_t* out, int cap)
+{
+    const auto& v = r->ex->mnFeaturesPerLevel;
+    for (int i = 0; i < (int)v.size() && i < cap; i++) out[i] = v[i];
+    return (int)v.size();
+}
+
+int orbx_ref_umax(orbx_ref_extractor* r, int32_t* out, int cap)
+{
+    const auto& v = r->ex->umax;
+    for (int i = 0; i < (int)v.size() && i < cap; i++) out[i] = v[i];
+    return (int)v.size();
+}
+
+int orbx_ref_scale_factors(orbx_ref_extractor* r, float* out, float* inv, int cap)
+{
+    const int n = r->ex->nlevels;
+    for (int i = 0; i < n && i < cap; i++) {
+        out[i] = r->ex->mvScaleFactor[i];
+        inv[i] = r->ex->mvInvScaleFactor[i];
+    }
+    return n;
+}
+
+// Times `iters` extract() calls on one core; returns seconds.
+double orbx_ref_time_extract(orbx_ref_extractor* r, const uint8_t* imgs, int nimg, int w, int h,
+                             size_t stride, int iters)
+{
+    std::vector<KeyPoint> k;
+    std::vector<uint8_t> d;
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; i++)
+        r->ex->extract(imgs + (size_t)(i % nimg) * h * stride, w, h, stride, k, d);
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// ---- primitives ----
+float orbx_ref_fast_atan2(float y, float x) { return fast_atan2_cv24(y, x); }
+float orbx_ref_cosf(float x) { return cr_cosf(x); }
+float orbx_ref_sinf(float x) { return cr_sinf(x); }
+int orbx_ref_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
+
+int orbx_ref_fast_cell(const uint8_t* img, int step, int rows, int cols, int threshold,
+                       orbx_keypoint* out, int cap, int* n)
+{
+    std::vector<KeyPoint> k;
+    cv24_fast16(img, step, rows, cols, threshold, true, k);
+    *n = (int)k.size();
+    if ((int)k.size() > cap) return ORBX_ERR_CAPACITY;
+    std::memcpy(out, k.data(), k.size() * sizeof(KeyPoint));
+    return ORBX_OK;
+}
+
+int orbx_ref_resize(const uint8_t* src, int sstep, int sw, int sh, uint8_t* dst, int dstep,
+                    int dw, int dh)
+{
+    try {
+        cv24_resize_linear_u8(src, sstep, sw, sh, dst, dstep, dw, dh);
+        return ORBX_OK;
+    } catch (const std::exception&) {
+        return ORBX_ERR_UNSUPPORTED;
+    }
+}
+
+// retainBest over a list of responses; writes the surviving original indices.
+int orbx_ref_retain_best(const float* responses, int n, int n_points, int32_t* out_idx)
+{
+    std::vector<KeyPoint> k(n);
+    for (int i = 0; i < n; i++) {
+        std::memset(&k[i], 0, sizeof(KeyPoint));
+        k[i].response = responses[i];
+        k[i].class_id = i;
+    }
+    cv24_retain_best(k, n_points);
+    if ((int)k.size() > n_points && n_points >= 0) k.resize(n_points);
+    for (size_t i = 0; i < k.size(); i++) out_idx[i] = k[i].class_id;
+    return (int)k.size();
+}
+
+// ---- matchers ----
+static void to_frame(const orbx_frame_view* v, FrameRef& F)
+{
+    F.build(reinterpret_cast<const KeyPoint*>(v->keys_un), v->desc, v->n, v->min_x, v->max_x,
+            v->min_y, v->max_y, v->nlevels, v->scale_factor);
+}
+
+int orbx_ref_search_for_initialization(const orbx_frame_view* F1v, const orbx_frame_view* F2v,
+                                       float* prev_matched, int32_t* matches12, int window,
+                                       float nnratio, int check_ori, int* n_matches)
+{
+    static thread_local FrameRef F1, F2;
+    to_frame(F1v, F1);
+    to_frame(F2v, F2);
+    std::vector<float> pm(prev_matched, prev_matched + 2 * F1v->n);
+    std::vector<int> m;
+    *n_matches = search_for_initialization(F1, F2, pm, m, window, nnratio, check_ori != 0);
+    std::memcpy(prev_matched, pm.data(), pm.size() * sizeof(float));
+    for (int i = 0; i < F1v->n; i++) matches12[i] = m[i];
+    return ORBX_OK;
+}
+
+int orbx_ref_window_search(const orbx_frame_view* F1v, const orbx_frame_view* F2v,
+                           const uint8_t* f1_mp, int window, int min_level, int max_level,
+                           float nnratio, int check_ori, int32_t* matches21, int* n_matches)
+{
+    static thread_local FrameRef F1, F2;
+    to_frame(F1v, F1);
+    to_frame(F2v, F2);
+    std::vector<int> m;
+    *n_matches = window_search(F1, F2, f1_mp, window, min_level, max_level < 0 ? 2147483647 : max_level,
+                               nnratio, check_ori != 0, m);
+    for (int i = 0; i < F2v->n; i++) matches21[i] = m[i];
+    return ORBX_OK;
+}
+
+int orbx_ref_search_by_projection_pair(const orbx_frame_view* F1v, const orbx_frame_view* F2v,
+                                       const float* xyz, const uint8_t* valid,
+                                       const uint8_t* f2_assigned, const float* Tcw,
+                                       const float* cam, int window, float nnratio,
+                                       int32_t* matches21, int* n_matches)
+{
+    static thread_local FrameRef F1, F2;
+    to_frame(F1v, F1);
+    to_frame(F2v, F2);
+    std::vector<int> m;
+    *n_matches = search_by_projection_pair(F1, F2, xyz, valid, f2_assigned, Tcw, cam, window, nnratio, m);
+    for (int i = 0; i < F2v->n; i++) matches21[i] = m[i];
+    return ORBX_OK;
+}
+
+int orbx_ref_search_by_projection_motion(const orbx_frame_view* Cv, const orbx_frame_view* Lv,
+                                         const float* xyz, const uint8_t* valid,
+                                         const uint8_t* cur_assigned, const float* Tcw,
+                                         const float* cam, float th, int check_ori,
+                                         int32_t* matches_cur, int* n_matches)
+{
+    static thread_local FrameRef C, L;
+    to_frame(Cv, C);
+    to_frame(Lv, L);
+    std::vector<int> m;
+    *n_matches = search_by_projection_motion(C, L, xyz, valid, cur_assigned, Tcw, cam, th, check_ori != 0, m);
+    for (int i = 0; i < Cv->n; i++) matches_cur[i] = m[i];
+    return ORBX_OK;
+}
+
+int orbx_ref_search_by_projection_local(const orbx_frame_view* Fv, int n_mp, const uint8_t* in_view,
+                                        const float* proj_xy, const int32_t* pred_level,
+                                        const float* view_cos, const uint8_t* mp_desc,
+                                        const uint8_t* f_assigned, float th, float nnratio,
+                                        int32_t* matches_f, int* n_matches)
+{
+    static thread_local FrameRef F;
+    to_frame(Fv, F);
+    std::vector<int> m;
+    *n_matches = search_by_projection_local(F, n_mp, in_view, proj_xy, pred_level, view_cos, mp_desc,
+                                            f_assigned, th, nnratio, m);
+    for (int i = 0; i < Fv->n; i++) matches_f[i] = m[i];
+    return ORBX_OK;
+}
+
+int orbx_ref_hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
+                        int32_t* best, int32_t* second)
+{
+    hamming_bf(dA, nA, dB, nB, best_idx, best, second);
+    return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,223 @@
+"""orb_slam_amd -- MI355X-native ORB-SLAM front end and local-BA kernels.
+
+Python view of liborbx (include/orbx.h), used by tests and bench.py.  The
+product is the C ABI + HIP kernels in orb_slam_amd/csrc; the production
+binding is the C++ adapter in orb_slam_amd/adapters.
+
+There is no CPU fallback: if liborbx.so is missing or no GPU is visible, the
+entry points raise.
+"""
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "liborbx.so"
+
+ORBX_OK = 0
+ERRORS = {-1: "ORBX_ERR_ARG", -2: "ORBX_ERR_HIP", -3: "ORBX_ERR_CAPACITY",
+          -4: "ORBX_ERR_UNSUPPORTED", -5: "ORBX_ERR_NOMEM", -6: "ORBX_ERR_NOT_POSDEF"}
+
+# cv::KeyPoint / orbx_keypoint (28 bytes)
+KEYPOINT = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT.itemsize == 28
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code, where):
+        super().__init__(f"{where}: {ERRORS.get(code, code)}")
+        self.code = code
+
+
+class FrameView(ctypes.Structure):
+    _fields_ = [("keys_un", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("n", ctypes.c_int),
+                ("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("nlevels", ctypes.c_int), ("scale_factor", ctypes.c_float)]
+
+
+_lib = None
+
+
+def lib():
+    """Load liborbx.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise OrbxError(-2, f"liborbx.so missing at {LIB_PATH}; run python -m orb_slam_amd.build")
+        _lib = ctypes.CDLL(str(LIB_PATH))
+        _declare(_lib)
+    return _lib
+
+
+def _declare(L):
+    vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    ip = ctypes.POINTER(ctypes.c_int)
+    dp = ctypes.POINTER(ctypes.c_double)
+    sigs = {
+        "orbx_create": ([ctypes.POINTER(vp), i, i, f, i, i, i, i, i, i], i),
+        "orbx_destroy": ([vp], None),
+        "orbx_get_levels": ([vp], i),
+        "orbx_get_scale_factor": ([vp], f),
+        "orbx_get_features_per_level": ([vp, vp, i], i),
+        "orbx_get_scale_factors": ([vp, vp, i], i),
+        "orbx_extract": ([vp, vp, i, i, sz, vp, vp, i, ip], i),
+        "orbx_extract_batch": ([vp, i, vp, i, i, sz, vp, vp, i, vp], i),
+        "orbx_dev_upload": ([vp, i, i, vp, i, i, sz], i),
+        "orbx_dev_extract": ([vp, i, i], i),
+        "orbx_dev_match_prev": ([vp, i, i, i, i, f, i], i),
+        "orbx_dev_sync": ([vp], i),
+        "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
+        "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
+        "orbx_dev_kernel_time": ([vp, ctypes.c_char_p, dp, dp], i),
+        "orbx_dev_kernel_time_enable": ([vp, i], i),
+        "orbx_dev_read_level": ([vp, i, i, i, vp, i, ip, ip], i),
+        "orbx_descriptor_distance": ([vp, vp], i),
+        "orbx_hamming_bf": ([vp, vp, i, vp, i, vp, vp, vp], i),
+        "orbx_match_bf": ([vp, vp, i, vp, i, i, f, vp, ip], i),
+        "orbx_search_for_initialization": ([vp, vp, vp, vp, vp, i, f, i, ip], i),
+        "orbx_window_search": ([vp, vp, vp, vp, i, i, i, f, i, vp, ip], i),
+        "orbx_search_by_projection_pair": ([vp, vp, vp, vp, vp, vp, vp, vp, i, f, vp, ip], i),
+        "orbx_search_by_projection_motion": ([vp, vp, vp, vp, vp, vp, vp, vp, f, i, vp, ip], i),
+        "orbx_search_by_projection_local": ([vp, vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, ip], i),
+        "orbx_lba_solve": ([vp, vp, i, i, vp, vp, vp, vp], i),
+        "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp], i),
+        "orbx_version": ([], ctypes.c_char_p),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(code, where):
+    if code != ORBX_OK:
+        raise OrbxError(code, where)
+
+
+class Context:
+    """An orbx_ctx: one device, one HIP stream, `slots` device frame slots.
+
+    Mirrors ORB_SLAM::ORBextractor(nfeatures, scaleFactor, nlevels,
+    scoreType, fastTh) (include/ORBextractor.h:37) plus the batched,
+    device-resident pipeline.
+    """
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, score_type=1, fast_th=20,
+                 max_w=640, max_h=480, slots=1, device=0):
+        self._h = ctypes.c_void_p()
+        self.nfeatures = nfeatures
+        self.slots = slots
+        _check(lib().orbx_create(ctypes.byref(self._h), device, nfeatures, scale_factor, nlevels,
+                                 score_type, fast_th, max_w, max_h, slots), "orbx_create")
+
+    def close(self):
+        if self._h:
+            lib().orbx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- ORBextractor API -------------------------------------------------
+    def GetLevels(self):
+        return lib().orbx_get_levels(self._h)
+
+    def GetScaleFactor(self):
+        return lib().orbx_get_scale_factor(self._h)
+
+    def features_per_level(self):
+        out = np.zeros(64, np.int32)
+        n = lib().orbx_get_features_per_level(self._h, _ptr(out), 64)
+        return out[:n]
+
+    def __call__(self, image, mask=None):
+        """ORBextractor::operator()(image, mask, keypoints, descriptors)."""
+        if mask is not None and np.asarray(mask).size:
+            raise OrbxError(-4, "masked extraction (the reference never passes a mask)")
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape if img.ndim == 2 else (0, 0)
+        kps = np.zeros(self.nfeatures, KEYPOINT)
+        desc = np.zeros((self.nfeatures, 32), np.uint8)
+        n = ctypes.c_int(0)
+        _check(lib().orbx_extract(self._h, _ptr(img) if img.size else None, w, h, w, _ptr(kps),
+                                  _ptr(desc), self.nfeatures, ctypes.byref(n)), "orbx_extract")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    # --- device-resident pipeline ------------------------------------------
+    def upload(self, frames, first=0):
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        if frames.ndim == 2:
+            frames = frames[None]
+        cnt, h, w = frames.shape
+        _check(lib().orbx_dev_upload(self._h, first, cnt, _ptr(frames), w, h, w), "orbx_dev_upload")
+
+    def extract(self, first, count):
+        _check(lib().orbx_dev_extract(self._h, first, count), "orbx_dev_extract")
+
+    def match_prev(self, first, count, seq_len, window=100, nnratio=0.9, check_ori=True):
+        _check(lib().orbx_dev_match_prev(self._h, first, count, seq_len, window, nnratio,
+                                         int(check_ori)), "orbx_dev_match_prev")
+
+    def sync(self):
+        _check(lib().orbx_dev_sync(self._h), "orbx_dev_sync")
+
+    def features(self, slot):
+        kps = np.zeros(self.nfeatures, KEYPOINT)
+        desc = np.zeros((self.nfeatures, 32), np.uint8)
+        n = ctypes.c_int(0)
+        _check(lib().orbx_dev_read_features(self._h, slot, _ptr(kps), _ptr(desc), self.nfeatures,
+                                            ctypes.byref(n)), "orbx_dev_read_features")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def matches(self, slot):
+        m = np.zeros(self.nfeatures, np.int32)
+        nm, n1 = ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().orbx_dev_read_matches(self._h, slot, _ptr(m), self.nfeatures, ctypes.byref(nm),
+                                           ctypes.byref(n1)), "orbx_dev_read_matches")
+        return m, nm.value
+
+    def level(self, slot, level, blurred=False, cap=4 << 20):
+        buf = np.zeros(cap, np.uint8)
+        pw, ph = ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().orbx_dev_read_level(self._h, slot, level, int(blurred), _ptr(buf), cap,
+                                         ctypes.byref(pw), ctypes.byref(ph)), "orbx_dev_read_level")
+        return buf[:pw.value * ph.value].reshape(ph.value, pw.value).copy()
+
+    def timing(self, enable=True):
+        _check(lib().orbx_dev_kernel_time_enable(self._h, int(enable)), "timing")
+
+    def kernel_time(self, name):
+        avg, tot = ctypes.c_double(0), ctypes.c_double(0)
+        n = lib().orbx_dev_kernel_time(self._h, name.encode(), ctypes.byref(avg), ctypes.byref(tot))
+        if n < 0:
+            raise OrbxError(n, "orbx_dev_kernel_time")
+        return n, avg.value, tot.value
+
+    @property
+    def handle(self):
+        return self._h
+
+
+def frame_view(kps, desc, w, h, nlevels=8, scale_factor=1.2):
+    """orbx_frame_view over numpy keypoints/descriptors (Frame without
+    distortion: bounds 0..w, 0..h, src/Frame.cc:341-347).  Keep the arrays
+    alive while the view is used."""
+    v = FrameView()
+    v.keys_un = kps.ctypes.data
+    v.desc = desc.ctypes.data
+    v.n = len(kps)
+    v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(w), 0.0, float(h)
+    v.nlevels = nlevels
+    v.scale_factor = scale_factor
+    return v

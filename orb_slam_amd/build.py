@@ -1,0 +1,73 @@
+"""Build liborbx.so (HIP kernels + C ABI) in-tree for gfx950.
+
+Usage: python -m orb_slam_amd.build  (or orb_slam_amd.build.build()).
+Compiles every orb_slam_amd/csrc/*.hip and *.cpp with hipcc in parallel and
+links orb_slam_amd/liborbx.so.  Objects go to orb_slam_amd/build/ and are
+rebuilt only when a source or header is newer.
+"""
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "build"
+LIB = PKG / "liborbx.so"
+ARCH = os.environ.get("ORBX_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+          "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value",
+          f"-I{PKG.parent / 'include'}", f"-I{CSRC}"]
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build liborbx)")
+
+
+def _needs(obj, src, headers):
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+
+
+def build(verbose=False, jobs=None):
+    cc = hipcc()
+    OBJ.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) + [PKG.parent / "include" / "orbx.h"]
+    srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
+    cmds = []
+    objs = []
+    for s in srcs:
+        o = OBJ / (s.name + ".o")
+        objs.append(o)
+        if _needs(o, s, headers):
+            lang = ["-x", "hip", f"--offload-arch={ARCH}"] if s.suffix == ".hip" else ["-D__HIP_PLATFORM_AMD__"]
+            cmds.append([cc, *lang, *COMMON, "-c", str(s), "-o", str(o)])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+        return p.stderr
+
+    with cf.ThreadPoolExecutor(max_workers=jobs or min(8, os.cpu_count() or 4)) as ex:
+        for err in ex.map(run, cmds):
+            if err and verbose:
+                print(err, file=sys.stderr)
+    if cmds or not LIB.exists():
+        link = [cc, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)]
+        run(link)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

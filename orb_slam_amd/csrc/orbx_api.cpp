@@ -1,0 +1,419 @@
+// C ABI of liborbx (include/orbx.h): context lifetime, device buffers,
+// host <-> HBM transfers, kernel timing, and the drop-in entry points that
+// replace ORBextractor::operator() / ORBmatcher / Optimizer calls.
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "orbx_internal.h"
+
+using namespace orbx;
+
+namespace orbx {
+
+static KernelTimer* find_timer(orbx_ctx* ctx, const char* name)
+{
+    for (auto& t : ctx->timers)
+        if (t.name == name) return &t;
+    ctx->timers.push_back(KernelTimer{name, {}, {}, 0});
+    return &ctx->timers.back();
+}
+
+void timer_begin(orbx_ctx* ctx, const char* name)
+{
+    if (!ctx->timing) return;
+    KernelTimer* t = find_timer(ctx, name);
+    if (t->used == (int)t->start.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+        t->start.push_back(a);
+        t->stop.push_back(b);
+    }
+    hipEventRecord(t->start[t->used], ctx->stream);
+}
+
+void timer_end(orbx_ctx* ctx, const char* name)
+{
+    if (!ctx->timing) return;
+    KernelTimer* t = find_timer(ctx, name);
+    if (t->used >= (int)t->stop.size()) return;
+    hipEventRecord(t->stop[t->used], ctx->stream);
+    t->used++;
+}
+
+int ensure_scratch(orbx_ctx* ctx, size_t bytes)
+{
+    if (bytes <= ctx->scratch_bytes) return ORBX_OK;
+    if (ctx->scratch) hipFree(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    if (hipMalloc(&ctx->scratch, bytes) != hipSuccess) return ORBX_ERR_NOMEM;
+    ctx->scratch_bytes = bytes;
+    return ORBX_OK;
+}
+
+int ensure_pinned(orbx_ctx* ctx, size_t bytes)
+{
+    if (bytes <= ctx->host_pinned_bytes) return ORBX_OK;
+    if (ctx->host_pinned) hipHostFree(ctx->host_pinned);
+    ctx->host_pinned = nullptr;
+    ctx->host_pinned_bytes = 0;
+    if (hipHostMalloc(&ctx->host_pinned, bytes, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_NOMEM;
+    ctx->host_pinned_bytes = bytes;
+    return ORBX_OK;
+}
+
+template <typename T>
+static int realloc_dev(T*& p, size_t count)
+{
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)) != hipSuccess) return ORBX_ERR_NOMEM;
+    return ORBX_OK;
+}
+
+static void free_buffers(orbx_ctx* ctx)
+{
+    void* ptrs[] = {ctx->frames, ctx->pyr_raw, ctx->pyr_blur, ctx->cell_lists, ctx->cell_count,
+                    ctx->level_keys, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
+                    ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
+                    ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
+                    ctx->scratch};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+}
+
+// Make the device tables and buffers describe frames of w x h.
+static int set_geometry(orbx_ctx* ctx, int w, int h)
+{
+    if (ctx->geom_w == w && ctx->geom_h == h) return ORBX_OK;
+    if (w > ctx->max_w || h > ctx->max_h) return ORBX_ERR_CAPACITY;
+    hipStreamSynchronize(ctx->stream);
+    Geometry& g = ctx->geom;
+    int r = compute_geometry(g, w, h);
+    if (r != ORBX_OK) return r;
+    const int S = ctx->slots;
+    // per-slot buffers depend on the frame size / config only
+    if ((long long)w * h > (long long)ctx->cap_frame_px) {
+        if ((r = realloc_dev(ctx->frames, (size_t)S * w * h)) != ORBX_OK) return r;
+        ctx->cap_frame_px = (long long)w * h;
+    }
+    if (g.frame_pyr_bytes > ctx->cap_pyr_bytes) {
+        if ((r = realloc_dev(ctx->pyr_raw, (size_t)S * g.frame_pyr_bytes)) != ORBX_OK) return r;
+        if ((r = realloc_dev(ctx->pyr_blur, (size_t)S * g.frame_pyr_bytes)) != ORBX_OK) return r;
+        ctx->cap_pyr_bytes = g.frame_pyr_bytes;
+    }
+    if (g.list_entries > ctx->cap_list_entries) {
+        if ((r = realloc_dev(ctx->cell_lists, (size_t)S * g.list_entries)) != ORBX_OK) return r;
+        ctx->cap_list_entries = g.list_entries;
+    }
+    if ((int)g.cells.size() > ctx->cap_cells) {
+        if ((r = realloc_dev(ctx->cell_count, (size_t)S * g.cells.size())) != ORBX_OK) return r;
+        if ((r = realloc_dev(ctx->dgeom.cells, g.cells.size())) != ORBX_OK) return r;
+        ctx->cap_cells = (int)g.cells.size();
+    }
+    if (g.level_entries > ctx->cap_level_entries) {
+        if ((r = realloc_dev(ctx->level_keys, (size_t)S * g.level_entries)) != ORBX_OK) return r;
+        ctx->cap_level_entries = g.level_entries;
+    }
+    if ((int)g.res_cols.size() > ctx->cap_res_cols) {
+        if ((r = realloc_dev(ctx->dgeom.res_cols, g.res_cols.size())) != ORBX_OK) return r;
+        ctx->cap_res_cols = (int)g.res_cols.size();
+    }
+    if ((int)g.res_rows.size() > ctx->cap_res_rows) {
+        if ((r = realloc_dev(ctx->dgeom.res_rows, g.res_rows.size())) != ORBX_OK) return r;
+        ctx->cap_res_rows = (int)g.res_rows.size();
+    }
+    // blur tiles: (level, x0, y0) covering stride x ph of every level
+    std::vector<int4> tiles;
+    for (int l = 0; l < g.nlevels; l++) {
+        const LevelGeom& L = g.levels[l];
+        for (int y = 0; y < L.ph; y += 16)
+            for (int x = 0; x < L.stride; x += 64) tiles.push_back(make_int4(l, x, y, 0));
+    }
+    if ((int)tiles.size() > ctx->cap_blur_tiles) {
+        if ((r = realloc_dev(ctx->blur_tiles, tiles.size())) != ORBX_OK) return r;
+        ctx->cap_blur_tiles = (int)tiles.size();
+    }
+    ctx->blur_tiles_n = (int)tiles.size();
+    ORBX_HIP_CHECK(hipMemcpy(ctx->dgeom.levels, g.levels.data(), g.levels.size() * sizeof(LevelGeom), hipMemcpyHostToDevice));
+    ORBX_HIP_CHECK(hipMemcpy(ctx->dgeom.cells, g.cells.data(), g.cells.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
+    if (!g.res_cols.empty())
+        ORBX_HIP_CHECK(hipMemcpy(ctx->dgeom.res_cols, g.res_cols.data(), g.res_cols.size() * sizeof(ResizeCol), hipMemcpyHostToDevice));
+    if (!g.res_rows.empty())
+        ORBX_HIP_CHECK(hipMemcpy(ctx->dgeom.res_rows, g.res_rows.data(), g.res_rows.size() * sizeof(ResizeRow), hipMemcpyHostToDevice));
+    ORBX_HIP_CHECK(hipMemcpy(ctx->blur_tiles, tiles.data(), tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
+    // The retain kernel keeps per-cell state for up to 256 cells per level.
+    if (g.max_cells_per_level > 256) return ORBX_ERR_UNSUPPORTED;
+    ctx->geom_w = w;
+    ctx->geom_h = h;
+    return ORBX_OK;
+}
+
+static int check_errors(orbx_ctx* ctx)
+{
+    int32_t flags = 0;
+    ORBX_HIP_CHECK(hipMemcpy(&flags, ctx->error_flags, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (flags) {
+        hipMemset(ctx->error_flags, 0, sizeof(int32_t));
+        return ORBX_ERR_CAPACITY;
+    }
+    return ORBX_OK;
+}
+
+}  // namespace orbx
+
+extern "C" {
+
+const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+
+int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, int nlevels,
+                int score_type, int fast_th, int max_w, int max_h, int max_batch)
+{
+    if (!out) return ORBX_ERR_ARG;
+    *out = nullptr;
+    if (nfeatures <= 0 || nfeatures > 4096 || nlevels <= 0 || nlevels > kMaxLevels ||
+        !(scale_factor > 1.0f) || max_w <= 0 || max_h <= 0 || max_w > 4095 || max_h > 4095 ||
+        max_batch <= 0 || fast_th < 1 || fast_th > 255)
+        return ORBX_ERR_ARG;
+    if (score_type != 1) return ORBX_ERR_UNSUPPORTED;   // HARRIS_SCORE not implemented
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_HIP;
+    if (device < 0 || device >= ndev) return ORBX_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return ORBX_ERR_HIP;
+    orbx_ctx* ctx = new (std::nothrow) orbx_ctx();
+    if (!ctx) return ORBX_ERR_NOMEM;
+    ctx->device = device;
+    ctx->max_w = max_w;
+    ctx->max_h = max_h;
+    ctx->slots = max_batch;
+    init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
+    int r = ORBX_OK;
+    const int S = max_batch;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
+    if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
+    if (r == ORBX_OK) r = realloc_dev(ctx->level_count, (size_t)S * nlevels);
+    if (r == ORBX_OK) r = realloc_dev(ctx->out_kps, (size_t)S * nfeatures);
+    if (r == ORBX_OK) r = realloc_dev(ctx->out_desc, (size_t)S * nfeatures * 32);
+    if (r == ORBX_OK) r = realloc_dev(ctx->out_n, (size_t)S);
+    if (r == ORBX_OK) r = realloc_dev(ctx->match12, (size_t)S * nfeatures);
+    if (r == ORBX_OK) r = realloc_dev(ctx->match_n, (size_t)S);
+    if (r == ORBX_OK) r = realloc_dev(ctx->error_flags, 4);
+    if (r == ORBX_OK && hipMemset(ctx->error_flags, 0, 4 * sizeof(int32_t)) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK && hipMemset(ctx->out_n, 0, S * sizeof(int32_t)) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK &&
+        hipMemcpy(ctx->dgeom.umax, ctx->geom.umax.data(), ctx->geom.umax.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+        r = ORBX_ERR_HIP;
+    // size the per-frame buffers for the largest frame up front
+    if (r == ORBX_OK) r = set_geometry(ctx, max_w, max_h);
+    if (r != ORBX_OK) {
+        orbx_destroy(ctx);
+        return r;
+    }
+    *out = ctx;
+    return ORBX_OK;
+}
+
+void orbx_destroy(orbx_ctx* ctx)
+{
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    for (auto& t : ctx->timers) {
+        for (auto e : t.start) hipEventDestroy(e);
+        for (auto e : t.stop) hipEventDestroy(e);
+    }
+    free_buffers(ctx);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int orbx_get_levels(const orbx_ctx* ctx) { return ctx ? ctx->geom.nlevels : 0; }
+float orbx_get_scale_factor(const orbx_ctx* ctx) { return ctx ? ctx->geom.scale_factor : 0.f; }
+
+int orbx_get_features_per_level(const orbx_ctx* ctx, int32_t* out, int cap)
+{
+    if (!ctx || !out) return ORBX_ERR_ARG;
+    const auto& v = ctx->geom.features_per_level;
+    for (int i = 0; i < (int)v.size() && i < cap; i++) out[i] = v[i];
+    return (int)v.size();
+}
+
+int orbx_get_scale_factors(const orbx_ctx* ctx, float* out, int cap)
+{
+    if (!ctx || !out) return ORBX_ERR_ARG;
+    const auto& v = ctx->geom.scale;
+    for (int i = 0; i < (int)v.size() && i < cap; i++) out[i] = v[i];
+    return (int)v.size();
+}
+
+int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs, int w, int h, size_t stride)
+{
+    if (!ctx || !imgs || count <= 0 || first < 0 || first + count > ctx->slots || stride < (size_t)w)
+        return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    int r = set_geometry(ctx, w, h);
+    if (r != ORBX_OK) return r;
+    ORBX_HIP_CHECK(hipMemcpy2DAsync(ctx->frames + (size_t)first * w * h, (size_t)w, imgs, stride, (size_t)w,
+                                    (size_t)h * count, hipMemcpyHostToDevice, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_dev_extract(orbx_ctx* ctx, int first, int count)
+{
+    if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || ctx->geom_w <= 0) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ctx->last_first = first;
+    ctx->last_count = count;
+    return launch_extract(ctx, first, count);
+}
+
+int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window, float nnratio,
+                        int check_ori)
+{
+    if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || seq_len <= 0 || window < 0)
+        return ORBX_ERR_ARG;
+    if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
+    if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    return launch_match_prev(ctx, first, count, seq_len, window, nnratio, check_ori);
+}
+
+int orbx_dev_sync(orbx_ctx* ctx)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return check_errors(ctx);
+}
+
+int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out)
+{
+    if (!ctx || slot < 0 || slot >= ctx->slots || !n_out) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    int32_t n = 0;
+    ORBX_HIP_CHECK(hipMemcpy(&n, ctx->out_n + slot, sizeof(int32_t), hipMemcpyDeviceToHost));
+    *n_out = n;
+    if (n > cap) return ORBX_ERR_CAPACITY;
+    const size_t nf = ctx->geom.nfeatures;
+    if (n > 0 && kps)
+        ORBX_HIP_CHECK(hipMemcpy(kps, ctx->out_kps + slot * nf, n * sizeof(orbx_keypoint), hipMemcpyDeviceToHost));
+    if (n > 0 && desc)
+        ORBX_HIP_CHECK(hipMemcpy(desc, ctx->out_desc + slot * nf * 32, (size_t)n * 32, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+int orbx_dev_read_matches(orbx_ctx* ctx, int slot, int32_t* matches12, int cap, int* n_matches, int* n1)
+{
+    if (!ctx || slot < 0 || slot >= ctx->slots) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const int seq_prev_unknown = 0;
+    (void)seq_prev_unknown;
+    int32_t nm = 0;
+    ORBX_HIP_CHECK(hipMemcpy(&nm, ctx->match_n + slot, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (n_matches) *n_matches = nm;
+    const int nf = ctx->geom.nfeatures;
+    if (n1) *n1 = nf;
+    if (matches12) {
+        if (cap < nf) return ORBX_ERR_CAPACITY;
+        ORBX_HIP_CHECK(hipMemcpy(matches12, ctx->match12 + (size_t)slot * nf, nf * sizeof(int32_t), hipMemcpyDeviceToHost));
+    }
+    return ORBX_OK;
+}
+
+int orbx_dev_kernel_time_enable(orbx_ctx* ctx, int enable)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    ctx->timing = enable != 0;
+    for (auto& t : ctx->timers) t.used = 0;
+    return ORBX_OK;
+}
+
+int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms, double* total_ms)
+{
+    if (!ctx || !name) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (auto& t : ctx->timers) {
+        if (t.name != name) continue;
+        double tot = 0;
+        for (int i = 0; i < t.used; i++) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, t.start[i], t.stop[i]) == hipSuccess) tot += ms;
+        }
+        const int n = t.used;
+        if (avg_ms) *avg_ms = n ? tot / n : 0.0;
+        if (total_ms) *total_ms = tot;
+        t.used = 0;
+        return n;
+    }
+    if (avg_ms) *avg_ms = 0;
+    if (total_ms) *total_ms = 0;
+    return 0;
+}
+
+int orbx_dev_read_level(orbx_ctx* ctx, int slot, int level, int blurred, uint8_t* out, int cap, int* pw, int* ph)
+{
+    if (!ctx || level < 0 || level >= ctx->geom.nlevels) return ORBX_ERR_ARG;
+    const int f = slot - ctx->last_first;
+    if (f < 0 || f >= ctx->last_count) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const LevelGeom& L = ctx->geom.levels[level];
+    *pw = L.pw;
+    *ph = L.ph;
+    if (cap < L.pw * L.ph) return ORBX_ERR_CAPACITY;
+    const uint8_t* src = (blurred ? ctx->pyr_blur : ctx->pyr_raw) + (size_t)f * ctx->geom.frame_pyr_bytes + L.off;
+    ORBX_HIP_CHECK(hipMemcpy2D(out, L.pw, src, L.stride, L.pw, L.ph, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
+int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride, orbx_keypoint* kps,
+                 uint8_t* desc, int cap, int* n_out)
+{
+    if (!ctx || !n_out) return ORBX_ERR_ARG;
+    if (w == 0 || h == 0 || img == nullptr) {   // _image.empty(): return untouched
+        *n_out = 0;
+        return ORBX_OK;
+    }
+    if (w < 0 || h < 0) return ORBX_ERR_ARG;
+    int r = orbx_dev_upload(ctx, 0, 1, img, w, h, stride);
+    if (r != ORBX_OK) return r;
+    if ((r = orbx_dev_extract(ctx, 0, 1)) != ORBX_OK) return r;
+    if ((r = orbx_dev_sync(ctx)) != ORBX_OK) return r;
+    return orbx_dev_read_features(ctx, 0, kps, desc, cap, n_out);
+}
+
+int orbx_extract_batch(orbx_ctx* ctx, int B, const uint8_t* const* imgs, int w, int h, size_t stride,
+                       orbx_keypoint* kps, uint8_t* desc, int cap, int32_t* n_out)
+{
+    if (!ctx || !imgs || !n_out || B <= 0 || B > ctx->slots) return ORBX_ERR_ARG;
+    int r;
+    for (int b = 0; b < B; b++)
+        if ((r = orbx_dev_upload(ctx, b, 1, imgs[b], w, h, stride)) != ORBX_OK) return r;
+    if ((r = orbx_dev_extract(ctx, 0, B)) != ORBX_OK) return r;
+    if ((r = orbx_dev_sync(ctx)) != ORBX_OK) return r;
+    for (int b = 0; b < B; b++) {
+        int n = 0;
+        r = orbx_dev_read_features(ctx, b, kps ? kps + (size_t)b * cap : nullptr,
+                                   desc ? desc + (size_t)b * cap * 32 : nullptr, cap, &n);
+        n_out[b] = n;
+        if (r != ORBX_OK) return r;
+    }
+    return ORBX_OK;
+}
+
+int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int d = 0;
+    for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+}  // extern "C"

@@ -1,0 +1,365 @@
+// Device-side building blocks shared by the orbx kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbx_sincos.h"
+
+namespace orbx {
+
+#include "orbx_sincos_table.inc"
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+// --------------------------------------------------------------------------
+// cv::fastAtan2 (OpenCV 2.4 mathfuncs.cpp), degrees in [0, 360].
+// Called by IC_Angle (src/ORBextractor.cc:150).  Division is IEEE (built
+// with -fhip-fp32-correctly-rounded-divide-sqrt) and no FMA contraction.
+// --------------------------------------------------------------------------
+__device__ inline float fast_atan2_deg(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float eps = (float)2.220446049250313e-16;   // (float)DBL_EPSILON
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (ax >= ay) {
+        const float c = __fdiv_rn(ay, __fadd_rn(ax, eps));
+        const float c2 = __fmul_rn(c, c);
+        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    } else {
+        const float c = __fdiv_rn(ax, __fadd_rn(ay, eps));
+        const float c2 = __fmul_rn(c, c);
+        a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+    }
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+// Correctly rounded sinf/cosf of a float angle (see orbx_sincos.h).
+__device__ inline float hard_case(float x, int kind, float fallback)
+{
+    uint32_t xb = __float_as_uint(x);
+    int lo = 0, hi = ORBX_SINCOS_HARD_N - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t mb = kSincosHard[mid][0];
+        const int mk = (int)kSincosHard[mid][1];
+        if (mb == xb && mk == kind) return __uint_as_float(kSincosHard[mid][2]);
+        if (mb < xb || (mb == xb && mk < kind)) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return fallback;
+}
+
+__device__ inline void cr_sincosf(float x, float* s, float* c)
+{
+    double ds, dc;
+    sincos_double(x, &ds, &dc);
+    float fs = (float)ds, fc = (float)dc;
+    if (near_float_midpoint(ds)) fs = hard_case(x, 0, fs);
+    if (near_float_midpoint(dc)) fc = hard_case(x, 1, fc);
+    *s = fs;
+    *c = fc;
+}
+
+// cvRound of a float (SSE2 cvtsd2si, round half to even).
+__device__ inline int cv_round(float v) { return __float2int_rn(v); }
+
+// ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1794-1810): Hamming
+// distance of two 256-bit descriptors = popcount of XOR.
+__device__ inline int hamming256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1)
+{
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// --------------------------------------------------------------------------
+// Block-wide scans / reductions for 256-thread blocks (4 waves).
+// --------------------------------------------------------------------------
+struct BlockScratch {
+    int wave[2][kWaves];
+    int vars[8];
+};
+
+__device__ inline int wave_inclusive_scan(int v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ inline int wave_sum(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ inline int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Exclusive prefix of v over threadIdx order; *total = block sum.
+__device__ inline int block_exclusive_scan(int v, int* total, BlockScratch& s, int buf)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int inc = wave_inclusive_scan(v);
+    if (lane == 63) s.wave[buf][w] = inc;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; i++) {
+        const int x = s.wave[buf][i];
+        base += (i < w) ? x : 0;
+        tot += x;
+    }
+    *total = tot;
+    return base + inc - v;
+}
+
+__device__ inline int block_sum(int v, BlockScratch& s, int buf)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) s.wave[buf][w] = v;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; i++) t += s.wave[buf][i];
+    return t;
+}
+
+__device__ inline int block_max(int v, BlockScratch& s, int buf)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v = wave_max(v);
+    if (lane == 0) s.wave[buf][w] = v;
+    __syncthreads();
+    int t = s.wave[buf][0];
+#pragma unroll
+    for (int i = 1; i < kWaves; i++) t = max(t, s.wave[buf][i]);
+    return t;
+}
+
+// --------------------------------------------------------------------------
+// std::nth_element (libstdc++ 11, bits/stl_algo.h:1964-1986 __introselect)
+// replayed exactly on a keypoint list, with the comparator of OpenCV's
+// KeyPointsFilter::retainBest (response greater).  Elements are packed
+// score<<24 | y<<12 | x; only the score takes part in comparisons, so the
+// permutation equals the one libstdc++ applies to the cv::KeyPoint vector
+// (src/ORBextractor.cc:683, :699).
+//
+// The Hoare partition (__unguarded_partition, stl_algo.h:1880-1896) is
+// computed block-parallel: with L = ascending positions whose key <= pivot
+// and R = descending positions whose key >= pivot, it swaps (L_k, R_k) for
+// k = 1..m where m = max_s min(#L before s, #R at/after s), and returns
+// L_1 (m == 0) or min(L_{m+1}, R_m).
+// --------------------------------------------------------------------------
+__device__ inline uint32_t kp_key(uint32_t e) { return e >> 24; }
+__device__ inline bool kp_greater(uint32_t a, uint32_t b) { return kp_key(a) > kp_key(b); }
+
+// libstdc++ bits/stl_heap.h helpers (sequential, thread 0 only).
+__device__ inline void heap_push(uint32_t* first, int hole, int top, uint32_t value)
+{
+    int parent = (hole - 1) / 2;
+    while (hole > top && kp_greater(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+__device__ inline void heap_adjust(uint32_t* first, int hole, int len, uint32_t value)
+{
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (kp_greater(first[second], first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    heap_push(first, hole, top, value);
+}
+
+__device__ inline void heap_select(uint32_t* first, int middle, int last)
+{
+    // __make_heap(first, first+middle)
+    if (middle >= 2) {
+        int parent = (middle - 2) / 2;
+        while (true) {
+            heap_adjust(first, parent, middle, first[parent]);
+            if (parent == 0) break;
+            parent--;
+        }
+    }
+    for (int i = middle; i < last; ++i) {
+        if (kp_greater(first[i], first[0])) {
+            // __pop_heap(first, first+middle, first+i)
+            const uint32_t value = first[i];
+            first[i] = first[0];
+            heap_adjust(first, 0, middle, value);
+        }
+    }
+}
+
+__device__ inline void insertion_sort(uint32_t* a, int first, int last)
+{
+    if (first == last) return;
+    for (int i = first + 1; i < last; ++i) {
+        const uint32_t val = a[i];
+        if (kp_greater(val, a[first])) {
+            for (int k = i; k > first; --k) a[k] = a[k - 1];
+            a[first] = val;
+        } else {
+            int k = i;
+            while (kp_greater(val, a[k - 1])) {
+                a[k] = a[k - 1];
+                --k;
+            }
+            a[k] = val;
+        }
+    }
+}
+
+__device__ inline void move_median_to_first(uint32_t* a, int result, int x, int y, int z)
+{
+    int t;
+    if (kp_greater(a[x], a[y])) {
+        if (kp_greater(a[y], a[z])) t = y;
+        else if (kp_greater(a[x], a[z])) t = z;
+        else t = x;
+    } else if (kp_greater(a[x], a[z])) {
+        t = x;
+    } else if (kp_greater(a[y], a[z])) {
+        t = z;
+    } else {
+        t = y;
+    }
+    const uint32_t tmp = a[result];
+    a[result] = a[t];
+    a[t] = tmp;
+}
+
+// Partition [lo+1, hi) around the pivot key at a[lo]; returns the cut.
+// pos: scratch of 2 * ((hi-lo)/2 + 1) ints.  Must be called by all threads.
+__device__ inline int block_hoare_partition(uint32_t* a, int lo, int hi, int* pos, BlockScratch& s)
+{
+    int* posR = pos;
+    int* posL = pos + (hi - lo) / 2 + 1;
+    const int tid = threadIdx.x;
+    const uint32_t P = kp_key(a[lo]);
+    const int len = hi - lo - 1;
+    const int chunk = (len + kBlock - 1) / kBlock;
+    const int s0 = min(lo + 1 + tid * chunk, hi), s1 = min(s0 + chunk, hi);
+    int nle = 0, nge = 0;
+    for (int x = s0; x < s1; x++) {
+        const uint32_t k = kp_key(a[x]);
+        nle += (k <= P);
+        nge += (k >= P);
+    }
+    int tot_le, tot_ge;
+    const int le_before = block_exclusive_scan(nle, &tot_le, s, 0);
+    const int ge_before = block_exclusive_scan(nge, &tot_ge, s, 1);
+    const int ge_after_chunk = tot_ge - ge_before - nge;   // #ge in chunks after this one
+    // m = max over splits of min(CL, CR)
+    int cl = le_before, cr = ge_after_chunk + nge, best = 0;
+    for (int x = s0; x < s1; x++) {
+        best = max(best, min(cl, cr));
+        const uint32_t k = kp_key(a[x]);
+        cl += (k <= P);
+        cr -= (k >= P);
+    }
+    best = max(best, min(cl, cr));
+    __syncthreads();   // scan scratch reuse
+    const int m = block_max(best, s, 0);
+    // locate R_k (k <= m), L_{m+1}, R_m, L_1
+    if (tid == 0) {
+        s.vars[0] = 0x7fffffff;   // L_{m+1}
+        s.vars[1] = -1;           // R_m
+        s.vars[2] = 0x7fffffff;   // L_1
+    }
+    __syncthreads();
+    cl = le_before;
+    cr = ge_after_chunk + nge;
+    for (int x = s0; x < s1; x++) {
+        const uint32_t k = kp_key(a[x]);
+        if (k <= P) {
+            cl++;
+            if (cl <= m) posL[cl - 1] = x;
+            if (cl == m + 1) s.vars[0] = x;
+            if (cl == 1) s.vars[2] = x;
+        }
+        if (k >= P) {
+            if (cr <= m) posR[cr - 1] = x;
+            if (cr == m) s.vars[1] = x;
+            cr--;
+        }
+    }
+    __syncthreads();
+    // swaps (L_k, R_k), k = 1..m: disjoint pairs, positions fixed above
+    for (int k = tid; k < m; k += kBlock) {
+        const int i = posL[k], j = posR[k];
+        const uint32_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+    const int cut = (m == 0) ? s.vars[2] : min(s.vars[0], s.vars[1]);
+    __syncthreads();
+    return cut;
+}
+
+__device__ inline int floor_log2(int n)
+{
+    return 31 - __clz(n);
+}
+
+// std::nth_element(a, a + nth, a + n, greater-by-response).
+// pos: scratch of n + 4 ints.
+__device__ inline void block_nth_element(uint32_t* a, int n, int nth, int* pos, BlockScratch& s)
+{
+    if (n == 0 || nth == n) return;
+    int first = 0, last = n;
+    int depth = 2 * floor_log2(n);
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (threadIdx.x == 0) {
+                heap_select(a + first, nth + 1 - first, last - first);
+                const uint32_t t = a[first];
+                a[first] = a[nth];
+                a[nth] = t;
+            }
+            __syncthreads();
+            return;
+        }
+        --depth;
+        if (threadIdx.x == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        __syncthreads();
+        const int cut = block_hoare_partition(a, first, last, pos, s);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    if (threadIdx.x == 0) insertion_sort(a, first, last);
+    __syncthreads();
+}
+
+}  // namespace orbx

@@ -1,0 +1,568 @@
+// ORB extraction on MI355X (gfx950): ORBextractor::operator()
+// (src/ORBextractor.cc:718-779) for a batch of frames, one launch per stage:
+//
+//   k_pyr_level0   copyMakeBorder(REFLECT_101) of the input   (:814)
+//   k_pyr_resize   resize INTER_LINEAR + border, level l      (:800, :806)
+//   k_fast_cells   FAST-9/16 + cell-local NMS + threshold-7
+//                  fallback + raster-order compaction, one
+//                  workgroup per grid cell                    (:599-614)
+//   k_retain       per-level quota redistribution and the two
+//                  retainBest passes (libstdc++ introselect)  (:622-701)
+//   k_blur         GaussianBlur 7x7 sigma 2 on each level     (:760)
+//   k_describe     IC_Angle + rBRIEF + coordinate scaling,
+//                  one wave per keypoint                      (:124-194, :705,
+//                                                              :764-777)
+//
+// All integer / byte work; the bounds are HBM or latency, never MFMA.
+#include "orbx_device.h"
+#include "orbx_internal.h"
+
+namespace orbx {
+
+__constant__ int8_t c_pattern[256][4] = {
+#include "orbx_pattern.inc"
+};
+
+struct ExtractArgs {
+    const LevelGeom* levels;
+    const CellGeom* cells;
+    const ResizeCol* res_cols;
+    const ResizeRow* res_rows;
+    const int* umax;
+    const uint8_t* frames;
+    uint8_t* pyr_raw;
+    uint8_t* pyr_blur;
+    uint32_t* cell_lists;
+    int32_t* cell_count;
+    uint32_t* level_keys;
+    int32_t* level_count;
+    orbx_keypoint* out_kps;
+    uint8_t* out_desc;
+    int32_t* out_n;
+    int32_t* error_flags;
+    long long frame_pyr_bytes;
+    int first_slot;
+    int w, h;
+    int nlevels, ncells, list_entries, level_entries, nfeatures;
+    int fast_th, fast_th_low;       // FAST thresholds (fastTh, 7), clamped
+    int max_list_cap, max_level_cap;
+};
+
+__device__ inline int reflect101(int p, int len)
+{
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+__device__ inline uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
+__device__ inline int sat_s16(int v) { return min(max(v, -32768), 32767); }
+
+// ---------------------------------------------------------------------------
+// Level 0: padded copy with BORDER_REFLECT_101.  4 output bytes per thread.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
+{
+    const int f = blockIdx.y;
+    const LevelGeom L = a.levels[0];
+    const int words_per_row = L.stride >> 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= words_per_row * L.ph) return;
+    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
+    const uint8_t* src = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
+    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
+    const int sy = reflect101(py - kEdge, L.h);
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int px = px0 + b;
+        uint32_t v = 0;
+        if (px < L.pw) v = src[(size_t)sy * a.w + reflect101(px - kEdge, L.w)];
+        word |= v << (8 * b);
+    }
+    *reinterpret_cast<uint32_t*>(dst + px0) = word;
+}
+
+// ---------------------------------------------------------------------------
+// Level l >= 1: cv::resize INTER_LINEAR from level l-1 (fixed point, 11-bit
+// weights; columns < nvec use the SSE2 VResizeLinearVec_32s8u arithmetic,
+// the rest the scalar FixedPtCast<int,uchar,22>), then copyMakeBorder
+// REFLECT_101 of the level itself (border pixels recompute their source).
+// ---------------------------------------------------------------------------
+__device__ inline uint8_t resize_pixel(const uint8_t* prev, int pstride, const ResizeCol& c,
+                                       const ResizeRow& r, bool vec)
+{
+    const uint8_t* r0 = prev + (size_t)r.sy0 * pstride;
+    const uint8_t* r1 = prev + (size_t)r.sy1 * pstride;
+    const int S0 = r0[c.sx0] * c.a0 + r0[c.sx1] * c.a1;
+    const int S1 = r1[c.sx0] * c.a0 + r1[c.sx1] * c.a1;
+    if (vec) {
+        const int x0 = sat_s16(S0 >> 4), y0 = sat_s16(S1 >> 4);
+        int v = sat_s16(((x0 * r.b0) >> 16) + ((y0 * r.b1) >> 16));
+        v = sat_s16(v + 2) >> 2;
+        return sat_u8(v);
+    }
+    return sat_u8((S0 * r.b0 + S1 * r.b1 + (1 << 21)) >> 22);
+}
+
+__global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
+{
+    const int f = blockIdx.y;
+    const LevelGeom L = a.levels[level];
+    const LevelGeom P = a.levels[level - 1];
+    const int words_per_row = L.stride >> 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= words_per_row * L.ph) return;
+    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
+    const uint8_t* frame = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
+    const uint8_t* prev = frame + P.off + (size_t)kEdge * P.stride + kEdge;
+    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
+    const int y = reflect101(py - kEdge, L.h);
+    const ResizeRow r = a.res_rows[L.res_row_off + y];
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int px = px0 + b;
+        uint32_t v = 0;
+        if (px < L.pw) {
+            const int x = reflect101(px - kEdge, L.w);
+            v = resize_pixel(prev, P.stride, a.res_cols[L.res_col_off + x], r, x < L.nvec_resize);
+        }
+        word |= v << (8 * b);
+    }
+    *reinterpret_cast<uint32_t*>(dst + px0) = word;
+}
+
+// ---------------------------------------------------------------------------
+// FAST-9/16 score map.  For a pixel with value v and ring d_k = v - p_k
+// (k = 0..15, OpenCV offsets), S = max(M_dark, M_bright) - 1 where M_dark is
+// the best 9-arc minimum of d and M_bright that of -d.  FAST at threshold t
+// classifies the pixel as a corner iff S >= t, and cornerScore<16> returns
+// exactly S (OpenCV 2.4 fast.cpp / fast_score.cpp).  Returns S if S >= tmin,
+// else 0.
+// ---------------------------------------------------------------------------
+__device__ inline int fast_score(const uint8_t* t, int pitch, int tmin)
+{
+    const int v = t[0];
+    const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
+                         3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
+                         -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
+                         -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
+    // quick rejection: a 9-arc contains >= 2 of the 4 compass points
+    int nb = 0, nd = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 4) {
+        nd += d[k] > tmin;
+        nb += d[k] < -tmin;
+    }
+    if (nd < 2 && nb < 2) return 0;
+    int m2[16], m4[16], mx2[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m4[k] = min(m2[k], m2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int dark = -1000, bright = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn = min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int mx = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        dark = max(dark, mn);
+        bright = min(bright, mx);
+    }
+    const int S = max(dark, -bright) - 1;
+    return S >= tmin ? S : 0;
+}
+
+// One workgroup per (cell, frame).  LDS: tile (hx*hy bytes, reused for the
+// NMS result) + score map (hx*hy bytes).
+__global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ BlockScratch bs;
+    const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const CellGeom C = a.cells[cell];
+    int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
+    if (!C.valid) {
+        if (tid == 0) *count_out = 0;
+        return;
+    }
+    const LevelGeom L = a.levels[C.level];
+    const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off +
+                         (size_t)(kEdge + C.ini_y) * L.stride + kEdge + C.ini_x;
+    const int hx = C.hx, hy = C.hy, n = hx * hy;
+    uint8_t* tile = smem;
+    uint8_t* sm = smem + tile_pitch_bytes;
+    for (int i = tid; i < n; i += kBlock) {
+        const int r = i / hx, c = i - r * hx;
+        tile[i] = src[(size_t)r * L.stride + c];
+    }
+    __syncthreads();
+    const int tmin = min(a.fast_th, a.fast_th_low);
+    for (int i = tid; i < n; i += kBlock) {
+        const int r = i / hx, c = i - r * hx;
+        int s = 0;
+        if (r >= 3 && r <= hy - 4 && c >= 3 && c <= hx - 4) s = fast_score(tile + i, hx, tmin);
+        sm[i] = (uint8_t)s;
+    }
+    __syncthreads();
+    // non-max suppression inside the cell: keep[p] = S'(p) if it beats all 8
+    // neighbours' S' (out-of-interior neighbours are 0), stored over `tile`.
+    const int iw = hx - 6, ih = hy - 6, ni = iw * ih;
+    for (int i = tid; i < ni; i += kBlock) {
+        const int r = 3 + i / iw, c = 3 + (i - (i / iw) * iw);
+        const uint8_t* p = sm + r * hx + c;
+        const int s = p[0];
+        int m = max(max(p[-1], p[1]), max(p[-hx - 1], p[-hx]));
+        m = max(m, max(max(p[-hx + 1], p[hx - 1]), max(p[hx], p[hx + 1])));
+        tile[i] = (uint8_t)((s > m) ? s : 0);
+    }
+    __syncthreads();
+    // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
+    const int chunk = (ni + kBlock - 1) / kBlock;
+    const int p0 = min(tid * chunk, ni), p1 = min(p0 + chunk, ni);
+    int c1 = 0;
+    for (int i = p0; i < p1; i++) c1 += tile[i] >= a.fast_th && tile[i] > 0;
+    const int n1 = block_sum(c1, bs, 0);
+    const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
+    int c = 0;
+    for (int i = p0; i < p1; i++) c += tile[i] >= t && tile[i] > 0;
+    int total;
+    int off = block_exclusive_scan(c, &total, bs, 1);
+    uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
+    for (int i = p0; i < p1; i++) {
+        const int s = tile[i];
+        if (s >= t && s > 0) {
+            const int r = 3 + i / iw, cc = 3 + (i - (i / iw) * iw);
+            out[off++] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+        }
+    }
+    if (tid == 0) {
+        *count_out = total;
+        if (total > C.list_cap) atomicOr(a.error_flags, 1);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per (level, frame): cell quota redistribution (:622-670), retainBest per
+// cell (:683-685) and per level (:697-701), output in reference order.
+// LDS: cell buffer (max_list_cap) | level buffer (max_level_cap) | scratch.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_retain(ExtractArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
+    __shared__ BlockScratch bs;
+    __shared__ int s_total[256], s_retain[256];
+    __shared__ uint8_t s_nomore[256];
+    __shared__ int s_nlev;
+    const int level = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom L = a.levels[level];
+    uint32_t* cellbuf = sbuf;
+    uint32_t* levbuf = sbuf + a.max_list_cap;
+    int* pos = reinterpret_cast<int*>(levbuf + a.max_level_cap);
+    const int nCells = L.n_cells;
+    const int32_t* counts = a.cell_count + (size_t)f * a.ncells + L.cell_base;
+    for (int c = tid; c < nCells; c += kBlock) s_total[c] = counts[c];
+    __syncthreads();
+    if (tid == 0) {
+        // bNoMore / nToRetain exactly as the reference loop (skipped cells keep
+        // nToRetain = 0, bNoMore = false until the redistribution loop).
+        uint8_t* nomore = s_nomore;
+        const int nfc = L.nfeatures_cell;
+        int nNoMore = 0, nToDistribute = 0;
+        for (int c = 0; c < nCells; c++) {
+            nomore[c] = 0;
+            s_retain[c] = 0;
+            if (!a.cells[L.cell_base + c].valid) continue;
+            const int nKeys = s_total[c];
+            if (nKeys > nfc) {
+                s_retain[c] = nfc;
+            } else {
+                s_retain[c] = nKeys;
+                nToDistribute += nfc - nKeys;
+                nomore[c] = 1;
+                nNoMore++;
+            }
+        }
+        while (nToDistribute > 0 && nNoMore < nCells) {
+            const int nNew = nfc + (int)ceilf(__fdiv_rn((float)nToDistribute, (float)(nCells - nNoMore)));
+            nToDistribute = 0;
+            for (int c = 0; c < nCells; c++) {
+                if (!nomore[c]) {
+                    if (s_total[c] > nNew) {
+                        s_retain[c] = nNew;
+                    } else {
+                        s_retain[c] = s_total[c];
+                        nToDistribute += nNew - s_total[c];
+                        nomore[c] = 1;
+                        nNoMore++;
+                    }
+                }
+            }
+        }
+        s_nlev = 0;
+    }
+    __syncthreads();
+    const uint32_t* lists = a.cell_lists + (size_t)f * a.list_entries;
+    for (int c = 0; c < nCells; c++) {
+        const int n = s_total[c], keep = s_retain[c];
+        if (n == 0 || keep == 0) continue;
+        const int take = min(n, keep);
+        const int base = s_nlev;
+        if (base + take > a.max_level_cap) {
+            if (tid == 0) atomicOr(a.error_flags, 2);
+            break;
+        }
+        const uint32_t* src = lists + a.cells[L.cell_base + c].list_off;
+        if (n > keep) {
+            for (int i = tid; i < n; i += kBlock) cellbuf[i] = src[i];
+            __syncthreads();
+            block_nth_element(cellbuf, n, keep, pos, bs);
+            for (int i = tid; i < take; i += kBlock) levbuf[base + i] = cellbuf[i];
+        } else {
+            for (int i = tid; i < take; i += kBlock) levbuf[base + i] = src[i];
+        }
+        __syncthreads();
+        if (tid == 0) s_nlev = base + take;
+        __syncthreads();
+    }
+    int nlev = s_nlev;
+    if (nlev > L.n_desired) {
+        block_nth_element(levbuf, nlev, L.n_desired, pos, bs);
+        nlev = L.n_desired;
+    }
+    uint32_t* out = a.level_keys + (size_t)f * a.level_entries + L.level_off;
+    for (int i = tid; i < nlev; i += kBlock) out[i] = levbuf[i];
+    if (tid == 0) a.level_count[(size_t)f * a.nlevels + level] = nlev;
+}
+
+// ---------------------------------------------------------------------------
+// GaussianBlur 7x7, sigma 2, BORDER_REFLECT_101 on the level ROI with the
+// parent border as context (OpenCV 2.4 8U fixed-point separable filter:
+// taps {18,34,49,55,49,34,18}/256 per pass).  Column pass rounding: columns
+// < nvec follow SymmColumnVec_32s8u (float, round-half-even), the tail
+// FixedPtCastEx (+2^15 >> 16).  The padded border is copied unblurred.
+// Tiles of 64x16 output pixels in padded coordinates.
+// ---------------------------------------------------------------------------
+constexpr int kBlurTW = 64, kBlurTH = 16;
+
+__global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
+{
+    __shared__ uint8_t in[kBlurTH + 6][kBlurTW + 8];
+    __shared__ int rowsum[kBlurTH + 6][kBlurTW];
+    const int f = blockIdx.y, tid = threadIdx.x;
+    const int4 tl = tiles[blockIdx.x];   // level, x0, y0 (padded coords)
+    const LevelGeom L = a.levels[tl.x];
+    const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
+    uint8_t* dst = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
+    const int x0 = tl.y, y0 = tl.z;
+    for (int i = tid; i < (kBlurTH + 6) * (kBlurTW + 6); i += kBlock) {
+        const int r = i / (kBlurTW + 6), c = i - r * (kBlurTW + 6);
+        const int py = min(max(y0 + r - 3, 0), L.ph - 1);
+        const int px = min(max(x0 + c - 3, 0), L.pw - 1);
+        in[r][c] = src[(size_t)py * L.stride + px];
+    }
+    __syncthreads();
+    for (int i = tid; i < (kBlurTH + 6) * kBlurTW; i += kBlock) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const uint8_t* p = &in[r][c + 3];
+        rowsum[r][c] = 55 * p[0] + 49 * (p[-1] + p[1]) + 34 * (p[-2] + p[2]) + 18 * (p[-3] + p[3]);
+    }
+    __syncthreads();
+    for (int i = tid; i < kBlurTH * kBlurTW; i += kBlock) {
+        const int r = i / kBlurTW, c = i - r * kBlurTW;
+        const int py = y0 + r, px = x0 + c;
+        if (py >= L.ph || px >= L.stride) continue;
+        uint8_t v = in[r + 3][c + 3];
+        const int x = px - kEdge, y = py - kEdge;
+        if (x >= 0 && x < L.w && y >= 0 && y < L.h) {
+            const int N = 55 * rowsum[r + 3][c] + 49 * (rowsum[r + 2][c] + rowsum[r + 4][c]) +
+                          34 * (rowsum[r + 1][c] + rowsum[r + 5][c]) + 18 * (rowsum[r][c] + rowsum[r + 6][c]);
+            int q;
+            if (x < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
+                q = N >> 16;
+                const int rem = N & 0xFFFF;
+                if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
+            } else {
+                q = (N + (1 << 15)) >> 16;
+            }
+            v = sat_u8(q);
+        } else if (px >= L.pw) {
+            v = 0;
+        }
+        dst[(size_t)py * L.stride + px] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// IC_Angle + computeOrbDescriptor + output assembly, one wave per keypoint.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
+{
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int k = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int32_t* lc = a.level_count + (size_t)f * a.nlevels;
+    int total = 0, level = -1, local = 0;
+    for (int l = 0; l < a.nlevels; l++) {
+        const int c = lc[l];
+        if (level < 0 && k < total + c) {
+            level = l;
+            local = k - total;
+        }
+        total += c;
+    }
+    if (k == 0 && lane == 0) a.out_n[a.first_slot + f] = total;
+    if (level < 0) return;
+    const LevelGeom L = a.levels[level];
+    const uint32_t e = a.level_keys[(size_t)f * a.level_entries + L.level_off + local];
+    const int score = (int)(e >> 24), y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
+    // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151)
+    const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off +
+                         (size_t)(kEdge + y) * L.stride + kEdge + x;
+    int m01 = 0, m10 = 0;
+    if (lane < 2 * kHalfPatch + 1) {
+        const int u = lane - kHalfPatch;
+        m10 = u * raw[u];
+        for (int v = 1; v <= kHalfPatch; v++) {
+            const int d = a.umax[v];
+            if (u >= -d && u <= d) {
+                const int vp = raw[u + v * L.stride], vm = raw[u - v * L.stride];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
+            }
+        }
+    }
+    m01 = wave_sum(m01);
+    m10 = wave_sum(m10);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    // computeOrbDescriptor on the blurred level (src/ORBextractor.cc:155-194)
+    const float factorPI = (float)(M_PI / 180.f);
+    float sa, ca;
+    cr_sincosf(__fmul_rn(angle, factorPI), &sa, &ca);
+    const uint8_t* blur = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off +
+                          (size_t)(kEdge + y) * L.stride + kEdge + x;
+    uint8_t* desc = a.out_desc + ((size_t)(a.first_slot + f) * a.nfeatures + k) * 32;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int q = r * 64 + lane;
+        const float px1 = c_pattern[q][0], py1 = c_pattern[q][1];
+        const float px2 = c_pattern[q][2], py2 = c_pattern[q][3];
+        const int t0 = blur[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * L.stride +
+                            cv_round(__fsub_rn(__fmul_rn(px1, ca), __fmul_rn(py1, sa)))];
+        const int t1 = blur[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * L.stride +
+                            cv_round(__fsub_rn(__fmul_rn(px2, ca), __fmul_rn(py2, sa)))];
+        const unsigned long long bits = __ballot(t0 < t1);
+        if (lane == r) *reinterpret_cast<unsigned long long*>(desc + 8 * r) = bits;
+    }
+    if (lane == 0) {
+        orbx_keypoint kp;
+        kp.x = (float)x;
+        kp.y = (float)y;
+        if (level != 0) {
+            kp.x = __fmul_rn(kp.x, L.scale);
+            kp.y = __fmul_rn(kp.y, L.scale);
+        }
+        kp.size = L.patch_size;
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = level;
+        kp.class_id = -1;
+        a.out_kps[(size_t)(a.first_slot + f) * a.nfeatures + k] = kp;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host launcher
+// ---------------------------------------------------------------------------
+int launch_extract(orbx_ctx* ctx, int first, int count)
+{
+    const Geometry& g = ctx->geom;
+    ExtractArgs a;
+    a.levels = ctx->dgeom.levels;
+    a.cells = ctx->dgeom.cells;
+    a.res_cols = ctx->dgeom.res_cols;
+    a.res_rows = ctx->dgeom.res_rows;
+    a.umax = ctx->dgeom.umax;
+    a.frames = ctx->frames;
+    a.pyr_raw = ctx->pyr_raw;
+    a.pyr_blur = ctx->pyr_blur;
+    a.cell_lists = ctx->cell_lists;
+    a.cell_count = ctx->cell_count;
+    a.level_keys = ctx->level_keys;
+    a.level_count = ctx->level_count;
+    a.out_kps = ctx->out_kps;
+    a.out_desc = ctx->out_desc;
+    a.out_n = ctx->out_n;
+    a.error_flags = ctx->error_flags;
+    a.frame_pyr_bytes = g.frame_pyr_bytes;
+    a.w = g.w;
+    a.h = g.h;
+    a.nlevels = g.nlevels;
+    a.ncells = (int)g.cells.size();
+    a.list_entries = g.list_entries;
+    a.level_entries = g.level_entries;
+    a.nfeatures = g.nfeatures;
+    a.fast_th = min(max(g.fast_th, 0), 255);
+    a.fast_th_low = 7;
+    a.max_list_cap = g.max_list_cap;
+    a.max_level_cap = g.max_level_cap;
+
+    hipStream_t st = ctx->stream;
+    // The work buffers hold `count` frames starting at batch index 0; the
+    // frame store and outputs are indexed by slot.
+    for (int b0 = 0; b0 < count; b0 += ctx->slots) {
+        const int nb = min(ctx->slots, count - b0);
+        a.first_slot = first + b0;
+        timer_begin(ctx, "pyramid");
+        {
+            const LevelGeom& L = g.levels[0];
+            const int words = (L.stride / 4) * L.ph;
+            hipLaunchKernelGGL(k_pyr_level0, dim3((words + 255) / 256, nb), dim3(256), 0, st, a);
+        }
+        for (int l = 1; l < g.nlevels; l++) {
+            const LevelGeom& L = g.levels[l];
+            const int words = (L.stride / 4) * L.ph;
+            hipLaunchKernelGGL(k_pyr_resize, dim3((words + 255) / 256, nb), dim3(256), 0, st, a, l);
+        }
+        timer_end(ctx, "pyramid");
+        timer_begin(ctx, "fast");
+        {
+            const int pitch = (g.max_tile_bytes + 15) & ~15;
+            hipLaunchKernelGGL(k_fast_cells, dim3((int)g.cells.size(), nb), dim3(256), 2 * pitch, st, a, pitch);
+        }
+        timer_end(ctx, "fast");
+        timer_begin(ctx, "retain");
+        {
+            const size_t lds = (size_t)(g.max_list_cap + g.max_level_cap) * 4 +
+                               (size_t)(std::max(g.max_list_cap, g.max_level_cap) + 8) * 4;
+            hipLaunchKernelGGL(k_retain, dim3(g.nlevels, nb), dim3(256), lds, st, a);
+        }
+        timer_end(ctx, "retain");
+        timer_begin(ctx, "blur");
+        {
+            const int ntiles = ctx->blur_tiles_n;
+            hipLaunchKernelGGL(k_blur, dim3(ntiles, nb), dim3(256), 0, st, a, ctx->blur_tiles);
+        }
+        timer_end(ctx, "blur");
+        timer_begin(ctx, "describe");
+        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + kWaves - 1) / kWaves, nb), dim3(256), 0, st, a);
+        timer_end(ctx, "describe");
+    }
+    if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+    return ORBX_OK;
+}
+
+}  // namespace orbx

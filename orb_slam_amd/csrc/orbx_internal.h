@@ -1,0 +1,176 @@
+// Internal definitions shared by the orbx host code and HIP kernels.
+//
+// Data layout in HBM (one orbx_ctx, `slots` frames):
+//   frames      slots x (w*h)                  input mono8, dense rows
+//   pyr_raw     slots x frame_pyr_bytes        padded levels (w_l+32)x(h_l+32),
+//                                              rows padded to 64 B; level l at
+//                                              LevelGeom::off.  Unblurred.
+//   pyr_blur    slots x frame_pyr_bytes        same layout; interior blurred,
+//                                              border = unblurred border
+//   cell_lists  slots x list_entries  u32      FAST corners per cell, raster
+//                                              order, packed score<<24|y<<12|x
+//                                              (level coordinates)
+//   cell_count  slots x n_cells_total i32
+//   level_keys  slots x level_entries u32      retained keypoints per level
+//   level_count slots x nlevels       i32
+//   out_kps     slots x nfeatures     orbx_keypoint (reference output order)
+//   out_desc    slots x nfeatures x 32 B
+//   out_n       slots                 i32
+//   match12     slots x nfeatures     i32      SearchForInitialization result
+//   match_n     slots                 i32
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+constexpr int kEdge = 16;        // EDGE_THRESHOLD (src/ORBextractor.cc:77)
+constexpr int kHalfPatch = 15;   // HALF_PATCH_SIZE (:76)
+constexpr int kPatch = 31;       // PATCH_SIZE (:75)
+constexpr int kMaxLevels = 16;
+constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
+constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
+
+struct LevelGeom {
+    int w, h;             // level size
+    int pw, ph;           // padded size
+    int stride;           // row pitch of the padded buffer
+    int nvec_resize;      // columns on the SSE2 VResize path (rest: scalar)
+    int nvec_blur;        // columns on the SSE2 SymmColumn path
+    long long off;        // byte offset inside one frame's pyramid
+    int n_desired;        // mnFeaturesPerLevel
+    int cell_base;        // first cell of this level in the cell table
+    int n_cells;          // levelRows * levelCols
+    int level_cols, level_rows;
+    int nfeatures_cell;
+    int level_off;        // offset (entries) of this level in level_keys
+    int level_cap;        // capacity of that slot
+    float scale;          // mvScaleFactor[level]
+    float patch_size;     // (int)(PATCH_SIZE * scale)
+    int res_col_off;      // offset into the resize column table (level >= 1)
+    int res_row_off;      // offset into the resize row table
+};
+
+struct CellGeom {
+    int level, i, j;
+    int ini_x, ini_y;     // ROI origin in level coordinates
+    int hx, hy;           // ROI size (FAST runs on rows/cols [3, h-4])
+    int valid;            // 0 when the reference skips the cell (h <= 0)
+    int list_off;         // offset (entries) in the per-frame corner arena
+    int list_cap;         // ceil(iw/2)*ceil(ih/2): bound on NMS survivors
+};
+
+struct ResizeCol { int16_t sx0, sx1, a0, a1; };
+struct ResizeRow { int16_t sy0, sy1, b0, b1; };
+
+// Extractor configuration and per-image-size geometry (host computed, the
+// way OpenCV computes its tables per call).
+struct Geometry {
+    int nfeatures = 0, nlevels = 0, fast_th = 20;
+    float scale_factor = 1.2f;
+    std::vector<float> scale, inv_scale;
+    std::vector<int> features_per_level;
+    std::vector<int> umax;
+    int w = 0, h = 0;
+    std::vector<LevelGeom> levels;
+    std::vector<CellGeom> cells;
+    std::vector<ResizeCol> res_cols;
+    std::vector<ResizeRow> res_rows;
+    long long frame_pyr_bytes = 0;
+    int list_entries = 0;     // corner arena entries per frame
+    int level_entries = 0;    // level_keys entries per frame
+    int max_tile_bytes = 0;   // max hx*hy over cells
+    int max_list_cap = 0;     // max list_cap over cells
+    int max_level_cap = 0;
+    int max_cells_per_level = 0;
+};
+
+// ORBextractor constructor tables (src/ORBextractor.cc:457-511).
+void init_extractor_tables(Geometry& g, int nfeatures, float scale_factor, int nlevels, int fast_th);
+// Per image size: level sizes, cell grid, resize coefficient tables.
+// Returns ORBX_OK or ORBX_ERR_UNSUPPORTED for sizes the reference cannot
+// handle (empty cell grid, 2x INTER_AREA decimation).
+int compute_geometry(Geometry& g, int w, int h);
+
+// Device copies of the geometry tables.
+struct DeviceGeometry {
+    LevelGeom* levels = nullptr;
+    CellGeom* cells = nullptr;
+    ResizeCol* res_cols = nullptr;
+    ResizeRow* res_rows = nullptr;
+    int* umax = nullptr;
+};
+
+struct KernelTimer {
+    std::string name;
+    std::vector<hipEvent_t> start, stop;   // pairs recorded since reset
+    int used = 0;
+};
+
+}  // namespace orbx
+
+struct orbx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    orbx::Geometry geom;
+    orbx::DeviceGeometry dgeom;
+    int max_w = 0, max_h = 0, slots = 0;
+    int geom_w = -1, geom_h = -1;   // size the device tables describe
+    // device buffers
+    uint8_t* frames = nullptr;
+    uint8_t* pyr_raw = nullptr;
+    uint8_t* pyr_blur = nullptr;
+    uint32_t* cell_lists = nullptr;
+    int32_t* cell_count = nullptr;
+    uint32_t* level_keys = nullptr;
+    int32_t* level_count = nullptr;
+    orbx_keypoint* out_kps = nullptr;
+    uint8_t* out_desc = nullptr;
+    int32_t* out_n = nullptr;
+    int32_t* match12 = nullptr;
+    int32_t* match_n = nullptr;
+    int32_t* error_flags = nullptr;   // kernel-side overflow / invariant flags
+    // capacities the buffers were allocated for
+    long long cap_frame_px = 0;
+    long long cap_pyr_bytes = 0;
+    long long cap_list_entries = 0;
+    long long cap_level_entries = 0;
+    int cap_cells = 0;
+    int cap_res_cols = 0, cap_res_rows = 0, cap_blur_tiles = 0;
+    int4* blur_tiles = nullptr;        // (level, x0, y0, -) blur work tiles
+    int blur_tiles_n = 0;
+    int last_first = 0, last_count = 0;   // batch of the most recent extract
+    // generic scratch for the one-shot matcher / BA entry points
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    void* host_pinned = nullptr;
+    size_t host_pinned_bytes = 0;
+    // timing
+    bool timing = false;
+    std::vector<orbx::KernelTimer> timers;
+};
+
+namespace orbx {
+// orbx_extract.hip
+int launch_extract(orbx_ctx* ctx, int first, int count);
+// orbx_match.hip
+int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window,
+                      float nnratio, int check_ori);
+// timing helpers (orbx_api.cpp)
+void timer_begin(orbx_ctx* ctx, const char* name);
+void timer_end(orbx_ctx* ctx, const char* name);
+int ensure_scratch(orbx_ctx* ctx, size_t bytes);
+int ensure_pinned(orbx_ctx* ctx, size_t bytes);
+}  // namespace orbx
+
+#define ORBX_HIP_CHECK(expr)                              \
+    do {                                                  \
+        hipError_t _e = (expr);                           \
+        if (_e != hipSuccess) return ORBX_ERR_HIP;        \
+    } while (0)

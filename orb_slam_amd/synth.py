@@ -1,0 +1,61 @@
+"""Deterministic synthetic mono8 inputs.
+
+The reference ships no images (its example rosbag is an external download,
+README.md:150), so tests and the benchmark use generated frames:
+
+* texture_frame -- smoothed uniform noise, contrast-stretched, plus random
+  axis-aligned rectangles: FAST density of a few percent with saturated and
+  starved cells.
+* noise_frame   -- pure uniform noise (FAST fires almost everywhere).
+* flat_frame    -- constant 128 (FAST finds nothing: threshold-7 fallback and
+  the empty-level paths).
+* sequence      -- "TUM-style" camera motion: frame k is a w x h window of a
+  larger texture shifted by (2k mod 40, k mod 20) pixels.
+"""
+import numpy as np
+
+
+def _rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def _box5(a):
+    """5x5 box mean with edge replication (float64)."""
+    p = np.pad(a.astype(np.float64), 2, mode="edge")
+    c = np.cumsum(np.cumsum(p, axis=0), axis=1)
+    c = np.pad(c, ((1, 0), (1, 0)))
+    h, w = a.shape
+    s = c[5:5 + h, 5:5 + w] - c[0:h, 5:5 + w] - c[5:5 + h, 0:w] + c[0:h, 0:w]
+    return s / 25.0
+
+
+def texture_frame(w, h, seed, n_rects=200):
+    r = _rng(seed)
+    base = _box5(r.integers(0, 256, size=(h, w)))
+    lo, hi = base.min(), base.max()
+    img = ((base - lo) * (255.0 / max(hi - lo, 1e-9))).astype(np.uint8)
+    for _ in range(n_rects):
+        x0 = int(r.integers(0, w))
+        y0 = int(r.integers(0, h))
+        rw = int(r.integers(4, max(5, w // 8)))
+        rh = int(r.integers(4, max(5, h // 8)))
+        img[y0:y0 + rh, x0:x0 + rw] = np.uint8(r.integers(0, 256))
+    return img
+
+
+def noise_frame(w, h, seed):
+    return _rng(seed).integers(0, 256, size=(h, w), dtype=np.uint8)
+
+
+def flat_frame(w, h, value=128):
+    return np.full((h, w), value, dtype=np.uint8)
+
+
+def sequence(w, h, n_frames, seed):
+    """n_frames x h x w uint8 frames of one synthetic camera sequence."""
+    big = texture_frame(w + 40, h + 20, seed, n_rects=260)
+    out = np.empty((n_frames, h, w), dtype=np.uint8)
+    for k in range(n_frames):
+        dx, dy = (2 * k) % 40, k % 20
+        out[k] = big[dy:dy + h, dx:dx + w]
+    return out

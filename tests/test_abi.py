@@ -1,0 +1,45 @@
+"""The C-ABI library loads and exports every entry point include/orbx.h
+declares (no compute calls: runs without a GPU)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+import orb_slam_amd as ox
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_functions():
+    text = (ROOT / "include" / "orbx.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(orbx_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ["orbx_create", "orbx_extract", "orbx_dev_extract", "orbx_search_for_initialization",
+                 "orbx_hamming_bf", "orbx_lba_solve", "orbx_window_search"]:
+        assert must in names
+
+
+def test_library_exports_all_declared_symbols():
+    lib = ox.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_version_string():
+    assert b"gfx950" in ox.lib().orbx_version()
+
+
+def test_keypoint_layout_is_cv_keypoint():
+    assert ox.KEYPOINT.itemsize == 28
+    assert list(ox.KEYPOINT.names) == ["x", "y", "size", "angle", "response", "octave", "class_id"]
+
+
+def test_descriptor_distance_host_entry():
+    a = (ctypes.c_uint8 * 32)(*([0xFF] * 32))
+    b = (ctypes.c_uint8 * 32)(*([0x0F] * 32))
+    assert ox.lib().orbx_descriptor_distance(a, b) == 128

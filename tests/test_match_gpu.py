@@ -1,0 +1,50 @@
+"""GPU parity of ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:
+598-713) on consecutive frames of a synthetic sequence.  The oracle runs on
+the GPU-extracted features (themselves checked bit-exact in
+test_extract_gpu.py), so this isolates the greedy matcher replay."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth
+from oracle_lib import load, ptr
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_search_init(L, k1, d1, k2, d2, w, h, window=100, nnratio=0.9, check_ori=True):
+    F1 = ox.frame_view(k1, d1, w, h)
+    F2 = ox.frame_view(k2, d2, w, h)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32).copy()
+    m12 = np.zeros(len(k1), np.int32)
+    nm = ctypes.c_int()
+    assert L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), ptr(prev), ptr(m12),
+                                                window, nnratio, int(check_ori), ctypes.byref(nm)) == 0
+    return m12, nm.value
+
+
+@pytest.mark.parametrize("n,seq_len", [(1000, 8), (2000, 5)])
+def test_match_prev_matches_oracle(n, seq_len):
+    w, h = 640, 480
+    frames = synth.sequence(w, h, seq_len, seed=21 + n)
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_prev(0, seq_len, seq_len, window=100, nnratio=0.9, check_ori=True)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    total = 0
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        k1, d1 = feats[p]
+        k2, d2 = feats[s]
+        rm, rn = ref_search_init(L, k1, d1, k2, d2, w, h)
+        gm, gn = ctx.matches(s)
+        assert gn == rn, (s, gn, rn)
+        assert np.array_equal(gm[:len(k1)], rm), (s, np.count_nonzero(gm[:len(k1)] != rm))
+        total += gn
+    assert total > 0
+    ctx.close()
