@@ -526,18 +526,20 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
     for (int b0 = 0; b0 < count; b0 += ctx->slots) {
         const int nb = min(ctx->slots, count - b0);
         a.first_slot = first + b0;
-        timer_begin(ctx, "pyramid");
+        timer_begin(ctx, "pyr0");
         {
             const LevelGeom& L = g.levels[0];
             const int words = (L.stride / 4) * L.ph;
             hipLaunchKernelGGL(k_pyr_level0, dim3((words + 255) / 256, nb), dim3(256), 0, st, a);
         }
+        timer_end(ctx, "pyr0");
         for (int l = 1; l < g.nlevels; l++) {
             const LevelGeom& L = g.levels[l];
             const int words = (L.stride / 4) * L.ph;
+            timer_begin(ctx, "resize");
             hipLaunchKernelGGL(k_pyr_resize, dim3((words + 255) / 256, nb), dim3(256), 0, st, a, l);
+            timer_end(ctx, "resize");
         }
-        timer_end(ctx, "pyramid");
         timer_begin(ctx, "fast");
         {
             const int pitch = (g.max_tile_bytes + 15) & ~15;
