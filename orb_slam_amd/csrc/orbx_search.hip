@@ -1,0 +1,725 @@
+// Host-pointer entry points of the ORBmatcher searches (include/orbx.h,
+// section B): frames are uploaded, one wave replays the reference's greedy
+// query loop on the device, results come back.  Also the all-pairs Hamming
+// kernel (brute-force matching, C3).
+//
+// Candidate order everywhere is Frame::GetFeaturesInArea order (cell x, then
+// cell y, then keypoint index; src/Frame.cc:232-257) and ties resolve to the
+// earliest candidate, as the reference's strict `<` comparisons do.  The
+// second-best of a query is the earliest candidate holding the minimum over
+// all admissible candidates except the best one.
+#include <vector>
+
+#include "orbx_match_common.h"
+
+namespace orbx {
+
+// LDS candidate table over all keypoints of the searched frame.
+struct CandTab {
+    float* x;
+    float* y;
+    int* cell_oct;   // cell (or -1) | octave << 16
+    int* taken;      // assignment state (-1 free)
+};
+
+__device__ inline void carve_tab(uint8_t* base, int cap, CandTab& t)
+{
+    t.x = reinterpret_cast<float*>(base);
+    t.y = t.x + cap;
+    t.cell_oct = reinterpret_cast<int*>(t.y + cap);
+    t.taken = t.cell_oct + cap;
+}
+
+__device__ inline void fill_tab(const FrameDev& F, const uint8_t* assigned, CandTab& t)
+{
+    for (int i = threadIdx.x; i < F.n; i += 64) {
+        const orbx_keypoint k = F.kps[i];
+        t.x[i] = k.x;
+        t.y[i] = k.y;
+        const int cell = grid_cell(F, k.x, k.y);
+        t.cell_oct[i] = (cell & 0xFFFF) | (k.octave << 16);
+        t.taken[i] = (assigned && assigned[i]) ? -2 : -1;
+    }
+    wave_sync();
+}
+
+struct LevelFilter {
+    bool check, same;
+    int lo, hi;
+};
+
+__device__ inline LevelFilter level_filter(int minLevel, int maxLevel)
+{
+    LevelFilter f;
+    f.check = !(minLevel == -1 && maxLevel == -1);
+    f.same = f.check && (minLevel == maxLevel);
+    f.lo = minLevel;
+    f.hi = maxLevel;
+    return f;
+}
+
+__device__ inline bool level_ok(const LevelFilter& f, int oct)
+{
+    if (f.check && !f.same) return !(oct < f.lo || oct > f.hi);
+    if (f.same) return oct == f.lo;
+    return true;
+}
+
+// best and second keys (dist << 32 | cell << 12 | index) over admissible
+// candidates: inside the area, level filter passed, not taken.
+struct Best2 {
+    unsigned long long best, second;
+    bool any;   // GetFeaturesInArea returned something (before `taken`)
+};
+
+__device__ inline Best2 eval_query(const CandTab& t, int n, const AreaQuery& q, float qx, float qy, float r,
+                                   const LevelFilter& lf, const uint4& d1a, const uint4& d1b,
+                                   const uint8_t* desc2)
+{
+    Best2 res;
+    unsigned long long best = ~0ull;
+    int any = 0;
+    for (int j = threadIdx.x; j < n; j += 64) {
+        const int co = t.cell_oct[j];
+        const int cell = (co & 0xFFFF) == 0xFFFF ? -1 : (co & 0xFFFF);
+        if (!level_ok(lf, co >> 16)) continue;
+        if (!in_area(q, cell, t.x[j], t.y[j], qx, qy, r)) continue;
+        any = 1;
+        if (t.taken[j] != -1) continue;
+        uint4 a, b;
+        load_desc(desc2 + (size_t)j * 32, a, b);
+        const unsigned long long key = ((unsigned long long)hamming256(d1a, d1b, a, b) << 32) |
+                                       ((unsigned long long)cell << 12) | (unsigned long long)j;
+        best = key < best ? key : best;
+    }
+    res.any = __any(any);
+    best = wave_min_u64(best);
+    unsigned long long second = ~0ull;
+    if (best != ~0ull) {
+        const int bj = (int)(best & 0xFFF);
+        for (int j = threadIdx.x; j < n; j += 64) {
+            if (j == bj) continue;
+            const int co = t.cell_oct[j];
+            const int cell = (co & 0xFFFF) == 0xFFFF ? -1 : (co & 0xFFFF);
+            if (!level_ok(lf, co >> 16)) continue;
+            if (!in_area(q, cell, t.x[j], t.y[j], qx, qy, r)) continue;
+            if (t.taken[j] != -1) continue;
+            uint4 a, b;
+            load_desc(desc2 + (size_t)j * 32, a, b);
+            const unsigned long long key = ((unsigned long long)hamming256(d1a, d1b, a, b) << 32) |
+                                           ((unsigned long long)cell << 12) | (unsigned long long)j;
+            second = key < second ? key : second;
+        }
+        second = wave_min_u64(second);
+    }
+    res.best = best;
+    res.second = second;
+    return res;
+}
+
+__device__ inline int key_dist(unsigned long long k) { return k == ~0ull ? 0x7fffffff : (int)(k >> 32); }
+__device__ inline int key_idx(unsigned long long k) { return k == ~0ull ? -1 : (int)(k & 0xFFF); }
+
+// x3Dc = R * x3Dw + t in float, left-to-right sums; u = fx*xc*invzc + cx
+// with invzc = 1.0/zc evaluated in double (src/ORBmatcher.cc:541-549).
+__device__ inline void project(const float* T, const float* cam, const float* X, float* u, float* v, float* zc)
+{
+    float c[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+        c[r] = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(T[4 * r], X[0]), __fmul_rn(T[4 * r + 1], X[1])),
+                                   __fmul_rn(T[4 * r + 2], X[2])),
+                         T[4 * r + 3]);
+    const float invzc = (float)(1.0 / (double)c[2]);
+    *u = __fadd_rn(__fmul_rn(__fmul_rn(cam[0], c[0]), invzc), cam[2]);
+    *v = __fadd_rn(__fmul_rn(__fmul_rn(cam[1], c[1]), invzc), cam[3]);
+    *zc = c[2];
+}
+
+// Rotation-consistency filter over entries pushed[i] = bin (or -1) of the
+// keys listed in order; resets out[key[i]] when its bin is not a top-3 bin.
+__device__ inline int rotation_filter(const signed char* bins, const int* keys, int npushed, int32_t* out,
+                                      int* hist)
+{
+    int removed = 0;
+    for (int b = 0; b < kHistoLength; b++) hist[b] = 0;
+    for (int i = 0; i < npushed; i++) hist[bins[i]]++;
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    for (int i = 0; i < npushed; i++) {
+        const int b = bins[i];
+        if (b == ind1 || b == ind2 || b == ind3) continue;
+        out[keys[i]] = -1;
+        removed++;
+    }
+    return removed;
+}
+
+struct SearchArgs {
+    FrameDev F1, F2;              // query frame, searched frame
+    const uint8_t* q_valid;       // per query
+    const float* q_xyz;           // per query world point (projection searches)
+    const uint8_t* f2_assigned;
+    const float* prev_xy;         // SearchForInitialization
+    float* prev_out;
+    const float* proj_xy;         // local map
+    const int32_t* pred_level;
+    const float* view_cos;
+    const uint8_t* q_desc;        // local map: map point descriptors
+    int nq;
+    float T[12];
+    float cam[4];
+    float scale[kMaxLevels];
+    int window, min_level, max_level;
+    float nnratio, th;
+    int check_ori;
+    int32_t* out;                 // result array
+    int32_t* out_n;
+};
+
+// ORBmatcher::WindowSearch (src/ORBmatcher.cc:409-516)
+__global__ __launch_bounds__(64) void k_window_search(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CandTab t;
+    carve_tab(smem, a.F2.n, t);
+    signed char* bins = reinterpret_cast<signed char*>(t.taken + a.F2.n);
+    int* keys = reinterpret_cast<int*>(bins + ((a.F2.n + 15) & ~15));
+    int* hist = keys + a.F2.n;
+    fill_tab(a.F2, nullptr, t);
+    const bool bMin = a.min_level > 0, bMax = a.max_level < 0x7fffffff;
+    int nmatches = 0, npushed = 0;
+    for (int i1 = 0; i1 < a.F1.n; i1++) {
+        if (!a.q_valid[i1]) continue;
+        const orbx_keypoint k1 = a.F1.kps[i1];
+        const int level1 = k1.octave;
+        if (bMin && level1 < a.min_level) continue;
+        if (bMax && level1 > a.max_level) continue;
+        const float r = (float)a.window;
+        const AreaQuery q = area_cells(a.F2, k1.x, k1.y, r);
+        if (q.empty) continue;
+        uint4 d1a, d1b;
+        load_desc(a.F1.desc + (size_t)i1 * 32, d1a, d1b);
+        const Best2 b = eval_query(t, a.F2.n, q, k1.x, k1.y, r, level_filter(level1, level1), d1a, d1b, a.F2.desc);
+        if (!b.any) continue;
+        const int bestDist = key_dist(b.best), bestDist2 = key_dist(b.second), bestIdx2 = key_idx(b.best);
+        if ((float)bestDist <= __fmul_rn((float)bestDist2, a.nnratio) && bestDist <= kTHHigh) {
+            if (threadIdx.x == 0) {
+                t.taken[bestIdx2] = i1;
+                a.out[bestIdx2] = i1;
+                bins[npushed] = (signed char)rot_bin(k1.angle, a.F2.kps[bestIdx2].angle);
+                keys[npushed] = bestIdx2;
+            }
+            npushed++;
+            nmatches++;
+            wave_sync();
+        }
+    }
+    wave_sync();
+    if (threadIdx.x == 0) {
+        if (a.check_ori) nmatches -= rotation_filter(bins, keys, npushed, a.out, hist);
+        *a.out_n = nmatches;
+    }
+}
+
+// ORBmatcher::SearchByProjection(Frame&, Frame&, int, vector<MapPoint*>&)
+// (src/ORBmatcher.cc:519-594)
+__global__ __launch_bounds__(64) void k_proj_pair(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CandTab t;
+    carve_tab(smem, a.F2.n, t);
+    fill_tab(a.F2, a.f2_assigned, t);
+    int nmatches = 0;
+    for (int i1 = 0; i1 < a.F1.n; i1++) {
+        if (!a.q_valid[i1]) continue;
+        const int level1 = a.F1.kps[i1].octave;
+        float u, v, zc;
+        project(a.T, a.cam, a.q_xyz + 3 * i1, &u, &v, &zc);
+        const float r = (float)a.window;
+        const AreaQuery q = area_cells(a.F2, u, v, r);
+        if (q.empty) continue;
+        uint4 d1a, d1b;
+        load_desc(a.F1.desc + (size_t)i1 * 32, d1a, d1b);
+        const Best2 b = eval_query(t, a.F2.n, q, u, v, r, level_filter(level1, level1), d1a, d1b, a.F2.desc);
+        if (!b.any) continue;
+        const int bestDist = key_dist(b.best), bestDist2 = key_dist(b.second), bestIdx2 = key_idx(b.best);
+        if ((float)bestDist <= __fmul_rn((float)bestDist2, a.nnratio) && bestDist <= kTHHigh) {
+            if (threadIdx.x == 0) {
+                t.taken[bestIdx2] = i1;
+                a.out[bestIdx2] = i1;
+            }
+            nmatches++;
+            wave_sync();
+        }
+    }
+    if (threadIdx.x == 0) *a.out_n = nmatches;
+}
+
+// ORBmatcher::SearchByProjection(Frame& Current, const Frame& Last, float th)
+// (src/ORBmatcher.cc:1507-1620).  F1 = LastFrame, F2 = CurrentFrame.
+__global__ __launch_bounds__(64) void k_proj_motion(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CandTab t;
+    carve_tab(smem, a.F2.n, t);
+    signed char* bins = reinterpret_cast<signed char*>(t.taken + a.F2.n);
+    int* keys = reinterpret_cast<int*>(bins + ((a.F2.n + 15) & ~15));
+    int* hist = keys + a.F2.n;
+    fill_tab(a.F2, a.f2_assigned, t);
+    int nmatches = 0, npushed = 0;
+    for (int i = 0; i < a.F1.n; i++) {
+        if (!a.q_valid[i]) continue;
+        float u, v, zc;
+        project(a.T, a.cam, a.q_xyz + 3 * i, &u, &v, &zc);
+        if (u < a.F2.min_x || u > a.F2.max_x) continue;
+        if (v < a.F2.min_y || v > a.F2.max_y) continue;
+        const orbx_keypoint kl = a.F1.kps[i];
+        const int oct = kl.octave;
+        const float radius = __fmul_rn(a.th, a.scale[oct]);
+        const AreaQuery q = area_cells(a.F2, u, v, radius);
+        if (q.empty) continue;
+        uint4 d1a, d1b;
+        load_desc(a.F1.desc + (size_t)i * 32, d1a, d1b);
+        const Best2 b = eval_query(t, a.F2.n, q, u, v, radius, level_filter(oct - 1, oct + 1), d1a, d1b, a.F2.desc);
+        if (!b.any) continue;
+        const int bestDist = key_dist(b.best), bestIdx2 = key_idx(b.best);
+        if (bestDist <= kTHHigh) {
+            if (threadIdx.x == 0) {
+                t.taken[bestIdx2] = i;
+                a.out[bestIdx2] = i;
+                if (a.check_ori) {
+                    bins[npushed] = (signed char)rot_bin(kl.angle, a.F2.kps[bestIdx2].angle);
+                    keys[npushed] = bestIdx2;
+                }
+            }
+            if (a.check_ori) npushed++;
+            nmatches++;
+            wave_sync();
+        }
+    }
+    wave_sync();
+    if (threadIdx.x == 0) {
+        if (a.check_ori) nmatches -= rotation_filter(bins, keys, npushed, a.out, hist);
+        *a.out_n = nmatches;
+    }
+}
+
+// ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, float)
+// (src/ORBmatcher.cc:49-125) with RadiusByViewingCos (:127-133).
+__global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CandTab t;
+    carve_tab(smem, a.F2.n, t);
+    fill_tab(a.F2, a.f2_assigned, t);
+    const bool bFactor = a.th != 1.0f;
+    int nmatches = 0;
+    for (int m = 0; m < a.nq; m++) {
+        if (!a.q_valid[m]) continue;
+        const int pred = a.pred_level[m];
+        float r = ((double)a.view_cos[m] > 0.998) ? 2.5f : 4.0f;
+        if (bFactor) r = __fmul_rn(r, a.th);
+        const float radius = __fmul_rn(r, a.scale[pred]);
+        const float qx = a.proj_xy[2 * m], qy = a.proj_xy[2 * m + 1];
+        const AreaQuery q = area_cells(a.F2, qx, qy, radius);
+        if (q.empty) continue;
+        uint4 d1a, d1b;
+        load_desc(a.q_desc + (size_t)m * 32, d1a, d1b);
+        const Best2 b = eval_query(t, a.F2.n, q, qx, qy, radius, level_filter(pred - 1, pred), d1a, d1b, a.F2.desc);
+        if (!b.any) continue;
+        const int bestDist = key_dist(b.best), bestDist2 = key_dist(b.second), bestIdx = key_idx(b.best);
+        if (bestDist <= kTHHigh) {
+            const int bestLevel = (t.cell_oct[bestIdx] >> 16);
+            const int j2 = key_idx(b.second);
+            const int bestLevel2 = j2 >= 0 ? (t.cell_oct[j2] >> 16) : -1;
+            if (bestLevel == bestLevel2 && (float)bestDist > __fmul_rn(a.nnratio, (float)bestDist2)) continue;
+            if (threadIdx.x == 0) {
+                t.taken[bestIdx] = m;
+                a.out[bestIdx] = m;
+            }
+            nmatches++;
+            wave_sync();
+        }
+    }
+    if (threadIdx.x == 0) *a.out_n = nmatches;
+}
+
+// SearchForInitialization with host inputs (prev_xy in/out).
+__global__ __launch_bounds__(64) void k_search_init_one(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CandLDS c;
+    int *m12, *hist;
+    signed char* pushed;
+    carve(smem, max(a.F2.n, 1), max(a.F1.n, 1), c, m12, pushed, hist);
+    search_for_init_wave(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n,
+                         a.prev_out, c, m12, pushed, hist);
+}
+
+// ---------------------------------------------------------------------------
+// All-pairs Hamming (B8): one thread per query row, B streamed through LDS
+// in chunks of 256 descriptors; ascending b with strict `<` keeps the
+// reference's first-index tie rule.  grid.y indexes independent pairs.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB,
+                                                    int32_t* best_idx, int32_t* best, int32_t* second,
+                                                    int32_t* m12, int th_low, float nnratio)
+{
+    __shared__ uint4 sb[256][2];
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
+    if (a < nA) load_desc(dA + (size_t)a * 32, qa, qb);
+    int b1 = 0x7fffffff, b2 = 0x7fffffff, bi = -1;
+    for (int base = 0; base < nB; base += 256) {
+        __syncthreads();
+        const int j = base + threadIdx.x;
+        if (j < nB) load_desc(dB + (size_t)j * 32, sb[threadIdx.x][0], sb[threadIdx.x][1]);
+        __syncthreads();
+        const int cnt = min(256, nB - base);
+        for (int k = 0; k < cnt; k++) {
+            const int d = hamming256(qa, qb, sb[k][0], sb[k][1]);
+            if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                bi = base + k;
+            } else if (d < b2) {
+                b2 = d;
+            }
+        }
+    }
+    if (a < nA) {
+        best_idx[a] = bi;
+        best[a] = b1;
+        second[a] = b2;
+        // C3 acceptance: best <= TH_LOW and best < nnratio * second
+        if (m12) m12[a] = (b1 <= th_low && (float)b1 < __fmul_rn((float)b2, nnratio)) ? bi : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Uploader {
+    orbx_ctx* ctx;
+    std::vector<std::pair<size_t, size_t>> parts;   // offset, bytes
+    size_t total = 0;
+    size_t reserve(size_t bytes)
+    {
+        const size_t off = total;
+        total += (bytes + 255) & ~size_t(255);
+        return off;
+    }
+    uint8_t* base() const { return static_cast<uint8_t*>(ctx->scratch); }
+};
+
+int put(orbx_ctx* ctx, size_t off, const void* src, size_t bytes)
+{
+    if (bytes == 0 || !src) return ORBX_OK;
+    ORBX_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(ctx->scratch) + off, src, bytes, hipMemcpyHostToDevice,
+                                  ctx->stream));
+    return ORBX_OK;
+}
+
+int get(orbx_ctx* ctx, void* dst, size_t off, size_t bytes)
+{
+    if (bytes == 0 || !dst) return ORBX_OK;
+    ORBX_HIP_CHECK(hipMemcpyAsync(dst, static_cast<uint8_t*>(ctx->scratch) + off, bytes, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    return ORBX_OK;
+}
+
+bool valid_view(const orbx_frame_view* v)
+{
+    return v && v->n >= 0 && v->n <= 4096 && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
+           v->max_y > v->min_y && v->nlevels > 0 && v->nlevels <= kMaxLevels;
+}
+
+FrameDev dev_frame(const orbx_frame_view* v, const uint8_t* base, size_t kp_off, size_t desc_off)
+{
+    FrameDev F;
+    F.kps = reinterpret_cast<const orbx_keypoint*>(base + kp_off);
+    F.desc = base + desc_off;
+    F.n = v->n;
+    F.min_x = v->min_x;
+    F.max_x = v->max_x;
+    F.min_y = v->min_y;
+    F.max_y = v->max_y;
+    // src/Frame.cc:76-77: FRAME_GRID_COLS / (mnMaxX - mnMinX) in float
+    F.grid_w_inv = static_cast<float>(kGridCols) / (v->max_x - v->min_x);
+    F.grid_h_inv = static_cast<float>(kGridRows) / (v->max_y - v->min_y);
+    return F;
+}
+
+void frame_scales(const orbx_frame_view* v, float* s)
+{
+    s[0] = 1.0f;
+    for (int i = 1; i < v->nlevels; i++) s[i] = s[i - 1] * v->scale_factor;   // src/Frame.cc:98-102
+}
+
+// Uploads a frame view; returns offsets.
+struct FrameOffs { size_t kp, desc; };
+
+FrameOffs reserve_frame(Uploader& u, const orbx_frame_view* v)
+{
+    FrameOffs o;
+    o.kp = u.reserve((size_t)v->n * sizeof(orbx_keypoint));
+    o.desc = u.reserve((size_t)v->n * 32);
+    return o;
+}
+
+int put_frame(orbx_ctx* ctx, const FrameOffs& o, const orbx_frame_view* v)
+{
+    int r = put(ctx, o.kp, v->keys_un, (size_t)v->n * sizeof(orbx_keypoint));
+    if (r == ORBX_OK) r = put(ctx, o.desc, v->desc, (size_t)v->n * 32);
+    return r;
+}
+
+size_t tab_lds(int n) { return (size_t)n * 16 + ((n + 15) & ~15) + (size_t)n * 4 + 32 * 4 + 64; }
+
+}  // namespace
+}  // namespace orbx
+
+using namespace orbx;
+
+extern "C" {
+
+int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_frame_view* F2,
+                                   float* prev_matched, int32_t* matches12, int window, float nnratio,
+                                   int check_ori, int* n_matches)
+{
+    if (!ctx || !valid_view(F1) || !valid_view(F2) || !prev_matched || !matches12 || !n_matches || window < 0)
+        return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
+    const size_t op = u.reserve((size_t)F1->n * 8), oo = u.reserve((size_t)F1->n * 4 + 4), on = u.reserve(4);
+    const size_t opo = u.reserve((size_t)F1->n * 8);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, op, prev_matched, (size_t)F1->n * 8)) ||
+        (r = put(ctx, opo, prev_matched, (size_t)F1->n * 8)))
+        return r;
+    SearchArgs a{};
+    a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
+    a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
+    a.prev_xy = reinterpret_cast<const float*>(u.base() + op);
+    a.prev_out = reinterpret_cast<float*>(u.base() + opo);
+    a.window = window;
+    a.nnratio = nnratio;
+    a.check_ori = check_ori;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    const size_t lds = search_init_lds_bytes(std::max(F2->n, 1), std::max(F1->n, 1));
+    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(64), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, matches12, oo, (size_t)F1->n * 4)) || (r = get(ctx, n_matches, on, 4)) ||
+        (r = get(ctx, prev_matched, opo, (size_t)F1->n * 8)))
+        return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_frame_view* F2, const uint8_t* f1_mp,
+                       int window, int min_level, int max_level, float nnratio, int check_ori, int32_t* matches21,
+                       int* n_matches)
+{
+    if (!ctx || !valid_view(F1) || !valid_view(F2) || !f1_mp || !matches21 || !n_matches || window < 0)
+        return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
+    const size_t ov = u.reserve(F1->n), oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, ov, f1_mp, F1->n))) return r;
+    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F2->n * 4 + 4, ctx->stream));
+    SearchArgs a{};
+    a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
+    a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
+    a.q_valid = u.base() + ov;
+    a.window = window;
+    a.min_level = min_level;
+    a.max_level = max_level < 0 ? 0x7fffffff : max_level;
+    a.nnratio = nnratio;
+    a.check_ori = check_ori;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    hipLaunchKernelGGL(k_window_search, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, matches21, oo, (size_t)F2->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_frame_view* F2,
+                                   const float* f1_mp_xyz, const uint8_t* f1_mp_valid, const uint8_t* f2_assigned,
+                                   const float* Tcw2, const float* cam, int window, float nnratio, int32_t* matches21,
+                                   int* n_matches)
+{
+    if (!ctx || !valid_view(F1) || !valid_view(F2) || !f1_mp_xyz || !f1_mp_valid || !f2_assigned || !Tcw2 || !cam ||
+        !matches21 || !n_matches || window < 0)
+        return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
+    const size_t ox = u.reserve((size_t)F1->n * 12), ov = u.reserve(F1->n), oa = u.reserve(F2->n);
+    const size_t oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, ox, f1_mp_xyz, (size_t)F1->n * 12)) ||
+        (r = put(ctx, ov, f1_mp_valid, F1->n)) || (r = put(ctx, oa, f2_assigned, F2->n)))
+        return r;
+    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F2->n * 4 + 4, ctx->stream));
+    SearchArgs a{};
+    a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
+    a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
+    a.q_xyz = reinterpret_cast<const float*>(u.base() + ox);
+    a.q_valid = u.base() + ov;
+    a.f2_assigned = u.base() + oa;
+    for (int i = 0; i < 12; i++) a.T[i] = Tcw2[i];
+    for (int i = 0; i < 4; i++) a.cam[i] = cam[i];
+    a.window = window;
+    a.nnratio = nnratio;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    hipLaunchKernelGGL(k_proj_pair, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, matches21, oo, (size_t)F2->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, const orbx_frame_view* Last,
+                                     const float* last_mp_xyz, const uint8_t* last_mp_valid,
+                                     const uint8_t* cur_assigned, const float* Tcw, const float* cam, float th,
+                                     int check_ori, int32_t* matches_cur, int* n_matches)
+{
+    if (!ctx || !valid_view(Cur) || !valid_view(Last) || !last_mp_xyz || !last_mp_valid || !cur_assigned || !Tcw ||
+        !cam || !matches_cur || !n_matches)
+        return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const FrameOffs oL = reserve_frame(u, Last), oC = reserve_frame(u, Cur);
+    const size_t ox = u.reserve((size_t)Last->n * 12), ov = u.reserve(Last->n), oa = u.reserve(Cur->n);
+    const size_t oo = u.reserve((size_t)Cur->n * 4 + 4), on = u.reserve(4);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put_frame(ctx, oL, Last)) || (r = put_frame(ctx, oC, Cur)) ||
+        (r = put(ctx, ox, last_mp_xyz, (size_t)Last->n * 12)) || (r = put(ctx, ov, last_mp_valid, Last->n)) ||
+        (r = put(ctx, oa, cur_assigned, Cur->n)))
+        return r;
+    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)Cur->n * 4 + 4, ctx->stream));
+    SearchArgs a{};
+    a.F1 = dev_frame(Last, u.base(), oL.kp, oL.desc);
+    a.F2 = dev_frame(Cur, u.base(), oC.kp, oC.desc);
+    a.q_xyz = reinterpret_cast<const float*>(u.base() + ox);
+    a.q_valid = u.base() + ov;
+    a.f2_assigned = u.base() + oa;
+    for (int i = 0; i < 12; i++) a.T[i] = Tcw[i];
+    for (int i = 0; i < 4; i++) a.cam[i] = cam[i];
+    frame_scales(Cur, a.scale);
+    a.th = th;
+    a.check_ori = check_ori;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    hipLaunchKernelGGL(k_proj_motion, dim3(1), dim3(64), tab_lds(std::max(Cur->n, 1)), ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, matches_cur, oo, (size_t)Cur->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int n_mp, const uint8_t* in_view,
+                                    const float* proj_xy, const int32_t* pred_level, const float* view_cos,
+                                    const uint8_t* mp_desc, const uint8_t* f_assigned, float th, float nnratio,
+                                    int32_t* matches_f, int* n_matches)
+{
+    if (!ctx || !valid_view(F) || n_mp < 0 || (n_mp > 0 && (!in_view || !proj_xy || !pred_level || !view_cos || !mp_desc)) ||
+        !f_assigned || !matches_f || !n_matches)
+        return ORBX_ERR_ARG;
+    for (int m = 0; m < n_mp; m++)
+        if (in_view[m] && (pred_level[m] < 0 || pred_level[m] >= F->nlevels)) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const FrameOffs oF = reserve_frame(u, F);
+    const size_t ov = u.reserve(n_mp), op = u.reserve((size_t)n_mp * 8), ol = u.reserve((size_t)n_mp * 4);
+    const size_t oc = u.reserve((size_t)n_mp * 4), od = u.reserve((size_t)n_mp * 32), oa = u.reserve(F->n);
+    const size_t oo = u.reserve((size_t)F->n * 4 + 4), on = u.reserve(4);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put_frame(ctx, oF, F)) || (r = put(ctx, ov, in_view, n_mp)) || (r = put(ctx, op, proj_xy, (size_t)n_mp * 8)) ||
+        (r = put(ctx, ol, pred_level, (size_t)n_mp * 4)) || (r = put(ctx, oc, view_cos, (size_t)n_mp * 4)) ||
+        (r = put(ctx, od, mp_desc, (size_t)n_mp * 32)) || (r = put(ctx, oa, f_assigned, F->n)))
+        return r;
+    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F->n * 4 + 4, ctx->stream));
+    SearchArgs a{};
+    a.F2 = dev_frame(F, u.base(), oF.kp, oF.desc);
+    a.nq = n_mp;
+    a.q_valid = u.base() + ov;
+    a.proj_xy = reinterpret_cast<const float*>(u.base() + op);
+    a.pred_level = reinterpret_cast<const int32_t*>(u.base() + ol);
+    a.view_cos = reinterpret_cast<const float*>(u.base() + oc);
+    a.q_desc = u.base() + od;
+    a.f2_assigned = u.base() + oa;
+    frame_scales(F, a.scale);
+    a.th = th;
+    a.nnratio = nnratio;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    hipLaunchKernelGGL(k_proj_local, dim3(1), dim3(64), tab_lds(std::max(F->n, 1)), ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, matches_f, oo, (size_t)F->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
+                           int32_t* best, int32_t* second, int32_t* m12, int th_low, float nnratio)
+{
+    if (!ctx || nA < 0 || nB < 0 || (nA && (!dA || !best_idx || !best || !second)) || (nB && !dB)) return ORBX_ERR_ARG;
+    if (nA == 0) return ORBX_OK;
+    hipSetDevice(ctx->device);
+    Uploader u{ctx};
+    const size_t oa = u.reserve((size_t)nA * 32), ob = u.reserve((size_t)nB * 32);
+    const size_t oi = u.reserve((size_t)nA * 4), o1 = u.reserve((size_t)nA * 4), o2 = u.reserve((size_t)nA * 4);
+    const size_t om = u.reserve((size_t)nA * 4);
+    int r = ensure_scratch(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    if ((r = put(ctx, oa, dA, (size_t)nA * 32)) || (r = put(ctx, ob, dB, (size_t)nB * 32))) return r;
+    uint8_t* base = u.base();
+    hipLaunchKernelGGL(k_hamming_bf, dim3((nA + 255) / 256), dim3(256), 0, ctx->stream, base + oa, nA, base + ob, nB,
+                       reinterpret_cast<int32_t*>(base + oi), reinterpret_cast<int32_t*>(base + o1),
+                       reinterpret_cast<int32_t*>(base + o2), m12 ? reinterpret_cast<int32_t*>(base + om) : nullptr,
+                       th_low, nnratio);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = get(ctx, best_idx, oi, (size_t)nA * 4)) || (r = get(ctx, best, o1, (size_t)nA * 4)) ||
+        (r = get(ctx, second, o2, (size_t)nA * 4)) || (r = get(ctx, m12, om, (size_t)nA * 4)))
+        return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+int orbx_hamming_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
+                    int32_t* best, int32_t* second)
+{
+    return hamming_bf_impl(ctx, dA, nA, dB, nB, best_idx, best, second, nullptr, 0, 0.f);
+}
+
+// Brute-force matcher (C3): best <= th_low && best < nnratio * second.
+int orbx_match_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, int nB, int th_low, float nnratio,
+                  int32_t* m12, int* n_matches)
+{
+    if (!m12 || !n_matches || nA < 0) return ORBX_ERR_ARG;
+    std::vector<int32_t> bi(nA), b1(nA), b2(nA);
+    int r = hamming_bf_impl(ctx, dA, nA, dB, nB, bi.data(), b1.data(), b2.data(), m12, th_low, nnratio);
+    if (r != ORBX_OK) return r;
+    int n = 0;
+    for (int a = 0; a < nA; a++) n += m12[a] >= 0;
+    *n_matches = n;
+    return ORBX_OK;
+}
+
+}  // extern "C"
