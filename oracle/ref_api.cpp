@@ -245,3 +245,70 @@ int orbx_ref_hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB, in
 }
 
 }  // extern "C"
+
+// ---- local BA ----
+#include "ref_lba.h"
+
+extern "C" int orbx_ref_lba(orbx_ba_problem* p, int iters0, int iters1, uint8_t* edge_status, uint8_t* point_bad,
+                            orbx_ba_stats* stats)
+{
+    LBAInput in;
+    in.n_poses = p->n_poses;
+    in.n_points = p->n_points;
+    in.n_edges = p->n_edges;
+    in.poses.resize(p->n_poses);
+    for (int i = 0; i < p->n_poses; i++) {
+        in.poses[i].q = {p->pose_q[4 * i], p->pose_q[4 * i + 1], p->pose_q[4 * i + 2], p->pose_q[4 * i + 3]};
+        for (int k = 0; k < 3; k++) in.poses[i].t[k] = p->pose_t[3 * i + k];
+    }
+    in.pose_fixed.assign(p->pose_fixed, p->pose_fixed + p->n_poses);
+    in.pose_id.assign(p->pose_id, p->pose_id + p->n_poses);
+    in.pose_cam.assign(p->pose_cam, p->pose_cam + 4 * p->n_poses);
+    in.points.assign(p->points, p->points + 3 * p->n_points);
+    in.point_id.assign(p->point_id, p->point_id + p->n_points);
+    in.point_nobs.assign(p->point_nobs, p->point_nobs + p->n_points);
+    in.edge_point.assign(p->edge_point, p->edge_point + p->n_edges);
+    in.edge_pose.assign(p->edge_pose, p->edge_pose + p->n_edges);
+    in.edge_obs.assign(p->edge_obs, p->edge_obs + 2 * p->n_edges);
+    in.edge_inv_sigma2.assign(p->edge_inv_sigma2, p->edge_inv_sigma2 + p->n_edges);
+    in.huber_delta = p->huber_delta;
+    in.chi2_threshold = p->chi2_threshold;
+    std::vector<uint8_t> es, pb;
+    LBAStats st;
+    local_ba(in, iters0, iters1, es, pb, st);
+    for (int i = 0; i < p->n_poses; i++) {
+        p->pose_q[4 * i] = in.poses[i].q.x;
+        p->pose_q[4 * i + 1] = in.poses[i].q.y;
+        p->pose_q[4 * i + 2] = in.poses[i].q.z;
+        p->pose_q[4 * i + 3] = in.poses[i].q.w;
+        for (int k = 0; k < 3; k++) p->pose_t[3 * i + k] = in.poses[i].t[k];
+    }
+    std::memcpy(p->points, in.points.data(), in.points.size() * sizeof(double));
+    std::memcpy(edge_status, es.data(), es.size());
+    std::memcpy(point_bad, pb.data(), pb.size());
+    if (stats) {
+        for (int k = 0; k < 2; k++) {
+            stats->iterations[k] = st.iterations[k];
+            stats->levenberg_trials[k] = st.trials[k];
+            stats->chi2_initial[k] = st.chi2_initial[k];
+            stats->chi2_final[k] = st.chi2_final[k];
+            stats->n_outliers[k] = st.n_outliers[k];
+        }
+        stats->not_posdef = st.not_posdef;
+    }
+    return ORBX_OK;
+}
+
+// SE3 primitives for unit tests
+extern "C" void orbx_ref_se3_exp(const double* u, double* q, double* t)
+{
+    SE3 s = se3_exp(u);
+    q[0] = s.q.x; q[1] = s.q.y; q[2] = s.q.z; q[3] = s.q.w;
+    for (int k = 0; k < 3; k++) t[k] = s.t[k];
+}
+
+extern "C" void orbx_ref_quat_from_matrix(const double* R, double* q)
+{
+    Quat r = quat_from_matrix(R);
+    q[0] = r.x; q[1] = r.y; q[2] = r.z; q[3] = r.w;
+}

@@ -1,0 +1,966 @@
+// Local bundle adjustment on MI355X (FP64): the inner loop of
+// Optimizer::LocalBundleAdjustment (src/Optimizer.cc:287-536) on the g2o
+// subset it uses (BlockSolverX + Schur over the points, Levenberg).
+//
+// Device work per LM iteration (one 256-thread workgroup per problem, one
+// launch per iteration so the caller's abort flag is polled between
+// iterations exactly where SparseOptimizer::optimize polls terminate()):
+//   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2
+//   linearize EdgeSE3ProjectXYZ::linearizeOplus + constructQuadraticForm per
+//             edge into SoA contribution rows; segmented reductions per pose
+//             (Hpp, bp) and per point (Hll, bl) in g2o's edge order
+//   trial     Schur: per point Dinv, db, B*Dinv, B*db; per upper 6x6 block of
+//             the reduced camera system, the landmark-ordered sum of
+//             B_i Dinv B_j^T; dense LLT of the reduced system (LDS when it
+//             fits); back-substitution for the points; exp-map update;
+//             accept / reject with g2o's rho rule
+//   Raul stop rule (levenberg.cpp:154-161)
+// Index structures (g2o's initializeOptimization / buildStructure) are built
+// on the host once per optimize() call.
+#include <algorithm>
+#include <cmath>
+#include <cstddef>
+#include <cstring>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+
+namespace orbx {
+
+struct LbaDev {
+    int nP, nL, nE, nblk;          // free poses, active points, active edges, Schur blocks
+    int nposes_all, npoints_all, nedges_all;
+    int dim_p;                     // 6 * nP
+    double* pose;                  // [nposes_all][7]: qx qy qz qw tx ty tz
+    double* point;                 // [npoints_all][3]
+    double* pose_bk;
+    double* point_bk;
+    const double* cam;             // [nposes_all][4]
+    // active edges in g2o order (SoA over active index)
+    const int* e_orig;             // original edge index
+    const int* e_pose;             // pose index
+    const int* e_point;            // point index
+    const int* e_ph;               // pose hessian index or -1 (fixed)
+    const int* e_lh;               // point hessian index
+    const double* e_obs;           // [nE][2]
+    const double* e_isig;          // [nE]
+    double* err;                   // [nedges_all][2] last computed errors (original index)
+    const int* iv_pose;            // [nP]
+    const int* iv_point;           // [nL]
+    const int* pe_ptr; const int* pe_idx;   // per free pose: active edges, edge order
+    const int* le_ptr; const int* le_idx;   // per point: active edges, edge order
+    const int* lc_ptr; const int* lc_idx;   // per point: Schur column (free poses, pose order)
+    const int* pc_ptr; const int* pc_idx;   // per free pose: Schur-column edges, landmark order
+    const int* blk_ij;             // [nblk][2]
+    const int* blk_ptr;            // [nblk+1]
+    const int* blk_c;              // [..][2] active-edge pairs, landmark order
+    // scratch
+    double* ce;                    // [nE][54]: Hpp 21 | bp 6 | Hll 6 | bl 3 | Hpl 18
+    double* eb;                    // [nE][24]: B*Dinv 18 | B*db 6
+    double* hp;                    // [nP][27]: Hpp upper 21 | bp 6
+    double* hl;                    // [nL][9]: Hll upper 6 | bl 3
+    double* dl;                    // [nL][12]: Dinv 9 | db 3
+    double* S;                     // [dim_p][dim_p] (global fallback)
+    double* x;                     // [dim_p + 3 nL]
+    double* bs;                    // [dim_p]
+    double huber_delta;
+    // LM state
+    double lambda, ni, current_chi, last_chi, chi2_initial;
+    int nBad, status, iterations, trials, not_posdef;
+    int abort;
+};
+
+enum { kRunning = 0, kTerminated = 1 };
+
+// ---------------------------------------------------------------------------
+// SE3 / quaternion primitives (g2o se3quat.h with Eigen's formulas)
+// ---------------------------------------------------------------------------
+struct Q { double x, y, z, w; };
+
+__device__ inline void qrot(const Q& q, const double v[3], double o[3])
+{
+    double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+    for (int i = 0; i < 3; i++) uv[i] += uv[i];
+    const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
+    for (int i = 0; i < 3; i++) o[i] = v[i] + q.w * uv[i] + c[i];
+}
+
+__device__ inline Q qmul(const Q& a, const Q& b)
+{
+    Q r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+__device__ inline void qmat(const Q& q, double R[9])
+{
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+__device__ inline Q qfrom(const double m[9])
+{
+    Q q;
+    double t = m[0] + m[4] + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (m[7] - m[5]) * t;
+        q.y = (m[2] - m[6]) * t;
+        q.z = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        c[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        c[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+        q.x = c[0];
+        q.y = c[1];
+        q.z = c[2];
+    }
+    return q;
+}
+
+__device__ inline void qnormalize(Q& q)
+{
+    if (q.w < 0) {
+        q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w;
+    }
+    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x /= n; q.y /= n; q.z /= n; q.w /= n;
+}
+
+// VertexSE3Expmap::oplusImpl: estimate = SE3Quat::exp(update) * estimate
+__device__ inline void se3_oplus(double* pose, const double* u)
+{
+    const double om[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
+    const double theta = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    const double O[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};
+    double O2[9], R[9], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) O2[i * 3 + j] = O[i * 3] * O[j] + O[i * 3 + 1] * O[3 + j] + O[i * 3 + 2] * O[6 + j];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i];
+        for (int i = 0; i < 9; i++) V[i] = R[i];
+    } else {
+        const double s = sin(theta), c = cos(theta);
+        const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / pow(theta, 3);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4 == 0 ? 1.0 : 0.0);
+            R[i] = I + a * O[i] + b * O2[i];
+            V[i] = I + b * O[i] + d * O2[i];
+        }
+    }
+    Q eq = qfrom(R);
+    double et[3];
+    for (int i = 0; i < 3; i++) et[i] = V[i * 3] * up[0] + V[i * 3 + 1] * up[1] + V[i * 3 + 2] * up[2];
+    qnormalize(eq);
+    // (exp) * estimate  (SE3Quat::operator*)
+    const Q pq{pose[0], pose[1], pose[2], pose[3]};
+    const double pt[3] = {pose[4], pose[5], pose[6]};
+    double rt[3];
+    qrot(eq, pt, rt);
+    Q nq = qmul(eq, pq);
+    qnormalize(nq);
+    pose[0] = nq.x; pose[1] = nq.y; pose[2] = nq.z; pose[3] = nq.w;
+    for (int i = 0; i < 3; i++) pose[4 + i] = et[i] + rt[i];
+}
+
+__device__ inline void se3_map(const double* pose, const double* p, double* o)
+{
+    const Q q{pose[0], pose[1], pose[2], pose[3]};
+    qrot(q, p, o);
+    for (int i = 0; i < 3; i++) o[i] += pose[4 + i];
+}
+
+// ---------------------------------------------------------------------------
+// Block reductions in double
+// ---------------------------------------------------------------------------
+struct DScratch {
+    double w[kWaves];
+    double v[4];
+    int iv[4];
+};
+
+__device__ inline double wave_sum_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ inline double wave_max_d(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ inline double block_sum_d(double v, DScratch& s)
+{
+    v = wave_sum_d(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0;
+    for (int i = 0; i < kWaves; i++) t += s.w[i];
+    return t;
+}
+
+__device__ inline double block_max_d(double v, DScratch& s)
+{
+    v = wave_max_d(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = s.w[0];
+    for (int i = 1; i < kWaves; i++) t = fmax(t, s.w[i]);
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// Phases
+// ---------------------------------------------------------------------------
+__device__ inline void huber(double e2, double delta, double* rho0, double* rho1)
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) {
+        *rho0 = e2;
+        *rho1 = 1.;
+    } else {
+        const double sq = sqrt(e2);
+        *rho0 = 2 * sq * delta - dsqr;
+        *rho1 = delta / sq;
+    }
+}
+
+__device__ inline double edge_chi2(const LbaDev& P, int a)
+{
+    const int e = P.e_orig[a];
+    const double s = P.e_isig[a];
+    const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+    return e0 * (s * e0) + e1 * (s * e1);
+}
+
+// computeActiveErrors + activeRobustChi2
+__device__ double compute_errors(LbaDev& P, DScratch& sc)
+{
+    double part = 0;
+    for (int a = threadIdx.x; a < P.nE; a += kBlock) {
+        const int e = P.e_orig[a];
+        double pc[3];
+        se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
+        const double* c = P.cam + 4 * P.e_pose[a];
+        const double u = pc[0] / pc[2] * c[0] + c[2];
+        const double v = pc[1] / pc[2] * c[1] + c[3];
+        P.err[2 * e] = P.e_obs[2 * a] - u;
+        P.err[2 * e + 1] = P.e_obs[2 * a + 1] - v;
+        double r0, r1;
+        huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
+        part += r0;
+    }
+    __syncthreads();
+    return block_sum_d(part, sc);
+}
+
+// linearizeOplus + constructQuadraticForm contributions per edge
+__device__ void linearize(LbaDev& P)
+{
+    for (int a = threadIdx.x; a < P.nE; a += kBlock) {
+        const double* T = P.pose + 7 * P.e_pose[a];
+        double pc[3];
+        se3_map(T, P.point + 3 * P.e_point[a], pc);
+        const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+        const double* c = P.cam + 4 * P.e_pose[a];
+        const double fx = c[0], fy = c[1];
+        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+        double R[9];
+        qmat(Q{T[0], T[1], T[2], T[3]}, R);
+        const double s = -1. / z;
+        double A[6], B[12];
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++)
+                A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
+        B[0] = x * y / z_2 * fx;
+        B[1] = -(1 + (x * x / z_2)) * fx;
+        B[2] = y / z * fx;
+        B[3] = -1. / z * fx;
+        B[4] = 0;
+        B[5] = x / z_2 * fx;
+        B[6] = (1 + y * y / z_2) * fy;
+        B[7] = -x * y / z_2 * fy;
+        B[8] = -x / z * fy;
+        B[9] = 0;
+        B[10] = -1. / z * fy;
+        B[11] = y / z_2 * fy;
+        const int e = P.e_orig[a];
+        const double sg = P.e_isig[a];
+        double r0, r1;
+        huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
+        const double w = r1 * sg;
+        const double om0 = -(sg * P.err[2 * e]) * r1, om1 = -(sg * P.err[2 * e + 1]) * r1;
+        double* ce = P.ce + 54 * (size_t)a;
+        int k = 0;
+        for (int i = 0; i < 6; i++)
+            for (int j = i; j < 6; j++) ce[k++] = (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
+        for (int i = 0; i < 6; i++) ce[21 + i] = B[i] * om0 + B[6 + i] * om1;
+        k = 27;
+        for (int i = 0; i < 3; i++)
+            for (int j = i; j < 3; j++) ce[k++] = (A[i] * w) * A[j] + (A[3 + i] * w) * A[3 + j];
+        for (int i = 0; i < 3; i++) ce[33 + i] = A[i] * om0 + A[3 + i] * om1;
+        for (int i = 0; i < 6; i++)
+            for (int j = 0; j < 3; j++) ce[36 + i * 3 + j] = (B[i] * w) * A[j] + (B[6 + i] * w) * A[3 + j];
+    }
+    __syncthreads();
+    // per free pose: Hpp (21) + bp (6), summed in edge order; one lane per value
+    for (int item = threadIdx.x; item < P.nP * 27; item += kBlock) {
+        const int p = item / 27, v = item - p * 27;
+        double acc = 0;
+        for (int q = P.pe_ptr[p]; q < P.pe_ptr[p + 1]; q++) acc += P.ce[54 * (size_t)P.pe_idx[q] + v];
+        P.hp[27 * p + v] = acc;
+    }
+    // per point: Hll (6) + bl (3) in edge order
+    for (int item = threadIdx.x; item < P.nL * 9; item += kBlock) {
+        const int l = item / 9, v = item - l * 9;
+        double acc = 0;
+        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) acc += P.ce[54 * (size_t)P.le_idx[q] + 27 + v];
+        P.hl[9 * l + v] = acc;
+    }
+    __syncthreads();
+}
+
+__device__ inline int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
+__device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
+
+// One Levenberg trial: Schur complement, LLT, back-substitution, update.
+// Returns false when the reduced system is not positive definite.
+__device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
+{
+    const int n = P.dim_p;
+    // per point: D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse), db
+    for (int l = threadIdx.x; l < P.nL; l += kBlock) {
+        const double* h = P.hl + 9 * l;
+        double m[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) m[i * 3 + j] = h[i <= j ? up3(i, j) : up3(j, i)] + (i == j ? lambda : 0.0);
+        auto cof = [&](int i, int j) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            return m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
+        };
+        const double det = cof(0, 0) * m[0] + cof(1, 0) * m[3] + cof(2, 0) * m[6];
+        const double inv = 1.0 / det;
+        double* d = P.dl + 12 * l;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) d[i * 3 + j] = cof(j, i) * inv;
+        const double* bl = h + 6;
+        for (int i = 0; i < 3; i++) d[9 + i] = d[3 * i] * bl[0] + d[3 * i + 1] * bl[1] + d[3 * i + 2] * bl[2];
+        for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
+            const int a = P.lc_idx[q];
+            const double* Bi = P.ce + 54 * (size_t)a + 36;
+            double* o = P.eb + 24 * (size_t)a;
+            for (int r = 0; r < 6; r++) {
+                for (int c = 0; c < 3; c++) o[r * 3 + c] = Bi[r * 3] * d[c] + Bi[r * 3 + 1] * d[3 + c] + Bi[r * 3 + 2] * d[6 + c];
+                o[18 + r] = Bi[r * 3] * d[9] + Bi[r * 3 + 1] * d[10] + Bi[r * 3 + 2] * d[11];
+            }
+        }
+    }
+    for (int i = threadIdx.x; i < n * n; i += kBlock) S[i] = 0.0;   // blocks without shared points
+    __syncthreads();
+    // reduced camera system, upper 6x6 blocks: Hpp (+lambda) - sum_l B_i Dinv B_j^T
+    for (int item = threadIdx.x; item < P.nblk * 36; item += kBlock) {
+        const int bk = item / 36, rc = item - bk * 36, r = rc / 6, c = rc - (rc / 6) * 6;
+        const int i1 = P.blk_ij[2 * bk], i2 = P.blk_ij[2 * bk + 1];
+        double acc = 0;
+        if (i1 == i2) acc = P.hp[27 * i1 + (r <= c ? up6(r, c) : up6(c, r))] + (r == c ? lambda : 0.0);
+        for (int q = P.blk_ptr[bk]; q < P.blk_ptr[bk + 1]; q++) {
+            const int e1 = P.blk_c[2 * q], e2 = P.blk_c[2 * q + 1];
+            const double* BD = P.eb + 24 * (size_t)e1 + r * 3;
+            const double* Bj = P.ce + 54 * (size_t)e2 + 36 + c * 3;
+            acc -= BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+        }
+        S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
+        S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
+    }
+    // bschur = bp - coef (coef summed in landmark order)
+    for (int item = threadIdx.x; item < n; item += kBlock) {
+        const int p = item / 6, r = item - p * 6;
+        double coef = 0;
+        for (int q = P.pc_ptr[p]; q < P.pc_ptr[p + 1]; q++) coef += P.eb[24 * (size_t)P.pc_idx[q] + 18 + r];
+        P.bs[item] = P.hp[27 * p + 21 + r] - coef;
+    }
+    __syncthreads();
+    // dense LLT (right-looking), lower triangle
+    for (int k = 0; k < n; k++) {
+        if (threadIdx.x == 0) {
+            const double akk = S[(size_t)k * n + k];
+            sc.iv[0] = (akk > 0) ? 1 : 0;
+            S[(size_t)k * n + k] = (akk > 0) ? sqrt(akk) : akk;
+        }
+        __syncthreads();
+        if (!sc.iv[0]) return false;
+        const double lkk = S[(size_t)k * n + k];
+        for (int i = k + 1 + threadIdx.x; i < n; i += kBlock) S[(size_t)i * n + k] /= lkk;
+        __syncthreads();
+        const int m = n - k - 1;
+        for (int item = threadIdx.x; item < m * m; item += kBlock) {
+            const int i = k + 1 + item / m, j = k + 1 + (item - (item / m) * m);
+            if (j <= i) S[(size_t)i * n + j] -= S[(size_t)i * n + k] * S[(size_t)j * n + k];
+        }
+        __syncthreads();
+    }
+    // forward / backward substitution
+    double* xp = P.x;
+    for (int i = threadIdx.x; i < n; i += kBlock) xp[i] = P.bs[i];
+    __syncthreads();
+    for (int k = 0; k < n; k++) {
+        if (threadIdx.x == 0) xp[k] /= S[(size_t)k * n + k];
+        __syncthreads();
+        for (int i = k + 1 + threadIdx.x; i < n; i += kBlock) xp[i] -= S[(size_t)i * n + k] * xp[k];
+        __syncthreads();
+    }
+    for (int k = n - 1; k >= 0; k--) {
+        if (threadIdx.x == 0) xp[k] /= S[(size_t)k * n + k];
+        __syncthreads();
+        for (int i = threadIdx.x; i < k; i += kBlock) xp[i] -= S[(size_t)k * n + i] * xp[k];
+        __syncthreads();
+    }
+    // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i)
+    for (int l = threadIdx.x; l < P.nL; l += kBlock) {
+        const double* h = P.hl + 9 * l;
+        double cl[3] = {h[6], h[7], h[8]};
+        for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
+            const int a = P.lc_idx[q];
+            const int i1 = P.e_ph[a];
+            const double* Bi = P.ce + 54 * (size_t)a + 36;
+            for (int c = 0; c < 3; c++) {
+                double acc = 0;
+                for (int r = 0; r < 6; r++) acc += Bi[r * 3 + c] * (-xp[6 * i1 + r]);
+                cl[c] += acc;
+            }
+        }
+        const double* d = P.dl + 12 * l;
+        for (int i = 0; i < 3; i++) P.x[n + 3 * l + i] = d[3 * i] * cl[0] + d[3 * i + 1] * cl[1] + d[3 * i + 2] * cl[2];
+    }
+    __syncthreads();
+    return true;
+}
+
+// OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
+__global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
+{
+    extern __shared__ __attribute__((aligned(16))) double s_S[];
+    __shared__ DScratch sc;
+    LbaDev& P = probs[blockIdx.x];
+    if (P.status != kRunning || P.abort) return;
+    if (P.nE == 0 || P.nP + P.nL == 0) {
+        if (threadIdx.x == 0) P.status = kTerminated;
+        return;
+    }
+    const int n = P.dim_p;
+    double* S = (n * n <= lds_S_cap) ? s_S : P.S;
+    double currentChi = compute_errors(P, sc);
+    const double iniChi = currentChi;
+    if (iteration == 0 && threadIdx.x == 0) P.chi2_initial = currentChi;
+    linearize(P);
+    double lambda = P.lambda, ni = P.ni;
+    if (iteration == 0) {
+        double m = 0;
+        for (int item = threadIdx.x; item < P.nP * 6; item += kBlock)
+            m = fmax(m, fabs(P.hp[27 * (item / 6) + up6(item % 6, item % 6)]));
+        for (int item = threadIdx.x; item < P.nL * 3; item += kBlock)
+            m = fmax(m, fabs(P.hl[9 * (item / 3) + up3(item % 3, item % 3)]));
+        m = block_max_d(m, sc);
+        lambda = 1e-5 * m;
+        ni = 2;
+        if (threadIdx.x == 0) P.nBad = 0;
+    }
+    const int nx = n + 3 * P.nL;
+    double rho = 0;
+    int qmax = 0;
+    do {
+        // push
+        for (int i = threadIdx.x; i < P.nposes_all * 7; i += kBlock) P.pose_bk[i] = P.pose[i];
+        for (int i = threadIdx.x; i < P.npoints_all * 3; i += kBlock) P.point_bk[i] = P.point[i];
+        __syncthreads();
+        const bool ok2 = trial_solve(P, lambda, S, sc);
+        if (ok2) {
+            for (int p = threadIdx.x; p < P.nP; p += kBlock) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
+            for (int item = threadIdx.x; item < P.nL * 3; item += kBlock) {
+                const int l = item / 3, i = item - l * 3;
+                P.point[3 * P.iv_point[l] + i] += P.x[n + item];
+            }
+        } else {
+            for (int i = threadIdx.x; i < nx; i += kBlock) P.x[i] = 0.0;
+            if (threadIdx.x == 0) P.not_posdef++;
+        }
+        __syncthreads();
+        double tempChi = compute_errors(P, sc);
+        if (!ok2) tempChi = 1.79769313486231570815e+308;
+        // computeScale: sum_j x_j (lambda x_j + b_j)
+        double part = 0;
+        for (int j = threadIdx.x; j < nx; j += kBlock) {
+            const double bj = j < n ? P.hp[27 * (j / 6) + 21 + (j % 6)] : P.hl[9 * ((j - n) / 3) + 6 + ((j - n) % 3)];
+            part += P.x[j] * (lambda * P.x[j] + bj);
+        }
+        double scale = block_sum_d(part, sc);
+        scale += 1e-3;
+        rho = (currentChi - tempChi) / scale;
+        const bool accept = rho > 0 && isfinite(tempChi);
+        if (accept) {
+            double alpha = 1. - pow((2 * rho - 1), 3);
+            alpha = fmin(alpha, 2. / 3.);
+            lambda *= fmax(1. / 3., alpha);
+            ni = 2;
+            currentChi = tempChi;
+        } else {
+            lambda *= ni;
+            ni *= 2;
+            for (int i = threadIdx.x; i < P.nposes_all * 7; i += kBlock) P.pose[i] = P.pose_bk[i];
+            for (int i = threadIdx.x; i < P.npoints_all * 3; i += kBlock) P.point[i] = P.point_bk[i];
+        }
+        __syncthreads();
+        qmax++;
+    } while (rho < 0 && qmax < 10 && !P.abort);
+    if (threadIdx.x == 0) {
+        P.lambda = lambda;
+        P.ni = ni;
+        P.trials += qmax;
+        P.iterations++;
+        P.last_chi = currentChi;
+        int status = kRunning;
+        if (qmax == 10 || rho == 0) {
+            status = kTerminated;
+        } else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) P.nBad++;
+            else P.nBad = 0;
+            if (P.nBad >= 3) status = kTerminated;
+        }
+        P.status = status;
+    }
+}
+
+// Outlier passes of LocalBundleAdjustment (src/Optimizer.cc:452-470,
+// :497-515): sequential in edge order (MapPoint bad state depends on it).
+__global__ void k_lba_outliers(LbaDev* probs, const int* edge_point_all, const int* edge_pose_all,
+                               int* nobs_all, uint8_t* status_all, uint8_t* bad_all, int pass, double thr,
+                               const double* isig_all, int* n_out, const long long* offs)
+{
+    LbaDev& P = probs[blockIdx.x];
+    if (threadIdx.x != 0) return;
+    const long long eo = offs[3 * blockIdx.x], po = offs[3 * blockIdx.x + 1];
+    const int* ep = edge_point_all + eo;
+    const int* eps = edge_pose_all + eo;
+    const double* isig = isig_all + eo;
+    int* nobs = nobs_all + po;
+    uint8_t* st = status_all + eo;
+    uint8_t* bad = bad_all + po;
+    int cnt = 0;
+    for (int e = 0; e < P.nedges_all; e++) {
+        if (st[e] != 0) continue;          // removed in pass 1
+        const int p = ep[e];
+        if (bad[p]) continue;
+        const double s = isig[e];
+        const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+        const double chi2 = e0 * (s * e0) + e1 * (s * e1);
+        double pc[3];
+        se3_map(P.pose + 7 * eps[e], P.point + 3 * p, pc);
+        if (chi2 > thr || !(pc[2] > 0.0)) {
+            if (--nobs[p] <= 2) bad[p] = 1;
+            st[e] = (uint8_t)pass;
+            cnt++;
+        }
+    }
+    n_out[blockIdx.x] = cnt;
+}
+
+// ---------------------------------------------------------------------------
+// Host: structure build (initializeOptimization + buildStructure) and driver
+// ---------------------------------------------------------------------------
+namespace {
+
+struct HostStruct {
+    std::vector<int> e_orig, e_pose, e_point, e_ph, e_lh;
+    std::vector<double> e_obs, e_isig;
+    std::vector<int> iv_pose, iv_point;
+    std::vector<int> pe_ptr, pe_idx, le_ptr, le_idx, lc_ptr, lc_idx, pc_ptr, pc_idx;
+    std::vector<int> blk_ij, blk_ptr, blk_c;
+    int nP = 0, nL = 0;
+};
+
+void build_struct(const orbx_ba_problem& p, const uint8_t* removed, HostStruct& s)
+{
+    const int NP = p.n_poses, NL = p.n_points, NE = p.n_edges;
+    std::vector<uint8_t> pact(NP, 0), lact(NL, 0);
+    std::vector<int> act;
+    for (int e = 0; e < NE; e++) {
+        if (removed && removed[e]) continue;
+        act.push_back(e);
+        pact[p.edge_pose[e]] = 1;
+        lact[p.edge_point[e]] = 1;
+    }
+    std::vector<int> ps, ls;
+    for (int i = 0; i < NP; i++)
+        if (pact[i] && !p.pose_fixed[i]) ps.push_back(i);
+    for (int i = 0; i < NL; i++)
+        if (lact[i]) ls.push_back(i);
+    std::stable_sort(ps.begin(), ps.end(), [&](int a, int b) { return p.pose_id[a] < p.pose_id[b]; });
+    std::stable_sort(ls.begin(), ls.end(), [&](int a, int b) { return p.point_id[a] < p.point_id[b]; });
+    std::vector<int> ph(NP, -1), lh(NL, -1);
+    for (size_t i = 0; i < ps.size(); i++) ph[ps[i]] = (int)i;
+    for (size_t i = 0; i < ls.size(); i++) lh[ls[i]] = (int)i;
+    s.nP = (int)ps.size();
+    s.nL = (int)ls.size();
+    s.iv_pose = ps;
+    s.iv_point = ls;
+    const int nE = (int)act.size();
+    s.e_orig = act;
+    s.e_pose.resize(nE);
+    s.e_point.resize(nE);
+    s.e_ph.resize(nE);
+    s.e_lh.resize(nE);
+    s.e_obs.resize(2 * nE);
+    s.e_isig.resize(nE);
+    for (int a = 0; a < nE; a++) {
+        const int e = act[a];
+        s.e_pose[a] = p.edge_pose[e];
+        s.e_point[a] = p.edge_point[e];
+        s.e_ph[a] = ph[p.edge_pose[e]];
+        s.e_lh[a] = lh[p.edge_point[e]];
+        s.e_obs[2 * a] = p.edge_obs[2 * e];
+        s.e_obs[2 * a + 1] = p.edge_obs[2 * e + 1];
+        s.e_isig[a] = p.edge_inv_sigma2[e];
+    }
+    // CSR helpers
+    auto csr = [](int n, const std::vector<std::vector<int>>& lists, std::vector<int>& ptr, std::vector<int>& idx) {
+        ptr.assign(n + 1, 0);
+        idx.clear();
+        for (int i = 0; i < n; i++) {
+            ptr[i] = (int)idx.size();
+            idx.insert(idx.end(), lists[i].begin(), lists[i].end());
+        }
+        ptr[n] = (int)idx.size();
+    };
+    std::vector<std::vector<int>> pe(s.nP), le(s.nL), lc(s.nL), pc(s.nP);
+    for (int a = 0; a < nE; a++) {
+        if (s.e_ph[a] >= 0) pe[s.e_ph[a]].push_back(a);
+        le[s.e_lh[a]].push_back(a);
+        if (s.e_ph[a] >= 0) lc[s.e_lh[a]].push_back(a);
+    }
+    for (auto& v : lc) std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return s.e_ph[x] < s.e_ph[y]; });
+    for (int l = 0; l < s.nL; l++)
+        for (int a : lc[l]) pc[s.e_ph[a]].push_back(a);   // landmark order per pose
+    csr(s.nP, pe, s.pe_ptr, s.pe_idx);
+    csr(s.nL, le, s.le_ptr, s.le_idx);
+    csr(s.nL, lc, s.lc_ptr, s.lc_idx);
+    csr(s.nP, pc, s.pc_ptr, s.pc_idx);
+    // Schur blocks (i1 <= i2): diagonal blocks always, plus pairs sharing a point
+    std::vector<int> blk_id((size_t)s.nP * s.nP, -1);
+    std::vector<std::vector<int>> contrib;
+    s.blk_ij.clear();
+    auto block = [&](int i1, int i2) {
+        int& id = blk_id[(size_t)i1 * s.nP + i2];
+        if (id < 0) {
+            id = (int)contrib.size();
+            contrib.emplace_back();
+            s.blk_ij.push_back(i1);
+            s.blk_ij.push_back(i2);
+        }
+        return id;
+    };
+    for (int i = 0; i < s.nP; i++) block(i, i);
+    for (int l = 0; l < s.nL; l++) {
+        const auto& col = lc[l];
+        for (size_t x = 0; x < col.size(); x++)
+            for (size_t y = x; y < col.size(); y++) {
+                const int id = block(s.e_ph[col[x]], s.e_ph[col[y]]);
+                contrib[id].push_back(col[x]);
+                contrib[id].push_back(col[y]);
+            }
+    }
+    s.blk_ptr.assign(contrib.size() + 1, 0);
+    s.blk_c.clear();
+    for (size_t b = 0; b < contrib.size(); b++) {
+        s.blk_ptr[b] = (int)(s.blk_c.size() / 2);
+        s.blk_c.insert(s.blk_c.end(), contrib[b].begin(), contrib[b].end());
+    }
+    s.blk_ptr[contrib.size()] = (int)(s.blk_c.size() / 2);
+}
+
+// Packs host vectors into one device allocation.
+struct Packer {
+    std::vector<uint8_t> host;
+    template <typename T>
+    size_t add(const std::vector<T>& v)
+    {
+        const size_t off = host.size();
+        host.resize(off + ((v.size() * sizeof(T) + 255) & ~size_t(255)));
+        if (!v.empty()) std::memcpy(host.data() + off, v.data(), v.size() * sizeof(T));
+        return off;
+    }
+    size_t reserve(size_t bytes)
+    {
+        const size_t off = host.size();
+        host.resize(off + ((bytes + 255) & ~size_t(255)));
+        return off;
+    }
+};
+
+constexpr int kLdsSCap = (144 * 1024) / 8;   // doubles of LDS for the reduced system
+
+}  // namespace
+
+// Solves P problems; per problem a workgroup.  The problems' pose/point
+// arrays are updated in place.
+static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int iters1,
+                   const volatile uint8_t* abort, uint8_t* const* edge_status, uint8_t* const* point_bad,
+                   orbx_ba_stats* stats)
+{
+    for (int i = 0; i < P; i++) {
+        const orbx_ba_problem& p = probs[i];
+        if (p.n_poses < 0 || p.n_points < 0 || p.n_edges < 0) return ORBX_ERR_ARG;
+        for (int e = 0; e < p.n_edges; e++)
+            if (p.edge_point[e] < 0 || p.edge_point[e] >= p.n_points || p.edge_pose[e] < 0 ||
+                p.edge_pose[e] >= p.n_poses)
+                return ORBX_ERR_ARG;
+    }
+    hipSetDevice(ctx->device);
+    // persistent per-problem device state: poses, points, errors, counters
+    std::vector<long long> offs(3 * P);
+    Packer base;
+    std::vector<size_t> o_pose(P), o_point(P), o_posebk(P), o_pointbk(P), o_cam(P), o_err(P);
+    std::vector<size_t> o_ep(P), o_eps(P), o_isig(P), o_nobs(P), o_st(P), o_bad(P);
+    std::vector<int> all_ep, all_eps, all_nobs;
+    std::vector<double> all_isig;
+    std::vector<uint8_t> all_st, all_bad;
+    long long eacc = 0, pacc = 0;
+    for (int i = 0; i < P; i++) {
+        const orbx_ba_problem& p = probs[i];
+        std::vector<double> pose(7 * (size_t)p.n_poses);
+        for (int k = 0; k < p.n_poses; k++) {
+            for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
+            for (int j = 0; j < 3; j++) pose[7 * k + 4 + j] = p.pose_t[3 * k + j];
+        }
+        o_pose[i] = base.add(pose);
+        o_point[i] = base.add(std::vector<double>(p.points, p.points + 3 * (size_t)p.n_points));
+        o_posebk[i] = base.reserve(pose.size() * 8);
+        o_pointbk[i] = base.reserve(3 * (size_t)p.n_points * 8);
+        o_cam[i] = base.add(std::vector<double>(p.pose_cam, p.pose_cam + 4 * (size_t)p.n_poses));
+        o_err[i] = base.add(std::vector<double>(2 * (size_t)p.n_edges, 0.0));
+        offs[3 * i] = eacc;
+        offs[3 * i + 1] = pacc;
+        all_ep.insert(all_ep.end(), p.edge_point, p.edge_point + p.n_edges);
+        all_eps.insert(all_eps.end(), p.edge_pose, p.edge_pose + p.n_edges);
+        all_isig.insert(all_isig.end(), p.edge_inv_sigma2, p.edge_inv_sigma2 + p.n_edges);
+        all_nobs.insert(all_nobs.end(), p.point_nobs, p.point_nobs + p.n_points);
+        all_st.insert(all_st.end(), p.n_edges, 0);
+        all_bad.insert(all_bad.end(), p.n_points, 0);
+        eacc += p.n_edges;
+        pacc += p.n_points;
+    }
+    const size_t o_all_ep = base.add(all_ep), o_all_eps = base.add(all_eps), o_all_isig = base.add(all_isig);
+    const size_t o_all_nobs = base.add(all_nobs), o_all_st = base.add(all_st), o_all_bad = base.add(all_bad);
+    const size_t o_offs = base.add(offs);
+    const size_t o_nout = base.reserve(4 * (size_t)P);
+    // per-pass structures follow the persistent block
+    const size_t base_bytes = base.host.size();
+    std::vector<LbaDev> devs(P);
+    int r = ORBX_OK;
+    for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
+        Packer pk;
+        pk.host = base.host;
+        std::vector<HostStruct> hs(P);
+        std::vector<size_t> o[32];
+        for (auto& v : o) v.resize(P);
+        for (int i = 0; i < P; i++) {
+            const orbx_ba_problem& p = probs[i];
+            const uint8_t* removed = pass == 0 ? nullptr : all_st.data() + offs[3 * i];
+            build_struct(p, removed, hs[i]);
+            HostStruct& s = hs[i];
+            o[0][i] = pk.add(s.e_orig); o[1][i] = pk.add(s.e_pose); o[2][i] = pk.add(s.e_point);
+            o[3][i] = pk.add(s.e_ph); o[4][i] = pk.add(s.e_lh); o[5][i] = pk.add(s.e_obs);
+            o[6][i] = pk.add(s.e_isig); o[7][i] = pk.add(s.iv_pose); o[8][i] = pk.add(s.iv_point);
+            o[9][i] = pk.add(s.pe_ptr); o[10][i] = pk.add(s.pe_idx); o[11][i] = pk.add(s.le_ptr);
+            o[12][i] = pk.add(s.le_idx); o[13][i] = pk.add(s.lc_ptr); o[14][i] = pk.add(s.lc_idx);
+            o[15][i] = pk.add(s.pc_ptr); o[16][i] = pk.add(s.pc_idx); o[17][i] = pk.add(s.blk_ij);
+            o[18][i] = pk.add(s.blk_ptr); o[19][i] = pk.add(s.blk_c);
+            const size_t nE = s.e_orig.size();
+            o[20][i] = pk.reserve(54 * nE * 8);
+            o[21][i] = pk.reserve(24 * nE * 8);
+            o[22][i] = pk.reserve(27 * (size_t)s.nP * 8);
+            o[23][i] = pk.reserve(9 * (size_t)s.nL * 8);
+            o[24][i] = pk.reserve(12 * (size_t)s.nL * 8);
+            const size_t n = 6 * (size_t)s.nP;
+            o[25][i] = pk.reserve(n * n > (size_t)kLdsSCap ? n * n * 8 : 8);
+            o[26][i] = pk.reserve((n + 3 * (size_t)s.nL) * 8);
+            o[27][i] = pk.reserve(n * 8 + 8);
+        }
+        const size_t o_devs = pk.reserve(sizeof(LbaDev) * P);
+        bool full_upload = pass == 0;
+        if (pk.host.size() > ctx->scratch_bytes) {
+            if (pass == 1) {   // keep the device-resident state across the reallocation
+                ORBX_HIP_CHECK(hipMemcpy(pk.host.data(), ctx->scratch, base_bytes, hipMemcpyDeviceToHost));
+                full_upload = true;
+            }
+            if ((r = ensure_scratch(ctx, pk.host.size())) != ORBX_OK) break;
+        }
+        uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+        for (int i = 0; i < P; i++) {
+            const HostStruct& s = hs[i];
+            const orbx_ba_problem& p = probs[i];
+            LbaDev& D = devs[i];
+            D = LbaDev{};
+            D.nP = s.nP;
+            D.nL = s.nL;
+            D.nE = (int)s.e_orig.size();
+            D.nblk = (int)(s.blk_ij.size() / 2);
+            D.nposes_all = p.n_poses;
+            D.npoints_all = p.n_points;
+            D.nedges_all = p.n_edges;
+            D.dim_p = 6 * s.nP;
+            D.pose = reinterpret_cast<double*>(d + o_pose[i]);
+            D.point = reinterpret_cast<double*>(d + o_point[i]);
+            D.pose_bk = reinterpret_cast<double*>(d + o_posebk[i]);
+            D.point_bk = reinterpret_cast<double*>(d + o_pointbk[i]);
+            D.cam = reinterpret_cast<const double*>(d + o_cam[i]);
+            D.err = reinterpret_cast<double*>(d + o_err[i]);
+            D.e_orig = reinterpret_cast<const int*>(d + o[0][i]);
+            D.e_pose = reinterpret_cast<const int*>(d + o[1][i]);
+            D.e_point = reinterpret_cast<const int*>(d + o[2][i]);
+            D.e_ph = reinterpret_cast<const int*>(d + o[3][i]);
+            D.e_lh = reinterpret_cast<const int*>(d + o[4][i]);
+            D.e_obs = reinterpret_cast<const double*>(d + o[5][i]);
+            D.e_isig = reinterpret_cast<const double*>(d + o[6][i]);
+            D.iv_pose = reinterpret_cast<const int*>(d + o[7][i]);
+            D.iv_point = reinterpret_cast<const int*>(d + o[8][i]);
+            D.pe_ptr = reinterpret_cast<const int*>(d + o[9][i]);
+            D.pe_idx = reinterpret_cast<const int*>(d + o[10][i]);
+            D.le_ptr = reinterpret_cast<const int*>(d + o[11][i]);
+            D.le_idx = reinterpret_cast<const int*>(d + o[12][i]);
+            D.lc_ptr = reinterpret_cast<const int*>(d + o[13][i]);
+            D.lc_idx = reinterpret_cast<const int*>(d + o[14][i]);
+            D.pc_ptr = reinterpret_cast<const int*>(d + o[15][i]);
+            D.pc_idx = reinterpret_cast<const int*>(d + o[16][i]);
+            D.blk_ij = reinterpret_cast<const int*>(d + o[17][i]);
+            D.blk_ptr = reinterpret_cast<const int*>(d + o[18][i]);
+            D.blk_c = reinterpret_cast<const int*>(d + o[19][i]);
+            D.ce = reinterpret_cast<double*>(d + o[20][i]);
+            D.eb = reinterpret_cast<double*>(d + o[21][i]);
+            D.hp = reinterpret_cast<double*>(d + o[22][i]);
+            D.hl = reinterpret_cast<double*>(d + o[23][i]);
+            D.dl = reinterpret_cast<double*>(d + o[24][i]);
+            D.S = reinterpret_cast<double*>(d + o[25][i]);
+            D.x = reinterpret_cast<double*>(d + o[26][i]);
+            D.bs = reinterpret_cast<double*>(d + o[27][i]);
+            D.huber_delta = p.huber_delta;
+            D.status = kRunning;
+            D.ni = 2;
+        }
+        std::memcpy(pk.host.data() + o_devs, devs.data(), sizeof(LbaDev) * P);
+        if (full_upload) {
+            ORBX_HIP_CHECK(hipMemcpy(d, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice));
+        } else {   // keep the persistent block (poses/points/errors/status) on the device
+            ORBX_HIP_CHECK(hipMemcpy(d + base_bytes, pk.host.data() + base_bytes, pk.host.size() - base_bytes,
+                                     hipMemcpyHostToDevice));
+        }
+        LbaDev* dd = reinterpret_cast<LbaDev*>(d + o_devs);
+        const int iters = pass == 0 ? iters0 : iters1;
+        size_t max_n2 = 0;
+        for (int i = 0; i < P; i++) max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p);
+        const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;
+        const int lds_cap = (int)(lds / 8);
+        for (int it = 0; it < iters; it++) {
+            if (abort && *abort) {
+                const int one = 1;
+                for (int i = 0; i < P; i++)
+                    ORBX_HIP_CHECK(hipMemcpy(reinterpret_cast<uint8_t*>(dd + i) + offsetof(LbaDev, abort), &one, 4,
+                                             hipMemcpyHostToDevice));
+                break;
+            }
+            hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kBlock), lds, ctx->stream, dd, it, lds_cap);
+            ORBX_HIP_CHECK(hipGetLastError());
+            ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+            ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+            bool running = false;
+            for (int i = 0; i < P; i++) running |= devs[i].status == kRunning;
+            if (!running) break;
+        }
+        hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(64), 0, ctx->stream, dd,
+                           reinterpret_cast<const int*>(d + o_all_ep), reinterpret_cast<const int*>(d + o_all_eps),
+                           reinterpret_cast<int*>(d + o_all_nobs), d + o_all_st, d + o_all_bad, pass + 1,
+                           probs[0].chi2_threshold, reinterpret_cast<const double*>(d + o_all_isig),
+                           reinterpret_cast<int*>(d + o_nout), reinterpret_cast<const long long*>(d + o_offs));
+        ORBX_HIP_CHECK(hipGetLastError());
+        std::vector<int> nout(P);
+        ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + o_nout, 4 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (stats)
+            for (int i = 0; i < P; i++) {
+                stats[i].iterations[pass] = devs[i].iterations;
+                stats[i].levenberg_trials[pass] = devs[i].trials;
+                stats[i].chi2_initial[pass] = devs[i].chi2_initial;
+                stats[i].chi2_final[pass] = devs[i].last_chi;
+                stats[i].n_outliers[pass] = nout[i];
+                stats[i].not_posdef += devs[i].not_posdef;
+            }
+    }
+    if (r != ORBX_OK) return r;
+    // results
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    std::vector<uint8_t> bad(all_bad.size());
+    ORBX_HIP_CHECK(hipMemcpy(bad.data(), d + o_all_bad, bad.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < P; i++) {
+        orbx_ba_problem& p = probs[i];
+        std::vector<double> pose(7 * (size_t)p.n_poses);
+        ORBX_HIP_CHECK(hipMemcpy(pose.data(), d + o_pose[i], pose.size() * 8, hipMemcpyDeviceToHost));
+        for (int k = 0; k < p.n_poses; k++) {
+            for (int j = 0; j < 4; j++) p.pose_q[4 * k + j] = pose[7 * k + j];
+            for (int j = 0; j < 3; j++) p.pose_t[3 * k + j] = pose[7 * k + 4 + j];
+        }
+        ORBX_HIP_CHECK(hipMemcpy(p.points, d + o_point[i], 3 * (size_t)p.n_points * 8, hipMemcpyDeviceToHost));
+        if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st.data() + offs[3 * i], p.n_edges);
+        if (point_bad && point_bad[i]) std::memcpy(point_bad[i], bad.data() + offs[3 * i + 1], p.n_points);
+    }
+    return ORBX_OK;
+}
+
+}  // namespace orbx
+
+extern "C" {
+
+int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1, const volatile uint8_t* abort,
+                   uint8_t* edge_status, uint8_t* point_bad, orbx_ba_stats* stats)
+{
+    if (!ctx || !p || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    uint8_t* es[1] = {edge_status};
+    uint8_t* pb[1] = {point_bad};
+    return orbx::lba_run(ctx, 1, p, iters0, iters1, abort, es, pb, stats);
+}
+
+int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems, int iters0, int iters1,
+                         uint8_t* const* edge_status, uint8_t* const* point_bad, orbx_ba_stats* stats)
+{
+    if (!ctx || P <= 0 || !problems || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
+    if (stats) std::memset(stats, 0, sizeof(*stats) * P);
+    return orbx::lba_run(ctx, P, problems, iters0, iters1, nullptr, edge_status, point_bad, stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+"""GPU local BA (Optimizer::LocalBundleAdjustment core, src/Optimizer.cc:
+449-535) against the FP64 CPU restatement.
+
+Tolerance (north_star): pose updates within 1e-5 (quaternion and
+translation components, absolute).  Points are checked at 1e-4, edge
+outlier decisions and MapPoint bad flags must be identical, and so must the
+LM iteration counts (same accept/reject trajectory).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth_ba as sb
+from oracle_lib import load
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-5
+POINT_TOL = 1e-4
+
+
+def run_ref(prob, i0=5, i1=10):
+    L = load()
+    L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    p, arrs = sb.to_ctypes(prob)
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    st = sb.BAStats()
+    assert L.orbx_ref_lba(ctypes.byref(p), i0, i1, es.ctypes.data, pb.ctypes.data, ctypes.byref(st)) == 0
+    return arrs, es, pb, st
+
+
+def run_gpu(ctx, prob, i0=5, i1=10, abort=None):
+    p, arrs = sb.to_ctypes(prob)
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    st = sb.BAStats()
+    ab = None if abort is None else ctypes.byref(ctypes.c_uint8(abort))
+    r = ox.lib().orbx_lba_solve(ctx.handle, ctypes.byref(p), i0, i1, ab, es.ctypes.data, pb.ctypes.data,
+                                ctypes.byref(st))
+    assert r == 0, r
+    return arrs, es, pb, st
+
+
+def compare(ref, gpu):
+    ra, res, rpb, rst = ref
+    ga, ges, gpb, gst = gpu
+    dq = np.abs(ga["pose_q"] - ra["pose_q"]).max()
+    dt = np.abs(ga["pose_t"] - ra["pose_t"]).max()
+    dp = np.abs(ga["points"] - ra["points"]).max()
+    assert dq <= POSE_TOL and dt <= POSE_TOL, (dq, dt)
+    assert dp <= POINT_TOL, dp
+    assert np.array_equal(ges, res), np.count_nonzero(ges != res)
+    assert np.array_equal(gpb, rpb)
+    assert list(gst.iterations) == list(rst.iterations)
+    assert list(gst.levenberg_trials) == list(rst.levenberg_trials)
+    assert list(gst.n_outliers) == list(rst.n_outliers)
+    return dq, dt, dp
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("nkf,npts,seed,outl", [(6, 200, 1, 0.01), (20, 2000, 0, 0.01), (10, 600, 3, 0.05),
+                                                 (3, 150, 4, 0.0)])
+def test_lba_matches_oracle(ctx, nkf, npts, seed, outl):
+    prob = sb.make_problem(n_kf=nkf, n_points=npts, seed=seed, outlier_frac=outl)
+    ref = run_ref(prob)
+    gpu = run_gpu(ctx, prob)
+    compare(ref, gpu)
+    # the optimisation did something
+    assert gpu[3].chi2_final[0] < gpu[3].chi2_initial[0]
+
+
+def test_lba_without_extra_fixed_keyframes(ctx):
+    prob = sb.make_problem(n_kf=8, n_points=400, n_fixed_extra=0, seed=7)
+    compare(run_ref(prob), run_gpu(ctx, prob))
+
+
+def test_lba_abort_flag_skips_iterations(ctx):
+    prob = sb.make_problem(n_kf=5, n_points=150, seed=9)
+    arrs, es, pb, st = run_gpu(ctx, prob, abort=1)
+    assert list(st.iterations) == [0, 0]
+    assert np.array_equal(arrs["pose_q"], prob["pose_q"])
+
+
+def test_lba_batch_equals_single(ctx):
+    probs = [sb.make_problem(n_kf=6 + k, n_points=200 + 50 * k, seed=20 + k) for k in range(4)]
+    singles = [run_gpu(ctx, pr) for pr in probs]
+    cps = [sb.to_ctypes(pr) for pr in probs]
+    arr = (sb.BAProblem * 4)(*[c[0] for c in cps])
+    es = [np.zeros(c[0].n_edges, np.uint8) for c in cps]
+    pb = [np.zeros(c[0].n_points, np.uint8) for c in cps]
+    esp = (ctypes.c_void_p * 4)(*[e.ctypes.data for e in es])
+    pbp = (ctypes.c_void_p * 4)(*[b.ctypes.data for b in pb])
+    st = (sb.BAStats * 4)()
+    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, esp, pbp, st) == 0
+    for k in range(4):
+        a = cps[k][1]
+        s = singles[k]
+        assert np.array_equal(a["pose_q"], s[0]["pose_q"]) and np.array_equal(a["points"], s[0]["points"])
+        assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
