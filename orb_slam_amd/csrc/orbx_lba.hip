@@ -386,6 +386,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
     for (int item = threadIdx.x; item < P.nblk * 36; item += kBlock) {
         const int bk = item / 36, rc = item - bk * 36, r = rc / 6, c = rc - (rc / 6) * 6;
         const int i1 = P.blk_ij[2 * bk], i2 = P.blk_ij[2 * bk + 1];
+        if (i1 == i2 && r > c) continue;   // CHOLMOD reads the upper triangle only
         double acc = 0;
         if (i1 == i2) acc = P.hp[27 * i1 + (r <= c ? up6(r, c) : up6(c, r))] + (r == c ? lambda : 0.0);
         for (int q = P.blk_ptr[bk]; q < P.blk_ptr[bk + 1]; q++) {
