@@ -26,7 +26,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 import orb_slam_amd as ox  # noqa: E402
-from orb_slam_amd import synth  # noqa: E402
+from orb_slam_amd import dist as odist, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -102,9 +102,7 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = odist.env()
     dist = None
     if world > 1:
         import torch
@@ -115,7 +113,7 @@ def main():
 
     wl = WORKLOADS[args.workload]
     w, h, nf, B = wl["w"], wl["h"], wl["nfeatures"], args.batch
-    frames = synth.sequence(w, h, B, seed=1000 * 2 + rank)
+    frames = synth.sequence(w, h, B, seed=odist.shard_seed(2000, rank))
     ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=B, device=local if world > 1 else 0)
     ctx.upload(frames)
 
@@ -152,19 +150,10 @@ def main():
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
     stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
-    if dist is not None:
-        import torch
-        t = torch.tensor(stats, device="cuda")
-        gathered = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(gathered, t)
-        allst = torch.stack(gathered).cpu().numpy()
-        elapsed = float(allst[:, 0].max())
-        frames_total = float(allst[:, 1].sum())
-    else:
-        frames_total = float(stats[1])
+    allst = odist.gather_stats(stats, dist, device="cuda")
+    value, elapsed, _ = odist.job_rate(allst)
 
     if rank == 0:
-        value = frames_total / elapsed
         ab = algorithmic_bytes(w, h, nf)
         dom = max((k for k in kernels if kernels[k]["launches"]), key=lambda k: kernels[k]["total_ms"])
         per_launch = ab[dom] * B / max(1, kernels[dom]["launches"] // args.steps)

@@ -70,6 +70,13 @@ float orbx_get_scale_factor(const orbx_ctx* ctx);
 int   orbx_get_features_per_level(const orbx_ctx* ctx, int32_t* out, int cap);
 int   orbx_get_scale_factors(const orbx_ctx* ctx, float* out, int cap);
 
+/* Host-side extractor tables for a frame size, computed without a device:
+ * per level 8 ints {w, h, n_desired, level_cols, level_rows, nfeatures_cell,
+ * n_cells, n_valid_cells} (src/ORBextractor.cc:462-487, 527-547, 786).
+ * Returns the number of levels or a negative error. */
+int orbx_describe_levels(int nfeatures, float scale_factor, int nlevels, int fast_th,
+                         int w, int h, int32_t* out, int cap);
+
 /* ------------------------------------------------------------------------ */
 /* A. Extraction                                                             */
 /* ------------------------------------------------------------------------ */

@@ -312,3 +312,30 @@ extern "C" void orbx_ref_quat_from_matrix(const double* R, double* q)
     Quat r = quat_from_matrix(R);
     q[0] = r.x; q[1] = r.y; q[2] = r.z; q[3] = r.w;
 }
+
+// EdgeSE3ProjectXYZ error and analytic Jacobians for a single observation
+// (unit tests against finite differences).  pose: q(4) t(3); A: 2x3, B: 2x6.
+extern "C" void orbx_ref_edge_linearize(const double* pose, const double* point, const double* cam,
+                                        const double* obs, double* err, double* A, double* B)
+{
+    LBAInput in;
+    in.n_poses = 1;
+    in.n_points = 1;
+    in.n_edges = 1;
+    in.poses.resize(1);
+    in.poses[0].q = {pose[0], pose[1], pose[2], pose[3]};
+    for (int k = 0; k < 3; k++) in.poses[0].t[k] = pose[4 + k];
+    in.pose_fixed = {0};
+    in.pose_id = {0};
+    in.pose_cam.assign(cam, cam + 4);
+    in.points.assign(point, point + 3);
+    in.point_id = {1};
+    in.point_nobs = {3};
+    in.edge_point = {0};
+    in.edge_pose = {0};
+    in.edge_obs.assign(obs, obs + 2);
+    in.edge_inv_sigma2 = {1.0};
+    in.huber_delta = 1e9;
+    in.chi2_threshold = 1e9;
+    edge_linearize_for_test(in, err, A, B);
+}

@@ -541,6 +541,15 @@ struct Optimizer {
 
 }  // namespace
 
+void edge_linearize_for_test(LBAInput& in, double err[2], double A[6], double B[12])
+{
+    Optimizer opt(in);
+    opt.compute_error(0);
+    err[0] = opt.err[0];
+    err[1] = opt.err[1];
+    opt.linearize(0, A, B);
+}
+
 // Optimizer::LocalBundleAdjustment core (src/Optimizer.cc:449-535).
 void local_ba(LBAInput& in, int iters0, int iters1, std::vector<uint8_t>& edge_status,
               std::vector<uint8_t>& point_bad, LBAStats& st)

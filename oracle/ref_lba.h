@@ -51,6 +51,9 @@ struct LBAStats {
     int not_posdef = 0;
 };
 
+// Error and analytic Jacobians of edge 0 of `in` at the current estimate.
+void edge_linearize_for_test(LBAInput& in, double err[2], double A[6], double B[12]);
+
 // Runs optimize(iters0), outlier pass 1, optimize(iters1), outlier pass 2.
 // edge_status: 0 inlier, 1 erased in pass 1, 2 erased in pass 2.
 void local_ba(LBAInput& in, int iters0, int iters1, std::vector<uint8_t>& edge_status,

@@ -86,6 +86,7 @@ def _declare(L):
         "orbx_lba_solve": ([vp, vp, i, i, vp, vp, vp, vp], i),
         "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp], i),
         "orbx_version": ([], ctypes.c_char_p),
+        "orbx_describe_levels": ([i, f, i, i, i, i, vp, i], i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -207,6 +208,16 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+
+def describe_levels(w, h, nfeatures=1000, scale_factor=1.2, nlevels=8, fast_th=20):
+    """Per-level host tables of the extractor (no device needed): list of
+    dicts {w, h, n_desired, cols, rows, nfeatures_cell, n_cells, n_valid}."""
+    out = np.zeros(8 * nlevels, np.int32)
+    n = lib().orbx_describe_levels(nfeatures, scale_factor, nlevels, fast_th, w, h, _ptr(out), out.size)
+    _check(0 if n > 0 else n, "orbx_describe_levels")
+    keys = ["w", "h", "n_desired", "cols", "rows", "nfeatures_cell", "n_cells", "n_valid"]
+    return [dict(zip(keys, map(int, out[8 * l:8 * l + 8]))) for l in range(n)]
 
 
 def frame_view(kps, desc, w, h, nlevels=8, scale_factor=1.2):

@@ -409,6 +409,25 @@ int orbx_extract_batch(orbx_ctx* ctx, int B, const uint8_t* const* imgs, int w, 
     return ORBX_OK;
 }
 
+int orbx_describe_levels(int nfeatures, float scale_factor, int nlevels, int fast_th, int w, int h, int32_t* out,
+                         int cap)
+{
+    if (nfeatures <= 0 || nlevels <= 0 || nlevels > kMaxLevels || !(scale_factor > 1.0f) || !out) return ORBX_ERR_ARG;
+    Geometry g;
+    init_extractor_tables(g, nfeatures, scale_factor, nlevels, fast_th);
+    const int r = compute_geometry(g, w, h);
+    if (r != ORBX_OK) return r;
+    if (cap < 8 * nlevels) return ORBX_ERR_CAPACITY;
+    for (int l = 0; l < nlevels; l++) {
+        const LevelGeom& L = g.levels[l];
+        int valid = 0;
+        for (int c = 0; c < L.n_cells; c++) valid += g.cells[L.cell_base + c].valid;
+        const int32_t v[8] = {L.w, L.h, L.n_desired, L.level_cols, L.level_rows, L.nfeatures_cell, L.n_cells, valid};
+        for (int k = 0; k < 8; k++) out[8 * l + k] = v[k];
+    }
+    return nlevels;
+}
+
 int orbx_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

@@ -1,0 +1,151 @@
+"""Golden vectors (tests/golden/*.npz, made by tools/gen_golden.py).
+
+CPU tests: the oracle still reproduces every committed vector (catches any
+drift of the restatement).  GPU tests: the product (liborbx through the C
+ABI) reproduces the same vectors from data alone -- bit-exact for
+extraction and matching, 1e-5 on poses for local BA (north_star tolerance).
+"""
+import ctypes
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth_ba as sb
+from oracle_lib import KEYPOINT, RefExtractor, load, ptr
+
+GOLD = Path(__file__).resolve().parent / "golden"
+EXTRACT = ["extract_texture_320x240", "extract_noise_160x120", "extract_ragged_97x71"]
+
+
+def g(name):
+    return np.load(GOLD / f"{name}.npz")
+
+
+def kps(a):
+    return np.ascontiguousarray(a).view(KEYPOINT).reshape(-1)
+
+
+def lba_problem(z):
+    prob = {k[3:]: z[k] for k in z.files if k.startswith("in_")}
+    prob["huber_delta"] = float(z["huber_delta"])
+    prob["chi2_threshold"] = float(z["chi2_threshold"])
+    return prob
+
+
+# ------------------------------------------------------------------ oracle
+@pytest.mark.parametrize("name", EXTRACT)
+def test_oracle_extract_golden(name):
+    z = g(name)
+    k, d = RefExtractor(int(z["nfeatures"]))(z["image"])
+    assert np.array_equal(k.view(np.uint8).reshape(-1, 28), z["keypoints"])
+    assert np.array_equal(d, z["descriptors"])
+
+
+def test_oracle_search_init_golden():
+    z = g("search_init_320x240")
+    k1, k2 = kps(z["kps1"]), kps(z["kps2"])
+    d1, d2 = np.ascontiguousarray(z["desc1"]), np.ascontiguousarray(z["desc2"])
+    F1, F2 = ox.frame_view(k1, d1, int(z["w"]), int(z["h"])), ox.frame_view(k2, d2, int(z["w"]), int(z["h"]))
+    prev = z["prev_in"].copy()
+    m = np.zeros(len(k1), np.int32)
+    n = ctypes.c_int()
+    assert load().orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), ptr(prev), ptr(m),
+                                                     int(z["window"]), float(z["nnratio"]), int(z["check_ori"]),
+                                                     ctypes.byref(n)) == 0
+    assert n.value == int(z["n_matches"])
+    assert np.array_equal(m, z["matches12"]) and np.array_equal(prev, z["prev_out"])
+
+
+def test_oracle_hamming_golden():
+    z = g("hamming_bf")
+    a, b = np.ascontiguousarray(z["desc_a"]), np.ascontiguousarray(z["desc_b"])
+    bi, best, sec = (np.zeros(len(a), np.int32) for _ in range(3))
+    load().orbx_ref_hamming_bf(ptr(a), len(a), ptr(b), len(b), ptr(bi), ptr(best), ptr(sec))
+    assert np.array_equal(bi, z["best_idx"]) and np.array_equal(best, z["best"]) and np.array_equal(sec, z["second"])
+    # size-independent properties: best is the minimum, second >= best
+    dist = np.unpackbits(a[:, None, :] ^ b[None, :, :], axis=2).sum(2)
+    assert np.array_equal(best, dist.min(1)) and (sec >= best).all()
+    assert np.array_equal(bi, dist.argmin(1))       # first index among ties
+
+
+def test_oracle_lba_golden():
+    z = g("lba_small")
+    p, arrs = sb.to_ctypes(lba_problem(z))
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    st = sb.BAStats()
+    L = load()
+    L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    assert L.orbx_ref_lba(ctypes.byref(p), int(z["iters0"]), int(z["iters1"]), ptr(es), ptr(pb),
+                          ctypes.byref(st)) == 0
+    assert np.abs(arrs["pose_q"] - z["out_pose_q"]).max() < 1e-9
+    assert np.abs(arrs["pose_t"] - z["out_pose_t"]).max() < 1e-9
+    assert np.array_equal(es, z["edge_status"]) and np.array_equal(pb, z["point_bad"])
+    assert list(st.iterations) == list(z["iterations"])
+
+
+# ------------------------------------------------------------------ product
+@pytest.fixture(scope="module")
+def gctx():
+    c = ox.Context(nfeatures=500, max_w=320, max_h=240, slots=1)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", EXTRACT)
+def test_gpu_extract_golden(name):
+    z = g(name)
+    img = z["image"]
+    c = ox.Context(nfeatures=int(z["nfeatures"]), max_w=img.shape[1], max_h=img.shape[0], slots=1)
+    try:
+        k, d = c(img)
+    finally:
+        c.close()
+    assert np.array_equal(k.view(np.uint8).reshape(-1, 28), z["keypoints"])
+    assert np.array_equal(d, z["descriptors"])
+
+
+@pytest.mark.gpu
+def test_gpu_search_init_golden(gctx):
+    z = g("search_init_320x240")
+    k1, k2 = kps(z["kps1"]), kps(z["kps2"])
+    d1, d2 = np.ascontiguousarray(z["desc1"]), np.ascontiguousarray(z["desc2"])
+    F1, F2 = ox.frame_view(k1, d1, int(z["w"]), int(z["h"])), ox.frame_view(k2, d2, int(z["w"]), int(z["h"]))
+    prev = z["prev_in"].copy()
+    m = np.zeros(len(k1), np.int32)
+    n = ctypes.c_int()
+    assert ox.lib().orbx_search_for_initialization(gctx.handle, ctypes.byref(F1), ctypes.byref(F2), ox._ptr(prev),
+                                                   ox._ptr(m), int(z["window"]), float(z["nnratio"]),
+                                                   int(z["check_ori"]), ctypes.byref(n)) == 0
+    assert n.value == int(z["n_matches"])
+    assert np.array_equal(m, z["matches12"]) and np.array_equal(prev, z["prev_out"])
+
+
+@pytest.mark.gpu
+def test_gpu_hamming_golden(gctx):
+    z = g("hamming_bf")
+    a, b = np.ascontiguousarray(z["desc_a"]), np.ascontiguousarray(z["desc_b"])
+    bi, best, sec = (np.zeros(len(a), np.int32) for _ in range(3))
+    assert ox.lib().orbx_hamming_bf(gctx.handle, ox._ptr(a), len(a), ox._ptr(b), len(b), ox._ptr(bi), ox._ptr(best),
+                                    ox._ptr(sec)) == 0
+    assert np.array_equal(bi, z["best_idx"]) and np.array_equal(best, z["best"]) and np.array_equal(sec, z["second"])
+
+
+@pytest.mark.gpu
+def test_gpu_lba_golden(gctx):
+    z = g("lba_small")
+    p, arrs = sb.to_ctypes(lba_problem(z))
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    st = sb.BAStats()
+    assert ox.lib().orbx_lba_solve(gctx.handle, ctypes.byref(p), int(z["iters0"]), int(z["iters1"]), None,
+                                   es.ctypes.data, pb.ctypes.data, ctypes.byref(st)) == 0
+    assert np.abs(arrs["pose_q"] - z["out_pose_q"]).max() <= 1e-5
+    assert np.abs(arrs["pose_t"] - z["out_pose_t"]).max() <= 1e-5
+    assert np.abs(arrs["points"] - z["out_points"]).max() <= 1e-4
+    assert np.array_equal(es, z["edge_status"]) and np.array_equal(pb, z["point_bad"])
+    assert list(st.iterations) == list(z["iterations"])
