@@ -126,12 +126,13 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
         if ((r = realloc_dev(ctx->dgeom.res_rows, g.res_rows.size())) != ORBX_OK) return r;
         ctx->cap_res_rows = (int)g.res_rows.size();
     }
-    // blur tiles: (level, x0, y0) covering stride x ph of every level
+    // blur work blocks: per level, items = (row strip, dword column) in
+    // strip-major order; one block = kBlurItems consecutive items of a level.
     std::vector<int4> tiles;
     for (int l = 0; l < g.nlevels; l++) {
         const LevelGeom& L = g.levels[l];
-        for (int y = 0; y < L.ph; y += 16)
-            for (int x = 0; x < L.stride; x += 64) tiles.push_back(make_int4(l, x, y, 0));
+        const int ndw = L.stride / 4, nstrips = (L.ph + kBlurStrip - 1) / kBlurStrip;
+        for (int b = 0; b < ndw * nstrips; b += kBlurItems) tiles.push_back(make_int4(l, b, ndw, nstrips));
     }
     if ((int)tiles.size() > ctx->cap_blur_tiles) {
         if ((r = realloc_dev(ctx->blur_tiles, tiles.size())) != ORBX_OK) return r;

@@ -354,56 +354,91 @@ __global__ __launch_bounds__(256) void k_retain(ExtractArgs a)
 // taps {18,34,49,55,49,34,18}/256 per pass).  Column pass rounding: columns
 // < nvec follow SymmColumnVec_32s8u (float, round-half-even), the tail
 // FixedPtCastEx (+2^15 >> 16).  The padded border is copied unblurred.
-// Tiles of 64x16 output pixels in padded coordinates.
+// Each thread owns one dword column (4 pixels) of a kBlurStrip-row strip and
+// slides a 7-row window of horizontal sums down it in registers: one pass
+// over the input rows it needs, one dword store per output row, no LDS.
 // ---------------------------------------------------------------------------
-constexpr int kBlurTW = 64, kBlurTH = 16;
+__device__ inline void blur_hsum(const uint8_t* row, int x, int hs[4])
+{
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row + x);
+    const uint32_t wl = w[-1], wc = w[0], wr = w[1];
+    int b[12];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        b[k] = (wl >> (8 * k)) & 0xFF;
+        b[4 + k] = (wc >> (8 * k)) & 0xFF;
+        b[8 + k] = (wr >> (8 * k)) & 0xFF;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int c = 4 + j;
+        hs[j] = 55 * b[c] + 49 * (b[c - 1] + b[c + 1]) + 34 * (b[c - 2] + b[c + 2]) + 18 * (b[c - 3] + b[c + 3]);
+    }
+}
 
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
 {
-    __shared__ uint8_t in[kBlurTH + 6][kBlurTW + 8];
-    __shared__ int rowsum[kBlurTH + 6][kBlurTW];
-    const int f = blockIdx.y, tid = threadIdx.x;
-    const int4 tl = tiles[blockIdx.x];   // level, x0, y0 (padded coords)
+    const int f = blockIdx.y;
+    const int4 tl = tiles[blockIdx.x];   // level, first item, dwords per row, strips
+    const int item = tl.y + threadIdx.x;
+    if (item >= tl.z * tl.w) return;
     const LevelGeom L = a.levels[tl.x];
+    const int strip = item / tl.z, dw = item - strip * tl.z;
+    const int x = dw * 4;
+    const int y0 = strip * kBlurStrip, y1 = min(y0 + kBlurStrip, L.ph);
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
     uint8_t* dst = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
-    const int x0 = tl.y, y0 = tl.z;
-    for (int i = tid; i < (kBlurTH + 6) * (kBlurTW + 6); i += kBlock) {
-        const int r = i / (kBlurTW + 6), c = i - r * (kBlurTW + 6);
-        const int py = min(max(y0 + r - 3, 0), L.ph - 1);
-        const int px = min(max(x0 + c - 3, 0), L.pw - 1);
-        in[r][c] = src[(size_t)py * L.stride + px];
-    }
-    __syncthreads();
-    for (int i = tid; i < (kBlurTH + 6) * kBlurTW; i += kBlock) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const uint8_t* p = &in[r][c + 3];
-        rowsum[r][c] = 55 * p[0] + 49 * (p[-1] + p[1]) + 34 * (p[-2] + p[2]) + 18 * (p[-3] + p[3]);
-    }
-    __syncthreads();
-    for (int i = tid; i < kBlurTH * kBlurTW; i += kBlock) {
-        const int r = i / kBlurTW, c = i - r * kBlurTW;
-        const int py = y0 + r, px = x0 + c;
-        if (py >= L.ph || px >= L.stride) continue;
-        uint8_t v = in[r + 3][c + 3];
-        const int x = px - kEdge, y = py - kEdge;
-        if (x >= 0 && x < L.w && y >= 0 && y < L.h) {
-            const int N = 55 * rowsum[r + 3][c] + 49 * (rowsum[r + 2][c] + rowsum[r + 4][c]) +
-                          34 * (rowsum[r + 1][c] + rowsum[r + 5][c]) + 18 * (rowsum[r][c] + rowsum[r + 6][c]);
-            int q;
-            if (x < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
-                q = N >> 16;
-                const int rem = N & 0xFFFF;
-                if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
-            } else {
-                q = (N + (1 << 15)) >> 16;
+    // interior columns / rows of this level in padded coordinates
+    const int ix0 = kEdge, ix1 = kEdge + L.w, iy0 = kEdge, iy1 = kEdge + L.h;
+    const bool col_interior = (x + 3 >= ix0) && (x < ix1);
+    // rows [ya, yb) of this strip are blurred, the rest copied
+    const int ya = col_interior ? max(y0, iy0) : y1;
+    const int yb = col_interior ? min(y1, iy1) : y1;
+    // bytes beyond the padded width (row pitch padding) are zero
+    uint32_t keep_mask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (x + j < L.pw) keep_mask |= 0xFFu << (8 * j);
+    for (int y = y0; y < min(ya, y1); y++)
+        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) =
+            *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x) & keep_mask;
+    if (ya < yb) {
+        int R[7][4];
+#pragma unroll
+        for (int k = 0; k < 6; k++) blur_hsum(src + (size_t)(ya - 3 + k) * L.stride, x, R[k]);
+        for (int y = ya; y < yb; y++) {
+            blur_hsum(src + (size_t)(y + 3) * L.stride, x, R[6]);
+            const uint32_t raw = *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x);
+            uint32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int xi = x + j - kEdge;
+                uint32_t v = (raw >> (8 * j)) & 0xFF;
+                if (xi >= 0 && xi < L.w) {
+                    const int N = 55 * R[3][j] + 49 * (R[2][j] + R[4][j]) + 34 * (R[1][j] + R[5][j]) +
+                                  18 * (R[0][j] + R[6][j]);
+                    int q;
+                    if (xi < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
+                        q = N >> 16;
+                        const int rem = N & 0xFFFF;
+                        if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
+                    } else {
+                        q = (N + (1 << 15)) >> 16;
+                    }
+                    v = (uint32_t)sat_u8(q);
+                }
+                word |= v << (8 * j);
             }
-            v = sat_u8(q);
-        } else if (px >= L.pw) {
-            v = 0;
+            *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) = word & keep_mask;
+#pragma unroll
+            for (int k = 0; k < 6; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) R[k][j] = R[k + 1][j];
         }
-        dst[(size_t)py * L.stride + px] = v;
     }
+    for (int y = max(yb, ya); y < y1; y++)
+        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) =
+            *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x) & keep_mask;
 }
 
 // ---------------------------------------------------------------------------
@@ -556,7 +591,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         timer_begin(ctx, "blur");
         {
             const int ntiles = ctx->blur_tiles_n;
-            hipLaunchKernelGGL(k_blur, dim3(ntiles, nb), dim3(256), 0, st, a, ctx->blur_tiles);
+            hipLaunchKernelGGL(k_blur, dim3(ntiles, nb), dim3(kBlurItems), 0, st, a, ctx->blur_tiles);
         }
         timer_end(ctx, "blur");
         timer_begin(ctx, "describe");

@@ -36,6 +36,8 @@ constexpr int kPatch = 31;       // PATCH_SIZE (:75)
 constexpr int kMaxLevels = 16;
 constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
 constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
+constexpr int kBlurStrip = 32;   // output rows per blur thread (rolling window)
+constexpr int kBlurItems = 256;  // blur items (strip x dword column) per block
 
 struct LevelGeom {
     int w, h;             // level size
@@ -143,7 +145,7 @@ struct orbx_ctx {
     long long cap_level_entries = 0;
     int cap_cells = 0;
     int cap_res_cols = 0, cap_res_rows = 0, cap_blur_tiles = 0;
-    int4* blur_tiles = nullptr;        // (level, x0, y0, -) blur work tiles
+    int4* blur_tiles = nullptr;        // (level, first item, dwords/row, strips) blur blocks
     int blur_tiles_n = 0;
     int last_first = 0, last_count = 0;   // batch of the most recent extract
     // generic scratch for the one-shot matcher / BA entry points

@@ -9,6 +9,8 @@
 // descriptor), reducing best / second-best with wave shuffles.  Ties resolve
 // to the first candidate in GetFeaturesInArea order (cell x, cell y, index:
 // src/Frame.cc:232-257), as the reference's strict `<` does.
+#include <algorithm>
+
 #include "orbx_match_common.h"
 
 namespace orbx {
@@ -23,14 +25,17 @@ struct MatchPrevArgs {
     int first, seq_len, window;
     float nnratio;
     int check_ori;
+    int cap_c, cap_keys;
+    int32_t* error_flags;
     float min_x, max_x, min_y, max_y, gw_inv, gh_inv;
 };
 
-// One wave (block of 64) per frame pair: slot s vs its predecessor in a
+// One 256-thread block per frame pair: slot s vs its predecessor in a
 // cyclic sequence of seq_len slots.
-__global__ __launch_bounds__(64) void k_match_prev(MatchPrevArgs a)
+__global__ __launch_bounds__(256) void k_match_prev(MatchPrevArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ BlockScratch bs;
     const int s = a.first + blockIdx.x;
     const int prev = (s % a.seq_len == 0) ? s + a.seq_len - 1 : s - 1;
     FrameDev F1, F2;
@@ -46,12 +51,9 @@ __global__ __launch_bounds__(64) void k_match_prev(MatchPrevArgs a)
     F1.max_y = F2.max_y = a.max_y;
     F1.grid_w_inv = F2.grid_w_inv = a.gw_inv;
     F1.grid_h_inv = F2.grid_h_inv = a.gh_inv;
-    CandLDS c;
-    int *m12, *hist;
-    signed char* pushed;
-    carve(smem, a.nfeatures, a.nfeatures, c, m12, pushed, hist);
-    search_for_init_wave(F1, F2, nullptr, a.window, a.nnratio, a.check_ori != 0,
-                         a.match12 + (size_t)s * a.nfeatures, a.match_n + s, nullptr, c, m12, pushed, hist);
+    const InitLDS L = carve_init(smem, a.cap_c, a.nfeatures, a.cap_keys);
+    search_for_init_block(F1, F2, nullptr, a.window, a.nnratio, a.check_ori != 0,
+                          a.match12 + (size_t)s * a.nfeatures, a.match_n + s, nullptr, L, bs, a.error_flags);
 }
 
 int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window, float nnratio,
@@ -77,9 +79,15 @@ int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wind
     a.max_y = (float)g.h;
     a.gw_inv = static_cast<float>(kGridCols) / static_cast<float>(g.w - 0);
     a.gh_inv = static_cast<float>(kGridRows) / static_cast<float>(g.h - 0);
-    const size_t lds = search_init_lds_bytes(g.nfeatures, g.nfeatures);
+    // candidates = keypoints of octave 0, at most the level-0 quota
+    a.cap_c = std::min(g.levels[0].n_desired, g.nfeatures);
+    if (a.cap_c > kInitMaxCand) return ORBX_ERR_UNSUPPORTED;
+    a.error_flags = ctx->error_flags;
+    const size_t fixed = init_lds_bytes(a.cap_c, g.nfeatures, 0);
+    a.cap_keys = std::max<int>(a.cap_c, (int)((kInitLdsBudget - std::min(fixed, kInitLdsBudget)) / 4));
+    const size_t lds = init_lds_bytes(a.cap_c, g.nfeatures, a.cap_keys);
     timer_begin(ctx, "match");
-    hipLaunchKernelGGL(k_match_prev, dim3(count), dim3(64), lds, ctx->stream, a);
+    hipLaunchKernelGGL(k_match_prev, dim3(count), dim3(256), lds, ctx->stream, a);
     timer_end(ctx, "match");
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;

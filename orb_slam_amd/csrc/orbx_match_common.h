@@ -1,7 +1,7 @@
 // Shared device code of the ORBmatcher kernels (orbx_match.hip,
 // orbx_search.hip): Frame grid queries (src/Frame.cc:199-276), rotation
 // histogram (src/ORBmatcher.cc:1748-1789), wave reductions, and the
-// SearchForInitialization wave routine.
+// SearchForInitialization block routine.
 #pragma once
 #include "orbx_device.h"
 #include "orbx_internal.h"
@@ -32,6 +32,13 @@ __device__ inline unsigned long long wave_min_u64(unsigned long long v)
         const unsigned long long t = __shfl_xor(v, o, 64);
         v = t < v ? t : v;
     }
+    return v;
+}
+
+__device__ inline uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
     return v;
 }
 
@@ -120,166 +127,223 @@ __device__ inline void load_desc(const uint8_t* d, uint4& a, uint4& b)
 }
 
 // ---------------------------------------------------------------------------
-// SearchForInitialization (src/ORBmatcher.cc:598-713) for one pair, one wave.
-// LDS (per wave): candidate table of F2's octave-0 keypoints in index order
-// {x, y, cell, vMatchedDistance, vnMatches21, index} and, per F1 keypoint,
-// vnMatches12 and the rotation bin it was pushed to.
+// SearchForInitialization (src/ORBmatcher.cc:598-713) for one pair, one
+// 256-thread block, in two phases per group of 256 F1 keypoints:
+//
+//  1. (all threads, state-free) each F1 octave-0 keypoint gathers its
+//     candidate window -- F2 octave-0 keypoints passing GetFeaturesInArea's
+//     cell and box tests -- and stores one 32-bit key per candidate:
+//     dist (9 bits) << 23 | grid cell (12 bits) << 11 | candidate slot.
+//     Keys order candidates by (distance, GetFeaturesInArea order), so the
+//     minimum key is the reference's first strict minimum.
+//  2. (wave 0, sequential in i1 order) the greedy replay: admissible keys
+//     (vMatchedDistance[i2] > dist) -> best key and second-best distance by
+//     wave reductions, then the accept / steal update in LDS.
+//
+// Descriptors of the candidates are staged in LDS.  The rotation histogram
+// (with the reference's stale entries of stolen matches) is built with LDS
+// atomics and filtered in parallel after ComputeThreeMaxima.
 // ---------------------------------------------------------------------------
-struct CandLDS {
+constexpr int kInitMaxCand = 2048;     // slot field of the key (11 bits)
+constexpr size_t kInitLdsBudget = 64 * 1024;
+
+struct InitLDS {
     float* x;
     float* y;
+    float* ang;
     int* cell;
+    int* idx;
     int* mdist;
     int* m21;
-    int* idx;
+    uint4* desc;        // 2 per candidate
+    int* m12;           // per F1 keypoint
+    signed char* pushed;
+    int* offs;          // 257 list offsets of the current group
+    int* hist;          // 32 bins + 3 maxima indices
+    uint32_t* keys;     // candidate lists
+    int cap_c, cap1, cap_keys;
 };
 
-__device__ inline void search_for_init_wave(const FrameDev& F1, const FrameDev& F2, const float* prev_xy,
-                                     int window, float nnratio, bool check_ori, int32_t* out_m12,
-                                     int32_t* out_n, float* out_prev_xy, CandLDS c, int* m12,
-                                     signed char* pushed, int* hist)
+__host__ __device__ inline size_t init_lds_bytes(int cap_c, int cap1, int cap_keys)
 {
-    const int lane = threadIdx.x & 63;
-    // compact F2 octave-0 keypoints (index order)
+    return (size_t)cap_c * (7 * 4 + 32) + (size_t)cap1 * 4 + (size_t)((cap1 + 15) & ~15) + 257 * 4 + 36 * 4 +
+           (size_t)cap_keys * 4 + 64;
+}
+
+__device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap_keys)
+{
+    InitLDS s;
+    s.cap_c = cap_c;
+    s.cap1 = cap1;
+    s.cap_keys = cap_keys;
+    s.desc = reinterpret_cast<uint4*>(base);
+    s.x = reinterpret_cast<float*>(s.desc + 2 * cap_c);
+    s.y = s.x + cap_c;
+    s.ang = s.y + cap_c;
+    s.cell = reinterpret_cast<int*>(s.ang + cap_c);
+    s.idx = s.cell + cap_c;
+    s.mdist = s.idx + cap_c;
+    s.m21 = s.mdist + cap_c;
+    s.m12 = s.m21 + cap_c;
+    s.offs = s.m12 + cap1;
+    s.hist = s.offs + 257;
+    s.keys = reinterpret_cast<uint32_t*>(s.hist + 36);
+    s.pushed = reinterpret_cast<signed char*>(s.keys + cap_keys);
+    return s;
+}
+
+__device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev& F2, const float* prev_xy,
+                                             int window, float nnratio, bool check_ori, int32_t* out_m12,
+                                             int32_t* out_n, float* out_prev_xy, InitLDS s, BlockScratch& bs,
+                                             int32_t* error_flags)
+{
+    const int tid = threadIdx.x, lane = tid & 63;
+    // F2 octave-0 keypoints in index order -> candidate slots
     int nc = 0;
-    for (int base = 0; base < F2.n; base += 64) {
-        const int i2 = base + lane;
-        bool ok = false;
+    for (int base = 0; base < F2.n; base += kBlock) {
+        const int i2 = base + tid;
         orbx_keypoint k;
+        bool ok = false;
         if (i2 < F2.n) {
             k = F2.kps[i2];
             ok = (k.octave == 0);
         }
-        const unsigned long long bal = __ballot(ok);
-        if (ok) {
-            const int pos = nc + __popcll(bal & ((1ull << lane) - 1ull));
-            c.x[pos] = k.x;
-            c.y[pos] = k.y;
-            c.cell[pos] = grid_cell(F2, k.x, k.y);
-            c.mdist[pos] = 0x7fffffff;
-            c.m21[pos] = -1;
-            c.idx[pos] = i2;
+        int tot;
+        const int pos = nc + block_exclusive_scan(ok ? 1 : 0, &tot, bs, (base / kBlock) & 1);
+        if (ok && pos < s.cap_c) {
+            s.x[pos] = k.x;
+            s.y[pos] = k.y;
+            s.ang[pos] = k.angle;
+            s.cell[pos] = grid_cell(F2, k.x, k.y);
+            s.idx[pos] = i2;
+            s.mdist[pos] = 0x7fffffff;
+            s.m21[pos] = -1;
+            const uint4* d = reinterpret_cast<const uint4*>(F2.desc + (size_t)i2 * 32);
+            s.desc[2 * pos] = d[0];
+            s.desc[2 * pos + 1] = d[1];
         }
-        nc += __popcll(bal);
+        nc += tot;
     }
-    for (int i = lane; i < F1.n; i += 64) {
-        m12[i] = -1;
-        pushed[i] = -1;
+    if (nc > s.cap_c) {
+        if (tid == 0) {
+            atomicOr(error_flags, 4);
+            *out_n = ORBX_ERR_CAPACITY;
+        }
+        return;
     }
-    wave_sync();
+    for (int i = tid; i < F1.n; i += kBlock) {
+        s.m12[i] = -1;
+        s.pushed[i] = -1;
+    }
+    if (tid < 36) s.hist[tid] = 0;
+    __syncthreads();
     const float r = (float)window;
-    int nmatches = 0;
-    for (int i1 = 0; i1 < F1.n; i1++) {
-        const orbx_keypoint k1 = F1.kps[i1];
-        if (k1.octave > 0) continue;
-        const float qx = prev_xy ? prev_xy[2 * i1] : k1.x;
-        const float qy = prev_xy ? prev_xy[2 * i1 + 1] : k1.y;
-        const AreaQuery q = area_cells(F2, qx, qy, r);
-        if (q.empty) continue;
-        uint4 d1a, d1b;
-        load_desc(F1.desc + (size_t)i1 * 32, d1a, d1b);
-        unsigned long long best = ~0ull;
-        int any = 0;
-        for (int j = lane; j < nc; j += 64) {
-            const int cell = c.cell[j];
-            if (!in_area(q, cell, c.x[j], c.y[j], qx, qy, r)) continue;
-            any = 1;
-            uint4 d2a, d2b;
-            load_desc(F2.desc + (size_t)c.idx[j] * 32, d2a, d2b);
-            const int dist = hamming256(d1a, d1b, d2a, d2b);
-            if (c.mdist[j] <= dist) continue;
-            const unsigned long long key = ((unsigned long long)dist << 32) |
-                                           ((unsigned long long)cell << 12) | (unsigned long long)c.idx[j];
-            best = key < best ? key : best;
-        }
-        if (!__any(any)) continue;   // vIndices2.empty()
-        best = wave_min_u64(best);
-        if (best == ~0ull) continue;
-        const int bestDist = (int)(best >> 32);
-        const int bestIdx2 = (int)(best & 0xFFF);
-        // second smallest of the multiset of admissible distances
-        int second = 0x7fffffff;
-        for (int j = lane; j < nc; j += 64) {
-            const int cell = c.cell[j];
-            if (c.idx[j] == bestIdx2) continue;
-            if (!in_area(q, cell, c.x[j], c.y[j], qx, qy, r)) continue;
-            uint4 d2a, d2b;
-            load_desc(F2.desc + (size_t)c.idx[j] * 32, d2a, d2b);
-            const int dist = hamming256(d1a, d1b, d2a, d2b);
-            if (c.mdist[j] <= dist) continue;
-            second = min(second, dist);
-        }
-        second = wave_min_i32(second);
-        if (bestDist <= kTHLow && (float)bestDist < __fmul_rn((float)second, nnratio)) {
-            // locate bestIdx2's candidate slot (unique)
-            int slot = -1;
-            for (int j = lane; j < nc; j += 64)
-                if (c.idx[j] == bestIdx2) slot = j;
-            slot = wave_max(slot);
-            if (lane == 0) {
-                const int prev = c.m21[slot];
-                if (prev >= 0) {
-                    m12[prev] = -1;
-                    nmatches--;
-                }
-                m12[i1] = bestIdx2;
-                c.m21[slot] = i1;
-                c.mdist[slot] = bestDist;
-                nmatches++;
-                if (check_ori) pushed[i1] = (signed char)rot_bin(k1.angle, F2.kps[bestIdx2].angle);
-            }
-            wave_sync();
-        }
-    }
-    wave_sync();
-    if (lane == 0) {
-        if (check_ori) {
-            for (int b = 0; b < kHistoLength; b++) hist[b] = 0;
-            for (int i = 0; i < F1.n; i++)
-                if (pushed[i] >= 0) hist[pushed[i]]++;
-            int ind1, ind2, ind3;
-            three_maxima(hist, ind1, ind2, ind3);
-            for (int i = 0; i < F1.n; i++) {
-                const int b = pushed[i];
-                if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
-                if (m12[i] >= 0) {
-                    m12[i] = -1;
-                    nmatches--;
-                }
+    for (int g0 = 0; g0 < F1.n; g0 += kBlock) {
+        const int i1 = g0 + tid;
+        bool act = false;
+        float qx = 0.f, qy = 0.f;
+        AreaQuery q;
+        q.empty = true;
+        uint4 d1a = make_uint4(0, 0, 0, 0), d1b = d1a;
+        if (i1 < F1.n) {
+            const orbx_keypoint k1 = F1.kps[i1];
+            if (k1.octave == 0) {
+                qx = prev_xy ? prev_xy[2 * i1] : k1.x;
+                qy = prev_xy ? prev_xy[2 * i1 + 1] : k1.y;
+                q = area_cells(F2, qx, qy, r);
+                act = !q.empty;
+                if (act) load_desc(F1.desc + (size_t)i1 * 32, d1a, d1b);
             }
         }
-        *out_n = nmatches;
+        int cnt = 0;
+        if (act)
+            for (int j = 0; j < nc; j++) cnt += in_area(q, s.cell[j], s.x[j], s.y[j], qx, qy, r);
+        int total;
+        const int off = block_exclusive_scan(cnt, &total, bs, 0);
+        s.offs[tid] = off;
+        if (tid == kBlock - 1) s.offs[kBlock] = total;
+        __syncthreads();
+        for (int lo = 0; lo < kBlock;) {
+            // largest hi with offs[hi] - offs[lo] <= cap_keys (one list always fits: cnt <= nc <= cap)
+            const int base_off = s.offs[lo];
+            const int fits = (tid >= lo && s.offs[tid + 1] - base_off <= s.cap_keys) ? 1 : 0;
+            const int hi = lo + block_sum(fits, bs, 1);
+            if (tid >= lo && tid < hi && cnt > 0) {
+                uint32_t* out = s.keys + (off - base_off);
+                int w = 0;
+                for (int j = 0; j < nc; j++) {
+                    const int cell = s.cell[j];
+                    if (!in_area(q, cell, s.x[j], s.y[j], qx, qy, r)) continue;
+                    const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
+                    out[w++] = ((uint32_t)dist << 23) | ((uint32_t)cell << 11) | (uint32_t)j;
+                }
+            }
+            __syncthreads();
+            if (tid < 64) {
+                for (int t = lo; t < hi; t++) {
+                    const int b = s.offs[t] - base_off, n = s.offs[t + 1] - s.offs[t];
+                    if (n == 0) continue;   // vIndices2.empty(), or not an octave-0 query
+                    uint32_t best = 0xFFFFFFFFu;
+                    for (int e = lane; e < n; e += 64) {
+                        const uint32_t key = s.keys[b + e];
+                        const int dist = (int)(key >> 23);
+                        if (s.mdist[key & 0x7FF] > dist) best = min(best, key);
+                    }
+                    best = wave_min_u32(best);
+                    if (best == 0xFFFFFFFFu) continue;
+                    const int bestDist = (int)(best >> 23);
+                    int second = 0x7fffffff;
+                    for (int e = lane; e < n; e += 64) {
+                        const uint32_t key = s.keys[b + e];
+                        const int dist = (int)(key >> 23);
+                        if (key != best && s.mdist[key & 0x7FF] > dist) second = min(second, dist);
+                    }
+                    second = wave_min_i32(second);
+                    if (bestDist <= kTHLow && (float)bestDist < __fmul_rn((float)second, nnratio)) {
+                        if (lane == 0) {
+                            const int slot = (int)(best & 0x7FF);
+                            const int ii1 = g0 + t;
+                            const int prev = s.m21[slot];
+                            if (prev >= 0) s.m12[prev] = -1;
+                            s.m12[ii1] = s.idx[slot];
+                            s.m21[slot] = ii1;
+                            s.mdist[slot] = bestDist;
+                            if (check_ori) s.pushed[ii1] = (signed char)rot_bin(F1.kps[ii1].angle, s.ang[slot]);
+                        }
+                        wave_sync();
+                    }
+                }
+            }
+            __syncthreads();
+            lo = hi;
+        }
     }
-    wave_sync();
-    for (int i = lane; i < F1.n; i += 64) {
-        const int m = m12[i];
+    if (check_ori) {
+        for (int i = tid; i < F1.n; i += kBlock)
+            if (s.pushed[i] >= 0) atomicAdd(&s.hist[s.pushed[i]], 1);
+        __syncthreads();
+        if (tid == 0) three_maxima(s.hist, s.hist[32], s.hist[33], s.hist[34]);
+        __syncthreads();
+        const int ind1 = s.hist[32], ind2 = s.hist[33], ind3 = s.hist[34];
+        for (int i = tid; i < F1.n; i += kBlock) {
+            const int b = s.pushed[i];
+            if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+            s.m12[i] = -1;
+        }
+        __syncthreads();
+    }
+    int nm = 0;
+    for (int i = tid; i < F1.n; i += kBlock) {
+        const int m = s.m12[i];
         out_m12[i] = m;
+        nm += m >= 0;
         if (out_prev_xy && m >= 0) {
             out_prev_xy[2 * i] = F2.kps[m].x;
             out_prev_xy[2 * i + 1] = F2.kps[m].y;
         }
     }
-}
-
-// Shared-memory carve for one wave: 6 candidate arrays of cap_c, m12 of cap1,
-// pushed bins of cap1, histogram of 32.
-__device__ inline void carve(uint8_t* base, int cap_c, int cap1, CandLDS& c, int*& m12,
-                             signed char*& pushed, int*& hist)
-{
-    c.x = reinterpret_cast<float*>(base);
-    c.y = c.x + cap_c;
-    c.cell = reinterpret_cast<int*>(c.y + cap_c);
-    c.mdist = c.cell + cap_c;
-    c.m21 = c.mdist + cap_c;
-    c.idx = c.m21 + cap_c;
-    m12 = c.idx + cap_c;
-    hist = m12 + cap1;
-    pushed = reinterpret_cast<signed char*>(hist + 32);
-}
-
-__host__ __device__ inline size_t search_init_lds_bytes(int cap_c, int cap1)
-{
-    return (size_t)cap_c * 24 + (size_t)cap1 * 4 + 32 * 4 + (size_t)((cap1 + 15) & ~15);
+    nm = block_sum(nm, bs, 0);
+    if (tid == 0) *out_n = nm;
 }
 
 }  // namespace orbx

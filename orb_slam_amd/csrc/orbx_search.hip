@@ -346,15 +346,13 @@ __global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
 }
 
 // SearchForInitialization with host inputs (prev_xy in/out).
-__global__ __launch_bounds__(64) void k_search_init_one(SearchArgs a)
+__global__ __launch_bounds__(256) void k_search_init_one(SearchArgs a, int cap_c, int cap_keys, int32_t* error_flags)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    CandLDS c;
-    int *m12, *hist;
-    signed char* pushed;
-    carve(smem, max(a.F2.n, 1), max(a.F1.n, 1), c, m12, pushed, hist);
-    search_for_init_wave(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n,
-                         a.prev_out, c, m12, pushed, hist);
+    __shared__ BlockScratch bs;
+    const InitLDS L = carve_init(smem, cap_c, max(a.F1.n, 1), cap_keys);
+    search_for_init_block(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n, a.prev_out,
+                          L, bs, error_flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -512,14 +510,23 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     a.check_ori = check_ori;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    const size_t lds = search_init_lds_bytes(std::max(F2->n, 1), std::max(F1->n, 1));
-    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(64), lds, ctx->stream, a);
+    // candidate slots = F2 keypoints of octave 0
+    int cap_c = 0;
+    for (int i = 0; i < F2->n; i++) cap_c += F2->keys_un[i].octave == 0;
+    cap_c = std::max(cap_c, 1);
+    if (cap_c > kInitMaxCand) return ORBX_ERR_UNSUPPORTED;
+    const int cap1 = std::max(F1->n, 1);
+    const size_t fixed = init_lds_bytes(cap_c, cap1, 0);
+    const int cap_keys = std::max<int>(cap_c, (int)((kInitLdsBudget - std::min(fixed, kInitLdsBudget)) / 4));
+    const size_t lds = init_lds_bytes(cap_c, cap1, cap_keys);
+    if (lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(256), lds, ctx->stream, a, cap_c, cap_keys, ctx->error_flags);
     ORBX_HIP_CHECK(hipGetLastError());
     if ((r = get(ctx, matches12, oo, (size_t)F1->n * 4)) || (r = get(ctx, n_matches, on, 4)) ||
         (r = get(ctx, prev_matched, opo, (size_t)F1->n * 8)))
         return r;
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    return ORBX_OK;
+    return *n_matches < 0 ? *n_matches : ORBX_OK;
 }
 
 int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_frame_view* F2, const uint8_t* f1_mp,
