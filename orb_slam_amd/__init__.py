@@ -14,7 +14,7 @@ from pathlib import Path
 import numpy as np
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / "liborbx.so"
+LIB_PATH = Path(os.environ.get("ORBX_LIBRARY", _PKG / "liborbx.so"))
 
 ORBX_OK = 0
 ERRORS = {-1: "ORBX_ERR_ARG", -2: "ORBX_ERR_HIP", -3: "ORBX_ERR_CAPACITY",

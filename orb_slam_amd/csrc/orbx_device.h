@@ -362,4 +362,110 @@ __device__ inline void block_nth_element(uint32_t* a, int n, int nth, int* pos, 
     __syncthreads();
 }
 
+// --------------------------------------------------------------------------
+// Wave-level (64 lanes, no block barriers) variants of the partition and
+// nth_element above, for lists held in a wave-private LDS buffer.
+// --------------------------------------------------------------------------
+__device__ inline void lds_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline int wave_min_int(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos)
+{
+    int* posR = pos;
+    int* posL = pos + (hi - lo) / 2 + 1;
+    const int lane = threadIdx.x & 63;
+    const uint32_t P = kp_key(a[lo]);
+    const int len = hi - lo - 1;
+    const int chunk = (len + 63) / 64;
+    const int s0 = min(lo + 1 + lane * chunk, hi), s1 = min(s0 + chunk, hi);
+    int nle = 0, nge = 0;
+    for (int x = s0; x < s1; x++) {
+        const uint32_t k = kp_key(a[x]);
+        nle += (k <= P);
+        nge += (k >= P);
+    }
+    const int le_incl = wave_inclusive_scan(nle), ge_incl = wave_inclusive_scan(nge);
+    const int tot_ge = __shfl(ge_incl, 63, 64);
+    const int le_before = le_incl - nle;
+    const int ge_after_chunk = tot_ge - ge_incl;
+    int cl = le_before, cr = ge_after_chunk + nge, best = 0;
+    for (int x = s0; x < s1; x++) {
+        best = max(best, min(cl, cr));
+        const uint32_t k = kp_key(a[x]);
+        cl += (k <= P);
+        cr -= (k >= P);
+    }
+    best = max(best, min(cl, cr));
+    const int m = wave_max(best);
+    int lm1 = 0x7fffffff, rm = -1, l1 = 0x7fffffff;
+    cl = le_before;
+    cr = ge_after_chunk + nge;
+    for (int x = s0; x < s1; x++) {
+        const uint32_t k = kp_key(a[x]);
+        if (k <= P) {
+            cl++;
+            if (cl <= m) posL[cl - 1] = x;
+            if (cl == m + 1) lm1 = x;
+            if (cl == 1) l1 = x;
+        }
+        if (k >= P) {
+            if (cr <= m) posR[cr - 1] = x;
+            if (cr == m) rm = x;
+            cr--;
+        }
+    }
+    lm1 = wave_min_int(lm1);
+    l1 = wave_min_int(l1);
+    rm = wave_max(rm);
+    lds_wave_sync();
+    for (int k = lane; k < m; k += 64) {
+        const int i = posL[k], j = posR[k];
+        const uint32_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+    lds_wave_sync();
+    return (m == 0) ? l1 : min(lm1, rm);
+}
+
+// std::nth_element(a, a + nth, a + n, greater-by-response), one wave.
+__device__ inline void wave_nth_element(uint32_t* a, int n, int nth, int* pos)
+{
+    if (n == 0 || nth == n) return;
+    const int lane = threadIdx.x & 63;
+    int first = 0, last = n;
+    int depth = 2 * floor_log2(n);
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (lane == 0) {
+                heap_select(a + first, nth + 1 - first, last - first);
+                const uint32_t t = a[first];
+                a[first] = a[nth];
+                a[nth] = t;
+            }
+            lds_wave_sync();
+            return;
+        }
+        --depth;
+        if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        lds_wave_sync();
+        const int cut = wave_hoare_partition(a, first, last, pos);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    if (lane == 0) insertion_sort(a, first, last);
+    lds_wave_sync();
+}
+
 }  // namespace orbx

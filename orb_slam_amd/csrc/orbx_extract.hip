@@ -14,10 +14,14 @@
 //                                                              :764-777)
 //
 // All integer / byte work; the bounds are HBM or latency, never MFMA.
+#include <algorithm>
+
 #include "orbx_device.h"
 #include "orbx_internal.h"
 
 namespace orbx {
+
+constexpr size_t kRetainLds = 128 * 1024;   // LDS budget of a retain block
 
 __constant__ int8_t c_pattern[256][4] = {
 #include "orbx_pattern.inc"
@@ -186,13 +190,28 @@ __device__ inline int fast_score(const uint8_t* t, int pitch, int tmin)
     return S >= tmin ? S : 0;
 }
 
-// One workgroup per (cell, frame).  LDS: tile (hx*hy bytes, reused for the
-// NMS result) + score map (hx*hy bytes).
+// One workgroup per (cell, frame).  LDS: the cell ROI with dword-aligned rows
+// (tile), its S' map (sm), and one candidate buffer per wave.
+//  1. compass pre-test, 4 pixels per thread: a 9-arc covers two adjacent
+//     compass points, so S >= tmin needs d > tmin (or < -tmin) on both;
+//     survivors are compacted per wave and scored with all lanes busy;
+//  2. non-max suppression, 4 pixels per thread (result kept over `tile`);
+//  3. raster-order compaction of the corners at the chosen threshold.
+// ---------------------------------------------------------------------------
+__device__ inline int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFF); }
+
+// byte k (0..11) of the 12-byte window lo|mid|hi
+__device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
+{
+    return k < 4 ? byte_of(lo, k) : (k < 8 ? byte_of(mid, k - 4) : byte_of(hi, k - 8));
+}
+
 __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
-    const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    __shared__ uint16_t cand[kWaves][256];
+    const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
     if (!C.valid) {
@@ -200,152 +219,276 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         return;
     }
     const LevelGeom L = a.levels[C.level];
-    const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off +
-                         (size_t)(kEdge + C.ini_y) * L.stride + kEdge + C.ini_x;
-    const int hx = C.hx, hy = C.hy, n = hx * hy;
+    const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~3, sh = roi_x - x_al;
+    const int hx = C.hx, hy = C.hy;
+    const int P = (sh + hx + 3) & ~3, nq = P >> 2;     // tile pitch, dwords per row
+    const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
     uint8_t* tile = smem;
     uint8_t* sm = smem + tile_pitch_bytes;
-    for (int i = tid; i < n; i += kBlock) {
-        const int r = i / hx, c = i - r * hx;
-        tile[i] = src[(size_t)r * L.stride + c];
+    uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
+    uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
+    for (int i = tid; i < hy * nq; i += kBlock) {
+        const int r = i / nq, q = i - r * nq;
+        tile32[i] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * L.stride + 4 * q);
+    }
+    // S' is 0 outside the interior rows [3, hy-4]; the interior rows are
+    // fully rewritten below
+    for (int i = tid; i < nq; i += kBlock) {
+        sm32[2 * nq + i] = 0;
+        sm32[(hy - 3) * nq + i] = 0;
     }
     __syncthreads();
     const int tmin = min(a.fast_th, a.fast_th_low);
-    for (int i = tid; i < n; i += kBlock) {
-        const int r = i / hx, c = i - r * hx;
-        int s = 0;
-        if (r >= 3 && r <= hy - 4 && c >= 3 && c <= hx - 4) s = fast_score(tile + i, hx, tmin);
-        sm[i] = (uint8_t)s;
+    const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
+    const int nunits = (hy - 6) * nq;
+    for (int u0 = wv * 64; u0 < nunits; u0 += kBlock) {
+        const int u = u0 + lane;
+        int mask = 0;
+        if (u < nunits) {
+            const int r = 3 + u / nq, q = u - (u / nq) * nq;
+            const uint32_t* row = tile32 + r * nq + q;
+            const uint32_t mid = row[0];
+            const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
+            const uint32_t up = row[-3 * nq], dn = row[3 * nq];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int tc = 4 * q + j;
+                if (tc < c_lo || tc > c_hi) continue;
+                const int v = byte_of(mid, j);
+                const int p0 = byte_of(dn, j), p8 = byte_of(up, j);
+                const int p4 = byte12(lo, mid, hi, 4 + j + 3), p12 = byte12(lo, mid, hi, 4 + j - 3);
+                const bool d0 = v - p0 > tmin, d4 = v - p4 > tmin, d8 = v - p8 > tmin, d12 = v - p12 > tmin;
+                const bool b0 = p0 - v > tmin, b4 = p4 - v > tmin, b8 = p8 - v > tmin, b12 = p12 - v > tmin;
+                const bool ok = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
+                                (b4 && b8) || (b8 && b12) || (b12 && b0);
+                mask |= ok << j;
+            }
+            sm32[r * nq + q] = 0;
+        }
+        const int cnt = __popc(mask);
+        const int incl = wave_inclusive_scan(cnt);
+        const int ntot = __shfl(incl, 63, 64);
+        int w = incl - cnt;
+        if (mask) {
+            const int r = 3 + u / nq, q = u - (u / nq) * nq;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (mask & (1 << j)) cand[wv][w++] = (uint16_t)(r * P + 4 * q + j);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = lane; i < ntot; i += 64) {
+            const int pos = cand[wv][i];
+            sm[pos] = (uint8_t)fast_score(tile + pos, P, tmin);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     __syncthreads();
-    // non-max suppression inside the cell: keep[p] = S'(p) if it beats all 8
-    // neighbours' S' (out-of-interior neighbours are 0), stored over `tile`.
-    const int iw = hx - 6, ih = hy - 6, ni = iw * ih;
-    for (int i = tid; i < ni; i += kBlock) {
-        const int r = 3 + i / iw, c = 3 + (i - (i / iw) * iw);
-        const uint8_t* p = sm + r * hx + c;
-        const int s = p[0];
-        int m = max(max(p[-1], p[1]), max(p[-hx - 1], p[-hx]));
-        m = max(m, max(max(p[-hx + 1], p[hx - 1]), max(p[hx], p[hx + 1])));
-        tile[i] = (uint8_t)((s > m) ? s : 0);
-    }
-    __syncthreads();
-    // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
-    const int chunk = (ni + kBlock - 1) / kBlock;
-    const int p0 = min(tid * chunk, ni), p1 = min(p0 + chunk, ni);
+    // non-max suppression: keep S' if it beats all 8 neighbours' S'
     int c1 = 0;
-    for (int i = p0; i < p1; i++) c1 += tile[i] >= a.fast_th && tile[i] > 0;
+    for (int u = tid; u < nunits; u += kBlock) {
+        const int r = 3 + u / nq, q = u - (u / nq) * nq;
+        uint32_t word = 0;
+        const uint32_t* m = sm32 + r * nq + q;
+        const uint32_t mid = m[0];
+        if (mid) {
+            uint32_t w3[3][3];
+#pragma unroll
+            for (int dr = 0; dr < 3; dr++) {
+                const uint32_t* mr = m + (dr - 1) * nq;
+                w3[dr][0] = q > 0 ? mr[-1] : 0u;
+                w3[dr][1] = mr[0];
+                w3[dr][2] = q + 1 < nq ? mr[1] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int s = byte_of(mid, j);
+                if (s == 0) continue;
+                int mx = max(byte12(w3[1][0], w3[1][1], w3[1][2], 3 + j), byte12(w3[1][0], w3[1][1], w3[1][2], 5 + j));
+#pragma unroll
+                for (int dr = 0; dr < 3; dr += 2)
+#pragma unroll
+                    for (int dc = 3; dc <= 5; dc++) mx = max(mx, byte12(w3[dr][0], w3[dr][1], w3[dr][2], dc + j));
+                if (s > mx) {
+                    word |= (uint32_t)s << (8 * j);
+                    c1 += s >= a.fast_th;
+                }
+            }
+        }
+        tile32[r * nq + q] = word;
+    }
+    // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
     const int n1 = block_sum(c1, bs, 0);
     const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
-    int c = 0;
-    for (int i = p0; i < p1; i++) c += tile[i] >= t && tile[i] > 0;
-    int total;
-    int off = block_exclusive_scan(c, &total, bs, 1);
     uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    for (int i = p0; i < p1; i++) {
-        const int s = tile[i];
-        if (s >= t && s > 0) {
-            const int r = 3 + i / iw, cc = 3 + (i - (i / iw) * iw);
-            out[off++] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+    int base = 0, buf = 1;
+    for (int u0 = 0; u0 < nunits; u0 += kBlock) {
+        const int u = u0 + tid;
+        uint32_t word = 0;
+        int cnt = 0;
+        if (u < nunits) {
+            word = tile32[(3 + u / nq) * nq + (u - (u / nq) * nq)];
+#pragma unroll
+            for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
         }
+        int total;
+        int off = base + block_exclusive_scan(cnt, &total, bs, buf);
+        buf ^= 1;
+        if (cnt) {
+            const int r = 3 + u / nq, q = u - (u / nq) * nq;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int s = byte_of(word, j);
+                if (s >= t && s > 0 && off < C.list_cap) {
+                    const int cc = 4 * q + j - sh;   // ROI column
+                    out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                }
+                off += (s >= t && s > 0);
+            }
+        }
+        base += total;
     }
     if (tid == 0) {
-        *count_out = total;
-        if (total > C.list_cap) atomicOr(a.error_flags, 1);
+        *count_out = base;
+        if (base > C.list_cap) atomicOr(a.error_flags, 1);
     }
 }
 
 // ---------------------------------------------------------------------------
-// Per (level, frame): cell quota redistribution (:622-670), retainBest per
-// cell (:683-685) and per level (:697-701), output in reference order.
-// LDS: cell buffer (max_list_cap) | level buffer (max_level_cap) | scratch.
+// retainBest, in two launches (src/ORBextractor.cc:622-701):
+//  k_retain_cells   one wave per (cell, frame): the level's quota
+//                   redistribution (:622-670, wave-parallel over cells),
+//                   nth_element of the cell list in a wave-private LDS
+//                   buffer (:683-685), and the retained prefix written to
+//                   the cell's slot of the level list (cell order, :687-694);
+//  k_retain_levels  one wave per (level, frame): nth_element of the level
+//                   list when it exceeds the level quota (:697-701).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_retain(ExtractArgs a)
+__device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, const int32_t* counts, int* keep,
+                                   int* pre, int* level_total)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
-    __shared__ BlockScratch bs;
-    __shared__ int s_total[256], s_retain[256];
-    __shared__ uint8_t s_nomore[256];
-    __shared__ int s_nlev;
-    const int level = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-    const LevelGeom L = a.levels[level];
-    uint32_t* cellbuf = sbuf;
-    uint32_t* levbuf = sbuf + a.max_list_cap;
-    int* pos = reinterpret_cast<int*>(levbuf + a.max_level_cap);
-    const int nCells = L.n_cells;
-    const int32_t* counts = a.cell_count + (size_t)f * a.ncells + L.cell_base;
-    for (int c = tid; c < nCells; c += kBlock) s_total[c] = counts[c];
-    __syncthreads();
-    if (tid == 0) {
-        // bNoMore / nToRetain exactly as the reference loop (skipped cells keep
-        // nToRetain = 0, bNoMore = false until the redistribution loop).
-        uint8_t* nomore = s_nomore;
-        const int nfc = L.nfeatures_cell;
-        int nNoMore = 0, nToDistribute = 0;
-        for (int c = 0; c < nCells; c++) {
-            nomore[c] = 0;
-            s_retain[c] = 0;
-            if (!a.cells[L.cell_base + c].valid) continue;
-            const int nKeys = s_total[c];
-            if (nKeys > nfc) {
-                s_retain[c] = nfc;
-            } else {
-                s_retain[c] = nKeys;
-                nToDistribute += nfc - nKeys;
-                nomore[c] = 1;
-                nNoMore++;
-            }
-        }
-        while (nToDistribute > 0 && nNoMore < nCells) {
-            const int nNew = nfc + (int)ceilf(__fdiv_rn((float)nToDistribute, (float)(nCells - nNoMore)));
-            nToDistribute = 0;
-            for (int c = 0; c < nCells; c++) {
-                if (!nomore[c]) {
-                    if (s_total[c] > nNew) {
-                        s_retain[c] = nNew;
-                    } else {
-                        s_retain[c] = s_total[c];
-                        nToDistribute += nNew - s_total[c];
-                        nomore[c] = 1;
-                        nNoMore++;
-                    }
+    const int lane = threadIdx.x & 63;
+    const int nCells = L.n_cells, nfc = L.nfeatures_cell;
+    constexpr int kPer = 4;   // cells per lane (<= 256 cells per level)
+    int tot[kPer], ret[kPer];
+    bool nomore[kPer];
+    int toDist = 0, nNoMore = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int c = lane + 64 * k;
+        tot[k] = 0;
+        ret[k] = 0;
+        nomore[k] = false;
+        if (c < nCells) {
+            tot[k] = counts[c];
+            if (a.cells[L.cell_base + c].valid) {
+                if (tot[k] > nfc) {
+                    ret[k] = nfc;
+                } else {
+                    ret[k] = tot[k];
+                    toDist += nfc - tot[k];
+                    nomore[k] = true;
+                    nNoMore++;
                 }
             }
         }
-        s_nlev = 0;
     }
-    __syncthreads();
-    const uint32_t* lists = a.cell_lists + (size_t)f * a.list_entries;
-    for (int c = 0; c < nCells; c++) {
-        const int n = s_total[c], keep = s_retain[c];
-        if (n == 0 || keep == 0) continue;
-        const int take = min(n, keep);
-        const int base = s_nlev;
-        if (base + take > a.max_level_cap) {
-            if (tid == 0) atomicOr(a.error_flags, 2);
-            break;
+    toDist = wave_sum(toDist);
+    nNoMore = wave_sum(nNoMore);
+    while (toDist > 0 && nNoMore < nCells) {
+        const int nNew = nfc + (int)ceilf(__fdiv_rn((float)toDist, (float)(nCells - nNoMore)));
+        int td = 0, nm = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int c = lane + 64 * k;
+            if (c < nCells && !nomore[k]) {
+                if (tot[k] > nNew) {
+                    ret[k] = nNew;
+                } else {
+                    ret[k] = tot[k];
+                    td += nNew - tot[k];
+                    nomore[k] = true;
+                    nm++;
+                }
+            }
         }
-        const uint32_t* src = lists + a.cells[L.cell_base + c].list_off;
-        if (n > keep) {
-            for (int i = tid; i < n; i += kBlock) cellbuf[i] = src[i];
-            __syncthreads();
-            block_nth_element(cellbuf, n, keep, pos, bs);
-            for (int i = tid; i < take; i += kBlock) levbuf[base + i] = cellbuf[i];
-        } else {
-            for (int i = tid; i < take; i += kBlock) levbuf[base + i] = src[i];
+        toDist = wave_sum(td);
+        nNoMore += wave_sum(nm);
+    }
+    int base = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int c = lane + 64 * k;
+        const int take = (c < nCells && tot[k] > 0 && ret[k] > 0) ? min(tot[k], ret[k]) : 0;
+        const int incl = wave_inclusive_scan(take);
+        if (c < nCells) {
+            keep[c] = ret[k];
+            pre[c] = base + incl - take;
         }
-        __syncthreads();
-        if (tid == 0) s_nlev = base + take;
-        __syncthreads();
+        base += __shfl(incl, 63, 64);
     }
-    int nlev = s_nlev;
-    if (nlev > L.n_desired) {
-        block_nth_element(levbuf, nlev, L.n_desired, pos, bs);
-        nlev = L.n_desired;
+    *level_total = base;
+}
+
+__global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_per_block, int wave_words)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int cell = blockIdx.x * waves_per_block + wv, f = blockIdx.y;
+    if (cell >= a.ncells) return;
+    uint32_t* wbuf = sbuf + (size_t)wv * wave_words;
+    int* keep = reinterpret_cast<int*>(wbuf);
+    int* pre = keep + 256;
+    uint32_t* list = wbuf + 512;
+    int* pos = reinterpret_cast<int*>(list + a.max_list_cap);
+    const CellGeom C = a.cells[cell];
+    const LevelGeom L = a.levels[C.level];
+    const int c = cell - L.cell_base;
+    const int32_t* counts = a.cell_count + (size_t)f * a.ncells + L.cell_base;
+    int level_total;
+    level_quota(a, L, counts, keep, pre, &level_total);
+    lds_wave_sync();
+    if (c == 0 && lane == 0) a.level_count[(size_t)f * a.nlevels + C.level] = min(level_total, L.level_cap);
+    if (level_total > L.level_cap) {
+        if (lane == 0) atomicOr(a.error_flags, 2);
+        return;
     }
-    uint32_t* out = a.level_keys + (size_t)f * a.level_entries + L.level_off;
-    for (int i = tid; i < nlev; i += kBlock) out[i] = levbuf[i];
-    if (tid == 0) a.level_count[(size_t)f * a.nlevels + level] = nlev;
+    const int n = counts[c], k = keep[c];
+    if (n == 0 || k == 0) return;
+    const int take = min(n, k);
+    const uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
+    uint32_t* dst = a.level_keys + (size_t)f * a.level_entries + L.level_off + pre[c];
+    if (n > k) {
+        for (int i = lane; i < n; i += 64) list[i] = src[i];
+        lds_wave_sync();
+        wave_nth_element(list, n, k, pos);
+        for (int i = lane; i < take; i += 64) dst[i] = list[i];
+    } else {
+        for (int i = lane; i < take; i += 64) dst[i] = src[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_per_block, int wave_words)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int level = blockIdx.x * waves_per_block + wv, f = blockIdx.y;
+    if (level >= a.nlevels) return;
+    const LevelGeom L = a.levels[level];
+    int32_t* cnt = a.level_count + (size_t)f * a.nlevels + level;
+    const int nlev = *cnt;
+    if (nlev <= L.n_desired) return;
+    uint32_t* list = sbuf + (size_t)wv * wave_words;
+    int* pos = reinterpret_cast<int*>(list + a.max_level_cap);
+    uint32_t* g = a.level_keys + (size_t)f * a.level_entries + L.level_off;
+    for (int i = lane; i < nlev; i += 64) list[i] = g[i];
+    lds_wave_sync();
+    wave_nth_element(list, nlev, L.n_desired, pos);
+    for (int i = lane; i < L.n_desired; i += 64) g[i] = list[i];
+    if (lane == 0) *cnt = L.n_desired;
 }
 
 // ---------------------------------------------------------------------------
@@ -583,9 +726,15 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         timer_end(ctx, "fast");
         timer_begin(ctx, "retain");
         {
-            const size_t lds = (size_t)(g.max_list_cap + g.max_level_cap) * 4 +
-                               (size_t)(std::max(g.max_list_cap, g.max_level_cap) + 8) * 4;
-            hipLaunchKernelGGL(k_retain, dim3(g.nlevels, nb), dim3(256), lds, st, a);
+            // wave-private LDS: keep/pre tables + cell list + partition scratch
+            const int cw = 512 + 2 * g.max_list_cap + 8;
+            const int cwaves = std::max(1, std::min(4, (int)(kRetainLds / (4 * (size_t)cw))));
+            hipLaunchKernelGGL(k_retain_cells, dim3(((int)g.cells.size() + cwaves - 1) / cwaves, nb), dim3(64 * cwaves),
+                               (size_t)cwaves * cw * 4, st, a, cwaves, cw);
+            const int lw = 2 * g.max_level_cap + 8;
+            const int lwaves = std::max(1, std::min(4, (int)(kRetainLds / (4 * (size_t)lw))));
+            hipLaunchKernelGGL(k_retain_levels, dim3((g.nlevels + lwaves - 1) / lwaves, nb), dim3(64 * lwaves),
+                               (size_t)lwaves * lw * 4, st, a, lwaves, lw);
         }
         timer_end(ctx, "retain");
         timer_begin(ctx, "blur");

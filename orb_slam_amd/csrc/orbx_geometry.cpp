@@ -222,7 +222,8 @@ int compute_geometry(Geometry& g, int w, int h)
                 c.list_cap = ((iw + 1) / 2) * ((ih + 1) / 2);
                 c.list_off = list_off;
                 list_off += c.list_cap;
-                g.max_tile_bytes = std::max(g.max_tile_bytes, c.hx * c.hy);
+                // FAST tile: dword-aligned rows (up to 3 bytes of lead-in)
+                g.max_tile_bytes = std::max(g.max_tile_bytes, c.hy * ((c.hx + 6) & ~3));
                 g.max_list_cap = std::max(g.max_list_cap, c.list_cap);
                 g.cells.push_back(c);
             }
@@ -232,7 +233,7 @@ int compute_geometry(Geometry& g, int w, int h)
         // because row 0 is always processed first.
         L.level_cap = nDesired + nCells * (nCells + 1) + 64;
         L.level_off = level_off;
-        level_off += nDesired;
+        level_off += L.level_cap;   // the cell pass writes up to level_cap entries
         g.max_level_cap = std::max(g.max_level_cap, L.level_cap);
         g.max_cells_per_level = std::max(g.max_cells_per_level, nCells);
     }
