@@ -75,7 +75,7 @@ static int realloc_dev(T*& p, size_t count)
 
 static void free_buffers(orbx_ctx* ctx)
 {
-    void* ptrs[] = {ctx->frames, ctx->pyr_raw, ctx->pyr_blur, ctx->cell_lists, ctx->cell_count,
+    void* ptrs[] = {ctx->frames, ctx->pyr_raw, ctx->pyr_blur, ctx->cell_lists, ctx->retain_scratch, ctx->cell_count,
                     ctx->level_keys, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
@@ -105,9 +105,11 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
         if ((r = realloc_dev(ctx->pyr_blur, (size_t)S * g.frame_pyr_bytes)) != ORBX_OK) return r;
         ctx->cap_pyr_bytes = g.frame_pyr_bytes;
     }
-    if (g.list_entries > ctx->cap_list_entries) {
-        if ((r = realloc_dev(ctx->cell_lists, (size_t)S * g.list_entries)) != ORBX_OK) return r;
-        ctx->cap_list_entries = g.list_entries;
+    if (g.list_entries + 4LL * (long long)g.cells.size() > ctx->cap_list_entries) {
+        const long long e = g.list_entries + 4LL * (long long)g.cells.size();
+        if ((r = realloc_dev(ctx->cell_lists, (size_t)S * e)) != ORBX_OK) return r;
+        if ((r = realloc_dev(ctx->retain_scratch, (size_t)S * e)) != ORBX_OK) return r;
+        ctx->cap_list_entries = e;
     }
     if ((int)g.cells.size() > ctx->cap_cells) {
         if ((r = realloc_dev(ctx->cell_count, (size_t)S * g.cells.size())) != ORBX_OK) return r;

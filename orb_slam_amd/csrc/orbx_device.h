@@ -373,6 +373,22 @@ __device__ inline void lds_wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Ordering point for a wave working on a list in global memory (same CU:
+// workgroup scope keeps the CU's L1 coherent with its own stores).
+__device__ inline void global_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <bool kGlobal>
+__device__ inline void nth_sync()
+{
+    if constexpr (kGlobal) global_wave_sync();
+    else lds_wave_sync();
+}
+
 __device__ inline int wave_min_int(int v)
 {
 #pragma unroll
@@ -380,6 +396,7 @@ __device__ inline int wave_min_int(int v)
     return v;
 }
 
+template <bool kGlobal = false>
 __device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos)
 {
     int* posR = pos;
@@ -428,18 +445,20 @@ __device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos
     lm1 = wave_min_int(lm1);
     l1 = wave_min_int(l1);
     rm = wave_max(rm);
-    lds_wave_sync();
+    nth_sync<kGlobal>();
     for (int k = lane; k < m; k += 64) {
         const int i = posL[k], j = posR[k];
         const uint32_t t = a[i];
         a[i] = a[j];
         a[j] = t;
     }
-    lds_wave_sync();
+    nth_sync<kGlobal>();
     return (m == 0) ? l1 : min(lm1, rm);
 }
 
 // std::nth_element(a, a + nth, a + n, greater-by-response), one wave.
+// kGlobal: list and scratch in global memory (lists too long for LDS).
+template <bool kGlobal = false>
 __device__ inline void wave_nth_element(uint32_t* a, int n, int nth, int* pos)
 {
     if (n == 0 || nth == n) return;
@@ -454,18 +473,18 @@ __device__ inline void wave_nth_element(uint32_t* a, int n, int nth, int* pos)
                 a[first] = a[nth];
                 a[nth] = t;
             }
-            lds_wave_sync();
+            nth_sync<kGlobal>();
             return;
         }
         --depth;
         if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
-        lds_wave_sync();
-        const int cut = wave_hoare_partition(a, first, last, pos);
+        nth_sync<kGlobal>();
+        const int cut = wave_hoare_partition<kGlobal>(a, first, last, pos);
         if (cut <= nth) first = cut;
         else last = cut;
     }
     if (lane == 0) insertion_sort(a, first, last);
-    lds_wave_sync();
+    nth_sync<kGlobal>();
 }
 
 }  // namespace orbx

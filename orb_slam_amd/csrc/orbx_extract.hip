@@ -22,6 +22,7 @@
 namespace orbx {
 
 constexpr size_t kRetainLds = 128 * 1024;   // LDS budget of a retain block
+constexpr int kRetainCellCap = 1024;        // cell lists up to this length sort in LDS
 
 __constant__ int8_t c_pattern[256][4] = {
 #include "orbx_pattern.inc"
@@ -44,6 +45,7 @@ struct ExtractArgs {
     uint8_t* out_desc;
     int32_t* out_n;
     int32_t* error_flags;
+    int32_t* retain_scratch;        // slots x (list_entries + 4 ncells): global nth_element scratch
     long long frame_pyr_bytes;
     int first_slot;
     int w, h;
@@ -146,48 +148,29 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 // (k = 0..15, OpenCV offsets), S = max(M_dark, M_bright) - 1 where M_dark is
 // the best 9-arc minimum of d and M_bright that of -d.  FAST at threshold t
 // classifies the pixel as a corner iff S >= t, and cornerScore<16> returns
-// exactly S (OpenCV 2.4 fast.cpp / fast_score.cpp).  Returns S if S >= tmin,
-// else 0.
+// exactly S (OpenCV 2.4 fast.cpp / fast_score.cpp).  A pixel whose compass
+// pre-test passes in one direction only has S = that direction's arc - 1.
 // ---------------------------------------------------------------------------
-__device__ inline int fast_score(const uint8_t* t, int pitch, int tmin)
+// Best 9-arc minimum of sgn * (v - p_k) (the "dark" arc for sgn = +1, the
+// "bright" arc for sgn = -1).
+__device__ inline int fast_arc(const uint8_t* t, int pitch, int sgn)
 {
     const int v = t[0];
     const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
                          3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
                          -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
                          -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
-    int d[16];
+    int d[16], m2[16], m4[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
-    // quick rejection: a 9-arc contains >= 2 of the 4 compass points
-    int nb = 0, nd = 0;
+    for (int k = 0; k < 16; k++) d[k] = sgn * (v - (int)t[off[k]]);
 #pragma unroll
-    for (int k = 0; k < 16; k += 4) {
-        nd += d[k] > tmin;
-        nb += d[k] < -tmin;
-    }
-    if (nd < 2 && nb < 2) return 0;
-    int m2[16], m4[16], mx2[16], mx4[16];
+    for (int k = 0; k < 16; k++) m2[k] = min(d[k], d[(k + 1) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
+    for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
+    int best = -1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        m4[k] = min(m2[k], m2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-    }
-    int dark = -1000, bright = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn = min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        dark = max(dark, mn);
-        bright = min(bright, mx);
-    }
-    const int S = max(dark, -bright) - 1;
-    return S >= tmin ? S : 0;
+    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]));
+    return best;
 }
 
 // One workgroup per (cell, frame).  LDS: the cell ROI with dword-aligned rows
@@ -206,11 +189,33 @@ __device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
     return k < 4 ? byte_of(lo, k) : (k < 8 ? byte_of(mid, k - 4) : byte_of(hi, k - 8));
 }
 
+// (row, column) walk of a row-major index advancing by a fixed stride,
+// without a division per step.
+struct RowWalk {
+    int r, q, dr, dq, nq;
+    __device__ RowWalk(int start, int stride, int n_q) : nq(n_q)
+    {
+        r = start / n_q;
+        q = start - r * n_q;
+        dr = stride / n_q;
+        dq = stride - dr * n_q;
+    }
+    __device__ void next()
+    {
+        r += dr;
+        q += dq;
+        if (q >= nq) {
+            q -= nq;
+            r++;
+        }
+    }
+};
+
 __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
-    __shared__ uint16_t cand[kWaves][256];
+    __shared__ uint32_t cand[kWaves][256];   // tile position | direction flags << 16
     const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
@@ -227,9 +232,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     uint8_t* sm = smem + tile_pitch_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
-    for (int i = tid; i < hy * nq; i += kBlock) {
-        const int r = i / nq, q = i - r * nq;
-        tile32[i] = *reinterpret_cast<const uint32_t*>(src + (size_t)r * L.stride + 4 * q);
+    {
+        RowWalk w(tid, kBlock, nq);
+        for (int i = tid; i < hy * nq; i += kBlock, w.next())
+            tile32[i] = *reinterpret_cast<const uint32_t*>(src + (size_t)w.r * L.stride + 4 * w.q);
     }
     // S' is 0 outside the interior rows [3, hy-4]; the interior rows are
     // fully rewritten below
@@ -241,11 +247,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     const int tmin = min(a.fast_th, a.fast_th_low);
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
     const int nunits = (hy - 6) * nq;
-    for (int u0 = wv * 64; u0 < nunits; u0 += kBlock) {
+    RowWalk cw_(wv * 64 + lane, kBlock, nq);
+    for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
         const int u = u0 + lane;
+        const int r = 3 + cw_.r, q = cw_.q;
         int mask = 0;
         if (u < nunits) {
-            const int r = 3 + u / nq, q = u - (u / nq) * nq;
             const uint32_t* row = tile32 + r * nq + q;
             const uint32_t mid = row[0];
             const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
@@ -259,28 +266,36 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 const int p4 = byte12(lo, mid, hi, 4 + j + 3), p12 = byte12(lo, mid, hi, 4 + j - 3);
                 const bool d0 = v - p0 > tmin, d4 = v - p4 > tmin, d8 = v - p8 > tmin, d12 = v - p12 > tmin;
                 const bool b0 = p0 - v > tmin, b4 = p4 - v > tmin, b8 = p8 - v > tmin, b12 = p12 - v > tmin;
-                const bool ok = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) ||
-                                (b4 && b8) || (b8 && b12) || (b12 && b0);
-                mask |= ok << j;
+                const bool okd = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0);
+                const bool okb = (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0);
+                mask |= (okd ? 1 : 0) << (2 * j);
+                mask |= (okb ? 2 : 0) << (2 * j);
             }
             sm32[r * nq + q] = 0;
         }
-        const int cnt = __popc(mask);
+        const int cnt = __popc((mask | (mask >> 1)) & 0x55);
         const int incl = wave_inclusive_scan(cnt);
         const int ntot = __shfl(incl, 63, 64);
         int w = incl - cnt;
         if (mask) {
-            const int r = 3 + u / nq, q = u - (u / nq) * nq;
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (mask & (1 << j)) cand[wv][w++] = (uint16_t)(r * P + 4 * q + j);
+            for (int j = 0; j < 4; j++) {
+                const int fl = (mask >> (2 * j)) & 3;
+                if (fl) cand[wv][w++] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int i = lane; i < ntot; i += 64) {
-            const int pos = cand[wv][i];
-            sm[pos] = (uint8_t)fast_score(tile + pos, P, tmin);
+        for (int i0 = 0; i0 < ntot; i0 += 64) {
+            const int i = i0 + lane;
+            const uint32_t cw = i < ntot ? cand[wv][i] : 0u;
+            const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
+            int S = 0;
+            if (fl) S = fast_arc(tile + pos, P, (fl & 1) ? 1 : -1);
+            if (__any(fl == 3) && fl == 3) S = max(S, fast_arc(tile + pos, P, -1));
+            S -= 1;
+            if (fl) sm[pos] = (uint8_t)(S >= tmin ? S : 0);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -289,8 +304,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     __syncthreads();
     // non-max suppression: keep S' if it beats all 8 neighbours' S'
     int c1 = 0;
-    for (int u = tid; u < nunits; u += kBlock) {
-        const int r = 3 + u / nq, q = u - (u / nq) * nq;
+    RowWalk nw(tid, kBlock, nq);
+    for (int u = tid; u < nunits; u += kBlock, nw.next()) {
+        const int r = 3 + nw.r, q = nw.q;
         uint32_t word = 0;
         const uint32_t* m = sm32 + r * nq + q;
         const uint32_t mid = m[0];
@@ -325,12 +341,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
     uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
     int base = 0, buf = 1;
-    for (int u0 = 0; u0 < nunits; u0 += kBlock) {
+    RowWalk ow(tid, kBlock, nq);
+    for (int u0 = 0; u0 < nunits; u0 += kBlock, ow.next()) {
         const int u = u0 + tid;
         uint32_t word = 0;
         int cnt = 0;
         if (u < nunits) {
-            word = tile32[(3 + u / nq) * nq + (u - (u / nq) * nq)];
+            word = tile32[(3 + ow.r) * nq + ow.q];
 #pragma unroll
             for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
         }
@@ -338,7 +355,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         int off = base + block_exclusive_scan(cnt, &total, bs, buf);
         buf ^= 1;
         if (cnt) {
-            const int r = 3 + u / nq, q = u - (u / nq) * nq;
+            const int r = 3 + ow.r, q = ow.q;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int s = byte_of(word, j);
@@ -367,8 +384,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
 //  k_retain_levels  one wave per (level, frame): nth_element of the level
 //                   list when it exceeds the level quota (:697-701).
 // ---------------------------------------------------------------------------
-__device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, const int32_t* counts, int* keep,
-                                   int* pre, int* level_total)
+__device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, const int32_t* counts, int cell,
+                                   int* keep_c, int* pre_c, int* level_total)
 {
     const int lane = threadIdx.x & 63;
     const int nCells = L.n_cells, nfc = L.nfeatures_cell;
@@ -418,18 +435,21 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
         toDist = wave_sum(td);
         nNoMore += wave_sum(nm);
     }
-    int base = 0;
+    int base = 0, my_keep = 0, my_pre = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         const int c = lane + 64 * k;
         const int take = (c < nCells && tot[k] > 0 && ret[k] > 0) ? min(tot[k], ret[k]) : 0;
         const int incl = wave_inclusive_scan(take);
-        if (c < nCells) {
-            keep[c] = ret[k];
-            pre[c] = base + incl - take;
+        const int kk = __shfl(ret[k], cell & 63, 64), pp = __shfl(base + incl - take, cell & 63, 64);
+        if ((cell >> 6) == k) {
+            my_keep = kk;
+            my_pre = pp;
         }
         base += __shfl(incl, 63, 64);
     }
+    *keep_c = my_keep;
+    *pre_c = my_pre;
     *level_total = base;
 }
 
@@ -439,33 +459,34 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cell = blockIdx.x * waves_per_block + wv, f = blockIdx.y;
     if (cell >= a.ncells) return;
-    uint32_t* wbuf = sbuf + (size_t)wv * wave_words;
-    int* keep = reinterpret_cast<int*>(wbuf);
-    int* pre = keep + 256;
-    uint32_t* list = wbuf + 512;
-    int* pos = reinterpret_cast<int*>(list + a.max_list_cap);
+    uint32_t* list = sbuf + (size_t)wv * wave_words;
+    int* pos = reinterpret_cast<int*>(list + kRetainCellCap);
     const CellGeom C = a.cells[cell];
     const LevelGeom L = a.levels[C.level];
     const int c = cell - L.cell_base;
     const int32_t* counts = a.cell_count + (size_t)f * a.ncells + L.cell_base;
-    int level_total;
-    level_quota(a, L, counts, keep, pre, &level_total);
-    lds_wave_sync();
+    int k, pre, level_total;
+    level_quota(a, L, counts, c, &k, &pre, &level_total);
     if (c == 0 && lane == 0) a.level_count[(size_t)f * a.nlevels + C.level] = min(level_total, L.level_cap);
     if (level_total > L.level_cap) {
         if (lane == 0) atomicOr(a.error_flags, 2);
         return;
     }
-    const int n = counts[c], k = keep[c];
+    const int n = counts[c];
     if (n == 0 || k == 0) return;
     const int take = min(n, k);
-    const uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    uint32_t* dst = a.level_keys + (size_t)f * a.level_entries + L.level_off + pre[c];
-    if (n > k) {
+    uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
+    uint32_t* dst = a.level_keys + (size_t)f * a.level_entries + L.level_off + pre;
+    if (n > k && n <= kRetainCellCap) {
         for (int i = lane; i < n; i += 64) list[i] = src[i];
         lds_wave_sync();
         wave_nth_element(list, n, k, pos);
         for (int i = lane; i < take; i += 64) dst[i] = list[i];
+    } else if (n > k) {
+        // long list: replay in place in global memory
+        int* gpos = a.retain_scratch + (size_t)f * (a.list_entries + 4 * a.ncells) + C.list_off + 4 * cell;
+        wave_nth_element<true>(src, n, k, gpos);
+        for (int i = lane; i < take; i += 64) dst[i] = src[i];
     } else {
         for (int i = lane; i < take; i += 64) dst[i] = src[i];
     }
@@ -586,12 +607,24 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
 
 // ---------------------------------------------------------------------------
 // IC_Angle + computeOrbDescriptor + output assembly, one wave per keypoint.
+// The wave first stages, with independent dword loads, the 31x31 unblurred
+// patch (IC_Angle reads radius 15) and the 37x37 blurred patch (rotated
+// pattern points reach cvRound(13*sqrt(2)) = 18) in LDS, so the gathers
+// cost one memory round trip instead of a dependent chain.
 // ---------------------------------------------------------------------------
+constexpr int kIcRows = 2 * kHalfPatch + 1;          // 31
+constexpr int kIcPitch = 36;                         // 9 dwords: 31 bytes + alignment
+constexpr int kBrR = 18;                             // pattern reach
+constexpr int kBrRows = 2 * kBrR + 1;                // 37
+constexpr int kBrPitch = 40;                         // 10 dwords: 37 bytes + alignment
+constexpr int kDescWaveBytes = kIcRows * kIcPitch + kBrRows * kBrPitch;
+
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
 {
+    __shared__ __attribute__((aligned(16))) uint8_t s_patch[kWaves][kDescWaveBytes];
     const int f = blockIdx.y;
-    const int lane = threadIdx.x & 63;
-    const int k = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k = blockIdx.x * kWaves + wv;
     const int32_t* lc = a.level_count + (size_t)f * a.nlevels;
     int total = 0, level = -1, local = 0;
     for (int l = 0; l < a.nlevels; l++) {
@@ -607,19 +640,44 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     const LevelGeom L = a.levels[level];
     const uint32_t e = a.level_keys[(size_t)f * a.level_entries + L.level_off + local];
     const int score = (int)(e >> 24), y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
-    // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151)
-    const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off +
-                         (size_t)(kEdge + y) * L.stride + kEdge + x;
+    const int X = kEdge + x, Y = kEdge + y;   // padded coordinates
+    uint8_t* ic = s_patch[wv];
+    uint8_t* br = ic + kIcRows * kIcPitch;
+    {
+        const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
+        const uint8_t* blr = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
+        const int ix0 = (X - kHalfPatch) & ~3, bx0 = (X - kBrR) & ~3;
+        uint32_t* ic32 = reinterpret_cast<uint32_t*>(ic);
+        uint32_t* br32 = reinterpret_cast<uint32_t*>(br);
+        for (int i = lane; i < kIcRows * (kIcPitch / 4); i += 64) {
+            const int r = i / (kIcPitch / 4), q = i - r * (kIcPitch / 4);
+            ic32[i] = *reinterpret_cast<const uint32_t*>(raw + (size_t)(Y - kHalfPatch + r) * L.stride + ix0 + 4 * q);
+        }
+        for (int i = lane; i < kBrRows * (kBrPitch / 4); i += 64) {
+            const int r = i / (kBrPitch / 4), q = i - r * (kBrPitch / 4);
+            br32[i] = *reinterpret_cast<const uint32_t*>(blr + (size_t)(Y - kBrR + r) * L.stride + bx0 + 4 * q);
+        }
+        ic += (X - kHalfPatch) - ix0 + kHalfPatch * kIcPitch + kHalfPatch;   // -> patch center
+        br += (X - kBrR) - bx0 + kBrR * kBrPitch + kBrR;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151); lanes
+    // 0..30 take rows v = 1..8 and the centre row, lanes 32..62 rows 9..15
     int m01 = 0, m10 = 0;
-    if (lane < 2 * kHalfPatch + 1) {
-        const int u = lane - kHalfPatch;
-        m10 = u * raw[u];
-        for (int v = 1; v <= kHalfPatch; v++) {
-            const int d = a.umax[v];
-            if (u >= -d && u <= d) {
-                const int vp = raw[u + v * L.stride], vm = raw[u - v * L.stride];
-                m01 += v * (vp - vm);
-                m10 += u * (vp + vm);
+    {
+        const int u = (lane & 31) - kHalfPatch;
+        if ((lane & 31) < kIcRows) {
+            const int v0 = lane < 32 ? 1 : 9, v1 = lane < 32 ? 8 : kHalfPatch;
+            if (lane < 32) m10 = u * ic[u];
+            for (int v = v0; v <= v1; v++) {
+                const int d = a.umax[v];
+                if (u >= -d && u <= d) {
+                    const int vp = ic[u + v * kIcPitch], vm = ic[u - v * kIcPitch];
+                    m01 += v * (vp - vm);
+                    m10 += u * (vp + vm);
+                }
             }
         }
     }
@@ -630,18 +688,16 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     const float factorPI = (float)(M_PI / 180.f);
     float sa, ca;
     cr_sincosf(__fmul_rn(angle, factorPI), &sa, &ca);
-    const uint8_t* blur = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off +
-                          (size_t)(kEdge + y) * L.stride + kEdge + x;
     uint8_t* desc = a.out_desc + ((size_t)(a.first_slot + f) * a.nfeatures + k) * 32;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const int q = r * 64 + lane;
         const float px1 = c_pattern[q][0], py1 = c_pattern[q][1];
         const float px2 = c_pattern[q][2], py2 = c_pattern[q][3];
-        const int t0 = blur[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * L.stride +
-                            cv_round(__fsub_rn(__fmul_rn(px1, ca), __fmul_rn(py1, sa)))];
-        const int t1 = blur[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * L.stride +
-                            cv_round(__fsub_rn(__fmul_rn(px2, ca), __fmul_rn(py2, sa)))];
+        const int t0 = br[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * kBrPitch +
+                          cv_round(__fsub_rn(__fmul_rn(px1, ca), __fmul_rn(py1, sa)))];
+        const int t1 = br[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * kBrPitch +
+                          cv_round(__fsub_rn(__fmul_rn(px2, ca), __fmul_rn(py2, sa)))];
         const unsigned long long bits = __ballot(t0 < t1);
         if (lane == r) *reinterpret_cast<unsigned long long*>(desc + 8 * r) = bits;
     }
@@ -685,6 +741,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
     a.out_desc = ctx->out_desc;
     a.out_n = ctx->out_n;
     a.error_flags = ctx->error_flags;
+    a.retain_scratch = ctx->retain_scratch;
     a.frame_pyr_bytes = g.frame_pyr_bytes;
     a.w = g.w;
     a.h = g.h;
@@ -726,9 +783,10 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         timer_end(ctx, "fast");
         timer_begin(ctx, "retain");
         {
-            // wave-private LDS: keep/pre tables + cell list + partition scratch
-            const int cw = 512 + 2 * g.max_list_cap + 8;
-            const int cwaves = std::max(1, std::min(4, (int)(kRetainLds / (4 * (size_t)cw))));
+            // wave-private LDS: cell list + partition scratch (longer lists
+            // are replayed in global memory)
+            const int cw = 2 * kRetainCellCap + 8;
+            const int cwaves = 4;
             hipLaunchKernelGGL(k_retain_cells, dim3(((int)g.cells.size() + cwaves - 1) / cwaves, nb), dim3(64 * cwaves),
                                (size_t)cwaves * cw * 4, st, a, cwaves, cw);
             const int lw = 2 * g.max_level_cap + 8;

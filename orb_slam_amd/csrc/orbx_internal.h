@@ -10,6 +10,8 @@
 //   cell_lists  slots x list_entries  u32      FAST corners per cell, raster
 //                                              order, packed score<<24|y<<12|x
 //                                              (level coordinates)
+//   retain_scratch slots x (list_entries + 4 n_cells) i32  nth_element
+//                                              scratch for lists too long for LDS
 //   cell_count  slots x n_cells_total i32
 //   level_keys  slots x level_entries u32      retained keypoints per level
 //   level_count slots x nlevels       i32
@@ -129,6 +131,7 @@ struct orbx_ctx {
     uint8_t* pyr_raw = nullptr;
     uint8_t* pyr_blur = nullptr;
     uint32_t* cell_lists = nullptr;
+    int32_t* retain_scratch = nullptr;   // slots x (list_entries + 4 cells)
     int32_t* cell_count = nullptr;
     uint32_t* level_keys = nullptr;
     int32_t* level_count = nullptr;

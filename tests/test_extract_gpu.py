@@ -20,6 +20,7 @@ CASES = [
     ("texture", 96, 80, 100, 3),
     ("noise", 333, 251, 500, 4),
     ("texture", 1920, 1080, 2000, 5),
+    ("noise", 1920, 1080, 2000, 7),      # cell lists beyond the LDS replay cap
     ("rects", 640, 480, 1000, 6),
 ]
 
