@@ -1,14 +1,22 @@
 """Benchmark: frames/sec ORB extract+match (640x480, 1000 kp) on MI355X.
 
-Workload (BASELINE.json configs[1]): synthetic 640x480
-mono8 "TUM-style" sequences (one per rank, already resident in HBM), 8-level
-pyramid, 1000 keypoints.  One step = one batch of B frames: ORB extraction of
-every frame (ORBextractor::operator()) plus SearchForInitialization of every
-frame against its predecessor (window 100, nnratio 0.9, orientation check;
-the sequence is treated as cyclic so every frame is matched).
+Workloads (BASELINE.json configs):
+  c2 (default, the headline metric): synthetic 640x480 mono8 "TUM-style"
+     sequences (one per rank, already resident in HBM), 8-level pyramid, 1000
+     keypoints.  One step = one batch of B frames: ORB extraction of every
+     frame (ORBextractor::operator()) plus SearchForInitialization of every
+     frame against its predecessor (window 100, nnratio 0.9, orientation
+     check; the sequence is treated as cyclic so every frame is matched).
+  c3: 1920x1080, 2000 keypoints, extraction + brute-force Hamming matching of
+     every frame against its predecessor (pairs/s; one new pair per frame).
+  c5: local BA, 20 keyframes x 2000 map points (5 + 10 LM iterations, two
+     outlier passes), a batch of independent problems per step (problems/s);
+     inputs cross the host boundary (the reference hands BA its graph from
+     host memory), so this rate includes the H2D/D2H copies.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns its sequence; the
-only collective is the end-of-run gather of stats (RCCL).  Weak scaling.
+Multi-GPU: one process per GPU (torchrun); each rank owns its sequence (or
+problems); the only collective is the end-of-run gather of stats (RCCL).
+Weak scaling.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 """
@@ -31,10 +39,15 @@ from orb_slam_amd import dist as odist, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 WORKLOADS = {
-    "c2": dict(w=640, h=480, nfeatures=1000, desc="640x480 mono8, 8 levels x1.2, 1000 kp: ORB extract + "
-               "SearchForInitialization vs previous frame"),
-    "c3": dict(w=1920, h=1080, nfeatures=2000, desc="1920x1080 mono8, 8 levels x1.2, 2000 kp: ORB extract + "
-               "SearchForInitialization vs previous frame"),
+    "c2": dict(w=640, h=480, nfeatures=1000, batch=256,
+               metric="frames/sec ORB extract+match (640x480, 1000 kp)", unit="frames/s",
+               desc="640x480 mono8, 8 levels x1.2, 1000 kp: ORB extract + SearchForInitialization vs previous frame"),
+    "c3": dict(w=1920, h=1080, nfeatures=2000, batch=64,
+               metric="pairs/sec ORB extract + brute-force Hamming match (1920x1080, 2000 kp)", unit="pairs/s",
+               desc="1920x1080 mono8, 8 levels x1.2, 2000 kp: ORB extract + brute-force Hamming vs previous frame"),
+    "c5": dict(batch=32, metric="local BA problems/sec (20 KF x 2000 MP, 5+10 LM iterations)", unit="problems/s",
+               desc="Optimizer::LocalBundleAdjustment core: 20 keyframes (+2 fixed) x 2000 map points, "
+                    "Huber, Schur + LLT, 5+10 LM iterations, two outlier passes"),
 }
 
 
@@ -48,8 +61,9 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return sizes
 
 
-def algorithmic_bytes(w, h, nfeatures):
-    """Per-frame algorithmic bytes per stage."""
+def algorithmic_bytes(w, h, nfeatures, match="init"):
+    """Per-frame algorithmic bytes per stage: each
+    stage's compulsory HBM reads + writes of its inputs/outputs."""
     sz = level_sizes(w, h)
     px = [a * b for a, b in sz]
     return {
@@ -58,11 +72,17 @@ def algorithmic_bytes(w, h, nfeatures):
         "fast": sum(px),                                     # one read of every level
         "blur": 2 * sum(px),                                 # read + write
         "describe": nfeatures * (512 + 700 + 60),            # samples, IC patch, outputs
-        "retain": 0, "match": 0,
+        "retain": 0,
+        "match": (2 * nfeatures * 32 + nfeatures * 4) if match == "bf" else 0,
     }
 
 
-def cpu_baseline(frames, nfeatures, budget_s):
+def lba_bytes(n_kf, n_pts, n_edges):
+    """Algorithmic bytes of one LM iteration."""
+    return n_edges * (2 * 8 + 4 + 8) + n_edges * 144 + n_kf * 7 * 8 + n_pts * 3 * 8
+
+
+def cpu_baseline_frames(frames, nfeatures, budget_s, bf=False):
     """Oracle (C++ restatement, 1 core) on a bounded sample of the workload."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
@@ -75,56 +95,126 @@ def cpu_baseline(frames, nfeatures, budget_s):
     while time.perf_counter() - t0 < budget_s and n < len(frames) * 4:
         k, d = ex(frames[n % len(frames)])
         if prev is not None:
-            F1 = ox.frame_view(prev[0], prev[1], w, h)
-            F2 = ox.frame_view(k, d, w, h)
-            pm = np.stack([prev[0]["x"], prev[0]["y"]], 1).astype(np.float32).copy()
-            m = np.zeros(len(prev[0]), np.int32)
-            nm = ctypes.c_int()
-            L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), oracle_lib.ptr(pm),
-                                                 oracle_lib.ptr(m), 100, 0.9, 1, ctypes.byref(nm))
+            if bf:
+                bi, b1, b2 = (np.zeros(len(prev[1]), np.int32) for _ in range(3))
+                L.orbx_ref_hamming_bf(oracle_lib.ptr(prev[1]), len(prev[1]), oracle_lib.ptr(d), len(d),
+                                      oracle_lib.ptr(bi), oracle_lib.ptr(b1), oracle_lib.ptr(b2))
+            else:
+                F1 = ox.frame_view(prev[0], prev[1], w, h)
+                F2 = ox.frame_view(k, d, w, h)
+                pm = np.stack([prev[0]["x"], prev[0]["y"]], 1).astype(np.float32).copy()
+                m = np.zeros(len(prev[0]), np.int32)
+                nm = ctypes.c_int()
+                L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), oracle_lib.ptr(pm),
+                                                     oracle_lib.ptr(m), 100, 0.9, 1, ctypes.byref(nm))
         prev = (k, d)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames of the same sequence, extract + SearchForInitialization, "
+    what = "brute-force Hamming" if bf else "SearchForInitialization"
+    return {"value": round(n / dt, 3), "unit": "pairs/s" if bf else "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames of the same synthetic sequence ({w}x{h}), extract + {what}, "
                       f"oracle/liborbx_ref.so (g++ -O3), 1 thread, {dt:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verbose", action="store_true")
-    args = ap.parse_args()
+def cpu_baseline_lba(probs, budget_s):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_ba as sb
+    L = oracle_lib.load()
+    L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < budget_s and n < len(probs):
+        p, arrs = sb.to_ctypes(probs[n])
+        es = np.zeros(p.n_edges, np.uint8)
+        pb = np.zeros(p.n_points, np.uint8)
+        st = sb.BAStats()
+        L.orbx_ref_lba(ctypes.byref(p), 5, 10, es.ctypes.data, pb.ctypes.data, ctypes.byref(st))
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "problems/s", "cores": 1, "kind": "port",
+            "sample": f"{n} problems (20 KF x 2000 MP), oracle LBA (dense LLT in place of CHOLMOD), "
+                      f"1 thread, {dt:.1f} s"}
 
-    world, rank, local = odist.env()
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-        dist = tdist
 
-    wl = WORKLOADS[args.workload]
-    w, h, nf, B = wl["w"], wl["h"], wl["nfeatures"], args.batch
+def run_frames(args, wl, rank, local, world, dist):
+    w, h, nf, B = wl["w"], wl["h"], wl["nfeatures"], args.batch or wl["batch"]
+    bf = args.workload == "c3"
     frames = synth.sequence(w, h, B, seed=odist.shard_seed(2000, rank))
     ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=B, device=local if world > 1 else 0)
     ctx.upload(frames)
 
     def step():
         ctx.extract(0, B)
-        ctx.match_prev(0, B, B, window=100, nnratio=0.9, check_ori=True)
+        if bf:
+            ctx.match_bf_prev(0, B, B, th_low=50, nnratio=0.9)
+        else:
+            ctx.match_prev(0, B, B, window=100, nnratio=0.9, check_ori=True)
 
     for _ in range(args.warmup):
         step()
     ctx.sync()
+    elapsed, kernels = timed(args, ctx, step, dist,
+                             ["pyr0", "resize", "fast", "retain", "blur", "describe", "match"])
+    k0, _ = ctx.features(B - 1)
+    _, nm = ctx.matches(B - 1)
+    stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
+    ab = algorithmic_bytes(w, h, nf, "bf" if bf else "init")
+    units_per_launch = {k: B for k in ab}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_frames(frames, nf, args.cpu_budget, bf=bf)
+    check = {"last_frame_keypoints": int(stats[2]), "last_frame_matches": int(stats[3])}
+    cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf, "image": f"{w}x{h}",
+           "parallelism": f"dp{world} (one sequence per GPU)"}
+    ctx.close()
+    return stats, kernels, ab, units_per_launch, cpu, check, cfg
 
+
+def run_lba(args, wl, rank, local, world, dist):
+    from orb_slam_amd import synth_ba as sb
+    P = args.batch or wl["batch"]
+    probs = [sb.make_problem(n_kf=20, n_points=2000, seed=odist.shard_seed(5000, rank) * 1000 + i)
+             for i in range(P)]
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
+    cps = [sb.to_ctypes(pr) for pr in probs]
+    n_edges = int(np.mean([c[0].n_edges for c in cps]))
+
+    def step():
+        fresh = [sb.to_ctypes(pr) for pr in probs]     # BA updates poses in place: restart from the same state
+        arr = (sb.BAProblem * P)(*[c[0] for c in fresh])
+        es = [np.zeros(c[0].n_edges, np.uint8) for c in fresh]
+        pb = [np.zeros(c[0].n_points, np.uint8) for c in fresh]
+        esp = (ctypes.c_void_p * P)(*[e.ctypes.data for e in es])
+        pbp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in pb])
+        st = (sb.BAStats * P)()
+        r = ox.lib().orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, esp, pbp, st)
+        if r != 0:
+            raise ox.OrbxError(r, "orbx_lba_solve_batch")
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    elapsed, kernels = timed(args, ctx, step, dist, ["lba_iter", "lba_outliers"])
+    st = step()
+    stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
+                     dtype=np.float64)
+    ab = {"lba_iter": lba_bytes(22, 2000, n_edges), "lba_outliers": n_edges * 16}
+    units_per_launch = {"lba_iter": P, "lba_outliers": P}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_lba(probs, args.cpu_budget)
+    check = {"iterations_problem0": int(stats[2]), "outliers_pass1_problem0": int(stats[3]),
+             "edges_per_problem": n_edges}
+    cfg = {"workload": wl["desc"], "problems_per_step_per_gpu": P, "keyframes": 20, "map_points": 2000,
+           "parallelism": f"dp{world} (independent problems per GPU; replicas)",
+           "boundary": "host arrays in/out (H2D/D2H inside the timed region)"}
+    ctx.close()
+    return stats, kernels, ab, units_per_launch, cpu, check, cfg
+
+
+def timed(args, ctx, step, dist, names):
     def barrier():
         if dist is not None:
             import torch
@@ -141,46 +231,62 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kernels = {}
-    for name in ["pyr0", "resize", "fast", "retain", "blur", "describe", "match"]:
+    for name in names:
         n, avg, tot = ctx.kernel_time(name)
         kernels[name] = {"launches": n, "avg_ms": avg, "total_ms": tot}
     ctx.timing(False)
+    return elapsed, kernels
 
-    # sanity: the last batch produced features and matches
-    k0, _ = ctx.features(B - 1)
-    _, nm = ctx.matches(B - 1)
-    stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=0, help="frames (or BA problems) per step per GPU")
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = odist.env()
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    wl = WORKLOADS[args.workload]
+    run = run_lba if args.workload == "c5" else run_frames
+    stats, kernels, ab, units, cpu, check, cfg = run(args, wl, rank, local, world, dist)
     allst = odist.gather_stats(stats, dist, device="cuda")
     value, elapsed, _ = odist.job_rate(allst)
 
     if rank == 0:
-        ab = algorithmic_bytes(w, h, nf)
+        # dominant kernel: largest total time; its algorithmic bytes per launch
+        # over its mean launch duration (HIP events on the context stream)
         dom = max((k for k in kernels if kernels[k]["launches"]), key=lambda k: kernels[k]["total_ms"])
-        per_launch = ab[dom] * B / max(1, kernels[dom]["launches"] // args.steps)
+        launches_per_step = max(1, kernels[dom]["launches"] // args.steps)
+        per_launch = ab.get(dom, 0) * units.get(dom, 1) / launches_per_step
         avg_s = kernels[dom]["avg_ms"] / 1e3
         achieved = per_launch / avg_s / 1e9 if avg_s > 0 and per_launch > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
                 "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": kernels[dom]["avg_ms"]}
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(frames, nf, args.cpu_budget)
         out = {
-            "metric": "frames/sec ORB extract+match (640x480, 1000 kp)" if args.workload == "c2"
-            else "pairs/sec ORB extract+match (1920x1080, 2000 kp)",
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (orb_slam_amd/synth.py sequence, seed 2000+rank)",
-            "config": {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf,
-                       "image": f"{w}x{h}", "parallelism": f"dp{world} (one sequence per GPU)"},
-            "roofline": roof, "cpu_baseline": cpu,
-            "check": {"last_frame_keypoints": int(stats[2]), "last_frame_matches": int(stats[3])},
+            "metric": wl["metric"], "value": round(value, 2), "unit": wl["unit"], "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if args.workload == "c5" else "u8",
+            "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py, seeded per rank)",
+            "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -114,6 +114,13 @@ int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */
 int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len,
                         int window, float nnratio, int check_ori);
+/* Brute-force matching (config C3) of slots [first, first+count) against
+ * their predecessors, same slot pairing as orbx_dev_match_prev: every
+ * keypoint of s-1 against every keypoint of s, accepted when best <= th_low
+ * and best < nnratio * second (rule of src/ORBmatcher.cc:640-654); results
+ * via orbx_dev_read_matches. */
+int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len,
+                           int th_low, float nnratio);
 int orbx_dev_sync(orbx_ctx* ctx);
 /* Read back one slot's features / its match result (after sync). */
 int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps,
@@ -121,8 +128,8 @@ int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps,
 int orbx_dev_read_matches(orbx_ctx* ctx, int slot, int32_t* matches12, int cap,
                           int* n_matches, int* n1);
 /* Timing of the dominant kernels over the launches issued since the last
- * reset, measured with hipEvents on the context stream.  name: "fast",
- * "retain", "pyramid", "blur", "describe", "match".  Returns the number of
+ * reset, measured with hipEvents on the context stream.  name: "pyr0",
+ * "resize", "fast", "retain", "blur", "describe", "match".  Returns the number of
  * timed launches; *avg_ms receives the mean duration. */
 int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms,
                          double* total_ms);

@@ -66,6 +66,13 @@ def build(verbose=False, jobs=None):
     if cmds or not LIB.exists():
         link = [cc, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)]
         run(link)
+    # C++ adapter demo (the reference-style C++ binding)
+    demo_src = PKG / "adapters" / "adapter_demo.cpp"
+    demo = PKG / "adapters" / "adapter_demo"
+    adapter_hdr = PKG / "adapters" / "orbx_adapters.hpp"
+    if demo_src.exists() and (not demo.exists() or _needs(demo, demo_src, [adapter_hdr, LIB])):
+        run(["g++", "-O2", "-std=c++17", "-Wall", f"-I{PKG.parent / 'include'}", str(demo_src), "-o", str(demo),
+             f"-L{PKG}", "-lorbx", "-Wl,-rpath,$ORIGIN/.."])
     return LIB
 
 

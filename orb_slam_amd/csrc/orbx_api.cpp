@@ -286,6 +286,15 @@ int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wi
     return launch_match_prev(ctx, first, count, seq_len, window, nnratio, check_ori);
 }
 
+int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)
+{
+    if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || seq_len <= 0) return ORBX_ERR_ARG;
+    if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
+    if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
+    hipSetDevice(ctx->device);
+    return launch_match_bf_prev(ctx, first, count, seq_len, th_low, nnratio);
+}
+
 int orbx_dev_sync(orbx_ctx* ctx)
 {
     if (!ctx) return ORBX_ERR_ARG;

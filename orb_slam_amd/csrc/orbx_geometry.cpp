@@ -153,6 +153,7 @@ int compute_geometry(Geometry& g, int w, int h)
         L.scale = g.scale[l];
         L.patch_size = (float)(int)(kPatch * g.scale[l]);
         L.n_desired = g.features_per_level[l];
+        while (g.res_cols.size() % 4) g.res_cols.push_back(ResizeCol{0, 0, 0, 0});   // 32-byte aligned runs
         L.res_col_off = (int)g.res_cols.size();
         L.res_row_off = (int)g.res_rows.size();
         if (l > 0) {

@@ -167,6 +167,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count);
 // orbx_match.hip
 int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window,
                       float nnratio, int check_ori);
+int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio);
 // timing helpers (orbx_api.cpp)
 void timer_begin(orbx_ctx* ctx, const char* name);
 void timer_end(orbx_ctx* ctx, const char* name);

@@ -893,7 +893,9 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
                                              hipMemcpyHostToDevice));
                 break;
             }
+            timer_begin(ctx, "lba_iter");
             hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kBlock), lds, ctx->stream, dd, it, lds_cap);
+            timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
             ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
             ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -901,11 +903,13 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             for (int i = 0; i < P; i++) running |= devs[i].status == kRunning;
             if (!running) break;
         }
+        timer_begin(ctx, "lba_outliers");
         hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(64), 0, ctx->stream, dd,
                            reinterpret_cast<const int*>(d + o_all_ep), reinterpret_cast<const int*>(d + o_all_eps),
                            reinterpret_cast<int*>(d + o_all_nobs), d + o_all_st, d + o_all_bad, pass + 1,
                            probs[0].chi2_threshold, reinterpret_cast<const double*>(d + o_all_isig),
                            reinterpret_cast<int*>(d + o_nout), reinterpret_cast<const long long*>(d + o_offs));
+        timer_end(ctx, "lba_outliers");
         ORBX_HIP_CHECK(hipGetLastError());
         std::vector<int> nout(P);
         ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));

@@ -56,6 +56,72 @@ __global__ __launch_bounds__(256) void k_match_prev(MatchPrevArgs a)
                           a.match12 + (size_t)s * a.nfeatures, a.match_n + s, nullptr, L, bs, a.error_flags);
 }
 
+// Brute-force matching of slot s against its predecessor (config C3): for
+// each keypoint a of the previous frame, the first index of the smallest
+// Hamming distance over all keypoints of frame s and the second smallest
+// value; accept best <= th_low && best < nnratio * second (the B3 rule of
+// src/ORBmatcher.cc:640-654 applied to all pairs).  grid = (query blocks,
+// pairs); candidates stream through LDS 256 descriptors at a time.
+__global__ __launch_bounds__(256) void k_match_bf_prev(MatchPrevArgs a, int th_low)
+{
+    __shared__ uint4 sb[256][2];
+    const int s = a.first + blockIdx.y;
+    const int prev = (s % a.seq_len == 0) ? s + a.seq_len - 1 : s - 1;
+    const int nA = a.nkp[prev], nB = a.nkp[s];
+    const uint8_t* dA = a.desc + (size_t)prev * a.nfeatures * 32;
+    const uint8_t* dB = a.desc + (size_t)s * a.nfeatures * 32;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= nA) return;   // block-uniform
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
+    if (q < nA) load_desc(dA + (size_t)q * 32, qa, qb);
+    int b1 = 0x7fffffff, b2 = 0x7fffffff, bi = -1;
+    for (int base = 0; base < nB; base += 256) {
+        __syncthreads();
+        const int j = base + threadIdx.x;
+        if (j < nB) load_desc(dB + (size_t)j * 32, sb[threadIdx.x][0], sb[threadIdx.x][1]);
+        __syncthreads();
+        const int cnt = min(256, nB - base);
+        for (int k = 0; k < cnt; k++) {
+            const int d = hamming256(qa, qb, sb[k][0], sb[k][1]);
+            if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                bi = base + k;
+            } else if (d < b2) {
+                b2 = d;
+            }
+        }
+    }
+    int ok = 0;
+    if (q < nA) {
+        ok = (b1 <= th_low && (float)b1 < __fmul_rn((float)b2, a.nnratio));
+        a.match12[(size_t)s * a.nfeatures + q] = ok ? bi : -1;
+    }
+    ok = wave_sum(ok);
+    if ((threadIdx.x & 63) == 0 && ok) atomicAdd(a.match_n + s, ok);
+}
+
+int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)
+{
+    const Geometry& g = ctx->geom;
+    MatchPrevArgs a{};
+    a.kps = ctx->out_kps;
+    a.desc = ctx->out_desc;
+    a.nkp = ctx->out_n;
+    a.match12 = ctx->match12;
+    a.match_n = ctx->match_n;
+    a.nfeatures = g.nfeatures;
+    a.first = first;
+    a.seq_len = seq_len;
+    a.nnratio = nnratio;
+    ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, ctx->stream));
+    timer_begin(ctx, "match");
+    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 255) / 256, count), dim3(256), 0, ctx->stream, a, th_low);
+    timer_end(ctx, "match");
+    if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+    return ORBX_OK;
+}
+
 int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window, float nnratio,
                       int check_ori)
 {

@@ -48,3 +48,27 @@ def test_match_prev_matches_oracle(n, seq_len):
         total += gn
     assert total > 0
     ctx.close()
+
+
+def test_match_bf_prev_matches_oracle():
+    """Device-resident brute-force pairs (C3) against the oracle's all-pairs
+    best/second + the acceptance rule."""
+    w, h, n, seq_len = 640, 480, 1000, 4
+    frames = synth.sequence(w, h, seq_len, seed=5)
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_bf_prev(0, seq_len, seq_len, th_low=50, nnratio=0.9)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        dA, dB = feats[p][1], feats[s][1]
+        bi, b1, b2 = (np.zeros(len(dA), np.int32) for _ in range(3))
+        L.orbx_ref_hamming_bf(ptr(dA), len(dA), ptr(dB), len(dB), ptr(bi), ptr(b1), ptr(b2))
+        want = np.where((b1 <= 50) & (b1.astype(np.float32) < b2.astype(np.float32) * np.float32(0.9)), bi, -1)
+        gm, gn = ctx.matches(s)
+        assert np.array_equal(gm[:len(dA)], want)
+        assert gn == int((want >= 0).sum()) and gn > 0
+    ctx.close()
