@@ -221,7 +221,7 @@ def timed(args, ctx, step, dist, names):
             dist.barrier()
             torch.cuda.synchronize()
 
-    ctx.timing(True)
+    ctx.timing(not args.no_kernel_timing)
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()
 
     world, rank, local = odist.env()
@@ -268,7 +270,8 @@ def main():
     if rank == 0:
         # dominant kernel: largest total time; its algorithmic bytes per launch
         # over its mean launch duration (HIP events on the context stream)
-        dom = max((k for k in kernels if kernels[k]["launches"]), key=lambda k: kernels[k]["total_ms"])
+        timed_k = [k for k in kernels if kernels[k]["launches"]] or list(kernels)
+        dom = max(timed_k, key=lambda k: kernels[k]["total_ms"])
         launches_per_step = max(1, kernels[dom]["launches"] // args.steps)
         per_launch = ab.get(dom, 0) * units.get(dom, 1) / launches_per_step
         avg_s = kernels[dom]["avg_ms"] / 1e3

@@ -6,8 +6,9 @@
 //   k_fast_cells   FAST-9/16 + cell-local NMS + threshold-7
 //                  fallback + raster-order compaction, one
 //                  workgroup per grid cell                    (:599-614)
-//   k_retain       per-level quota redistribution and the two
-//                  retainBest passes (libstdc++ introselect)  (:622-701)
+//   k_retain_cells per-level quota redistribution + cell retainBest,
+//                  one wave per cell (libstdc++ introselect)  (:622-694)
+//   k_retain_levels level retainBest, one wave per level      (:697-701)
 //   k_blur         GaussianBlur 7x7 sigma 2 on each level     (:760)
 //   k_describe     IC_Angle + rBRIEF + coordinate scaling,
 //                  one wave per keypoint                      (:124-194, :705,
@@ -68,17 +69,34 @@ __device__ inline int reflect101(int p, int len)
 __device__ inline uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
 __device__ inline int sat_s16(int v) { return min(max(v, -32768), 32767); }
 
+// (row, column) walk of a row-major index advancing by a fixed stride,
+// without a division per step.
+struct RowWalk {
+    int r, q, dr, dq, nq;
+    __device__ RowWalk(int start, int stride, int n_q) : nq(n_q)
+    {
+        r = start / n_q;
+        q = start - r * n_q;
+        dr = stride / n_q;
+        dq = stride - dr * n_q;
+    }
+    __device__ void next()
+    {
+        r += dr;
+        q += dq;
+        if (q >= nq) {
+            q -= nq;
+            r++;
+        }
+    }
+};
+
+
 // ---------------------------------------------------------------------------
 // Level 0: padded copy with BORDER_REFLECT_101.  4 output bytes per thread.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
+__device__ inline void pyr_level0_word(const ExtractArgs& a, const LevelGeom& L, int f, int py, int px0)
 {
-    const int f = blockIdx.y;
-    const LevelGeom L = a.levels[0];
-    const int words_per_row = L.stride >> 2;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= words_per_row * L.ph) return;
-    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
     const uint8_t* src = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
     uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
     const int sy = reflect101(py - kEdge, L.h);
@@ -91,6 +109,17 @@ __global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
         word |= v << (8 * b);
     }
     *reinterpret_cast<uint32_t*>(dst + px0) = word;
+}
+
+__global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
+{
+    const int f = blockIdx.y;
+    const LevelGeom L = a.levels[0];
+    const int words_per_row = L.stride >> 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= words_per_row * L.ph) return;
+    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
+    pyr_level0_word(a, L, f, py, px0);
 }
 
 // ---------------------------------------------------------------------------
@@ -115,15 +144,9 @@ __device__ inline uint8_t resize_pixel(const uint8_t* prev, int pstride, const R
     return sat_u8((S0 * r.b0 + S1 * r.b1 + (1 << 21)) >> 22);
 }
 
-__global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
+__device__ inline void pyr_resize_word(const ExtractArgs& a, const LevelGeom& L, const LevelGeom& P, int f, int py,
+                                       int px0)
 {
-    const int f = blockIdx.y;
-    const LevelGeom L = a.levels[level];
-    const LevelGeom P = a.levels[level - 1];
-    const int words_per_row = L.stride >> 2;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= words_per_row * L.ph) return;
-    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
     const uint8_t* frame = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
     const uint8_t* prev = frame + P.off + (size_t)kEdge * P.stride + kEdge;
     uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
@@ -141,6 +164,18 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
         word |= v << (8 * b);
     }
     *reinterpret_cast<uint32_t*>(dst + px0) = word;
+}
+
+__global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
+{
+    const int f = blockIdx.y;
+    const LevelGeom L = a.levels[level];
+    const LevelGeom P = a.levels[level - 1];
+    const int words_per_row = L.stride >> 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= words_per_row * L.ph) return;
+    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
+    pyr_resize_word(a, L, P, f, py, px0);
 }
 
 // ---------------------------------------------------------------------------
@@ -188,28 +223,6 @@ __device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
 {
     return k < 4 ? byte_of(lo, k) : (k < 8 ? byte_of(mid, k - 4) : byte_of(hi, k - 8));
 }
-
-// (row, column) walk of a row-major index advancing by a fixed stride,
-// without a division per step.
-struct RowWalk {
-    int r, q, dr, dq, nq;
-    __device__ RowWalk(int start, int stride, int n_q) : nq(n_q)
-    {
-        r = start / n_q;
-        q = start - r * n_q;
-        dr = stride / n_q;
-        dq = stride - dr * n_q;
-    }
-    __device__ void next()
-    {
-        r += dr;
-        q += dq;
-        if (q >= nq) {
-            q -= nq;
-            r++;
-        }
-    }
-};
 
 __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
 {

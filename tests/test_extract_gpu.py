@@ -95,3 +95,23 @@ def test_operator_call_and_batch_consistency():
     k0, d0 = ctx(np.zeros((0, 0), np.uint8))
     assert len(k0) == 0 and len(d0) == 0
     ctx.close()
+
+
+def test_large_batch_paths_match_oracle():
+    """A 64-frame batch (the bench's launch shape, many workgroups per
+    launch): spot-check frames of the batch bit-exactly."""
+    w, h, B = 640, 480, 64
+    frames = synth.sequence(w, h, B, seed=99)
+    ctx = ox.Context(nfeatures=1000, max_w=w, max_h=h, slots=B)
+    ctx.upload(frames)
+    ctx.extract(0, B)
+    ctx.sync()
+    ref = RefExtractor(1000)
+    for s in (0, 17, 63):
+        rk, rd = ref(frames[s])
+        gk, gd = ctx.features(s)
+        assert_kps_equal(gk, rk)
+        assert np.array_equal(gd, rd)
+        for lvl in (1, 4, 7):
+            assert np.array_equal(ctx.level(s, lvl), ref.level(lvl)), (s, lvl)
+    ctx.close()
