@@ -2,7 +2,7 @@
 // Optimizer::LocalBundleAdjustment (src/Optimizer.cc:287-536) on the g2o
 // subset it uses (BlockSolverX + Schur over the points, Levenberg).
 //
-// Device work per LM iteration (one 256-thread workgroup per problem, one
+// Device work per LM iteration (one 512-thread workgroup per problem, one
 // launch per iteration so the caller's abort flag is polled between
 // iterations exactly where SparseOptimizer::optimize polls terminate()):
 //   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2
@@ -73,6 +73,9 @@ struct LbaDev {
 
 enum { kRunning = 0, kTerminated = 1 };
 
+constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem
+constexpr int kLbaWaves = kLbaThreads / 64;
+
 // ---------------------------------------------------------------------------
 // SE3 / quaternion primitives (g2o se3quat.h with Eigen's formulas)
 // ---------------------------------------------------------------------------
@@ -119,20 +122,33 @@ __device__ inline Q qfrom(const double m[9])
         q.y = (m[2] - m[6]) * t;
         q.z = (m[3] - m[1]) * t;
     } else {
+        // Eigen's branch on the largest diagonal entry, spelled out per case
+        // (no dynamically indexed private arrays)
         int i = 0;
         if (m[4] > m[0]) i = 1;
         if (m[8] > m[i * 4]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (m[k * 3 + j] - m[j * 3 + k]) * t;
-        c[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
-        c[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
-        q.x = c[0];
-        q.y = c[1];
-        q.z = c[2];
+        if (i == 0) {
+            t = sqrt(m[0] - m[4] - m[8] + 1.0);
+            q.x = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[7] - m[5]) * t;
+            q.y = (m[3] + m[1]) * t;
+            q.z = (m[6] + m[2]) * t;
+        } else if (i == 1) {
+            t = sqrt(m[4] - m[8] - m[0] + 1.0);
+            q.y = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[2] - m[6]) * t;
+            q.z = (m[7] + m[5]) * t;
+            q.x = (m[1] + m[3]) * t;
+        } else {
+            t = sqrt(m[8] - m[0] - m[4] + 1.0);
+            q.z = 0.5 * t;
+            t = 0.5 / t;
+            q.w = (m[3] - m[1]) * t;
+            q.x = (m[2] + m[6]) * t;
+            q.y = (m[5] + m[7]) * t;
+        }
     }
     return q;
 }
@@ -193,7 +209,7 @@ __device__ inline void se3_map(const double* pose, const double* p, double* o)
 // Block reductions in double
 // ---------------------------------------------------------------------------
 struct DScratch {
-    double w[kWaves];
+    double w[kLbaWaves];
     double v[4];
     int iv[4];
 };
@@ -219,7 +235,7 @@ __device__ inline double block_sum_d(double v, DScratch& s)
     if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = 0;
-    for (int i = 0; i < kWaves; i++) t += s.w[i];
+    for (int i = 0; i < kLbaWaves; i++) t += s.w[i];
     return t;
 }
 
@@ -230,7 +246,7 @@ __device__ inline double block_max_d(double v, DScratch& s)
     if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = s.w[0];
-    for (int i = 1; i < kWaves; i++) t = fmax(t, s.w[i]);
+    for (int i = 1; i < kLbaWaves; i++) t = fmax(t, s.w[i]);
     return t;
 }
 
@@ -262,7 +278,7 @@ __device__ inline double edge_chi2(const LbaDev& P, int a)
 __device__ double compute_errors(LbaDev& P, DScratch& sc)
 {
     double part = 0;
-    for (int a = threadIdx.x; a < P.nE; a += kBlock) {
+    for (int a = threadIdx.x; a < P.nE; a += kLbaThreads) {
         const int e = P.e_orig[a];
         double pc[3];
         se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
@@ -282,7 +298,7 @@ __device__ double compute_errors(LbaDev& P, DScratch& sc)
 // linearizeOplus + constructQuadraticForm contributions per edge
 __device__ void linearize(LbaDev& P)
 {
-    for (int a = threadIdx.x; a < P.nE; a += kBlock) {
+    for (int a = threadIdx.x; a < P.nE; a += kLbaThreads) {
         const double* T = P.pose + 7 * P.e_pose[a];
         double pc[3];
         se3_map(T, P.point + 3 * P.e_point[a], pc);
@@ -328,19 +344,38 @@ __device__ void linearize(LbaDev& P)
             for (int j = 0; j < 3; j++) ce[36 + i * 3 + j] = (B[i] * w) * A[j] + (B[6 + i] * w) * A[3 + j];
     }
     __syncthreads();
-    // per free pose: Hpp (21) + bp (6), summed in edge order; one lane per value
-    for (int item = threadIdx.x; item < P.nP * 27; item += kBlock) {
-        const int p = item / 27, v = item - p * 27;
-        double acc = 0;
-        for (int q = P.pe_ptr[p]; q < P.pe_ptr[p + 1]; q++) acc += P.ce[54 * (size_t)P.pe_idx[q] + v];
-        P.hp[27 * p + v] = acc;
+    // per free pose: Hpp (21) + bp (6); one wave per pose, lanes stride the
+    // pose's edges, fixed-shape butterfly reduction (deterministic)
+    {
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int p = wv; p < P.nP; p += kLbaWaves) {
+            double acc[27];
+#pragma unroll
+            for (int v = 0; v < 27; v++) acc[v] = 0.0;
+            for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
+                const double* c = P.ce + 54 * (size_t)P.pe_idx[q];
+#pragma unroll
+                for (int v = 0; v < 27; v++) acc[v] += c[v];
+            }
+#pragma unroll
+            for (int v = 0; v < 27; v++) {
+                const double t = wave_sum_d(acc[v]);
+                if (lane == 0) P.hp[27 * p + v] = t;
+            }
+        }
     }
-    // per point: Hll (6) + bl (3) in edge order
-    for (int item = threadIdx.x; item < P.nL * 9; item += kBlock) {
-        const int l = item / 9, v = item - l * 9;
-        double acc = 0;
-        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) acc += P.ce[54 * (size_t)P.le_idx[q] + 27 + v];
-        P.hl[9 * l + v] = acc;
+    // per point: Hll (6) + bl (3) in edge order, one thread per point
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+        double acc[9];
+#pragma unroll
+        for (int v = 0; v < 9; v++) acc[v] = 0.0;
+        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) {
+            const double* c = P.ce + 54 * (size_t)P.le_idx[q] + 27;
+#pragma unroll
+            for (int v = 0; v < 9; v++) acc[v] += c[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
     }
     __syncthreads();
 }
@@ -354,7 +389,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
 {
     const int n = P.dim_p;
     // per point: D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse), db
-    for (int l = threadIdx.x; l < P.nL; l += kBlock) {
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
         double m[9];
         for (int i = 0; i < 3; i++)
@@ -380,30 +415,62 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
             }
         }
     }
-    for (int i = threadIdx.x; i < n * n; i += kBlock) S[i] = 0.0;   // blocks without shared points
+    for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;   // blocks without shared points
     __syncthreads();
-    // reduced camera system, upper 6x6 blocks: Hpp (+lambda) - sum_l B_i Dinv B_j^T
-    for (int item = threadIdx.x; item < P.nblk * 36; item += kBlock) {
-        const int bk = item / 36, rc = item - bk * 36, r = rc / 6, c = rc - (rc / 6) * 6;
-        const int i1 = P.blk_ij[2 * bk], i2 = P.blk_ij[2 * bk + 1];
-        if (i1 == i2 && r > c) continue;   // CHOLMOD reads the upper triangle only
-        double acc = 0;
-        if (i1 == i2) acc = P.hp[27 * i1 + (r <= c ? up6(r, c) : up6(c, r))] + (r == c ? lambda : 0.0);
-        for (int q = P.blk_ptr[bk]; q < P.blk_ptr[bk + 1]; q++) {
-            const int e1 = P.blk_c[2 * q], e2 = P.blk_c[2 * q + 1];
-            const double* BD = P.eb + 24 * (size_t)e1 + r * 3;
-            const double* Bj = P.ce + 54 * (size_t)e2 + 36 + c * 3;
-            acc -= BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+    // reduced camera system, upper 6x6 blocks: Hpp (+lambda) - sum_l B_i Dinv B_j^T;
+    // one wave per block, lanes stride the shared landmarks, butterfly reduction
+    {
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int bk = wv; bk < P.nblk; bk += kLbaWaves) {
+            const int i1 = P.blk_ij[2 * bk], i2 = P.blk_ij[2 * bk + 1];
+            double acc[36];
+#pragma unroll
+            for (int k = 0; k < 36; k++) acc[k] = 0.0;
+            for (int q = P.blk_ptr[bk] + lane; q < P.blk_ptr[bk + 1]; q += 64) {
+                const int e1 = P.blk_c[2 * q], e2 = P.blk_c[2 * q + 1];
+                const double* BD = P.eb + 24 * (size_t)e1;
+                const double* Bj = P.ce + 54 * (size_t)e2 + 36;
+                double bj[18];
+#pragma unroll
+                for (int k = 0; k < 18; k++) bj[k] = Bj[k];
+#pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    const double d0 = BD[r * 3], d1 = BD[r * 3 + 1], d2 = BD[r * 3 + 2];
+#pragma unroll
+                    for (int c = 0; c < 6; c++) acc[r * 6 + c] += d0 * bj[c * 3] + d1 * bj[c * 3 + 1] + d2 * bj[c * 3 + 2];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 36; k++) {
+                const double t = wave_sum_d(acc[k]);
+                const int r = k / 6, c = k % 6;
+                if (lane == k && !(i1 == i2 && r > c)) {   // CHOLMOD reads the upper triangle only
+                    double v = -t;
+                    if (i1 == i2) v += P.hp[27 * i1 + up6(r, c)] + (r == c ? lambda : 0.0);
+                    S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = v;
+                    S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = v;
+                }
+            }
         }
-        S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc;
-        S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = acc;
     }
-    // bschur = bp - coef (coef summed in landmark order)
-    for (int item = threadIdx.x; item < n; item += kBlock) {
-        const int p = item / 6, r = item - p * 6;
-        double coef = 0;
-        for (int q = P.pc_ptr[p]; q < P.pc_ptr[p + 1]; q++) coef += P.eb[24 * (size_t)P.pc_idx[q] + 18 + r];
-        P.bs[item] = P.hp[27 * p + 21 + r] - coef;
+    // bschur = bp - coef; one wave per pose, lanes stride its Schur edges
+    {
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int p = wv; p < P.nP; p += kLbaWaves) {
+            double acc[6];
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[r] = 0.0;
+            for (int q = P.pc_ptr[p] + lane; q < P.pc_ptr[p + 1]; q += 64) {
+                const double* o = P.eb + 24 * (size_t)P.pc_idx[q] + 18;
+#pragma unroll
+                for (int r = 0; r < 6; r++) acc[r] += o[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double t = wave_sum_d(acc[r]);
+                if (lane == r) P.bs[6 * p + r] = P.hp[27 * p + 21 + r] - t;
+            }
+        }
     }
     __syncthreads();
     // dense LLT (right-looking), lower triangle
@@ -416,33 +483,43 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
         __syncthreads();
         if (!sc.iv[0]) return false;
         const double lkk = S[(size_t)k * n + k];
-        for (int i = k + 1 + threadIdx.x; i < n; i += kBlock) S[(size_t)i * n + k] /= lkk;
+        for (int i = k + 1 + threadIdx.x; i < n; i += kLbaThreads) S[(size_t)i * n + k] /= lkk;
         __syncthreads();
         const int m = n - k - 1;
-        for (int item = threadIdx.x; item < m * m; item += kBlock) {
+        for (int item = threadIdx.x; item < m * m; item += kLbaThreads) {
             const int i = k + 1 + item / m, j = k + 1 + (item - (item / m) * m);
             if (j <= i) S[(size_t)i * n + j] -= S[(size_t)i * n + k] * S[(size_t)j * n + k];
         }
         __syncthreads();
     }
-    // forward / backward substitution
+    // forward / backward substitution by one wave (no block barriers per step)
     double* xp = P.x;
-    for (int i = threadIdx.x; i < n; i += kBlock) xp[i] = P.bs[i];
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        for (int i = lane; i < n; i += 64) xp[i] = P.bs[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int k = 0; k < n; k++) {
+            const double xk = xp[k] / S[(size_t)k * n + k];
+            for (int i = k + 1 + lane; i < n; i += 64) xp[i] -= S[(size_t)i * n + k] * xk;
+            if (lane == 0) xp[k] = xk;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        for (int k = n - 1; k >= 0; k--) {
+            const double xk = xp[k] / S[(size_t)k * n + k];
+            for (int i = lane; i < k; i += 64) xp[i] -= S[(size_t)k * n + i] * xk;
+            if (lane == 0) xp[k] = xk;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    }
     __syncthreads();
-    for (int k = 0; k < n; k++) {
-        if (threadIdx.x == 0) xp[k] /= S[(size_t)k * n + k];
-        __syncthreads();
-        for (int i = k + 1 + threadIdx.x; i < n; i += kBlock) xp[i] -= S[(size_t)i * n + k] * xp[k];
-        __syncthreads();
-    }
-    for (int k = n - 1; k >= 0; k--) {
-        if (threadIdx.x == 0) xp[k] /= S[(size_t)k * n + k];
-        __syncthreads();
-        for (int i = threadIdx.x; i < k; i += kBlock) xp[i] -= S[(size_t)k * n + i] * xp[k];
-        __syncthreads();
-    }
     // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i)
-    for (int l = threadIdx.x; l < P.nL; l += kBlock) {
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
         double cl[3] = {h[6], h[7], h[8]};
         for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
@@ -463,7 +540,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
 }
 
 // OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
-__global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
+__global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
 {
     extern __shared__ __attribute__((aligned(16))) double s_S[];
     __shared__ DScratch sc;
@@ -482,9 +559,9 @@ __global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iterat
     double lambda = P.lambda, ni = P.ni;
     if (iteration == 0) {
         double m = 0;
-        for (int item = threadIdx.x; item < P.nP * 6; item += kBlock)
+        for (int item = threadIdx.x; item < P.nP * 6; item += kLbaThreads)
             m = fmax(m, fabs(P.hp[27 * (item / 6) + up6(item % 6, item % 6)]));
-        for (int item = threadIdx.x; item < P.nL * 3; item += kBlock)
+        for (int item = threadIdx.x; item < P.nL * 3; item += kLbaThreads)
             m = fmax(m, fabs(P.hl[9 * (item / 3) + up3(item % 3, item % 3)]));
         m = block_max_d(m, sc);
         lambda = 1e-5 * m;
@@ -496,18 +573,18 @@ __global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iterat
     int qmax = 0;
     do {
         // push
-        for (int i = threadIdx.x; i < P.nposes_all * 7; i += kBlock) P.pose_bk[i] = P.pose[i];
-        for (int i = threadIdx.x; i < P.npoints_all * 3; i += kBlock) P.point_bk[i] = P.point[i];
+        for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose_bk[i] = P.pose[i];
+        for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point_bk[i] = P.point[i];
         __syncthreads();
         const bool ok2 = trial_solve(P, lambda, S, sc);
         if (ok2) {
-            for (int p = threadIdx.x; p < P.nP; p += kBlock) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
-            for (int item = threadIdx.x; item < P.nL * 3; item += kBlock) {
+            for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
+            for (int item = threadIdx.x; item < P.nL * 3; item += kLbaThreads) {
                 const int l = item / 3, i = item - l * 3;
                 P.point[3 * P.iv_point[l] + i] += P.x[n + item];
             }
         } else {
-            for (int i = threadIdx.x; i < nx; i += kBlock) P.x[i] = 0.0;
+            for (int i = threadIdx.x; i < nx; i += kLbaThreads) P.x[i] = 0.0;
             if (threadIdx.x == 0) P.not_posdef++;
         }
         __syncthreads();
@@ -515,7 +592,7 @@ __global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iterat
         if (!ok2) tempChi = 1.79769313486231570815e+308;
         // computeScale: sum_j x_j (lambda x_j + b_j)
         double part = 0;
-        for (int j = threadIdx.x; j < nx; j += kBlock) {
+        for (int j = threadIdx.x; j < nx; j += kLbaThreads) {
             const double bj = j < n ? P.hp[27 * (j / 6) + 21 + (j % 6)] : P.hl[9 * ((j - n) / 3) + 6 + ((j - n) % 3)];
             part += P.x[j] * (lambda * P.x[j] + bj);
         }
@@ -532,8 +609,8 @@ __global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iterat
         } else {
             lambda *= ni;
             ni *= 2;
-            for (int i = threadIdx.x; i < P.nposes_all * 7; i += kBlock) P.pose[i] = P.pose_bk[i];
-            for (int i = threadIdx.x; i < P.npoints_all * 3; i += kBlock) P.point[i] = P.point_bk[i];
+            for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose[i] = P.pose_bk[i];
+            for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point[i] = P.point_bk[i];
         }
         __syncthreads();
         qmax++;
@@ -557,37 +634,44 @@ __global__ __launch_bounds__(256) void k_lba_iteration(LbaDev* probs, int iterat
 }
 
 // Outlier passes of LocalBundleAdjustment (src/Optimizer.cc:452-470,
-// :497-515): sequential in edge order (MapPoint bad state depends on it).
-__global__ void k_lba_outliers(LbaDev* probs, const int* edge_point_all, const int* edge_pose_all,
-                               int* nobs_all, uint8_t* status_all, uint8_t* bad_all, int pass, double thr,
-                               const double* isig_all, int* n_out, const long long* offs)
+// :497-515).  The reference walks the edges in order; an edge's outcome
+// depends only on earlier edges of the same map point (EraseObservation ->
+// SetBadFlag), so each point's active edges are walked in edge order by one
+// thread, points in parallel.
+__global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_all, uint8_t* status_all,
+                                                      uint8_t* bad_all, int pass, double thr, int* n_out,
+                                                      const long long* offs)
 {
+    __shared__ int s_cnt;
     LbaDev& P = probs[blockIdx.x];
-    if (threadIdx.x != 0) return;
     const long long eo = offs[3 * blockIdx.x], po = offs[3 * blockIdx.x + 1];
-    const int* ep = edge_point_all + eo;
-    const int* eps = edge_pose_all + eo;
-    const double* isig = isig_all + eo;
     int* nobs = nobs_all + po;
     uint8_t* st = status_all + eo;
     uint8_t* bad = bad_all + po;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
     int cnt = 0;
-    for (int e = 0; e < P.nedges_all; e++) {
-        if (st[e] != 0) continue;          // removed in pass 1
-        const int p = ep[e];
-        if (bad[p]) continue;
-        const double s = isig[e];
-        const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
-        const double chi2 = e0 * (s * e0) + e1 * (s * e1);
-        double pc[3];
-        se3_map(P.pose + 7 * eps[e], P.point + 3 * p, pc);
-        if (chi2 > thr || !(pc[2] > 0.0)) {
-            if (--nobs[p] <= 2) bad[p] = 1;
-            st[e] = (uint8_t)pass;
-            cnt++;
+    for (int l = threadIdx.x; l < P.nL; l += blockDim.x) {
+        const int p = P.iv_point[l];
+        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) {
+            if (bad[p]) break;
+            const int a = P.le_idx[q];
+            const int e = P.e_orig[a];
+            const double s = P.e_isig[a];
+            const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+            const double chi2 = e0 * (s * e0) + e1 * (s * e1);
+            double pc[3];
+            se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * p, pc);
+            if (chi2 > thr || !(pc[2] > 0.0)) {
+                if (--nobs[p] <= 2) bad[p] = 1;
+                st[e] = (uint8_t)pass;
+                cnt++;
+            }
         }
     }
-    n_out[blockIdx.x] = cnt;
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) n_out[blockIdx.x] = s_cnt;
 }
 
 // ---------------------------------------------------------------------------
@@ -745,9 +829,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     std::vector<long long> offs(3 * P);
     Packer base;
     std::vector<size_t> o_pose(P), o_point(P), o_posebk(P), o_pointbk(P), o_cam(P), o_err(P);
-    std::vector<size_t> o_ep(P), o_eps(P), o_isig(P), o_nobs(P), o_st(P), o_bad(P);
-    std::vector<int> all_ep, all_eps, all_nobs;
-    std::vector<double> all_isig;
+    std::vector<int> all_nobs;
     std::vector<uint8_t> all_st, all_bad;
     long long eacc = 0, pacc = 0;
     for (int i = 0; i < P; i++) {
@@ -765,16 +847,12 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         o_err[i] = base.add(std::vector<double>(2 * (size_t)p.n_edges, 0.0));
         offs[3 * i] = eacc;
         offs[3 * i + 1] = pacc;
-        all_ep.insert(all_ep.end(), p.edge_point, p.edge_point + p.n_edges);
-        all_eps.insert(all_eps.end(), p.edge_pose, p.edge_pose + p.n_edges);
-        all_isig.insert(all_isig.end(), p.edge_inv_sigma2, p.edge_inv_sigma2 + p.n_edges);
         all_nobs.insert(all_nobs.end(), p.point_nobs, p.point_nobs + p.n_points);
         all_st.insert(all_st.end(), p.n_edges, 0);
         all_bad.insert(all_bad.end(), p.n_points, 0);
         eacc += p.n_edges;
         pacc += p.n_points;
     }
-    const size_t o_all_ep = base.add(all_ep), o_all_eps = base.add(all_eps), o_all_isig = base.add(all_isig);
     const size_t o_all_nobs = base.add(all_nobs), o_all_st = base.add(all_st), o_all_bad = base.add(all_bad);
     const size_t o_offs = base.add(offs);
     const size_t o_nout = base.reserve(4 * (size_t)P);
@@ -800,25 +878,35 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             o[12][i] = pk.add(s.le_idx); o[13][i] = pk.add(s.lc_ptr); o[14][i] = pk.add(s.lc_idx);
             o[15][i] = pk.add(s.pc_ptr); o[16][i] = pk.add(s.pc_idx); o[17][i] = pk.add(s.blk_ij);
             o[18][i] = pk.add(s.blk_ptr); o[19][i] = pk.add(s.blk_c);
-            const size_t nE = s.e_orig.size();
-            o[20][i] = pk.reserve(54 * nE * 8);
-            o[21][i] = pk.reserve(24 * nE * 8);
-            o[22][i] = pk.reserve(27 * (size_t)s.nP * 8);
-            o[23][i] = pk.reserve(9 * (size_t)s.nL * 8);
-            o[24][i] = pk.reserve(12 * (size_t)s.nL * 8);
-            const size_t n = 6 * (size_t)s.nP;
-            o[25][i] = pk.reserve(n * n > (size_t)kLdsSCap ? n * n * 8 : 8);
-            o[26][i] = pk.reserve((n + 3 * (size_t)s.nL) * 8);
-            o[27][i] = pk.reserve(n * 8 + 8);
         }
         const size_t o_devs = pk.reserve(sizeof(LbaDev) * P);
+        // device-only scratch after the staged block (never copied)
+        size_t dev_end = pk.host.size();
+        auto dev_reserve = [&](size_t bytes) {
+            const size_t off = dev_end;
+            dev_end += (bytes + 255) & ~size_t(255);
+            return off;
+        };
+        for (int i = 0; i < P; i++) {
+            const HostStruct& s = hs[i];
+            const size_t nE = s.e_orig.size();
+            o[20][i] = dev_reserve(54 * nE * 8);
+            o[21][i] = dev_reserve(24 * nE * 8);
+            o[22][i] = dev_reserve(27 * (size_t)s.nP * 8);
+            o[23][i] = dev_reserve(9 * (size_t)s.nL * 8);
+            o[24][i] = dev_reserve(12 * (size_t)s.nL * 8);
+            const size_t n = 6 * (size_t)s.nP;
+            o[25][i] = dev_reserve(n * n > (size_t)kLdsSCap ? n * n * 8 : 8);
+            o[26][i] = dev_reserve((n + 3 * (size_t)s.nL) * 8);
+            o[27][i] = dev_reserve(n * 8 + 8);
+        }
         bool full_upload = pass == 0;
-        if (pk.host.size() > ctx->scratch_bytes) {
+        if (dev_end > ctx->scratch_bytes) {
             if (pass == 1) {   // keep the device-resident state across the reallocation
                 ORBX_HIP_CHECK(hipMemcpy(pk.host.data(), ctx->scratch, base_bytes, hipMemcpyDeviceToHost));
                 full_upload = true;
             }
-            if ((r = ensure_scratch(ctx, pk.host.size())) != ORBX_OK) break;
+            if ((r = ensure_scratch(ctx, dev_end)) != ORBX_OK) break;
         }
         uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
         for (int i = 0; i < P; i++) {
@@ -894,21 +982,26 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
                 break;
             }
             timer_begin(ctx, "lba_iter");
-            hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kBlock), lds, ctx->stream, dd, it, lds_cap);
+            hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, lds_cap);
             timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
-            ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-            ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-            bool running = false;
-            for (int i = 0; i < P; i++) running |= devs[i].status == kRunning;
-            if (!running) break;
+            // With an abort flag the host polls it between iterations (where
+            // g2o polls its force-stop flag), which needs the device state;
+            // without one, iterations are queued back to back and a
+            // terminated problem's later launches return immediately.
+            if (abort) {
+                ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+                ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+                bool running = false;
+                for (int i = 0; i < P; i++) running |= devs[i].status == kRunning;
+                if (!running) break;
+            }
         }
         timer_begin(ctx, "lba_outliers");
-        hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(64), 0, ctx->stream, dd,
-                           reinterpret_cast<const int*>(d + o_all_ep), reinterpret_cast<const int*>(d + o_all_eps),
+        hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(256), 0, ctx->stream, dd,
                            reinterpret_cast<int*>(d + o_all_nobs), d + o_all_st, d + o_all_bad, pass + 1,
-                           probs[0].chi2_threshold, reinterpret_cast<const double*>(d + o_all_isig),
-                           reinterpret_cast<int*>(d + o_nout), reinterpret_cast<const long long*>(d + o_offs));
+                           probs[0].chi2_threshold, reinterpret_cast<int*>(d + o_nout),
+                           reinterpret_cast<const long long*>(d + o_offs));
         timer_end(ctx, "lba_outliers");
         ORBX_HIP_CHECK(hipGetLastError());
         std::vector<int> nout(P);
