@@ -64,7 +64,7 @@ def build(verbose=False, jobs=None):
             if err and verbose:
                 print(err, file=sys.stderr)
     if cmds or not LIB.exists():
-        link = [cc, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)]
+        link = [cc, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(LIB), *map(str, objs)]
         run(link)
     # C++ adapter demo (the reference-style C++ binding)
     demo_src = PKG / "adapters" / "adapter_demo.cpp"

@@ -7,13 +7,16 @@
 // iterations exactly where SparseOptimizer::optimize polls terminate()):
 //   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2
 //   linearize EdgeSE3ProjectXYZ::linearizeOplus + constructQuadraticForm per
-//             edge into SoA contribution rows; segmented reductions per pose
-//             (Hpp, bp) and per point (Hll, bl) in g2o's edge order
-//   trial     Schur: per point Dinv, db, B*Dinv, B*db; per upper 6x6 block of
-//             the reduced camera system, the landmark-ordered sum of
-//             B_i Dinv B_j^T; dense LLT of the reduced system (LDS when it
-//             fits); back-substitution for the points; exp-map update;
-//             accept / reject with g2o's rho rule
+//             edge into component-major (SoA) rows; per pose (Hpp, bp) one
+//             wave with a fixed butterfly reduction, per point (Hll, bl) one
+//             thread in edge order
+//   trial     Schur point by point (a point's edges are contiguous): Dinv,
+//             db, then bs -= W_i db and S(i,j) -= W_i Dinv W_j^T for every
+//             pair of its edges, FP64 atomics into the reduced camera system
+//             held in LDS (summation order differs from g2o's only by
+//             rounding); dense LLT; one-wave triangular solves;
+//             back-substitution for the points; exp-map update; accept /
+//             reject with g2o's rho rule
 //   Raul stop rule (levenberg.cpp:154-161)
 // Index structures (g2o's initializeOptimization / buildStructure) are built
 // on the host once per optimize() call.
@@ -21,6 +24,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "orbx_device.h"
@@ -29,7 +33,7 @@
 namespace orbx {
 
 struct LbaDev {
-    int nP, nL, nE, nblk;          // free poses, active points, active edges, Schur blocks
+    int nP, nL, nE;                // free poses, active points, active edges
     int nposes_all, npoints_all, nedges_all;
     int dim_p;                     // 6 * nP
     double* pose;                  // [nposes_all][7]: qx qy qz qw tx ty tz
@@ -51,13 +55,8 @@ struct LbaDev {
     const int* pe_ptr; const int* pe_idx;   // per free pose: active edges, edge order
     const int* le_ptr; const int* le_idx;   // per point: active edges, edge order
     const int* lc_ptr; const int* lc_idx;   // per point: Schur column (free poses, pose order)
-    const int* pc_ptr; const int* pc_idx;   // per free pose: Schur-column edges, landmark order
-    const int* blk_ij;             // [nblk][2]
-    const int* blk_ptr;            // [nblk+1]
-    const int* blk_c;              // [..][2] active-edge pairs, landmark order
     // scratch
-    double* ce;                    // [nE][54]: Hpp 21 | bp 6 | Hll 6 | bl 3 | Hpl 18
-    double* eb;                    // [nE][24]: B*Dinv 18 | B*db 6
+    double* ce;                    // [18][nE] (SoA): Hpl = B^T W A per edge
     double* hp;                    // [nP][27]: Hpp upper 21 | bp 6
     double* hl;                    // [nL][9]: Hll upper 6 | bl 3
     double* dl;                    // [nL][12]: Dinv 9 | db 3
@@ -73,8 +72,31 @@ struct LbaDev {
 
 enum { kRunning = 0, kTerminated = 1 };
 
+// Phase timing of block 0 (diagnostic build only: -DORBX_LBA_PROFILE).
+#ifdef ORBX_LBA_PROFILE
+__device__ unsigned long long g_lba_prof[16];
+__device__ inline unsigned long long lba_stamp()
+{
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define LBA_T0() unsigned long long _t = lba_stamp()
+#define LBA_MARK(k)                                                         \
+    do {                                                                    \
+        __syncthreads();                                                    \
+        const unsigned long long _n = lba_stamp();                          \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_lba_prof[k] += _n - _t;  \
+        _t = _n;                                                            \
+    } while (0)
+#else
+#define LBA_T0()
+#define LBA_MARK(k)
+#endif
+
 constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem
 constexpr int kLbaWaves = kLbaThreads / 64;
+
 
 // ---------------------------------------------------------------------------
 // SE3 / quaternion primitives (g2o se3quat.h with Eigen's formulas)
@@ -295,84 +317,104 @@ __device__ double compute_errors(LbaDev& P, DScratch& sc)
     return block_sum_d(part, sc);
 }
 
-// linearizeOplus + constructQuadraticForm contributions per edge
+// EdgeSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:384-420) for
+// active edge a: A = d e / d point (2x3), B = d e / d pose (2x6); plus the
+// robust weight w = rho' * invSigma2 and the weighted error -Omega e rho'.
+struct EdgeLin {
+    double A[6], B[12], w, om0, om1;
+};
+
+__device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
+{
+    const double* T = P.pose + 7 * P.e_pose[a];
+    double pc[3];
+    se3_map(T, P.point + 3 * P.e_point[a], pc);
+    const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+    const double* c = P.cam + 4 * P.e_pose[a];
+    const double fx = c[0], fy = c[1];
+    const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+    double R[9];
+    qmat(Q{T[0], T[1], T[2], T[3]}, R);
+    const double s = -1. / z;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            L.A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
+    L.B[0] = x * y / z_2 * fx;
+    L.B[1] = -(1 + (x * x / z_2)) * fx;
+    L.B[2] = y / z * fx;
+    L.B[3] = -1. / z * fx;
+    L.B[4] = 0;
+    L.B[5] = x / z_2 * fx;
+    L.B[6] = (1 + y * y / z_2) * fy;
+    L.B[7] = -x * y / z_2 * fy;
+    L.B[8] = -x / z * fy;
+    L.B[9] = 0;
+    L.B[10] = -1. / z * fy;
+    L.B[11] = y / z_2 * fy;
+    const int e = P.e_orig[a];
+    const double sg = P.e_isig[a];
+    double r0, r1;
+    huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
+    L.w = r1 * sg;
+    L.om0 = -(sg * P.err[2 * e]) * r1;
+    L.om1 = -(sg * P.err[2 * e + 1]) * r1;
+}
+
+// constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
+//  - per free pose (one wave, lanes stride the pose's edges in edge order,
+//    fixed butterfly reduction): Hpp += B^T W B, bp += B^T (-Omega e)
+//  - per point (one thread, its edges in order): Hll += A^T W A,
+//    bl += A^T (-Omega e), and the edge's Hpl = B^T W A stored component-major
+//    (hpl[k * nE + a]) for the Schur complement and back-substitution.
 __device__ void linearize(LbaDev& P)
 {
-    for (int a = threadIdx.x; a < P.nE; a += kLbaThreads) {
-        const double* T = P.pose + 7 * P.e_pose[a];
-        double pc[3];
-        se3_map(T, P.point + 3 * P.e_point[a], pc);
-        const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
-        const double* c = P.cam + 4 * P.e_pose[a];
-        const double fx = c[0], fy = c[1];
-        const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
-        double R[9];
-        qmat(Q{T[0], T[1], T[2], T[3]}, R);
-        const double s = -1. / z;
-        double A[6], B[12];
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++)
-                A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
-        B[0] = x * y / z_2 * fx;
-        B[1] = -(1 + (x * x / z_2)) * fx;
-        B[2] = y / z * fx;
-        B[3] = -1. / z * fx;
-        B[4] = 0;
-        B[5] = x / z_2 * fx;
-        B[6] = (1 + y * y / z_2) * fy;
-        B[7] = -x * y / z_2 * fy;
-        B[8] = -x / z * fy;
-        B[9] = 0;
-        B[10] = -1. / z * fy;
-        B[11] = y / z_2 * fy;
-        const int e = P.e_orig[a];
-        const double sg = P.e_isig[a];
-        double r0, r1;
-        huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
-        const double w = r1 * sg;
-        const double om0 = -(sg * P.err[2 * e]) * r1, om1 = -(sg * P.err[2 * e + 1]) * r1;
-        double* ce = P.ce + 54 * (size_t)a;
-        int k = 0;
-        for (int i = 0; i < 6; i++)
-            for (int j = i; j < 6; j++) ce[k++] = (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
-        for (int i = 0; i < 6; i++) ce[21 + i] = B[i] * om0 + B[6 + i] * om1;
-        k = 27;
-        for (int i = 0; i < 3; i++)
-            for (int j = i; j < 3; j++) ce[k++] = (A[i] * w) * A[j] + (A[3 + i] * w) * A[3 + j];
-        for (int i = 0; i < 3; i++) ce[33 + i] = A[i] * om0 + A[3 + i] * om1;
-        for (int i = 0; i < 6; i++)
-            for (int j = 0; j < 3; j++) ce[36 + i * 3 + j] = (B[i] * w) * A[j] + (B[6 + i] * w) * A[3 + j];
-    }
-    __syncthreads();
-    // per free pose: Hpp (21) + bp (6); one wave per pose, lanes stride the
-    // pose's edges, fixed-shape butterfly reduction (deterministic)
-    {
-        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int p = wv; p < P.nP; p += kLbaWaves) {
-            double acc[27];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int p = wv; p < P.nP; p += kLbaWaves) {
+        double acc[27];
 #pragma unroll
-            for (int v = 0; v < 27; v++) acc[v] = 0.0;
-            for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
-                const double* c = P.ce + 54 * (size_t)P.pe_idx[q];
+        for (int v = 0; v < 27; v++) acc[v] = 0.0;
+        for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
+            EdgeLin L;
+            edge_linearize(P, P.pe_idx[q], L);
+            int k = 0;
 #pragma unroll
-                for (int v = 0; v < 27; v++) acc[v] += c[v];
-            }
+            for (int i = 0; i < 6; i++)
 #pragma unroll
-            for (int v = 0; v < 27; v++) {
-                const double t = wave_sum_d(acc[v]);
-                if (lane == 0) P.hp[27 * p + v] = t;
-            }
+                for (int j = i; j < 6; j++) acc[k++] += (L.B[i] * L.w) * L.B[j] + (L.B[6 + i] * L.w) * L.B[6 + j];
+#pragma unroll
+            for (int i = 0; i < 6; i++) acc[21 + i] += L.B[i] * L.om0 + L.B[6 + i] * L.om1;
+        }
+#pragma unroll
+        for (int v = 0; v < 27; v++) {
+            const double t = wave_sum_d(acc[v]);
+            if (lane == 0) P.hp[27 * p + v] = t;
         }
     }
-    // per point: Hll (6) + bl (3) in edge order, one thread per point
+    const size_t st = (size_t)P.nE;
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         double acc[9];
 #pragma unroll
         for (int v = 0; v < 9; v++) acc[v] = 0.0;
         for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) {
-            const double* c = P.ce + 54 * (size_t)P.le_idx[q] + 27;
+            const int a = P.le_idx[q];
+            EdgeLin L;
+            edge_linearize(P, a, L);
+            int k = 0;
 #pragma unroll
-            for (int v = 0; v < 9; v++) acc[v] += c[v];
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = i; j < 3; j++) acc[k++] += (L.A[i] * L.w) * L.A[j] + (L.A[3 + i] * L.w) * L.A[3 + j];
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[6 + i] += L.A[i] * L.om0 + L.A[3 + i] * L.om1;
+            if (P.e_ph[a] >= 0) {
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+#pragma unroll
+                    for (int j = 0; j < 3; j++)
+                        P.ce[st * (i * 3 + j) + a] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
+            }
         }
 #pragma unroll
         for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
@@ -385,118 +427,107 @@ __device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j 
 
 // One Levenberg trial: Schur complement, LLT, back-substitution, update.
 // Returns false when the reduced system is not positive definite.
-__device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
+__device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DScratch& sc)
 {
+    LBA_T0();
     const int n = P.dim_p;
-    // per point: D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse), db
+    const size_t st = (size_t)P.nE;
+    // S <- 0, then the diagonal blocks Hpp + lambda I (full, symmetric); bs <- bp
+    for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;
+    __syncthreads();
+    for (int item = threadIdx.x; item < P.nP * 36; item += kLbaThreads) {
+        const int p = item / 36, rc = item - p * 36, r = rc / 6, c = rc - r * 6;
+        S[(size_t)(6 * p + r) * n + 6 * p + c] = P.hp[27 * p + (r <= c ? up6(r, c) : up6(c, r))] + (r == c ? lambda : 0.0);
+    }
+    for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = P.hp[27 * (i / 6) + 21 + (i % 6)];
+    __syncthreads();
+    LBA_MARK(1);
+    // Schur complement, point by point (one thread per point, its edges are
+    // contiguous): D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse),
+    // db; then bs -= W_i db and S(i, j) -= (W_i Dinv) W_j^T for every pair of
+    // the point's free-pose edges (upper blocks; diagonal blocks upper
+    // triangle), accumulated with FP64 atomics into the reduced camera system
+    // held in LDS.
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
         double m[9];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) m[i * 3 + j] = h[i <= j ? up3(i, j) : up3(j, i)] + (i == j ? lambda : 0.0);
-        auto cof = [&](int i, int j) {
-            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-            return m[i1 * 3 + j1] * m[i2 * 3 + j2] - m[i1 * 3 + j2] * m[i2 * 3 + j1];
-        };
-        const double det = cof(0, 0) * m[0] + cof(1, 0) * m[3] + cof(2, 0) * m[6];
-        const double inv = 1.0 / det;
-        double* d = P.dl + 12 * l;
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) d[i * 3 + j] = cof(j, i) * inv;
-        const double* bl = h + 6;
-        for (int i = 0; i < 3; i++) d[9 + i] = d[3 * i] * bl[0] + d[3 * i + 1] * bl[1] + d[3 * i + 2] * bl[2];
-        for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
-            const int a = P.lc_idx[q];
-            const double* Bi = P.ce + 54 * (size_t)a + 36;
-            double* o = P.eb + 24 * (size_t)a;
-            for (int r = 0; r < 6; r++) {
-                for (int c = 0; c < 3; c++) o[r * 3 + c] = Bi[r * 3] * d[c] + Bi[r * 3 + 1] * d[3 + c] + Bi[r * 3 + 2] * d[6 + c];
-                o[18 + r] = Bi[r * 3] * d[9] + Bi[r * 3 + 1] * d[10] + Bi[r * 3 + 2] * d[11];
-            }
-        }
-    }
-    for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;   // blocks without shared points
-    __syncthreads();
-    // reduced camera system, upper 6x6 blocks: Hpp (+lambda) - sum_l B_i Dinv B_j^T;
-    // one wave per block, lanes stride the shared landmarks, butterfly reduction
-    {
-        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int bk = wv; bk < P.nblk; bk += kLbaWaves) {
-            const int i1 = P.blk_ij[2 * bk], i2 = P.blk_ij[2 * bk + 1];
-            double acc[36];
 #pragma unroll
-            for (int k = 0; k < 36; k++) acc[k] = 0.0;
-            for (int q = P.blk_ptr[bk] + lane; q < P.blk_ptr[bk + 1]; q += 64) {
-                const int e1 = P.blk_c[2 * q], e2 = P.blk_c[2 * q + 1];
-                const double* BD = P.eb + 24 * (size_t)e1;
-                const double* Bj = P.ce + 54 * (size_t)e2 + 36;
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) m[i * 3 + j] = h[i <= j ? up3(i, j) : up3(j, i)] + (i == j ? lambda : 0.0);
+        double d[12];
+        {
+            const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
+            const double c01 = m[5] * m[6] - m[3] * m[8], c11 = m[8] * m[0] - m[6] * m[2], c21 = m[2] * m[3] - m[0] * m[5];
+            const double c02 = m[3] * m[7] - m[4] * m[6], c12 = m[6] * m[1] - m[7] * m[0], c22 = m[0] * m[4] - m[1] * m[3];
+            const double det = c00 * m[0] + c10 * m[3] + c20 * m[6];
+            const double inv = 1.0 / det;
+            d[0] = c00 * inv; d[1] = c10 * inv; d[2] = c20 * inv;   // d[i*3+j] = cof(j, i) / det
+            d[3] = c01 * inv; d[4] = c11 * inv; d[5] = c21 * inv;
+            d[6] = c02 * inv; d[7] = c12 * inv; d[8] = c22 * inv;
+        }
+        const double* bl = h + 6;
+#pragma unroll
+        for (int i = 0; i < 3; i++) d[9 + i] = d[3 * i] * bl[0] + d[3 * i + 1] * bl[1] + d[3 * i + 2] * bl[2];
+        double* dl = P.dl + 12 * l;
+#pragma unroll
+        for (int i = 0; i < 12; i++) dl[i] = d[i];
+        const int q0 = P.lc_ptr[l], q1 = P.lc_ptr[l + 1];
+        for (int qi = q0; qi < q1; qi++) {
+            const int ai = P.lc_idx[qi], i1 = P.e_ph[ai];
+            double wd[18];   // W_i Dinv (6x3)
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double b0 = P.ce[st * (r * 3) + ai], b1 = P.ce[st * (r * 3 + 1) + ai], b2 = P.ce[st * (r * 3 + 2) + ai];
+#pragma unroll
+                for (int c = 0; c < 3; c++) wd[r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
+                atomicAdd(&bs[6 * i1 + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
+            }
+            for (int qj = qi; qj < q1; qj++) {
+                const int aj = P.lc_idx[qj], i2 = P.e_ph[aj];
                 double bj[18];
 #pragma unroll
-                for (int k = 0; k < 18; k++) bj[k] = Bj[k];
+                for (int k = 0; k < 18; k++) bj[k] = P.ce[st * k + aj];
 #pragma unroll
-                for (int r = 0; r < 6; r++) {
-                    const double d0 = BD[r * 3], d1 = BD[r * 3 + 1], d2 = BD[r * 3 + 2];
+                for (int r = 0; r < 6; r++)
 #pragma unroll
-                    for (int c = 0; c < 6; c++) acc[r * 6 + c] += d0 * bj[c * 3] + d1 * bj[c * 3 + 1] + d2 * bj[c * 3 + 2];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 36; k++) {
-                const double t = wave_sum_d(acc[k]);
-                const int r = k / 6, c = k % 6;
-                if (lane == k && !(i1 == i2 && r > c)) {   // CHOLMOD reads the upper triangle only
-                    double v = -t;
-                    if (i1 == i2) v += P.hp[27 * i1 + up6(r, c)] + (r == c ? lambda : 0.0);
-                    S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = v;
-                    S[(size_t)(6 * i2 + c) * n + 6 * i1 + r] = v;
-                }
-            }
-        }
-    }
-    // bschur = bp - coef; one wave per pose, lanes stride its Schur edges
-    {
-        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int p = wv; p < P.nP; p += kLbaWaves) {
-            double acc[6];
-#pragma unroll
-            for (int r = 0; r < 6; r++) acc[r] = 0.0;
-            for (int q = P.pc_ptr[p] + lane; q < P.pc_ptr[p + 1]; q += 64) {
-                const double* o = P.eb + 24 * (size_t)P.pc_idx[q] + 18;
-#pragma unroll
-                for (int r = 0; r < 6; r++) acc[r] += o[r];
-            }
-#pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double t = wave_sum_d(acc[r]);
-                if (lane == r) P.bs[6 * p + r] = P.hp[27 * p + 21 + r] - t;
+                    for (int c = 0; c < 6; c++) {
+                        if (i1 == i2 && c < r) continue;
+                        const double v = wd[r * 3] * bj[c * 3] + wd[r * 3 + 1] * bj[c * 3 + 1] + wd[r * 3 + 2] * bj[c * 3 + 2];
+                        atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
+                    }
             }
         }
     }
     __syncthreads();
-    // dense LLT (right-looking), lower triangle
+    // the factorisation reads the lower triangle: mirror the upper blocks
+    for (int item = threadIdx.x; item < n * n; item += kLbaThreads) {
+        const int r = item / n, c = item - r * n;
+        if (c < r) S[item] = S[(size_t)c * n + r];
+    }
+    __syncthreads();
+    LBA_MARK(2);
+    // dense LLT (right-looking), lower triangle; two barriers per column
     for (int k = 0; k < n; k++) {
-        if (threadIdx.x == 0) {
-            const double akk = S[(size_t)k * n + k];
-            sc.iv[0] = (akk > 0) ? 1 : 0;
-            S[(size_t)k * n + k] = (akk > 0) ? sqrt(akk) : akk;
-        }
-        __syncthreads();
-        if (!sc.iv[0]) return false;
-        const double lkk = S[(size_t)k * n + k];
+        const double akk = S[(size_t)k * n + k];
+        if (!(akk > 0)) return false;   // same value in every thread
+        const double lkk = sqrt(akk);
+        __syncthreads();                // everyone has read S[k][k]
+        if (threadIdx.x == 0) S[(size_t)k * n + k] = lkk;
         for (int i = k + 1 + threadIdx.x; i < n; i += kLbaThreads) S[(size_t)i * n + k] /= lkk;
         __syncthreads();
-        const int m = n - k - 1;
-        for (int item = threadIdx.x; item < m * m; item += kLbaThreads) {
-            const int i = k + 1 + item / m, j = k + 1 + (item - (item / m) * m);
-            if (j <= i) S[(size_t)i * n + j] -= S[(size_t)i * n + k] * S[(size_t)j * n + k];
+        for (int i = k + 1 + (threadIdx.x >> 5); i < n; i += kLbaThreads / 32) {
+            const double lik = S[(size_t)i * n + k];
+            for (int j = k + 1 + (threadIdx.x & 31); j <= i; j += 32) S[(size_t)i * n + j] -= lik * S[(size_t)j * n + k];
         }
         __syncthreads();
     }
+    LBA_MARK(3);
     // forward / backward substitution by one wave (no block barriers per step)
     double* xp = P.x;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        for (int i = lane; i < n; i += 64) xp[i] = P.bs[i];
+        for (int i = lane; i < n; i += 64) xp[i] = bs[i];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -518,6 +549,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
         }
     }
     __syncthreads();
+    LBA_MARK(4);
     // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i)
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
@@ -525,10 +557,9 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
         for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
             const int a = P.lc_idx[q];
             const int i1 = P.e_ph[a];
-            const double* Bi = P.ce + 54 * (size_t)a + 36;
             for (int c = 0; c < 3; c++) {
                 double acc = 0;
-                for (int r = 0; r < 6; r++) acc += Bi[r * 3 + c] * (-xp[6 * i1 + r]);
+                for (int r = 0; r < 6; r++) acc += P.ce[(size_t)P.nE * (r * 3 + c) + a] * (-xp[6 * i1 + r]);
                 cl[c] += acc;
             }
         }
@@ -536,6 +567,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, DScratch& sc)
         for (int i = 0; i < 3; i++) P.x[n + 3 * l + i] = d[3 * i] * cl[0] + d[3 * i + 1] * cl[1] + d[3 * i + 2] * cl[2];
     }
     __syncthreads();
+    LBA_MARK(5);
     return true;
 }
 
@@ -551,11 +583,16 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         return;
     }
     const int n = P.dim_p;
-    double* S = (n * n <= lds_S_cap) ? s_S : P.S;
+    const bool in_lds = n * n + n <= lds_S_cap;
+    double* S = in_lds ? s_S : P.S;
+    double* bsv = in_lds ? s_S + (size_t)n * n : P.bs;
+    LBA_T0();
     double currentChi = compute_errors(P, sc);
     const double iniChi = currentChi;
     if (iteration == 0 && threadIdx.x == 0) P.chi2_initial = currentChi;
+    LBA_MARK(6);
     linearize(P);
+    LBA_MARK(7);
     double lambda = P.lambda, ni = P.ni;
     if (iteration == 0) {
         double m = 0;
@@ -576,7 +613,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose_bk[i] = P.pose[i];
         for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point_bk[i] = P.point[i];
         __syncthreads();
-        const bool ok2 = trial_solve(P, lambda, S, sc);
+        const bool ok2 = trial_solve(P, lambda, S, bsv, sc);
         if (ok2) {
             for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
             for (int item = threadIdx.x; item < P.nL * 3; item += kLbaThreads) {
@@ -588,7 +625,9 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
             if (threadIdx.x == 0) P.not_posdef++;
         }
         __syncthreads();
+        LBA_T0();
         double tempChi = compute_errors(P, sc);
+        LBA_MARK(8);
         if (!ok2) tempChi = 1.79769313486231570815e+308;
         // computeScale: sum_j x_j (lambda x_j + b_j)
         double part = 0;
@@ -683,8 +722,7 @@ struct HostStruct {
     std::vector<int> e_orig, e_pose, e_point, e_ph, e_lh;
     std::vector<double> e_obs, e_isig;
     std::vector<int> iv_pose, iv_point;
-    std::vector<int> pe_ptr, pe_idx, le_ptr, le_idx, lc_ptr, lc_idx, pc_ptr, pc_idx;
-    std::vector<int> blk_ij, blk_ptr, blk_c;
+    std::vector<int> pe_ptr, pe_idx, le_ptr, le_idx, lc_ptr, lc_idx;
     int nP = 0, nL = 0;
 };
 
@@ -741,50 +779,16 @@ void build_struct(const orbx_ba_problem& p, const uint8_t* removed, HostStruct& 
         }
         ptr[n] = (int)idx.size();
     };
-    std::vector<std::vector<int>> pe(s.nP), le(s.nL), lc(s.nL), pc(s.nP);
+    std::vector<std::vector<int>> pe(s.nP), le(s.nL), lc(s.nL);
     for (int a = 0; a < nE; a++) {
         if (s.e_ph[a] >= 0) pe[s.e_ph[a]].push_back(a);
         le[s.e_lh[a]].push_back(a);
         if (s.e_ph[a] >= 0) lc[s.e_lh[a]].push_back(a);
     }
     for (auto& v : lc) std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return s.e_ph[x] < s.e_ph[y]; });
-    for (int l = 0; l < s.nL; l++)
-        for (int a : lc[l]) pc[s.e_ph[a]].push_back(a);   // landmark order per pose
     csr(s.nP, pe, s.pe_ptr, s.pe_idx);
     csr(s.nL, le, s.le_ptr, s.le_idx);
     csr(s.nL, lc, s.lc_ptr, s.lc_idx);
-    csr(s.nP, pc, s.pc_ptr, s.pc_idx);
-    // Schur blocks (i1 <= i2): diagonal blocks always, plus pairs sharing a point
-    std::vector<int> blk_id((size_t)s.nP * s.nP, -1);
-    std::vector<std::vector<int>> contrib;
-    s.blk_ij.clear();
-    auto block = [&](int i1, int i2) {
-        int& id = blk_id[(size_t)i1 * s.nP + i2];
-        if (id < 0) {
-            id = (int)contrib.size();
-            contrib.emplace_back();
-            s.blk_ij.push_back(i1);
-            s.blk_ij.push_back(i2);
-        }
-        return id;
-    };
-    for (int i = 0; i < s.nP; i++) block(i, i);
-    for (int l = 0; l < s.nL; l++) {
-        const auto& col = lc[l];
-        for (size_t x = 0; x < col.size(); x++)
-            for (size_t y = x; y < col.size(); y++) {
-                const int id = block(s.e_ph[col[x]], s.e_ph[col[y]]);
-                contrib[id].push_back(col[x]);
-                contrib[id].push_back(col[y]);
-            }
-    }
-    s.blk_ptr.assign(contrib.size() + 1, 0);
-    s.blk_c.clear();
-    for (size_t b = 0; b < contrib.size(); b++) {
-        s.blk_ptr[b] = (int)(s.blk_c.size() / 2);
-        s.blk_c.insert(s.blk_c.end(), contrib[b].begin(), contrib[b].end());
-    }
-    s.blk_ptr[contrib.size()] = (int)(s.blk_c.size() / 2);
 }
 
 // Packs host vectors into one device allocation.
@@ -824,7 +828,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
                 p.edge_pose[e] >= p.n_poses)
                 return ORBX_ERR_ARG;
     }
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     // persistent per-problem device state: poses, points, errors, counters
     std::vector<long long> offs(3 * P);
     Packer base;
@@ -866,18 +870,24 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         std::vector<HostStruct> hs(P);
         std::vector<size_t> o[32];
         for (auto& v : o) v.resize(P);
+        {
+            // index structures of independent problems are built on host threads
+            const int nth = std::max(1, std::min<int>(P, std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+            std::vector<std::thread> pool;
+            for (int t = 0; t < nth; t++)
+                pool.emplace_back([&, t]() {
+                    for (int i = t; i < P; i += nth)
+                        build_struct(probs[i], pass == 0 ? nullptr : all_st.data() + offs[3 * i], hs[i]);
+                });
+            for (auto& th : pool) th.join();
+        }
         for (int i = 0; i < P; i++) {
-            const orbx_ba_problem& p = probs[i];
-            const uint8_t* removed = pass == 0 ? nullptr : all_st.data() + offs[3 * i];
-            build_struct(p, removed, hs[i]);
             HostStruct& s = hs[i];
             o[0][i] = pk.add(s.e_orig); o[1][i] = pk.add(s.e_pose); o[2][i] = pk.add(s.e_point);
             o[3][i] = pk.add(s.e_ph); o[4][i] = pk.add(s.e_lh); o[5][i] = pk.add(s.e_obs);
             o[6][i] = pk.add(s.e_isig); o[7][i] = pk.add(s.iv_pose); o[8][i] = pk.add(s.iv_point);
             o[9][i] = pk.add(s.pe_ptr); o[10][i] = pk.add(s.pe_idx); o[11][i] = pk.add(s.le_ptr);
             o[12][i] = pk.add(s.le_idx); o[13][i] = pk.add(s.lc_ptr); o[14][i] = pk.add(s.lc_idx);
-            o[15][i] = pk.add(s.pc_ptr); o[16][i] = pk.add(s.pc_idx); o[17][i] = pk.add(s.blk_ij);
-            o[18][i] = pk.add(s.blk_ptr); o[19][i] = pk.add(s.blk_c);
         }
         const size_t o_devs = pk.reserve(sizeof(LbaDev) * P);
         // device-only scratch after the staged block (never copied)
@@ -890,13 +900,12 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         for (int i = 0; i < P; i++) {
             const HostStruct& s = hs[i];
             const size_t nE = s.e_orig.size();
-            o[20][i] = dev_reserve(54 * nE * 8);
-            o[21][i] = dev_reserve(24 * nE * 8);
+            o[20][i] = dev_reserve(18 * nE * 8);
             o[22][i] = dev_reserve(27 * (size_t)s.nP * 8);
             o[23][i] = dev_reserve(9 * (size_t)s.nL * 8);
             o[24][i] = dev_reserve(12 * (size_t)s.nL * 8);
             const size_t n = 6 * (size_t)s.nP;
-            o[25][i] = dev_reserve(n * n > (size_t)kLdsSCap ? n * n * 8 : 8);
+            o[25][i] = dev_reserve(n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8);
             o[26][i] = dev_reserve((n + 3 * (size_t)s.nL) * 8);
             o[27][i] = dev_reserve(n * 8 + 8);
         }
@@ -917,7 +926,6 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             D.nP = s.nP;
             D.nL = s.nL;
             D.nE = (int)s.e_orig.size();
-            D.nblk = (int)(s.blk_ij.size() / 2);
             D.nposes_all = p.n_poses;
             D.npoints_all = p.n_points;
             D.nedges_all = p.n_edges;
@@ -943,13 +951,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             D.le_idx = reinterpret_cast<const int*>(d + o[12][i]);
             D.lc_ptr = reinterpret_cast<const int*>(d + o[13][i]);
             D.lc_idx = reinterpret_cast<const int*>(d + o[14][i]);
-            D.pc_ptr = reinterpret_cast<const int*>(d + o[15][i]);
-            D.pc_idx = reinterpret_cast<const int*>(d + o[16][i]);
-            D.blk_ij = reinterpret_cast<const int*>(d + o[17][i]);
-            D.blk_ptr = reinterpret_cast<const int*>(d + o[18][i]);
-            D.blk_c = reinterpret_cast<const int*>(d + o[19][i]);
             D.ce = reinterpret_cast<double*>(d + o[20][i]);
-            D.eb = reinterpret_cast<double*>(d + o[21][i]);
             D.hp = reinterpret_cast<double*>(d + o[22][i]);
             D.hl = reinterpret_cast<double*>(d + o[23][i]);
             D.dl = reinterpret_cast<double*>(d + o[24][i]);
@@ -970,7 +972,8 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         LbaDev* dd = reinterpret_cast<LbaDev*>(d + o_devs);
         const int iters = pass == 0 ? iters0 : iters1;
         size_t max_n2 = 0;
-        for (int i = 0; i < P; i++) max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p);
+        for (int i = 0; i < P; i++)
+            max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p + (size_t)devs[i].dim_p);
         const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;
         const int lds_cap = (int)(lds / 8);
         for (int it = 0; it < iters; it++) {
@@ -1042,6 +1045,13 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
 }  // namespace orbx
 
 extern "C" {
+
+#ifdef ORBX_LBA_PROFILE
+int orbx_debug_lba_prof(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_lba_prof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1, const volatile uint8_t* abort,
                    uint8_t* edge_status, uint8_t* point_bad, orbx_ba_stats* stats)

@@ -105,5 +105,6 @@ def test_lba_batch_equals_single(ctx):
     for k in range(4):
         a = cps[k][1]
         s = singles[k]
-        assert np.array_equal(a["pose_q"], s[0]["pose_q"]) and np.array_equal(a["points"], s[0]["points"])
+        # FP64 atomics make the summation order run-dependent: equal up to rounding
+        assert np.abs(a["pose_q"] - s[0]["pose_q"]).max() < 1e-10 and np.abs(a["points"] - s[0]["points"]).max() < 1e-9
         assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
