@@ -56,7 +56,7 @@ struct LbaDev {
     const int* le_ptr; const int* le_idx;   // per point: active edges, edge order
     const int* lc_ptr; const int* lc_idx;   // per point: Schur column (free poses, pose order)
     // scratch
-    double* ce;                    // [18][nE] (SoA): Hpl = B^T W A per edge
+    double* ce;                    // [nE][18]: Hpl = B^T W A per edge (row-major 6x3)
     double* hp;                    // [nP][27]: Hpp upper 21 | bp 6
     double* hl;                    // [nL][9]: Hll upper 6 | bl 3
     double* dl;                    // [nL][12]: Dinv 9 | db 3
@@ -392,7 +392,6 @@ __device__ void linearize(LbaDev& P)
             if (lane == 0) P.hp[27 * p + v] = t;
         }
     }
-    const size_t st = (size_t)P.nE;
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         double acc[9];
 #pragma unroll
@@ -408,12 +407,15 @@ __device__ void linearize(LbaDev& P)
                 for (int j = i; j < 3; j++) acc[k++] += (L.A[i] * L.w) * L.A[j] + (L.A[3 + i] * L.w) * L.A[3 + j];
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[6 + i] += L.A[i] * L.om0 + L.A[3 + i] * L.om1;
-            if (P.e_ph[a] >= 0) {
+            if (P.e_ph[a] >= 0) {   // Hpl row of the edge: 18 contiguous doubles, 16-byte stores
+                double hpl[18];
 #pragma unroll
                 for (int i = 0; i < 6; i++)
 #pragma unroll
-                    for (int j = 0; j < 3; j++)
-                        P.ce[st * (i * 3 + j) + a] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
+                    for (int j = 0; j < 3; j++) hpl[i * 3 + j] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
+                double2* o = reinterpret_cast<double2*>(P.ce + 18 * (size_t)a);
+#pragma unroll
+                for (int i = 0; i < 9; i++) o[i] = make_double2(hpl[2 * i], hpl[2 * i + 1]);
             }
         }
 #pragma unroll
@@ -431,7 +433,6 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
 {
     LBA_T0();
     const int n = P.dim_p;
-    const size_t st = (size_t)P.nE;
     // S <- 0, then the diagonal blocks Hpp + lambda I (full, symmetric); bs <- bp
     for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;
     __syncthreads();
@@ -476,9 +477,19 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
         for (int qi = q0; qi < q1; qi++) {
             const int ai = P.lc_idx[qi], i1 = P.e_ph[ai];
             double wd[18];   // W_i Dinv (6x3)
+            double wi[18];
+            {
+                const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)ai);
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    const double2 v = src[k];
+                    wi[2 * k] = v.x;
+                    wi[2 * k + 1] = v.y;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 6; r++) {
-                const double b0 = P.ce[st * (r * 3) + ai], b1 = P.ce[st * (r * 3 + 1) + ai], b2 = P.ce[st * (r * 3 + 2) + ai];
+                const double b0 = wi[r * 3], b1 = wi[r * 3 + 1], b2 = wi[r * 3 + 2];
 #pragma unroll
                 for (int c = 0; c < 3; c++) wd[r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
                 atomicAdd(&bs[6 * i1 + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
@@ -486,8 +497,13 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
             for (int qj = qi; qj < q1; qj++) {
                 const int aj = P.lc_idx[qj], i2 = P.e_ph[aj];
                 double bj[18];
+                const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)aj);
 #pragma unroll
-                for (int k = 0; k < 18; k++) bj[k] = P.ce[st * k + aj];
+                for (int k = 0; k < 9; k++) {
+                    const double2 v = src[k];
+                    bj[2 * k] = v.x;
+                    bj[2 * k + 1] = v.y;
+                }
 #pragma unroll
                 for (int r = 0; r < 6; r++)
 #pragma unroll
@@ -559,7 +575,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
             const int i1 = P.e_ph[a];
             for (int c = 0; c < 3; c++) {
                 double acc = 0;
-                for (int r = 0; r < 6; r++) acc += P.ce[(size_t)P.nE * (r * 3 + c) + a] * (-xp[6 * i1 + r]);
+                for (int r = 0; r < 6; r++) acc += P.ce[18 * (size_t)a + r * 3 + c] * (-xp[6 * i1 + r]);
                 cl[c] += acc;
             }
         }
