@@ -87,29 +87,39 @@ struct BlockScratch {
     int vars[8];
 };
 
+// Wave64 scans / reductions on DPP row shifts + row broadcasts (gfx9):
+// VALU-only, no ds_bpermute round trips.  All 64 lanes must be active.
+template <int kCtrl, int kRowMask>
+__device__ inline int dpp_or0(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xf, false);
+}
+
 __device__ inline int wave_inclusive_scan(int v)
 {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    v += dpp_or0<0x111, 0xf>(v);   // row_shr:1
+    v += dpp_or0<0x112, 0xf>(v);   // row_shr:2
+    v += dpp_or0<0x114, 0xf>(v);   // row_shr:4
+    v += dpp_or0<0x118, 0xf>(v);   // row_shr:8
+    v += dpp_or0<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+    v += dpp_or0<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
     return v;
 }
 
 __device__ inline int wave_sum(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return __builtin_amdgcn_readlane(wave_inclusive_scan(v), 63);
 }
 
 __device__ inline int wave_max(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // Exclusive prefix of v over threadIdx order; *total = block sum.
@@ -413,7 +423,7 @@ __device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos
         nge += (k >= P);
     }
     const int le_incl = wave_inclusive_scan(nle), ge_incl = wave_inclusive_scan(nge);
-    const int tot_ge = __shfl(ge_incl, 63, 64);
+    const int tot_ge = __builtin_amdgcn_readlane(ge_incl, 63);
     const int le_before = le_incl - nle;
     const int ge_after_chunk = tot_ge - ge_incl;
     int cl = le_before, cr = ge_after_chunk + nge, best = 0;

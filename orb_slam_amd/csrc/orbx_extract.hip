@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         }
         const int cnt = __popc((mask | (mask >> 1)) & 0x55);
         const int incl = wave_inclusive_scan(cnt);
-        const int ntot = __shfl(incl, 63, 64);
+        const int ntot = __builtin_amdgcn_readlane(incl, 63);
         int w = incl - cnt;
         if (mask) {
 #pragma unroll
@@ -454,12 +454,12 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
         const int c = lane + 64 * k;
         const int take = (c < nCells && tot[k] > 0 && ret[k] > 0) ? min(tot[k], ret[k]) : 0;
         const int incl = wave_inclusive_scan(take);
-        const int kk = __shfl(ret[k], cell & 63, 64), pp = __shfl(base + incl - take, cell & 63, 64);
+        const int kk = __builtin_amdgcn_readlane(ret[k], cell & 63), pp = __builtin_amdgcn_readlane(base + incl - take, cell & 63);
         if ((cell >> 6) == k) {
             my_keep = kk;
             my_pre = pp;
         }
-        base += __shfl(incl, 63, 64);
+        base += __builtin_amdgcn_readlane(incl, 63);
     }
     *keep_c = my_keep;
     *pre_c = my_pre;

@@ -35,18 +35,30 @@ __device__ inline unsigned long long wave_min_u64(unsigned long long v)
     return v;
 }
 
+// Wave-wide min through DPP row shifts and row broadcasts (gfx9 wave64)
+// instead of ds_bpermute shuffles: a handful of VALU ops, no LDS round trips.
+// Lanes whose DPP source is out of range keep their own value, so the
+// partial results stay correct for min.  Result broadcast from lane 63.
 __device__ inline uint32_t wave_min_u32(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 __device__ inline int wave_min_i32(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // Frame::PosInGrid (src/Frame.cc:266-276): cell or -1.
@@ -157,6 +169,7 @@ struct InitLDS {
     int* m21;
     uint4* desc;        // 2 per candidate
     int* m12;           // per F1 keypoint
+    float* ang1;        // per F1 keypoint: angle (rotation check)
     signed char* pushed;
     int* offs;          // 257 list offsets of the current group
     int* hist;          // 32 bins + 3 maxima indices
@@ -166,7 +179,7 @@ struct InitLDS {
 
 __host__ __device__ inline size_t init_lds_bytes(int cap_c, int cap1, int cap_keys)
 {
-    return (size_t)cap_c * (7 * 4 + 32) + (size_t)cap1 * 4 + (size_t)((cap1 + 15) & ~15) + 257 * 4 + 36 * 4 +
+    return (size_t)cap_c * (7 * 4 + 32) + (size_t)cap1 * 8 + (size_t)((cap1 + 15) & ~15) + 257 * 4 + 36 * 4 +
            (size_t)cap_keys * 4 + 64;
 }
 
@@ -185,7 +198,8 @@ __device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap
     s.mdist = s.idx + cap_c;
     s.m21 = s.mdist + cap_c;
     s.m12 = s.m21 + cap_c;
-    s.offs = s.m12 + cap1;
+    s.ang1 = reinterpret_cast<float*>(s.m12 + cap1);
+    s.offs = reinterpret_cast<int*>(s.ang1 + cap1);
     s.hist = s.offs + 257;
     s.keys = reinterpret_cast<uint32_t*>(s.hist + 36);
     s.pushed = reinterpret_cast<signed char*>(s.keys + cap_keys);
@@ -234,6 +248,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     for (int i = tid; i < F1.n; i += kBlock) {
         s.m12[i] = -1;
         s.pushed[i] = -1;
+        s.ang1[i] = F1.kps[i].angle;
     }
     if (tid < 36) s.hist[tid] = 0;
     __syncthreads();
@@ -308,7 +323,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
                             s.m12[ii1] = s.idx[slot];
                             s.m21[slot] = ii1;
                             s.mdist[slot] = bestDist;
-                            if (check_ori) s.pushed[ii1] = (signed char)rot_bin(F1.kps[ii1].angle, s.ang[slot]);
+                            if (check_ori) s.pushed[ii1] = (signed char)rot_bin(s.ang1[ii1], s.ang[slot]);
                         }
                         wave_sync();
                     }
