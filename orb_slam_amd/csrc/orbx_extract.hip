@@ -95,31 +95,42 @@ struct RowWalk {
 // ---------------------------------------------------------------------------
 // Level 0: padded copy with BORDER_REFLECT_101.  4 output bytes per thread.
 // ---------------------------------------------------------------------------
-__device__ inline void pyr_level0_word(const ExtractArgs& a, const LevelGeom& L, int f, int py, int px0)
-{
-    const uint8_t* src = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
-    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
-    const int sy = reflect101(py - kEdge, L.h);
-    uint32_t word = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const int px = px0 + b;
-        uint32_t v = 0;
-        if (px < L.pw) v = src[(size_t)sy * a.w + reflect101(px - kEdge, L.w)];
-        word |= v << (8 * b);
-    }
-    *reinterpret_cast<uint32_t*>(dst + px0) = word;
-}
+// One thread per (dword column, strip of kPyrRows rows): the column's
+// reflected source offsets are computed once and the strip's independent
+// row loads are in flight together.
+constexpr int kPyrRows = 8;
 
 __global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
 {
     const int f = blockIdx.y;
     const LevelGeom L = a.levels[0];
-    const int words_per_row = L.stride >> 2;
+    const int wpr = L.stride >> 2, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= words_per_row * L.ph) return;
-    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
-    pyr_level0_word(a, L, f, py, px0);
+    if (idx >= wpr * nstrips) return;
+    const int strip = idx / wpr, q = idx - strip * wpr, px0 = 4 * q;
+    const uint8_t* src = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
+    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
+    const bool aligned = (px0 - kEdge) >= 0 && (px0 - kEdge + 3) < L.w && (a.w & 3) == 0;
+    int sx[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) sx[b] = (px0 + b < L.pw) ? reflect101(px0 + b - kEdge, L.w) : -1;
+#pragma unroll
+    for (int rr = 0; rr < kPyrRows; rr++) {
+        // rows past the level repeat the last one (loads stay in bounds and
+        // can all be issued up front); their stores are skipped
+        const int py = min(strip * kPyrRows + rr, L.ph - 1);
+        const uint8_t* row = src + (size_t)reflect101(py - kEdge, L.h) * a.w;
+        uint32_t word;
+        if (aligned) {
+            word = *reinterpret_cast<const uint32_t*>(row + px0 - kEdge);
+        } else {
+            word = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (sx[b] >= 0) word |= (uint32_t)row[sx[b]] << (8 * b);
+        }
+        if (strip * kPyrRows + rr < L.ph) *reinterpret_cast<uint32_t*>(dst + (size_t)py * L.stride + px0) = word;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -144,38 +155,36 @@ __device__ inline uint8_t resize_pixel(const uint8_t* prev, int pstride, const R
     return sat_u8((S0 * r.b0 + S1 * r.b1 + (1 << 21)) >> 22);
 }
 
-__device__ inline void pyr_resize_word(const ExtractArgs& a, const LevelGeom& L, const LevelGeom& P, int f, int py,
-                                       int px0)
-{
-    const uint8_t* frame = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
-    const uint8_t* prev = frame + P.off + (size_t)kEdge * P.stride + kEdge;
-    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py * L.stride;
-    const int y = reflect101(py - kEdge, L.h);
-    const ResizeRow r = a.res_rows[L.res_row_off + y];
-    uint32_t word = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const int px = px0 + b;
-        uint32_t v = 0;
-        if (px < L.pw) {
-            const int x = reflect101(px - kEdge, L.w);
-            v = resize_pixel(prev, P.stride, a.res_cols[L.res_col_off + x], r, x < L.nvec_resize);
-        }
-        word |= v << (8 * b);
-    }
-    *reinterpret_cast<uint32_t*>(dst + px0) = word;
-}
-
 __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 {
     const int f = blockIdx.y;
     const LevelGeom L = a.levels[level];
     const LevelGeom P = a.levels[level - 1];
-    const int words_per_row = L.stride >> 2;
+    const int wpr = L.stride >> 2, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= words_per_row * L.ph) return;
-    const int py = idx / words_per_row, px0 = (idx - py * words_per_row) * 4;
-    pyr_resize_word(a, L, P, f, py, px0);
+    if (idx >= wpr * nstrips) return;
+    const int strip = idx / wpr, q = idx - strip * wpr, px0 = 4 * q;
+    const uint8_t* prev = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + P.off + (size_t)kEdge * P.stride + kEdge;
+    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
+    ResizeCol c[4];
+    bool vec[4], on[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        on[b] = px0 + b < L.pw;
+        const int x = on[b] ? reflect101(px0 + b - kEdge, L.w) : 0;
+        c[b] = a.res_cols[L.res_col_off + x];
+        vec[b] = x < L.nvec_resize;
+    }
+#pragma unroll
+    for (int rr = 0; rr < kPyrRows; rr++) {
+        const int py = min(strip * kPyrRows + rr, L.ph - 1);
+        const ResizeRow r = a.res_rows[L.res_row_off + reflect101(py - kEdge, L.h)];
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (on[b]) word |= (uint32_t)resize_pixel(prev, P.stride, c[b], r, vec[b]) << (8 * b);
+        if (strip * kPyrRows + rr < L.ph) *reinterpret_cast<uint32_t*>(dst + (size_t)py * L.stride + px0) = word;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -777,15 +786,15 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         timer_begin(ctx, "pyr0");
         {
             const LevelGeom& L = g.levels[0];
-            const int words = (L.stride / 4) * L.ph;
-            hipLaunchKernelGGL(k_pyr_level0, dim3((words + 255) / 256, nb), dim3(256), 0, st, a);
+            const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
+            hipLaunchKernelGGL(k_pyr_level0, dim3((items + 255) / 256, nb), dim3(256), 0, st, a);
         }
         timer_end(ctx, "pyr0");
         for (int l = 1; l < g.nlevels; l++) {
             const LevelGeom& L = g.levels[l];
-            const int words = (L.stride / 4) * L.ph;
+            const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
             timer_begin(ctx, "resize");
-            hipLaunchKernelGGL(k_pyr_resize, dim3((words + 255) / 256, nb), dim3(256), 0, st, a, l);
+            hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, a, l);
             timer_end(ctx, "resize");
         }
         timer_begin(ctx, "fast");
