@@ -155,8 +155,16 @@ def run_frames(args, wl, rank, local, world, dist):
     for _ in range(args.warmup):
         step()
     ctx.sync()
-    elapsed, kernels = timed(args, ctx, step, dist,
-                             ["pyr0", "resize", "fast", "retain", "blur", "describe", "match"])
+    names = ["pyr0", "resize", "fast", "retain", "blur", "describe", "match"]
+    elapsed, kernels = timed(args, ctx, step, dist, names)
+    # Diagnostic pass after the timed region: the same steps with the two
+    # extraction halves serialised, so each kernel's launch time is not shared
+    # with the other stream's kernels (per-kernel roofline without overlap).
+    ctx.set_split(False)
+    iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
+    _, iso = timed(iso_args, ctx, step, None, names)
+    ctx.set_split(True)
+    kernels = {"overlapped": kernels, "isolated": iso}
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
     stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
@@ -197,6 +205,7 @@ def run_lba(args, wl, rank, local, world, dist):
     for _ in range(args.warmup):
         step()
     elapsed, kernels = timed(args, ctx, step, dist, ["lba_iter", "lba_outliers"])
+    kernels = {"overlapped": kernels, "isolated": None}
     st = step()
     stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
                      dtype=np.float64)
@@ -268,17 +277,22 @@ def main():
     value, elapsed, _ = odist.job_rate(allst)
 
     if rank == 0:
-        # dominant kernel: largest total time; its algorithmic bytes per launch
-        # over its mean launch duration (HIP events on the context stream)
-        timed_k = [k for k in kernels if kernels[k]["launches"]] or list(kernels)
-        dom = max(timed_k, key=lambda k: kernels[k]["total_ms"])
-        launches_per_step = max(1, kernels[dom]["launches"] // args.steps)
-        per_launch = ab.get(dom, 0) * units.get(dom, 1) / launches_per_step
-        avg_s = kernels[dom]["avg_ms"] / 1e3
-        achieved = per_launch / avg_s / 1e9 if avg_s > 0 and per_launch > 0 else 0.0
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
-                "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": kernels[dom]["avg_ms"]}
+        def roofline(kern, steps):
+            # dominant kernel: largest total time; its algorithmic bytes per
+            # launch over its mean launch duration (HIP events on the stream
+            # the kernel is launched on)
+            timed_k = [k for k in kern if kern[k]["launches"]] or list(kern)
+            dom = max(timed_k, key=lambda k: kern[k]["total_ms"])
+            launches_per_step = max(1, kern[dom]["launches"] // steps)
+            per_launch = ab.get(dom, 0) * units.get(dom, 1) / launches_per_step
+            avg_s = kern[dom]["avg_ms"] / 1e3
+            achieved = per_launch / avg_s / 1e9 if avg_s > 0 and per_launch > 0 else 0.0
+            return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
+                    "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": kern[dom]["avg_ms"]}
+
+        roof = roofline(kernels["overlapped"], args.steps)
+        roof_iso = roofline(kernels["isolated"], 3) if kernels["isolated"] else None
         out = {
             "metric": wl["metric"], "value": round(value, 2), "unit": wl["unit"], "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -287,6 +301,8 @@ def main():
             "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
+        if roof_iso:
+            out["roofline_isolated"] = roof_iso
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)

@@ -107,8 +107,11 @@ int orbx_extract_batch(orbx_ctx* ctx, int B, const uint8_t* const* imgs,
  * context share one frame size (set by the first upload). */
 int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
                     int w, int h, size_t stride);
-/* Extract slots [first, first+count) (async, on the context stream). */
+/* Extract slots [first, first+count) (async, on the context stream).
+ * Batches of 32+ frames run as two halves on two internal streams (joined
+ * before the call's later work) unless disabled with orbx_dev_set_split. */
 int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
+int orbx_dev_set_split(orbx_ctx* ctx, int enable);
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */

@@ -71,6 +71,7 @@ def _declare(L):
         "orbx_dev_match_prev": ([vp, i, i, i, i, f, i], i),
         "orbx_dev_sync": ([vp], i),
         "orbx_dev_match_bf_prev": ([vp, i, i, i, i, f], i),
+        "orbx_dev_set_split": ([vp, i], i),
         "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
         "orbx_dev_kernel_time": ([vp, ctypes.c_char_p, dp, dp], i),
@@ -170,6 +171,10 @@ class Context:
     def match_prev(self, first, count, seq_len, window=100, nnratio=0.9, check_ori=True):
         _check(lib().orbx_dev_match_prev(self._h, first, count, seq_len, window, nnratio,
                                          int(check_ori)), "orbx_dev_match_prev")
+
+    def set_split(self, enable):
+        """Two concurrent half-batch streams for large extraction batches."""
+        _check(lib().orbx_dev_set_split(self._h, int(enable)), "orbx_dev_set_split")
 
     def match_bf_prev(self, first, count, seq_len, th_low=50, nnratio=0.9):
         _check(lib().orbx_dev_match_bf_prev(self._h, first, count, seq_len, th_low, nnratio),

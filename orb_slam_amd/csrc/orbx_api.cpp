@@ -19,7 +19,7 @@ static KernelTimer* find_timer(orbx_ctx* ctx, const char* name)
     return &ctx->timers.back();
 }
 
-void timer_begin(orbx_ctx* ctx, const char* name)
+void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st)
 {
     if (!ctx->timing) return;
     KernelTimer* t = find_timer(ctx, name);
@@ -29,15 +29,15 @@ void timer_begin(orbx_ctx* ctx, const char* name)
         t->start.push_back(a);
         t->stop.push_back(b);
     }
-    hipEventRecord(t->start[t->used], ctx->stream);
+    (void)hipEventRecord(t->start[t->used], st ? st : ctx->stream);
 }
 
-void timer_end(orbx_ctx* ctx, const char* name)
+void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st)
 {
     if (!ctx->timing) return;
     KernelTimer* t = find_timer(ctx, name);
     if (t->used >= (int)t->stop.size()) return;
-    hipEventRecord(t->stop[t->used], ctx->stream);
+    (void)hipEventRecord(t->stop[t->used], st ? st : ctx->stream);
     t->used++;
 }
 
@@ -196,6 +196,10 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     int r = ORBX_OK;
     const int S = max_batch;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK && (hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess))
+        r = ORBX_ERR_HIP;
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
     if (r == ORBX_OK) r = realloc_dev(ctx->level_count, (size_t)S * nlevels);
@@ -224,13 +228,17 @@ void orbx_destroy(orbx_ctx* ctx)
 {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     for (auto& t : ctx->timers) {
         for (auto e : t.start) hipEventDestroy(e);
         for (auto e : t.stop) hipEventDestroy(e);
     }
     free_buffers(ctx);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
@@ -284,6 +292,13 @@ int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wi
     if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
     hipSetDevice(ctx->device);
     return launch_match_prev(ctx, first, count, seq_len, window, nnratio, check_ori);
+}
+
+int orbx_dev_set_split(orbx_ctx* ctx, int enable)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    ctx->split = enable != 0;
+    return ORBX_OK;
 }
 
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)

@@ -24,6 +24,7 @@ namespace orbx {
 
 constexpr size_t kRetainLds = 128 * 1024;   // LDS budget of a retain block
 constexpr int kRetainCellCap = 1024;        // cell lists up to this length sort in LDS
+constexpr int kSplitMinFrames = 16;         // batches >= 2x this run as two concurrent halves
 
 __constant__ int8_t c_pattern[256][4] = {
 #include "orbx_pattern.inc"
@@ -777,55 +778,73 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
     a.max_list_cap = g.max_list_cap;
     a.max_level_cap = g.max_level_cap;
 
-    hipStream_t st = ctx->stream;
-    // The work buffers hold `count` frames starting at batch index 0; the
-    // frame store and outputs are indexed by slot.
-    for (int b0 = 0; b0 < count; b0 += ctx->slots) {
-        const int nb = min(ctx->slots, count - b0);
-        a.first_slot = first + b0;
-        timer_begin(ctx, "pyr0");
+    // One pass of the stage sequence over nb frames on stream st.
+    auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
+        timer_begin(ctx, "pyr0", st);
         {
             const LevelGeom& L = g.levels[0];
             const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
-            hipLaunchKernelGGL(k_pyr_level0, dim3((items + 255) / 256, nb), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(k_pyr_level0, dim3((items + 255) / 256, nb), dim3(256), 0, st, x);
         }
-        timer_end(ctx, "pyr0");
+        timer_end(ctx, "pyr0", st);
         for (int l = 1; l < g.nlevels; l++) {
             const LevelGeom& L = g.levels[l];
             const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
-            timer_begin(ctx, "resize");
-            hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, a, l);
-            timer_end(ctx, "resize");
+            timer_begin(ctx, "resize", st);
+            hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, l);
+            timer_end(ctx, "resize", st);
         }
-        timer_begin(ctx, "fast");
+        timer_begin(ctx, "fast", st);
         {
             const int pitch = (g.max_tile_bytes + 15) & ~15;
-            hipLaunchKernelGGL(k_fast_cells, dim3((int)g.cells.size(), nb), dim3(256), 2 * pitch, st, a, pitch);
+            hipLaunchKernelGGL(k_fast_cells, dim3((int)g.cells.size(), nb), dim3(256), 2 * pitch, st, x, pitch);
         }
-        timer_end(ctx, "fast");
-        timer_begin(ctx, "retain");
+        timer_end(ctx, "fast", st);
+        timer_begin(ctx, "retain", st);
         {
             // wave-private LDS: cell list + partition scratch (longer lists
             // are replayed in global memory)
             const int cw = 2 * kRetainCellCap + 8;
             const int cwaves = 4;
             hipLaunchKernelGGL(k_retain_cells, dim3(((int)g.cells.size() + cwaves - 1) / cwaves, nb), dim3(64 * cwaves),
-                               (size_t)cwaves * cw * 4, st, a, cwaves, cw);
+                               (size_t)cwaves * cw * 4, st, x, cwaves, cw);
             const int lw = 2 * g.max_level_cap + 8;
             const int lwaves = std::max(1, std::min(4, (int)(kRetainLds / (4 * (size_t)lw))));
             hipLaunchKernelGGL(k_retain_levels, dim3((g.nlevels + lwaves - 1) / lwaves, nb), dim3(64 * lwaves),
-                               (size_t)lwaves * lw * 4, st, a, lwaves, lw);
+                               (size_t)lwaves * lw * 4, st, x, lwaves, lw);
         }
-        timer_end(ctx, "retain");
-        timer_begin(ctx, "blur");
-        {
-            const int ntiles = ctx->blur_tiles_n;
-            hipLaunchKernelGGL(k_blur, dim3(ntiles, nb), dim3(kBlurItems), 0, st, a, ctx->blur_tiles);
-        }
-        timer_end(ctx, "blur");
-        timer_begin(ctx, "describe");
-        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + kWaves - 1) / kWaves, nb), dim3(256), 0, st, a);
-        timer_end(ctx, "describe");
+        timer_end(ctx, "retain", st);
+        timer_begin(ctx, "blur", st);
+        hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
+        timer_end(ctx, "blur", st);
+        timer_begin(ctx, "describe", st);
+        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + kWaves - 1) / kWaves, nb), dim3(256), 0, st, x);
+        timer_end(ctx, "describe", st);
+    };
+    // Work buffers are indexed by batch position (frame f of a pass uses
+    // work slot f); the frame store and outputs by slot.  Large batches run
+    // as two halves on two streams so that the VALU-bound FAST pass of one
+    // half overlaps the latency-bound passes of the other.
+    a.first_slot = first;
+    if (ctx->split && count >= 2 * kSplitMinFrames && ctx->stream2) {
+        const int n0 = count / 2, n1 = count - n0;
+        ExtractArgs b = a;
+        b.first_slot = first + n0;
+        b.pyr_raw += (size_t)n0 * a.frame_pyr_bytes;
+        b.pyr_blur += (size_t)n0 * a.frame_pyr_bytes;
+        b.cell_lists += (size_t)n0 * a.list_entries;
+        b.retain_scratch += (size_t)n0 * (a.list_entries + 4 * a.ncells);
+        b.cell_count += (size_t)n0 * a.ncells;
+        b.level_keys += (size_t)n0 * a.level_entries;
+        b.level_count += (size_t)n0 * a.nlevels;
+        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+        ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+        run(a, n0, ctx->stream);
+        run(b, n1, ctx->stream2);
+        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream2));
+        ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    } else {
+        run(a, count, ctx->stream);
     }
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;

@@ -122,6 +122,9 @@ struct KernelTimer {
 struct orbx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;      // second half of large extraction batches
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool split = true;                  // run large batches as two concurrent halves
     orbx::Geometry geom;
     orbx::DeviceGeometry dgeom;
     int max_w = 0, max_h = 0, slots = 0;
@@ -169,8 +172,8 @@ int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wind
                       float nnratio, int check_ori);
 int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio);
 // timing helpers (orbx_api.cpp)
-void timer_begin(orbx_ctx* ctx, const char* name);
-void timer_end(orbx_ctx* ctx, const char* name);
+void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
+void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 int ensure_scratch(orbx_ctx* ctx, size_t bytes);
 int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 }  // namespace orbx
