@@ -200,21 +200,21 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 // "bright" arc for sgn = -1).
 __device__ inline int fast_arc(const uint8_t* t, int pitch, int sgn)
 {
-    const int v = t[0];
     const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
                          3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
                          -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
                          -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
-    int d[16], m2[16], m4[16];
+    // x_k = sgn * (v - p_k) as one 24-bit multiply-add per ring pixel
+    const int c = sgn * (int)t[0], s = -sgn;
+    int x[16], m3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = sgn * (v - (int)t[off[k]]);
+    for (int k = 0; k < 16; k++) x[k] = (int)t[off[k]] * s + c;
+    // min over 9 consecutive = min of three consecutive 3-minima
 #pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = min(d[k], d[(k + 1) & 15]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
+    for (int k = 0; k < 16; k++) m3[k] = min(min(x[k], x[(k + 1) & 15]), x[(k + 2) & 15]);
     int best = -1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15]));
+    for (int k = 0; k < 16; k++) best = max(best, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
     return best;
 }
 
@@ -227,6 +227,18 @@ __device__ inline int fast_arc(const uint8_t* t, int pitch, int sgn)
 //  3. raster-order compaction of the corners at the chosen threshold.
 // ---------------------------------------------------------------------------
 __device__ inline int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFF); }
+
+// Packed 16-bit lanes (v_pk_sub_i16 / v_pk_max_i16).
+typedef short orbx_s16x2 __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t pk_sub16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, (orbx_s16x2)(__builtin_bit_cast(orbx_s16x2, a) - __builtin_bit_cast(orbx_s16x2, b)));
+}
+__device__ inline uint32_t pk_max16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t,
+                              __builtin_elementwise_max(__builtin_bit_cast(orbx_s16x2, a), __builtin_bit_cast(orbx_s16x2, b)));
+}
 
 // byte k (0..11) of the 12-byte window lo|mid|hi
 __device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
@@ -280,20 +292,39 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             const uint32_t mid = row[0];
             const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
             const uint32_t up = row[-3 * nq], dn = row[3 * nq];
+            // 4 pixels at once: even / odd bytes as two u16x2 halves, packed
+            // 16-bit arithmetic; a lane's sign bit set = "test fails"
+            const uint32_t p4w = __builtin_amdgcn_alignbyte(hi, mid, 3);    // bytes j+3
+            const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
+            const uint32_t T1 = (uint32_t)(tmin + 1) * 0x00010001u;
+            const uint32_t NT1 = (uint32_t)(-(tmin + 1) & 0xFFFF) * 0x00010001u;
+            int ok[2][2];   // [half][dark, bright] sign-bit masks of passing lanes
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int tc = 4 * q + j;
-                if (tc < c_lo || tc > c_hi) continue;
-                const int v = byte_of(mid, j);
-                const int p0 = byte_of(dn, j), p8 = byte_of(up, j);
-                const int p4 = byte12(lo, mid, hi, 4 + j + 3), p12 = byte12(lo, mid, hi, 4 + j - 3);
-                const bool d0 = v - p0 > tmin, d4 = v - p4 > tmin, d8 = v - p8 > tmin, d12 = v - p12 > tmin;
-                const bool b0 = p0 - v > tmin, b4 = p4 - v > tmin, b8 = p8 - v > tmin, b12 = p12 - v > tmin;
-                const bool okd = (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0);
-                const bool okb = (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0);
-                mask |= (okd ? 1 : 0) << (2 * j);
-                mask |= (okb ? 2 : 0) << (2 * j);
+            for (int hf = 0; hf < 2; hf++) {
+                const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;   // bytes 1,3 or 0,2 -> u16x2
+                const uint32_t v = __builtin_amdgcn_perm(0u, mid, sel);
+                const uint32_t pk[4] = {__builtin_amdgcn_perm(0u, dn, sel), __builtin_amdgcn_perm(0u, p4w, sel),
+                                        __builtin_amdgcn_perm(0u, up, sel), __builtin_amdgcn_perm(0u, p12w, sel)};
+                uint32_t xd[4], xb[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t d = pk_sub16(v, pk[k]);     // v - p
+                    xd[k] = pk_sub16(d, T1);                   // >= 0 <=> v - p > t
+                    xb[k] = pk_sub16(NT1, d);                  // >= 0 <=> p - v > t
+                }
+                const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
+                const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
+                ok[hf][0] = (int)(~failD & 0x80008000u);
+                ok[hf][1] = (int)(~failB & 0x80008000u);
             }
+            // pixel j: bit 2j dark, 2j+1 bright (even half: j = 0, 2; odd: 1, 3)
+            mask = ((ok[0][0] >> 15) & 1) | ((ok[0][1] >> 14) & 2) |                          // j = 0
+                   (((ok[1][0] >> 15) & 1) << 2) | (((ok[1][1] >> 14) & 2) << 2) |              // j = 1
+                   (((ok[0][0] >> 31) & 1) << 4) | ((((unsigned)ok[0][1] >> 30) & 2) << 4) |     // j = 2
+                   (((ok[1][0] >> 31) & 1) << 6) | ((((unsigned)ok[1][1] >> 30) & 2) << 6);     // j = 3
+            // interior columns only
+            const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
+            mask = (j1 < j0) ? 0 : (mask & (((1 << (2 * (j1 + 1))) - 1) & ~((1 << (2 * j0)) - 1)));
             sm32[r * nq + q] = 0;
         }
         const int cnt = __popc((mask | (mask >> 1)) & 0x55);
@@ -334,27 +365,32 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         const uint32_t* m = sm32 + r * nq + q;
         const uint32_t mid = m[0];
         if (mid) {
-            uint32_t w3[3][3];
+            // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
+            // rows r-1, r, r+1), byte-wise max on even / odd u16x2 halves
+            uint32_t nb[8];
+            int k = 0;
 #pragma unroll
             for (int dr = 0; dr < 3; dr++) {
                 const uint32_t* mr = m + (dr - 1) * nq;
-                w3[dr][0] = q > 0 ? mr[-1] : 0u;
-                w3[dr][1] = mr[0];
-                w3[dr][2] = q + 1 < nq ? mr[1] : 0u;
+                const uint32_t lo = q > 0 ? mr[-1] : 0u, mm = mr[0], hi = q + 1 < nq ? mr[1] : 0u;
+                nb[k++] = __builtin_amdgcn_alignbyte(mm, lo, 3);   // j-1
+                if (dr != 1) nb[k++] = mm;
+                nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
             }
+            const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int s = byte_of(mid, j);
-                if (s == 0) continue;
-                int mx = max(byte12(w3[1][0], w3[1][1], w3[1][2], 3 + j), byte12(w3[1][0], w3[1][1], w3[1][2], 5 + j));
+            for (int hf = 0; hf < 2; hf++) {
+                const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
+                uint32_t mx = __builtin_amdgcn_perm(0u, nb[0], sel);
 #pragma unroll
-                for (int dr = 0; dr < 3; dr += 2)
-#pragma unroll
-                    for (int dc = 3; dc <= 5; dc++) mx = max(mx, byte12(w3[dr][0], w3[dr][1], w3[dr][2], dc + j));
-                if (s > mx) {
-                    word |= (uint32_t)s << (8 * j);
-                    c1 += s >= a.fast_th;
-                }
+                for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
+                const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
+                // keep where mx - s < 0 (s > every neighbour)
+                const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
+                const uint32_t kept = sv & keep;
+                word |= kept << (8 * hf);
+                // corners at fastTh among the kept (kept >= max(fastTh, 1))
+                c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
             }
         }
         tile32[r * nq + q] = word;
