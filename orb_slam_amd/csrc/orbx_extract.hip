@@ -678,12 +678,31 @@ constexpr int kBrRows = 2 * kBrR + 1;                // 37
 constexpr int kBrPitch = 40;                         // 10 dwords: 37 bytes + alignment
 constexpr int kDescWaveBytes = kIcRows * kIcPitch + kBrRows * kBrPitch;
 
+// Half-wave (32-lane) sums: DPP row shifts inside each 16-lane row, then
+// row_bcast:15 folds row 0 into row 1 and row 2 into row 3; lane 31 holds the
+// lower half's sum, lane 63 the upper half's.
+__device__ inline int half_wave_sum(int v)
+{
+    v += dpp_or0<0x111, 0xf>(v);
+    v += dpp_or0<0x112, 0xf>(v);
+    v += dpp_or0<0x114, 0xf>(v);
+    v += dpp_or0<0x118, 0xf>(v);
+    v += dpp_or0<0x142, 0xa>(v);
+    const int lo = __builtin_amdgcn_readlane(v, 31), hi = __builtin_amdgcn_readlane(v, 63);
+    return (threadIdx.x & 32) ? hi : lo;
+}
+
+// Two keypoints per wave, one per 32-lane half: every per-keypoint scalar
+// step (fastAtan2, the correctly rounded sin/cos) is shared by two
+// keypoints per instruction, and the pattern's 256 tests map onto 8 rounds
+// of 32 lanes (ballot halves = 32 descriptor bits each).
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_patch[kWaves][kDescWaveBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t s_patch[2 * kWaves][kDescWaveBytes];
     const int f = blockIdx.y;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int k = blockIdx.x * kWaves + wv;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+    const int slot = wv * 2 + half;
+    const int k = blockIdx.x * (2 * kWaves) + slot;
     const int32_t* lc = a.level_count + (size_t)f * a.nlevels;
     int total = 0, level = -1, local = 0;
     for (int l = 0; l < a.nlevels; l++) {
@@ -695,12 +714,19 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         total += c;
     }
     if (k == 0 && lane == 0) a.out_n[a.first_slot + f] = total;
-    if (level < 0) return;
+    // a wave keeps running while either half has a keypoint (DPP/ballot need
+    // the whole wave); an empty half works on level 0 / key 0 and stores nothing
+    const bool valid = level >= 0;
+    if (!__any(valid)) return;
+    if (!valid) {
+        level = 0;
+        local = 0;
+    }
     const LevelGeom L = a.levels[level];
     const uint32_t e = a.level_keys[(size_t)f * a.level_entries + L.level_off + local];
     const int score = (int)(e >> 24), y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
-    const int X = kEdge + x, Y = kEdge + y;   // padded coordinates
-    uint8_t* ic = s_patch[wv];
+    const int X = kEdge + (valid ? x : kHalfPatch + 8), Y = kEdge + (valid ? y : kHalfPatch + 8);
+    uint8_t* ic = s_patch[slot];
     uint8_t* br = ic + kIcRows * kIcPitch;
     {
         const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
@@ -708,11 +734,11 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         const int ix0 = (X - kHalfPatch) & ~3, bx0 = (X - kBrR) & ~3;
         uint32_t* ic32 = reinterpret_cast<uint32_t*>(ic);
         uint32_t* br32 = reinterpret_cast<uint32_t*>(br);
-        for (int i = lane; i < kIcRows * (kIcPitch / 4); i += 64) {
+        for (int i = hl; i < kIcRows * (kIcPitch / 4); i += 32) {
             const int r = i / (kIcPitch / 4), q = i - r * (kIcPitch / 4);
             ic32[i] = *reinterpret_cast<const uint32_t*>(raw + (size_t)(Y - kHalfPatch + r) * L.stride + ix0 + 4 * q);
         }
-        for (int i = lane; i < kBrRows * (kBrPitch / 4); i += 64) {
+        for (int i = hl; i < kBrRows * (kBrPitch / 4); i += 32) {
             const int r = i / (kBrPitch / 4), q = i - r * (kBrPitch / 4);
             br32[i] = *reinterpret_cast<const uint32_t*>(blr + (size_t)(Y - kBrR + r) * L.stride + bx0 + 4 * q);
         }
@@ -722,26 +748,23 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151); lanes
-    // 0..30 take rows v = 1..8 and the centre row, lanes 32..62 rows 9..15
+    // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151): lane u
+    // of the half takes column u - 15 over all rows of the circular patch
     int m01 = 0, m10 = 0;
-    {
-        const int u = (lane & 31) - kHalfPatch;
-        if ((lane & 31) < kIcRows) {
-            const int v0 = lane < 32 ? 1 : 9, v1 = lane < 32 ? 8 : kHalfPatch;
-            if (lane < 32) m10 = u * ic[u];
-            for (int v = v0; v <= v1; v++) {
-                const int d = a.umax[v];
-                if (u >= -d && u <= d) {
-                    const int vp = ic[u + v * kIcPitch], vm = ic[u - v * kIcPitch];
-                    m01 += v * (vp - vm);
-                    m10 += u * (vp + vm);
-                }
+    if (hl < kIcRows) {
+        const int u = hl - kHalfPatch;
+        m10 = u * ic[u];
+        for (int v = 1; v <= kHalfPatch; v++) {
+            const int d = a.umax[v];
+            if (u >= -d && u <= d) {
+                const int vp = ic[u + v * kIcPitch], vm = ic[u - v * kIcPitch];
+                m01 += v * (vp - vm);
+                m10 += u * (vp + vm);
             }
         }
     }
-    m01 = wave_sum(m01);
-    m10 = wave_sum(m10);
+    m01 = half_wave_sum(m01);
+    m10 = half_wave_sum(m10);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
     // computeOrbDescriptor on the blurred level (src/ORBextractor.cc:155-194)
     const float factorPI = (float)(M_PI / 180.f);
@@ -749,8 +772,8 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     cr_sincosf(__fmul_rn(angle, factorPI), &sa, &ca);
     uint8_t* desc = a.out_desc + ((size_t)(a.first_slot + f) * a.nfeatures + k) * 32;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int q = r * 64 + lane;
+    for (int r = 0; r < 8; r++) {
+        const int q = r * 32 + hl;
         const float px1 = c_pattern[q][0], py1 = c_pattern[q][1];
         const float px2 = c_pattern[q][2], py2 = c_pattern[q][3];
         const int t0 = br[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * kBrPitch +
@@ -758,9 +781,10 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         const int t1 = br[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * kBrPitch +
                           cv_round(__fsub_rn(__fmul_rn(px2, ca), __fmul_rn(py2, sa)))];
         const unsigned long long bits = __ballot(t0 < t1);
-        if (lane == r) *reinterpret_cast<unsigned long long*>(desc + 8 * r) = bits;
+        // this half's 32 bits are descriptor bits 32r .. 32r+31 (bytes 4r .. 4r+3)
+        if (valid && hl == r) reinterpret_cast<uint32_t*>(desc)[r] = (uint32_t)(bits >> (32 * half));
     }
-    if (lane == 0) {
+    if (valid && hl == 0) {
         orbx_keypoint kp;
         kp.x = (float)x;
         kp.y = (float)y;
@@ -854,7 +878,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
         timer_end(ctx, "blur", st);
         timer_begin(ctx, "describe", st);
-        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + kWaves - 1) / kWaves, nb), dim3(256), 0, st, x);
+        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), nb), dim3(256), 0, st, x);
         timer_end(ctx, "describe", st);
     };
     // Work buffers are indexed by batch position (frame f of a pass uses
