@@ -146,6 +146,12 @@ def run_frames(args, wl, rank, local, world, dist):
     ctx.upload(frames)
 
     def step():
+        if args.pipelined:
+            # matching of each half-batch overlapped with the other half's
+            # extraction; pairs straddling the halves after the join
+            ctx.extract_match(0, B, B, mode="bf" if bf else "init", window=100, th_low=50, nnratio=0.9,
+                              check_ori=True)
+            return
         ctx.extract(0, B)
         if bf:
             ctx.match_bf_prev(0, B, B, th_low=50, nnratio=0.9)
@@ -257,6 +263,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="overlap each half-batch's matching with the other half's extraction")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()

@@ -112,6 +112,13 @@ int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
  * before the call's later work) unless disabled with orbx_dev_set_split. */
 int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
 int orbx_dev_set_split(orbx_ctx* ctx, int enable);
+/* orbx_dev_extract followed by matching every slot of the batch against its
+ * predecessor (mode 1: orbx_dev_match_prev with window / nnratio / check_ori;
+ * mode 2: orbx_dev_match_bf_prev with th_low / nnratio), pipelined: with the
+ * two-stream split each half's internal pairs are matched while the other
+ * half is still being extracted.  Results as for the separate calls. */
+int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int mode,
+                           int window, int th_low, float nnratio, int check_ori);
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */

@@ -72,6 +72,7 @@ def _declare(L):
         "orbx_dev_sync": ([vp], i),
         "orbx_dev_match_bf_prev": ([vp, i, i, i, i, f], i),
         "orbx_dev_set_split": ([vp, i], i),
+        "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
         "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
         "orbx_dev_kernel_time": ([vp, ctypes.c_char_p, dp, dp], i),
@@ -171,6 +172,13 @@ class Context:
     def match_prev(self, first, count, seq_len, window=100, nnratio=0.9, check_ori=True):
         _check(lib().orbx_dev_match_prev(self._h, first, count, seq_len, window, nnratio,
                                          int(check_ori)), "orbx_dev_match_prev")
+
+    def extract_match(self, first, count, seq_len, mode="init", window=100, th_low=50, nnratio=0.9,
+                      check_ori=True):
+        """Extract a batch and match each frame against its predecessor
+        (mode "init": SearchForInitialization, "bf": brute force), pipelined."""
+        _check(lib().orbx_dev_extract_match(self._h, first, count, seq_len, 1 if mode == "init" else 2, window,
+                                            th_low, nnratio, int(check_ori)), "orbx_dev_extract_match")
 
     def set_split(self, enable):
         """Two concurrent half-batch streams for large extraction batches."""

@@ -37,19 +37,24 @@ def _needs(obj, src, headers):
     return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
 
 
-def build(verbose=False, jobs=None):
+def build(verbose=False, jobs=None, defines=(), lib=None):
+    """defines: extra -D flags for an instrumented variant (e.g.
+    ORBX_MATCH_PROFILE); such a variant is linked to `lib` with its own
+    object directory and loaded through ORBX_LIBRARY."""
     cc = hipcc()
-    OBJ.mkdir(exist_ok=True)
+    obj_dir = OBJ if not defines else OBJ.parent / ("build_" + "_".join(d.lower() for d in defines))
+    out = Path(lib) if lib else LIB
+    obj_dir.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) + [PKG.parent / "include" / "orbx.h"]
     srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
     cmds = []
     objs = []
     for s in srcs:
-        o = OBJ / (s.name + ".o")
+        o = obj_dir / (s.name + ".o")
         objs.append(o)
         if _needs(o, s, headers):
             lang = ["-x", "hip", f"--offload-arch={ARCH}"] if s.suffix == ".hip" else ["-D__HIP_PLATFORM_AMD__"]
-            cmds.append([cc, *lang, *COMMON, "-c", str(s), "-o", str(o)])
+            cmds.append([cc, *lang, *COMMON, *(f"-D{d}" for d in defines), "-c", str(s), "-o", str(o)])
 
     def run(cmd):
         if verbose:
@@ -63,9 +68,11 @@ def build(verbose=False, jobs=None):
         for err in ex.map(run, cmds):
             if err and verbose:
                 print(err, file=sys.stderr)
-    if cmds or not LIB.exists():
-        link = [cc, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(LIB), *map(str, objs)]
+    if cmds or not out.exists():
+        link = [cc, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(out), *map(str, objs)]
         run(link)
+    if defines:
+        return out
     # C++ adapter demo (the reference-style C++ binding)
     demo_src = PKG / "adapters" / "adapter_demo.cpp"
     demo = PKG / "adapters" / "adapter_demo"
@@ -77,4 +84,6 @@ def build(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
+    outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
+    print(build(verbose="-v" in sys.argv, defines=defs, lib=outs[0] if outs else None))

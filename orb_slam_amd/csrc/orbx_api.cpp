@@ -294,6 +294,22 @@ int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wi
     return launch_match_prev(ctx, first, count, seq_len, window, nnratio, check_ori);
 }
 
+int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int mode, int window, int th_low,
+                           float nnratio, int check_ori)
+{
+    if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || seq_len <= 0 || window < 0 ||
+        (mode != 1 && mode != 2))
+        return ORBX_ERR_ARG;
+    if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
+    if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
+    if (ctx->geom_w <= 0) return ORBX_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    ctx->last_first = first;
+    ctx->last_count = count;
+    MatchSpec m{mode, seq_len, window, th_low, check_ori, nnratio};
+    return launch_extract(ctx, first, count, &m);
+}
+
 int orbx_dev_set_split(orbx_ctx* ctx, int enable)
 {
     if (!ctx) return ORBX_ERR_ARG;

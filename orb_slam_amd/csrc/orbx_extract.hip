@@ -25,8 +25,9 @@ namespace orbx {
 constexpr size_t kRetainLds = 128 * 1024;   // LDS budget of a retain block
 constexpr int kRetainCellCap = 1024;        // cell lists up to this length sort in LDS
 constexpr int kSplitMinFrames = 16;         // batches >= 2x this run as two concurrent halves
+constexpr size_t kResizeLds = 96 * 1024;    // LDS budget of a staged resize strip
 
-__constant__ int8_t c_pattern[256][4] = {
+__constant__ __attribute__((aligned(4))) int8_t c_pattern[256][4] = {
 #include "orbx_pattern.inc"
 };
 
@@ -93,45 +94,84 @@ struct RowWalk {
 };
 
 
-// ---------------------------------------------------------------------------
-// Level 0: padded copy with BORDER_REFLECT_101.  4 output bytes per thread.
-// ---------------------------------------------------------------------------
-// One thread per (dword column, strip of kPyrRows rows): the column's
-// reflected source offsets are computed once and the strip's independent
-// row loads are in flight together.
-constexpr int kPyrRows = 8;
+// Copy n items into LDS, kBatch per thread per round: the loads are
+// unconditional (index clamped to n - 1, whose entry out-of-range lanes
+// rewrite with its own value), so no branch separates them and all kBatch
+// are in flight before the first wait.
+template <int kBatch, typename T, typename Load>
+__device__ inline void stage_to_lds(T* dst, int n, int tid, int nthr, Load load)
+{
+    for (int u0 = 0; u0 < n; u0 += kBatch * nthr) {
+        T v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) v[k] = load(min(u0 + k * nthr + tid, n - 1));
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) dst[min(u0 + k * nthr + tid, n - 1)] = v[k];
+    }
+}
 
-__global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a)
+// ---------------------------------------------------------------------------
+// Level 0: padded copy with BORDER_REFLECT_101.  16 output bytes per thread
+// and row: interior words are two aligned 16-byte loads funnel-shifted by
+// the border offset; words touching the border gather reflected bytes.
+// ---------------------------------------------------------------------------
+// One thread per (16-byte column, strip of kPyrRows rows): the strip's
+// independent row loads are in flight together.
+constexpr int kPyrRows = 8;
+constexpr int kPyr0Shift = (16 - kEdge % 16) % 16;   // (16q - kEdge) mod 16
+
+// Work items: first the interior words (q_lo .. q_lo + nint - 1) in strips of
+// kPyrRows rows, then the border words one (word, row) each, so border
+// gathers run in waves of their own.
+__global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a, int q_lo, int nint)
 {
     const int f = blockIdx.y;
     const LevelGeom L = a.levels[0];
-    const int wpr = L.stride >> 2, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= wpr * nstrips) return;
-    const int strip = idx / wpr, q = idx - strip * wpr, px0 = 4 * q;
+    const int qpr = L.stride >> 4, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
+    const int nbord = qpr - nint;
+    int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t* src = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
     uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
-    const bool aligned = (px0 - kEdge) >= 0 && (px0 - kEdge + 3) < L.w && (a.w & 3) == 0;
-    int sx[4];
+    if (idx < nint * nstrips) {
+        const int strip = idx / nint, q = q_lo + (idx - strip * nint), px0 = 16 * q;
+        const int al = px0 - kEdge - kPyr0Shift;   // 16-byte aligned source column
+        const int py_first = strip * kPyrRows;
+        // all the strip's loads first (rows past the level repeat the last
+        // one, their stores are skipped), then the funnel shifts and stores
+        uint4 lo[kPyrRows], hi[kPyrRows];
 #pragma unroll
-    for (int b = 0; b < 4; b++) sx[b] = (px0 + b < L.pw) ? reflect101(px0 + b - kEdge, L.w) : -1;
-#pragma unroll
-    for (int rr = 0; rr < kPyrRows; rr++) {
-        // rows past the level repeat the last one (loads stay in bounds and
-        // can all be issued up front); their stores are skipped
-        const int py = min(strip * kPyrRows + rr, L.ph - 1);
-        const uint8_t* row = src + (size_t)reflect101(py - kEdge, L.h) * a.w;
-        uint32_t word;
-        if (aligned) {
-            word = *reinterpret_cast<const uint32_t*>(row + px0 - kEdge);
-        } else {
-            word = 0;
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                if (sx[b] >= 0) word |= (uint32_t)row[sx[b]] << (8 * b);
+        for (int rr = 0; rr < kPyrRows; rr++) {
+            const int py = min(py_first + rr, L.ph - 1);
+            const uint8_t* row = src + (size_t)reflect101(py - kEdge, L.h) * a.w + al;
+            lo[rr] = *reinterpret_cast<const uint4*>(row);
+            hi[rr] = *reinterpret_cast<const uint4*>(row + 16);
         }
-        if (strip * kPyrRows + rr < L.ph) *reinterpret_cast<uint32_t*>(dst + (size_t)py * L.stride + px0) = word;
+#pragma unroll
+        for (int rr = 0; rr < kPyrRows; rr++) {
+            const uint32_t w[8] = {lo[rr].x, lo[rr].y, lo[rr].z, lo[rr].w, hi[rr].x, hi[rr].y, hi[rr].z, hi[rr].w};
+            constexpr int d = kPyr0Shift >> 2, b = kPyr0Shift & 3;
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                o[k] = b ? __builtin_amdgcn_alignbyte(w[k + d + 1], w[k + d], b) : w[k + d];
+            if (py_first + rr < L.ph)
+                *reinterpret_cast<uint4*>(dst + (size_t)(py_first + rr) * L.stride + px0) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        return;
     }
+    idx -= nint * nstrips;
+    if (idx >= nbord * L.ph) return;
+    const int py = idx / nbord, k = idx - py * nbord;
+    const int q = k < q_lo ? k : k + nint, px0 = 16 * q;
+    const uint8_t* row = src + (size_t)reflect101(py - kEdge, L.h) * a.w;
+    uint8_t v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = px0 + i < L.pw ? row[reflect101(px0 + i - kEdge, L.w)] : 0;
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        o[i] = v[4 * i] | (uint32_t)v[4 * i + 1] << 8 | (uint32_t)v[4 * i + 2] << 16 | (uint32_t)v[4 * i + 3] << 24;
+    *reinterpret_cast<uint4*>(dst + (size_t)py * L.stride + px0) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -185,6 +225,134 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
         for (int b = 0; b < 4; b++)
             if (on[b]) word |= (uint32_t)resize_pixel(prev, P.stride, c[b], r, vec[b]) << (8 * b);
         if (strip * kPyrRows + rr < L.ph) *reinterpret_cast<uint32_t*>(dst + (size_t)py * L.stride + px0) = word;
+    }
+}
+
+// The same resize with the strip's source rows staged in LDS: one
+// workgroup per (strip of kResRows output rows, frame).  The previous
+// level's rows [lo, hi] feeding the strip are copied with 16-byte loads
+// (padded columns 0 .. kEdge + P.w), together with the level's column and
+// row tables; every output pixel then reads its 2x2 sources from LDS.
+// The host guarantees hi - lo + 1 <= L.res_span (computed from the tables).
+__global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, int level, int pitch)
+{
+    extern __shared__ uint4 s_dyn[];
+    __shared__ ResizeRow s_rows[kResRows];
+    __shared__ int s_lo;
+    const int f = blockIdx.y, tid = threadIdx.x;
+    const LevelGeom L = a.levels[level];
+    const LevelGeom P = a.levels[level - 1];
+    const int py0 = blockIdx.x * kResRows, nrows = min(kResRows, L.ph - py0);
+    const int nch = pitch >> 4;
+    ResizeCol* s_cols = reinterpret_cast<ResizeCol*>(s_dyn + (size_t)L.res_span * nch);
+    uint8_t* s_src = reinterpret_cast<uint8_t*>(s_dyn);
+    if (tid < 64) {
+        int lo = 0x7fffffff;
+        if (tid < nrows) {
+            const ResizeRow r = a.res_rows[L.res_row_off + reflect101(py0 + tid - kEdge, L.h)];
+            s_rows[tid] = r;
+            lo = min(r.sy0, r.sy1);
+        }
+        lo = -wave_max(-lo);
+        if (tid == 0) s_lo = lo;
+    }
+    stage_to_lds<4>(s_cols, L.w, tid, (int)blockDim.x, [&](int x) { return a.res_cols[L.res_col_off + x]; });
+    __syncthreads();
+    const int lo = s_lo;
+    const int nsrc = min(L.res_span, P.h - lo);
+    const uint8_t* pbase = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + P.off + (size_t)(lo + kEdge) * P.stride;
+#ifndef RES_NO_STAGE
+    stage_to_lds<8>(s_dyn, nsrc * nch, tid, (int)blockDim.x, [&](int u) {
+        const int r = u / nch, c = u - r * nch;
+        return *reinterpret_cast<const uint4*>(pbase + (size_t)r * P.stride + 16 * c);
+    });
+#endif
+    __syncthreads();
+    uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py0 * L.stride;
+    // One thread per 4-pixel output word, sliding down the strip's rows.
+    // Its four columns' LDS offsets and weights are fixed; the horizontal
+    // sums of a source row are computed once and reused by the next output
+    // row when it shares the row (rows are uniform across the block).
+    // sx1 is sx0 + 1, or sx0 with a1 = 0 (HResizeLinear tail), so the
+    // second tap is always read at offset +1.
+#ifdef RES_NO_COMPUTE
+    if (tid < 64) reinterpret_cast<uint32_t*>(dst)[tid] = s_src[tid * 7];
+    return;
+#endif
+    for (int q = tid; q < (L.stride >> 2); q += blockDim.x) {
+        const int px0 = 4 * q;
+        int ca[4], a0[4], a1[4];
+        bool vb[4], vec = true;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const bool on = px0 + b < L.pw;
+            const int x = on ? reflect101(px0 + b - kEdge, L.w) : 0;
+            const ResizeCol c = s_cols[x];
+            ca[b] = kEdge + c.sx0;
+            a0[b] = on ? c.a0 : 0;
+            a1[b] = on ? c.a1 : 0;
+            vb[b] = x < L.nvec_resize;
+            vec = vec && (!on || vb[b]);
+        }
+        auto hrow = [&](int sy, int (&S)[4]) {
+            const uint8_t* base = s_src + (sy - lo) * pitch;
+#pragma unroll
+            for (int b = 0; b < 4; b++) S[b] = base[ca[b]] * a0[b] + base[ca[b] + 1] * a1[b];
+        };
+        int H0[4], H1[4], c0 = -1, c1 = -1;
+        for (int rr = 0; rr < nrows; rr++) {
+            const int sy0 = __builtin_amdgcn_readfirstlane(s_rows[rr].sy0);
+            const int sy1 = __builtin_amdgcn_readfirstlane(s_rows[rr].sy1);
+            const int b0 = __builtin_amdgcn_readfirstlane(s_rows[rr].b0);
+            const int b1 = __builtin_amdgcn_readfirstlane(s_rows[rr].b1);
+            int A[4], B[4];
+            if (sy0 == c1) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) A[b] = H1[b];
+            } else if (sy0 == c0) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) A[b] = H0[b];
+            } else {
+                hrow(sy0, A);
+            }
+            if (sy1 == sy0) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) B[b] = A[b];
+            } else if (sy1 == c1) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) B[b] = H1[b];
+            } else {
+                hrow(sy1, B);
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                H0[b] = A[b];
+                H1[b] = B[b];
+            }
+            c0 = sy0;
+            c1 = sy1;
+            uint32_t word = 0;
+            if (vec) {
+                // VResizeLinearVec_32s8u; S >> 4 <= 32640 and the weights are
+                // <= 2048, so none of its 16-bit saturations can trigger
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
+                    word |= (uint32_t)min(v, 255) << (8 * b);
+                }
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    int v;
+                    if (vb[b])
+                        v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
+                    else   // FixedPtCast<int, uchar, 22>
+                        v = (A[b] * b0 + B[b] * b1 + (1 << 21)) >> 22;
+                    word |= (uint32_t)sat_u8(v) << (8 * b);
+                }
+            }
+            *reinterpret_cast<uint32_t*>(dst + (size_t)rr * L.stride + px0) = word;
+        }
     }
 }
 
@@ -267,11 +435,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     uint8_t* sm = smem + tile_pitch_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
-    {
-        RowWalk w(tid, kBlock, nq);
-        for (int i = tid; i < hy * nq; i += kBlock, w.next())
-            tile32[i] = *reinterpret_cast<const uint32_t*>(src + (size_t)w.r * L.stride + 4 * w.q);
-    }
+    stage_to_lds<8>(tile32, hy * nq, tid, kBlock, [&](int i) {
+        const int r = i / nq;
+        return *reinterpret_cast<const uint32_t*>(src + (size_t)r * L.stride + 4 * (i - r * nq));
+    });
     // S' is 0 outside the interior rows [3, hy-4]; the interior rows are
     // fully rewritten below
     for (int i = tid; i < nq; i += kBlock) {
@@ -622,46 +789,86 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
 #pragma unroll
     for (int j = 0; j < 4; j++)
         if (x + j < L.pw) keep_mask |= 0xFFu << (8 * j);
-    for (int y = y0; y < min(ya, y1); y++)
-        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) =
-            *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x) & keep_mask;
+    // copied (border) rows, 4 loads in flight per round
+    auto copy_rows = [&](int ylo, int yhi) {
+        for (int yc = ylo; yc < yhi; yc += 4) {
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)min(yc + k, yhi - 1) * L.stride + x);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (yc + k < yhi) *reinterpret_cast<uint32_t*>(dst + (size_t)(yc + k) * L.stride + x) = v[k] & keep_mask;
+        }
+    };
+    copy_rows(y0, min(ya, y1));
     if (ya < yb) {
         int R[7][4];
 #pragma unroll
         for (int k = 0; k < 6; k++) blur_hsum(src + (size_t)(ya - 3 + k) * L.stride, x, R[k]);
-        for (int y = ya; y < yb; y++) {
-            blur_hsum(src + (size_t)(y + 3) * L.stride, x, R[6]);
-            const uint32_t raw = *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x);
-            uint32_t word = 0;
+        // chunks of kBlurChunk output rows: the chunk's input rows (y + 3) and
+        // raw centre words are loaded together, then filtered from registers
+        constexpr int kBlurChunk = 8;
+        for (int yc = ya; yc < yb; yc += kBlurChunk) {
+            uint32_t wl[kBlurChunk], wc[kBlurChunk], wr[kBlurChunk], raw[kBlurChunk];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int xi = x + j - kEdge;
-                uint32_t v = (raw >> (8 * j)) & 0xFF;
-                if (xi >= 0 && xi < L.w) {
-                    const int N = 55 * R[3][j] + 49 * (R[2][j] + R[4][j]) + 34 * (R[1][j] + R[5][j]) +
-                                  18 * (R[0][j] + R[6][j]);
-                    int q;
-                    if (xi < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
-                        q = N >> 16;
-                        const int rem = N & 0xFFFF;
-                        if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
-                    } else {
-                        q = (N + (1 << 15)) >> 16;
-                    }
-                    v = (uint32_t)sat_u8(q);
-                }
-                word |= v << (8 * j);
+            for (int k = 0; k < kBlurChunk; k++) {
+                // rows past yb + 2 repeat the last one (never used)
+                const int yy = min(yc + k, yb - 1);
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + (size_t)(yy + 3) * L.stride + x);
+                wl[k] = w[-1];
+                wc[k] = w[0];
+                wr[k] = w[1];
+                raw[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)yy * L.stride + x);
             }
-            *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) = word & keep_mask;
 #pragma unroll
-            for (int k = 0; k < 6; k++)
+            for (int k = 0; k < kBlurChunk; k++) {
+                const int y = yc + k;
+                if (y >= yb) break;
+                {
+                    int b[12];
 #pragma unroll
-                for (int j = 0; j < 4; j++) R[k][j] = R[k + 1][j];
+                    for (int j = 0; j < 4; j++) {
+                        b[j] = (wl[k] >> (8 * j)) & 0xFF;
+                        b[4 + j] = (wc[k] >> (8 * j)) & 0xFF;
+                        b[8 + j] = (wr[k] >> (8 * j)) & 0xFF;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int c = 4 + j;
+                        R[6][j] = 55 * b[c] + 49 * (b[c - 1] + b[c + 1]) + 34 * (b[c - 2] + b[c + 2]) +
+                                  18 * (b[c - 3] + b[c + 3]);
+                    }
+                }
+                uint32_t word = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int xi = x + j - kEdge;
+                    uint32_t v = (raw[k] >> (8 * j)) & 0xFF;
+                    if (xi >= 0 && xi < L.w) {
+                        const int N = 55 * R[3][j] + 49 * (R[2][j] + R[4][j]) + 34 * (R[1][j] + R[5][j]) +
+                                      18 * (R[0][j] + R[6][j]);
+                        int q;
+                        if (xi < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
+                            q = N >> 16;
+                            const int rem = N & 0xFFFF;
+                            if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
+                        } else {
+                            q = (N + (1 << 15)) >> 16;
+                        }
+                        v = (uint32_t)sat_u8(q);
+                    }
+                    word |= v << (8 * j);
+                }
+                *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) = word & keep_mask;
+#pragma unroll
+                for (int kk = 0; kk < 6; kk++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) R[kk][j] = R[kk + 1][j];
+            }
         }
     }
-    for (int y = max(yb, ya); y < y1; y++)
-        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) =
-            *reinterpret_cast<const uint32_t*>(src + (size_t)y * L.stride + x) & keep_mask;
+    copy_rows(max(yb, ya), y1);
 }
 
 // ---------------------------------------------------------------------------
@@ -703,6 +910,12 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
     const int slot = wv * 2 + half;
     const int k = blockIdx.x * (2 * kWaves) + slot;
+    // tables needed later, loaded up front (independent of the keypoint):
+    // umax[0..15] one entry per lane, this lane's 8 pattern pairs
+    const int umax_l = a.umax[min(lane, kHalfPatch)];
+    uint32_t pat[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) pat[r] = *reinterpret_cast<const uint32_t*>(c_pattern[r * 32 + hl]);
     const int32_t* lc = a.level_count + (size_t)f * a.nlevels;
     int total = 0, level = -1, local = 0;
     for (int l = 0; l < a.nlevels; l++) {
@@ -734,14 +947,23 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         const int ix0 = (X - kHalfPatch) & ~3, bx0 = (X - kBrR) & ~3;
         uint32_t* ic32 = reinterpret_cast<uint32_t*>(ic);
         uint32_t* br32 = reinterpret_cast<uint32_t*>(br);
-        for (int i = hl; i < kIcRows * (kIcPitch / 4); i += 32) {
-            const int r = i / (kIcPitch / 4), q = i - r * (kIcPitch / 4);
-            ic32[i] = *reinterpret_cast<const uint32_t*>(raw + (size_t)(Y - kHalfPatch + r) * L.stride + ix0 + 4 * q);
+        // both patches' loads (9 + 12 per lane) in flight together
+        constexpr int nic = kIcRows * (kIcPitch / 4), nbr = kBrRows * (kBrPitch / 4);
+        uint32_t vi[(nic + 31) / 32], vb[(nbr + 31) / 32];
+#pragma unroll
+        for (int k = 0; k < (nic + 31) / 32; k++) {
+            const int i = min(hl + 32 * k, nic - 1), r = i / (kIcPitch / 4), q = i - r * (kIcPitch / 4);
+            vi[k] = *reinterpret_cast<const uint32_t*>(raw + (size_t)(Y - kHalfPatch + r) * L.stride + ix0 + 4 * q);
         }
-        for (int i = hl; i < kBrRows * (kBrPitch / 4); i += 32) {
-            const int r = i / (kBrPitch / 4), q = i - r * (kBrPitch / 4);
-            br32[i] = *reinterpret_cast<const uint32_t*>(blr + (size_t)(Y - kBrR + r) * L.stride + bx0 + 4 * q);
+#pragma unroll
+        for (int k = 0; k < (nbr + 31) / 32; k++) {
+            const int i = min(hl + 32 * k, nbr - 1), r = i / (kBrPitch / 4), q = i - r * (kBrPitch / 4);
+            vb[k] = *reinterpret_cast<const uint32_t*>(blr + (size_t)(Y - kBrR + r) * L.stride + bx0 + 4 * q);
         }
+#pragma unroll
+        for (int k = 0; k < (nic + 31) / 32; k++) ic32[min(hl + 32 * k, nic - 1)] = vi[k];
+#pragma unroll
+        for (int k = 0; k < (nbr + 31) / 32; k++) br32[min(hl + 32 * k, nbr - 1)] = vb[k];
         ic += (X - kHalfPatch) - ix0 + kHalfPatch * kIcPitch + kHalfPatch;   // -> patch center
         br += (X - kBrR) - bx0 + kBrR * kBrPitch + kBrR;
     }
@@ -751,11 +973,13 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     // IC_Angle on the unblurred level (src/ORBextractor.cc:124-151): lane u
     // of the half takes column u - 15 over all rows of the circular patch
     int m01 = 0, m10 = 0;
+    // umax read back from the lanes with readlane: no table loads in the loop
     if (hl < kIcRows) {
         const int u = hl - kHalfPatch;
         m10 = u * ic[u];
+#pragma unroll
         for (int v = 1; v <= kHalfPatch; v++) {
-            const int d = a.umax[v];
+            const int d = __builtin_amdgcn_readlane(umax_l, v);
             if (u >= -d && u <= d) {
                 const int vp = ic[u + v * kIcPitch], vm = ic[u - v * kIcPitch];
                 m01 += v * (vp - vm);
@@ -773,9 +997,8 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     uint8_t* desc = a.out_desc + ((size_t)(a.first_slot + f) * a.nfeatures + k) * 32;
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const int q = r * 32 + hl;
-        const float px1 = c_pattern[q][0], py1 = c_pattern[q][1];
-        const float px2 = c_pattern[q][2], py2 = c_pattern[q][3];
+        const float px1 = (float)(int8_t)(pat[r] & 0xFF), py1 = (float)(int8_t)((pat[r] >> 8) & 0xFF);
+        const float px2 = (float)(int8_t)((pat[r] >> 16) & 0xFF), py2 = (float)(int8_t)(pat[r] >> 24);
         const int t0 = br[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * kBrPitch +
                           cv_round(__fsub_rn(__fmul_rn(px1, ca), __fmul_rn(py1, sa)))];
         const int t1 = br[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * kBrPitch +
@@ -804,7 +1027,7 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
 // ---------------------------------------------------------------------------
 // Host launcher
 // ---------------------------------------------------------------------------
-int launch_extract(orbx_ctx* ctx, int first, int count)
+int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
 {
     const Geometry& g = ctx->geom;
     ExtractArgs a;
@@ -843,15 +1066,31 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         timer_begin(ctx, "pyr0", st);
         {
             const LevelGeom& L = g.levels[0];
-            const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
-            hipLaunchKernelGGL(k_pyr_level0, dim3((items + 255) / 256, nb), dim3(256), 0, st, x);
+            // interior 16-byte words: two aligned source loads cover them
+            // (frames rows are 16-byte aligned when w % 16 == 0)
+            const int qpr = L.stride / 16;
+            int q_lo = (kEdge + 15) / 16, q_hi = (L.w + kEdge + kPyr0Shift - 32) / 16;
+            q_hi = std::min(q_hi, qpr - 1);
+            const int nint = (g.w % 16 == 0 && q_hi >= q_lo) ? q_hi - q_lo + 1 : 0;
+            if (nint == 0) q_lo = 0;
+            const int items = nint * ((L.ph + kPyrRows - 1) / kPyrRows) + (qpr - nint) * L.ph;
+            hipLaunchKernelGGL(k_pyr_level0, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, q_lo, nint);
         }
         timer_end(ctx, "pyr0", st);
         for (int l = 1; l < g.nlevels; l++) {
             const LevelGeom& L = g.levels[l];
-            const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
+            const LevelGeom& P = g.levels[l - 1];
+            const int pitch = (kEdge + P.w + 15) & ~15;
+            const size_t lds = (size_t)L.res_span * pitch + (size_t)L.w * sizeof(ResizeCol);
             timer_begin(ctx, "resize", st);
-            hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, l);
+            if (lds <= kResizeLds) {
+                const int threads = std::min(256, ((L.stride / 4) + 63) & ~63);
+                hipLaunchKernelGGL(k_pyr_resize_lds, dim3((L.ph + kResRows - 1) / kResRows, nb), dim3(threads), lds, st,
+                                   x, l, pitch);
+            } else {   // very wide levels: per-pixel gathers from global memory
+                const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
+                hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, l);
+            }
             timer_end(ctx, "resize", st);
         }
         timer_begin(ctx, "fast", st);
@@ -885,6 +1124,37 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
     // work slot f); the frame store and outputs by slot.  Large batches run
     // as two halves on two streams so that the VALU-bound FAST pass of one
     // half overlaps the latency-bound passes of the other.
+    // Matching of slot s against prev(s) (the rule of orbx_dev_match_prev),
+    // for the slots of [lo, hi) whose predecessor lies in [plo, phi) (all of
+    // them when phi < 0), launched as contiguous runs on stream st.
+    int err = ORBX_OK;
+    auto match_runs = [&](int lo, int hi, int plo, int phi, hipStream_t st) {
+        if (!m || m->kind == 0) return;
+        auto prev = [&](int sl) { return (sl % m->seq_len == 0) ? sl + m->seq_len - 1 : sl - 1; };
+        auto take = [&](int sl) {
+            const int p = prev(sl);
+            return phi < 0 || (p >= plo && p < phi);
+        };
+        for (int s0 = lo; s0 < hi;) {
+            if (!take(s0)) {
+                s0++;
+                continue;
+            }
+            int s1 = s0 + 1;
+            while (s1 < hi && take(s1)) s1++;
+            const int r = m->kind == 1 ? launch_match_prev(ctx, s0, s1 - s0, m->seq_len, m->window, m->nnratio,
+                                                           m->check_ori, st)
+                                       : launch_match_bf_prev(ctx, s0, s1 - s0, m->seq_len, m->th_low, m->nnratio, st);
+            if (r != ORBX_OK) err = r;
+            s0 = s1;
+        }
+    };
+    // Work buffers are indexed by batch position (frame f of a pass uses
+    // work slot f); the frame store and outputs by slot.  Large batches run
+    // as two halves on two streams so that the VALU-bound FAST pass of one
+    // half overlaps the latency-bound passes of the other; each half's
+    // internal frame pairs are matched on its own stream, the pairs that
+    // straddle the halves after the join.
     a.first_slot = first;
     if (ctx->split && count >= 2 * kSplitMinFrames && ctx->stream2) {
         const int n0 = count / 2, n1 = count - n0;
@@ -900,12 +1170,22 @@ int launch_extract(orbx_ctx* ctx, int first, int count)
         ORBX_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
         ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
         run(a, n0, ctx->stream);
+        match_runs(first, first + n0, first, first + n0, ctx->stream);
         run(b, n1, ctx->stream2);
+        match_runs(first + n0, first + count, first + n0, first + count, ctx->stream2);
         ORBX_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream2));
         ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+        // straddling pairs (predecessor in the other half, or outside the batch)
+        match_runs(first, first + n0, first + n0, 0x7fffffff, ctx->stream);
+        match_runs(first, first + n0, -0x7fffffff, first, ctx->stream);
+        match_runs(first + n0, first + count, first, first + n0, ctx->stream);
+        match_runs(first + n0, first + count, first + count, 0x7fffffff, ctx->stream);
+        match_runs(first + n0, first + count, -0x7fffffff, first, ctx->stream);
     } else {
         run(a, count, ctx->stream);
+        match_runs(first, first + count, 0, -1, ctx->stream);
     }
+    if (err != ORBX_OK) return err;
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
 }

@@ -21,6 +21,12 @@ namespace orbx {
 namespace {
 inline int cv_round(double v) { return (int)std::nearbyint(v); }
 inline int cv_floor(double v) { int i = (int)v; return i - (i > v); }
+inline int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
 inline int16_t sat16(int v) { return (int16_t)std::min(32767, std::max(-32768, v)); }
 
 int vec_count(int width, bool strict4)
@@ -156,9 +162,20 @@ int compute_geometry(Geometry& g, int w, int h)
         while (g.res_cols.size() % 4) g.res_cols.push_back(ResizeCol{0, 0, 0, 0});   // 32-byte aligned runs
         L.res_col_off = (int)g.res_cols.size();
         L.res_row_off = (int)g.res_rows.size();
+        L.res_span = 0;
         if (l > 0) {
             const int r = resize_tables(g, g.levels[l - 1].w, g.levels[l - 1].h, L.w, L.h);
             if (r != ORBX_OK) return r;
+            // source rows feeding each strip of kResRows padded output rows
+            for (int py0 = 0; py0 < L.ph; py0 += kResRows) {
+                int lo = 1 << 30, hi = -1;
+                for (int py = py0; py < std::min(py0 + kResRows, L.ph); py++) {
+                    const ResizeRow& rr = g.res_rows[L.res_row_off + reflect101(py - kEdge, L.h)];
+                    lo = std::min(lo, (int)std::min(rr.sy0, rr.sy1));
+                    hi = std::max(hi, (int)std::max(rr.sy0, rr.sy1));
+                }
+                L.res_span = std::max(L.res_span, hi - lo + 1);
+            }
         }
     }
     g.frame_pyr_bytes = off;

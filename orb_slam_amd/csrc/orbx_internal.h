@@ -41,6 +41,8 @@ constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
 constexpr int kBlurStrip = 32;   // output rows per blur thread (rolling window)
 constexpr int kBlurItems = 256;  // blur items (strip x dword column) per block
 
+constexpr int kResRows = 16;   // output rows per staged resize strip (k_pyr_resize_lds)
+
 struct LevelGeom {
     int w, h;             // level size
     int pw, ph;           // padded size
@@ -59,6 +61,7 @@ struct LevelGeom {
     float patch_size;     // (int)(PATCH_SIZE * scale)
     int res_col_off;      // offset into the resize column table (level >= 1)
     int res_row_off;      // offset into the resize row table
+    int res_span;         // max source rows feeding one strip of kResRows output rows
 };
 
 struct CellGeom {
@@ -165,12 +168,21 @@ struct orbx_ctx {
 };
 
 namespace orbx {
-// orbx_extract.hip
-int launch_extract(orbx_ctx* ctx, int first, int count);
+// orbx_extract.hip (declared below with the match spec)
 // orbx_match.hip
 int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window,
-                      float nnratio, int check_ori);
-int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio);
+                      float nnratio, int check_ori, hipStream_t st = nullptr);
+int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio,
+                         hipStream_t st = nullptr);
+// Extraction of slots [first, first+count) followed by matching each slot
+// against its predecessor; with two streams, each half's internal pairs are
+// matched right after that half is extracted (overlapping the other half).
+struct MatchSpec {
+    int kind;           // 0 none, 1 SearchForInitialization, 2 brute force
+    int seq_len, window, th_low, check_ori;
+    float nnratio;
+};
+int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nullptr);
 // timing helpers (orbx_api.cpp)
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);

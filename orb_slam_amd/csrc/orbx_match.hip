@@ -101,8 +101,17 @@ __global__ __launch_bounds__(256) void k_match_bf_prev(MatchPrevArgs a, int th_l
     if ((threadIdx.x & 63) == 0 && ok) atomicAdd(a.match_n + s, ok);
 }
 
-int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)
+#ifdef ORBX_MATCH_PROFILE
+extern "C" int orbx_debug_match_prof(unsigned long long* out)
 {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_match_prof), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -2;
+}
+#endif
+
+int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio,
+                         hipStream_t st)
+{
+    if (!st) st = ctx->stream;
     const Geometry& g = ctx->geom;
     MatchPrevArgs a{};
     a.kps = ctx->out_kps;
@@ -114,17 +123,18 @@ int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int t
     a.first = first;
     a.seq_len = seq_len;
     a.nnratio = nnratio;
-    ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, ctx->stream));
-    timer_begin(ctx, "match");
-    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 255) / 256, count), dim3(256), 0, ctx->stream, a, th_low);
-    timer_end(ctx, "match");
+    ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, st));
+    timer_begin(ctx, "match", st);
+    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 255) / 256, count), dim3(256), 0, st, a, th_low);
+    timer_end(ctx, "match", st);
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
 }
 
 int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int window, float nnratio,
-                      int check_ori)
+                      int check_ori, hipStream_t st)
 {
+    if (!st) st = ctx->stream;
     const Geometry& g = ctx->geom;
     MatchPrevArgs a;
     a.kps = ctx->out_kps;
@@ -152,9 +162,9 @@ int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wind
     const size_t fixed = init_lds_bytes(a.cap_c, g.nfeatures, 0);
     a.cap_keys = std::max<int>(a.cap_c, (int)((kInitLdsBudget - std::min(fixed, kInitLdsBudget)) / 4));
     const size_t lds = init_lds_bytes(a.cap_c, g.nfeatures, a.cap_keys);
-    timer_begin(ctx, "match");
-    hipLaunchKernelGGL(k_match_prev, dim3(count), dim3(256), lds, ctx->stream, a);
-    timer_end(ctx, "match");
+    timer_begin(ctx, "match", st);
+    hipLaunchKernelGGL(k_match_prev, dim3(count), dim3(256), lds, st, a);
+    timer_end(ctx, "match", st);
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
 }

@@ -50,6 +50,30 @@ __device__ inline uint32_t wave_min_u32(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Wave-wide (best key, second-best distance) over 64 lanes' partial
+// results: (a1, a2) + (b1, b2) -> (min(a1, b1), min(a2, b2, dist(max(a1, b1)))),
+// keys being distinct.  DPP scan pattern; result broadcast from lane 63.
+template <int kCtrl, int kRowMask>
+__device__ inline void best_second_step(uint32_t& m1, int& m2)
+{
+    const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)m1, kCtrl, kRowMask, 0xf, false);
+    const int p2 = __builtin_amdgcn_update_dpp(511, m2, kCtrl, kRowMask, 0xf, false);
+    m2 = min(min(m2, p2), (int)(max(m1, p1) >> 23));
+    m1 = min(m1, p1);
+}
+
+__device__ inline void best_second_reduce(uint32_t& m1, int& m2)
+{
+    best_second_step<0x111, 0xf>(m1, m2);
+    best_second_step<0x112, 0xf>(m1, m2);
+    best_second_step<0x114, 0xf>(m1, m2);
+    best_second_step<0x118, 0xf>(m1, m2);
+    best_second_step<0x142, 0xa>(m1, m2);
+    best_second_step<0x143, 0xc>(m1, m2);
+    m1 = (uint32_t)__builtin_amdgcn_readlane((int)m1, 63);
+    m2 = __builtin_amdgcn_readlane(m2, 63);
+}
+
 __device__ inline int wave_min_i32(int v)
 {
     v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));
@@ -98,7 +122,7 @@ __device__ inline bool in_area(const AreaQuery& q, int cell, float kx, float ky,
 
 __device__ inline int rot_bin(float a1, float a2)
 {
-    const float factor = __fdiv_rn(1.0f, (float)kHistoLength);
+    constexpr float factor = 1.0f / kHistoLength;   // compile-time float division, as the reference
     float rot = __fsub_rn(a1, a2);
     if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
     int bin = (int)roundf(__fmul_rn(rot, factor));   // round half away from zero
@@ -157,6 +181,36 @@ __device__ inline void load_desc(const uint8_t* d, uint4& a, uint4& b)
 // atomics and filtered in parallel after ComputeThreeMaxima.
 // ---------------------------------------------------------------------------
 constexpr int kInitMaxCand = 2048;     // slot field of the key (11 bits)
+
+// Frame::GetFeaturesInArea membership (src/Frame.cc:222-257) on a packed
+// candidate record, branch-free: the candidate loops stream 16-byte records.
+__device__ inline bool in_area_rec(const AreaQuery& q, const float4& rc, float qx, float qy, float r)
+{
+    const int cxcy = __float_as_int(rc.z);
+    const int cx = cxcy & 0xFF, cy = (cxcy >> 8) & 0xFF;
+    return (cxcy >= 0) & (cx >= q.min_cx) & (cx <= q.max_cx) & (cy >= q.min_cy) & (cy <= q.max_cy) &
+           !(fabsf(__fsub_rn(rc.x, qx)) > r) & !(fabsf(__fsub_rn(rc.y, qy)) > r);
+}
+
+#ifdef ORBX_MATCH_PROFILE
+__device__ unsigned long long g_match_prof[8];
+__device__ inline unsigned long long match_stamp()
+{
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define MP_T0() unsigned long long _mt = match_stamp()
+#define MP_MARK(k)                                                               \
+    do {                                                                         \
+        const unsigned long long _n = match_stamp();                             \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_match_prof[k] += _n - _mt;     \
+        _mt = _n;                                                                \
+    } while (0)
+#else
+#define MP_T0()
+#define MP_MARK(k)
+#endif
 constexpr size_t kInitLdsBudget = 64 * 1024;
 
 struct InitLDS {
@@ -174,13 +228,17 @@ struct InitLDS {
     int* offs;          // 257 list offsets of the current group
     int* hist;          // 32 bins + 3 maxima indices
     uint32_t* keys;     // candidate lists
+    float4* rec;        // per candidate: x, y, (cx | cy << 8) or -1, grid cell (as int bits)
+    uint4* qdesc;       // per query of the current group (256): descriptor (2 x uint4)
+    float2* qxy;        // query position
+    int4* qarea;        // cell range (min_cx, max_cx, min_cy, max_cy); min_cx > max_cx when inactive
     int cap_c, cap1, cap_keys;
 };
 
 __host__ __device__ inline size_t init_lds_bytes(int cap_c, int cap1, int cap_keys)
 {
-    return (size_t)cap_c * (7 * 4 + 32) + (size_t)cap1 * 8 + (size_t)((cap1 + 15) & ~15) + 257 * 4 + 36 * 4 +
-           (size_t)cap_keys * 4 + 64;
+    return (size_t)cap_c * (7 * 4 + 32 + 16) + (size_t)cap1 * 8 + (size_t)((cap1 + 15) & ~15) + 257 * 4 + 36 * 4 +
+           (size_t)cap_keys * 4 + 256 * (32 + 8 + 16) + 64;
 }
 
 __device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap_keys)
@@ -190,7 +248,11 @@ __device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap
     s.cap1 = cap1;
     s.cap_keys = cap_keys;
     s.desc = reinterpret_cast<uint4*>(base);
-    s.x = reinterpret_cast<float*>(s.desc + 2 * cap_c);
+    s.qdesc = s.desc + 2 * cap_c;
+    s.qarea = reinterpret_cast<int4*>(s.qdesc + 2 * 256);
+    s.qxy = reinterpret_cast<float2*>(s.qarea + 256);
+    s.rec = reinterpret_cast<float4*>(s.qxy + 256);
+    s.x = reinterpret_cast<float*>(s.rec + cap_c);
     s.y = s.x + cap_c;
     s.ang = s.y + cap_c;
     s.cell = reinterpret_cast<int*>(s.ang + cap_c);
@@ -212,6 +274,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
                                              int32_t* error_flags)
 {
     const int tid = threadIdx.x, lane = tid & 63;
+    MP_T0();
     // F2 octave-0 keypoints in index order -> candidate slots
     int nc = 0;
     for (int base = 0; base < F2.n; base += kBlock) {
@@ -228,7 +291,10 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
             s.x[pos] = k.x;
             s.y[pos] = k.y;
             s.ang[pos] = k.angle;
-            s.cell[pos] = grid_cell(F2, k.x, k.y);
+            const int cell = grid_cell(F2, k.x, k.y);
+            s.cell[pos] = cell;
+            s.rec[pos] = make_float4(k.x, k.y, __int_as_float(cell < 0 ? -1 : ((cell / kGridRows) | ((cell % kGridRows) << 8))),
+                                     __int_as_float(cell));
             s.idx[pos] = i2;
             s.mdist[pos] = 0x7fffffff;
             s.m21[pos] = -1;
@@ -252,27 +318,49 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     }
     if (tid < 36) s.hist[tid] = 0;
     __syncthreads();
+    MP_MARK(0);
     const float r = (float)window;
+    const int wv = tid >> 6;
+    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int g0 = 0; g0 < F1.n; g0 += kBlock) {
-        const int i1 = g0 + tid;
-        bool act = false;
-        float qx = 0.f, qy = 0.f;
-        AreaQuery q;
-        q.empty = true;
-        uint4 d1a = make_uint4(0, 0, 0, 0), d1b = d1a;
-        if (i1 < F1.n) {
-            const orbx_keypoint k1 = F1.kps[i1];
-            if (k1.octave == 0) {
-                qx = prev_xy ? prev_xy[2 * i1] : k1.x;
-                qy = prev_xy ? prev_xy[2 * i1 + 1] : k1.y;
-                q = area_cells(F2, qx, qy, r);
-                act = !q.empty;
-                if (act) load_desc(F1.desc + (size_t)i1 * 32, d1a, d1b);
+        const int gn = min(kBlock, F1.n - g0);
+        // stage the group's queries (one thread each): position, cell range,
+        // descriptor; inactive (octave > 0 or empty area) get an empty range
+        {
+            const int i1 = g0 + tid;
+            int4 qa = make_int4(1, 0, 1, 0);
+            float2 qp = make_float2(0.f, 0.f);
+            if (tid < gn) {
+                const orbx_keypoint k1 = F1.kps[i1];
+                if (k1.octave == 0) {
+                    qp = make_float2(prev_xy ? prev_xy[2 * i1] : k1.x, prev_xy ? prev_xy[2 * i1 + 1] : k1.y);
+                    const AreaQuery q = area_cells(F2, qp.x, qp.y, r);
+                    if (!q.empty) qa = make_int4(q.min_cx, q.max_cx, q.min_cy, q.max_cy);
+                    load_desc(F1.desc + (size_t)i1 * 32, s.qdesc[2 * tid], s.qdesc[2 * tid + 1]);
+                }
             }
+            s.qarea[tid] = qa;
+            s.qxy[tid] = qp;
         }
-        int cnt = 0;
-        if (act)
-            for (int j = 0; j < nc; j++) cnt += in_area(q, s.cell[j], s.x[j], s.y[j], qx, qy, r);
+        __syncthreads();
+        // count pass, one wave per query (lanes over the candidates): balanced
+        // whatever the window population of individual queries
+        for (int t = wv; t < gn; t += kWaves) {
+            const int4 qa = s.qarea[t];
+            int cnt = 0;
+            if (qa.x <= qa.y) {
+                const float2 qp = s.qxy[t];
+                AreaQuery q;
+                q.min_cx = qa.x; q.max_cx = qa.y; q.min_cy = qa.z; q.max_cy = qa.w; q.empty = false;
+                for (int j = lane; j < nc; j += 64) cnt += in_area_rec(q, s.rec[j], qp.x, qp.y, r);
+                cnt = wave_sum(cnt);
+            }
+            if (lane == 0) s.offs[t] = cnt;
+        }
+        if (g0 == 0) MP_MARK(4);
+        __syncthreads();
+        const int cnt = tid < gn ? s.offs[tid] : 0;
+        if (g0 == 0) MP_MARK(5);
         int total;
         const int off = block_exclusive_scan(cnt, &total, bs, 0);
         s.offs[tid] = off;
@@ -283,56 +371,109 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
             const int base_off = s.offs[lo];
             const int fits = (tid >= lo && s.offs[tid + 1] - base_off <= s.cap_keys) ? 1 : 0;
             const int hi = lo + block_sum(fits, bs, 1);
-            if (tid >= lo && tid < hi && cnt > 0) {
-                uint32_t* out = s.keys + (off - base_off);
+            // fill pass, one wave per query: keys of the in-area candidates
+            for (int t = lo + wv; t < hi; t += kWaves) {
+                const int n = s.offs[t + 1] - s.offs[t];
+                if (n == 0) continue;
+                const int4 qa = s.qarea[t];
+                const float2 qp = s.qxy[t];
+                const float qx = qp.x, qy = qp.y;
+                AreaQuery q;
+                q.min_cx = qa.x; q.max_cx = qa.y; q.min_cy = qa.z; q.max_cy = qa.w; q.empty = false;
+                const uint4 d1a = s.qdesc[2 * t], d1b = s.qdesc[2 * t + 1];
+                uint32_t* out = s.keys + (s.offs[t] - base_off);
                 int w = 0;
-                for (int j = 0; j < nc; j++) {
-                    const int cell = s.cell[j];
-                    if (!in_area(q, cell, s.x[j], s.y[j], qx, qy, r)) continue;
-                    const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
-                    out[w++] = ((uint32_t)dist << 23) | ((uint32_t)cell << 11) | (uint32_t)j;
+                for (int j0 = 0; j0 < nc; j0 += 64) {
+                    const int j = j0 + lane;
+                    bool ok = false;
+                    float4 rc;
+                    if (j < nc) {
+                        rc = s.rec[j];
+                        ok = in_area_rec(q, rc, qx, qy, r);
+                    }
+                    const unsigned long long bal = __ballot(ok);
+                    if (ok) {
+                        const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
+                        out[w + __popcll(bal & lt_mask)] =
+                            ((uint32_t)dist << 23) | ((uint32_t)__float_as_int(rc.w) << 11) | (uint32_t)j;
+                    }
+                    w += __popcll(bal);
                 }
             }
+            if (g0 == 0) MP_MARK(6);
             __syncthreads();
+            MP_MARK(1);
             if (tid < 64) {
+                // keys of query t+1 are loaded while t is decided: only the
+                // mdist reads depend on the previous query's outcome
+                int oa = s.offs[lo], ob = s.offs[lo + 1];
+                uint32_t kn = lane < ob - oa ? s.keys[oa - base_off + lane] : 0xFFFFFFFFu;
                 for (int t = lo; t < hi; t++) {
-                    const int b = s.offs[t] - base_off, n = s.offs[t + 1] - s.offs[t];
+                    const int n = ob - oa;
+                    const int b = oa - base_off;
+                    const uint32_t k0 = kn;
+                    if (t + 1 < hi) {
+                        const int oc = s.offs[t + 2];
+                        kn = lane < oc - ob ? s.keys[ob - base_off + lane] : 0xFFFFFFFFu;
+                        oa = ob;
+                        ob = oc;
+                    }
                     if (n == 0) continue;   // vIndices2.empty(), or not an octave-0 query
-                    uint32_t best = 0xFFFFFFFFu;
-                    for (int e = lane; e < n; e += 64) {
+                    // one pass: lane-local best key and second-best distance
+                    // over the admissible candidates (vMatchedDistance > dist)
+                    uint32_t m1 = 0xFFFFFFFFu;
+                    int m2 = 511;   // "none" (> any Hamming distance)
+                    if (lane < n && s.mdist[k0 & 0x7FF] > (int)(k0 >> 23)) m1 = k0;
+                    for (int e = lane + 64; e < n; e += 64) {   // lists longer than a wave
                         const uint32_t key = s.keys[b + e];
                         const int dist = (int)(key >> 23);
-                        if (s.mdist[key & 0x7FF] > dist) best = min(best, key);
-                    }
-                    best = wave_min_u32(best);
-                    if (best == 0xFFFFFFFFu) continue;
-                    const int bestDist = (int)(best >> 23);
-                    int second = 0x7fffffff;
-                    for (int e = lane; e < n; e += 64) {
-                        const uint32_t key = s.keys[b + e];
-                        const int dist = (int)(key >> 23);
-                        if (key != best && s.mdist[key & 0x7FF] > dist) second = min(second, dist);
-                    }
-                    second = wave_min_i32(second);
-                    if (bestDist <= kTHLow && (float)bestDist < __fmul_rn((float)second, nnratio)) {
-                        if (lane == 0) {
-                            const int slot = (int)(best & 0x7FF);
-                            const int ii1 = g0 + t;
-                            const int prev = s.m21[slot];
-                            if (prev >= 0) s.m12[prev] = -1;
-                            s.m12[ii1] = s.idx[slot];
-                            s.m21[slot] = ii1;
-                            s.mdist[slot] = bestDist;
-                            if (check_ori) s.pushed[ii1] = (signed char)rot_bin(s.ang1[ii1], s.ang[slot]);
+                        if (s.mdist[key & 0x7FF] > dist) {
+                            if (key < m1) {
+                                m2 = min(m2, (int)(m1 >> 23));
+                                m1 = key;
+                            } else {
+                                m2 = min(m2, dist);
+                            }
                         }
-                        wave_sync();
+                    }
+                    best_second_reduce(m1, m2);
+                    if (m1 == 0xFFFFFFFFu) continue;
+                    const int bestDist = (int)(m1 >> 23);
+                    const int second = m2 >= 511 ? 0x7fffffff : m2;
+                    if (bestDist <= kTHLow && (float)bestDist < __fmul_rn((float)second, nnratio)) {
+                        // accept: the slot now belongs to ii1.  A steal needs no
+                        // read-modify-write here: m12 is rebuilt at the end from
+                        // "ii1 still owns the slot it took" (m21[slot] == ii1),
+                        // and the rotation bin from the slot ii1 took.
+                        if (lane == 0) {
+                            const int slot = (int)(m1 & 0x7FF);
+                            s.m12[g0 + t] = slot;
+                            s.m21[slot] = g0 + t;
+                            s.mdist[slot] = bestDist;
+                        }
+                        // LDS operations of one wave complete in order: the next
+                        // query's mdist reads see these writes; only keep the
+                        // compiler from moving memory operations across
+                        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                        __builtin_amdgcn_wave_barrier();
                     }
                 }
             }
+            MP_MARK(7);   // wave 0: the replay of this chunk
             __syncthreads();
             lo = hi;
         }
     }
+    MP_MARK(2);
+    __syncthreads();
+    // m12[i] held the slot i took; keep it only if i still owns that slot
+    // (rotHist keeps the entries of stolen matches too: src/ORBmatcher.cc:675, 688-703)
+    for (int i = tid; i < F1.n; i += kBlock) {
+        const int sl = s.m12[i];
+        if (check_ori && sl >= 0) s.pushed[i] = (signed char)rot_bin(s.ang1[i], s.ang[sl]);
+        s.m12[i] = (sl >= 0 && s.m21[sl] == i) ? s.idx[sl] : -1;
+    }
+    __syncthreads();
     if (check_ori) {
         for (int i = tid; i < F1.n; i += kBlock)
             if (s.pushed[i] >= 0) atomicAdd(&s.hist[s.pushed[i]], 1);
@@ -359,6 +500,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     }
     nm = block_sum(nm, bs, 0);
     if (tid == 0) *out_n = nm;
+    MP_MARK(3);
 }
 
 }  // namespace orbx

@@ -72,3 +72,30 @@ def test_match_bf_prev_matches_oracle():
         assert np.array_equal(gm[:len(dA)], want)
         assert gn == int((want >= 0).sum()) and gn > 0
     ctx.close()
+
+
+@pytest.mark.parametrize("mode,seq_len", [("init", 64), ("init", 16), ("bf", 64)])
+def test_extract_match_pipeline_equals_separate_calls(mode, seq_len):
+    """orbx_dev_extract_match (two-stream pipelined, pairs straddling the
+    halves matched after the join) gives exactly the separate calls' result."""
+    w, h, B = 640, 480, 64
+    frames = synth.sequence(w, h, B, seed=13)
+    ctx = ox.Context(nfeatures=1000, max_w=w, max_h=h, slots=B)
+    ctx.upload(frames)
+    ctx.extract_match(0, B, seq_len, mode=mode)
+    ctx.sync()
+    piped = [ctx.matches(s) for s in range(B)]
+    feats = [ctx.features(s) for s in range(B)]
+    ctx.set_split(False)
+    ctx.extract(0, B)
+    if mode == "init":
+        ctx.match_prev(0, B, seq_len)
+    else:
+        ctx.match_bf_prev(0, B, seq_len)
+    ctx.sync()
+    for s in range(B):
+        m, n = ctx.matches(s)
+        k, d = ctx.features(s)
+        assert np.array_equal(k.view(np.uint8), feats[s][0].view(np.uint8)) and np.array_equal(d, feats[s][1])
+        assert n == piped[s][1] and np.array_equal(m[:len(k)], piped[s][0][:len(k)]), s
+    ctx.close()
