@@ -31,6 +31,32 @@ __constant__ __attribute__((aligned(4))) int8_t c_pattern[256][4] = {
 #include "orbx_pattern.inc"
 };
 
+#ifdef ORBX_FAST_PROFILE
+__device__ unsigned long long g_fast_prof[16];
+__device__ inline unsigned long long fp_stamp()
+{
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define FP_T0() unsigned long long _ft = fp_stamp()
+#define FP_MARK(k)                                                                  \
+    do {                                                                            \
+        const unsigned long long _n = fp_stamp();                                   \
+        if (threadIdx.x == 0) atomicAdd(&g_fast_prof[k], _n - _ft);                 \
+        _ft = _n;                                                                   \
+    } while (0)
+#define FP_ADD(k, v) atomicAdd(&g_fast_prof[k], (unsigned long long)(v))
+extern "C" int orbx_debug_fast_prof(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_prof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+}
+#else
+#define FP_T0()
+#define FP_MARK(k)
+#define FP_ADD(k, v)
+#endif
+
 struct ExtractArgs {
     const LevelGeom* levels;
     const CellGeom* cells;
@@ -427,18 +453,23 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         return;
     }
     const LevelGeom L = a.levels[C.level];
-    const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~3, sh = roi_x - x_al;
+    const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15, sh = roi_x - x_al;
     const int hx = C.hx, hy = C.hy;
-    const int P = (sh + hx + 3) & ~3, nq = P >> 2;     // tile pitch, dwords per row
+    const int P = (sh + hx + 15) & ~15, nq = P >> 2;   // tile pitch, dwords per row
+    const int nq16 = P >> 4;                             // 16-byte words per row
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
     uint8_t* tile = smem;
     uint8_t* sm = smem + tile_pitch_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
-    stage_to_lds<8>(tile32, hy * nq, tid, kBlock, [&](int i) {
-        const int r = i / nq;
-        return *reinterpret_cast<const uint32_t*>(src + (size_t)r * L.stride + 4 * (i - r * nq));
-    });
+    FP_T0();
+    auto load_tile = [&]() {
+        stage_to_lds<4>(reinterpret_cast<uint4*>(tile32), hy * nq16, tid, kBlock, [&](int i) {
+            const int r = i / nq16;
+            return *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * (i - r * nq16));
+        });
+    };
+    load_tile();
     // S' is 0 outside the interior rows [3, hy-4]; the interior rows are
     // fully rewritten below
     for (int i = tid; i < nq; i += kBlock) {
@@ -446,158 +477,210 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         sm32[(hy - 3) * nq + i] = 0;
     }
     __syncthreads();
-    const int tmin = min(a.fast_th, a.fast_th_low);
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
     const int nunits = (hy - 6) * nq;
-    RowWalk cw_(wv * 64 + lane, kBlock, nq);
-    for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
-        const int u = u0 + lane;
-        const int r = 3 + cw_.r, q = cw_.q;
-        int mask = 0;
-        if (u < nunits) {
-            const uint32_t* row = tile32 + r * nq + q;
-            const uint32_t mid = row[0];
-            const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
-            const uint32_t up = row[-3 * nq], dn = row[3 * nq];
-            // 4 pixels at once: even / odd bytes as two u16x2 halves, packed
-            // 16-bit arithmetic; a lane's sign bit set = "test fails"
-            const uint32_t p4w = __builtin_amdgcn_alignbyte(hi, mid, 3);    // bytes j+3
-            const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
-            const uint32_t T1 = (uint32_t)(tmin + 1) * 0x00010001u;
-            const uint32_t NT1 = (uint32_t)(-(tmin + 1) & 0xFFFF) * 0x00010001u;
-            int ok[2][2];   // [half][dark, bright] sign-bit masks of passing lanes
-#pragma unroll
-            for (int hf = 0; hf < 2; hf++) {
-                const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;   // bytes 1,3 or 0,2 -> u16x2
-                const uint32_t v = __builtin_amdgcn_perm(0u, mid, sel);
-                const uint32_t pk[4] = {__builtin_amdgcn_perm(0u, dn, sel), __builtin_amdgcn_perm(0u, p4w, sel),
-                                        __builtin_amdgcn_perm(0u, up, sel), __builtin_amdgcn_perm(0u, p12w, sel)};
-                uint32_t xd[4], xb[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t d = pk_sub16(v, pk[k]);     // v - p
-                    xd[k] = pk_sub16(d, T1);                   // >= 0 <=> v - p > t
-                    xb[k] = pk_sub16(NT1, d);                  // >= 0 <=> p - v > t
+    // S' map at threshold tmin: S' = S where S >= tmin, else 0
+    auto score_pass = [&](const int tmin) {
+        RowWalk cw_(wv * 64 + lane, kBlock, nq);
+        for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
+            const int u = u0 + lane;
+            const int r = 3 + cw_.r, q = cw_.q;
+            int mask = 0;
+            if (u < nunits) {
+                const uint32_t* row = tile32 + r * nq + q;
+                const uint32_t mid = row[0];
+                const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
+                const uint32_t up = row[-3 * nq], dn = row[3 * nq];
+                // 4 pixels at once: even / odd bytes as two u16x2 halves, packed
+                // 16-bit arithmetic; a lane's sign bit set = "test fails"
+                const uint32_t p4w = __builtin_amdgcn_alignbyte(hi, mid, 3);    // bytes j+3
+                const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
+                const uint32_t T1 = (uint32_t)(tmin + 1) * 0x00010001u;
+                const uint32_t NT1 = (uint32_t)(-(tmin + 1) & 0xFFFF) * 0x00010001u;
+                int ok[2][2];   // [half][dark, bright] sign-bit masks of passing lanes
+    #pragma unroll
+                for (int hf = 0; hf < 2; hf++) {
+                    const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;   // bytes 1,3 or 0,2 -> u16x2
+                    const uint32_t v = __builtin_amdgcn_perm(0u, mid, sel);
+                    const uint32_t pk[4] = {__builtin_amdgcn_perm(0u, dn, sel), __builtin_amdgcn_perm(0u, p4w, sel),
+                                            __builtin_amdgcn_perm(0u, up, sel), __builtin_amdgcn_perm(0u, p12w, sel)};
+                    uint32_t xd[4], xb[4];
+    #pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t d = pk_sub16(v, pk[k]);     // v - p
+                        xd[k] = pk_sub16(d, T1);                   // >= 0 <=> v - p > t
+                        xb[k] = pk_sub16(NT1, d);                  // >= 0 <=> p - v > t
+                    }
+                    const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
+                    const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
+                    ok[hf][0] = (int)(~failD & 0x80008000u);
+                    ok[hf][1] = (int)(~failB & 0x80008000u);
                 }
-                const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
-                const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
-                ok[hf][0] = (int)(~failD & 0x80008000u);
-                ok[hf][1] = (int)(~failB & 0x80008000u);
+                // pixel j: bit 2j dark, 2j+1 bright (even half: j = 0, 2; odd: 1, 3)
+                mask = ((ok[0][0] >> 15) & 1) | ((ok[0][1] >> 14) & 2) |                          // j = 0
+                       (((ok[1][0] >> 15) & 1) << 2) | (((ok[1][1] >> 14) & 2) << 2) |              // j = 1
+                       (((ok[0][0] >> 31) & 1) << 4) | ((((unsigned)ok[0][1] >> 30) & 2) << 4) |     // j = 2
+                       (((ok[1][0] >> 31) & 1) << 6) | ((((unsigned)ok[1][1] >> 30) & 2) << 6);     // j = 3
+                // interior columns only
+                const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
+                mask = (j1 < j0) ? 0 : (mask & (((1 << (2 * (j1 + 1))) - 1) & ~((1 << (2 * j0)) - 1)));
+                sm32[r * nq + q] = 0;
             }
-            // pixel j: bit 2j dark, 2j+1 bright (even half: j = 0, 2; odd: 1, 3)
-            mask = ((ok[0][0] >> 15) & 1) | ((ok[0][1] >> 14) & 2) |                          // j = 0
-                   (((ok[1][0] >> 15) & 1) << 2) | (((ok[1][1] >> 14) & 2) << 2) |              // j = 1
-                   (((ok[0][0] >> 31) & 1) << 4) | ((((unsigned)ok[0][1] >> 30) & 2) << 4) |     // j = 2
-                   (((ok[1][0] >> 31) & 1) << 6) | ((((unsigned)ok[1][1] >> 30) & 2) << 6);     // j = 3
-            // interior columns only
-            const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
-            mask = (j1 < j0) ? 0 : (mask & (((1 << (2 * (j1 + 1))) - 1) & ~((1 << (2 * j0)) - 1)));
-            sm32[r * nq + q] = 0;
-        }
-        const int cnt = __popc((mask | (mask >> 1)) & 0x55);
-        const int incl = wave_inclusive_scan(cnt);
-        const int ntot = __builtin_amdgcn_readlane(incl, 63);
-        int w = incl - cnt;
-        if (mask) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int fl = (mask >> (2 * j)) & 3;
-                if (fl) cand[wv][w++] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
+            const int cnt = __popc((mask | (mask >> 1)) & 0x55);
+            const int incl = wave_inclusive_scan(cnt);
+            const int ntot = __builtin_amdgcn_readlane(incl, 63);
+#ifdef ORBX_FAST_PROFILE
+            if (lane == 0) FP_ADD(10 + (tmin < 10), ntot);
+            if (lane == 0) FP_ADD(12, 1);
+#endif
+            int w = incl - cnt;
+            if (mask) {
+    #pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int fl = (mask >> (2 * j)) & 3;
+                    if (fl) cand[wv][w++] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
+                }
             }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int i0 = 0; i0 < ntot; i0 += 64) {
-            const int i = i0 + lane;
-            const uint32_t cw = i < ntot ? cand[wv][i] : 0u;
-            const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
-            int S = 0;
-            if (fl) S = fast_arc(tile + pos, P, (fl & 1) ? 1 : -1);
-            if (__any(fl == 3) && fl == 3) S = max(S, fast_arc(tile + pos, P, -1));
-            S -= 1;
-            if (fl) sm[pos] = (uint8_t)(S >= tmin ? S : 0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    __syncthreads();
-    // non-max suppression: keep S' if it beats all 8 neighbours' S'
-    int c1 = 0;
-    RowWalk nw(tid, kBlock, nq);
-    for (int u = tid; u < nunits; u += kBlock, nw.next()) {
-        const int r = 3 + nw.r, q = nw.q;
-        uint32_t word = 0;
-        const uint32_t* m = sm32 + r * nq + q;
-        const uint32_t mid = m[0];
-        if (mid) {
-            // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
-            // rows r-1, r, r+1), byte-wise max on even / odd u16x2 halves
-            uint32_t nb[8];
-            int k = 0;
-#pragma unroll
-            for (int dr = 0; dr < 3; dr++) {
-                const uint32_t* mr = m + (dr - 1) * nq;
-                const uint32_t lo = q > 0 ? mr[-1] : 0u, mm = mr[0], hi = q + 1 < nq ? mr[1] : 0u;
-                nb[k++] = __builtin_amdgcn_alignbyte(mm, lo, 3);   // j-1
-                if (dr != 1) nb[k++] = mm;
-                nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i0 = 0; i0 < ntot; i0 += 64) {
+                const int i = i0 + lane;
+                const uint32_t cw = i < ntot ? cand[wv][i] : 0u;
+                const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
+                int S = 0;
+                if (fl) S = fast_arc(tile + pos, P, (fl & 1) ? 1 : -1);
+                if (__any(fl == 3) && fl == 3) S = max(S, fast_arc(tile + pos, P, -1));
+                S -= 1;
+                if (fl) sm[pos] = (uint8_t)(S >= tmin ? S : 0);
             }
-            const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
-#pragma unroll
-            for (int hf = 0; hf < 2; hf++) {
-                const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
-                uint32_t mx = __builtin_amdgcn_perm(0u, nb[0], sel);
-#pragma unroll
-                for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
-                const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
-                // keep where mx - s < 0 (s > every neighbour)
-                const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
-                const uint32_t kept = sv & keep;
-                word |= kept << (8 * hf);
-                // corners at fastTh among the kept (kept >= max(fastTh, 1))
-                c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
-            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        tile32[r * nq + q] = word;
+    };
+    // non-max suppression over the S' map (kept S' written over the tile);
+    // returns this thread's count of kept corners at fastTh
+    auto nms_pass = [&]() {
+        // non-max suppression: keep S' if it beats all 8 neighbours' S'
+        int c1 = 0;
+        RowWalk nw(tid, kBlock, nq);
+        for (int u = tid; u < nunits; u += kBlock, nw.next()) {
+            const int r = 3 + nw.r, q = nw.q;
+            uint32_t word = 0;
+            const uint32_t* m = sm32 + r * nq + q;
+            const uint32_t mid = m[0];
+            if (mid) {
+                // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
+                // rows r-1, r, r+1), byte-wise max on even / odd u16x2 halves
+                uint32_t nb[8];
+                int k = 0;
+    #pragma unroll
+                for (int dr = 0; dr < 3; dr++) {
+                    const uint32_t* mr = m + (dr - 1) * nq;
+                    const uint32_t lo = q > 0 ? mr[-1] : 0u, mm = mr[0], hi = q + 1 < nq ? mr[1] : 0u;
+                    nb[k++] = __builtin_amdgcn_alignbyte(mm, lo, 3);   // j-1
+                    if (dr != 1) nb[k++] = mm;
+                    nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
+                }
+                const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
+    #pragma unroll
+                for (int hf = 0; hf < 2; hf++) {
+                    const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
+                    uint32_t mx = __builtin_amdgcn_perm(0u, nb[0], sel);
+    #pragma unroll
+                    for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
+                    const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
+                    // keep where mx - s < 0 (s > every neighbour)
+                    const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
+                    const uint32_t kept = sv & keep;
+                    word |= kept << (8 * hf);
+                    // corners at fastTh among the kept (kept >= max(fastTh, 1))
+                    c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
+                }
+            }
+            tile32[r * nq + q] = word;
+        }
+        return c1;
+    };
+    // Thresholds (:599-614): FAST(fastTh), and FAST(7) when that finds <= 3
+    // corners.  The S' map at threshold t gives both answers for t <= min
+    // (NMS against S' equals NMS against the t-score map for corners >= t),
+    // so a cell is scored at fastTh first (far fewer compass survivors) and
+    // rescored at 7 only when it needs the fallback.
+    int n1;
+    FP_MARK(0);
+    if (a.fast_th > a.fast_th_low) {
+        score_pass(a.fast_th);
+        __syncthreads();
+        FP_MARK(1);
+        n1 = block_sum(nms_pass(), bs, 0);
+        FP_MARK(2);
+        if (n1 <= 3) {   // uniform over the block
+            if (threadIdx.x == 0) FP_ADD(8, 1);
+            __syncthreads();
+            load_tile();
+            __syncthreads();
+            score_pass(a.fast_th_low);
+            __syncthreads();
+            nms_pass();
+            __syncthreads();
+            FP_MARK(3);
+        }
+    } else {
+        score_pass(a.fast_th);
+        __syncthreads();
+        n1 = block_sum(nms_pass(), bs, 0);
     }
     // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
-    const int n1 = block_sum(c1, bs, 0);
     const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
     uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    int base = 0, buf = 1;
-    RowWalk ow(tid, kBlock, nq);
-    for (int u0 = 0; u0 < nunits; u0 += kBlock, ow.next()) {
-        const int u = u0 + tid;
-        uint32_t word = 0;
-        int cnt = 0;
-        if (u < nunits) {
-            word = tile32[(3 + ow.r) * nq + ow.q];
+    // raster-order compaction with one block scan: thread tid owns the
+    // contiguous units [tid * per, (tid + 1) * per)
+    const int per = (nunits + kBlock - 1) / kBlock;
+    const int ua = min(tid * per, nunits), ub = min(ua + per, nunits);
+    int cnt = 0;
+    {
+        int r = 3 + ua / nq, q = ua - (r - 3) * nq;
+        for (int u = ua; u < ub; u++) {
+            const uint32_t word = tile32[r * nq + q];
 #pragma unroll
             for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
+            if (++q == nq) {
+                q = 0;
+                r++;
+            }
         }
-        int total;
-        int off = base + block_exclusive_scan(cnt, &total, bs, buf);
-        buf ^= 1;
-        if (cnt) {
-            const int r = 3 + ow.r, q = ow.q;
+    }
+    int base;
+    int off = block_exclusive_scan(cnt, &base, bs, 1);
+    if (cnt) {
+        int r = 3 + ua / nq, q = ua - (r - 3) * nq;
+        for (int u = ua; u < ub; u++) {
+            const uint32_t word = tile32[r * nq + q];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int s = byte_of(word, j);
-                if (s >= t && s > 0 && off < C.list_cap) {
-                    const int cc = 4 * q + j - sh;   // ROI column
-                    out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                if (s >= t && s > 0) {
+                    if (off < C.list_cap) {
+                        const int cc = 4 * q + j - sh;   // ROI column
+                        out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                    }
+                    off++;
                 }
-                off += (s >= t && s > 0);
+            }
+            if (++q == nq) {
+                q = 0;
+                r++;
             }
         }
-        base += total;
     }
     if (tid == 0) {
         *count_out = base;
         if (base > C.list_cap) atomicOr(a.error_flags, 1);
     }
+    FP_MARK(4);
+    if (tid == 0) FP_ADD(9, 1);
 }
 
 // ---------------------------------------------------------------------------

@@ -240,8 +240,8 @@ int compute_geometry(Geometry& g, int w, int h)
                 c.list_cap = ((iw + 1) / 2) * ((ih + 1) / 2);
                 c.list_off = list_off;
                 list_off += c.list_cap;
-                // FAST tile: dword-aligned rows (up to 3 bytes of lead-in)
-                g.max_tile_bytes = std::max(g.max_tile_bytes, c.hy * ((c.hx + 6) & ~3));
+                // FAST tile: 16-byte aligned rows (up to 15 bytes of lead-in)
+                g.max_tile_bytes = std::max(g.max_tile_bytes, c.hy * ((c.hx + 30) & ~15));
                 g.max_list_cap = std::max(g.max_list_cap, c.list_cap);
                 g.cells.push_back(c);
             }
