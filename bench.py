@@ -142,21 +142,26 @@ def run_frames(args, wl, rank, local, world, dist):
     w, h, nf, B = wl["w"], wl["h"], wl["nfeatures"], args.batch or wl["batch"]
     bf = args.workload == "c3"
     frames = synth.sequence(w, h, B, seed=odist.shard_seed(2000, rank))
-    ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=B, device=local if world > 1 else 0)
-    ctx.upload(frames)
+    # two slot ranges: step k extracts range k % 2 while the matching of
+    # step k - 1 (the other range) finishes on the context's match stream
+    ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=2 * B, device=local if world > 1 else 0)
+    ctx.upload(frames, first=0)
+    ctx.upload(frames, first=B)
+    ctx.set_async_match(not args.sync_match)
+    it = [0]
 
     def step():
-        if args.pipelined:
-            # matching of each half-batch overlapped with the other half's
-            # extraction; pairs straddling the halves after the join
-            ctx.extract_match(0, B, B, mode="bf" if bf else "init", window=100, th_low=50, nnratio=0.9,
-                              check_ori=True)
+        first = (it[0] % 2) * B
+        it[0] += 1
+        if args.sync_match:   # extraction, then matching, in order on the context stream
+            ctx.extract(first, B)
+            if bf:
+                ctx.match_bf_prev(first, B, B, th_low=50, nnratio=0.9)
+            else:
+                ctx.match_prev(first, B, B, window=100, nnratio=0.9, check_ori=True)
             return
-        ctx.extract(0, B)
-        if bf:
-            ctx.match_bf_prev(0, B, B, th_low=50, nnratio=0.9)
-        else:
-            ctx.match_prev(0, B, B, window=100, nnratio=0.9, check_ori=True)
+        ctx.extract_match(first, B, B, mode="bf" if bf else "init", window=100, th_low=50, nnratio=0.9,
+                          check_ori=True)
 
     for _ in range(args.warmup):
         step()
@@ -167,9 +172,11 @@ def run_frames(args, wl, rank, local, world, dist):
     # extraction halves serialised, so each kernel's launch time is not shared
     # with the other stream's kernels (per-kernel roofline without overlap).
     ctx.set_split(False)
+    ctx.set_async_match(False)
     iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
     _, iso = timed(iso_args, ctx, step, None, names)
     ctx.set_split(True)
+    ctx.set_async_match(not args.sync_match)
     kernels = {"overlapped": kernels, "isolated": iso}
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
@@ -263,8 +270,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--pipelined", action="store_true",
-                    help="overlap each half-batch's matching with the other half's extraction")
+    ap.add_argument("--sync-match", action="store_true",
+                    help="match each batch after its extraction on the same stream (no overlap with the next "
+                         "batch's extraction)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()

@@ -119,6 +119,13 @@ int orbx_dev_set_split(orbx_ctx* ctx, int enable);
  * half is still being extracted.  Results as for the separate calls. */
 int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int mode,
                            int window, int th_low, float nnratio, int check_ori);
+/* Asynchronous matching for orbx_dev_extract_match: the batch's matching is
+ * queued on an internal stream after its extraction, and the call returns;
+ * a later extract_match of *other* slots overlaps it (a stream of batches
+ * alternating between two slot ranges keeps extraction and matching of
+ * consecutive batches concurrent).  Any other call on the context, or an
+ * extraction into slots the pending match reads, waits for it first. */
+int orbx_dev_set_async_match(orbx_ctx* ctx, int enable);
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */

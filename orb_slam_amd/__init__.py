@@ -72,6 +72,7 @@ def _declare(L):
         "orbx_dev_sync": ([vp], i),
         "orbx_dev_match_bf_prev": ([vp, i, i, i, i, f], i),
         "orbx_dev_set_split": ([vp, i], i),
+        "orbx_dev_set_async_match": ([vp, i], i),
         "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
         "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
@@ -183,6 +184,11 @@ class Context:
     def set_split(self, enable):
         """Two concurrent half-batch streams for large extraction batches."""
         _check(lib().orbx_dev_set_split(self._h, int(enable)), "orbx_dev_set_split")
+
+    def set_async_match(self, enable):
+        """Queue extract_match's matching behind the extraction on an internal
+        stream; later extract_match calls on other slots overlap it."""
+        _check(lib().orbx_dev_set_async_match(self._h, int(enable)), "orbx_dev_set_async_match")
 
     def match_bf_prev(self, first, count, seq_len, th_low=50, nnratio=0.9):
         _check(lib().orbx_dev_match_bf_prev(self._h, first, count, seq_len, th_low, nnratio),

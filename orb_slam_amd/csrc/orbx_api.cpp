@@ -197,8 +197,11 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     const int S = max_batch;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK && (hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess))
+                         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->ev_extracted, hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming) != hipSuccess))
         r = ORBX_ERR_HIP;
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
@@ -227,9 +230,10 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
 void orbx_destroy(orbx_ctx* ctx)
 {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
     for (auto& t : ctx->timers) {
         for (auto e : t.start) hipEventDestroy(e);
         for (auto e : t.stop) hipEventDestroy(e);
@@ -237,6 +241,9 @@ void orbx_destroy(orbx_ctx* ctx)
     free_buffers(ctx);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->ev_extracted) (void)hipEventDestroy(ctx->ev_extracted);
+    if (ctx->ev_matched) (void)hipEventDestroy(ctx->ev_matched);
+    if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -265,7 +272,7 @@ int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs, in
 {
     if (!ctx || !imgs || count <= 0 || first < 0 || first + count > ctx->slots || stride < (size_t)w)
         return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     int r = set_geometry(ctx, w, h);
     if (r != ORBX_OK) return r;
     ORBX_HIP_CHECK(hipMemcpy2DAsync(ctx->frames + (size_t)first * w * h, (size_t)w, imgs, stride, (size_t)w,
@@ -277,7 +284,7 @@ int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs, in
 int orbx_dev_extract(orbx_ctx* ctx, int first, int count)
 {
     if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || ctx->geom_w <= 0) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ctx->last_first = first;
     ctx->last_count = count;
     return launch_extract(ctx, first, count);
@@ -290,7 +297,7 @@ int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wi
         return ORBX_ERR_ARG;
     if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
     if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     return launch_match_prev(ctx, first, count, seq_len, window, nnratio, check_ori);
 }
 
@@ -303,7 +310,7 @@ int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int
     if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
     if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
     if (ctx->geom_w <= 0) return ORBX_ERR_ARG;
-    (void)hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);   // launch_extract orders against a pending match
     ctx->last_first = first;
     ctx->last_count = count;
     MatchSpec m{mode, seq_len, window, th_low, check_ori, nnratio};
@@ -317,19 +324,27 @@ int orbx_dev_set_split(orbx_ctx* ctx, int enable)
     return ORBX_OK;
 }
 
+int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->async_match = enable != 0;
+    return ORBX_OK;
+}
+
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)
 {
     if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || seq_len <= 0) return ORBX_ERR_ARG;
     if (first % seq_len != 0 && first + count > ((first / seq_len) + 1) * seq_len) return ORBX_ERR_ARG;
     if (((first + count - 1) / seq_len + 1) * seq_len > ctx->slots) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     return launch_match_bf_prev(ctx, first, count, seq_len, th_low, nnratio);
 }
 
 int orbx_dev_sync(orbx_ctx* ctx)
 {
     if (!ctx) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return check_errors(ctx);
 }
@@ -337,7 +352,7 @@ int orbx_dev_sync(orbx_ctx* ctx)
 int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out)
 {
     if (!ctx || slot < 0 || slot >= ctx->slots || !n_out) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     int32_t n = 0;
     ORBX_HIP_CHECK(hipMemcpy(&n, ctx->out_n + slot, sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -354,7 +369,7 @@ int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps, uint8_t*
 int orbx_dev_read_matches(orbx_ctx* ctx, int slot, int32_t* matches12, int cap, int* n_matches, int* n1)
 {
     if (!ctx || slot < 0 || slot >= ctx->slots) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     const int seq_prev_unknown = 0;
     (void)seq_prev_unknown;
@@ -381,7 +396,7 @@ int orbx_dev_kernel_time_enable(orbx_ctx* ctx, int enable)
 int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms, double* total_ms)
 {
     if (!ctx || !name) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     for (auto& t : ctx->timers) {
         if (t.name != name) continue;
@@ -406,7 +421,7 @@ int orbx_dev_read_level(orbx_ctx* ctx, int slot, int level, int blurred, uint8_t
     if (!ctx || level < 0 || level >= ctx->geom.nlevels) return ORBX_ERR_ARG;
     const int f = slot - ctx->last_first;
     if (f < 0 || f >= ctx->last_count) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     const LevelGeom& L = ctx->geom.levels[level];
     *pw = L.pw;

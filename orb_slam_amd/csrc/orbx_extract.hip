@@ -390,26 +390,34 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, int level
 // exactly S (OpenCV 2.4 fast.cpp / fast_score.cpp).  A pixel whose compass
 // pre-test passes in one direction only has S = that direction's arc - 1.
 // ---------------------------------------------------------------------------
-// Best 9-arc minimum of sgn * (v - p_k) (the "dark" arc for sgn = +1, the
-// "bright" arc for sgn = -1).
-__device__ inline int fast_arc(const uint8_t* t, int pitch, int sgn)
+// Best 9-arc minima of d_k = v - p_k ("dark" arc, fl bit 0) and of -d_k
+// ("bright" arc, fl bit 1), both from one set of differences: the bright arc
+// is -(min over 9-arcs of the 9-maximum of d).  Returns the larger of the
+// requested directions' values.
+__device__ inline int fast_arc(const uint8_t* t, int pitch, int fl)
 {
     const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
                          3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
                          -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
                          -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
-    // x_k = sgn * (v - p_k) as one 24-bit multiply-add per ring pixel
-    const int c = sgn * (int)t[0], s = -sgn;
-    int x[16], m3[16];
+    const int v = t[0];
+    int d[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = (int)t[off[k]] * s + c;
-    // min over 9 consecutive = min of three consecutive 3-minima
+    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
+    // 9-minimum / 9-maximum = min / max of three consecutive 3-windows
+    int lo3[16], hi3[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) m3[k] = min(min(x[k], x[(k + 1) & 15]), x[(k + 2) & 15]);
-    int best = -1000;
+    for (int k = 0; k < 16; k++) {
+        lo3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        hi3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    }
+    int dark = -1000, bright = 1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
-    return best;
+    for (int k = 0; k < 16; k++) {
+        dark = max(dark, min(min(lo3[k], lo3[(k + 3) & 15]), lo3[(k + 6) & 15]));
+        bright = min(bright, max(max(hi3[k], hi3[(k + 3) & 15]), hi3[(k + 6) & 15]));
+    }
+    return max((fl & 1) ? dark : -1000, (fl & 2) ? -bright : -1000);
 }
 
 // One workgroup per (cell, frame).  LDS: the cell ROI with dword-aligned rows
@@ -440,6 +448,9 @@ __device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
     return k < 4 ? byte_of(lo, k) : (k < 8 ? byte_of(mid, k - 4) : byte_of(hi, k - 8));
 }
 
+// kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
+// offsets and row strides are immediates; kP == 0: per-cell pitch.
+template <int kP>
 __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -455,8 +466,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     const LevelGeom L = a.levels[C.level];
     const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15, sh = roi_x - x_al;
     const int hx = C.hx, hy = C.hy;
-    const int P = (sh + hx + 15) & ~15, nq = P >> 2;   // tile pitch, dwords per row
-    const int nq16 = P >> 4;                             // 16-byte words per row
+    const int nq16 = (sh + hx + 15) >> 4;               // 16-byte words loaded per row
+    const int P = kP ? kP : 16 * nq16, nq = P >> 2;     // tile pitch, dwords per row
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
     uint8_t* tile = smem;
     uint8_t* sm = smem + tile_pitch_bytes;
@@ -464,27 +475,36 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
     FP_T0();
     auto load_tile = [&]() {
-        stage_to_lds<4>(reinterpret_cast<uint4*>(tile32), hy * nq16, tid, kBlock, [&](int i) {
-            const int r = i / nq16;
-            return *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * (i - r * nq16));
-        });
+        uint4* t16 = reinterpret_cast<uint4*>(tile32);
+        const int n = hy * nq16;
+        for (int u0 = 0; u0 < n; u0 += 4 * kBlock) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = min(u0 + k * kBlock + tid, n - 1), r = i / nq16;
+                v[k] = *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * (i - r * nq16));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = min(u0 + k * kBlock + tid, n - 1), r = i / nq16;
+                t16[r * (P >> 4) + (i - r * nq16)] = v[k];
+            }
+        }
     };
     load_tile();
-    // S' is 0 outside the interior rows [3, hy-4]; the interior rows are
-    // fully rewritten below
-    for (int i = tid; i < nq; i += kBlock) {
-        sm32[2 * nq + i] = 0;
-        sm32[(hy - 3) * nq + i] = 0;
-    }
+    // S' is 0 outside the interior rows [3, hy-4] and outside the dwords
+    // that hold interior columns; the interior units are rewritten below
+    for (int i = tid; i < hy * (P >> 4); i += kBlock) reinterpret_cast<uint4*>(sm32)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
-    const int nunits = (hy - 6) * nq;
+    const int q0 = c_lo >> 2, nqe = (c_hi >> 2) - q0 + 1; // dwords holding them
+    const int nunits = (hy - 6) * nqe;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {
-        RowWalk cw_(wv * 64 + lane, kBlock, nq);
+        RowWalk cw_(wv * 64 + lane, kBlock, nqe);
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
             const int u = u0 + lane;
-            const int r = 3 + cw_.r, q = cw_.q;
+            const int r = 3 + cw_.r, q = q0 + cw_.q;
             int mask = 0;
             if (u < nunits) {
                 const uint32_t* row = tile32 + r * nq + q;
@@ -549,8 +569,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 const uint32_t cw = i < ntot ? cand[wv][i] : 0u;
                 const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
                 int S = 0;
-                if (fl) S = fast_arc(tile + pos, P, (fl & 1) ? 1 : -1);
-                if (__any(fl == 3) && fl == 3) S = max(S, fast_arc(tile + pos, P, -1));
+                if (fl) S = fast_arc(tile + pos, P, fl);
                 S -= 1;
                 if (fl) sm[pos] = (uint8_t)(S >= tmin ? S : 0);
             }
@@ -564,9 +583,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     auto nms_pass = [&]() {
         // non-max suppression: keep S' if it beats all 8 neighbours' S'
         int c1 = 0;
-        RowWalk nw(tid, kBlock, nq);
+        RowWalk nw(tid, kBlock, nqe);
         for (int u = tid; u < nunits; u += kBlock, nw.next()) {
-            const int r = 3 + nw.r, q = nw.q;
+            const int r = 3 + nw.r, q = q0 + nw.q;
             uint32_t word = 0;
             const uint32_t* m = sm32 + r * nq + q;
             const uint32_t mid = m[0];
@@ -641,13 +660,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     const int ua = min(tid * per, nunits), ub = min(ua + per, nunits);
     int cnt = 0;
     {
-        int r = 3 + ua / nq, q = ua - (r - 3) * nq;
+        int r = 3 + ua / nqe, q = q0 + ua - (r - 3) * nqe;
         for (int u = ua; u < ub; u++) {
             const uint32_t word = tile32[r * nq + q];
 #pragma unroll
             for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
-            if (++q == nq) {
-                q = 0;
+            if (++q == q0 + nqe) {
+                q = q0;
                 r++;
             }
         }
@@ -655,7 +674,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     int base;
     int off = block_exclusive_scan(cnt, &base, bs, 1);
     if (cnt) {
-        int r = 3 + ua / nq, q = ua - (r - 3) * nq;
+        int r = 3 + ua / nqe, q = q0 + ua - (r - 3) * nqe;
         for (int u = ua; u < ub; u++) {
             const uint32_t word = tile32[r * nq + q];
 #pragma unroll
@@ -669,8 +688,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                     off++;
                 }
             }
-            if (++q == nq) {
-                q = 0;
+            if (++q == q0 + nqe) {
+                q = q0;
                 r++;
             }
         }
@@ -1178,8 +1197,26 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         }
         timer_begin(ctx, "fast", st);
         {
-            const int pitch = (g.max_tile_bytes + 15) & ~15;
-            hipLaunchKernelGGL(k_fast_cells, dim3((int)g.cells.size(), nb), dim3(256), 2 * pitch, st, x, pitch);
+            // widest aligned cell row and tallest cell pick the tile pitch
+            int wmax = 0, hmax = 0;
+            for (const CellGeom& c : g.cells) {
+                if (!c.valid) continue;
+                wmax = std::max(wmax, (15 + c.hx + 15) & ~15);
+                hmax = std::max(hmax, c.hy);
+            }
+            const dim3 grid((int)g.cells.size(), nb);
+            auto fast = [&](auto kern, int P) {
+                const int bytes = (hmax * P + 15) & ~15;
+                hipLaunchKernelGGL(kern, grid, dim3(256), 2 * bytes, st, x, bytes);
+            };
+            if (wmax <= 96) fast(k_fast_cells<96>, 96);
+            else if (wmax <= 144) fast(k_fast_cells<144>, 144);
+            else if (wmax <= 208) fast(k_fast_cells<208>, 208);
+            else if (wmax <= 336) fast(k_fast_cells<336>, 336);
+            else {
+                const int pitch = (g.max_tile_bytes + 15) & ~15;
+                hipLaunchKernelGGL(k_fast_cells<0>, grid, dim3(256), 2 * pitch, st, x, pitch);
+            }
         }
         timer_end(ctx, "fast", st);
         timer_begin(ctx, "retain", st);
@@ -1239,6 +1276,39 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     // internal frame pairs are matched on its own stream, the pairs that
     // straddle the halves after the join.
     a.first_slot = first;
+    const bool async = m && m->kind != 0 && ctx->async_match && ctx->mstream;
+    // outputs of [first, first + count) are rewritten: a pending match that
+    // reads any of them must finish first
+    if (ctx->pend_hi > ctx->pend_lo) {
+        if (first < ctx->pend_hi && first + count > ctx->pend_lo) {
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
+            ctx->pend_lo = ctx->pend_hi = 0;
+        }
+    }
+    if (async) {
+        // extraction (split as usual) on the extraction streams; the whole
+        // batch's matching on mstream once it is extracted, overlapping the
+        // next call's extraction of other slots
+        const int r = launch_extract(ctx, first, count, nullptr);
+        if (r != ORBX_OK) return r;
+        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream));
+        ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
+        match_runs(first, first + count, 0, -1, ctx->mstream);
+        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_matched, ctx->mstream));
+        // the match reads the outputs of the batch's sequences
+        const int q = m->seq_len;
+        const int lo = (first / q) * q, hi = ((first + count + q - 1) / q) * q;
+        if (ctx->pend_hi > ctx->pend_lo) {   // an older match on mstream precedes this one
+            ctx->pend_lo = std::min(ctx->pend_lo, lo);
+            ctx->pend_hi = std::max(ctx->pend_hi, hi);
+        } else {
+            ctx->pend_lo = lo;
+            ctx->pend_hi = hi;
+        }
+        if (err != ORBX_OK) return err;
+        if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
+        return ORBX_OK;
+    }
     if (ctx->split && count >= 2 * kSplitMinFrames && ctx->stream2) {
         const int n0 = count / 2, n1 = count - n0;
         ExtractArgs b = a;

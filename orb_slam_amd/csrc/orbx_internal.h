@@ -128,6 +128,13 @@ struct orbx_ctx {
     hipStream_t stream2 = nullptr;      // second half of large extraction batches
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool split = true;                  // run large batches as two concurrent halves
+    // Asynchronous matching (orbx_dev_set_async_match): the matching of an
+    // extract_match call runs on mstream while later calls extract other
+    // slots; [pend_lo, pend_hi) are the slots that match still reads.
+    hipStream_t mstream = nullptr;
+    hipEvent_t ev_extracted = nullptr, ev_matched = nullptr;
+    bool async_match = false;
+    int pend_lo = 0, pend_hi = 0;
     orbx::Geometry geom;
     orbx::DeviceGeometry dgeom;
     int max_w = 0, max_h = 0, slots = 0;
@@ -195,3 +202,14 @@ int ensure_pinned(orbx_ctx* ctx, size_t bytes);
         hipError_t _e = (expr);                           \
         if (_e != hipSuccess) return ORBX_ERR_HIP;        \
     } while (0)
+
+// Entry of every API call that touches the context's device state: select
+// the device and order ctx->stream after a pending asynchronous match.
+inline void ctx_enter(orbx_ctx* ctx)
+{
+    (void)hipSetDevice(ctx->device);
+    if (ctx->pend_hi > ctx->pend_lo) {
+        (void)hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0);
+        ctx->pend_lo = ctx->pend_hi = 0;
+    }
+}

@@ -844,7 +844,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
                 p.edge_pose[e] >= p.n_poses)
                 return ORBX_ERR_ARG;
     }
-    (void)hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     // persistent per-problem device state: poses, points, errors, counters
     std::vector<long long> offs(3 * P);
     Packer base;

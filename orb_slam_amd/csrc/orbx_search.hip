@@ -490,7 +490,7 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
 {
     if (!ctx || !valid_view(F1) || !valid_view(F2) || !prev_matched || !matches12 || !n_matches || window < 0)
         return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t op = u.reserve((size_t)F1->n * 8), oo = u.reserve((size_t)F1->n * 4 + 4), on = u.reserve(4);
@@ -535,7 +535,7 @@ int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_fram
 {
     if (!ctx || !valid_view(F1) || !valid_view(F2) || !f1_mp || !matches21 || !n_matches || window < 0)
         return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t ov = u.reserve(F1->n), oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
@@ -569,7 +569,7 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     if (!ctx || !valid_view(F1) || !valid_view(F2) || !f1_mp_xyz || !f1_mp_valid || !f2_assigned || !Tcw2 || !cam ||
         !matches21 || !n_matches || window < 0)
         return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t ox = u.reserve((size_t)F1->n * 12), ov = u.reserve(F1->n), oa = u.reserve(F2->n);
@@ -607,7 +607,7 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     if (!ctx || !valid_view(Cur) || !valid_view(Last) || !last_mp_xyz || !last_mp_valid || !cur_assigned || !Tcw ||
         !cam || !matches_cur || !n_matches)
         return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs oL = reserve_frame(u, Last), oC = reserve_frame(u, Cur);
     const size_t ox = u.reserve((size_t)Last->n * 12), ov = u.reserve(Last->n), oa = u.reserve(Cur->n);
@@ -649,7 +649,7 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
         return ORBX_ERR_ARG;
     for (int m = 0; m < n_mp; m++)
         if (in_view[m] && (pred_level[m] < 0 || pred_level[m] >= F->nlevels)) return ORBX_ERR_ARG;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs oF = reserve_frame(u, F);
     const size_t ov = u.reserve(n_mp), op = u.reserve((size_t)n_mp * 8), ol = u.reserve((size_t)n_mp * 4);
@@ -688,7 +688,7 @@ static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8
 {
     if (!ctx || nA < 0 || nB < 0 || (nA && (!dA || !best_idx || !best || !second)) || (nB && !dB)) return ORBX_ERR_ARG;
     if (nA == 0) return ORBX_OK;
-    hipSetDevice(ctx->device);
+    ctx_enter(ctx);
     Uploader u{ctx};
     const size_t oa = u.reserve((size_t)nA * 32), ob = u.reserve((size_t)nB * 32);
     const size_t oi = u.reserve((size_t)nA * 4), o1 = u.reserve((size_t)nA * 4), o2 = u.reserve((size_t)nA * 4);

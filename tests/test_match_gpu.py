@@ -99,3 +99,32 @@ def test_extract_match_pipeline_equals_separate_calls(mode, seq_len):
         assert np.array_equal(k.view(np.uint8), feats[s][0].view(np.uint8)) and np.array_equal(d, feats[s][1])
         assert n == piped[s][1] and np.array_equal(m[:len(k)], piped[s][0][:len(k)]), s
     ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["init", "bf"])
+def test_async_extract_match_alternating_slots(mode):
+    """Asynchronous matching (orbx_dev_set_async_match): batches alternating
+    between two slot ranges, each batch's matching overlapping the next
+    batch's extraction, give the synchronous calls' results."""
+    w, h, B = 640, 480, 32
+    frames = synth.sequence(w, h, 2 * B, seed=17)
+    ctx = ox.Context(nfeatures=1000, max_w=w, max_h=h, slots=2 * B)
+    ctx.upload(frames)
+    ctx.set_async_match(True)
+    for it in range(3):
+        ctx.extract_match((it % 2) * B, B, B, mode=mode)
+    ctx.sync()
+    got = [ctx.matches(s) for s in range(2 * B)]
+    ctx.set_async_match(False)
+    for first in (0, B):
+        ctx.extract(first, B)
+        if mode == "init":
+            ctx.match_prev(first, B, B)
+        else:
+            ctx.match_bf_prev(first, B, B)
+    ctx.sync()
+    for s in range(2 * B):
+        m, n = ctx.matches(s)
+        k, _ = ctx.features(s)
+        assert n == got[s][1] and np.array_equal(m[:len(k)], got[s][0][:len(k)]), s
+    ctx.close()
