@@ -850,22 +850,24 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
 // slides a 7-row window of horizontal sums down it in registers: one pass
 // over the input rows it needs, one dword store per output row, no LDS.
 // ---------------------------------------------------------------------------
+// Horizontal 7-tap sums of the 4 pixels of dword wc (wl / wr: the dwords to
+// its left / right): taps j-3..j as one v_dot4_u32_u8 with {18,34,49,55},
+// taps j+1..j+3 as a second with {49,34,18,0}.
+__device__ inline void blur_hsum_w(uint32_t wl, uint32_t wc, uint32_t wr, int hs[4])
+{
+    constexpr uint32_t kWA = 0x37312212u, kWB = 0x00122231u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t A = j == 3 ? wc : __builtin_amdgcn_alignbyte(wc, wl, j + 1);   // bytes j-3 .. j
+        const uint32_t B = j == 3 ? wr : __builtin_amdgcn_alignbyte(wr, wc, j + 1);   // bytes j+1 .. j+4
+        hs[j] = (int)__builtin_amdgcn_udot4(B, kWB, __builtin_amdgcn_udot4(A, kWA, 0u, false), false);
+    }
+}
+
 __device__ inline void blur_hsum(const uint8_t* row, int x, int hs[4])
 {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(row + x);
-    const uint32_t wl = w[-1], wc = w[0], wr = w[1];
-    int b[12];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        b[k] = (wl >> (8 * k)) & 0xFF;
-        b[4 + k] = (wc >> (8 * k)) & 0xFF;
-        b[8 + k] = (wr >> (8 * k)) & 0xFF;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int c = 4 + j;
-        hs[j] = 55 * b[c] + 49 * (b[c - 1] + b[c + 1]) + 34 * (b[c - 2] + b[c + 2]) + 18 * (b[c - 3] + b[c + 3]);
-    }
+    blur_hsum_w(w[-1], w[0], w[1], hs);
 }
 
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
@@ -927,21 +929,7 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
             for (int k = 0; k < kBlurChunk; k++) {
                 const int y = yc + k;
                 if (y >= yb) break;
-                {
-                    int b[12];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        b[j] = (wl[k] >> (8 * j)) & 0xFF;
-                        b[4 + j] = (wc[k] >> (8 * j)) & 0xFF;
-                        b[8 + j] = (wr[k] >> (8 * j)) & 0xFF;
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int c = 4 + j;
-                        R[6][j] = 55 * b[c] + 49 * (b[c - 1] + b[c + 1]) + 34 * (b[c - 2] + b[c + 2]) +
-                                  18 * (b[c - 3] + b[c + 3]);
-                    }
-                }
+                blur_hsum_w(wl[k], wc[k], wr[k], R[6]);
                 uint32_t word = 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -950,15 +938,11 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
                     if (xi >= 0 && xi < L.w) {
                         const int N = 55 * R[3][j] + 49 * (R[2][j] + R[4][j]) + 34 * (R[1][j] + R[5][j]) +
                                       18 * (R[0][j] + R[6][j]);
-                        int q;
-                        if (xi < L.nvec_blur) {   // float path: exact N/2^16, cvtps2dq rounding
-                            q = N >> 16;
-                            const int rem = N & 0xFFFF;
-                            if (rem > 0x8000 || (rem == 0x8000 && (q & 1))) q++;
-                        } else {
-                            q = (N + (1 << 15)) >> 16;
-                        }
-                        v = (uint32_t)sat_u8(q);
+                        // Columns < nvec: float path, N / 2^16 rounded half to even
+                        // (cvtps2dq); the tail: FixedPtCastEx, +2^15 >> 16.  The
+                        // taps sum to 257, so N can exceed 255 * 2^16: saturate
+                        const int half = xi < L.nvec_blur ? 0x7FFF + ((N >> 16) & 1) : 0x8000;
+                        v = (uint32_t)min((N + half) >> 16, 255);
                     }
                     word |= v << (8 * j);
                 }
