@@ -171,12 +171,14 @@ def run_frames(args, wl, rank, local, world, dist):
     # Diagnostic pass after the timed region: the same steps with the two
     # extraction halves serialised, so each kernel's launch time is not shared
     # with the other stream's kernels (per-kernel roofline without overlap).
-    ctx.set_split(False)
-    ctx.set_async_match(False)
-    iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
-    _, iso = timed(iso_args, ctx, step, None, names)
-    ctx.set_split(True)
-    ctx.set_async_match(not args.sync_match)
+    iso = {}
+    if not args.no_isolated:
+        ctx.set_split(False)
+        ctx.set_async_match(False)
+        iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
+        _, iso = timed(iso_args, ctx, step, None, names)
+        ctx.set_split(True)
+        ctx.set_async_match(not args.sync_match)
     kernels = {"overlapped": kernels, "isolated": iso}
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
@@ -236,6 +238,30 @@ def run_lba(args, wl, rank, local, world, dist):
     return stats, kernels, ab, units_per_launch, cpu, check, cfg
 
 
+# bench timer name -> kernel symbol in the rocprofv3 CSVs
+KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": "k_pyr_resize", "fast": "k_fast_cells",
+                 "retain": "k_retain_cells", "blur": "k_blur", "describe": "k_describe",
+                 "match": "k_match_", "lba_iter": "k_lba_iteration", "lba_outliers": "k_lba_outliers"}
+
+
+def pmc_traffic(workload, name):
+    """HBM bytes per launch of kernel `name` from the committed PMC summary
+    of this bench command (profiles/r01_<workload>_pmc_hbm.json, written by
+    tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes of
+    `bench.py --no-isolated`): FETCH_SIZE x2 (gfx950 wide-read correction,
+    MI355X_MICROARCH.md HBM section) + WRITE_SIZE.  None when absent."""
+    path = Path(__file__).resolve().parent / "profiles" / f"r01_{workload}_pmc_hbm.json"
+    sym = KERNEL_SYMBOL.get(name)
+    if not path.exists() or not sym:
+        return {"traffic": None}
+    summary = json.loads(path.read_text())
+    hits = [v for k, v in summary.items() if sym in k]
+    if not hits:
+        return {"traffic": None}
+    return {"traffic": round(sum(h["hbm_bytes_fetch_x2"] for h in hits) / len(hits)),
+            "traffic_source": f"profiles/{path.name} (FETCH_SIZE x2 + WRITE_SIZE, per dispatch)"}
+
+
 def timed(args, ctx, step, dist, names):
     def barrier():
         if dist is not None:
@@ -270,6 +296,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the serialised per-kernel pass after the timed steps (PMC collection)")
     ap.add_argument("--sync-match", action="store_true",
                     help="match each batch after its extraction on the same stream (no overlap with the next "
                          "batch's extraction)")
@@ -294,6 +322,11 @@ def main():
 
     if rank == 0:
         def roofline(kern, steps):
+            roof = roofline_events(kern, steps)
+            roof.update(pmc_traffic(args.workload, roof["kernel"]))
+            return roof
+
+        def roofline_events(kern, steps):
             # dominant kernel: largest total time; its algorithmic bytes per
             # launch over its mean launch duration (HIP events on the stream
             # the kernel is launched on)

@@ -477,18 +477,21 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     auto load_tile = [&]() {
         uint4* t16 = reinterpret_cast<uint4*>(tile32);
         const int n = hy * nq16;
+        // four independent loads per round (named registers: an array here
+        // was kept in scratch memory), then the LDS stores
         for (int u0 = 0; u0 < n; u0 += 4 * kBlock) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int i = min(u0 + k * kBlock + tid, n - 1), r = i / nq16;
-                v[k] = *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * (i - r * nq16));
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int i = min(u0 + k * kBlock + tid, n - 1), r = i / nq16;
-                t16[r * (P >> 4) + (i - r * nq16)] = v[k];
-            }
+            const int i0 = min(u0 + tid, n - 1), i1 = min(u0 + kBlock + tid, n - 1);
+            const int i2 = min(u0 + 2 * kBlock + tid, n - 1), i3 = min(u0 + 3 * kBlock + tid, n - 1);
+            const int r0 = i0 / nq16, r1 = i1 / nq16, r2 = i2 / nq16, r3 = i3 / nq16;
+            const int c0 = i0 - r0 * nq16, c1 = i1 - r1 * nq16, c2 = i2 - r2 * nq16, c3 = i3 - r3 * nq16;
+            const uint4 v0 = *reinterpret_cast<const uint4*>(src + (size_t)r0 * L.stride + 16 * c0);
+            const uint4 v1 = *reinterpret_cast<const uint4*>(src + (size_t)r1 * L.stride + 16 * c1);
+            const uint4 v2 = *reinterpret_cast<const uint4*>(src + (size_t)r2 * L.stride + 16 * c2);
+            const uint4 v3 = *reinterpret_cast<const uint4*>(src + (size_t)r3 * L.stride + 16 * c3);
+            t16[r0 * (P >> 4) + c0] = v0;
+            t16[r1 * (P >> 4) + c1] = v1;
+            t16[r2 * (P >> 4) + c2] = v2;
+            t16[r3 * (P >> 4) + c3] = v3;
         }
     };
     load_tile();
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 if (s >= t && s > 0) {
                     if (off < C.list_cap) {
                         const int cc = 4 * q + j - sh;   // ROI column
-                        out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                        sm32[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
                     }
                     off++;
                 }
@@ -694,6 +697,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             }
         }
     }
+    // the list was assembled in the (no longer needed) S' map area; copy it
+    // out with consecutive lanes on consecutive dwords (list_cap <= the
+    // map's dword capacity: ceil(iw/2) * ceil(ih/2) <= hx * hy / 4)
+    __syncthreads();
+    for (int i = tid; i < min(base, C.list_cap); i += kBlock) out[i] = sm32[i];
     if (tid == 0) {
         *count_out = base;
         if (base > C.list_cap) atomicOr(a.error_flags, 1);
