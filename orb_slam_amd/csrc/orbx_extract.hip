@@ -455,7 +455,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
-    __shared__ uint32_t cand[kWaves][256];   // tile position | direction flags << 16
+    constexpr int kCandRing = 512;           // > 63 waiting + 256 new per iteration
+    __shared__ uint32_t cand[kWaves][kCandRing];
     const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
@@ -504,6 +505,16 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     const int nunits = (hy - 6) * nqe;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {
+        // per-wave ring of compass survivors (tile position | direction
+        // flags << 16), scored 64 at a time with every lane busy
+        int qh = 0, qt = 0;
+        auto score_batch = [&](uint32_t cw) {
+            const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
+            if (fl) {
+                const int S = fast_arc(tile + pos, P, fl) - 1;
+                sm[pos] = (uint8_t)(S >= tmin ? S : 0);
+            }
+        };
         RowWalk cw_(wv * 64 + lane, kBlock, nqe);
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
             const int u = u0 + lane;
@@ -547,7 +558,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 // interior columns only
                 const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
                 mask = (j1 < j0) ? 0 : (mask & (((1 << (2 * (j1 + 1))) - 1) & ~((1 << (2 * j0)) - 1)));
-                sm32[r * nq + q] = 0;
             }
             const int cnt = __popc((mask | (mask >> 1)) & 0x55);
             const int incl = wave_inclusive_scan(cnt);
@@ -556,30 +566,31 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             if (lane == 0) FP_ADD(10 + (tmin < 10), ntot);
             if (lane == 0) FP_ADD(12, 1);
 #endif
-            int w = incl - cnt;
+            int w = qt + incl - cnt;
             if (mask) {
     #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const int fl = (mask >> (2 * j)) & 3;
-                    if (fl) cand[wv][w++] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
+                    if (fl) cand[wv][(w++) & (kCandRing - 1)] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
                 }
             }
+            qt += ntot;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int i0 = 0; i0 < ntot; i0 += 64) {
-                const int i = i0 + lane;
-                const uint32_t cw = i < ntot ? cand[wv][i] : 0u;
-                const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
-                int S = 0;
-                if (fl) S = fast_arc(tile + pos, P, fl);
-                S -= 1;
-                if (fl) sm[pos] = (uint8_t)(S >= tmin ? S : 0);
+            // score only full waves of candidates; the rest waits in the ring
+            while (qt - qh >= 64) {
+                score_batch(cand[wv][(qh + lane) & (kCandRing - 1)]);
+                qh += 64;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        if (qt > qh) score_batch(lane < qt - qh ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // non-max suppression over the S' map (kept S' written over the tile);
     // returns this thread's count of kept corners at fastTh
