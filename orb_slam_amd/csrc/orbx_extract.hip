@@ -595,45 +595,68 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     // non-max suppression over the S' map (kept S' written over the tile);
     // returns this thread's count of kept corners at fastTh
     auto nms_pass = [&]() {
-        // non-max suppression: keep S' if it beats all 8 neighbours' S'
+        // non-max suppression: keep S' if it beats all 8 neighbours' S'.
+        // Units whose S' word is zero keep nothing (their tile word is
+        // cleared on the spot); the others are queued per wave in the
+        // candidate ring (tile word index) and suppressed 64 at a time.
         int c1 = 0;
-        RowWalk nw(tid, kBlock, nqe);
-        for (int u = tid; u < nunits; u += kBlock, nw.next()) {
-            const int r = 3 + nw.r, q = q0 + nw.q;
-            uint32_t word = 0;
-            const uint32_t* m = sm32 + r * nq + q;
+        const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
+        auto nms_unit = [&](int idx) {
+            if (idx < 0) return;
+            const int q = idx % nq;
+            const uint32_t* m = sm32 + idx;
             const uint32_t mid = m[0];
-            if (mid) {
-                // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
-                // rows r-1, r, r+1), byte-wise max on even / odd u16x2 halves
-                uint32_t nb[8];
-                int k = 0;
-    #pragma unroll
-                for (int dr = 0; dr < 3; dr++) {
-                    const uint32_t* mr = m + (dr - 1) * nq;
-                    const uint32_t lo = q > 0 ? mr[-1] : 0u, mm = mr[0], hi = q + 1 < nq ? mr[1] : 0u;
-                    nb[k++] = __builtin_amdgcn_alignbyte(mm, lo, 3);   // j-1
-                    if (dr != 1) nb[k++] = mm;
-                    nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
-                }
-                const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
-    #pragma unroll
-                for (int hf = 0; hf < 2; hf++) {
-                    const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
-                    uint32_t mx = __builtin_amdgcn_perm(0u, nb[0], sel);
-    #pragma unroll
-                    for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
-                    const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
-                    // keep where mx - s < 0 (s > every neighbour)
-                    const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
-                    const uint32_t kept = sv & keep;
-                    word |= kept << (8 * hf);
-                    // corners at fastTh among the kept (kept >= max(fastTh, 1))
-                    c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
-                }
+            // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
+            // rows r-1, r, r+1), byte-wise max on even / odd u16x2 halves
+            uint32_t nb[8];
+            int k = 0;
+#pragma unroll
+            for (int dr = 0; dr < 3; dr++) {
+                const uint32_t* mr = m + (dr - 1) * nq;
+                const uint32_t lo = q > 0 ? mr[-1] : 0u, mm = mr[0], hi = q + 1 < nq ? mr[1] : 0u;
+                nb[k++] = __builtin_amdgcn_alignbyte(mm, lo, 3);   // j-1
+                if (dr != 1) nb[k++] = mm;
+                nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
             }
-            tile32[r * nq + q] = word;
+            uint32_t word = 0;
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
+                uint32_t mx = __builtin_amdgcn_perm(0u, nb[0], sel);
+#pragma unroll
+                for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
+                const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
+                // keep where mx - s < 0 (s > every neighbour)
+                const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
+                const uint32_t kept = sv & keep;
+                word |= kept << (8 * hf);
+                // corners at fastTh among the kept (kept >= max(fastTh, 1))
+                c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
+            }
+            tile32[idx] = word;
+        };
+        int qh = 0, qt = 0;
+        RowWalk nw(wv * 64 + lane, kBlock, nqe);
+        for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, nw.next()) {
+            const int u = u0 + lane;
+            const int idx = (3 + nw.r) * nq + q0 + nw.q;
+            const uint32_t mid = u < nunits ? sm32[idx] : 0u;
+            if (u < nunits && !mid) tile32[idx] = 0;
+            const unsigned long long bal = __ballot(mid != 0);
+            if (mid) cand[wv][(qt + __popcll(bal & ((1ull << lane) - 1))) & (kCandRing - 1)] = (uint32_t)idx;
+            qt += __popcll(bal);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            while (qt - qh >= 64) {
+                nms_unit((int)cand[wv][(qh + lane) & (kCandRing - 1)]);
+                qh += 64;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        if (qt > qh) nms_unit(lane < qt - qh ? (int)cand[wv][(qh + lane) & (kCandRing - 1)] : -1);
         return c1;
     };
     // Thresholds (:599-614): FAST(fastTh), and FAST(7) when that finds <= 3
