@@ -664,9 +664,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     // (NMS against S' equals NMS against the t-score map for corners >= t),
     // so a cell is scored at fastTh first (far fewer compass survivors) and
     // rescored at 7 only when it needs the fallback.
-    int n1;
+    int n1, tmin_final;
     FP_MARK(0);
     if (a.fast_th > a.fast_th_low) {
+        tmin_final = a.fast_th;
         score_pass(a.fast_th);
         __syncthreads();
         FP_MARK(1);
@@ -677,6 +678,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             __syncthreads();
             load_tile();
             __syncthreads();
+            tmin_final = a.fast_th_low;
             score_pass(a.fast_th_low);
             __syncthreads();
             nms_pass();
@@ -684,6 +686,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             FP_MARK(3);
         }
     } else {
+        tmin_final = a.fast_th;
         score_pass(a.fast_th);
         __syncthreads();
         n1 = block_sum(nms_pass(), bs, 0);
@@ -698,10 +701,20 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     int cnt = 0;
     {
         int r = 3 + ua / nqe, q = q0 + ua - (r - 3) * nqe;
+        // kept bytes are S' >= tmin of the final score pass; t == tmin there
+        // unless fastTh < 7 fell back to 7 (then compare each byte)
+        const bool all_nonzero = t == tmin_final;
         for (int u = ua; u < ub; u++) {
             const uint32_t word = tile32[r * nq + q];
+            if (all_nonzero) {
+                uint32_t x = word | (word >> 4);
+                x |= x >> 2;
+                x |= x >> 1;
+                cnt += __popc(x & 0x01010101u);
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
+                for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
+            }
             if (++q == q0 + nqe) {
                 q = q0;
                 r++;
