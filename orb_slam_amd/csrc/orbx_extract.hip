@@ -935,8 +935,12 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
     const int strip = item / tl.z, dw = item - strip * tl.z;
     const int x = dw * 4;
     const int y0 = strip * kBlurStrip, y1 = min(y0 + kBlurStrip, L.ph);
+    // uniform level bases + 32-bit per-lane offsets (saddr + voffset loads)
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
     uint8_t* dst = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
+    const uint32_t stride = (uint32_t)L.stride;
+    auto ld = [&](int y, int dx) { return *reinterpret_cast<const uint32_t*>(src + ((uint32_t)y * stride + (uint32_t)x) + dx); };
+    auto st = [&](int y, uint32_t v) { *reinterpret_cast<uint32_t*>(dst + ((uint32_t)y * stride + (uint32_t)x)) = v; };
     // interior columns / rows of this level in padded coordinates
     const int ix0 = kEdge, ix1 = kEdge + L.w, iy0 = kEdge, iy1 = kEdge + L.h;
     const bool col_interior = (x + 3 >= ix0) && (x < ix1);
@@ -953,59 +957,76 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
         for (int yc = ylo; yc < yhi; yc += 4) {
             uint32_t v[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                v[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)min(yc + k, yhi - 1) * L.stride + x);
+            for (int k = 0; k < 4; k++) v[k] = ld(min(yc + k, yhi - 1), 0);
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                if (yc + k < yhi) *reinterpret_cast<uint32_t*>(dst + (size_t)(yc + k) * L.stride + x) = v[k] & keep_mask;
+                if (yc + k < yhi) st(yc + k, v[k] & keep_mask);
         }
     };
     copy_rows(y0, min(ya, y1));
     if (ya < yb) {
-        int R[7][4];
+        // per column: float path (round half to even) below nvec, else +2^15
+        int half_even[4];
+        bool inside[4];
 #pragma unroll
-        for (int k = 0; k < 6; k++) blur_hsum(src + (size_t)(ya - 3 + k) * L.stride, x, R[k]);
-        // chunks of kBlurChunk output rows: the chunk's input rows (y + 3) and
-        // raw centre words are loaded together, then filtered from registers
-        constexpr int kBlurChunk = 8;
+        for (int j = 0; j < 4; j++) {
+            const int xi = x + j - kEdge;
+            inside[j] = xi >= 0 && xi < L.w;
+            half_even[j] = xi < L.nvec_blur;
+        }
+        int R[7][4];
+        uint32_t C[3];   // raw centre words of rows y, y+1, y+2 (loaded as rows y'+3 earlier)
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const uint32_t wc = ld(ya - 3 + k, 0);
+            blur_hsum_w(ld(ya - 3 + k, -4), wc, ld(ya - 3 + k, 4), R[k]);
+            if (k >= 3) C[k - 3] = wc;
+        }
+        // chunks of 7 output rows (the window's period: the register
+        // rotation needs no moves); the chunk's input rows y + 3 are loaded
+        // together, then filtered from registers
+        constexpr int kBlurChunk = 7;
         for (int yc = ya; yc < yb; yc += kBlurChunk) {
-            uint32_t wl[kBlurChunk], wc[kBlurChunk], wr[kBlurChunk], raw[kBlurChunk];
+            uint32_t wl[kBlurChunk], wc[kBlurChunk], wr[kBlurChunk];
 #pragma unroll
             for (int k = 0; k < kBlurChunk; k++) {
                 // rows past yb + 2 repeat the last one (never used)
-                const int yy = min(yc + k, yb - 1);
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + (size_t)(yy + 3) * L.stride + x);
-                wl[k] = w[-1];
-                wc[k] = w[0];
-                wr[k] = w[1];
-                raw[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)yy * L.stride + x);
+                const int yy = min(yc + k, yb - 1) + 3;
+                wl[k] = ld(yy, -4);
+                wc[k] = ld(yy, 0);
+                wr[k] = ld(yy, 4);
             }
 #pragma unroll
             for (int k = 0; k < kBlurChunk; k++) {
+                // rows past yb are computed on repeated input and not stored:
+                // no early exit, so the window rotation stays straight-line
                 const int y = yc + k;
-                if (y >= yb) break;
                 blur_hsum_w(wl[k], wc[k], wr[k], R[6]);
+                const uint32_t raw = C[0];
                 uint32_t word = 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const int xi = x + j - kEdge;
-                    uint32_t v = (raw[k] >> (8 * j)) & 0xFF;
-                    if (xi >= 0 && xi < L.w) {
-                        const int N = 55 * R[3][j] + 49 * (R[2][j] + R[4][j]) + 34 * (R[1][j] + R[5][j]) +
-                                      18 * (R[0][j] + R[6][j]);
+                    uint32_t v = (raw >> (8 * j)) & 0xFF;
+                    if (inside[j]) {
+                        // 24-bit multiplies: R <= 255 * 257
+                        const uint32_t N = __umul24(R[3][j], 55u) + __umul24(R[2][j] + R[4][j], 49u) +
+                                           __umul24(R[1][j] + R[5][j], 34u) + __umul24(R[0][j] + R[6][j], 18u);
                         // Columns < nvec: float path, N / 2^16 rounded half to even
                         // (cvtps2dq); the tail: FixedPtCastEx, +2^15 >> 16.  The
                         // taps sum to 257, so N can exceed 255 * 2^16: saturate
-                        const int half = xi < L.nvec_blur ? 0x7FFF + ((N >> 16) & 1) : 0x8000;
-                        v = (uint32_t)min((N + half) >> 16, 255);
+                        const uint32_t half = half_even[j] ? 0x7FFFu + ((N >> 16) & 1u) : 0x8000u;
+                        v = min((N + half) >> 16, 255u);
                     }
                     word |= v << (8 * j);
                 }
-                *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.stride + x) = word & keep_mask;
+                if (y < yb) st(y, word & keep_mask);
 #pragma unroll
                 for (int kk = 0; kk < 6; kk++)
 #pragma unroll
                     for (int j = 0; j < 4; j++) R[kk][j] = R[kk + 1][j];
+                C[0] = C[1];
+                C[1] = C[2];
+                C[2] = wc[k];
             }
         }
     }

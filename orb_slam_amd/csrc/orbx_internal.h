@@ -38,7 +38,7 @@ constexpr int kPatch = 31;       // PATCH_SIZE (:75)
 constexpr int kMaxLevels = 16;
 constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
 constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
-constexpr int kBlurStrip = 32;   // output rows per blur thread (rolling window)
+constexpr int kBlurStrip = 28;   // output rows per blur thread (rolling window; 4 chunks of 7)
 constexpr int kBlurItems = 256;  // blur items (strip x dword column) per block
 
 constexpr int kResRows = 16;   // output rows per staged resize strip (k_pyr_resize_lds)
