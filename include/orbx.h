@@ -151,6 +151,9 @@ int orbx_dev_read_matches(orbx_ctx* ctx, int slot, int32_t* matches12, int cap,
 int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms,
                          double* total_ms);
 int orbx_dev_kernel_time_enable(orbx_ctx* ctx, int enable);
+/* Restrict kernel timing to the launches of one timer name (NULL or "":
+ * all), so a timed region carries only the events it reports. */
+int orbx_dev_kernel_time_select(orbx_ctx* ctx, const char* name);
 
 /* Debug / parity taps: padded pyramid level (raw or blurred) of a slot.
  * Writes (w_l+32)*(h_l+32) bytes; *pw, *ph receive the padded size. */

@@ -78,6 +78,7 @@ def _declare(L):
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
         "orbx_dev_kernel_time": ([vp, ctypes.c_char_p, dp, dp], i),
         "orbx_dev_kernel_time_enable": ([vp, i], i),
+        "orbx_dev_kernel_time_select": ([vp, ctypes.c_char_p], i),
         "orbx_dev_read_level": ([vp, i, i, i, vp, i, ip, ip], i),
         "orbx_descriptor_distance": ([vp, vp], i),
         "orbx_hamming_bf": ([vp, vp, i, vp, i, vp, vp, vp], i),
@@ -219,7 +220,10 @@ class Context:
                                          ctypes.byref(pw), ctypes.byref(ph)), "orbx_dev_read_level")
         return buf[:pw.value * ph.value].reshape(ph.value, pw.value).copy()
 
-    def timing(self, enable=True):
+    def timing(self, enable=True, only=None):
+        """Kernel timing with hipEvents around every launch, or only around
+        the launches of timer `only`."""
+        _check(lib().orbx_dev_kernel_time_select(self._h, only.encode() if only else None), "timing")
         _check(lib().orbx_dev_kernel_time_enable(self._h, int(enable)), "timing")
 
     def kernel_time(self, name):

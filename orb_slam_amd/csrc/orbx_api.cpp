@@ -21,7 +21,7 @@ static KernelTimer* find_timer(orbx_ctx* ctx, const char* name)
 
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st)
 {
-    if (!ctx->timing) return;
+    if (!ctx->timing || (!ctx->timing_only.empty() && ctx->timing_only != name)) return;
     KernelTimer* t = find_timer(ctx, name);
     if (t->used == (int)t->start.size()) {
         hipEvent_t a, b;
@@ -34,7 +34,7 @@ void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st)
 
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st)
 {
-    if (!ctx->timing) return;
+    if (!ctx->timing || (!ctx->timing_only.empty() && ctx->timing_only != name)) return;
     KernelTimer* t = find_timer(ctx, name);
     if (t->used >= (int)t->stop.size()) return;
     (void)hipEventRecord(t->stop[t->used], st ? st : ctx->stream);
@@ -390,6 +390,13 @@ int orbx_dev_kernel_time_enable(orbx_ctx* ctx, int enable)
     if (!ctx) return ORBX_ERR_ARG;
     ctx->timing = enable != 0;
     for (auto& t : ctx->timers) t.used = 0;
+    return ORBX_OK;
+}
+
+int orbx_dev_kernel_time_select(orbx_ctx* ctx, const char* name)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    ctx->timing_only = name ? name : "";
     return ORBX_OK;
 }
 

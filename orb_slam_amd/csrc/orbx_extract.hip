@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
-    constexpr int kCandRing = 512;           // > 63 waiting + 256 new per iteration
+    constexpr int kCandRing = 256;           // per-wave ring (a full iteration's 256 fit after a drain)
     __shared__ uint32_t cand[kWaves][kCandRing];
     const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const CellGeom C = a.cells[cell];
@@ -566,6 +566,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             if (lane == 0) FP_ADD(10 + (tmin < 10), ntot);
             if (lane == 0) FP_ADD(12, 1);
 #endif
+            if (qt - qh + ntot > kCandRing) {   // rare (> 75 % survivors): drain the partial batch
+                score_batch(lane < qt - qh ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u);
+                qh = qt;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
             int w = qt + incl - cnt;
             if (mask) {
     #pragma unroll

@@ -171,6 +171,7 @@ struct orbx_ctx {
     size_t host_pinned_bytes = 0;
     // timing
     bool timing = false;
+    std::string timing_only;   // non-empty: only this timer records (orbx_dev_kernel_time_select)
     std::vector<orbx::KernelTimer> timers;
 };
 
