@@ -1085,10 +1085,16 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     uint32_t pat[8];
 #pragma unroll
     for (int r = 0; r < 8; r++) pat[r] = *reinterpret_cast<const uint32_t*>(c_pattern[r * 32 + hl]);
-    const int32_t* lc = a.level_count + (size_t)f * a.nlevels;
+    // per-level data, one level per lane, fetched in the same round trip as
+    // the tables above: keypoint count, offsets, stride, scale, patch size
+    const int ll = min(lane, a.nlevels - 1);
+    const int cnt_l = lane < a.nlevels ? a.level_count[(size_t)f * a.nlevels + lane] : 0;
+    const long long off_l = a.levels[ll].off;
+    const int stride_l = a.levels[ll].stride, loff_l = a.levels[ll].level_off;
+    const float scale_l = a.levels[ll].scale, psize_l = a.levels[ll].patch_size;
     int total = 0, level = -1, local = 0;
     for (int l = 0; l < a.nlevels; l++) {
-        const int c = lc[l];
+        const int c = __builtin_amdgcn_readlane(cnt_l, l);
         if (level < 0 && k < total + c) {
             level = l;
             local = k - total;
@@ -1104,30 +1110,66 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         level = 0;
         local = 0;
     }
-    const LevelGeom L = a.levels[level];
-    const uint32_t e = a.level_keys[(size_t)f * a.level_entries + L.level_off + local];
+    // this half's level data, read back from lane `level`
+    const int lv0 = __builtin_amdgcn_readlane(level, 0), lv1 = __builtin_amdgcn_readlane(level, 32);
+    auto pick = [&](int v) {
+        const int a0 = __builtin_amdgcn_readlane(v, lv0), a1 = __builtin_amdgcn_readlane(v, lv1);
+        return half ? a1 : a0;
+    };
+    const long long lev_off = (long long)(((unsigned long long)(uint32_t)pick((int)(off_l >> 32)) << 32) |
+                                          (uint32_t)pick((int)off_l));
+    const int lev_stride = pick(stride_l), lev_loff = pick(loff_l);
+    const float lev_scale = __int_as_float(pick(__float_as_int(scale_l)));
+    const float lev_psize = __int_as_float(pick(__float_as_int(psize_l)));
+    const uint32_t e = a.level_keys[(size_t)f * a.level_entries + lev_loff + local];
     const int score = (int)(e >> 24), y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
     const int X = kEdge + (valid ? x : kHalfPatch + 8), Y = kEdge + (valid ? y : kHalfPatch + 8);
     uint8_t* ic = s_patch[slot];
     uint8_t* br = ic + kIcRows * kIcPitch;
     {
-        const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
-        const uint8_t* blr = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
+        const uint8_t* raw = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + lev_off;
+        const uint8_t* blr = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + lev_off;
         const int ix0 = (X - kHalfPatch) & ~3, bx0 = (X - kBrR) & ~3;
         uint32_t* ic32 = reinterpret_cast<uint32_t*>(ic);
         uint32_t* br32 = reinterpret_cast<uint32_t*>(br);
-        // both patches' loads (9 + 12 per lane) in flight together
+        // both patches' loads (9 + 12 per lane) in flight together; 32-bit
+        // offsets from the patches' first rows, (row, dword) stepped per load
         constexpr int nic = kIcRows * (kIcPitch / 4), nbr = kBrRows * (kBrPitch / 4);
+        constexpr int qi = kIcPitch / 4, qb = kBrPitch / 4;
+        const uint8_t* ri = raw + (long long)(Y - kHalfPatch) * lev_stride + ix0;
+        const uint8_t* rb = blr + (long long)(Y - kBrR) * lev_stride + bx0;
+        const uint32_t stride = (uint32_t)lev_stride;
         uint32_t vi[(nic + 31) / 32], vb[(nbr + 31) / 32];
+        {
+            int r = hl / qi, q = hl - (hl / qi) * qi;
 #pragma unroll
-        for (int k = 0; k < (nic + 31) / 32; k++) {
-            const int i = min(hl + 32 * k, nic - 1), r = i / (kIcPitch / 4), q = i - r * (kIcPitch / 4);
-            vi[k] = *reinterpret_cast<const uint32_t*>(raw + (size_t)(Y - kHalfPatch + r) * L.stride + ix0 + 4 * q);
+            for (int k = 0; k < (nic + 31) / 32; k++) {
+                const bool in = hl + 32 * k < nic;
+                // lanes past the patch re-load (and below re-store) its last dword
+                vi[k] = *reinterpret_cast<const uint32_t*>(
+                    ri + (in ? (uint32_t)r * stride + 4u * (uint32_t)q : (uint32_t)(kIcRows - 1) * stride + 4u * (qi - 1)));
+                r += 32 / qi;
+                q += 32 % qi;
+                if (q >= qi) {
+                    q -= qi;
+                    r++;
+                }
+            }
         }
+        {
+            int r = hl / qb, q = hl - (hl / qb) * qb;
 #pragma unroll
-        for (int k = 0; k < (nbr + 31) / 32; k++) {
-            const int i = min(hl + 32 * k, nbr - 1), r = i / (kBrPitch / 4), q = i - r * (kBrPitch / 4);
-            vb[k] = *reinterpret_cast<const uint32_t*>(blr + (size_t)(Y - kBrR + r) * L.stride + bx0 + 4 * q);
+            for (int k = 0; k < (nbr + 31) / 32; k++) {
+                const bool in = hl + 32 * k < nbr;
+                vb[k] = *reinterpret_cast<const uint32_t*>(
+                    rb + (in ? (uint32_t)r * stride + 4u * (uint32_t)q : (uint32_t)(kBrRows - 1) * stride + 4u * (qb - 1)));
+                r += 32 / qb;
+                q += 32 % qb;
+                if (q >= qb) {
+                    q -= qb;
+                    r++;
+                }
+            }
         }
 #pragma unroll
         for (int k = 0; k < (nic + 31) / 32; k++) ic32[min(hl + 32 * k, nic - 1)] = vi[k];
@@ -1181,10 +1223,10 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         kp.x = (float)x;
         kp.y = (float)y;
         if (level != 0) {
-            kp.x = __fmul_rn(kp.x, L.scale);
-            kp.y = __fmul_rn(kp.y, L.scale);
+            kp.x = __fmul_rn(kp.x, lev_scale);
+            kp.y = __fmul_rn(kp.y, lev_scale);
         }
-        kp.size = L.patch_size;
+        kp.size = lev_psize;
         kp.angle = angle;
         kp.response = (float)score;
         kp.octave = level;
