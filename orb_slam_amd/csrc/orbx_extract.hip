@@ -868,7 +868,7 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
     uint32_t* dst = a.level_keys + (size_t)f * a.level_entries + L.level_off + pre;
     if (n > k && n <= kRetainCellCap) {
-        for (int i = lane; i < n; i += 64) list[i] = src[i];
+        stage_to_lds<8>(list, n, lane, 64, [&](int i) { return src[i]; });
         lds_wave_sync();
         wave_nth_element(list, n, k, pos);
         for (int i = lane; i < take; i += 64) dst[i] = list[i];
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
     uint32_t* list = sbuf + (size_t)wv * wave_words;
     int* pos = reinterpret_cast<int*>(list + a.max_level_cap);
     uint32_t* g = a.level_keys + (size_t)f * a.level_entries + L.level_off;
-    for (int i = lane; i < nlev; i += 64) list[i] = g[i];
+    stage_to_lds<8>(list, nlev, lane, 64, [&](int i) { return g[i]; });
     lds_wave_sync();
     wave_nth_element(list, nlev, L.n_desired, pos);
     for (int i = lane; i < L.n_desired; i += 64) g[i] = list[i];
