@@ -200,9 +200,10 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK && (hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->ev_extracted, hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&ctx->ev_matched, hipEventDisableTiming) != hipSuccess))
+                         hipEventCreateWithFlags(&ctx->ev_extracted, hipEventDisableTiming) != hipSuccess))
         r = ORBX_ERR_HIP;
+    for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxPending; i++)
+        if (hipEventCreateWithFlags(&ctx->ev_match[i], hipEventDisableTiming) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
     if (r == ORBX_OK) r = realloc_dev(ctx->level_count, (size_t)S * nlevels);
@@ -242,7 +243,8 @@ void orbx_destroy(orbx_ctx* ctx)
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_extracted) (void)hipEventDestroy(ctx->ev_extracted);
-    if (ctx->ev_matched) (void)hipEventDestroy(ctx->ev_matched);
+    for (auto e : ctx->ev_match)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

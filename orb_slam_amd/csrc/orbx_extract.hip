@@ -1388,32 +1388,39 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     const bool async = m && m->kind != 0 && ctx->async_match && ctx->mstream;
     // outputs of [first, first + count) are rewritten: a pending match that
     // reads any of them must finish first
-    if (ctx->pend_hi > ctx->pend_lo) {
-        if (first < ctx->pend_hi && first + count > ctx->pend_lo) {
-            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0));
-            ctx->pend_lo = ctx->pend_hi = 0;
-        }
-    }
+    if (!async) wait_pending_overlap(ctx, first, count, ctx->stream);
     if (async) {
-        // extraction (split as usual) on the extraction streams; the whole
-        // batch's matching on mstream once it is extracted, overlapping the
-        // next call's extraction of other slots
+        // Extraction (two concurrent halves, joined on the context stream),
+        // then the batch's matching on mstream, which overlaps the next
+        // call's extraction of other slots.  (Offsetting the halves so one
+        // half's FAST meets the other's latency-bound passes was measured
+        // slower: the step is VALU-bound overall.)
         const int r = launch_extract(ctx, first, count, nullptr);
         if (r != ORBX_OK) return r;
         ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream));
         ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
         match_runs(first, first + count, 0, -1, ctx->mstream);
-        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_matched, ctx->mstream));
         // the match reads the outputs of the batch's sequences
         const int q = m->seq_len;
         const int lo = (first / q) * q, hi = ((first + count + q - 1) / q) * q;
-        if (ctx->pend_hi > ctx->pend_lo) {   // an older match on mstream precedes this one
-            ctx->pend_lo = std::min(ctx->pend_lo, lo);
-            ctx->pend_hi = std::max(ctx->pend_hi, hi);
-        } else {
-            ctx->pend_lo = lo;
-            ctx->pend_hi = hi;
+        if (ctx->n_pend == orbx_ctx::kMaxPending) {   // table full: retire the oldest
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->pend[0].done, 0));
+            for (int i = 1; i < ctx->n_pend; i++) ctx->pend[i - 1] = ctx->pend[i];
+            ctx->n_pend--;
         }
+        // an event not referenced by any pending entry
+        hipEvent_t ev = nullptr;
+        for (int t = 0; t < orbx_ctx::kMaxPending && !ev; t++) {
+            hipEvent_t c = ctx->ev_match[(ctx->next_ev + t) % orbx_ctx::kMaxPending];
+            bool used = false;
+            for (int i = 0; i < ctx->n_pend; i++) used = used || ctx->pend[i].done == c;
+            if (!used) {
+                ev = c;
+                ctx->next_ev = (ctx->next_ev + t + 1) % orbx_ctx::kMaxPending;
+            }
+        }
+        ORBX_HIP_CHECK(hipEventRecord(ev, ctx->mstream));
+        ctx->pend[ctx->n_pend++] = orbx_ctx::PendingMatch{lo, hi, ev};
         if (err != ORBX_OK) return err;
         if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
         return ORBX_OK;

@@ -130,11 +130,19 @@ struct orbx_ctx {
     bool split = true;                  // run large batches as two concurrent halves
     // Asynchronous matching (orbx_dev_set_async_match): the matching of an
     // extract_match call runs on mstream while later calls extract other
-    // slots; [pend_lo, pend_hi) are the slots that match still reads.
+    // slots.  pend[] lists the matches queued on mstream, oldest first: the
+    // slots each reads and the event recorded after it.
+    static constexpr int kMaxPending = 4;
+    struct PendingMatch {
+        int lo, hi;
+        hipEvent_t done;
+    };
     hipStream_t mstream = nullptr;
-    hipEvent_t ev_extracted = nullptr, ev_matched = nullptr;
+    hipEvent_t ev_extracted = nullptr;
+    hipEvent_t ev_match[kMaxPending] = {};
+    PendingMatch pend[kMaxPending] = {};
+    int n_pend = 0, next_ev = 0;
     bool async_match = false;
-    int pend_lo = 0, pend_hi = 0;
     orbx::Geometry geom;
     orbx::DeviceGeometry dgeom;
     int max_w = 0, max_h = 0, slots = 0;
@@ -209,8 +217,21 @@ int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 inline void ctx_enter(orbx_ctx* ctx)
 {
     (void)hipSetDevice(ctx->device);
-    if (ctx->pend_hi > ctx->pend_lo) {
-        (void)hipStreamWaitEvent(ctx->stream, ctx->ev_matched, 0);
-        ctx->pend_lo = ctx->pend_hi = 0;
+    if (ctx->n_pend > 0) {   // mstream is in order: its newest event covers all
+        (void)hipStreamWaitEvent(ctx->stream, ctx->pend[ctx->n_pend - 1].done, 0);
+        ctx->n_pend = 0;
     }
+}
+
+// Order ctx->stream after every pending match that reads a slot of
+// [first, first + count) (and, mstream being in order, after the older ones).
+inline void wait_pending_overlap(orbx_ctx* ctx, int first, int count, hipStream_t st)
+{
+    int last = -1;
+    for (int i = 0; i < ctx->n_pend; i++)
+        if (first < ctx->pend[i].hi && first + count > ctx->pend[i].lo) last = i;
+    if (last < 0) return;
+    (void)hipStreamWaitEvent(st, ctx->pend[last].done, 0);
+    for (int i = last + 1; i < ctx->n_pend; i++) ctx->pend[i - last - 1] = ctx->pend[i];
+    ctx->n_pend -= last + 1;
 }
