@@ -260,37 +260,33 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 // (padded columns 0 .. kEdge + P.w), together with the level's column and
 // row tables; every output pixel then reads its 2x2 sources from LDS.
 // The host guarantees hi - lo + 1 <= L.res_span (computed from the tables).
-__global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, int level, int pitch)
+// The level's and its parent's geometry, passed by value: no dependent
+// table read before the staging loads.
+struct ResizeLevel {
+    long long off, poff;                 // level / parent offsets in a frame's pyramid
+    int stride, pstride, w, h, pw, ph, ph_parent_h, nvec, span, strip_off, row_off, col_off;
+};
+
+__global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLevel L, int pitch)
 {
     extern __shared__ uint4 s_dyn[];
     __shared__ ResizeRow s_rows[kResRows];
-    __shared__ int s_lo;
     const int f = blockIdx.y, tid = threadIdx.x;
-    const LevelGeom L = a.levels[level];
-    const LevelGeom P = a.levels[level - 1];
     const int py0 = blockIdx.x * kResRows, nrows = min(kResRows, L.ph - py0);
     const int nch = pitch >> 4;
-    ResizeCol* s_cols = reinterpret_cast<ResizeCol*>(s_dyn + (size_t)L.res_span * nch);
+    ResizeCol* s_cols = reinterpret_cast<ResizeCol*>(s_dyn + (size_t)L.span * nch);
     uint8_t* s_src = reinterpret_cast<uint8_t*>(s_dyn);
-    if (tid < 64) {
-        int lo = 0x7fffffff;
-        if (tid < nrows) {
-            const ResizeRow r = a.res_rows[L.res_row_off + reflect101(py0 + tid - kEdge, L.h)];
-            s_rows[tid] = r;
-            lo = min(r.sy0, r.sy1);
-        }
-        lo = -wave_max(-lo);
-        if (tid == 0) s_lo = lo;
-    }
-    stage_to_lds<4>(s_cols, L.w, tid, (int)blockDim.x, [&](int x) { return a.res_cols[L.res_col_off + x]; });
-    __syncthreads();
-    const int lo = s_lo;
-    const int nsrc = min(L.res_span, P.h - lo);
-    const uint8_t* pbase = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + P.off + (size_t)(lo + kEdge) * P.stride;
+    // the strip's first source row comes from a host table (uniform scalar
+    // load), so the staging loads go out together with the row/column tables
+    const int lo = a.res_rows[L.strip_off + blockIdx.x].sy0;
+    if (tid < nrows) s_rows[tid] = a.res_rows[L.row_off + reflect101(py0 + tid - kEdge, L.h)];
+    stage_to_lds<4>(s_cols, L.w, tid, (int)blockDim.x, [&](int x) { return a.res_cols[L.col_off + x]; });
+    const int nsrc = min(L.span, L.ph_parent_h - lo);
+    const uint8_t* pbase = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.poff + (size_t)(lo + kEdge) * L.pstride;
 #ifndef RES_NO_STAGE
     stage_to_lds<8>(s_dyn, nsrc * nch, tid, (int)blockDim.x, [&](int u) {
         const int r = u / nch, c = u - r * nch;
-        return *reinterpret_cast<const uint4*>(pbase + (size_t)r * P.stride + 16 * c);
+        return *reinterpret_cast<const uint4*>(pbase + (size_t)r * L.pstride + 16 * c);
     });
 #endif
     __syncthreads();
@@ -317,7 +313,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, int level
             ca[b] = kEdge + c.sx0;
             a0[b] = on ? c.a0 : 0;
             a1[b] = on ? c.a1 : 0;
-            vb[b] = x < L.nvec_resize;
+            vb[b] = x < L.nvec;
             vec = vec && (!on || vb[b]);
         }
         auto hrow = [&](int sy, int (&S)[4]) {
@@ -1296,8 +1292,10 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_begin(ctx, "resize", st);
             if (lds <= kResizeLds) {
                 const int threads = std::min(256, ((L.stride / 4) + 63) & ~63);
+                const ResizeLevel rl{L.off, P.off, L.stride, P.stride, L.w, L.h, L.pw, L.ph, P.h, L.nvec_resize,
+                                     L.res_span, L.res_strip_off, L.res_row_off, L.res_col_off};
                 hipLaunchKernelGGL(k_pyr_resize_lds, dim3((L.ph + kResRows - 1) / kResRows, nb), dim3(threads), lds, st,
-                                   x, l, pitch);
+                                   x, rl, pitch);
             } else {   // very wide levels: per-pixel gathers from global memory
                 const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
                 hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, l);

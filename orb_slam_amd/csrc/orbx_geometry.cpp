@@ -179,6 +179,21 @@ int compute_geometry(Geometry& g, int w, int h)
         }
     }
     g.frame_pyr_bytes = off;
+    // per (level >= 1, strip of kResRows padded rows): the first source row
+    // the strip reads, appended to the row table so the resize kernel can
+    // start its staging loads without a dependent table read
+    for (int l = 1; l < g.nlevels; l++) {
+        LevelGeom& L = g.levels[l];
+        L.res_strip_off = (int)g.res_rows.size();
+        for (int py0 = 0; py0 < L.ph; py0 += kResRows) {
+            int lo = 1 << 30;
+            for (int py = py0; py < std::min(py0 + kResRows, L.ph); py++) {
+                const ResizeRow& rr = g.res_rows[L.res_row_off + reflect101(py - kEdge, L.h)];
+                lo = std::min(lo, (int)std::min(rr.sy0, rr.sy1));
+            }
+            g.res_rows.push_back(ResizeRow{(int16_t)lo, 0, 0, 0});
+        }
+    }
 
     const float imageRatio = (float)g.levels[0].w / g.levels[0].h;
     for (int l = 0; l < g.nlevels; l++) {

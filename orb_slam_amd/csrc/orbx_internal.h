@@ -62,6 +62,7 @@ struct LevelGeom {
     int res_col_off;      // offset into the resize column table (level >= 1)
     int res_row_off;      // offset into the resize row table
     int res_span;         // max source rows feeding one strip of kResRows output rows
+    int res_strip_off;    // res_rows index of this level's per-strip entries (sy0 = first source row)
 };
 
 struct CellGeom {
