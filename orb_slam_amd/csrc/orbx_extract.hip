@@ -527,7 +527,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
                 const uint32_t T1 = (uint32_t)(tmin + 1) * 0x00010001u;
                 const uint32_t NT1 = (uint32_t)(-(tmin + 1) & 0xFFFF) * 0x00010001u;
-                int ok[2][2];   // [half][dark, bright] sign-bit masks of passing lanes
+                // A pixel whose compass test fails in one direction has that
+                // direction's 9-arc minimum <= tmin, so scoring both arcs for
+                // every survivor gives the same S' (no direction flags needed)
+                uint32_t okw[2];   // [half] sign bits of pixels passing either test
     #pragma unroll
                 for (int hf = 0; hf < 2; hf++) {
                     const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;   // bytes 1,3 or 0,2 -> u16x2
@@ -543,19 +546,15 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                     }
                     const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
                     const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
-                    ok[hf][0] = (int)(~failD & 0x80008000u);
-                    ok[hf][1] = (int)(~failB & 0x80008000u);
+                    okw[hf] = ~(failD & failB) & 0x80008000u;
                 }
-                // pixel j: bit 2j dark, 2j+1 bright (even half: j = 0, 2; odd: 1, 3)
-                mask = ((ok[0][0] >> 15) & 1) | ((ok[0][1] >> 14) & 2) |                          // j = 0
-                       (((ok[1][0] >> 15) & 1) << 2) | (((ok[1][1] >> 14) & 2) << 2) |              // j = 1
-                       (((ok[0][0] >> 31) & 1) << 4) | ((((unsigned)ok[0][1] >> 30) & 2) << 4) |     // j = 2
-                       (((ok[1][0] >> 31) & 1) << 6) | ((((unsigned)ok[1][1] >> 30) & 2) << 6);     // j = 3
+                // pixel j -> bit j (even half: j = 0, 2; odd half: j = 1, 3)
+                mask = (int)(((okw[0] >> 15) & 1) | ((okw[1] >> 14) & 2) | ((okw[0] >> 29) & 4) | ((okw[1] >> 28) & 8));
                 // interior columns only
                 const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
-                mask = (j1 < j0) ? 0 : (mask & (((1 << (2 * (j1 + 1))) - 1) & ~((1 << (2 * j0)) - 1)));
+                mask = (j1 < j0) ? 0 : (mask & (((1 << (j1 + 1)) - 1) & ~((1 << j0) - 1)));
             }
-            const int cnt = __popc((mask | (mask >> 1)) & 0x55);
+            const int cnt = __popc(mask);
             const int incl = wave_inclusive_scan(cnt);
             const int ntot = __builtin_amdgcn_readlane(incl, 63);
 #ifdef ORBX_FAST_PROFILE
@@ -572,10 +571,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             int w = qt + incl - cnt;
             if (mask) {
     #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int fl = (mask >> (2 * j)) & 3;
-                    if (fl) cand[wv][(w++) & (kCandRing - 1)] = (uint32_t)(r * P + 4 * q + j) | ((uint32_t)fl << 16);
-                }
+                for (int j = 0; j < 4; j++)
+                    if ((mask >> j) & 1) cand[wv][(w++) & (kCandRing - 1)] = (uint32_t)(r * P + 4 * q + j) | (3u << 16);
             }
             qt += ntot;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
