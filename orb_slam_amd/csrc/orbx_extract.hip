@@ -498,6 +498,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     __syncthreads();
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
     const int q0 = c_lo >> 2, nqe = (c_hi >> 2) - q0 + 1; // dwords holding them
+    const int q_last = q0 + nqe - 1;
+    const int m_first = 0xF & ~((1 << (c_lo & 3)) - 1);  // pixels j >= c_lo & 3 of dword q0
+    const int m_last = (1 << ((c_hi & 3) + 1)) - 1;      // pixels j <= c_hi & 3 of the last dword
     const int nunits = (hy - 6) * nqe;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {
@@ -537,12 +540,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                     const uint32_t v = __builtin_amdgcn_perm(0u, mid, sel);
                     const uint32_t pk[4] = {__builtin_amdgcn_perm(0u, dn, sel), __builtin_amdgcn_perm(0u, p4w, sel),
                                             __builtin_amdgcn_perm(0u, up, sel), __builtin_amdgcn_perm(0u, p12w, sel)};
+                    // v - p - (t+1) = (v - (t+1)) - p;  p - v - (t+1) = p - (v + (t+1))
+                    const uint32_t vd = pk_sub16(v, T1), vb = pk_sub16(v, NT1);
                     uint32_t xd[4], xb[4];
     #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t d = pk_sub16(v, pk[k]);     // v - p
-                        xd[k] = pk_sub16(d, T1);                   // >= 0 <=> v - p > t
-                        xb[k] = pk_sub16(NT1, d);                  // >= 0 <=> p - v > t
+                        xd[k] = pk_sub16(vd, pk[k]);               // >= 0 <=> v - p > t
+                        xb[k] = pk_sub16(pk[k], vb);               // >= 0 <=> p - v > t
                     }
                     const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
                     const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
@@ -550,9 +554,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
                 }
                 // pixel j -> bit j (even half: j = 0, 2; odd half: j = 1, 3)
                 mask = (int)(((okw[0] >> 15) & 1) | ((okw[1] >> 14) & 2) | ((okw[0] >> 29) & 4) | ((okw[1] >> 28) & 8));
-                // interior columns only
-                const int j0 = max(c_lo - 4 * q, 0), j1 = min(c_hi - 4 * q, 3);
-                mask = (j1 < j0) ? 0 : (mask & (((1 << (j1 + 1)) - 1) & ~((1 << j0) - 1)));
+                // interior columns only (q0 and the last dword are partial)
+                mask &= (q == q0 ? m_first : 0xF) & (q == q_last ? m_last : 0xF);
             }
             const int cnt = __popc(mask);
             const int incl = wave_inclusive_scan(cnt);
