@@ -428,8 +428,8 @@ int orbx_dev_kernel_time(orbx_ctx* ctx, const char* name, double* avg_ms, double
 int orbx_dev_read_level(orbx_ctx* ctx, int slot, int level, int blurred, uint8_t* out, int cap, int* pw, int* ph)
 {
     if (!ctx || level < 0 || level >= ctx->geom.nlevels) return ORBX_ERR_ARG;
-    const int f = slot - ctx->last_first;
-    if (f < 0 || f >= ctx->last_count) return ORBX_ERR_ARG;
+    const int f = slot;   // work buffers are per slot
+    if (f < 0 || f >= ctx->slots) return ORBX_ERR_ARG;
     ctx_enter(ctx);
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     const LevelGeom& L = ctx->geom.levels[level];

@@ -1244,17 +1244,19 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.res_rows = ctx->dgeom.res_rows;
     a.umax = ctx->dgeom.umax;
     a.frames = ctx->frames;
-    a.pyr_raw = ctx->pyr_raw;
-    a.pyr_blur = ctx->pyr_blur;
-    a.cell_lists = ctx->cell_lists;
-    a.cell_count = ctx->cell_count;
-    a.level_keys = ctx->level_keys;
-    a.level_count = ctx->level_count;
+    // work buffers are per slot (frame f of this pass uses slot first + f):
+    // batches on disjoint slots can be in flight at the same time
+    a.pyr_raw = ctx->pyr_raw + (size_t)first * g.frame_pyr_bytes;
+    a.pyr_blur = ctx->pyr_blur + (size_t)first * g.frame_pyr_bytes;
+    a.cell_lists = ctx->cell_lists + (size_t)first * g.list_entries;
+    a.cell_count = ctx->cell_count + (size_t)first * g.cells.size();
+    a.level_keys = ctx->level_keys + (size_t)first * g.level_entries;
+    a.level_count = ctx->level_count + (size_t)first * g.nlevels;
     a.out_kps = ctx->out_kps;
     a.out_desc = ctx->out_desc;
     a.out_n = ctx->out_n;
     a.error_flags = ctx->error_flags;
-    a.retain_scratch = ctx->retain_scratch;
+    a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
     a.frame_pyr_bytes = g.frame_pyr_bytes;
     a.w = g.w;
     a.h = g.h;
@@ -1268,8 +1270,8 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.max_list_cap = g.max_list_cap;
     a.max_level_cap = g.max_level_cap;
 
-    // One pass of the stage sequence over nb frames on stream st.
-    auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
+    // The pyramid stages over nb frames on stream st.
+    auto run_pyramid = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         timer_begin(ctx, "pyr0", st);
         {
             const LevelGeom& L = g.levels[0];
@@ -1302,6 +1304,9 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             }
             timer_end(ctx, "resize", st);
         }
+    };
+    // FAST .. describe over nb frames on stream st (after their pyramid).
+    auto run_rest = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         timer_begin(ctx, "fast", st);
         {
             // widest aligned cell row and tallest cell pick the tile pitch
@@ -1347,6 +1352,10 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), nb), dim3(256), 0, st, x);
         timer_end(ctx, "describe", st);
     };
+    auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
+        run_pyramid(x, nb, st);
+        run_rest(x, nb, st);
+    };
     // Work buffers are indexed by batch position (frame f of a pass uses
     // work slot f); the frame store and outputs by slot.  Large batches run
     // as two halves on two streams so that the VALU-bound FAST pass of one
@@ -1386,13 +1395,19 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     const bool async = m && m->kind != 0 && ctx->async_match && ctx->mstream;
     // outputs of [first, first + count) are rewritten: a pending match that
     // reads any of them must finish first
-    if (!async) wait_pending_overlap(ctx, first, count, ctx->stream);
+    if (!async) {
+        wait_pending_overlap(ctx, first, count, ctx->stream);
+        ctx->stream_dirty = true;
+    }
     if (async) {
         // Extraction (two concurrent halves, joined on the context stream),
         // then the batch's matching on mstream, which overlaps the next
-        // call's extraction of other slots.  (Offsetting the halves so one
-        // half's FAST meets the other's latency-bound passes was measured
-        // slower: the step is VALU-bound overall.)
+        // call's extraction of other slots.  Measured alternatives, both
+        // no faster because the step is VALU-bound overall: offsetting the
+        // halves (one half's FAST against the other's latency-bound passes),
+        // and running the next batch's pyramid on stream2 during this
+        // batch's FAST .. describe (work buffers are per slot, so that is
+        // safe; it stays possible).
         const int r = launch_extract(ctx, first, count, nullptr);
         if (r != ORBX_OK) return r;
         ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream));

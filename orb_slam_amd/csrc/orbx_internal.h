@@ -144,6 +144,7 @@ struct orbx_ctx {
     PendingMatch pend[kMaxPending] = {};
     int n_pend = 0, next_ev = 0;
     bool async_match = false;
+    bool stream_dirty = true;   // the context stream got work outside the async pipeline
     orbx::Geometry geom;
     orbx::DeviceGeometry dgeom;
     int max_w = 0, max_h = 0, slots = 0;
@@ -218,6 +219,7 @@ int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 inline void ctx_enter(orbx_ctx* ctx)
 {
     (void)hipSetDevice(ctx->device);
+    ctx->stream_dirty = true;
     if (ctx->n_pend > 0) {   // mstream is in order: its newest event covers all
         (void)hipStreamWaitEvent(ctx->stream, ctx->pend[ctx->n_pend - 1].done, 0);
         ctx->n_pend = 0;
