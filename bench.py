@@ -45,7 +45,7 @@ WORKLOADS = {
     "c3": dict(w=1920, h=1080, nfeatures=2000, batch=64,
                metric="pairs/sec ORB extract + brute-force Hamming match (1920x1080, 2000 kp)", unit="pairs/s",
                desc="1920x1080 mono8, 8 levels x1.2, 2000 kp: ORB extract + brute-force Hamming vs previous frame"),
-    "c5": dict(batch=32, metric="local BA problems/sec (20 KF x 2000 MP, 5+10 LM iterations)", unit="problems/s",
+    "c5": dict(batch=256, metric="local BA problems/sec (20 KF x 2000 MP, 5+10 LM iterations)", unit="problems/s",
                desc="Optimizer::LocalBundleAdjustment core: 20 keyframes (+2 fixed) x 2000 map points, "
                     "Huber, Schur + LLT, 5+10 LM iterations, two outlier passes"),
 }
@@ -203,8 +203,11 @@ def run_frames(args, wl, rank, local, world, dist):
 def run_lba(args, wl, rank, local, world, dist):
     from orb_slam_amd import synth_ba as sb
     P = args.batch or wl["batch"]
-    probs = [sb.make_problem(n_kf=20, n_points=2000, seed=odist.shard_seed(5000, rank) * 1000 + i)
-             for i in range(P)]
+    # 32 distinct synthetic problems (generation is slow in Python), repeated
+    # to fill the batch; every problem is solved independently from its own copy
+    uniq = [sb.make_problem(n_kf=20, n_points=2000, seed=odist.shard_seed(5000, rank) * 1000 + i)
+            for i in range(min(P, 32))]
+    probs = [uniq[i % len(uniq)] for i in range(P)]
     ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
     cps = [sb.to_ctypes(pr) for pr in probs]
     n_edges = int(np.mean([c[0].n_edges for c in cps]))

@@ -24,6 +24,9 @@
 #include <cmath>
 #include <cstddef>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -832,159 +835,215 @@ constexpr int kLdsSCap = (144 * 1024) / 8;   // doubles of LDS for the reduced s
 
 // Solves P problems; per problem a workgroup.  The problems' pose/point
 // arrays are updated in place.
+namespace {
+// Runs fn(i) for i in [0, n) on up to 16 host threads (independent problems).
+template <typename Fn>
+void host_parallel(int n, Fn fn)
+{
+    const int nth = std::max(1, std::min<int>(n, std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+    if (nth == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() {
+            for (int i = t; i < n; i += nth) fn(i);
+        });
+    for (auto& th : pool) th.join();
+}
+
+inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+}  // namespace
+
+// Solves P problems; per problem a workgroup.  The problems' pose/point
+// arrays are updated in place.  Host staging: one planned layout, filled by
+// host threads straight into the context's pinned buffer, one copy each way.
 static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int iters1,
                    const volatile uint8_t* abort, uint8_t* const* edge_status, uint8_t* const* point_bad,
                    orbx_ba_stats* stats)
 {
+    static const bool prof = getenv("ORBX_LBA_PROFILE_HOST") != nullptr;
+    auto tprev = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[lba host] %-22s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tprev).count());
+        tprev = t;
+    };
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         if (p.n_poses < 0 || p.n_points < 0 || p.n_edges < 0) return ORBX_ERR_ARG;
-        for (int e = 0; e < p.n_edges; e++)
-            if (p.edge_point[e] < 0 || p.edge_point[e] >= p.n_points || p.edge_pose[e] < 0 ||
-                p.edge_pose[e] >= p.n_poses)
-                return ORBX_ERR_ARG;
     }
+    std::vector<uint8_t> bad_edge(P, 0);
+    host_parallel(P, [&](int i) {
+        const orbx_ba_problem& p = probs[i];
+        for (int e = 0; e < p.n_edges; e++)
+            if (p.edge_point[e] < 0 || p.edge_point[e] >= p.n_points || p.edge_pose[e] < 0 || p.edge_pose[e] >= p.n_poses)
+                bad_edge[i] = 1;
+    });
+    for (int i = 0; i < P; i++)
+        if (bad_edge[i]) return ORBX_ERR_ARG;
     ctx_enter(ctx);
-    // persistent per-problem device state: poses, points, errors, counters
+    // ---- persistent block (device-resident across both passes) ----
+    struct PLay {
+        size_t pose, point, posebk, pointbk, cam, err;
+    };
+    std::vector<PLay> pl(P);
     std::vector<long long> offs(3 * P);
-    Packer base;
-    std::vector<size_t> o_pose(P), o_point(P), o_posebk(P), o_pointbk(P), o_cam(P), o_err(P);
-    std::vector<int> all_nobs;
-    std::vector<uint8_t> all_st, all_bad;
+    size_t at = 0;
     long long eacc = 0, pacc = 0;
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
-        std::vector<double> pose(7 * (size_t)p.n_poses);
-        for (int k = 0; k < p.n_poses; k++) {
-            for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
-            for (int j = 0; j < 3; j++) pose[7 * k + 4 + j] = p.pose_t[3 * k + j];
-        }
-        o_pose[i] = base.add(pose);
-        o_point[i] = base.add(std::vector<double>(p.points, p.points + 3 * (size_t)p.n_points));
-        o_posebk[i] = base.reserve(pose.size() * 8);
-        o_pointbk[i] = base.reserve(3 * (size_t)p.n_points * 8);
-        o_cam[i] = base.add(std::vector<double>(p.pose_cam, p.pose_cam + 4 * (size_t)p.n_poses));
-        o_err[i] = base.add(std::vector<double>(2 * (size_t)p.n_edges, 0.0));
+        pl[i].pose = at;    at += align256(7 * (size_t)p.n_poses * 8);
+        pl[i].point = at;   at += align256(3 * (size_t)p.n_points * 8);
+        pl[i].posebk = at;  at += align256(7 * (size_t)p.n_poses * 8);
+        pl[i].pointbk = at; at += align256(3 * (size_t)p.n_points * 8);
+        pl[i].cam = at;     at += align256(4 * (size_t)p.n_poses * 8);
+        pl[i].err = at;     at += align256(2 * (size_t)p.n_edges * 8);
         offs[3 * i] = eacc;
         offs[3 * i + 1] = pacc;
-        all_nobs.insert(all_nobs.end(), p.point_nobs, p.point_nobs + p.n_points);
-        all_st.insert(all_st.end(), p.n_edges, 0);
-        all_bad.insert(all_bad.end(), p.n_points, 0);
         eacc += p.n_edges;
         pacc += p.n_points;
     }
-    const size_t o_all_nobs = base.add(all_nobs), o_all_st = base.add(all_st), o_all_bad = base.add(all_bad);
-    const size_t o_offs = base.add(offs);
-    const size_t o_nout = base.reserve(4 * (size_t)P);
-    // per-pass structures follow the persistent block
-    const size_t base_bytes = base.host.size();
+    const size_t o_all_nobs = at; at += align256(4 * (size_t)pacc);
+    const size_t o_all_st = at;   at += align256((size_t)eacc);
+    const size_t o_all_bad = at;  at += align256((size_t)pacc);
+    const size_t o_offs = at;     at += align256(offs.size() * 8);
+    const size_t o_nout = at;     at += align256(4 * (size_t)P);
+    const size_t base_bytes = at;
+    std::vector<uint8_t> all_st((size_t)eacc, 0);
     std::vector<LbaDev> devs(P);
     int r = ORBX_OK;
     for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
-        Packer pk;
-        pk.host = base.host;
         std::vector<HostStruct> hs(P);
-        std::vector<size_t> o[32];
-        for (auto& v : o) v.resize(P);
-        {
-            // index structures of independent problems are built on host threads
-            const int nth = std::max(1, std::min<int>(P, std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
-            std::vector<std::thread> pool;
-            for (int t = 0; t < nth; t++)
-                pool.emplace_back([&, t]() {
-                    for (int i = t; i < P; i += nth)
-                        build_struct(probs[i], pass == 0 ? nullptr : all_st.data() + offs[3 * i], hs[i]);
-                });
-            for (auto& th : pool) th.join();
-        }
+        host_parallel(P, [&](int i) {
+            build_struct(probs[i], pass == 0 ? nullptr : all_st.data() + offs[3 * i], hs[i]);
+        });
+        mark("build_struct");
+        // ---- per-pass structures after the persistent block ----
+        constexpr int kArr = 15;
+        std::vector<size_t> so(kArr * (size_t)P);
+        size_t end = base_bytes;
         for (int i = 0; i < P; i++) {
-            HostStruct& s = hs[i];
-            o[0][i] = pk.add(s.e_orig); o[1][i] = pk.add(s.e_pose); o[2][i] = pk.add(s.e_point);
-            o[3][i] = pk.add(s.e_ph); o[4][i] = pk.add(s.e_lh); o[5][i] = pk.add(s.e_obs);
-            o[6][i] = pk.add(s.e_isig); o[7][i] = pk.add(s.iv_pose); o[8][i] = pk.add(s.iv_point);
-            o[9][i] = pk.add(s.pe_ptr); o[10][i] = pk.add(s.pe_idx); o[11][i] = pk.add(s.le_ptr);
-            o[12][i] = pk.add(s.le_idx); o[13][i] = pk.add(s.lc_ptr); o[14][i] = pk.add(s.lc_idx);
+            const HostStruct& h = hs[i];
+            const size_t bytes[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
+                                        h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
+                                        h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
+                                        h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
+                                        h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
+            for (int k = 0; k < kArr; k++) {
+                so[kArr * i + k] = end;
+                end += align256(bytes[k]);
+            }
         }
-        const size_t o_devs = pk.reserve(sizeof(LbaDev) * P);
+        const size_t o_devs = end;
+        end += align256(sizeof(LbaDev) * P);
+        const size_t staged_end = end;
         // device-only scratch after the staged block (never copied)
-        size_t dev_end = pk.host.size();
-        auto dev_reserve = [&](size_t bytes) {
-            const size_t off = dev_end;
-            dev_end += (bytes + 255) & ~size_t(255);
-            return off;
-        };
+        std::vector<size_t> sc(8 * (size_t)P);
         for (int i = 0; i < P; i++) {
-            const HostStruct& s = hs[i];
-            const size_t nE = s.e_orig.size();
-            o[20][i] = dev_reserve(18 * nE * 8);
-            o[22][i] = dev_reserve(27 * (size_t)s.nP * 8);
-            o[23][i] = dev_reserve(9 * (size_t)s.nL * 8);
-            o[24][i] = dev_reserve(12 * (size_t)s.nL * 8);
-            const size_t n = 6 * (size_t)s.nP;
-            o[25][i] = dev_reserve(n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8);
-            o[26][i] = dev_reserve((n + 3 * (size_t)s.nL) * 8);
-            o[27][i] = dev_reserve(n * 8 + 8);
+            const HostStruct& h = hs[i];
+            const size_t nE = h.e_orig.size(), n = 6 * (size_t)h.nP;
+            const size_t bytes[7] = {18 * nE * 8, 27 * (size_t)h.nP * 8, 9 * (size_t)h.nL * 8, 12 * (size_t)h.nL * 8,
+                                     n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * (size_t)h.nL) * 8, n * 8 + 8};
+            for (int k = 0; k < 7; k++) {
+                sc[8 * i + k] = end;
+                end += align256(bytes[k]);
+            }
         }
-        bool full_upload = pass == 0;
+        const size_t dev_end = end;
         if (dev_end > ctx->scratch_bytes) {
             if (pass == 1) {   // keep the device-resident state across the reallocation
-                ORBX_HIP_CHECK(hipMemcpy(pk.host.data(), ctx->scratch, base_bytes, hipMemcpyDeviceToHost));
-                full_upload = true;
+                if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) break;
+                ORBX_HIP_CHECK(hipMemcpy(ctx->host_pinned, ctx->scratch, base_bytes, hipMemcpyDeviceToHost));
             }
             if ((r = ensure_scratch(ctx, dev_end)) != ORBX_OK) break;
+            if (pass == 1)
+                ORBX_HIP_CHECK(hipMemcpy(ctx->scratch, ctx->host_pinned, base_bytes, hipMemcpyHostToDevice));
         }
+        if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) break;
+        uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
         uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
-        for (int i = 0; i < P; i++) {
-            const HostStruct& s = hs[i];
+        // fill the staged bytes on host threads
+        host_parallel(P, [&](int i) {
             const orbx_ba_problem& p = probs[i];
+            const HostStruct& h = hs[i];
+            if (pass == 0) {
+                double* pose = reinterpret_cast<double*>(hb + pl[i].pose);
+                for (int k = 0; k < p.n_poses; k++) {
+                    for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
+                    for (int j = 0; j < 3; j++) pose[7 * k + 4 + j] = p.pose_t[3 * k + j];
+                }
+                std::memcpy(hb + pl[i].point, p.points, 3 * (size_t)p.n_points * 8);
+                std::memcpy(hb + pl[i].cam, p.pose_cam, 4 * (size_t)p.n_poses * 8);
+                std::memset(hb + pl[i].err, 0, 2 * (size_t)p.n_edges * 8);
+                std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
+                std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
+                std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
+            }
+            const void* src[kArr] = {h.e_orig.data(), h.e_pose.data(), h.e_point.data(), h.e_ph.data(),
+                                     h.e_lh.data(),   h.e_obs.data(),  h.e_isig.data(),  h.iv_pose.data(),
+                                     h.iv_point.data(), h.pe_ptr.data(), h.pe_idx.data(), h.le_ptr.data(),
+                                     h.le_idx.data(), h.lc_ptr.data(), h.lc_idx.data()};
+            const size_t bytes[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
+                                        h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
+                                        h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
+                                        h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
+                                        h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
+            for (int k = 0; k < kArr; k++)
+                if (bytes[k]) std::memcpy(hb + so[kArr * i + k], src[k], bytes[k]);
             LbaDev& D = devs[i];
             D = LbaDev{};
-            D.nP = s.nP;
-            D.nL = s.nL;
-            D.nE = (int)s.e_orig.size();
+            D.nP = h.nP;
+            D.nL = h.nL;
+            D.nE = (int)h.e_orig.size();
             D.nposes_all = p.n_poses;
             D.npoints_all = p.n_points;
             D.nedges_all = p.n_edges;
-            D.dim_p = 6 * s.nP;
-            D.pose = reinterpret_cast<double*>(d + o_pose[i]);
-            D.point = reinterpret_cast<double*>(d + o_point[i]);
-            D.pose_bk = reinterpret_cast<double*>(d + o_posebk[i]);
-            D.point_bk = reinterpret_cast<double*>(d + o_pointbk[i]);
-            D.cam = reinterpret_cast<const double*>(d + o_cam[i]);
-            D.err = reinterpret_cast<double*>(d + o_err[i]);
-            D.e_orig = reinterpret_cast<const int*>(d + o[0][i]);
-            D.e_pose = reinterpret_cast<const int*>(d + o[1][i]);
-            D.e_point = reinterpret_cast<const int*>(d + o[2][i]);
-            D.e_ph = reinterpret_cast<const int*>(d + o[3][i]);
-            D.e_lh = reinterpret_cast<const int*>(d + o[4][i]);
-            D.e_obs = reinterpret_cast<const double*>(d + o[5][i]);
-            D.e_isig = reinterpret_cast<const double*>(d + o[6][i]);
-            D.iv_pose = reinterpret_cast<const int*>(d + o[7][i]);
-            D.iv_point = reinterpret_cast<const int*>(d + o[8][i]);
-            D.pe_ptr = reinterpret_cast<const int*>(d + o[9][i]);
-            D.pe_idx = reinterpret_cast<const int*>(d + o[10][i]);
-            D.le_ptr = reinterpret_cast<const int*>(d + o[11][i]);
-            D.le_idx = reinterpret_cast<const int*>(d + o[12][i]);
-            D.lc_ptr = reinterpret_cast<const int*>(d + o[13][i]);
-            D.lc_idx = reinterpret_cast<const int*>(d + o[14][i]);
-            D.ce = reinterpret_cast<double*>(d + o[20][i]);
-            D.hp = reinterpret_cast<double*>(d + o[22][i]);
-            D.hl = reinterpret_cast<double*>(d + o[23][i]);
-            D.dl = reinterpret_cast<double*>(d + o[24][i]);
-            D.S = reinterpret_cast<double*>(d + o[25][i]);
-            D.x = reinterpret_cast<double*>(d + o[26][i]);
-            D.bs = reinterpret_cast<double*>(d + o[27][i]);
+            D.dim_p = 6 * h.nP;
+            D.pose = reinterpret_cast<double*>(d + pl[i].pose);
+            D.point = reinterpret_cast<double*>(d + pl[i].point);
+            D.pose_bk = reinterpret_cast<double*>(d + pl[i].posebk);
+            D.point_bk = reinterpret_cast<double*>(d + pl[i].pointbk);
+            D.cam = reinterpret_cast<const double*>(d + pl[i].cam);
+            D.err = reinterpret_cast<double*>(d + pl[i].err);
+            const size_t* o = &so[kArr * i];
+            D.e_orig = reinterpret_cast<const int*>(d + o[0]);
+            D.e_pose = reinterpret_cast<const int*>(d + o[1]);
+            D.e_point = reinterpret_cast<const int*>(d + o[2]);
+            D.e_ph = reinterpret_cast<const int*>(d + o[3]);
+            D.e_lh = reinterpret_cast<const int*>(d + o[4]);
+            D.e_obs = reinterpret_cast<const double*>(d + o[5]);
+            D.e_isig = reinterpret_cast<const double*>(d + o[6]);
+            D.iv_pose = reinterpret_cast<const int*>(d + o[7]);
+            D.iv_point = reinterpret_cast<const int*>(d + o[8]);
+            D.pe_ptr = reinterpret_cast<const int*>(d + o[9]);
+            D.pe_idx = reinterpret_cast<const int*>(d + o[10]);
+            D.le_ptr = reinterpret_cast<const int*>(d + o[11]);
+            D.le_idx = reinterpret_cast<const int*>(d + o[12]);
+            D.lc_ptr = reinterpret_cast<const int*>(d + o[13]);
+            D.lc_idx = reinterpret_cast<const int*>(d + o[14]);
+            const size_t* c = &sc[8 * i];
+            D.ce = reinterpret_cast<double*>(d + c[0]);
+            D.hp = reinterpret_cast<double*>(d + c[1]);
+            D.hl = reinterpret_cast<double*>(d + c[2]);
+            D.dl = reinterpret_cast<double*>(d + c[3]);
+            D.S = reinterpret_cast<double*>(d + c[4]);
+            D.x = reinterpret_cast<double*>(d + c[5]);
+            D.bs = reinterpret_cast<double*>(d + c[6]);
             D.huber_delta = p.huber_delta;
             D.status = kRunning;
             D.ni = 2;
-        }
-        std::memcpy(pk.host.data() + o_devs, devs.data(), sizeof(LbaDev) * P);
-        if (full_upload) {
-            ORBX_HIP_CHECK(hipMemcpy(d, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice));
-        } else {   // keep the persistent block (poses/points/errors/status) on the device
-            ORBX_HIP_CHECK(hipMemcpy(d + base_bytes, pk.host.data() + base_bytes, pk.host.size() - base_bytes,
-                                     hipMemcpyHostToDevice));
-        }
+        });
+        if (pass == 0) std::memcpy(hb + o_offs, offs.data(), offs.size() * 8);
+        std::memcpy(hb + o_devs, devs.data(), sizeof(LbaDev) * P);
+        mark("pack");
+        // pass 0: everything; pass 1: only the per-pass structures (the
+        // persistent block - poses, points, errors, status - stays on device)
+        const size_t up0 = pass == 0 ? 0 : base_bytes;
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + up0, hb + up0, staged_end - up0, hipMemcpyHostToDevice, ctx->stream));
+        mark("upload");
         LbaDev* dd = reinterpret_cast<LbaDev*>(d + o_devs);
         const int iters = pass == 0 ? iters0 : iters1;
         size_t max_n2 = 0;
@@ -1028,6 +1087,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
         ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + o_nout, 4 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
         ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        mark("iterations+outliers");
         if (stats)
             for (int i = 0; i < P; i++) {
                 stats[i].iterations[pass] = devs[i].iterations;
@@ -1039,22 +1099,22 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             }
     }
     if (r != ORBX_OK) return r;
-    // results
-    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
-    std::vector<uint8_t> bad(all_bad.size());
-    ORBX_HIP_CHECK(hipMemcpy(bad.data(), d + o_all_bad, bad.size(), hipMemcpyDeviceToHost));
-    for (int i = 0; i < P; i++) {
+    // results: the persistent block in one copy, scattered on host threads
+    uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, ctx->scratch, base_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
-        std::vector<double> pose(7 * (size_t)p.n_poses);
-        ORBX_HIP_CHECK(hipMemcpy(pose.data(), d + o_pose[i], pose.size() * 8, hipMemcpyDeviceToHost));
+        const double* pose = reinterpret_cast<const double*>(hb + pl[i].pose);
         for (int k = 0; k < p.n_poses; k++) {
             for (int j = 0; j < 4; j++) p.pose_q[4 * k + j] = pose[7 * k + j];
             for (int j = 0; j < 3; j++) p.pose_t[3 * k + j] = pose[7 * k + 4 + j];
         }
-        ORBX_HIP_CHECK(hipMemcpy(p.points, d + o_point[i], 3 * (size_t)p.n_points * 8, hipMemcpyDeviceToHost));
+        std::memcpy(p.points, hb + pl[i].point, 3 * (size_t)p.n_points * 8);
         if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st.data() + offs[3 * i], p.n_edges);
-        if (point_bad && point_bad[i]) std::memcpy(point_bad[i], bad.data() + offs[3 * i + 1], p.n_points);
-    }
+        if (point_bad && point_bad[i]) std::memcpy(point_bad[i], hb + o_all_bad + offs[3 * i + 1], p.n_points);
+    });
+    mark("results");
     return ORBX_OK;
 }
 
