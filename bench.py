@@ -209,16 +209,21 @@ def run_lba(args, wl, rank, local, world, dist):
             for i in range(min(P, 32))]
     probs = [uniq[i % len(uniq)] for i in range(P)]
     ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
-    cps = [sb.to_ctypes(pr) for pr in probs]
-    n_edges = int(np.mean([c[0].n_edges for c in cps]))
+    # host-side problem arrays, marshalled once; BA updates poses and points
+    # in place, so each step first restores them from the problem's state
+    work = [sb.to_ctypes(pr) for pr in probs]
+    n_edges = int(np.mean([c[0].n_edges for c in work]))
+    arr = (sb.BAProblem * P)(*[c[0] for c in work])
+    es = [np.zeros(c[0].n_edges, np.uint8) for c in work]
+    pb = [np.zeros(c[0].n_points, np.uint8) for c in work]
+    esp = (ctypes.c_void_p * P)(*[e.ctypes.data for e in es])
+    pbp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in pb])
 
     def step():
-        fresh = [sb.to_ctypes(pr) for pr in probs]     # BA updates poses in place: restart from the same state
-        arr = (sb.BAProblem * P)(*[c[0] for c in fresh])
-        es = [np.zeros(c[0].n_edges, np.uint8) for c in fresh]
-        pb = [np.zeros(c[0].n_points, np.uint8) for c in fresh]
-        esp = (ctypes.c_void_p * P)(*[e.ctypes.data for e in es])
-        pbp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in pb])
+        for (_, a), pr in zip(work, probs):
+            np.copyto(a["pose_q"], pr["pose_q"])
+            np.copyto(a["pose_t"], pr["pose_t"])
+            np.copyto(a["points"], pr["points"])
         st = (sb.BAStats * P)()
         r = ox.lib().orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, esp, pbp, st)
         if r != 0:

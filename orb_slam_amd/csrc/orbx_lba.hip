@@ -788,26 +788,39 @@ void build_struct(const orbx_ba_problem& p, const uint8_t* removed, HostStruct& 
         s.e_obs[2 * a + 1] = p.edge_obs[2 * e + 1];
         s.e_isig[a] = p.edge_inv_sigma2[e];
     }
-    // CSR helpers
-    auto csr = [](int n, const std::vector<std::vector<int>>& lists, std::vector<int>& ptr, std::vector<int>& idx) {
+    // CSR lists by counting sort (edge order kept within a bucket): no
+    // per-bucket allocations, which contend in malloc across host threads
+    auto csr = [&](int n, auto key, std::vector<int>& ptr, std::vector<int>& idx) {
         ptr.assign(n + 1, 0);
-        idx.clear();
-        for (int i = 0; i < n; i++) {
-            ptr[i] = (int)idx.size();
-            idx.insert(idx.end(), lists[i].begin(), lists[i].end());
+        for (int a = 0; a < nE; a++) {
+            const int k = key(a);
+            if (k >= 0) ptr[k + 1]++;
         }
-        ptr[n] = (int)idx.size();
+        for (int i = 0; i < n; i++) ptr[i + 1] += ptr[i];
+        idx.resize(ptr[n]);
+        std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+        for (int a = 0; a < nE; a++) {
+            const int k = key(a);
+            if (k >= 0) idx[fill[k]++] = a;
+        }
     };
-    std::vector<std::vector<int>> pe(s.nP), le(s.nL), lc(s.nL);
-    for (int a = 0; a < nE; a++) {
-        if (s.e_ph[a] >= 0) pe[s.e_ph[a]].push_back(a);
-        le[s.e_lh[a]].push_back(a);
-        if (s.e_ph[a] >= 0) lc[s.e_lh[a]].push_back(a);
+    csr(s.nP, [&](int a) { return s.e_ph[a]; }, s.pe_ptr, s.pe_idx);
+    csr(s.nL, [&](int a) { return s.e_lh[a]; }, s.le_ptr, s.le_idx);
+    csr(s.nL, [&](int a) { return s.e_ph[a] >= 0 ? s.e_lh[a] : -1; }, s.lc_ptr, s.lc_idx);
+    // Schur columns of a point in pose order (stable: insertion sort of the
+    // point's few edges by pose hessian index)
+    for (int l = 0; l < s.nL; l++) {
+        int* v = s.lc_idx.data();
+        for (int i = s.lc_ptr[l] + 1; i < s.lc_ptr[l + 1]; i++) {
+            const int x = v[i];
+            int j = i - 1;
+            while (j >= s.lc_ptr[l] && s.e_ph[v[j]] > s.e_ph[x]) {
+                v[j + 1] = v[j];
+                j--;
+            }
+            v[j + 1] = x;
+        }
     }
-    for (auto& v : lc) std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return s.e_ph[x] < s.e_ph[y]; });
-    csr(s.nP, pe, s.pe_ptr, s.pe_idx);
-    csr(s.nL, le, s.le_ptr, s.le_idx);
-    csr(s.nL, lc, s.lc_ptr, s.lc_idx);
 }
 
 // Packs host vectors into one device allocation.
@@ -893,10 +906,16 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     std::vector<long long> offs(3 * P);
     size_t at = 0;
     long long eacc = 0, pacc = 0;
+    // poses and points of all problems first: the results copy reads back
+    // only that prefix
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         pl[i].pose = at;    at += align256(7 * (size_t)p.n_poses * 8);
         pl[i].point = at;   at += align256(3 * (size_t)p.n_points * 8);
+    }
+    const size_t result_bytes = at;
+    for (int i = 0; i < P; i++) {
+        const orbx_ba_problem& p = probs[i];
         pl[i].posebk = at;  at += align256(7 * (size_t)p.n_poses * 8);
         pl[i].pointbk = at; at += align256(3 * (size_t)p.n_points * 8);
         pl[i].cam = at;     at += align256(4 * (size_t)p.n_poses * 8);
@@ -1099,9 +1118,11 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             }
     }
     if (r != ORBX_OK) return r;
-    // results: the persistent block in one copy, scattered on host threads
+    // results: poses and points in one copy, scattered on host threads
     uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb, ctx->scratch, base_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, ctx->scratch, result_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb + o_all_bad, static_cast<uint8_t*>(ctx->scratch) + o_all_bad, (size_t)pacc,
+                                  hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
