@@ -23,7 +23,7 @@
 namespace orbx {
 
 constexpr size_t kRetainLds = 128 * 1024;   // LDS budget of a retain block
-constexpr int kRetainCellCap = 1024;        // cell lists up to this length sort in LDS
+constexpr int kRetainCellCap = 512;         // cell lists up to this length sort in LDS
 constexpr int kSplitMinFrames = 16;         // batches >= 2x this run as two concurrent halves
 constexpr size_t kResizeLds = 96 * 1024;    // LDS budget of a staged resize strip
 
