@@ -977,12 +977,32 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
             inside[j] = xi >= 0 && xi < L.w;
             half_even[j] = xi < L.nvec_blur;
         }
-        int R[7][4];
+        // Vertical pass in packed FP32 (two pixels per v_pk_fma_f32): the row
+        // sums are integers <= 255 * 257 and N <= 255 * 257^2; every partial
+        // sum below 2^24 is exact, and an N beyond 2^24 saturates to 255 either
+        // way.  Rounding and saturation by v_cvt_pk_u8_f32 (round half to even
+        // = cvtps2dq of SymmColumnVec_32s8u); the scalar tail columns
+        // (FixedPtCastEx, +2^15 >> 16) pass floor((N + 2^15) / 2^16).
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        constexpr float kInv = 1.0f / 65536.0f;
+        bool tail_col[4], any_tail = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            tail_col[j] = inside[j] && !half_even[j];
+            any_tail = any_tail || tail_col[j];
+        }
+        f2 R[7][2];
+        auto hrow = [&](uint32_t l, uint32_t c, uint32_t r, f2 (&out)[2]) {
+            int hs[4];
+            blur_hsum_w(l, c, r, hs);
+            out[0] = f2{(float)hs[0], (float)hs[1]};
+            out[1] = f2{(float)hs[2], (float)hs[3]};
+        };
         uint32_t C[3];   // raw centre words of rows y, y+1, y+2 (loaded as rows y'+3 earlier)
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const uint32_t wc = ld(ya - 3 + k, 0);
-            blur_hsum_w(ld(ya - 3 + k, -4), wc, ld(ya - 3 + k, 4), R[k]);
+            hrow(ld(ya - 3 + k, -4), wc, ld(ya - 3 + k, 4), R[k]);
             if (k >= 3) C[k - 3] = wc;
         }
         // chunks of 7 output rows (the window's period: the register
@@ -1004,29 +1024,32 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
                 // rows past yb are computed on repeated input and not stored:
                 // no early exit, so the window rotation stays straight-line
                 const int y = yc + k;
-                blur_hsum_w(wl[k], wc[k], wr[k], R[6]);
-                const uint32_t raw = C[0];
-                uint32_t word = 0;
+                hrow(wl[k], wc[k], wr[k], R[6]);
+                float sv[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    uint32_t v = (raw >> (8 * j)) & 0xFF;
-                    if (inside[j]) {
-                        // 24-bit multiplies: R <= 255 * 257
-                        const uint32_t N = __umul24(R[3][j], 55u) + __umul24(R[2][j] + R[4][j], 49u) +
-                                           __umul24(R[1][j] + R[5][j], 34u) + __umul24(R[0][j] + R[6][j], 18u);
-                        // Columns < nvec: float path, N / 2^16 rounded half to even
-                        // (cvtps2dq); the tail: FixedPtCastEx, +2^15 >> 16.  The
-                        // taps sum to 257, so N can exceed 255 * 2^16: saturate
-                        const uint32_t half = half_even[j] ? 0x7FFFu + ((N >> 16) & 1u) : 0x8000u;
-                        v = min((N + half) >> 16, 255u);
+                for (int h = 0; h < 2; h++) {
+                    f2 N = R[3][h] * 55.0f;
+                    N = __builtin_elementwise_fma(R[2][h] + R[4][h], f2{49.0f, 49.0f}, N);
+                    N = __builtin_elementwise_fma(R[1][h] + R[5][h], f2{34.0f, 34.0f}, N);
+                    N = __builtin_elementwise_fma(R[0][h] + R[6][h], f2{18.0f, 18.0f}, N);
+                    const f2 sc = N * kInv;
+                    sv[2 * h] = sc.x;
+                    sv[2 * h + 1] = sc.y;
+                    if (any_tail) {
+                        const f2 tl = (N + 32768.0f) * kInv;
+                        if (tail_col[2 * h]) sv[2 * h] = floorf(tl.x);
+                        if (tail_col[2 * h + 1]) sv[2 * h + 1] = floorf(tl.y);
                     }
-                    word |= v << (8 * j);
                 }
+                uint32_t word = C[0];   // border columns keep the raw byte
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (inside[j]) word = __builtin_amdgcn_cvt_pk_u8_f32(sv[j], j, word);
                 if (y < yb) st(y, word & keep_mask);
 #pragma unroll
                 for (int kk = 0; kk < 6; kk++)
 #pragma unroll
-                    for (int j = 0; j < 4; j++) R[kk][j] = R[kk + 1][j];
+                    for (int h = 0; h < 2; h++) R[kk][h] = R[kk + 1][h];
                 C[0] = C[1];
                 C[1] = C[2];
                 C[2] = wc[k];
