@@ -13,6 +13,11 @@ Workloads (BASELINE.json configs):
      outlier passes), a batch of independent problems per step (problems/s);
      inputs cross the host boundary (the reference hands BA its graph from
      host memory), so this rate includes the H2D/D2H copies.
+  pose: Optimizer::PoseOptimization (SURVEY.md 8(f) row 1): a batch of
+     independent 640x480 tracking frames (1000 keypoints, ~70 % with a map
+     point, ~10 % gross outliers) staged in HBM once; one step = the full
+     four-round robust pose optimisation of every frame from its initial
+     pose (frames/s).
 
 Multi-GPU: one process per GPU (torchrun); each rank owns its sequence (or
 problems); the only collective is the end-of-run gather of stats (RCCL).
@@ -48,7 +53,13 @@ WORKLOADS = {
     "c5": dict(batch=256, metric="local BA problems/sec (20 KF x 2000 MP, 5+10 LM iterations)", unit="problems/s",
                desc="Optimizer::LocalBundleAdjustment core: 20 keyframes (+2 fixed) x 2000 map points, "
                     "Huber, Schur + LLT, 5+10 LM iterations, two outlier passes"),
+    "pose": dict(batch=8192, metric="frames/sec Optimizer::PoseOptimization (1000 kp, ~700 map points)",
+                 unit="frames/s",
+                 desc="Optimizer::PoseOptimization: 1000 keypoints, ~700 map-point edges, ~10 % outliers, "
+                      "Huber, 4 robust rounds (10/10/7/5 LM iterations), Eigen-LDLT 6x6 trials"),
 }
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (AMD spec: 256 CU x 128 FLOP/clk x 2.4 GHz)
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
@@ -136,6 +147,74 @@ def cpu_baseline_lba(probs, budget_s):
     return {"value": round(n / dt, 4), "unit": "problems/s", "cores": 1, "kind": "port",
             "sample": f"{n} problems (20 KF x 2000 MP), oracle LBA (dense LLT in place of CHOLMOD), "
                       f"1 thread, {dt:.1f} s"}
+
+
+def pose_flops(stats, n_edges):
+    """FP64 flops of one PoseOptimization from its LM statistics: ~215 per
+    edge per fused error+Jacobian+H pass (one per LM iteration), ~55 per edge
+    per trial error pass and per classification (counted from the kernel's
+    arithmetic; orb_slam_amd/csrc/orbx_pose.hip)."""
+    f = 0.0
+    active = n_edges
+    for r in range(stats.rounds):
+        f += stats.iterations[r] * 215.0 * active + stats.levenberg_trials[r] * 55.0 * active + 55.0 * n_edges
+        active = n_edges - stats.n_bad[r]
+    return f
+
+
+def cpu_baseline_pose(frames, budget_s):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_pose as sp
+    L = oracle_lib.load()
+    L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    structs = [sp.to_ctypes(fr) for fr in frames]
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < budget_s and n < 64 * len(frames):
+        p, arrs = structs[n % len(structs)]
+        q = sp.PoseFrame.from_buffer_copy(p)          # fresh initial pose each time
+        L.orbx_ref_pose_optimization(ctypes.byref(q), None, None)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames of the same synthetic set, oracle PoseOptimization (Eigen-LDLT restatement), "
+                      f"1 thread, {dt:.1f} s"}
+
+
+def run_pose(args, wl, rank, local, world, dist):
+    from orb_slam_amd import synth_pose as sp
+    P = args.batch or wl["batch"]
+    uniq = [sp.make_frame(n_kp=1000, seed=odist.shard_seed(7000, rank) * 1000 + i) for i in range(min(P, 256))]
+    frames = [uniq[i % len(uniq)] for i in range(P)]
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
+    keep = [sp.to_ctypes(fr) for fr in frames]
+    ctx.pose_stage([k[0] for k in keep])
+    n_edges = int(np.mean([fr["has_mp"].sum() for fr in uniq]))
+
+    def step():
+        ctx.pose_run()
+
+    for _ in range(args.warmup):
+        step()
+    elapsed, kernels = timed(args, ctx, step, dist, ["pose"])
+    kernels = {"overlapped": kernels, "isolated": None}
+    arr, n_inl, st = ctx.pose_fetch()
+    stats = np.array([elapsed, P * args.steps, int(n_inl[0]), st[0].rounds], dtype=np.float64)
+    ab = {"pose": n_edges * 25 + 80 + 160}
+    units_per_launch = {"pose": P}
+    flops = float(np.mean([pose_flops(st[i], int(frames[i]["has_mp"].sum())) for i in range(len(uniq))]))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_pose(uniq, args.cpu_budget)
+    check = {"inliers_frame0": int(n_inl[0]), "edges_frame0": int(frames[0]["has_mp"].sum()),
+             "rounds_frame0": int(st[0].rounds), "lm_iterations_frame0": list(st[0].iterations),
+             "fp64_flops_per_frame": round(flops)}
+    cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": P, "keypoints": 1000, "map_point_edges": n_edges,
+           "parallelism": f"dp{world} (independent frames per GPU)",
+           "boundary": "frames staged in HBM before the timed region (orbx_pose_stage); results fetched after"}
+    ctx.close()
+    return stats, kernels, ab, units_per_launch, cpu, check, cfg
 
 
 def run_frames(args, wl, rank, local, world, dist):
@@ -254,7 +333,8 @@ def run_lba(args, wl, rank, local, world, dist):
 # bench timer name -> kernel symbol in the rocprofv3 CSVs
 KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": "k_pyr_resize", "fast": "k_fast_cells",
                  "retain": "k_retain_cells", "blur": "k_blur", "describe": "k_describe",
-                 "match": "k_match_", "lba_iter": "k_lba_iteration", "lba_outliers": "k_lba_outliers"}
+                 "match": "k_match_", "lba_iter": "k_lba_iteration", "lba_outliers": "k_lba_outliers",
+                 "pose": "k_pose_opt"}
 
 
 def pmc_traffic(workload, name):
@@ -328,7 +408,7 @@ def main():
         dist = tdist
 
     wl = WORKLOADS[args.workload]
-    run = run_lba if args.workload == "c5" else run_frames
+    run = {"c5": run_lba, "pose": run_pose}.get(args.workload, run_frames)
     stats, kernels, ab, units, cpu, check, cfg = run(args, wl, rank, local, world, dist)
     allst = odist.gather_stats(stats, dist, device="cuda")
     value, elapsed, _ = odist.job_rate(allst)
@@ -359,12 +439,17 @@ def main():
             "metric": wl["metric"], "value": round(value, 2), "unit": wl["unit"], "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64" if args.workload == "c5" else "u8",
-            "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py, seeded per rank)",
+            "dtype": "f64" if args.workload in ("c5", "pose") else "u8",
+            "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py / synth_pose.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
         if roof_iso:
             out["roofline_isolated"] = roof_iso
+        if args.workload == "pose" and roof.get("avg_launch_ms"):
+            fl = check["fp64_flops_per_frame"] * units["pose"] / (roof["avg_launch_ms"] / 1e3) / 1e12
+            out["roofline_fp64"] = {"bound": "fp64-valu", "achieved": round(fl, 3), "peak": FP64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": round(fl / FP64_PEAK_TFLOPS, 5),
+                                    "flops_per_frame": check["fp64_flops_per_frame"]}
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)

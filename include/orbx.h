@@ -300,6 +300,57 @@ int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems,
                          int iters0, int iters1, uint8_t* const* edge_status,
                          uint8_t* const* point_bad, orbx_ba_stats* stats);
 
+/* ------------------------------------------------------------------------ */
+/* D. Motion-only pose optimisation                   */
+/* ------------------------------------------------------------------------ */
+
+/* One Frame as Optimizer::PoseOptimization(Frame*) reads and writes it
+ * (src/Optimizer.cc:154-285).  Keypoints with a map point become
+ * EdgeSE3ProjectXYZ edges to fixed points (information = I *
+ * mvInvLevelSigma2[octave], Huber delta sqrt(5.991)); four robust rounds
+ * (chi2 9.210 / 7.378 / 5.991 / 5.991, LM iterations 10 / 10 / 7 / 5)
+ * classify outliers. */
+typedef struct {
+    int n;                           /* N = mvpMapPoints.size() (= keypoints)    */
+    const float* kp_un;              /* [n][2] mvKeysUn[i].pt                    */
+    const int32_t* octave;           /* [n] mvKeysUn[i].octave                   */
+    const float* inv_level_sigma2;   /* [nlevels] mvInvLevelSigma2               */
+    int nlevels;
+    const uint8_t* has_mp;           /* [n] mvpMapPoints[i] != NULL              */
+    const float* mp_xyz;             /* [n][3] mvpMapPoints[i]->GetWorldPos()    */
+    float cam[4];                    /* fx, fy, cx, cy                           */
+    float Tcw[16];                   /* mTcw, row-major 4x4 (in/out)             */
+    uint8_t* outlier;                /* [n] mvbOutlier (in/out: entries with a map
+                                        point are written, the rest untouched)   */
+} orbx_pose_frame;
+
+typedef struct {
+    int rounds;                      /* robust rounds run (stops after round 0
+                                        when the frame has < 10 edges)           */
+    int iterations[4];               /* LM iterations per round                  */
+    int levenberg_trials[4];         /* inner LM trials per round                */
+    int n_bad[4];                    /* outliers after each round                */
+    double chi2_final[4];            /* robust chi2 of the accepted state        */
+    int not_posdef;                  /* LDLT failures (step rejected)            */
+} orbx_pose_stats;
+
+/* Replaces Optimizer::PoseOptimization(Frame*): updates f->Tcw and
+ * f->outlier, *n_inliers = the function's return value
+ * (nInitialCorrespondences - nBad).  stats may be NULL. */
+int orbx_pose_optimization(orbx_ctx* ctx, orbx_pose_frame* f, int* n_inliers,
+                           orbx_pose_stats* stats);
+/* Batched form: P independent frames (one wavefront each, one launch). */
+int orbx_pose_optimization_batch(orbx_ctx* ctx, int P, orbx_pose_frame* frames,
+                                 int32_t* n_inliers, orbx_pose_stats* stats);
+/* Device-resident form of the batch (bench/tests): stage P frames in HBM
+ * once, run the optimisation from the staged initial poses any number of
+ * times (asynchronous, on the context stream; kernel timer "pose"), fetch
+ * the results of the last run into the frames' Tcw / outlier. */
+int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames);
+int orbx_pose_run(orbx_ctx* ctx);
+int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* n_inliers,
+                    orbx_pose_stats* stats);
+
 /* Library identification. */
 const char* orbx_version(void);
 

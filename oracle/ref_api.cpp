@@ -339,3 +339,37 @@ extern "C" void orbx_ref_edge_linearize(const double* pose, const double* point,
     in.chi2_threshold = 1e9;
     edge_linearize_for_test(in, err, A, B);
 }
+
+// ---- motion-only pose optimisation ----
+#include "ref_pose.h"
+
+extern "C" int orbx_ref_pose_optimization(orbx_pose_frame* f, int* n_inliers, orbx_pose_stats* stats)
+{
+    if (!f || f->n < 0 || f->nlevels <= 0) return ORBX_ERR_ARG;
+    std::vector<float> isig(f->n > 0 ? f->n : 1, 0.f);
+    for (int i = 0; i < f->n; i++) {
+        if (!f->has_mp[i]) continue;
+        if (f->octave[i] < 0 || f->octave[i] >= f->nlevels) return ORBX_ERR_ARG;
+        isig[i] = f->inv_level_sigma2[f->octave[i]];   // pFrame->mvInvLevelSigma2[kpUn.octave] (:212)
+    }
+    PoseStats st;
+    const int r = pose_optimization(f->Tcw, f->cam, f->n, f->kp_un, isig.data(), f->has_mp, f->mp_xyz, f->outlier, &st);
+    if (n_inliers) *n_inliers = r;
+    if (stats) {
+        stats->rounds = st.rounds;
+        for (int k = 0; k < 4; k++) {
+            stats->iterations[k] = st.iterations[k];
+            stats->levenberg_trials[k] = st.trials[k];
+            stats->n_bad[k] = st.n_bad[k];
+            stats->chi2_final[k] = st.chi2_final[k];
+        }
+        stats->not_posdef = st.not_posdef;
+    }
+    return ORBX_OK;
+}
+
+// Eigen LDLT restatement (unit test against numpy's solve)
+extern "C" int orbx_ref_ldlt_solve(int n, const double* a, const double* b, double* x)
+{
+    return ldlt_solve(n, a, b, x) ? 1 : 0;
+}

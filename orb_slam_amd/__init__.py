@@ -90,6 +90,11 @@ def _declare(L):
         "orbx_search_by_projection_local": ([vp, vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, ip], i),
         "orbx_lba_solve": ([vp, vp, i, i, vp, vp, vp, vp], i),
         "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp], i),
+        "orbx_pose_optimization": ([vp, vp, ip, vp], i),
+        "orbx_pose_optimization_batch": ([vp, i, vp, vp, vp], i),
+        "orbx_pose_stage": ([vp, i, vp], i),
+        "orbx_pose_run": ([vp], i),
+        "orbx_pose_fetch": ([vp, vp, vp, vp], i),
         "orbx_version": ([], ctypes.c_char_p),
         "orbx_describe_levels": ([i, f, i, i, i, i, vp, i], i),
     }
@@ -232,6 +237,37 @@ class Context:
         if n < 0:
             raise OrbxError(n, "orbx_dev_kernel_time")
         return n, avg.value, tot.value
+
+    # --- Optimizer::PoseOptimization --------------------------------------
+    def pose_optimization(self, frames):
+        """Optimizer::PoseOptimization on a list of orbx_pose_frame structs
+        (orb_slam_amd.synth_pose.to_ctypes): updates their Tcw / outlier in
+        place, returns (n_inliers, stats)."""
+        from .synth_pose import PoseStats
+        arr = (type(frames[0]) * len(frames))(*frames)
+        n = np.zeros(len(frames), np.int32)
+        st = (PoseStats * len(frames))()
+        _check(lib().orbx_pose_optimization_batch(self._h, len(frames), arr, _ptr(n), st),
+               "orbx_pose_optimization_batch")
+        for k in range(len(frames)):
+            frames[k].Tcw = arr[k].Tcw
+        return n, list(st)
+
+    def pose_stage(self, frames):
+        arr = (type(frames[0]) * len(frames))(*frames)
+        _check(lib().orbx_pose_stage(self._h, len(frames), arr), "orbx_pose_stage")
+        self._pose_staged = arr
+
+    def pose_run(self):
+        _check(lib().orbx_pose_run(self._h), "orbx_pose_run")
+
+    def pose_fetch(self):
+        from .synth_pose import PoseStats
+        arr = self._pose_staged
+        n = np.zeros(len(arr), np.int32)
+        st = (PoseStats * len(arr))()
+        _check(lib().orbx_pose_fetch(self._h, arr, _ptr(n), st), "orbx_pose_fetch")
+        return arr, n, list(st)
 
     @property
     def handle(self):

@@ -79,10 +79,11 @@ static void free_buffers(orbx_ctx* ctx)
                     ctx->level_keys, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
-                    ctx->scratch};
+                    ctx->scratch, ctx->pose_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    if (ctx->pose_host) (void)hipHostFree(ctx->pose_host);
 }
 
 // Make the device tables and buffers describe frames of w x h.

@@ -179,6 +179,17 @@ struct orbx_ctx {
     size_t scratch_bytes = 0;
     void* host_pinned = nullptr;
     size_t host_pinned_bytes = 0;
+    // staged pose-optimisation batch (orbx_pose_stage / run / fetch)
+    void* pose_dev = nullptr;
+    size_t pose_dev_bytes = 0;
+    void* pose_host = nullptr;
+    size_t pose_host_bytes = 0;
+    int pose_P = 0;
+    long long pose_E = 0;
+    size_t pose_o_flags = 0, pose_o_out = 0, pose_out_bytes = 0;
+    std::vector<int32_t> pose_edge_kp;     // edge -> keypoint index (frame-local)
+    std::vector<long long> pose_e0;        // first edge of each frame
+    bool pose_ran = false;
     // timing
     bool timing = false;
     std::string timing_only;   // non-empty: only this timer records (orbx_dev_kernel_time_select)

@@ -1,0 +1,674 @@
+// Motion-only pose optimisation on MI355X (FP64): Optimizer::PoseOptimization
+// (src/Optimizer.cc:154-285) for batches of frames.
+//
+// g2o subset (as the reference configures it): one VertexSE3Expmap against
+// fixed VertexSBAPointXYZ vertices through EdgeSE3ProjectXYZ edges with a
+// Huber kernel, BlockSolverX + LinearSolverDense (Eigen LDLT, diagonal
+// pivoting) and OptimizationAlgorithmLevenberg with ORB-SLAM's stop rule.
+// The points are fixed, so the Schur complement is empty and every LM trial
+// is a 6x6 solve.
+//
+// Mapping: one wavefront per frame, four frames per 256-thread workgroup,
+// the whole four-round robust optimisation (up to 32 LM iterations of up to
+// 10 trials) in ONE launch, no LDS and no barriers.  Lanes stride the frame's
+// edges (edge a on lane a % 64 for the whole run, so an edge's level flag is
+// lane-private); per LM iteration one fused pass computes the errors, the
+// robust chi2, the Jacobians and the 21 lower entries of H plus b; per trial
+// one pass computes the trial errors.  Sums are wave reductions whose result
+// is bitwise identical on every lane, so the LDLT, the exp-map update and
+// the accept/reject logic run redundantly on uniform data (no broadcast).
+//
+// Stored-error semantics: g2o's outlier test reads each edge's _error as
+// left by the LAST computeActiveErrors -- the final trial's state even when
+// that trial was rejected and the estimate popped.  The kernel keeps that
+// pose ("errpose") and re-evaluates active edges there; edges already
+// classified as outliers are recomputed at the current pose
+// (src/Optimizer.cc:250-251).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_se3.h"
+
+namespace orbx {
+
+struct PoseHdr {
+    long long e0;        // first edge in the SoA arrays
+    int nE;              // edges (keypoints with a map point)
+    int pad;
+    float T[12];         // initial Tcw rows 0..2
+    float cam[4];        // fx fy cx cy
+};
+
+struct PoseOut {
+    float T[12];
+    int n_inliers;
+    int rounds;
+    int iterations[4];
+    int trials[4];
+    int n_bad[4];
+    int not_posdef;
+    int pad;
+    double chi2_final[4];
+};
+
+constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
+
+// Wave sum whose result is the same double on every lane: DPP butterflies
+// inside each row of 16 (xor 1, xor 2 by quad_perm; the half-row and row
+// mirrors pair lanes symmetrically), then the four row sums combined by
+// readlane in a fixed order.
+__device__ inline double dpp_f64(double v, int ctrl_sel)
+{
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    int rlo, rhi;
+    switch (ctrl_sel) {
+    case 0:
+        rlo = __builtin_amdgcn_update_dpp(lo, lo, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+        rhi = __builtin_amdgcn_update_dpp(hi, hi, 0xB1, 0xf, 0xf, false);
+        break;
+    case 1:
+        rlo = __builtin_amdgcn_update_dpp(lo, lo, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+        rhi = __builtin_amdgcn_update_dpp(hi, hi, 0x4E, 0xf, 0xf, false);
+        break;
+    case 2:
+        rlo = __builtin_amdgcn_update_dpp(lo, lo, 0x141, 0xf, 0xf, false);  // row_half_mirror
+        rhi = __builtin_amdgcn_update_dpp(hi, hi, 0x141, 0xf, 0xf, false);
+        break;
+    default:
+        rlo = __builtin_amdgcn_update_dpp(lo, lo, 0x140, 0xf, 0xf, false);  // row_mirror
+        rhi = __builtin_amdgcn_update_dpp(hi, hi, 0x140, 0xf, 0xf, false);
+        break;
+    }
+    return __hiloint2double(rhi, rlo);
+}
+
+__device__ inline double lane_f64(double v, int lane)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ inline double wave_sum_uniform(double v)
+{
+    v += dpp_f64(v, 0);
+    v += dpp_f64(v, 1);
+    v += dpp_f64(v, 2);
+    v += dpp_f64(v, 3);
+    return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+
+__device__ inline int wave_sum_int(int v)
+{
+    v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+
+// Eigen::LDLT<MatrixXd> of the lower triangle of m (row-major 6x6) and the
+// solve of m x = b: the restatement of oracle/ref_pose.cpp ldlt_solve with
+// every index a compile-time constant (the runtime pivot selects among
+// unrolled swap variants), so the matrix stays in registers.
+__device__ inline void swap_d(double& a, double& b)
+{
+    const double t = a;
+    a = b;
+    b = t;
+}
+
+// Packed lower triangle: entry (i, j), j <= i, at i (i + 1) / 2 + j.
+#define LT(i, j) ((i) * ((i) + 1) / 2 + (j))
+
+__device__ inline bool ldlt6_solve(double m[21], const double b[6], double x[6])
+{
+    int tr[6];
+    double temp[6];
+    int sign = 0;   // 0 zero, 1 positive semidefinite, 2 negative semidefinite, 3 indefinite
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        int big = k;
+        double bv = fabs(m[LT(k, k)]);
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (fabs(m[LT(i, i)]) > bv) {
+                bv = fabs(m[LT(i, i)]);
+                big = i;
+            }
+        tr[k] = big;
+#pragma unroll
+        for (int q = k + 1; q < 6; q++) {
+            if (big == q) {
+#pragma unroll
+                for (int j = 0; j < k; j++) swap_d(m[LT(k, j)], m[LT(q, j)]);
+#pragma unroll
+                for (int i = q + 1; i < 6; i++) swap_d(m[LT(i, k)], m[LT(i, q)]);
+                swap_d(m[LT(k, k)], m[LT(q, q)]);
+#pragma unroll
+                for (int i = k + 1; i < q; i++) swap_d(m[LT(i, k)], m[LT(q, i)]);
+            }
+        }
+        if (k > 0) {
+#pragma unroll
+            for (int j = 0; j < k; j++) temp[j] = m[LT(j, j)] * m[LT(k, j)];
+            double acc = m[LT(k, 0)] * temp[0];
+#pragma unroll
+            for (int j = 1; j < k; j++) acc += m[LT(k, j)] * temp[j];
+            m[LT(k, k)] -= acc;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++)
+#pragma unroll
+                for (int j = 0; j < k; j++) m[LT(i, k)] -= m[LT(i, j)] * temp[j];
+        }
+        const double akk = m[LT(k, k)];
+        if (k < 5 && fabs(akk) > 0.0) {
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) m[LT(i, k)] /= akk;
+        }
+        if (sign == 1) {
+            if (akk < 0) sign = 3;
+        } else if (sign == 2) {
+            if (akk > 0) sign = 3;
+        } else if (sign == 0) {
+            if (akk > 0) sign = 1;
+            else if (akk < 0) sign = 2;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = b[i];
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+#pragma unroll
+        for (int q = k + 1; q < 6; q++)
+            if (tr[k] == q) swap_d(x[k], x[q]);
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < i; j++) x[i] -= m[LT(i, j)] * x[j];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        if (fabs(m[LT(i, i)]) > 2.2250738585072014e-308) x[i] /= m[LT(i, i)];
+        else x[i] = 0.0;
+    }
+#pragma unroll
+    for (int i = 4; i >= 0; i--) {
+        double s = m[LT(i + 1, i)] * x[i + 1];
+#pragma unroll
+        for (int j = i + 2; j < 6; j++) s += m[LT(j, i)] * x[j];
+        x[i] -= s;
+    }
+#pragma unroll
+    for (int k = 5; k >= 0; k--)
+#pragma unroll
+        for (int q = k + 1; q < 6; q++)
+            if (tr[k] == q) swap_d(x[k], x[q]);
+    return sign == 1 || sign == 0;
+}
+
+struct PoseEdgeArrays {
+    const float* ox;
+    const float* oy;
+    const float* isig;
+    const float* px;
+    const float* py;
+    const float* pz;
+};
+
+struct Cam {
+    double fx, fy, cx, cy;
+};
+
+// EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) at pose
+// (q x y z w, t): e = obs - (fx X/Z + cx, fy Y/Z + cy), Xc = q Xw + t.
+__device__ inline void pose_edge_error(const double* pose, const double X[3], double o0, double o1, const Cam& c,
+                                       double pc[3], double& e0, double& e1)
+{
+    se3_map(pose, X, pc);
+    const double u = pc[0] / pc[2] * c.fx + c.cx;
+    const double v = pc[1] / pc[2] * c.fy + c.cy;
+    e0 = o0 - u;
+    e1 = o1 - v;
+}
+
+// RobustKernelHuber::robustify (robust_kernel_impl.cpp:78-91)
+__device__ inline void huber2(double e2, double delta, double& rho0, double& rho1)
+{
+    const double dsqr = delta * delta;
+    if (e2 <= dsqr) {
+        rho0 = e2;
+        rho1 = 1.;
+    } else {
+        const double sq = sqrt(e2);
+        rho0 = 2 * sq * delta - dsqr;
+        rho1 = delta / sq;
+    }
+}
+
+__global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __restrict__ hdrs, PoseEdgeArrays ed,
+                                                          uint8_t* __restrict__ eflag, PoseOut* __restrict__ outs,
+                                                          int P, double delta)
+{
+    const int prob = blockIdx.x * (kPoseThreads / 64) + (threadIdx.x >> 6);
+    if (prob >= P) return;   // whole wavefront
+    const int lane = threadIdx.x & 63;
+    const PoseHdr& H = hdrs[prob];
+    const long long e0 = H.e0;
+    const int nE = H.nE;
+    const Cam cam{(double)H.cam[0], (double)H.cam[1], (double)H.cam[2], (double)H.cam[3]};
+    // Converter::toSE3Quat (src/Converter.cc:38-48)
+    double pose[7], errpose[7];
+    {
+        double R[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)H.T[i * 4 + j];
+        Q q = qfrom(R);
+        qnormalize(q);
+        pose[0] = q.x; pose[1] = q.y; pose[2] = q.z; pose[3] = q.w;
+#pragma unroll
+        for (int i = 0; i < 3; i++) pose[4 + i] = (double)H.T[i * 4 + 3];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) errpose[i] = pose[i];
+    const float* ox = ed.ox + e0;
+    const float* oy = ed.oy + e0;
+    const float* isg = ed.isig + e0;
+    const float* px = ed.px + e0;
+    const float* py = ed.py + e0;
+    const float* pz = ed.pz + e0;
+    uint8_t* flag = eflag + e0;
+    for (int a = lane; a < nE; a += 64) flag[a] = 0;
+
+    PoseOut& out = outs[prob];
+    int not_posdef = 0, rounds = 0;
+    int n_active = nE;
+    int nBadOut = 0;
+#pragma unroll 1
+    for (int it = 0; it < 4; it++) {
+        // const float chi2[4]={9.210,7.378,5.991,5.991}; const int its[4]={10,10,7,5}; (:236-237)
+        const float chi2th = it == 0 ? 9.210f : (it == 1 ? 7.378f : 5.991f);
+        const int its = it < 2 ? 10 : (it == 2 ? 7 : 5);
+        int r_iters = 0, r_trials = 0;
+        double r_chi = 0;
+        rounds = it + 1;
+        if (n_active > 0) {
+            double lambda = 0, ni = 2;
+            int nBadLM = 0;
+#pragma unroll 1
+            for (int iter = 0; iter < its; iter++) {
+                // computeActiveErrors + activeRobustChi2 + buildSystem (fused)
+                double h[21], bv[6], chi = 0;
+#pragma unroll
+                for (int k = 0; k < 21; k++) h[k] = 0;
+#pragma unroll
+                for (int k = 0; k < 6; k++) bv[k] = 0;
+        #pragma unroll 1
+        for (int a = lane; a < nE; a += 64) {
+                    if (flag[a]) continue;
+                    const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
+                    const double s = (double)isg[a];
+                    double pc[3], er0, er1;
+                    pose_edge_error(pose, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+                    const double c2 = er0 * (s * er0) + er1 * (s * er1);
+                    double rho0, rho1;
+                    huber2(c2, delta, rho0, rho1);
+                    chi += rho0;
+                    // EdgeSE3ProjectXYZ::linearizeOplus, pose block
+                    // (types_six_dof_expmap.cpp:384-420)
+                    const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+                    const double fx = cam.fx, fy = cam.fy;
+                    double B[12];
+                    B[0] = x * y / z_2 * fx;
+                    B[1] = -(1 + (x * x / z_2)) * fx;
+                    B[2] = y / z * fx;
+                    B[3] = -1. / z * fx;
+                    B[4] = 0;
+                    B[5] = x / z_2 * fx;
+                    B[6] = (1 + y * y / z_2) * fy;
+                    B[7] = -x * y / z_2 * fy;
+                    B[8] = -x / z * fy;
+                    B[9] = 0;
+                    B[10] = -1. / z * fy;
+                    B[11] = y / z_2 * fy;
+                    // constructQuadraticForm, toNotFixed branch
+                    // (base_binary_edge.hpp:96-113)
+                    const double w = rho1 * s;
+                    const double om0 = -(s * er0) * rho1, om1 = -(s * er1) * rho1;
+#pragma unroll
+                    for (int i = 0; i < 6; i++) bv[i] += B[i] * om0 + B[6 + i] * om1;
+                    int k = 0;
+#pragma unroll
+                    for (int i = 0; i < 6; i++)
+#pragma unroll
+                        for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
+                }
+                double currentChi = wave_sum_uniform(chi);
+                const double iniChi = currentChi;
+#pragma unroll
+                for (int k = 0; k < 21; k++) h[k] = wave_sum_uniform(h[k]);
+#pragma unroll
+                for (int k = 0; k < 6; k++) bv[k] = wave_sum_uniform(bv[k]);
+                if (iter == 0) {   // computeLambdaInit (levenberg.cpp:166-180)
+                    double mx = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) mx = fmax(fabs(h[LT(j, j)]), mx);
+                    lambda = 1e-5 * mx;
+                    ni = 2;
+                    nBadLM = 0;
+                }
+                double rho = 0;
+                int qmax = 0;
+                do {
+                    double m[21], xs[6], tp[7];
+#pragma unroll
+                    for (int k = 0; k < 21; k++) m[k] = h[k];
+#pragma unroll
+                    for (int j = 0; j < 6; j++) m[LT(j, j)] += lambda;
+                    const bool ok2 = ldlt6_solve(m, bv, xs);
+#pragma unroll
+                    for (int i = 0; i < 7; i++) tp[i] = pose[i];
+                    if (ok2) {
+                        se3_oplus(tp, xs);
+                    } else {
+                        not_posdef++;
+#pragma unroll
+                        for (int i = 0; i < 6; i++) xs[i] = 0.0;
+                    }
+                    // computeActiveErrors at the trial estimate
+                    double tchi = 0;
+            #pragma unroll 1
+        for (int a = lane; a < nE; a += 64) {
+                        if (flag[a]) continue;
+                        const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
+                        const double s = (double)isg[a];
+                        double pc[3], er0, er1;
+                        pose_edge_error(tp, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+                        double rho0, rho1;
+                        huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
+                        tchi += rho0;
+                    }
+                    double tempChi = wave_sum_uniform(tchi);
+#pragma unroll
+                    for (int i = 0; i < 7; i++) errpose[i] = tp[i];
+                    if (!ok2) tempChi = 1.79769313486231570815e+308;
+                    double scale = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) scale += xs[j] * (lambda * xs[j] + bv[j]);
+                    scale += 1e-3;
+                    rho = (currentChi - tempChi) / scale;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        alpha = fmin(alpha, 2. / 3.);
+                        lambda *= fmax(1. / 3., alpha);
+                        ni = 2;
+                        currentChi = tempChi;
+#pragma unroll
+                        for (int i = 0; i < 7; i++) pose[i] = tp[i];
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                    }
+                    qmax++;
+                } while (rho < 0 && qmax < 10);
+                r_iters++;
+                r_trials += qmax;
+                r_chi = currentChi;
+                if (qmax == 10 || rho == 0) break;
+                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                else nBadLM = 0;
+                if (nBadLM >= 3) break;
+            }
+        }
+        // outlier classification (src/Optimizer.cc:243-265)
+        int bad = 0, act = 0;
+        const double th = (double)chi2th;
+#pragma unroll 1
+        for (int a = lane; a < nE; a += 64) {
+            const uint8_t f = flag[a];
+            const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
+            const double s = (double)isg[a];
+            double pc[3], er0, er1;
+            pose_edge_error(f ? pose : errpose, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+            const double c2 = er0 * (s * er0) + er1 * (s * er1);
+            uint8_t nf = f;
+            if (c2 > th) {
+                nf = 1;
+                bad++;
+            } else if (c2 <= th) {
+                nf = 0;
+            }
+            act += nf == 0;
+            flag[a] = nf;
+        }
+        nBadOut = wave_sum_int(bad);
+        n_active = wave_sum_int(act);
+        if (lane == 0) {
+            out.iterations[it] = r_iters;
+            out.trials[it] = r_trials;
+            out.chi2_final[it] = r_chi;
+            out.n_bad[it] = nBadOut;
+        }
+        if (nE < 10) break;
+    }
+    if (lane == 0) {
+        double R[9];
+        qmat(Q{pose[0], pose[1], pose[2], pose[3]}, R);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) out.T[i * 4 + j] = (float)R[i * 3 + j];
+            out.T[i * 4 + 3] = (float)pose[4 + i];
+        }
+        out.n_inliers = nE - nBadOut;
+        out.rounds = rounds;
+        for (int r = rounds; r < 4; r++) {
+            out.iterations[r] = 0;
+            out.trials[r] = 0;
+            out.chi2_final[r] = 0;
+            out.n_bad[r] = 0;
+        }
+        out.not_posdef = not_posdef;
+    }
+}
+
+namespace {
+inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+template <typename Fn>
+void pose_parallel(int n, Fn fn)
+{
+    const int nth = std::max(1, std::min<int>(n / 64 + 1, std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+    if (nth == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nth; t++)
+        pool.emplace_back([&, t]() {
+            for (int i = t; i < n; i += nth) fn(i);
+        });
+    for (auto& th : pool) th.join();
+}
+}  // namespace
+
+}  // namespace orbx
+
+using namespace orbx;
+
+extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames)
+{
+    if (!ctx || P < 0 || (P > 0 && !frames)) return ORBX_ERR_ARG;
+    std::vector<long long> e0(P + 1, 0);
+    for (int i = 0; i < P; i++) {
+        const orbx_pose_frame& f = frames[i];
+        if (f.n < 0 || (f.n > 0 && (!f.kp_un || !f.octave || !f.has_mp || !f.mp_xyz || !f.outlier)) ||
+            f.nlevels <= 0 || !f.inv_level_sigma2)
+            return ORBX_ERR_ARG;
+        long long c = 0;
+        for (int k = 0; k < f.n; k++)
+            if (f.has_mp[k]) {
+                if (f.octave[k] < 0 || f.octave[k] >= f.nlevels) return ORBX_ERR_ARG;
+                c++;
+            }
+        e0[i + 1] = e0[i] + c;
+    }
+    const long long E = e0[P];
+    ctx_enter(ctx);
+    // layout: hdr[P] | 6 float edge arrays [E] | flags u8 [E] | out[P]
+    const size_t o_hdr = 0;
+    const size_t o_edges = align256(sizeof(PoseHdr) * (size_t)std::max(P, 1));
+    const size_t arr = align256(4 * (size_t)std::max<long long>(E, 1));
+    const size_t o_flags = o_edges + 6 * arr;
+    const size_t o_out = o_flags + align256((size_t)std::max<long long>(E, 1));
+    const size_t out_bytes = sizeof(PoseOut) * (size_t)std::max(P, 1);
+    const size_t total = o_out + align256(out_bytes);
+    const size_t staged = o_flags;                                  // copied H2D
+    const size_t host_need = std::max(staged, out_bytes + (size_t)std::max<long long>(E, 1));
+    if (total > ctx->pose_dev_bytes) {
+        if (ctx->pose_dev) (void)hipFree(ctx->pose_dev);
+        ctx->pose_dev = nullptr;
+        ctx->pose_dev_bytes = 0;
+        if (hipMalloc(&ctx->pose_dev, total) != hipSuccess) return ORBX_ERR_NOMEM;
+        ctx->pose_dev_bytes = total;
+    }
+    if (host_need > ctx->pose_host_bytes) {
+        if (ctx->pose_host) (void)hipHostFree(ctx->pose_host);
+        ctx->pose_host = nullptr;
+        ctx->pose_host_bytes = 0;
+        if (hipHostMalloc(&ctx->pose_host, host_need, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_NOMEM;
+        ctx->pose_host_bytes = host_need;
+    }
+    uint8_t* hb = static_cast<uint8_t*>(ctx->pose_host);
+    ctx->pose_edge_kp.assign((size_t)E, 0);
+    PoseHdr* hd = reinterpret_cast<PoseHdr*>(hb + o_hdr);
+    float* arrs[6];
+    for (int k = 0; k < 6; k++) arrs[k] = reinterpret_cast<float*>(hb + o_edges + k * arr);
+    pose_parallel(P, [&](int i) {
+        const orbx_pose_frame& f = frames[i];
+        PoseHdr& h = hd[i];
+        h.e0 = e0[i];
+        h.nE = (int)(e0[i + 1] - e0[i]);
+        h.pad = 0;
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 4; c++) h.T[r * 4 + c] = f.Tcw[r * 4 + c];
+        for (int c = 0; c < 4; c++) h.cam[c] = f.cam[c];
+        long long e = e0[i];
+        for (int k = 0; k < f.n; k++) {
+            if (!f.has_mp[k]) continue;
+            arrs[0][e] = f.kp_un[2 * k];
+            arrs[1][e] = f.kp_un[2 * k + 1];
+            arrs[2][e] = f.inv_level_sigma2[f.octave[k]];
+            arrs[3][e] = f.mp_xyz[3 * k];
+            arrs[4][e] = f.mp_xyz[3 * k + 1];
+            arrs[5][e] = f.mp_xyz[3 * k + 2];
+            ctx->pose_edge_kp[e] = k;
+            e++;
+        }
+    });
+    ORBX_HIP_CHECK(hipMemcpyAsync(ctx->pose_dev, hb, staged, hipMemcpyHostToDevice, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));   // the pinned buffer is reused by fetch
+    ctx->pose_P = P;
+    ctx->pose_E = E;
+    ctx->pose_o_flags = o_flags;
+    ctx->pose_o_out = o_out;
+    ctx->pose_out_bytes = out_bytes;
+    ctx->pose_e0 = e0;
+    ctx->pose_ran = false;
+    return ORBX_OK;
+}
+
+extern "C" int orbx_pose_run(orbx_ctx* ctx)
+{
+    if (!ctx || !ctx->pose_dev) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    const int P = ctx->pose_P;
+    ctx->pose_ran = true;
+    if (P == 0) return ORBX_OK;
+    uint8_t* d = static_cast<uint8_t*>(ctx->pose_dev);
+    const size_t arr = align256(4 * (size_t)std::max<long long>(ctx->pose_E, 1));
+    const size_t o_edges = align256(sizeof(PoseHdr) * (size_t)std::max(P, 1));
+    PoseEdgeArrays ed;
+    ed.ox = reinterpret_cast<const float*>(d + o_edges);
+    ed.oy = reinterpret_cast<const float*>(d + o_edges + arr);
+    ed.isig = reinterpret_cast<const float*>(d + o_edges + 2 * arr);
+    ed.px = reinterpret_cast<const float*>(d + o_edges + 3 * arr);
+    ed.py = reinterpret_cast<const float*>(d + o_edges + 4 * arr);
+    ed.pz = reinterpret_cast<const float*>(d + o_edges + 5 * arr);
+    const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
+    const int per = kPoseThreads / 64;
+    timer_begin(ctx, "pose");
+    k_pose_opt<<<(P + per - 1) / per, kPoseThreads, 0, ctx->stream>>>(
+        reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags, reinterpret_cast<PoseOut*>(d + ctx->pose_o_out),
+        P, delta);
+    timer_end(ctx, "pose");
+    ORBX_HIP_CHECK(hipGetLastError());
+    return ORBX_OK;
+}
+
+extern "C" int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* n_inliers, orbx_pose_stats* stats)
+{
+    if (!ctx || !ctx->pose_ran || (ctx->pose_P > 0 && !frames)) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    const int P = ctx->pose_P;
+    if (P == 0) return ORBX_OK;
+    const long long E = ctx->pose_E;
+    uint8_t* hb = static_cast<uint8_t*>(ctx->pose_host);
+    uint8_t* d = static_cast<uint8_t*>(ctx->pose_dev);
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d + ctx->pose_o_out, ctx->pose_out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (E > 0)
+        ORBX_HIP_CHECK(hipMemcpyAsync(hb + ctx->pose_out_bytes, d + ctx->pose_o_flags, (size_t)E,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const PoseOut* outs = reinterpret_cast<const PoseOut*>(hb);
+    const uint8_t* flags = hb + ctx->pose_out_bytes;
+    pose_parallel(P, [&](int i) {
+        orbx_pose_frame& f = frames[i];
+        const PoseOut& o = outs[i];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 4; c++) f.Tcw[r * 4 + c] = o.T[r * 4 + c];
+        f.Tcw[12] = 0.f;
+        f.Tcw[13] = 0.f;
+        f.Tcw[14] = 0.f;
+        f.Tcw[15] = 1.f;
+        for (long long e = ctx->pose_e0[i]; e < ctx->pose_e0[i + 1]; e++) f.outlier[ctx->pose_edge_kp[e]] = flags[e];
+        if (n_inliers) n_inliers[i] = o.n_inliers;
+        if (stats) {
+            orbx_pose_stats& s = stats[i];
+            s.rounds = o.rounds;
+            for (int r = 0; r < 4; r++) {
+                s.iterations[r] = o.iterations[r];
+                s.levenberg_trials[r] = o.trials[r];
+                s.n_bad[r] = o.n_bad[r];
+                s.chi2_final[r] = o.chi2_final[r];
+            }
+            s.not_posdef = o.not_posdef;
+        }
+    });
+    return ORBX_OK;
+}
+
+extern "C" int orbx_pose_optimization_batch(orbx_ctx* ctx, int P, orbx_pose_frame* frames, int32_t* n_inliers,
+                                            orbx_pose_stats* stats)
+{
+    int r = orbx_pose_stage(ctx, P, frames);
+    if (r != ORBX_OK) return r;
+    if ((r = orbx_pose_run(ctx)) != ORBX_OK) return r;
+    return orbx_pose_fetch(ctx, frames, n_inliers, stats);
+}
+
+extern "C" int orbx_pose_optimization(orbx_ctx* ctx, orbx_pose_frame* f, int* n_inliers, orbx_pose_stats* stats)
+{
+    if (!f) return ORBX_ERR_ARG;
+    int32_t n = 0;
+    const int r = orbx_pose_optimization_batch(ctx, 1, f, &n, stats);
+    if (r == ORBX_OK && n_inliers) *n_inliers = n;
+    return r;
+}
