@@ -98,10 +98,32 @@ int main()
             }
         }
         Optimizer::LocalBundleAdjustment(ex.context(), P);
+        // PoseOptimization of F2: every other keypoint gets a map point 3-5 m
+        // in front of the identity camera; the initial pose is off by 2 cm
+        PoseFrame PF;
+        PF.keys_un = F2.keys_un;
+        PF.fx = PF.fy = 500.f;
+        PF.cx = 320.f;
+        PF.cy = 240.f;
+        float sc = 1.f;
+        for (int l = 0; l < 8; l++, sc *= 1.2f) PF.inv_level_sigma2.push_back(1.f / (sc * sc));
+        for (size_t i = 0; i < PF.keys_un.size(); i++) {
+            const bool mp = (i % 2) == 0;
+            PF.has_mp.push_back(mp);
+            const float z = 3.f + (float)(i % 7) * 0.3f;
+            PF.mp_xyz.insert(PF.mp_xyz.end(), {(PF.keys_un[i].x - 320.f) / 500.f * z,
+                                               (PF.keys_un[i].y - 240.f) / 500.f * z, z});
+        }
+        PF.Tcw[3] = 0.02f;
+        const int n_pose_inliers = Optimizer::PoseOptimization(ex.context(), PF);
+        int n_mp = 0;
+        for (uint8_t m : PF.has_mp) n_mp += m;
         std::printf("{\"n1\": %zu, \"n2\": %zu, \"levels\": %d, \"scale\": %.3f, \"init_matches\": %d, "
-                    "\"bf_matches\": %d, \"ba_iterations\": [%d, %d], \"ba_chi2\": [%.6g, %.6g]}\n",
+                    "\"bf_matches\": %d, \"ba_iterations\": [%d, %d], \"ba_chi2\": [%.6g, %.6g], "
+                    "\"pose_inliers\": %d, \"pose_edges\": %d, \"pose_tx\": %.6g}\n",
                     F1.keys_un.size(), F2.keys_un.size(), ex.GetLevels(), ex.GetScaleFactor(), n_init, n_bf,
-                    P.stats.iterations[0], P.stats.iterations[1], P.stats.chi2_initial[0], P.stats.chi2_final[1]);
+                    P.stats.iterations[0], P.stats.iterations[1], P.stats.chi2_initial[0], P.stats.chi2_final[1],
+                    n_pose_inliers, n_mp, PF.Tcw[3]);
         return 0;
     } catch (const orbx_error& e) {
         std::fprintf(stderr, "%s\n", e.what());

@@ -290,8 +290,56 @@ struct LocalBAProblem {
     }
 };
 
+// ---------------------------------------------------------------------------
+// Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:154-285): the fields
+// of Frame it reads and writes.  mp_xyz holds pMP->GetWorldPos() for the
+// keypoints whose mvpMapPoints entry is set (has_mp).
+// ---------------------------------------------------------------------------
+struct PoseFrame {
+    std::vector<KeyPoint> keys_un;          // mvKeysUn
+    std::vector<float> inv_level_sigma2;    // mvInvLevelSigma2
+    std::vector<uint8_t> has_mp;            // mvpMapPoints[i] != NULL
+    std::vector<float> mp_xyz;              // 3 per keypoint
+    float fx = 0, fy = 0, cx = 0, cy = 0;
+    float Tcw[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};   // mTcw, row-major
+    std::vector<uint8_t> outlier;           // mvbOutlier
+    orbx_pose_stats stats{};
+};
+
 class Optimizer {
 public:
+    // Returns nInitialCorrespondences - nBad, updates F.Tcw and F.outlier.
+    static int PoseOptimization(orbx_ctx* ctx, PoseFrame& F)
+    {
+        const int n = (int)F.keys_un.size();
+        std::vector<float> kp(2 * (size_t)n);
+        std::vector<int32_t> oct(n);
+        for (int i = 0; i < n; i++) {
+            kp[2 * i] = F.keys_un[i].x;
+            kp[2 * i + 1] = F.keys_un[i].y;
+            oct[i] = F.keys_un[i].octave;
+        }
+        F.outlier.resize(n, 0);
+        orbx_pose_frame f;
+        f.n = n;
+        f.kp_un = kp.data();
+        f.octave = oct.data();
+        f.inv_level_sigma2 = F.inv_level_sigma2.data();
+        f.nlevels = (int)F.inv_level_sigma2.size();
+        f.has_mp = F.has_mp.data();
+        f.mp_xyz = F.mp_xyz.data();
+        f.cam[0] = F.fx;
+        f.cam[1] = F.fy;
+        f.cam[2] = F.cx;
+        f.cam[3] = F.cy;
+        for (int k = 0; k < 16; k++) f.Tcw[k] = F.Tcw[k];
+        f.outlier = F.outlier.data();
+        int inl = 0;
+        check(orbx_pose_optimization(ctx, &f, &inl, &F.stats), "Optimizer::PoseOptimization");
+        for (int k = 0; k < 16; k++) F.Tcw[k] = f.Tcw[k];
+        return inl;
+    }
+
     // pbStopFlag: LocalMapping's mbAbortBA, polled between LM iterations.
     static void LocalBundleAdjustment(orbx_ctx* ctx, LocalBAProblem& prob, bool* pbStopFlag = nullptr)
     {

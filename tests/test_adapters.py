@@ -40,3 +40,6 @@ def test_adapter_end_to_end(demo):
     assert r["init_matches"] > 50 and r["bf_matches"] > 50
     assert r["ba_iterations"][0] >= 1
     assert r["ba_chi2"][1] < r["ba_chi2"][0]
+    # noise-free map points: every edge an inlier, the 2 cm offset removed
+    assert r["pose_inliers"] == r["pose_edges"] > 100
+    assert abs(r["pose_tx"]) < 1e-3

@@ -149,3 +149,33 @@ def test_gpu_lba_golden(gctx):
     assert np.abs(arrs["points"] - z["out_points"]).max() <= 1e-4
     assert np.array_equal(es, z["edge_status"]) and np.array_equal(pb, z["point_bad"])
     assert list(st.iterations) == list(z["iterations"])
+
+
+# ------------------------------------------------------------------ pose optimisation
+def pose_frame(z):
+    return {k[3:]: z[k].copy() for k in z.files if k.startswith("in_")}
+
+
+def test_oracle_pose_golden():
+    from orb_slam_amd import synth_pose as sp
+    z = g("pose_frame")
+    p, arrs = sp.to_ctypes(pose_frame(z))
+    n = ctypes.c_int()
+    st = sp.PoseStats()
+    L = load()
+    L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    assert L.orbx_ref_pose_optimization(ctypes.byref(p), ctypes.byref(n), ctypes.byref(st)) == 0
+    assert np.array_equal(sp.pose_of(p), z["out_Tcw"])
+    assert np.array_equal(arrs["outlier"], z["out_outlier"]) and n.value == int(z["n_inliers"])
+    assert list(st.iterations) == list(z["iterations"]) and list(st.n_bad) == list(z["n_bad"])
+
+
+@pytest.mark.gpu
+def test_gpu_pose_golden(gctx):
+    from orb_slam_amd import synth_pose as sp
+    z = g("pose_frame")
+    p, arrs = sp.to_ctypes(pose_frame(z))
+    n, st = gctx.pose_optimization([p])
+    assert np.abs(sp.pose_of(p) - z["out_Tcw"]).max() <= 1e-5
+    assert np.array_equal(arrs["outlier"], z["out_outlier"]) and int(n[0]) == int(z["n_inliers"])
+    assert st[0].rounds == int(z["rounds"]) and list(st[0].n_bad) == list(z["n_bad"])

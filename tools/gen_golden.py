@@ -101,9 +101,28 @@ def gen_lba():
     print("lba", list(st.iterations), list(st.n_outliers))
 
 
+def gen_pose():
+    from orb_slam_amd import synth_pose as sp
+    fr = sp.make_frame(n_kp=300, seed=107, outlier_frac=0.15)
+    fr["outlier"][:] = 9
+    p, arrs = sp.to_ctypes(fr)
+    n = ctypes.c_int()
+    st = sp.PoseStats()
+    L = load()
+    L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    assert L.orbx_ref_pose_optimization(ctypes.byref(p), ctypes.byref(n), ctypes.byref(st)) == 0
+    inputs = {f"in_{k}": fr[k] for k in ["kp_un", "octave", "inv_level_sigma2", "has_mp", "mp_xyz", "cam", "Tcw",
+                                          "outlier"]}
+    np.savez_compressed(OUT / "pose_frame.npz", **inputs, out_Tcw=sp.pose_of(p), out_outlier=arrs["outlier"],
+                        n_inliers=n.value, rounds=st.rounds, iterations=np.array(st.iterations),
+                        n_bad=np.array(st.n_bad))
+    print("pose", n.value, list(st.iterations), list(st.n_bad))
+
+
 if __name__ == "__main__":
     OUT.mkdir(parents=True, exist_ok=True)
     gen_extract()
     gen_init_match()
     gen_hamming()
     gen_lba()
+    gen_pose()
