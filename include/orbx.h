@@ -249,6 +249,43 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F,
                                     const uint8_t* f_assigned, float th, float nnratio,
                                     int32_t* matches_f, int* n_matches);
 
+/* Vocabulary-node searches.  A keyframe or frame as
+ * the BoW matchers read it: keypoints (angle; pt and octave for the
+ * epipolar test), descriptors, the map-point state of every keypoint and
+ * its DBoW2::FeatureVector (node id -> feature indices, std::map order) as
+ * CSR arrays.  mp: 0 = no map point, 1 = map point, 2 = map point isBad().
+ * Every feature index appears in at most one node (DBoW2 transform). */
+typedef struct {
+    const orbx_keypoint* keys;      /* [n] mvKeysUn (Frame side of
+                                       SearchByBoW(KF, F): mvKeys)          */
+    const uint8_t* desc;            /* [n][32] mDescriptors                  */
+    int n;
+    const uint8_t* mp;              /* [n] map-point state                   */
+    int n_nodes;                    /* FeatureVector entries                 */
+    const uint32_t* node_id;        /* [n_nodes] ascending                   */
+    const int32_t* node_ptr;        /* [n_nodes + 1] offsets into feat_idx   */
+    const int32_t* feat_idx;        /* feature indices of each node, as stored */
+} orbx_bow_view;
+
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&)
+ * (src/ORBmatcher.cc:155-283).  matches_f (out, F->n): the KF keypoint whose
+ * map point was assigned to each F keypoint (vpMapPointMatches), or -1. */
+int orbx_search_by_bow_frame(orbx_ctx* ctx, const orbx_bow_view* KF, const orbx_bow_view* F,
+                             float nnratio, int check_ori, int32_t* matches_f, int* n_matches);
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>&)
+ * (src/ORBmatcher.cc:715-850).  matches12 (out, KF1->n): the KF2 keypoint
+ * whose map point matched each KF1 keypoint (vpMatches12), or -1. */
+int orbx_search_by_bow_kf(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bow_view* KF2,
+                          float nnratio, int check_ori, int32_t* matches12, int* n_matches);
+/* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, ...) (src/ORBmatcher.cc:
+ * 852-1014).  F12: 3x3 row-major fundamental matrix (float, as cv::Mat);
+ * sigma2_2: KF2's mvLevelSigma2 (nlevels entries).  matches12 (out, KF1->n):
+ * vMatches12 (KF2 index or -1); vMatchedPairs are its non-negative entries
+ * in KF1 order. */
+int orbx_search_for_triangulation(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bow_view* KF2,
+                                  const float* F12, const float* sigma2_2, int nlevels, int check_ori,
+                                  int32_t* matches12, int* n_matches);
+
 /* ------------------------------------------------------------------------ */
 /* C. Local bundle adjustment                                                */
 /* ------------------------------------------------------------------------ */

@@ -1,0 +1,326 @@
+// Vocabulary-node searches of ORBmatcher on MI355X: SearchByBoW(KF, F)
+// (src/ORBmatcher.cc:155-283), SearchByBoW(KF1, KF2) (:715-850) and
+// SearchForTriangulation (:852-1014).
+//
+// The reference walks the DBoW2 FeatureVector nodes both frames share and,
+// inside a node, replays a greedy loop over the first frame's features: each
+// takes its best still-unmatched candidate of the same node in the second
+// frame.  A feature belongs to one node only, so nodes are independent: one
+// workgroup per call, its four wavefronts take the common nodes round-robin.
+// Inside a node the wavefront replays the greedy loop in order with the
+// node's second-frame features spread over the lanes (lane j owns list
+// entries j, j + 64, ...; their "already matched" flags are a register
+// bitmask): each step is one Hamming distance per lane and one DPP
+// best/second reduction (SearchForTriangulation: a min-distance reduction,
+// then the first (distance, index) candidate passing the epipolar test).
+// The rotation histogram (ComputeThreeMaxima, :1748-1789) is built after all
+// nodes with LDS atomics and filtered in parallel.
+#include <algorithm>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_match_common.h"
+
+namespace orbx {
+
+constexpr int kBowMaxChunks = 32;   // second-frame features per node <= 64 * 32
+
+struct BowSideDev {
+    const orbx_keypoint* kps;
+    const uint8_t* desc;
+    const uint8_t* mp;
+    const int32_t* feat;
+};
+
+struct BowArgs {
+    BowSideDev s1, s2;
+    const int4* nodes;      // (first1, count1, first2, count2) per common node
+    int n_common;
+    int mode;               // 0 SearchByBoW(KF, F), 1 SearchByBoW(KF1, KF2), 2 SearchForTriangulation
+    float nnratio;
+    int check_ori;
+    float F12[9];
+    float sigma2[kMaxLevels];
+    int32_t* out;           // mode 0: [F.n] (KF index); modes 1, 2: [KF1.n] (KF2 index)
+    int out_len;
+    signed char* bins;      // rotation bin per out entry, -1 when none
+    int32_t* out_n;
+};
+
+// ORBmatcher::CheckDistEpipolarLine (src/ORBmatcher.cc:136-153): float line
+// coefficients summed left to right, threshold 3.84 * sigma2 in double.
+__device__ inline bool epipolar_ok(const orbx_keypoint& k1, const orbx_keypoint& k2, const float* F,
+                                   const float* sigma2)
+{
+    const float a = __fadd_rn(__fadd_rn(__fmul_rn(k1.x, F[0]), __fmul_rn(k1.y, F[3])), F[6]);
+    const float b = __fadd_rn(__fadd_rn(__fmul_rn(k1.x, F[1]), __fmul_rn(k1.y, F[4])), F[7]);
+    const float c = __fadd_rn(__fadd_rn(__fmul_rn(k1.x, F[2]), __fmul_rn(k1.y, F[5])), F[8]);
+    const float num = __fadd_rn(__fadd_rn(__fmul_rn(a, k2.x), __fmul_rn(b, k2.y)), c);
+    const float den = __fadd_rn(__fmul_rn(a, a), __fmul_rn(b, b));
+    if (den == 0.0f) return false;
+    const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
+    return (double)dsqr < 3.84 * (double)sigma2[k2.octave];
+}
+
+__global__ __launch_bounds__(256) void k_bow_match(BowArgs a)
+{
+    __shared__ int hist[kHistoLength];
+    __shared__ int s_acc, s_removed, s_ind[3];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    if (tid < kHistoLength) hist[tid] = 0;
+    if (tid == 0) {
+        s_acc = 0;
+        s_removed = 0;
+    }
+    __syncthreads();
+    int accepted = 0;
+    for (int k = wv; k < a.n_common; k += kBlock / 64) {
+        const int4 nd = a.nodes[k];
+        const int nch = (nd.w + 63) >> 6;
+        uint32_t taken = 0;   // bit c: list entry lane + 64 c already matched
+        for (int i = 0; i < nd.y; i++) {
+            const int idx1 = a.s1.feat[nd.x + i];
+            const int m1 = a.s1.mp[idx1];
+            if (a.mode == 2 ? m1 != 0 : m1 != 1) continue;   // uniform
+            uint4 d1a, d1b;
+            load_desc(a.s1.desc + (size_t)idx1 * 32, d1a, d1b);
+            int best_j;
+            if (a.mode < 2) {
+                // best (first strict minimum in list order) and second distance
+                uint32_t m1k = 0xFFFFFFFFu;
+                int m2d = 511;
+                for (int c = 0; c < nch; c++) {
+                    const int j = c * 64 + lane;
+                    if (j >= nd.w || ((taken >> c) & 1)) continue;
+                    const int idx2 = a.s2.feat[nd.z + j];
+                    if (a.mode == 1 && a.s2.mp[idx2] != 1) continue;
+                    uint4 b0, b1;
+                    load_desc(a.s2.desc + (size_t)idx2 * 32, b0, b1);
+                    const int dist = hamming256(d1a, d1b, b0, b1);
+                    const uint32_t key = ((uint32_t)dist << 23) | (uint32_t)j;
+                    if (key < m1k) {
+                        m2d = min(m2d, (int)(m1k >> 23));
+                        m1k = key;
+                    } else {
+                        m2d = min(m2d, dist);
+                    }
+                }
+                best_second_reduce(m1k, m2d);
+                if (m1k == 0xFFFFFFFFu) continue;
+                const int d1 = (int)(m1k >> 23);
+                const float second = m2d >= 511 ? 2147483648.0f : (float)m2d;   // (float)INT_MAX
+                const bool ok = (a.mode == 0 ? d1 <= kTHLow : d1 < kTHLow) && (float)d1 < __fmul_rn(a.nnratio, second);
+                if (!ok) continue;
+                best_j = (int)(m1k & 0x7FFFFF);
+            } else {
+                // vDistIndex: candidates with dist <= TH_LOW sorted by
+                // (dist, index); the first within 2 * best passing the
+                // epipolar test wins
+                int bd = 0x7fffffff;
+                for (int c = 0; c < nch; c++) {
+                    const int j = c * 64 + lane;
+                    if (j >= nd.w || ((taken >> c) & 1)) continue;
+                    const int idx2 = a.s2.feat[nd.z + j];
+                    if (a.s2.mp[idx2] != 0) continue;
+                    uint4 b0, b1;
+                    load_desc(a.s2.desc + (size_t)idx2 * 32, b0, b1);
+                    const int dist = hamming256(d1a, d1b, b0, b1);
+                    if (dist <= kTHLow) bd = min(bd, dist);
+                }
+                bd = wave_min_i32(bd);
+                if (bd > kTHLow) continue;
+                const int th = 2 * bd;   // round(2*BestDist)
+                const orbx_keypoint kp1 = a.s1.kps[idx1];
+                unsigned long long kb = ~0ull;
+                for (int c = 0; c < nch; c++) {
+                    const int j = c * 64 + lane;
+                    if (j >= nd.w || ((taken >> c) & 1)) continue;
+                    const int idx2 = a.s2.feat[nd.z + j];
+                    if (a.s2.mp[idx2] != 0) continue;
+                    uint4 b0, b1;
+                    load_desc(a.s2.desc + (size_t)idx2 * 32, b0, b1);
+                    const int dist = hamming256(d1a, d1b, b0, b1);
+                    if (dist > kTHLow || dist > th) continue;
+                    if (!epipolar_ok(kp1, a.s2.kps[idx2], a.F12, a.sigma2)) continue;
+                    const unsigned long long key = ((unsigned long long)dist << 48) |
+                                                   ((unsigned long long)(uint32_t)idx2 << 16) | (unsigned long long)j;
+                    kb = key < kb ? key : kb;
+                }
+                kb = wave_min_u64(kb);
+                if (kb == ~0ull) continue;
+                best_j = (int)(kb & 0xFFFF);
+            }
+            if ((best_j & 63) == lane) taken |= 1u << (best_j >> 6);
+            if (lane == 0) {
+                const int idx2 = a.s2.feat[nd.z + best_j];
+                const int slot = a.mode == 0 ? idx2 : idx1;
+                a.out[slot] = a.mode == 0 ? idx1 : idx2;
+                if (a.check_ori) a.bins[slot] = (signed char)rot_bin(a.s1.kps[idx1].angle, a.s2.kps[idx2].angle);
+            }
+            accepted++;
+        }
+    }
+    if (lane == 0 && accepted) atomicAdd(&s_acc, accepted);
+    __syncthreads();
+    if (a.check_ori) {
+        for (int i = tid; i < a.out_len; i += kBlock) {
+            const int b = a.bins[i];
+            if (b >= 0) atomicAdd(&hist[b], 1);
+        }
+        __syncthreads();
+        if (tid == 0) three_maxima(hist, s_ind[0], s_ind[1], s_ind[2]);
+        __syncthreads();
+        int rem = 0;
+        for (int i = tid; i < a.out_len; i += kBlock) {
+            const int b = a.bins[i];
+            if (b >= 0 && b != s_ind[0] && b != s_ind[1] && b != s_ind[2]) {
+                a.out[i] = -1;
+                rem++;
+            }
+        }
+        rem = wave_sum(rem);
+        if (lane == 0 && rem) atomicAdd(&s_removed, rem);
+        __syncthreads();
+    }
+    if (tid == 0) *a.out_n = s_acc - s_removed;
+}
+
+namespace {
+
+bool valid_bow(const orbx_bow_view* v, int max_octave)
+{
+    if (!v || v->n < 0 || v->n_nodes < 0) return false;
+    if (v->n > 0 && (!v->keys || !v->desc || !v->mp)) return false;
+    if (v->n_nodes == 0) return true;
+    if (!v->node_id || !v->node_ptr || !v->feat_idx || v->node_ptr[0] < 0) return false;
+    std::vector<uint8_t> seen(v->n, 0);
+    for (int k = 0; k < v->n_nodes; k++) {
+        if (v->node_ptr[k + 1] < v->node_ptr[k]) return false;
+        if (k > 0 && v->node_id[k] <= v->node_id[k - 1]) return false;
+        for (int e = v->node_ptr[k]; e < v->node_ptr[k + 1]; e++) {
+            const int f = v->feat_idx[e];
+            if (f < 0 || f >= v->n || seen[f]) return false;
+            seen[f] = 1;
+        }
+    }
+    if (max_octave > 0)
+        for (int i = 0; i < v->n; i++)
+            if (v->keys[i].octave < 0 || v->keys[i].octave >= max_octave) return false;
+    return true;
+}
+
+// The common node ids in ascending order (the reference's merge loop).
+std::vector<int4> common_nodes(const orbx_bow_view& a, const orbx_bow_view& b)
+{
+    std::vector<int4> out;
+    int i = 0, j = 0;
+    while (i < a.n_nodes && j < b.n_nodes) {
+        if (a.node_id[i] == b.node_id[j]) {
+            out.push_back(make_int4(a.node_ptr[i], a.node_ptr[i + 1] - a.node_ptr[i], b.node_ptr[j],
+                                    b.node_ptr[j + 1] - b.node_ptr[j]));
+            i++;
+            j++;
+        } else if (a.node_id[i] < b.node_id[j]) {
+            i = (int)(std::lower_bound(a.node_id + i, a.node_id + a.n_nodes, b.node_id[j]) - a.node_id);
+        } else {
+            j = (int)(std::lower_bound(b.node_id + j, b.node_id + b.n_nodes, a.node_id[i]) - b.node_id);
+        }
+    }
+    return out;
+}
+
+inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+int run_bow(orbx_ctx* ctx, const orbx_bow_view* V1, const orbx_bow_view* V2, int mode, float nnratio, int check_ori,
+            const float* F12, const float* sigma2, int nlevels, int32_t* out, int* n_out)
+{
+    if (!ctx || !out || !n_out) return ORBX_ERR_ARG;
+    if (mode == 2 && (!F12 || !sigma2 || nlevels <= 0 || nlevels > kMaxLevels)) return ORBX_ERR_ARG;
+    if (!valid_bow(V1, 0) || !valid_bow(V2, mode == 2 ? nlevels : 0)) return ORBX_ERR_ARG;
+    const std::vector<int4> nodes = common_nodes(*V1, *V2);
+    for (const int4& nd : nodes)
+        if (nd.w > 64 * kBowMaxChunks) return ORBX_ERR_UNSUPPORTED;
+    const int out_len = mode == 0 ? V2->n : V1->n;
+    ctx_enter(ctx);
+    const int nf1 = V1->n_nodes ? V1->node_ptr[V1->n_nodes] : 0, nf2 = V2->n_nodes ? V2->node_ptr[V2->n_nodes] : 0;
+    // layout in the context scratch
+    size_t at = 0;
+    auto res = [&](size_t bytes) {
+        const size_t o = at;
+        at += al256(std::max<size_t>(bytes, 1));
+        return o;
+    };
+    const size_t o_k1 = res((size_t)V1->n * sizeof(orbx_keypoint)), o_d1 = res((size_t)V1->n * 32),
+                 o_m1 = res(V1->n), o_f1 = res((size_t)nf1 * 4);
+    const size_t o_k2 = res((size_t)V2->n * sizeof(orbx_keypoint)), o_d2 = res((size_t)V2->n * 32),
+                 o_m2 = res(V2->n), o_f2 = res((size_t)nf2 * 4);
+    const size_t o_nd = res(nodes.size() * sizeof(int4)), o_out = res((size_t)out_len * 4), o_bin = res(out_len),
+                 o_n = res(4);
+    int r = ensure_scratch(ctx, at);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    auto put = [&](size_t off, const void* src, size_t bytes) -> int {
+        if (bytes == 0 || !src) return ORBX_OK;
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + off, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return ORBX_OK;
+    };
+    if ((r = put(o_k1, V1->keys, (size_t)V1->n * sizeof(orbx_keypoint))) ||
+        (r = put(o_d1, V1->desc, (size_t)V1->n * 32)) || (r = put(o_m1, V1->mp, V1->n)) ||
+        (r = put(o_f1, V1->n_nodes ? V1->feat_idx : nullptr, (size_t)nf1 * 4)) ||
+        (r = put(o_k2, V2->keys, (size_t)V2->n * sizeof(orbx_keypoint))) ||
+        (r = put(o_d2, V2->desc, (size_t)V2->n * 32)) || (r = put(o_m2, V2->mp, V2->n)) ||
+        (r = put(o_f2, V2->n_nodes ? V2->feat_idx : nullptr, (size_t)nf2 * 4)) ||
+        (r = put(o_nd, nodes.data(), nodes.size() * sizeof(int4))))
+        return r;
+    ORBX_HIP_CHECK(hipMemsetAsync(d + o_out, 0xFF, (size_t)out_len * 4, ctx->stream));
+    ORBX_HIP_CHECK(hipMemsetAsync(d + o_bin, 0xFF, (size_t)out_len, ctx->stream));
+    BowArgs a{};
+    a.s1 = {reinterpret_cast<const orbx_keypoint*>(d + o_k1), d + o_d1, d + o_m1,
+            reinterpret_cast<const int32_t*>(d + o_f1)};
+    a.s2 = {reinterpret_cast<const orbx_keypoint*>(d + o_k2), d + o_d2, d + o_m2,
+            reinterpret_cast<const int32_t*>(d + o_f2)};
+    a.nodes = reinterpret_cast<const int4*>(d + o_nd);
+    a.n_common = (int)nodes.size();
+    a.mode = mode;
+    a.nnratio = nnratio;
+    a.check_ori = check_ori;
+    if (mode == 2) {
+        for (int k = 0; k < 9; k++) a.F12[k] = F12[k];
+        for (int l = 0; l < nlevels; l++) a.sigma2[l] = sigma2[l];
+    }
+    a.out = reinterpret_cast<int32_t*>(d + o_out);
+    a.out_len = out_len;
+    a.bins = reinterpret_cast<signed char*>(d + o_bin);
+    a.out_n = reinterpret_cast<int32_t*>(d + o_n);
+    hipLaunchKernelGGL(k_bow_match, dim3(1), dim3(kBlock), 0, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if (out_len) ORBX_HIP_CHECK(hipMemcpyAsync(out, d + o_out, (size_t)out_len * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(n_out, d + o_n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+}  // namespace
+}  // namespace orbx
+
+using namespace orbx;
+
+extern "C" int orbx_search_by_bow_frame(orbx_ctx* ctx, const orbx_bow_view* KF, const orbx_bow_view* F,
+                                        float nnratio, int check_ori, int32_t* matches_f, int* n_matches)
+{
+    return run_bow(ctx, KF, F, 0, nnratio, check_ori, nullptr, nullptr, 0, matches_f, n_matches);
+}
+
+extern "C" int orbx_search_by_bow_kf(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bow_view* KF2,
+                                     float nnratio, int check_ori, int32_t* matches12, int* n_matches)
+{
+    return run_bow(ctx, KF1, KF2, 1, nnratio, check_ori, nullptr, nullptr, 0, matches12, n_matches);
+}
+
+extern "C" int orbx_search_for_triangulation(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bow_view* KF2,
+                                             const float* F12, const float* sigma2_2, int nlevels, int check_ori,
+                                             int32_t* matches12, int* n_matches)
+{
+    return run_bow(ctx, KF1, KF2, 2, 0.f, check_ori, F12, sigma2_2, nlevels, matches12, n_matches);
+}
