@@ -286,6 +286,51 @@ int orbx_search_for_triangulation(orbx_ctx* ctx, const orbx_bow_view* KF1, const
                                   const float* F12, const float* sigma2_2, int nlevels, int check_ori,
                                   int32_t* matches12, int* n_matches);
 
+/* Keyframe projection searches.  Map points as they
+ * read them, one entry per point (SoA). */
+typedef struct {
+    int n;
+    const float* pos;        /* [n][3] GetWorldPos()                        */
+    const float* normal;     /* [n][3] GetNormal() (Fuse; may be NULL else)  */
+    const float* min_dist;   /* [n] GetMinDistanceInvariance()               */
+    const float* max_dist;   /* [n] GetMaxDistanceInvariance()               */
+    const uint8_t* desc;     /* [n][32] GetDescriptor()                      */
+} orbx_mappoint_view;
+
+/* ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>&, th) (src/ORBmatcher.cc:
+ * 1016-1134; sim3 = 0, T = the keyframe's Tcw) and Fuse(KeyFrame*, Scw,
+ * vector<MapPoint*>&, th) (:1136-1265; sim3 = 1, T = Scw), 4x4 row-major
+ * float.  Computes the state-free part for every map point -- projection,
+ * image / distance / viewing-angle gates, predicted level, and the best
+ * keyframe keypoint within th * scale[level] at levels [pred - 1, pred]:
+ * best_idx (-1 when gated out or no candidate) and best_dist.  The caller
+ * replays the graph updates in map-point order (isBad / IsInKeyFrame /
+ * already-found checks, bestDist <= TH_LOW, Replace or AddObservation),
+ * which depend on the earlier points' updates. */
+int orbx_fuse_candidates(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
+                         const orbx_mappoint_view* mps, const float* T, int sim3, float th,
+                         int32_t* best_idx, int32_t* best_dist);
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+ * (src/ORBmatcher.cc:1267-1505).  mp1 / valid1: the map point of each KF1
+ * keypoint (valid = pMP && !isBad()); mp2 / valid2 likewise for KF2.  T1w,
+ * T2w: keyframe poses (4x4 row-major); R12 3x3 row-major, t12 3.  prior12
+ * (in, KF1->n): -2 where vpMatches12[i] is NULL, else the KF2 index of that
+ * map point (GetIndexInKeyFrame(pKF2), -1 if not observed).  new12 (out):
+ * the KF2 keypoint whose map point this call assigns (vpMatches12[i1] =
+ * vpMapPoints2[new12[i1]]), or -1.  cam: pKF1's fx, fy, cx, cy. */
+int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
+                        const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
+                        const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
+                        const float* T2w, float s12, const float* R12, const float* t12, float th,
+                        const int32_t* prior12, int32_t* new12, int* n_found);
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:185-250) for
+ * n_mp map points at once: point m's observed descriptors (non-bad
+ * keyframes, observation order) are rows obs_ptr[m] .. obs_ptr[m+1]-1 of
+ * desc.  best (out): the row (relative to obs_ptr[m]) with the least median
+ * distance to the others, -1 for a point without descriptors. */
+int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32_t* obs_ptr,
+                                 const uint8_t* desc, int32_t* best);
+
 /* ------------------------------------------------------------------------ */
 /* C. Local bundle adjustment                                                */
 /* ------------------------------------------------------------------------ */

@@ -1,0 +1,464 @@
+// Keyframe projection searches on MI355X: the state-free part of
+// ORBmatcher::Fuse (both overloads, src/ORBmatcher.cc:1016-1265),
+// SearchBySim3 (:1267-1505) and MapPoint::ComputeDistinctiveDescriptors
+// (src/MapPoint.cc:185-250).
+//
+// Projection: one wavefront per map point, four per 256-thread workgroup.
+// The keyframe's keypoint table (position, grid cell, octave) is staged in
+// LDS once per workgroup; each wavefront computes its point's projection
+// and gates redundantly on every lane (uniform), then the lanes stride the
+// keyframe's keypoints with the GetFeaturesInArea cell/box test and the
+// level window, and one 64-bit min reduction over (distance, cell, index)
+// gives the reference's first strict minimum in GetFeaturesInArea order.
+// cv::Mat arithmetic is restated as in oracle/ref_proj.cpp (float products
+// summed left to right, scalar scaling by a double factor, cv::norm and
+// Mat::dot accumulated in double).
+//
+// Distinctive descriptors: one wavefront per map point; lane i takes
+// descriptor i and finds the median of its distance row by a binary search
+// on the value (9 counting passes over the row), then a (median, i) min
+// reduction picks the first least median.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "orbx_device.h"
+#include "orbx_internal.h"
+#include "orbx_match_common.h"
+
+namespace orbx {
+
+struct KfProjArgs {
+    FrameDev K;                 // searched keyframe
+    float scales[kMaxLevels];
+    int nlevels;
+    float cam[4];
+    float Ra[9], ta[3];         // p = Ra X + ta
+    float Rb[9], tb[3];         // then p = Rb p + tb (two_stage)
+    float Ow[3];
+    int two_stage;
+    int mode;                   // 0 Fuse (1/z float), 1 Fuse Scw (1.0/z double), 2 SearchBySim3
+    float th;
+    int nq;
+    const float* pos;
+    const float* normal;
+    const float* dmin;
+    const float* dmax;
+    const uint8_t* qdesc;
+    const uint8_t* qvalid;      // may be null
+    int32_t* best_idx;
+    int32_t* best_dist;
+};
+
+__device__ inline void xform3(const float* R, const float* t, const float* X, float* o)
+{
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+        o[r] = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(R[3 * r], X[0]), __fmul_rn(R[3 * r + 1], X[1])),
+                                   __fmul_rn(R[3 * r + 2], X[2])),
+                         t[r]);
+}
+
+__device__ inline float norm3_cv(const float* v)
+{
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) s += (double)v[i] * (double)v[i];
+    return (float)sqrt(s);
+}
+
+__device__ inline double dot3_cv(const float* a, const float* b)
+{
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) s += (double)a[i] * (double)b[i];
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_kf_project(KfProjArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    float* tx = reinterpret_cast<float*>(smem);
+    float* ty = tx + a.K.n;
+    int* tco = reinterpret_cast<int*>(ty + a.K.n);   // cell | octave << 16
+    for (int i = threadIdx.x; i < a.K.n; i += kBlock) {
+        const orbx_keypoint k = a.K.kps[i];
+        tx[i] = k.x;
+        ty[i] = k.y;
+        const int cell = grid_cell(a.K, k.x, k.y);
+        tco[i] = (cell & 0xFFFF) | (k.octave << 16);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (m >= a.nq) return;
+    int best_idx = -1, best_dist = INT_MAX;
+    do {
+        if (a.qvalid && !a.qvalid[m]) break;
+        const float Xw[3] = {a.pos[3 * m], a.pos[3 * m + 1], a.pos[3 * m + 2]};
+        float pc[3];
+        xform3(a.Ra, a.ta, Xw, pc);
+        if (a.two_stage) {
+            const float p1[3] = {pc[0], pc[1], pc[2]};
+            xform3(a.Rb, a.tb, p1, pc);
+        }
+        if (pc[2] < 0.0f) break;
+        const float invz = a.mode == 0 ? __fdiv_rn(1.0f, pc[2]) : (float)(1.0 / (double)pc[2]);
+        const float x = __fmul_rn(pc[0], invz), y = __fmul_rn(pc[1], invz);
+        const float u = __fadd_rn(__fmul_rn(a.cam[0], x), a.cam[2]);
+        const float v = __fadd_rn(__fmul_rn(a.cam[1], y), a.cam[3]);
+        if (!(u >= a.K.min_x && u < a.K.max_x && v >= a.K.min_y && v < a.K.max_y)) break;   // IsInImage
+        const float maxDistance = a.dmax[m], minDistance = a.dmin[m];
+        float dist3D;
+        if (a.mode == 2) {
+            dist3D = norm3_cv(pc);   // SearchBySim3: norm of the camera point
+        } else {
+            const float PO[3] = {__fsub_rn(Xw[0], a.Ow[0]), __fsub_rn(Xw[1], a.Ow[1]), __fsub_rn(Xw[2], a.Ow[2])};
+            dist3D = norm3_cv(PO);
+            if (dist3D < minDistance || dist3D > maxDistance) break;
+            const float Pn[3] = {a.normal[3 * m], a.normal[3 * m + 1], a.normal[3 * m + 2]};
+            if (dot3_cv(PO, Pn) < 0.5 * (double)dist3D) break;
+        }
+        if (dist3D < minDistance || dist3D > maxDistance) break;
+        const float ratio = __fdiv_rn(dist3D, minDistance);
+        int pred = 0;
+        while (pred < a.nlevels && a.scales[pred] < ratio) pred++;   // lower_bound
+        pred = min(pred, a.nlevels - 1);
+        const float radius = __fmul_rn(a.th, a.scales[pred]);
+        const AreaQuery q = area_cells(a.K, u, v, radius);
+        if (q.empty) break;
+        uint4 d0, d1;
+        load_desc(a.qdesc + (size_t)m * 32, d0, d1);
+        unsigned long long bk = ~0ull;
+        for (int j = lane; j < a.K.n; j += 64) {
+            const int co = tco[j];
+            const int oct = co >> 16;
+            if (oct < pred - 1 || oct > pred) continue;
+            const int cell = (co & 0xFFFF) == 0xFFFF ? -1 : (co & 0xFFFF);
+            if (!in_area(q, cell, tx[j], ty[j], u, v, radius)) continue;
+            uint4 b0, b1;
+            load_desc(a.K.desc + (size_t)j * 32, b0, b1);
+            const unsigned long long key = ((unsigned long long)hamming256(d0, d1, b0, b1) << 32) |
+                                           ((unsigned long long)cell << 12) | (unsigned long long)j;
+            bk = key < bk ? key : bk;
+        }
+        bk = wave_min_u64(bk);
+        if (bk != ~0ull) {
+            best_idx = (int)(bk & 0xFFF);
+            best_dist = (int)(bk >> 32);
+        }
+    } while (false);
+    if (lane == 0) {
+        a.best_idx[m] = best_idx;
+        a.best_dist[m] = best_dist;
+    }
+}
+
+// MapPoint::ComputeDistinctiveDescriptors, one wavefront per map point.
+__global__ __launch_bounds__(256) void k_distinctive(const int32_t* ptr, const uint8_t* desc, int n_mp, int32_t* best)
+{
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (m >= n_mp) return;
+    const int b0 = ptr[m], N = ptr[m + 1] - b0;
+    if (N <= 0) {
+        if (lane == 0) best[m] = -1;
+        return;
+    }
+    const uint8_t* D = desc + (size_t)b0 * 32;
+    const int k = (N - 1) / 2;                     // vDists[0.5*(N-1)]
+    uint32_t key = 0xFFFFFFFFu;
+    for (int i = lane; i < N; i += 64) {
+        uint4 a0, a1;
+        load_desc(D + (size_t)i * 32, a0, a1);
+        int lo = 0, hi = 256;                       // smallest v with #{d(i,l) <= v} > k
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (int l = 0; l < N; l++) {
+                uint4 c0, c1;
+                load_desc(D + (size_t)l * 32, c0, c1);
+                cnt += hamming256(a0, a1, c0, c1) <= mid;
+            }
+            if (cnt > k) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t kk = ((uint32_t)lo << 20) | (uint32_t)i;
+        key = kk < key ? kk : key;
+    }
+    key = wave_min_u32(key);
+    if (lane == 0) best[m] = (int)(key & 0xFFFFF);
+}
+
+namespace {
+
+inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+bool valid_kf(const orbx_frame_view* v)
+{
+    return v && v->n >= 0 && v->n <= 4096 && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
+           v->max_y > v->min_y && v->nlevels > 0 && v->nlevels <= kMaxLevels;
+}
+
+bool valid_mps(const orbx_mappoint_view* p, bool need_normal)
+{
+    return p && p->n >= 0 &&
+           (p->n == 0 || (p->pos && p->min_dist && p->max_dist && p->desc && (!need_normal || p->normal)));
+}
+
+// Same arithmetic as oracle/ref_proj.cpp pose_parts (src/ORBmatcher.cc:
+// 1145-1149; KeyFrame::SetPose's Ow = -Rwc * tcw).
+void pose_parts(const float* T, int sim3, float* R, float* t, float* Ow)
+{
+    if (sim3) {
+        double s = 0;
+        for (int c = 0; c < 3; c++) s += (double)T[c] * (double)T[c];
+        const float scw = (float)std::sqrt(s);
+        const double inv = 1.0 / (double)scw;
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) R[3 * r + c] = (float)((double)T[4 * r + c] * inv);
+            t[r] = (float)((double)T[4 * r + 3] * inv);
+        }
+    } else {
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) R[3 * r + c] = T[4 * r + c];
+            t[r] = T[4 * r + 3];
+        }
+    }
+    for (int c = 0; c < 3; c++) Ow[c] = -(R[c] * t[0] + R[3 + c] * t[1] + R[6 + c] * t[2]);
+}
+
+FrameDev kf_dev(const orbx_frame_view* v, const uint8_t* base, size_t kp_off, size_t desc_off)
+{
+    FrameDev F;
+    F.kps = reinterpret_cast<const orbx_keypoint*>(base + kp_off);
+    F.desc = base + desc_off;
+    F.n = v->n;
+    F.min_x = v->min_x;
+    F.max_x = v->max_x;
+    F.min_y = v->min_y;
+    F.max_y = v->max_y;
+    F.grid_w_inv = static_cast<float>(kGridCols) / (v->max_x - v->min_x);   // src/Frame.cc:76-77
+    F.grid_h_inv = static_cast<float>(kGridRows) / (v->max_y - v->min_y);
+    return F;
+}
+
+struct Staging {
+    orbx_ctx* ctx;
+    size_t at = 0;
+    std::vector<std::pair<size_t, std::pair<const void*, size_t>>> puts;
+    size_t res(size_t bytes, const void* src = nullptr)
+    {
+        const size_t o = at;
+        at += al256(std::max<size_t>(bytes, 1));
+        if (src && bytes) puts.push_back({o, {src, bytes}});
+        return o;
+    }
+    int upload()
+    {
+        int r = ensure_scratch(ctx, at);
+        if (r != ORBX_OK) return r;
+        uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+        for (auto& p : puts)
+            ORBX_HIP_CHECK(hipMemcpyAsync(d + p.first, p.second.first, p.second.second, hipMemcpyHostToDevice,
+                                          ctx->stream));
+        return ORBX_OK;
+    }
+    uint8_t* base() const { return static_cast<uint8_t*>(ctx->scratch); }
+};
+
+// Stages the keyframe and the map points, fills the common fields.
+struct ProjStage {
+    size_t kp, kd, pos, nrm, dmin, dmax, qd, qv, bi, bd;
+};
+
+ProjStage stage_proj(Staging& s, const orbx_frame_view* K, const orbx_mappoint_view* P, const uint8_t* qvalid)
+{
+    ProjStage o;
+    o.kp = s.res((size_t)K->n * sizeof(orbx_keypoint), K->keys_un);
+    o.kd = s.res((size_t)K->n * 32, K->desc);
+    o.pos = s.res((size_t)P->n * 12, P->pos);
+    o.nrm = s.res((size_t)P->n * 12, P->normal);
+    o.dmin = s.res((size_t)P->n * 4, P->min_dist);
+    o.dmax = s.res((size_t)P->n * 4, P->max_dist);
+    o.qd = s.res((size_t)P->n * 32, P->desc);
+    o.qv = s.res((size_t)P->n, qvalid);
+    o.bi = s.res((size_t)P->n * 4);
+    o.bd = s.res((size_t)P->n * 4);
+    return o;
+}
+
+void fill_proj(KfProjArgs& a, const Staging& s, const ProjStage& o, const orbx_frame_view* K,
+               const orbx_mappoint_view* P, bool has_valid)
+{
+    uint8_t* d = s.base();
+    a.K = kf_dev(K, d, o.kp, o.kd);
+    a.nlevels = K->nlevels;
+    a.scales[0] = 1.0f;
+    for (int l = 1; l < K->nlevels; l++) a.scales[l] = a.scales[l - 1] * K->scale_factor;   // src/Frame.cc:98-102
+    a.nq = P->n;
+    a.pos = reinterpret_cast<const float*>(d + o.pos);
+    a.normal = reinterpret_cast<const float*>(d + o.nrm);
+    a.dmin = reinterpret_cast<const float*>(d + o.dmin);
+    a.dmax = reinterpret_cast<const float*>(d + o.dmax);
+    a.qdesc = d + o.qd;
+    a.qvalid = has_valid ? d + o.qv : nullptr;
+    a.best_idx = reinterpret_cast<int32_t*>(d + o.bi);
+    a.best_dist = reinterpret_cast<int32_t*>(d + o.bd);
+}
+
+int launch_proj(orbx_ctx* ctx, const KfProjArgs& a)
+{
+    if (a.nq == 0) return ORBX_OK;
+    const int per = kBlock / 64;
+    const size_t lds = (size_t)std::max(a.K.n, 1) * 12;
+    hipLaunchKernelGGL(k_kf_project, dim3((a.nq + per - 1) / per), dim3(kBlock), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    return ORBX_OK;
+}
+
+}  // namespace
+}  // namespace orbx
+
+using namespace orbx;
+
+extern "C" int orbx_fuse_candidates(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
+                                    const orbx_mappoint_view* mps, const float* T, int sim3, float th,
+                                    int32_t* best_idx, int32_t* best_dist)
+{
+    if (!ctx || !valid_kf(KF) || !cam || !valid_mps(mps, true) || !T || (mps->n > 0 && (!best_idx || !best_dist)))
+        return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    Staging s{ctx};
+    const ProjStage o = stage_proj(s, KF, mps, nullptr);
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    KfProjArgs a{};
+    fill_proj(a, s, o, KF, mps, false);
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    pose_parts(T, sim3, a.Ra, a.ta, a.Ow);
+    a.two_stage = 0;
+    a.mode = sim3 ? 1 : 0;
+    a.th = th;
+    if ((r = launch_proj(ctx, a)) != ORBX_OK) return r;
+    if (mps->n) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(best_idx, s.base() + o.bi, (size_t)mps->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(best_dist, s.base() + o.bd, (size_t)mps->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
+                                   const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
+                                   const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
+                                   const float* T2w, float s12, const float* R12, const float* t12, float th,
+                                   const int32_t* prior12, int32_t* new12, int* n_found)
+{
+    if (!ctx || !valid_kf(KF1) || !valid_kf(KF2) || !cam || !valid_mps(mp1, false) || !valid_mps(mp2, false) ||
+        mp1->n != KF1->n || mp2->n != KF2->n || (KF1->n && (!valid1 || !prior12 || !new12)) ||
+        (KF2->n && !valid2) || !T1w || !T2w || !R12 || !t12 || !n_found)
+        return ORBX_ERR_ARG;
+    const int N1 = KF1->n, N2 = KF2->n;
+    // vbAlreadyMatched1/2 (:1300-1313) folded into the query masks
+    std::vector<uint8_t> q1(N1), q2(N2);
+    std::vector<uint8_t> already2(N2, 0);
+    for (int i = 0; i < N1; i++)
+        if (prior12[i] >= 0 && prior12[i] < N2) already2[prior12[i]] = 1;
+    for (int i = 0; i < N1; i++) q1[i] = valid1[i] && prior12[i] == -2;
+    for (int i = 0; i < N2; i++) q2[i] = valid2[i] && !already2[i];
+    // sR12 = s12*R12, sR21 = (1.0/s12)*R12.t(), t21 = -sR21*t12 (:1284-1286)
+    float R1w[9], t1w[3], R2w[9], t2w[3], sR12[9], sR21[9], t21[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) {
+            R1w[3 * r + c] = T1w[4 * r + c];
+            R2w[3 * r + c] = T2w[4 * r + c];
+        }
+        t1w[r] = T1w[4 * r + 3];
+        t2w[r] = T2w[4 * r + 3];
+    }
+    const double inv_s = 1.0 / (double)s12;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[3 * r + c] = (float)((double)s12 * (double)R12[3 * r + c]);
+            sR21[3 * r + c] = (float)(inv_s * (double)R12[3 * c + r]);
+        }
+    for (int r = 0; r < 3; r++) t21[r] = -(sR21[3 * r] * t12[0] + sR21[3 * r + 1] * t12[1] + sR21[3 * r + 2] * t12[2]);
+    ctx_enter(ctx);
+    Staging s{ctx};
+    const ProjStage o1 = stage_proj(s, KF2, mp1, q1.data());   // KF1 points searched in KF2
+    const ProjStage o2 = stage_proj(s, KF1, mp2, q2.data());   // KF2 points searched in KF1
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    KfProjArgs a{};
+    fill_proj(a, s, o1, KF2, mp1, true);
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    std::copy(R1w, R1w + 9, a.Ra);
+    std::copy(t1w, t1w + 3, a.ta);
+    std::copy(sR21, sR21 + 9, a.Rb);
+    std::copy(t21, t21 + 3, a.tb);
+    a.two_stage = 1;
+    a.mode = 2;
+    a.th = th;
+    if ((r = launch_proj(ctx, a)) != ORBX_OK) return r;
+    KfProjArgs b{};
+    fill_proj(b, s, o2, KF1, mp2, true);
+    for (int k = 0; k < 4; k++) b.cam[k] = cam[k];
+    std::copy(R2w, R2w + 9, b.Ra);
+    std::copy(t2w, t2w + 3, b.ta);
+    std::copy(sR12, sR12 + 9, b.Rb);
+    std::copy(t12, t12 + 3, b.tb);
+    b.two_stage = 1;
+    b.mode = 2;
+    b.th = th;
+    if ((r = launch_proj(ctx, b)) != ORBX_OK) return r;
+    std::vector<int32_t> bi1(N1), bd1(N1), bi2(N2), bd2(N2);
+    if (N1) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(bi1.data(), s.base() + o1.bi, (size_t)N1 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(bd1.data(), s.base() + o1.bd, (size_t)N1 * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (N2) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(bi2.data(), s.base() + o2.bi, (size_t)N2 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(bd2.data(), s.base() + o2.bd, (size_t)N2 * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    // bestDist <= TH_HIGH (:1395, :1480), then the agreement check (:1486-1502)
+    int nFound = 0;
+    for (int i1 = 0; i1 < N1; i1++) {
+        new12[i1] = -1;
+        const int idx2 = bd1[i1] <= kTHHigh ? bi1[i1] : -1;
+        if (idx2 >= 0 && bd2[idx2] <= kTHHigh && bi2[idx2] == i1) {
+            new12[i1] = idx2;
+            nFound++;
+        }
+    }
+    *n_found = nFound;
+    return ORBX_OK;
+}
+
+extern "C" int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32_t* obs_ptr, const uint8_t* desc,
+                                            int32_t* best)
+{
+    if (!ctx || n_mp < 0 || (n_mp > 0 && (!obs_ptr || !best))) return ORBX_ERR_ARG;
+    if (n_mp == 0) return ORBX_OK;
+    if (obs_ptr[0] < 0) return ORBX_ERR_ARG;
+    for (int m = 0; m < n_mp; m++)
+        if (obs_ptr[m + 1] < obs_ptr[m] || obs_ptr[m + 1] - obs_ptr[m] >= (1 << 20)) return ORBX_ERR_ARG;
+    const size_t rows = (size_t)obs_ptr[n_mp];
+    if (rows && !desc) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    Staging s{ctx};
+    const size_t o_ptr = s.res((size_t)(n_mp + 1) * 4, obs_ptr), o_d = s.res(rows * 32, desc),
+                 o_b = s.res((size_t)n_mp * 4);
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    const int per = kBlock / 64;
+    hipLaunchKernelGGL(k_distinctive, dim3((n_mp + per - 1) / per), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const int32_t*>(s.base() + o_ptr), s.base() + o_d, n_mp,
+                       reinterpret_cast<int32_t*>(s.base() + o_b));
+    ORBX_HIP_CHECK(hipGetLastError());
+    ORBX_HIP_CHECK(hipMemcpyAsync(best, s.base() + o_b, (size_t)n_mp * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
