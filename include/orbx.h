@@ -323,6 +323,28 @@ int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_fr
                         const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
                         const float* T2w, float s12, const float* R12, const float* t12, float th,
                         const int32_t* prior12, int32_t* new12, int* n_found);
+/* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const
+ * vector<MapPoint*>& vpPoints, vector<MapPoint*>& vpMatched, int th)
+ * (src/ORBmatcher.cc:286-407), loop closing.  mps: vpPoints; mp_skip:
+ * pMP->isBad() or already in vpMatched (spAlreadyFound).  matched (in/out,
+ * KF->n): vpMatched as an index into mps (any value >= 0 for an entry set by
+ * the caller), -1 where NULL; the call writes the entries it assigns. */
+int orbx_search_by_projection_kf_sim3(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
+                                      const orbx_mappoint_view* mps, const uint8_t* mp_skip,
+                                      const float* Scw, int th, int32_t* matched, int* n_matches);
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const
+ * set<MapPoint*>& sAlreadyFound, float th, int ORBdist) (src/ORBmatcher.cc:
+ * 1622-1746), relocalisation.  KF: pKF's keypoints (mvKeysUn); kf_mps: the
+ * map point of each KF keypoint (pos, min_dist, desc); kf_valid: pMP &&
+ * !isBad() && !sAlreadyFound.count(pMP).  F: CurrentFrame; f_assigned:
+ * CurrentFrame.mvpMapPoints[i] != NULL; Tcw: CurrentFrame.mTcw (4x4
+ * row-major); cam: CurrentFrame's fx, fy, cx, cy.  matches_f (out, F->n):
+ * the KF keypoint whose map point this call assigns, or -1. */
+int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, const orbx_frame_view* KF,
+                                       const float* cam, const orbx_mappoint_view* kf_mps,
+                                       const uint8_t* kf_valid, const uint8_t* f_assigned,
+                                       const float* Tcw, float th, int orb_dist, int check_ori,
+                                       int32_t* matches_f, int* n_matches);
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:185-250) for
  * n_mp map points at once: point m's observed descriptors (non-bad
  * keyframes, observation order) are rows obs_ptr[m] .. obs_ptr[m+1]-1 of

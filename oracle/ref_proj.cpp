@@ -213,6 +213,145 @@ int search_by_sim3(const FrameRef& K1, const FrameRef& K2, const float* cam, con
     return nFound;
 }
 
+// ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
+// (src/ORBmatcher.cc:286-407).  matched: per KF keypoint, the vpPoints
+// index assigned (or any value >= 0 for an entry already set), -1 empty.
+int search_by_projection_kf_sim3(const FrameRef& KF, const float* cam, int n_mp, const float* pos,
+                                 const float* normal, const float* dmin, const float* dmax, const uint8_t* desc,
+                                 const uint8_t* skip, const float* Scw, int th, int32_t* matched)
+{
+    float R[9], t[3], Ow[3];
+    pose_parts(Scw, 1, R, t, Ow);
+    const int nMaxLevel = (int)KF.scaleFactors.size() - 1;
+    int nmatches = 0;
+    for (int m = 0; m < n_mp; m++) {
+        if (skip[m]) continue;   // isBad() || spAlreadyFound.count(pMP)
+        const float* Xw = pos + 3 * m;
+        float p3Dc[3];
+        xform(R, t, Xw, p3Dc);
+        if (p3Dc[2] < 0.0) continue;
+        const float invz = 1 / p3Dc[2];
+        const float x = p3Dc[0] * invz, y = p3Dc[1] * invz;
+        const float u = cam[0] * x + cam[2], v = cam[1] * y + cam[3];
+        if (!(u >= KF.minX && u < KF.maxX && v >= KF.minY && v < KF.maxY)) continue;
+        const float maxDistance = dmax[m], minDistance = dmin[m];
+        const float PO[3] = {Xw[0] - Ow[0], Xw[1] - Ow[1], Xw[2] - Ow[2]};
+        const float dist = norm3(PO);
+        if (dist < minDistance || dist > maxDistance) continue;
+        if (dot3(PO, normal + 3 * m) < 0.5 * dist) continue;
+        const float ratio = dist / minDistance;
+        const int pred = std::min(predicted_level(KF.scaleFactors, ratio), nMaxLevel);
+        const float radius = th * KF.scaleFactors[pred];
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (size_t idx : KF.featuresInArea(u, v, radius, -1, -1)) {
+            if (matched[idx] >= 0) continue;
+            const int lvl = KF.keys[idx].octave;
+            if (lvl < pred - 1 || lvl > pred) continue;
+            const int d = descriptor_distance(desc + (size_t)m * 32, KF.desc.data() + idx * 32);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx = (int)idx;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            matched[bestIdx] = m;
+            nmatches++;
+        }
+    }
+    return nmatches;
+}
+
+// ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th,
+// ORBdist) (src/ORBmatcher.cc:1622-1746).  kf_valid: pMP && !isBad() &&
+// !sAlreadyFound.count(pMP); f_assigned: CurrentFrame.mvpMapPoints[i].
+// matches_f: the KF keypoint whose map point this call assigns, or -1.
+int search_by_projection_frame_kf(const FrameRef& F, const FrameRef& KF, const float* cam, const float* pos,
+                                  const float* dmin, const uint8_t* desc, const uint8_t* kf_valid,
+                                  const uint8_t* f_assigned, const float* Tcw, float th, int ORBdist, bool checkOri,
+                                  int32_t* matches_f)
+{
+    float R[9], t[3], Ow[3];
+    pose_parts(Tcw, 0, R, t, Ow);
+    const int NF = (int)F.keys.size();
+    std::vector<uint8_t> taken(f_assigned, f_assigned + NF);
+    for (int i = 0; i < NF; i++) matches_f[i] = -1;
+    std::vector<int> rotHist[30];
+    int nmatches = 0;
+    const int nLevels = (int)F.scaleFactors.size();
+    for (int i = 0; i < (int)KF.keys.size(); i++) {
+        if (!kf_valid[i]) continue;
+        const float* Xw = pos + 3 * i;
+        float x3Dc[3];
+        xform(R, t, Xw, x3Dc);
+        const float xc = x3Dc[0], yc = x3Dc[1];
+        const float invzc = (float)(1.0 / (double)x3Dc[2]);
+        const float u = cam[0] * xc * invzc + cam[2];
+        const float v = cam[1] * yc * invzc + cam[3];
+        if (u < F.minX || u > F.maxX) continue;
+        if (v < F.minY || v > F.maxY) continue;
+        const float minDistance = dmin[i];
+        const float PO[3] = {Xw[0] - Ow[0], Xw[1] - Ow[1], Xw[2] - Ow[2]};
+        const float dist3D = norm3(PO);
+        const float ratio = dist3D / minDistance;
+        const int pred = std::min(predicted_level(F.scaleFactors, ratio), nLevels - 1);
+        const float radius = th * F.scaleFactors[pred];
+        const std::vector<size_t> idx2 = F.featuresInArea(u, v, radius, pred - 1, pred + 1);
+        if (idx2.empty()) continue;
+        int bestDist = INT_MAX, bestIdx2 = -1;
+        for (size_t i2 : idx2) {
+            if (taken[i2]) continue;
+            const int d = descriptor_distance(desc + (size_t)i * 32, F.desc.data() + i2 * 32);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx2 = (int)i2;
+            }
+        }
+        if (bestDist <= ORBdist) {
+            taken[bestIdx2] = 1;
+            matches_f[bestIdx2] = i;
+            nmatches++;
+            if (checkOri) {
+                const float factor = 1.0f / 30;
+                float rot = KF.keys[i].angle - F.keys[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == 30) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    if (checkOri) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int b = 0; b < 30; b++) {   // ComputeThreeMaxima (:1748-1789)
+            const int s = (int)rotHist[b].size();
+            if (s > max1) {
+                max3 = max2; max2 = max1; max1 = s;
+                ind3 = ind2; ind2 = ind1; ind1 = b;
+            } else if (s > max2) {
+                max3 = max2; max2 = s;
+                ind3 = ind2; ind2 = b;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = b;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        for (int b = 0; b < 30; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int k : rotHist[b]) {
+                matches_f[k] = -1;
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
+}
+
 // MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:185-250): the
 // descriptor with the least median distance to the others.
 int distinctive_descriptor(const uint8_t* desc, int N)
@@ -280,5 +419,31 @@ extern "C" int orbx_ref_distinctive_descriptors(int n_mp, const int32_t* obs_ptr
 {
     for (int m = 0; m < n_mp; m++)
         best[m] = distinctive_descriptor(desc + (size_t)obs_ptr[m] * 32, obs_ptr[m + 1] - obs_ptr[m]);
+    return ORBX_OK;
+}
+
+extern "C" int orbx_ref_search_by_projection_kf_sim3(const orbx_frame_view* KF, const float* cam, int n_mp,
+                                                     const float* pos, const float* normal, const float* dmin,
+                                                     const float* dmax, const uint8_t* desc, const uint8_t* skip,
+                                                     const float* Scw, int th, int32_t* matched, int* n_matches)
+{
+    static thread_local FrameRef F;
+    frame_ref(KF, F);
+    *n_matches = search_by_projection_kf_sim3(F, cam, n_mp, pos, normal, dmin, dmax, desc, skip, Scw, th, matched);
+    return ORBX_OK;
+}
+
+extern "C" int orbx_ref_search_by_projection_frame_kf(const orbx_frame_view* Fv, const orbx_frame_view* KFv,
+                                                      const float* cam, const float* pos, const float* dmin,
+                                                      const uint8_t* desc, const uint8_t* kf_valid,
+                                                      const uint8_t* f_assigned, const float* Tcw, float th,
+                                                      int orb_dist, int check_ori, int32_t* matches_f,
+                                                      int* n_matches)
+{
+    static thread_local FrameRef F, K;
+    frame_ref(Fv, F);
+    frame_ref(KFv, K);
+    *n_matches = search_by_projection_frame_kf(F, K, cam, pos, dmin, desc, kf_valid, f_assigned, Tcw, th, orb_dist,
+                                               check_ori != 0, matches_f);
     return ORBX_OK;
 }

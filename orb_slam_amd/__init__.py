@@ -96,6 +96,8 @@ def _declare(L):
         "orbx_fuse_candidates": ([vp, vp, vp, vp, vp, i, f, vp, vp], i),
         "orbx_search_by_sim3": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f, vp, vp, f, vp, vp, ip], i),
         "orbx_distinctive_descriptors": ([vp, i, vp, vp, vp], i),
+        "orbx_search_by_projection_kf_sim3": ([vp, vp, vp, vp, vp, vp, i, vp, ip], i),
+        "orbx_search_by_projection_frame_kf": ([vp, vp, vp, vp, vp, vp, vp, vp, f, i, i, vp, ip], i),
         "orbx_pose_optimization": ([vp, vp, ip, vp], i),
         "orbx_pose_optimization_batch": ([vp, i, vp, vp, vp], i),
         "orbx_pose_stage": ([vp, i, vp], i),

@@ -191,6 +191,149 @@ __global__ __launch_bounds__(256) void k_distinctive(const int32_t* ptr, const u
     if (lane == 0) best[m] = (int)(key & 0xFFFFF);
 }
 
+
+// Sequential projection searches (the candidate exclusion depends on the
+// earlier points' assignments): one wavefront replays the reference's loop
+// over the points in order; per point the lanes stride the searched
+// frame's keypoints (LDS table) and one min reduction gives the first
+// strict minimum in GetFeaturesInArea order.
+//  variant 0: SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)
+//             (src/ORBmatcher.cc:286-407)
+//  variant 1: SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th,
+//             ORBdist) (:1622-1746), with the rotation-consistency filter
+struct SeqProjArgs {
+    FrameDev T;                 // searched keyframe (variant 0) / frame (variant 1)
+    float scales[kMaxLevels];
+    int nlevels;
+    float cam[4];
+    float R[9], t[3], Ow[3];
+    float th;
+    int orb_dist, check_ori, variant;
+    int nq;
+    const float* pos;
+    const float* normal;
+    const float* dmin;
+    const float* dmax;
+    const uint8_t* qdesc;
+    const uint8_t* qskip;       // variant 0: isBad || already found; variant 1: !valid
+    const orbx_keypoint* qkps;  // variant 1: the KF keypoints (angles)
+    const uint8_t* assigned;    // variant 1: CurrentFrame.mvpMapPoints[i] != NULL
+    int32_t* out;               // variant 0: vpMatched (in/out); variant 1: matches_f
+    int32_t* out_n;
+};
+
+__global__ __launch_bounds__(64) void k_proj_seq(SeqProjArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int n = a.T.n, lane = threadIdx.x;
+    float* tx = reinterpret_cast<float*>(smem);
+    float* ty = tx + n;
+    int* tco = reinterpret_cast<int*>(ty + n);
+    int* taken = tco + n;
+    int* keys = taken + n;
+    int* hist = keys + n;
+    signed char* bins = reinterpret_cast<signed char*>(hist + 32);
+    for (int i = lane; i < n; i += 64) {
+        const orbx_keypoint k = a.T.kps[i];
+        tx[i] = k.x;
+        ty[i] = k.y;
+        const int cell = grid_cell(a.T, k.x, k.y);
+        tco[i] = (cell & 0xFFFF) | (k.octave << 16);
+        taken[i] = a.variant == 0 ? (a.out[i] >= 0) : (int)a.assigned[i];
+    }
+    wave_sync();
+    int nmatches = 0, npushed = 0;
+    for (int m = 0; m < a.nq; m++) {
+        if (a.qskip[m]) continue;
+        const float Xw[3] = {a.pos[3 * m], a.pos[3 * m + 1], a.pos[3 * m + 2]};
+        float pc[3];
+        xform3(a.R, a.t, Xw, pc);
+        float u, v;
+        int pred, lo, hi, accept;
+        const float PO[3] = {__fsub_rn(Xw[0], a.Ow[0]), __fsub_rn(Xw[1], a.Ow[1]), __fsub_rn(Xw[2], a.Ow[2])};
+        const float dist3D = norm3_cv(PO);
+        const float minDistance = a.dmin[m];
+        if (a.variant == 0) {
+            if (pc[2] < 0.0f) continue;
+            const float invz = __fdiv_rn(1.0f, pc[2]);
+            u = __fadd_rn(__fmul_rn(a.cam[0], __fmul_rn(pc[0], invz)), a.cam[2]);
+            v = __fadd_rn(__fmul_rn(a.cam[1], __fmul_rn(pc[1], invz)), a.cam[3]);
+            if (!(u >= a.T.min_x && u < a.T.max_x && v >= a.T.min_y && v < a.T.max_y)) continue;
+            if (dist3D < minDistance || dist3D > a.dmax[m]) continue;
+            const float Pn[3] = {a.normal[3 * m], a.normal[3 * m + 1], a.normal[3 * m + 2]};
+            if (dot3_cv(PO, Pn) < 0.5 * (double)dist3D) continue;
+        } else {
+            const float invzc = (float)(1.0 / (double)pc[2]);
+            u = __fadd_rn(__fmul_rn(__fmul_rn(a.cam[0], pc[0]), invzc), a.cam[2]);
+            v = __fadd_rn(__fmul_rn(__fmul_rn(a.cam[1], pc[1]), invzc), a.cam[3]);
+            if (u < a.T.min_x || u > a.T.max_x) continue;
+            if (v < a.T.min_y || v > a.T.max_y) continue;
+        }
+        const float ratio = __fdiv_rn(dist3D, minDistance);
+        pred = 0;
+        while (pred < a.nlevels && a.scales[pred] < ratio) pred++;
+        pred = min(pred, a.nlevels - 1);
+        const float radius = __fmul_rn(a.th, a.scales[pred]);
+        if (a.variant == 0) {
+            lo = pred - 1;
+            hi = pred;
+            accept = kTHLow;
+        } else {
+            lo = pred - 1;
+            hi = pred + 1;
+            accept = a.orb_dist;
+        }
+        const AreaQuery q = area_cells(a.T, u, v, radius);
+        if (q.empty) continue;
+        uint4 d0, d1;
+        load_desc(a.qdesc + (size_t)m * 32, d0, d1);
+        unsigned long long bk = ~0ull;
+        for (int j = lane; j < n; j += 64) {
+            const int co = tco[j];
+            const int oct = co >> 16;
+            if (oct < lo || oct > hi) continue;
+            const int cell = (co & 0xFFFF) == 0xFFFF ? -1 : (co & 0xFFFF);
+            if (!in_area(q, cell, tx[j], ty[j], u, v, radius)) continue;
+            if (taken[j]) continue;
+            uint4 b0, b1;
+            load_desc(a.T.desc + (size_t)j * 32, b0, b1);
+            const unsigned long long key = ((unsigned long long)hamming256(d0, d1, b0, b1) << 32) |
+                                           ((unsigned long long)cell << 12) | (unsigned long long)j;
+            bk = key < bk ? key : bk;
+        }
+        bk = wave_min_u64(bk);
+        if (bk == ~0ull || (int)(bk >> 32) > accept) continue;
+        const int j = (int)(bk & 0xFFF);
+        if (lane == 0) {
+            taken[j] = 1;
+            a.out[j] = m;
+            if (a.variant == 1 && a.check_ori) {
+                bins[npushed] = (signed char)rot_bin(a.qkps[m].angle, a.T.kps[j].angle);
+                keys[npushed] = j;
+            }
+        }
+        if (a.variant == 1 && a.check_ori) npushed++;
+        nmatches++;
+        wave_sync();
+    }
+    wave_sync();
+    if (lane == 0) {
+        if (npushed) {
+            for (int b = 0; b < kHistoLength; b++) hist[b] = 0;
+            for (int i = 0; i < npushed; i++) hist[bins[i]]++;
+            int i1, i2, i3;
+            three_maxima(hist, i1, i2, i3);
+            for (int i = 0; i < npushed; i++) {
+                const int b = bins[i];
+                if (b == i1 || b == i2 || b == i3) continue;
+                a.out[keys[i]] = -1;
+                nmatches--;
+            }
+        }
+        *a.out_n = nmatches;
+    }
+}
+
 namespace {
 
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -459,6 +602,102 @@ extern "C" int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32
                        reinterpret_cast<int32_t*>(s.base() + o_b));
     ORBX_HIP_CHECK(hipGetLastError());
     ORBX_HIP_CHECK(hipMemcpyAsync(best, s.base() + o_b, (size_t)n_mp * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+extern "C" int orbx_search_by_projection_kf_sim3(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
+                                                 const orbx_mappoint_view* mps, const uint8_t* mp_skip,
+                                                 const float* Scw, int th, int32_t* matched, int* n_matches)
+{
+    if (!ctx || !valid_kf(KF) || !cam || !valid_mps(mps, true) || !Scw || !n_matches || (mps->n && !mp_skip) ||
+        (KF->n && !matched))
+        return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    Staging s{ctx};
+    const size_t o_kp = s.res((size_t)KF->n * sizeof(orbx_keypoint), KF->keys_un), o_kd = s.res((size_t)KF->n * 32, KF->desc);
+    const size_t o_pos = s.res((size_t)mps->n * 12, mps->pos), o_nrm = s.res((size_t)mps->n * 12, mps->normal),
+                 o_mn = s.res((size_t)mps->n * 4, mps->min_dist), o_mx = s.res((size_t)mps->n * 4, mps->max_dist),
+                 o_qd = s.res((size_t)mps->n * 32, mps->desc), o_sk = s.res(mps->n, mp_skip),
+                 o_out = s.res((size_t)KF->n * 4, matched), o_n = s.res(4);
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    uint8_t* d = s.base();
+    SeqProjArgs a{};
+    a.T = kf_dev(KF, d, o_kp, o_kd);
+    a.nlevels = KF->nlevels;
+    a.scales[0] = 1.0f;
+    for (int l = 1; l < KF->nlevels; l++) a.scales[l] = a.scales[l - 1] * KF->scale_factor;
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    pose_parts(Scw, 1, a.R, a.t, a.Ow);
+    a.th = (float)th;
+    a.variant = 0;
+    a.nq = mps->n;
+    a.pos = reinterpret_cast<const float*>(d + o_pos);
+    a.normal = reinterpret_cast<const float*>(d + o_nrm);
+    a.dmin = reinterpret_cast<const float*>(d + o_mn);
+    a.dmax = reinterpret_cast<const float*>(d + o_mx);
+    a.qdesc = d + o_qd;
+    a.qskip = d + o_sk;
+    a.out = reinterpret_cast<int32_t*>(d + o_out);
+    a.out_n = reinterpret_cast<int32_t*>(d + o_n);
+    const size_t lds = (size_t)std::max(KF->n, 1) * 21 + 32 * 4 + 64;
+    hipLaunchKernelGGL(k_proj_seq, dim3(1), dim3(64), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if (KF->n) ORBX_HIP_CHECK(hipMemcpyAsync(matched, d + o_out, (size_t)KF->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(n_matches, d + o_n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+extern "C" int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, const orbx_frame_view* KF,
+                                                  const float* cam, const orbx_mappoint_view* kf_mps,
+                                                  const uint8_t* kf_valid, const uint8_t* f_assigned,
+                                                  const float* Tcw, float th, int orb_dist, int check_ori,
+                                                  int32_t* matches_f, int* n_matches)
+{
+    if (!ctx || !valid_kf(F) || !valid_kf(KF) || !cam || !valid_mps(kf_mps, false) || kf_mps->n != KF->n || !Tcw ||
+        !n_matches || (KF->n && !kf_valid) || (F->n && (!f_assigned || !matches_f)))
+        return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    Staging s{ctx};
+    const size_t o_kp = s.res((size_t)F->n * sizeof(orbx_keypoint), F->keys_un), o_kd = s.res((size_t)F->n * 32, F->desc);
+    const size_t o_qk = s.res((size_t)KF->n * sizeof(orbx_keypoint), KF->keys_un),
+                 o_pos = s.res((size_t)KF->n * 12, kf_mps->pos), o_mn = s.res((size_t)KF->n * 4, kf_mps->min_dist),
+                 o_qd = s.res((size_t)KF->n * 32, kf_mps->desc), o_sk = s.res(KF->n), o_as = s.res(F->n, f_assigned),
+                 o_out = s.res((size_t)F->n * 4), o_n = s.res(4);
+    std::vector<uint8_t> skip(KF->n);
+    for (int i = 0; i < KF->n; i++) skip[i] = !kf_valid[i];
+    if (KF->n) s.puts.push_back({o_sk, {skip.data(), (size_t)KF->n}});
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    uint8_t* d = s.base();
+    ORBX_HIP_CHECK(hipMemsetAsync(d + o_out, 0xFF, (size_t)std::max(F->n, 1) * 4, ctx->stream));
+    SeqProjArgs a{};
+    a.T = kf_dev(F, d, o_kp, o_kd);
+    a.nlevels = F->nlevels;
+    a.scales[0] = 1.0f;
+    for (int l = 1; l < F->nlevels; l++) a.scales[l] = a.scales[l - 1] * F->scale_factor;
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    pose_parts(Tcw, 0, a.R, a.t, a.Ow);
+    a.th = th;
+    a.orb_dist = orb_dist;
+    a.check_ori = check_ori;
+    a.variant = 1;
+    a.nq = KF->n;
+    a.pos = reinterpret_cast<const float*>(d + o_pos);
+    a.dmin = reinterpret_cast<const float*>(d + o_mn);
+    a.qdesc = d + o_qd;
+    a.qskip = d + o_sk;
+    a.qkps = reinterpret_cast<const orbx_keypoint*>(d + o_qk);
+    a.assigned = d + o_as;
+    a.out = reinterpret_cast<int32_t*>(d + o_out);
+    a.out_n = reinterpret_cast<int32_t*>(d + o_n);
+    const size_t lds = (size_t)std::max(F->n, 1) * 21 + 32 * 4 + 64;
+    hipLaunchKernelGGL(k_proj_seq, dim3(1), dim3(64), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if (F->n) ORBX_HIP_CHECK(hipMemcpyAsync(matches_f, d + o_out, (size_t)F->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(n_matches, d + o_n, 4, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return ORBX_OK;
 }

@@ -71,3 +71,41 @@ def test_distinctive_descriptors_match_oracle(ctx, seed):
     gb = np.zeros(len(p) - 1, np.int32)
     assert ox.lib().orbx_distinctive_descriptors(ctx.handle, len(p) - 1, ox._ptr(p), ox._ptr(d), ox._ptr(gb)) == 0
     assert np.array_equal(gb, rb)
+
+
+@pytest.mark.parametrize("seed,th,scale", [(0, 10, 1.5), (1, 5, 1.0), (2, 20, 0.8)])
+def test_search_by_projection_kf_sim3_matches_oracle(ctx, seed, th, scale):
+    from test_proj_oracle import ref_proj_kf_sim3, seq_case
+    k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
+    S = T2.copy()
+    S[:3, :] *= np.float32(scale)
+    skip = (rng.random(len(k1)) < 0.1).astype(np.uint8)
+    matched = np.full(len(k2), -1, np.int32)
+    matched[rng.random(len(k2)) < 0.05] = 10 ** 6
+    KF = pd.view(k2, d2)
+    ro, rn = ref_proj_kf_sim3(KF, mps, skip, S, th, matched)
+    go = matched.copy()
+    gn = ctypes.c_int()
+    assert ox.lib().orbx_search_by_projection_kf_sim3(ctx.handle, ctypes.byref(KF), ox._ptr(pd.CAM),
+                                                      ctypes.byref(mps[0]), ox._ptr(skip), ox._ptr(S), th,
+                                                      ox._ptr(go), ctypes.byref(gn)) == 0
+    assert gn.value == rn and rn > 100
+    assert np.array_equal(go, ro)
+
+
+@pytest.mark.parametrize("seed,th,orb,ori", [(0, 10.0, 100, 1), (1, 5.0, 64, 0), (2, 15.0, 50, 1)])
+def test_search_by_projection_frame_kf_matches_oracle(ctx, seed, th, orb, ori):
+    from test_proj_oracle import ref_proj_frame_kf, seq_case
+    k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
+    valid = (rng.random(len(k1)) < 0.8).astype(np.uint8)
+    assigned = (rng.random(len(k2)) < 0.1).astype(np.uint8)
+    F, KF = pd.view(k2, d2), pd.view(k1, d1)
+    ro, rn = ref_proj_frame_kf(F, KF, mps, valid, assigned, T2, th, orb, ori)
+    go = np.zeros(len(k2), np.int32)
+    gn = ctypes.c_int()
+    assert ox.lib().orbx_search_by_projection_frame_kf(ctx.handle, ctypes.byref(F), ctypes.byref(KF),
+                                                       ox._ptr(pd.CAM), ctypes.byref(mps[0]), ox._ptr(valid),
+                                                       ox._ptr(assigned), ox._ptr(T2), th, orb, ori, ox._ptr(go),
+                                                       ctypes.byref(gn)) == 0
+    assert gn.value == rn and rn > 100
+    assert np.array_equal(go, ro)

@@ -108,3 +108,63 @@ def test_distinctive_descriptor_is_the_medoid():
         D = (X[:, None, :] != X[None, :, :]).sum(2)
         med = np.sort(D, 1)[:, (N - 1) // 2]
         assert best[m] == int(np.argmin(med))
+
+
+def ref_proj_kf_sim3(KF, mps, skip, Scw, th, matched):
+    L = load()
+    L.orbx_ref_search_by_projection_kf_sim3.argtypes = ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] +
+                                                        [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p,
+                                                                                 ctypes.c_void_p])
+    out = matched.copy()
+    n = ctypes.c_int()
+    a = mps[1]
+    assert L.orbx_ref_search_by_projection_kf_sim3(ctypes.byref(KF), ptr(pd.CAM), mps[0].n, ptr(a["pos"]),
+                                                   ptr(a["normal"]), ptr(a["min_dist"]), ptr(a["max_dist"]),
+                                                   ptr(a["desc"]), ptr(skip), ptr(Scw), th, ptr(out),
+                                                   ctypes.byref(n)) == 0
+    return out, n.value
+
+
+def ref_proj_frame_kf(F, KF, kf_mps, kf_valid, assigned, Tcw, th, orb_dist, check_ori):
+    L = load()
+    L.orbx_ref_search_by_projection_frame_kf.argtypes = ([ctypes.c_void_p] * 9 + [ctypes.c_float, ctypes.c_int,
+                                                                                 ctypes.c_int, ctypes.c_void_p,
+                                                                                 ctypes.c_void_p])
+    out = np.zeros(F.n, np.int32)
+    n = ctypes.c_int()
+    a = kf_mps[1]
+    assert L.orbx_ref_search_by_projection_frame_kf(ctypes.byref(F), ctypes.byref(KF), ptr(pd.CAM), ptr(a["pos"]),
+                                                    ptr(a["min_dist"]), ptr(a["desc"]), ptr(kf_valid),
+                                                    ptr(assigned), ptr(Tcw), th, orb_dist, check_ori, ptr(out),
+                                                    ctypes.byref(n)) == 0
+    return out, n.value
+
+
+def seq_case(seed=0):
+    k1, d1, k2, d2, du, dv = pd.keyframes()
+    rng = np.random.default_rng(seed)
+    T2 = pd.pose_T([du * pd.Z0 / pd.CAM[0], dv * pd.Z0 / pd.CAM[1], 0.0])
+    mps = pd.mappoints(k1, d1, pd.pose_T([0, 0, 0]), rng)
+    return k1, d1, k2, d2, T2, mps, rng
+
+
+def test_search_by_projection_kf_sim3_assigns_each_keypoint_once():
+    k1, d1, k2, d2, T2, mps, rng = seq_case()
+    S = T2.copy()
+    S[:3, :] *= np.float32(1.5)
+    skip = (rng.random(len(k1)) < 0.1).astype(np.uint8)
+    matched = np.full(len(k2), -1, np.int32)
+    matched[rng.random(len(k2)) < 0.05] = 10 ** 6
+    out, n = ref_proj_kf_sim3(pd.view(k2, d2), mps, skip, S, 10, matched)
+    new = out[(out >= 0) & (out < 10 ** 6)]
+    assert n == len(new) > 200 and len(np.unique(new)) == len(new)
+    assert (out[matched == 10 ** 6] == 10 ** 6).all()
+
+
+def test_search_by_projection_frame_kf_relocalisation():
+    k1, d1, k2, d2, T2, mps, rng = seq_case(1)
+    valid = (rng.random(len(k1)) < 0.8).astype(np.uint8)
+    assigned = (rng.random(len(k2)) < 0.1).astype(np.uint8)
+    out, n = ref_proj_frame_kf(pd.view(k2, d2), pd.view(k1, d1), mps, valid, assigned, T2, 10.0, 100, 1)
+    assert n == int((out >= 0).sum()) > 200
+    assert (out[assigned == 1] == -1).all()
