@@ -353,6 +353,33 @@ int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, 
 int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32_t* obs_ptr,
                                  const uint8_t* desc, int32_t* best);
 
+/* DBoW2 vocabulary: the tree as
+ * TemplatedVocabulary::loadFromTextFile builds it (Thirdparty/DBoW2/DBoW2/
+ * TemplatedVocabulary.h:1338-1420) -- node 0 the root, node i (1..n-1) a
+ * child of parent[i] (children in increasing id order), word ids given to
+ * the nodes flagged is_leaf in id order, a 32-byte descriptor and a weight
+ * (idf) per node.  Kept in HBM for the vocabulary's lifetime. */
+typedef struct orbx_vocab orbx_vocab;
+int orbx_vocab_create(orbx_ctx* ctx, int k, int L, int n_nodes, const int32_t* parent,
+                      const uint8_t* is_leaf, const uint8_t* desc, const double* weight,
+                      orbx_vocab** out);
+void orbx_vocab_destroy(orbx_vocab* voc);
+int orbx_vocab_n_words(const orbx_vocab* voc);
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&,
+ * levelsup) (:1127-1259) as Frame::ComputeBoW calls it (src/Frame.cc:
+ * 279-286, levelsup 4), TF-IDF weighting with L1 scoring (ORBvoc.txt's).
+ * The tree descent of the n descriptors runs on the device; per feature:
+ * word_id, weight and the level-(L - levelsup) node (node_id, -1 if the
+ * descent ended above that level).  BowVector: n_words (word, value) pairs,
+ * words ascending, values L1-normalised.  FeatureVector: n_fv_nodes node
+ * ids ascending with CSR offsets fv_ptr (n_fv_nodes + 1) into fv_feat.
+ * Stopped words (weight 0) are left out of both.  Capacities: n entries
+ * (fv_ptr: n + 1). */
+int orbx_vocab_transform(orbx_ctx* ctx, const orbx_vocab* voc, int n, const uint8_t* desc,
+                         int levelsup, int32_t* word_id, double* weight, int32_t* node_id,
+                         uint32_t* bow_words, double* bow_values, int* n_words,
+                         uint32_t* fv_nodes, int32_t* fv_ptr, int32_t* fv_feat, int* n_fv_nodes);
+
 /* ------------------------------------------------------------------------ */
 /* C. Local bundle adjustment                                                */
 /* ------------------------------------------------------------------------ */

@@ -98,6 +98,10 @@ def _declare(L):
         "orbx_distinctive_descriptors": ([vp, i, vp, vp, vp], i),
         "orbx_search_by_projection_kf_sim3": ([vp, vp, vp, vp, vp, vp, i, vp, ip], i),
         "orbx_search_by_projection_frame_kf": ([vp, vp, vp, vp, vp, vp, vp, vp, f, i, i, vp, ip], i),
+        "orbx_vocab_create": ([vp, i, i, i, vp, vp, vp, vp, ctypes.POINTER(vp)], i),
+        "orbx_vocab_destroy": ([vp], None),
+        "orbx_vocab_n_words": ([vp], i),
+        "orbx_vocab_transform": ([vp, vp, i, vp, i, vp, vp, vp, vp, vp, ip, vp, vp, vp, ip], i),
         "orbx_pose_optimization": ([vp, vp, ip, vp], i),
         "orbx_pose_optimization_batch": ([vp, i, vp, vp, vp], i),
         "orbx_pose_stage": ([vp, i, vp], i),
