@@ -353,6 +353,19 @@ int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, 
 int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32_t* obs_ptr,
                                  const uint8_t* desc, int32_t* best);
 
+/* Frame construction.  Frame::UndistortKeyPoints
+ * (src/Frame.cc:288-318): cv::undistortPoints with P = K, K = (fx, fy, cx,
+ * cy), dist = (k1, k2, p1, p2, k3) (mDistCoef; k3 = 0 for 4 coefficients).
+ * A zero k1 copies the keypoints (:290-294), as the reference does. */
+int orbx_undistort_keypoints(orbx_ctx* ctx, int n, const orbx_keypoint* keys, const float* K,
+                             const float* dist, orbx_keypoint* keys_un);
+/* Frame::ComputeImageBounds (src/Frame.cc:320-348): bounds = mnMinX,
+ * mnMaxX, mnMinY, mnMaxY for a w x h image (host only, four points). */
+int orbx_compute_image_bounds(int w, int h, const float* K, const float* dist, float* bounds);
+/* Device-resident form: undistort the keypoints of extracted slots
+ * [first, first+count) in place (after orbx_dev_extract, before matching). */
+int orbx_dev_undistort(orbx_ctx* ctx, int first, int count, const float* K, const float* dist);
+
 /* DBoW2 vocabulary: the tree as
  * TemplatedVocabulary::loadFromTextFile builds it (Thirdparty/DBoW2/DBoW2/
  * TemplatedVocabulary.h:1338-1420) -- node 0 the root, node i (1..n-1) a

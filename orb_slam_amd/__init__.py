@@ -102,6 +102,9 @@ def _declare(L):
         "orbx_vocab_destroy": ([vp], None),
         "orbx_vocab_n_words": ([vp], i),
         "orbx_vocab_transform": ([vp, vp, i, vp, i, vp, vp, vp, vp, vp, ip, vp, vp, vp, ip], i),
+        "orbx_undistort_keypoints": ([vp, i, vp, vp, vp, vp], i),
+        "orbx_compute_image_bounds": ([i, i, vp, vp, vp], i),
+        "orbx_dev_undistort": ([vp, i, i, vp, vp], i),
         "orbx_pose_optimization": ([vp, vp, ip, vp], i),
         "orbx_pose_optimization_batch": ([vp, i, vp, vp, vp], i),
         "orbx_pose_stage": ([vp, i, vp], i),
