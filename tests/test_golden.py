@@ -179,3 +179,68 @@ def test_gpu_pose_golden(gctx):
     assert np.abs(sp.pose_of(p) - z["out_Tcw"]).max() <= 1e-5
     assert np.array_equal(arrs["outlier"], z["out_outlier"]) and int(n[0]) == int(z["n_inliers"])
     assert st[0].rounds == int(z["rounds"]) and list(st[0].n_bad) == list(z["n_bad"])
+
+
+# ------------------------------------------------------------------ vocabulary-node searches, DBoW2 transform
+def bow_views(z):
+    from bow_data import make_view
+    out = []
+    for tag in ("a", "b"):
+        kps = np.ascontiguousarray(z[f"{tag}_kps"]).view(ox.KEYPOINT).reshape(-1)
+        ids, ptr_, feat = z[f"{tag}_ids"], z[f"{tag}_ptr"], z[f"{tag}_feat"]
+        node_of = np.zeros(len(kps), np.int64)
+        for j in range(len(ids)):
+            node_of[feat[ptr_[j]:ptr_[j + 1]]] = ids[j]
+        out.append(make_view(kps, z[f"{tag}_desc"], z[f"{tag}_mp"], node_of))
+    return out
+
+
+def bow_pair(z):
+    (V1, a1), (V2, a2) = bow_views(z)
+    return {"V1": V1, "V2": V2, "keep": (a1, a2), "F12": z["F12"].copy(), "sigma2": z["sigma2"].copy()}
+
+
+def test_oracle_bow_golden():
+    from test_bow_oracle import run_ref
+    z = g("bow_pair")
+    P = bow_pair(z)
+    for mode, name in [(0, "bow_frame"), (1, "bow_kf"), (2, "triangulation")]:
+        m, n = run_ref(mode, P, 0.75, 1)
+        assert n == int(z[f"{name}_n"]) and np.array_equal(m, z[f"{name}_matches"])
+
+
+@pytest.mark.gpu
+def test_gpu_bow_golden(gctx):
+    from test_bow_gpu import run_gpu
+    z = g("bow_pair")
+    P = bow_pair(z)
+    for mode, name in [(0, "bow_frame"), (1, "bow_kf"), (2, "triangulation")]:
+        m, n = run_gpu(gctx, mode, P, 0.75, 1)
+        assert n == int(z[f"{name}_n"]) and np.array_equal(m, z[f"{name}_matches"])
+
+
+def vocab_from(z):
+    return {"k": int(z["k"]), "L": int(z["L"]), "parent": z["parent"].copy(), "is_leaf": z["is_leaf"].copy(),
+            "desc": np.ascontiguousarray(z["vdesc"]), "weight": z["weight"].copy()}
+
+
+def check_vocab(z, r):
+    nw, nf = len(z["bow_words"]), len(z["fv_nodes"])
+    assert np.array_equal(r["word"], z["word"]) and np.array_equal(r["weight"], z["w"])
+    assert np.array_equal(r["nid"], z["nid"]) and r["nw"] == nw and r["nf"] == nf
+    assert np.array_equal(r["bw"][:nw], z["bow_words"]) and np.array_equal(r["bv"][:nw], z["bow_values"])
+    assert np.array_equal(r["fn"][:nf], z["fv_nodes"]) and np.array_equal(r["fp"][:nf + 1], z["fv_ptr"])
+    assert np.array_equal(r["ff"][:len(z["fv_feat"])], z["fv_feat"])
+
+
+def test_oracle_vocab_golden():
+    from vocab_data import run_ref
+    z = g("vocab_small")
+    check_vocab(z, run_ref(vocab_from(z), np.ascontiguousarray(z["desc"]), int(z["levelsup"])))
+
+
+@pytest.mark.gpu
+def test_gpu_vocab_golden(gctx):
+    from test_vocab_gpu import gpu_transform
+    z = g("vocab_small")
+    check_vocab(z, gpu_transform(gctx, vocab_from(z), np.ascontiguousarray(z["desc"]), int(z["levelsup"])))

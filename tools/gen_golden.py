@@ -119,6 +119,36 @@ def gen_pose():
     print("pose", n.value, list(st.iterations), list(st.n_bad))
 
 
+def gen_bow():
+    from bow_data import make_pair
+    from test_bow_oracle import run_ref
+    P = make_pair(n1=300, n2=300, n_nodes=25, seed=108)
+    a1, a2 = P["keep"]
+    out = {}
+    for mode, name in [(0, "bow_frame"), (1, "bow_kf"), (2, "triangulation")]:
+        m, n = run_ref(mode, P, 0.75, 1)
+        out[f"{name}_matches"] = m
+        out[f"{name}_n"] = n
+    side = {}
+    for tag, a in (("a", a1), ("b", a2)):
+        for k in ["kps", "desc", "mp", "ids", "ptr", "feat"]:
+            side[f"{tag}_{k}"] = a[k] if k != "kps" else a[k].view(np.uint8).reshape(-1, 28)
+    np.savez_compressed(OUT / "bow_pair.npz", **side, F12=P["F12"], sigma2=P["sigma2"], **out)
+    print("bow", out["bow_frame_n"], out["bow_kf_n"], out["triangulation_n"])
+
+
+def gen_vocab():
+    from vocab_data import features, make_vocab, run_ref
+    V = make_vocab(k=6, L=4, seed=109, irregular=True)
+    d = features(V, n=400, seed=110)
+    r = run_ref(V, d, 2)
+    np.savez_compressed(OUT / "vocab_small.npz", k=V["k"], L=V["L"], parent=V["parent"], is_leaf=V["is_leaf"],
+                        vdesc=V["desc"], weight=V["weight"], desc=d, levelsup=2, word=r["word"], w=r["weight"],
+                        nid=r["nid"], bow_words=r["bw"][:r["nw"]], bow_values=r["bv"][:r["nw"]],
+                        fv_nodes=r["fn"][:r["nf"]], fv_ptr=r["fp"][:r["nf"] + 1], fv_feat=r["ff"][:r["fp"][r["nf"]]])
+    print("vocab", r["nw"], r["nf"])
+
+
 if __name__ == "__main__":
     OUT.mkdir(parents=True, exist_ok=True)
     gen_extract()
@@ -126,3 +156,5 @@ if __name__ == "__main__":
     gen_hamming()
     gen_lba()
     gen_pose()
+    gen_bow()
+    gen_vocab()
