@@ -416,6 +416,62 @@ __device__ inline int fast_arc(const uint8_t* t, int pitch, int fl)
     return max((fl & 1) ? dark : -1000, (fl & 2) ? -bright : -1000);
 }
 
+// Two candidates per lane (a, b) on packed fp16 halves: the 8-bit pixels
+// become the exact fp16 integers 1024 + p (bits 0x6400 | p), so the ring
+// differences d_k = v - p_k (|d| <= 255) are exact in fp16 and the 3-way
+// windows are single v_pk_minimum3_f16 / v_pk_maximum3_f16 instructions
+// (gfx950) for both candidates.  Returns max(dark, bright) per candidate,
+// the same value as fast_arc(..., 3).
+typedef _Float16 orbx_h2 __attribute__((ext_vector_type(2)));
+__device__ inline orbx_h2 h2_min3(orbx_h2 a, orbx_h2 b, orbx_h2 c)
+{
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ inline orbx_h2 h2_max3(orbx_h2 a, orbx_h2 b, orbx_h2 c)
+{
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ inline void fast_arc2(const uint8_t* t, int pa, int pb, int pitch, int& Sa, int& Sb)
+{
+    const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
+                         3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
+                         -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
+                         -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
+    const uint8_t* ta = t + pa;
+    const uint8_t* tb = t + pb;
+    const orbx_h2 v = __builtin_bit_cast(orbx_h2, ((uint32_t)ta[0] | ((uint32_t)tb[0] << 16)) | 0x64006400u);
+    orbx_h2 d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t w = ((uint32_t)ta[off[k]] | ((uint32_t)tb[off[k]] << 16)) | 0x64006400u;
+        d[k] = v - __builtin_bit_cast(orbx_h2, w);
+    }
+    orbx_h2 lo3[16], hi3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        lo3[k] = h2_min3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+        hi3[k] = h2_max3(d[k], d[(k + 1) & 15], d[(k + 2) & 15]);
+    }
+    orbx_h2 m9[16], x9[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        m9[k] = h2_min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
+        x9[k] = h2_max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
+    }
+    // dark = max_k m9[k], bright = min_k x9[k] (3-way trees)
+    orbx_h2 dk = h2_max3(m9[0], m9[1], m9[2]), br = h2_min3(x9[0], x9[1], x9[2]);
+#pragma unroll
+    for (int k = 3; k < 15; k += 2) {
+        dk = h2_max3(dk, m9[k], m9[k + 1]);
+        br = h2_min3(br, x9[k], x9[k + 1]);
+    }
+    dk = __builtin_elementwise_maximum(dk, m9[15]);
+    br = __builtin_elementwise_minimum(br, x9[15]);
+    const orbx_h2 r = __builtin_elementwise_maximum(dk, -br);
+    Sa = (int)(float)r.x;
+    Sb = (int)(float)r.y;
+}
+
 // One workgroup per (cell, frame).  LDS: the cell ROI with dword-aligned rows
 // (tile), its S' map (sm), and one candidate buffer per wave.
 //  1. compass pre-test, 4 pixels per thread: a 9-arc covers two adjacent
@@ -507,12 +563,23 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
         // per-wave ring of compass survivors (tile position | direction
         // flags << 16), scored 64 at a time with every lane busy
         int qh = 0, qt = 0;
-        auto score_batch = [&](uint32_t cw) {
-            const int pos = (int)(cw & 0xFFFF), fl = (int)(cw >> 16);
-            if (fl) {
-                const int S = fast_arc(tile + pos, P, fl) - 1;
-                sm[pos] = (uint8_t)(S >= tmin ? S : 0);
-            }
+        // two candidates per lane (packed fp16 arcs); cw = position |
+        // flags << 16, flags 0 = no candidate (a is filled before b)
+        auto score_pair = [&](uint32_t ca, uint32_t cb) {
+            if (!(ca >> 16)) return;
+            const int pa = (int)(ca & 0xFFFF);
+            const int pb = (cb >> 16) ? (int)(cb & 0xFFFF) : pa;
+            int Sa, Sb;
+            fast_arc2(tile, pa, pb, P, Sa, Sb);
+            Sa -= 1;
+            Sb -= 1;
+            sm[pa] = (uint8_t)(Sa >= tmin ? Sa : 0);
+            if (cb >> 16) sm[pb] = (uint8_t)(Sb >= tmin ? Sb : 0);
+        };
+        auto score_partial = [&]() {   // the qt - qh < 128 queued candidates
+            const int nq = qt - qh;
+            score_pair(lane < nq ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u,
+                       lane + 64 < nq ? cand[wv][(qh + 64 + lane) & (kCandRing - 1)] : 0u);
         };
         RowWalk cw_(wv * 64 + lane, kBlock, nqe);
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
@@ -564,8 +631,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             if (lane == 0) FP_ADD(10 + (tmin < 10), ntot);
             if (lane == 0) FP_ADD(12, 1);
 #endif
-            if (qt - qh + ntot > kCandRing) {   // rare (> 75 % survivors): drain the partial batch
-                score_batch(lane < qt - qh ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u);
+            if (qt - qh + ntot > kCandRing) {   // rare (> 50 % survivors): drain the partial batch
+                score_partial();
                 qh = qt;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -581,16 +648,16 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // score only full waves of candidates; the rest waits in the ring
-            while (qt - qh >= 64) {
-                score_batch(cand[wv][(qh + lane) & (kCandRing - 1)]);
-                qh += 64;
+            // score only full batches (two per lane); the rest waits in the ring
+            while (qt - qh >= 128) {
+                score_pair(cand[wv][(qh + lane) & (kCandRing - 1)], cand[wv][(qh + 64 + lane) & (kCandRing - 1)]);
+                qh += 128;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (qt > qh) score_batch(lane < qt - qh ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u);
+        if (qt > qh) score_partial();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
