@@ -503,7 +503,7 @@ __device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
 template <int kP>
-__global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
@@ -530,17 +530,23 @@ __global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int tile_pitc
     auto load_tile = [&]() {
         uint4* t16 = reinterpret_cast<uint4*>(tile32);
         const int n = hy * nq16;
+        // i / nq16 as a float product: (i + 1/2) / nq16 is at least 1/(2 nq16)
+        // from an integer and the product's error is < 2^-21 (i + 1) for
+        // i < 2^16, nq16 < 2^8 -- four integer divisions cost ~80 VALU
+        const float inv16 = 1.0f / (float)nq16;
+        auto row_of = [&](int i) { return (int)(((float)i + 0.5f) * inv16); };
         // four independent loads per round (named registers: an array here
         // was kept in scratch memory), then the LDS stores
         for (int u0 = 0; u0 < n; u0 += 4 * kBlock) {
             const int i0 = min(u0 + tid, n - 1), i1 = min(u0 + kBlock + tid, n - 1);
             const int i2 = min(u0 + 2 * kBlock + tid, n - 1), i3 = min(u0 + 3 * kBlock + tid, n - 1);
-            const int r0 = i0 / nq16, r1 = i1 / nq16, r2 = i2 / nq16, r3 = i3 / nq16;
+            const int r0 = row_of(i0), r1 = row_of(i1), r2 = row_of(i2), r3 = row_of(i3);
             const int c0 = i0 - r0 * nq16, c1 = i1 - r1 * nq16, c2 = i2 - r2 * nq16, c3 = i3 - r3 * nq16;
-            const uint4 v0 = *reinterpret_cast<const uint4*>(src + (size_t)r0 * L.stride + 16 * c0);
-            const uint4 v1 = *reinterpret_cast<const uint4*>(src + (size_t)r1 * L.stride + 16 * c1);
-            const uint4 v2 = *reinterpret_cast<const uint4*>(src + (size_t)r2 * L.stride + 16 * c2);
-            const uint4 v3 = *reinterpret_cast<const uint4*>(src + (size_t)r3 * L.stride + 16 * c3);
+            // 32-bit offsets from the uniform tile origin (saddr loads)
+            const uint4 v0 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r0 * L.stride + 16 * c0));
+            const uint4 v1 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r1 * L.stride + 16 * c1));
+            const uint4 v2 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r2 * L.stride + 16 * c2));
+            const uint4 v3 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r3 * L.stride + 16 * c3));
             t16[r0 * (P >> 4) + c0] = v0;
             t16[r1 * (P >> 4) + c1] = v1;
             t16[r2 * (P >> 4) + c2] = v2;
