@@ -807,8 +807,14 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     std::vector<uint8_t> all_st((size_t)eacc, 0);
     std::vector<LbaDev> devs(P);
     int r = ORBX_OK;
+    mark("setup");
+    struct HostCache {
+        std::vector<HostStruct> hs;
+    };
+    if (!ctx->lba_host) ctx->lba_host = std::make_shared<HostCache>();
+    std::vector<HostStruct>& hs = static_cast<HostCache*>(ctx->lba_host.get())->hs;
+    if ((int)hs.size() < P) hs.resize(P);
     for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
-        std::vector<HostStruct> hs(P);
         host_parallel(P, [&](int i) {
             build_struct(probs[i], pass == 0 ? nullptr : all_st.data() + offs[3 * i], hs[i]);
         });
@@ -997,6 +1003,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     ORBX_HIP_CHECK(hipMemcpyAsync(hb + o_all_bad, static_cast<uint8_t*>(ctx->scratch) + o_all_bad, (size_t)pacc,
                                   hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    mark("results copy");
     host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
         const double* pose = reinterpret_cast<const double*>(hb + pl[i].pose);
