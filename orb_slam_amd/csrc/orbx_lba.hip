@@ -100,6 +100,7 @@ __device__ inline unsigned long long lba_stamp()
 
 constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem
 constexpr int kLbaWaves = kLbaThreads / 64;
+constexpr int kSchurEdges = 8;                 // per-thread LDS edge table of the Schur pass (32 KB)
 
 
 
@@ -305,10 +306,20 @@ __device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j 
 
 // One Levenberg trial: Schur complement, LLT, back-substitution, update.
 // Returns false when the reduced system is not positive definite.
-__device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DScratch& sc)
+// per-thread edge table of the Schur pass (one allocation for both
+// instantiations below)
+__shared__ int2 s_edges[kLbaThreads][kSchurEdges];
+
+// kLds: the reduced system lives in the dynamic LDS block (its accesses then
+// compile to ds_* instructions instead of flat ones), else in P.S / P.bs.
+template <bool kLds>
+__device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
 {
+    extern __shared__ __attribute__((aligned(16))) double s_S[];
     LBA_T0();
     const int n = P.dim_p;
+    double* S = kLds ? s_S : P.S;
+    double* bs = kLds ? s_S + (size_t)n * n : P.bs;
     // S <- 0, then the diagonal blocks Hpp + lambda I (full, symmetric); bs <- bp
     for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;
     __syncthreads();
@@ -349,36 +360,49 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
         double* dl = P.dl + 12 * l;
 #pragma unroll
         for (int i = 0; i < 12; i++) dl[i] = d[i];
-        const int q0 = P.lc_ptr[l], q1 = P.lc_ptr[l + 1];
-        for (int qi = q0; qi < q1; qi++) {
-            const int ai = P.lc_idx[qi], i1 = P.e_ph[ai];
-            double wd[18];   // W_i Dinv (6x3)
-            double wi[18];
-            {
-                const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)ai);
-#pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    const double2 v = src[k];
-                    wi[2 * k] = v.x;
-                    wi[2 * k + 1] = v.y;
-                }
+        const int q0 = P.lc_ptr[l], q1 = P.lc_ptr[l + 1], k = q1 - q0;
+        // The point's free-pose edges (edge, pose block) go to this thread's
+        // LDS row first, so the pair loop below waits on one global load per
+        // pair (the edge's Hpl block, prefetched one pair ahead) instead of a
+        // chain of three.  Points with more than kSchurEdges such edges read
+        // the lists from global memory.
+        int2* te = s_edges[threadIdx.x];
+        const bool tab = k <= kSchurEdges;
+        if (tab)
+            for (int j = 0; j < k; j++) {
+                const int a = P.lc_idx[q0 + j];
+                te[j] = make_int2(a, P.e_ph[a]);
             }
+        auto edge_at = [&](int j) { return tab ? te[j] : make_int2(P.lc_idx[q0 + j], P.e_ph[P.lc_idx[q0 + j]]); };
+        auto load_hpl = [&](int a, double2 (&v)[9]) {
+            const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)a);
+#pragma unroll
+            for (int i = 0; i < 9; i++) v[i] = src[i];
+        };
+        for (int qi = 0; qi < k; qi++) {
+            const int2 ei = edge_at(qi);
+            const int i1 = ei.y;
+            double2 cur[9];
+            load_hpl(ei.x, cur);   // W_i, also the first pair's W_j (qj == qi)
+            double wd[18];         // W_i Dinv (6x3)
 #pragma unroll
             for (int r = 0; r < 6; r++) {
-                const double b0 = wi[r * 3], b1 = wi[r * 3 + 1], b2 = wi[r * 3 + 2];
+                const double b0 = (r & 1) ? cur[(3 * r) >> 1].y : cur[(3 * r) >> 1].x;
+                const double b1 = (r & 1) ? cur[(3 * r + 1) >> 1].x : cur[(3 * r + 1) >> 1].y;
+                const double b2 = (r & 1) ? cur[(3 * r + 2) >> 1].y : cur[(3 * r + 2) >> 1].x;
 #pragma unroll
                 for (int c = 0; c < 3; c++) wd[r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
                 atomicAdd(&bs[6 * i1 + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
             }
-            for (int qj = qi; qj < q1; qj++) {
-                const int aj = P.lc_idx[qj], i2 = P.e_ph[aj];
+            for (int qj = qi; qj < k; qj++) {
+                const int i2 = qj == qi ? i1 : edge_at(qj).y;
+                double2 nxt[9];
+                if (qj + 1 < k) load_hpl(edge_at(qj + 1).x, nxt);
                 double bj[18];
-                const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)aj);
 #pragma unroll
-                for (int k = 0; k < 9; k++) {
-                    const double2 v = src[k];
-                    bj[2 * k] = v.x;
-                    bj[2 * k + 1] = v.y;
+                for (int i = 0; i < 9; i++) {
+                    bj[2 * i] = cur[i].x;
+                    bj[2 * i + 1] = cur[i].y;
                 }
 #pragma unroll
                 for (int r = 0; r < 6; r++)
@@ -386,8 +410,15 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
                     for (int c = 0; c < 6; c++) {
                         if (i1 == i2 && c < r) continue;
                         const double v = wd[r * 3] * bj[c * 3] + wd[r * 3 + 1] * bj[c * 3 + 1] + wd[r * 3 + 2] * bj[c * 3 + 2];
+#ifdef LBA_EXP_NOATOMIC
+                        S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] -= v;
+#else
                         atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
+#endif
                     }
+                if (qj + 1 < k)
+#pragma unroll
+                    for (int i = 0; i < 9; i++) cur[i] = nxt[i];
             }
         }
     }
@@ -466,7 +497,6 @@ __device__ bool trial_solve(LbaDev& P, double lambda, double* S, double* bs, DSc
 // OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
 __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
 {
-    extern __shared__ __attribute__((aligned(16))) double s_S[];
     __shared__ DScratch sc;
     LbaDev& P = probs[blockIdx.x];
     if (P.status != kRunning || P.abort) return;
@@ -476,8 +506,6 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
     }
     const int n = P.dim_p;
     const bool in_lds = n * n + n <= lds_S_cap;
-    double* S = in_lds ? s_S : P.S;
-    double* bsv = in_lds ? s_S + (size_t)n * n : P.bs;
     LBA_T0();
     double currentChi = compute_errors(P, sc);
     const double iniChi = currentChi;
@@ -505,7 +533,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose_bk[i] = P.pose[i];
         for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point_bk[i] = P.point[i];
         __syncthreads();
-        const bool ok2 = trial_solve(P, lambda, S, bsv, sc);
+        const bool ok2 = in_lds ? trial_solve<true>(P, lambda, sc) : trial_solve<false>(P, lambda, sc);
         if (ok2) {
             for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
             for (int item = threadIdx.x; item < P.nL * 3; item += kLbaThreads) {
@@ -715,7 +743,8 @@ struct Packer {
     }
 };
 
-constexpr int kLdsSCap = (144 * 1024) / 8;   // doubles of LDS for the reduced system
+// doubles of LDS for the reduced system (160 KB less the Schur edge table)
+constexpr int kLdsSCap = (160 * 1024 - kLbaThreads * kSchurEdges * 8 - 1024) / 8;
 
 }  // namespace
 

@@ -1,0 +1,38 @@
+"""Local BA kernel phase breakdown (diagnostic build): s_memtime cycles of
+block 0 per phase, summed over a c5-sized batch solve.
+Build: python -m orb_slam_amd.build -DORBX_LBA_PROFILE --out=orb_slam_amd/liborbx_lbaprof.so
+Run:   ORBX_LIBRARY=orb_slam_amd/liborbx_lbaprof.so python3 tools/lba_phases.py"""
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import orb_slam_amd as ox  # noqa: E402
+from orb_slam_amd import synth_ba as sb  # noqa: E402
+
+P = 64
+uniq = [sb.make_problem(n_kf=20, n_points=2000, seed=5000 + i) for i in range(8)]
+cps = [sb.to_ctypes(uniq[i % 8]) for i in range(P)]
+arr = (sb.BAProblem * P)(*[c[0] for c in cps])
+es = [np.zeros(c[0].n_edges, np.uint8) for c in cps]
+pb = [np.zeros(c[0].n_points, np.uint8) for c in cps]
+esp = (ctypes.c_void_p * P)(*[e.ctypes.data for e in es])
+pbp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in pb])
+ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
+L = ox.lib()
+L.orbx_debug_lba_prof.argtypes = [ctypes.c_void_p]
+before = (ctypes.c_ulonglong * 16)()
+L.orbx_debug_lba_prof(before)
+st = (sb.BAStats * P)()
+assert L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, esp, pbp, st) == 0
+after = (ctypes.c_ulonglong * 16)()
+L.orbx_debug_lba_prof(after)
+d = [a - b for a, b in zip(after, before)]
+names = {6: "errors (iteration start)", 7: "linearize", 1: "S init", 2: "Schur complement", 3: "dense LLT",
+         4: "substitution", 5: "landmark back-subst", 8: "errors (trial)"}
+tot = sum(d[k] for k in names)
+for k, nm in names.items():
+    print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / max(tot, 1):5.1f} %)")
+print("iterations", list(st[0].iterations), "trials", list(st[0].levenberg_trials), "n_edges", cps[0][0].n_edges)
