@@ -410,11 +410,7 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
                     for (int c = 0; c < 6; c++) {
                         if (i1 == i2 && c < r) continue;
                         const double v = wd[r * 3] * bj[c * 3] + wd[r * 3 + 1] * bj[c * 3 + 1] + wd[r * 3 + 2] * bj[c * 3 + 2];
-#ifdef LBA_EXP_NOATOMIC
-                        S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] -= v;
-#else
                         atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
-#endif
                     }
                 if (qj + 1 < k)
 #pragma unroll
