@@ -57,6 +57,13 @@ struct PoseOut {
 };
 
 constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
+// Edges per frame kept in LDS (6 floats + the outlier flag, 25 B each):
+// 4 frames x 800 edges = 80 KB per workgroup, 2 workgroups per CU -- the
+// occupancy the kernel's 242 VGPRs allow anyway.  The passes over the edges
+// (one per LM iteration, one per trial, one per robust round) then read LDS
+// instead of re-fetching the frame from HBM; edges past the first 800 are
+// read from global memory.
+constexpr int kPoseLdsEdges = 800;
 
 // Wave sum whose result is the same double on every lane: DPP butterflies
 // inside each row of 16 (xor 1, xor 2 by quad_perm; the half-row and row
@@ -285,7 +292,41 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
     const float* py = ed.py + e0;
     const float* pz = ed.pz + e0;
     uint8_t* flag = eflag + e0;
-    for (int a = lane; a < nE; a += 64) flag[a] = 0;
+    __shared__ float s_e[kPoseThreads / 64][6][kPoseLdsEdges];
+    __shared__ uint8_t s_f[kPoseThreads / 64][kPoseLdsEdges];
+    const int wq = threadIdx.x >> 6;
+    const int nL = min(nE, kPoseLdsEdges);
+    float* lox = s_e[wq][0];
+    float* loy = s_e[wq][1];
+    float* lis = s_e[wq][2];
+    float* lpx = s_e[wq][3];
+    float* lpy = s_e[wq][4];
+    float* lpz = s_e[wq][5];
+    uint8_t* lfl = s_f[wq];
+#pragma unroll 1
+    for (int a = lane; a < nL; a += 64) {
+        const float v0 = ox[a], v1 = oy[a], v2 = isg[a], v3 = px[a], v4 = py[a], v5 = pz[a];
+        lox[a] = v0;
+        loy[a] = v1;
+        lis[a] = v2;
+        lpx[a] = v3;
+        lpy[a] = v4;
+        lpz[a] = v5;
+        lfl[a] = 0;
+    }
+    for (int a = nL + lane; a < nE; a += 64) flag[a] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the frame's edges: LDS part [0, nL), global part [nL, nE)
+    auto for_edges = [&](auto&& body) {
+#pragma unroll 1
+        for (int a = lane; a < nL; a += 64)
+            if (!lfl[a]) body(lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a]);
+#pragma unroll 1
+        for (int a = nL + lane; a < nE; a += 64)
+            if (!flag[a]) body(ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
+    };
 
     PoseOut& out = outs[prob];
     int not_posdef = 0, rounds = 0;
@@ -310,13 +351,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                 for (int k = 0; k < 21; k++) h[k] = 0;
 #pragma unroll
                 for (int k = 0; k < 6; k++) bv[k] = 0;
-        #pragma unroll 1
-        for (int a = lane; a < nE; a += 64) {
-                    if (flag[a]) continue;
-                    const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
-                    const double s = (double)isg[a];
+                for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
+                    const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
+                    const double s = (double)fis;
                     double pc[3], er0, er1;
-                    pose_edge_error(pose, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+                    pose_edge_error(pose, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
                     const double c2 = er0 * (s * er0) + er1 * (s * er1);
                     double rho0, rho1;
                     huber2(c2, delta, rho0, rho1);
@@ -349,7 +388,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                     for (int i = 0; i < 6; i++)
 #pragma unroll
                         for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
-                }
+                });
                 double currentChi = wave_sum_uniform(chi);
                 const double iniChi = currentChi;
 #pragma unroll
@@ -384,17 +423,15 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                     }
                     // computeActiveErrors at the trial estimate
                     double tchi = 0;
-            #pragma unroll 1
-        for (int a = lane; a < nE; a += 64) {
-                        if (flag[a]) continue;
-                        const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
-                        const double s = (double)isg[a];
+                    for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
+                        const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
+                        const double s = (double)fis;
                         double pc[3], er0, er1;
-                        pose_edge_error(tp, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+                        pose_edge_error(tp, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
                         double rho0, rho1;
                         huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
                         tchi += rho0;
-                    }
+                    });
                     double tempChi = wave_sum_uniform(tchi);
 #pragma unroll
                     for (int i = 0; i < 7; i++) errpose[i] = tp[i];
@@ -430,13 +467,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
         // outlier classification (src/Optimizer.cc:243-265)
         int bad = 0, act = 0;
         const double th = (double)chi2th;
-#pragma unroll 1
-        for (int a = lane; a < nE; a += 64) {
-            const uint8_t f = flag[a];
-            const double X[3] = {(double)px[a], (double)py[a], (double)pz[a]};
-            const double s = (double)isg[a];
+        auto classify = [&](uint8_t f, float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
+            const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
+            const double s = (double)fis;
             double pc[3], er0, er1;
-            pose_edge_error(f ? pose : errpose, X, (double)ox[a], (double)oy[a], cam, pc, er0, er1);
+            pose_edge_error(f ? pose : errpose, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
             const double c2 = er0 * (s * er0) + er1 * (s * er1);
             uint8_t nf = f;
             if (c2 > th) {
@@ -446,8 +481,12 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                 nf = 0;
             }
             act += nf == 0;
-            flag[a] = nf;
-        }
+            return nf;
+        };
+#pragma unroll 1
+        for (int a = lane; a < nL; a += 64) lfl[a] = classify(lfl[a], lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a]);
+#pragma unroll 1
+        for (int a = nL + lane; a < nE; a += 64) flag[a] = classify(flag[a], ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
         nBadOut = wave_sum_int(bad);
         n_active = wave_sum_int(act);
         if (lane == 0) {
@@ -458,6 +497,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
         }
         if (nE < 10) break;
     }
+    for (int a = lane; a < nL; a += 64) flag[a] = lfl[a];   // mvbOutlier of the LDS part
     if (lane == 0) {
         double R[9];
         qmat(Q{pose[0], pose[1], pose[2], pose[3]}, R);
