@@ -338,21 +338,34 @@ KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": "k_pyr_resize", "fast": "k_fa
 
 
 def pmc_traffic(workload, name):
-    """HBM bytes per launch of kernel `name` from the committed PMC summary
-    of this bench command (profiles/r01_<workload>_pmc_hbm.json, written by
-    tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes of
-    `bench.py --no-isolated`): FETCH_SIZE x2 (gfx950 wide-read correction,
-    MI355X_MICROARCH.md HBM section) + WRITE_SIZE.  None when absent."""
-    path = Path(__file__).resolve().parent / "profiles" / f"r01_{workload}_pmc_hbm.json"
+    """HBM bytes per launch of kernel `name` from the newest committed PMC
+    summary of this bench command (profiles/rNN_<workload>_pmc_hbm.json,
+    written by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE
+    passes of `bench.py --no-isolated`).  `traffic` = FETCH_SIZE x2 (gfx950
+    wide-read correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE;
+    `traffic_raw` = FETCH_SIZE + WRITE_SIZE as counted.  The profile names the
+    liborbx.so it measured (SHA-256): when that is not the library loaded now,
+    the numbers describe another build and `traffic` is null."""
+    import hashlib
+    cands = sorted((Path(__file__).resolve().parent / "profiles").glob(f"r*_{workload}_pmc_hbm.json"))
     sym = KERNEL_SYMBOL.get(name)
-    if not path.exists() or not sym:
+    if not cands or not sym:
         return {"traffic": None}
+    path = cands[-1]
     summary = json.loads(path.read_text())
+    meta = summary.pop("_meta", {})
     hits = [v for k, v in summary.items() if sym in k]
     if not hits:
         return {"traffic": None}
+    src = f"profiles/{path.name} (per dispatch)"
+    lib_sha = hashlib.sha256(Path(ox.LIB_PATH).read_bytes()).hexdigest()
+    if meta.get("liborbx_sha256") != lib_sha:
+        return {"traffic": None, "traffic_source": src,
+                "traffic_note": "profile snapshot of another liborbx.so build (SHA-256 differs): not reported"}
     return {"traffic": round(sum(h["hbm_bytes_fetch_x2"] for h in hits) / len(hits)),
-            "traffic_source": f"profiles/{path.name} (FETCH_SIZE x2 + WRITE_SIZE, per dispatch)"}
+            "traffic_raw": round(sum(h["hbm_bytes_raw"] for h in hits) / len(hits)),
+            "traffic_source": src + ", FETCH_SIZE x2 + WRITE_SIZE (traffic_raw: FETCH_SIZE + WRITE_SIZE), "
+                                    f"build {meta.get('git_head')}"}
 
 
 def timed(args, ctx, step, dist, names, only=None):
@@ -446,10 +459,16 @@ def main():
         if roof_iso:
             out["roofline_isolated"] = roof_iso
         if args.workload == "pose" and roof.get("avg_launch_ms"):
+            # PoseOptimization is FP64-VALU bound (its edges are read from HBM
+            # once and kept in LDS): the FP64 roofline is the headline one, the
+            # HBM figure is kept beside it
             fl = check["fp64_flops_per_frame"] * units["pose"] / (roof["avg_launch_ms"] / 1e3) / 1e12
-            out["roofline_fp64"] = {"bound": "fp64-valu", "achieved": round(fl, 3), "peak": FP64_PEAK_TFLOPS,
-                                    "unit": "TFLOP/s", "frac": round(fl / FP64_PEAK_TFLOPS, 5),
-                                    "flops_per_frame": check["fp64_flops_per_frame"]}
+            out["roofline_hbm"] = roof
+            out["roofline"] = {"bound": "fp64-valu", "achieved": round(fl, 3), "peak": FP64_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": round(fl / FP64_PEAK_TFLOPS, 5),
+                               "traffic": roof.get("traffic"), "kernel": roof["kernel"],
+                               "flops_per_frame": check["fp64_flops_per_frame"],
+                               "avg_launch_ms": roof["avg_launch_ms"]}
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)

@@ -17,6 +17,10 @@ CSRC = PKG / "csrc"
 OBJ = PKG / "build"
 LIB = PKG / "liborbx.so"
 ARCH = os.environ.get("ORBX_ARCH", "gfx950")
+if ARCH != "gfx950":
+    # the kernels are written for gfx950 only: 160 KB of LDS per CU (the pose
+    # and local-BA kernels size their LDS for it), v_pk_minimum3_f16, 32-lane SIMDs
+    raise RuntimeError(f"ORBX_ARCH={ARCH}: liborbx targets gfx950 (MI355X) only")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
           "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value",

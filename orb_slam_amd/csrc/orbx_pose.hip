@@ -10,9 +10,13 @@
 //
 // Mapping: one wavefront per frame, four frames per 256-thread workgroup,
 // the whole four-round robust optimisation (up to 32 LM iterations of up to
-// 10 trials) in ONE launch, no LDS and no barriers.  Lanes stride the frame's
-// edges (edge a on lane a % 64 for the whole run, so an edge's level flag is
-// lane-private); per LM iteration one fused pass computes the errors, the
+// 10 trials) in ONE launch, no workgroup barriers.  The frame's first
+// kPoseLdsEdges edges are copied into the wavefront's LDS area once (a
+// wavefront-scope fence, no barrier: each wave reads only its own area) and
+// every pass reads them there; edges past them are read from global memory.
+// Lanes stride the edges: edge a < nL on lane a % 64, edge a >= nL on lane
+// (a - nL) % 64, the same lane for the whole run, so an edge's level
+// (outlier) flag is lane-private.  Per LM iteration one fused pass computes the errors, the
 // robust chi2, the Jacobians and the 21 lower entries of H plus b; per trial
 // one pass computes the trial errors.  Sums are wave reductions whose result
 // is bitwise identical on every lane, so the LDLT, the exp-map update and
@@ -58,12 +62,14 @@ struct PoseOut {
 
 constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
 // Edges per frame kept in LDS (6 floats + the outlier flag, 25 B each):
-// 4 frames x 800 edges = 80 KB per workgroup, 2 workgroups per CU -- the
-// occupancy the kernel's 242 VGPRs allow anyway.  The passes over the edges
+// 4 frames x 800 edges = 80 KB per workgroup, 2 workgroups per CU of
+// gfx950's 160 KB -- the occupancy the kernel's 250 VGPRs allow anyway.  The passes over the edges
 // (one per LM iteration, one per trial, one per robust round) then read LDS
 // instead of re-fetching the frame from HBM; edges past the first 800 are
 // read from global memory.
 constexpr int kPoseLdsEdges = 800;
+static_assert((kPoseThreads / 64) * kPoseLdsEdges * (6 * sizeof(float) + 1) <= 80 * 1024,
+              "two pose workgroups per CU need <= 80 KB of LDS each (gfx950: 160 KB per CU)");
 
 // Wave sum whose result is the same double on every lane: DPP butterflies
 // inside each row of 16 (xor 1, xor 2 by quad_perm; the half-row and row

@@ -2,13 +2,36 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ based).
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
-the bytes of a wide coalesced streaming read; reported here both raw and x2.
-usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv> [trace stats csv]
+the bytes of a wide coalesced streaming read (16 B per lane); other access
+widths are uncalibrated.  Both figures are kept: hbm_bytes_raw (FETCH + WRITE
+as counted) and hbm_bytes_fetch_x2 (the streaming-read correction).  For a
+kernel whose reads are not wide coalesced streams (gathers, scattered 8-B
+rows, atomics) the truth lies between the two.
+The summary records the build it profiled (`_meta`: git HEAD and the SHA-256
+of orb_slam_amd/liborbx.so as shipped to the GPU box), so bench.py can refuse
+a stale profile.
+usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv>
 """
 import csv
+import hashlib
 import json
+import subprocess
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def build_id():
+    lib = ROOT / "orb_slam_amd" / "liborbx.so"
+    sha = hashlib.sha256(lib.read_bytes()).hexdigest() if lib.exists() else None
+    try:
+        head = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True).stdout.strip() or None
+    except OSError:
+        head = None
+    return {"git_head": head, "liborbx_sha256": sha}
 
 
 def load(path, counter):
@@ -23,7 +46,7 @@ def load(path, counter):
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
-    out = {}
+    out = {"_meta": build_id()}
     for k in sorted(set(fetch) | set(write)):
         if k.startswith("__amd"):
             continue
