@@ -386,43 +386,14 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
 // exactly S (OpenCV 2.4 fast.cpp / fast_score.cpp).  A pixel whose compass
 // pre-test passes in one direction only has S = that direction's arc - 1.
 // ---------------------------------------------------------------------------
-// Best 9-arc minima of d_k = v - p_k ("dark" arc, fl bit 0) and of -d_k
-// ("bright" arc, fl bit 1), both from one set of differences: the bright arc
-// is -(min over 9-arcs of the 9-maximum of d).  Returns the larger of the
-// requested directions' values.
-__device__ inline int fast_arc(const uint8_t* t, int pitch, int fl)
-{
-    const int off[16] = {3 * pitch,      1 + 3 * pitch, 2 + 2 * pitch,  3 + pitch,
-                         3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
-                         -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
-                         -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
-    const int v = t[0];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)t[off[k]];
-    // 9-minimum / 9-maximum = min / max of three consecutive 3-windows
-    int lo3[16], hi3[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        lo3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-        hi3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
-    }
-    int dark = -1000, bright = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        dark = max(dark, min(min(lo3[k], lo3[(k + 3) & 15]), lo3[(k + 6) & 15]));
-        bright = min(bright, max(max(hi3[k], hi3[(k + 3) & 15]), hi3[(k + 6) & 15]));
-    }
-    return max((fl & 1) ? dark : -1000, (fl & 2) ? -bright : -1000);
-}
-
 // Two candidates per lane (a, b) on packed fp16 halves: the 8-bit pixels
 // become the exact fp16 integers 1024 + p (bits 0x6400 | p), so the ring
 // differences d_k = v - p_k (|d| <= 255) are exact in fp16 and the 3-way
 // windows are single v_pk_minimum3_f16 / v_pk_maximum3_f16 instructions
-// (gfx950) for both candidates.  Returns max(dark, bright) per candidate,
-// the same value as fast_arc(..., 3).
+// (gfx950) for both candidates.  Returns max(dark, bright) (= S + 1) per
+// candidate.
 typedef _Float16 orbx_h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short orbx_u16x2 __attribute__((ext_vector_type(2)));
 __device__ inline orbx_h2 h2_min3(orbx_h2 a, orbx_h2 b, orbx_h2 c)
 {
     return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
@@ -437,13 +408,26 @@ __device__ inline void fast_arc2(const uint8_t* t, int pa, int pb, int pitch, in
                          3,              3 - pitch,     2 - 2 * pitch,  1 - 3 * pitch,
                          -3 * pitch,     -1 - 3 * pitch, -2 - 2 * pitch, -3 - pitch,
                          -3,             -3 + pitch,    -2 + 2 * pitch, -1 + 3 * pitch};
-    const uint8_t* ta = t + pa;
-    const uint8_t* tb = t + pb;
-    const orbx_h2 v = __builtin_bit_cast(orbx_h2, ((uint32_t)ta[0] | ((uint32_t)tb[0] << 16)) | 0x64006400u);
+    // bases at the ring's top-left corner: every offset is a non-negative
+    // ds_read immediate (no address arithmetic per ring point)
+    const int o = 3 * pitch + 3;
+    int ba = pa - o, bb = pb - o;
+    asm("" : "+v"(ba), "+v"(bb));   // opaque: keeps the constant offsets out of the bases
+    const uint8_t* ta = t + ba;
+    const uint8_t* tb = t + bb;
+    // (a, b) byte pairs assembled as 16-bit halves (ds_read_u8_d16 /
+    // _d16_hi), then the fp16 exponent bits
+    auto pair = [&](int k) {
+        orbx_u16x2 pv;
+        pv.x = ta[k];
+        pv.y = tb[k];
+        return __builtin_bit_cast(uint32_t, pv) | 0x64006400u;
+    };
+    const orbx_h2 v = __builtin_bit_cast(orbx_h2, pair(o));
     orbx_h2 d[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const uint32_t w = ((uint32_t)ta[off[k]] | ((uint32_t)tb[off[k]] << 16)) | 0x64006400u;
+        const uint32_t w = pair(off[k] + o);
         d[k] = v - __builtin_bit_cast(orbx_h2, w);
     }
     orbx_h2 lo3[16], hi3[16];
@@ -472,13 +456,18 @@ __device__ inline void fast_arc2(const uint8_t* t, int pa, int pb, int pitch, in
     Sb = (int)(float)r.y;
 }
 
-// One workgroup per (cell, frame).  LDS: the cell ROI with dword-aligned rows
-// (tile), its S' map (sm), and one candidate buffer per wave.
+// One workgroup per (cell, frame).  LDS (dynamic): the cell ROI with
+// 16-byte aligned rows (tile, kept intact for the threshold-7 rescore), its
+// S' map (sm), and two bitmaps: `nz` (one bit per tile dword whose S' word
+// is nonzero) and `kept` (one bit per tile byte that survives NMS).
 //  1. compass pre-test, 4 pixels per thread: a 9-arc covers two adjacent
 //     compass points, so S >= tmin needs d > tmin (or < -tmin) on both;
-//     survivors are compacted per wave and scored with all lanes busy;
-//  2. non-max suppression, 4 pixels per thread (result kept over `tile`);
-//  3. raster-order compaction of the corners at the chosen threshold.
+//     survivors are compacted per wave and scored with all lanes busy; a
+//     nonzero S' sets its dword's `nz` bit;
+//  2. non-max suppression on the `nz` dwords only (listed with one block
+//     scan), kept pixels set their `kept` bit;
+//  3. raster-order compaction of the `kept` bitmap (tile byte order is
+//     raster order), one block scan over ~2 bitmap words per thread.
 // ---------------------------------------------------------------------------
 __device__ inline int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFF); }
 
@@ -493,22 +482,28 @@ __device__ inline uint32_t pk_max16(uint32_t a, uint32_t b)
     return __builtin_bit_cast(uint32_t,
                               __builtin_elementwise_max(__builtin_bit_cast(orbx_s16x2, a), __builtin_bit_cast(orbx_s16x2, b)));
 }
-
-// byte k (0..11) of the 12-byte window lo|mid|hi
-__device__ inline int byte12(uint32_t lo, uint32_t mid, uint32_t hi, int k)
+// bytes (b0, b2) or (b1, b3) of w as the packed fp16 pair (1024 + b, 1024 + b')
+// (exact integers): one v_perm with the 0x64 exponent bytes from k64
+__device__ inline orbx_h2 h2_bytes(uint32_t w, uint32_t k64, uint32_t sel)
 {
-    return k < 4 ? byte_of(lo, k) : (k < 8 ? byte_of(mid, k - 4) : byte_of(hi, k - 8));
+    return __builtin_bit_cast(orbx_h2, __builtin_amdgcn_perm(k64, w, sel));
 }
+
+// Dynamic LDS of a FAST workgroup for tiles of `bytes` (host and device).
+__host__ __device__ constexpr int fast_tile_bytes(int hy_max, int pitch) { return (hy_max * pitch + 511) & ~511; }
+__host__ __device__ constexpr int fast_lds_bytes(int tile_bytes) { return 2 * tile_bytes + tile_bytes / 8 + tile_bytes / 32; }
 
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
 template <int kP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_fast_cells(ExtractArgs a, int tile_pitch_bytes)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_fast_cells(ExtractArgs a, int tile_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratch bs;
     constexpr int kCandRing = 256;           // per-wave ring (a full iteration's 256 fit after a drain)
-    __shared__ uint32_t cand[kWaves][kCandRing];
+    constexpr int kUnitCap = kWaves * kCandRing * 2;   // u16 NMS unit list aliasing the rings
+    __shared__ __attribute__((aligned(16))) uint32_t cand[kWaves][kCandRing];
+    uint16_t* ulist = reinterpret_cast<uint16_t*>(&cand[0][0]);
     const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
@@ -523,11 +518,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const int P = kP ? kP : 16 * nq16, nq = P >> 2;     // tile pitch, dwords per row
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
     uint8_t* tile = smem;
-    uint8_t* sm = smem + tile_pitch_bytes;
+    uint8_t* sm = smem + tile_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
+    uint32_t* kept = reinterpret_cast<uint32_t*>(sm + tile_bytes);               // bit per tile byte
+    uint32_t* nz = reinterpret_cast<uint32_t*>(sm + tile_bytes + tile_bytes / 8);  // bit per tile dword
     FP_T0();
-    auto load_tile = [&]() {
+    {
         uint4* t16 = reinterpret_cast<uint4*>(tile32);
         const int n = hy * nq16;
         // i / nq16 as a float product: (i + 1/2) / nq16 is at least 1/(2 nq16)
@@ -552,11 +549,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             t16[r2 * (P >> 4) + c2] = v2;
             t16[r3 * (P >> 4) + c3] = v3;
         }
+    }
+    // S' (0 where not scored) and both bitmaps start at zero (they are
+    // contiguous: tile_bytes * (1 + 1/8 + 1/32), a multiple of 16)
+    const int clear16 = (tile_bytes + tile_bytes / 8 + tile_bytes / 32) >> 4;
+    auto clear_maps = [&]() {
+        for (int i = tid; i < clear16; i += kBlock) reinterpret_cast<uint4*>(sm32)[i] = make_uint4(0, 0, 0, 0);
     };
-    load_tile();
-    // S' is 0 outside the interior rows [3, hy-4] and outside the dwords
-    // that hold interior columns; the interior units are rewritten below
-    for (int i = tid; i < hy * (P >> 4); i += kBlock) reinterpret_cast<uint4*>(sm32)[i] = make_uint4(0, 0, 0, 0);
+    clear_maps();
     __syncthreads();
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
     const int q0 = c_lo >> 2, nqe = (c_hi >> 2) - q0 + 1; // dwords holding them
@@ -564,13 +564,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const int m_first = 0xF & ~((1 << (c_lo & 3)) - 1);  // pixels j >= c_lo & 3 of dword q0
     const int m_last = (1 << ((c_hi & 3) + 1)) - 1;      // pixels j <= c_hi & 3 of the last dword
     const int nunits = (hy - 6) * nqe;
+    const uint32_t k64 = 0x64646464u;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {
-        // per-wave ring of compass survivors (tile position | direction
-        // flags << 16), scored 64 at a time with every lane busy
+        // per-wave ring of compass survivors (tile position | 3 << 16),
+        // scored 128 at a time (two per lane) with every lane busy
         int qh = 0, qt = 0;
-        // two candidates per lane (packed fp16 arcs); cw = position |
-        // flags << 16, flags 0 = no candidate (a is filled before b)
+        auto set_nz = [&](int p) { atomicOr(&nz[p >> 7], 1u << ((p >> 2) & 31)); };
+        // cw = position | flags << 16, flags 0 = no candidate (a is filled before b)
         auto score_pair = [&](uint32_t ca, uint32_t cb) {
             if (!(ca >> 16)) return;
             const int pa = (int)(ca & 0xFFFF);
@@ -579,14 +580,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             fast_arc2(tile, pa, pb, P, Sa, Sb);
             Sa -= 1;
             Sb -= 1;
-            sm[pa] = (uint8_t)(Sa >= tmin ? Sa : 0);
-            if (cb >> 16) sm[pb] = (uint8_t)(Sb >= tmin ? Sb : 0);
+            if (Sa >= tmin) {
+                sm[pa] = (uint8_t)Sa;
+                set_nz(pa);
+            }
+            if ((cb >> 16) && Sb >= tmin) {
+                sm[pb] = (uint8_t)Sb;
+                set_nz(pb);
+            }
         };
         auto score_partial = [&]() {   // the qt - qh < 128 queued candidates
-            const int nq = qt - qh;
-            score_pair(lane < nq ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u,
-                       lane + 64 < nq ? cand[wv][(qh + 64 + lane) & (kCandRing - 1)] : 0u);
+            const int nq_ = qt - qh;
+            score_pair(lane < nq_ ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u,
+                       lane + 64 < nq_ ? cand[wv][(qh + 64 + lane) & (kCandRing - 1)] : 0u);
         };
+        // pass <=> max(v - A, B - v) >= tmin + 1 with A = min of the four
+        // adjacent compass-pair maxima, B = max of the pair minima (exact
+        // on the fp16 integers 1024 + p; the sign bit of the difference
+        // is clear exactly when the test passes)
+        const orbx_h2 T1 = {(_Float16)(tmin + 1), (_Float16)(tmin + 1)};
         RowWalk cw_(wv * 64 + lane, kBlock, nqe);
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
             const int u = u0 + lane;
@@ -595,35 +607,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             if (u < nunits) {
                 const uint32_t* row = tile32 + r * nq + q;
                 const uint32_t mid = row[0];
-                const uint32_t lo = q > 0 ? row[-1] : 0u, hi = q + 1 < nq ? row[1] : 0u;
+                // row[-1] / row[1] past the row ends are the neighbouring rows'
+                // dwords (r is an interior row): only pixels outside the
+                // interior columns read them, and those are masked below
+                const uint32_t lo = row[-1], hi = row[1];
                 const uint32_t up = row[-3 * nq], dn = row[3 * nq];
-                // 4 pixels at once: even / odd bytes as two u16x2 halves, packed
-                // 16-bit arithmetic; a lane's sign bit set = "test fails"
+                // 4 pixels at once: even / odd bytes as two packed fp16 halves
                 const uint32_t p4w = __builtin_amdgcn_alignbyte(hi, mid, 3);    // bytes j+3
                 const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
-                const uint32_t T1 = (uint32_t)(tmin + 1) * 0x00010001u;
-                const uint32_t NT1 = (uint32_t)(-(tmin + 1) & 0xFFFF) * 0x00010001u;
-                // A pixel whose compass test fails in one direction has that
-                // direction's 9-arc minimum <= tmin, so scoring both arcs for
-                // every survivor gives the same S' (no direction flags needed)
-                uint32_t okw[2];   // [half] sign bits of pixels passing either test
-    #pragma unroll
+                uint32_t okw[2];   // [half] sign bits of pixels failing both tests
+#pragma unroll
                 for (int hf = 0; hf < 2; hf++) {
-                    const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;   // bytes 1,3 or 0,2 -> u16x2
-                    const uint32_t v = __builtin_amdgcn_perm(0u, mid, sel);
-                    const uint32_t pk[4] = {__builtin_amdgcn_perm(0u, dn, sel), __builtin_amdgcn_perm(0u, p4w, sel),
-                                            __builtin_amdgcn_perm(0u, up, sel), __builtin_amdgcn_perm(0u, p12w, sel)};
-                    // v - p - (t+1) = (v - (t+1)) - p;  p - v - (t+1) = p - (v + (t+1))
-                    const uint32_t vd = pk_sub16(v, T1), vb = pk_sub16(v, NT1);
-                    uint32_t xd[4], xb[4];
-    #pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        xd[k] = pk_sub16(vd, pk[k]);               // >= 0 <=> v - p > t
-                        xb[k] = pk_sub16(pk[k], vb);               // >= 0 <=> p - v > t
-                    }
-                    const uint32_t failD = (xd[0] | xd[1]) & (xd[1] | xd[2]) & (xd[2] | xd[3]) & (xd[3] | xd[0]);
-                    const uint32_t failB = (xb[0] | xb[1]) & (xb[1] | xb[2]) & (xb[2] | xb[3]) & (xb[3] | xb[0]);
-                    okw[hf] = ~(failD & failB) & 0x80008000u;
+                    const uint32_t sel = hf ? 0x04030401u : 0x04020400u;   // bytes 1,3 or 0,2 | 0x64
+                    const orbx_h2 v = h2_bytes(mid, k64, sel);
+                    // compass points in ring order 0, 4, 8, 12
+                    const orbx_h2 p0 = h2_bytes(dn, k64, sel), p4 = h2_bytes(p4w, k64, sel);
+                    const orbx_h2 p8 = h2_bytes(up, k64, sel), p12 = h2_bytes(p12w, k64, sel);
+                    // IEEE maximum / minimum: no canonicalising moves (the
+                    // operands are finite)
+                    const orbx_h2 A = h2_min3(__builtin_elementwise_maximum(p0, p4), __builtin_elementwise_maximum(p4, p8),
+                                              __builtin_elementwise_minimum(__builtin_elementwise_maximum(p8, p12),
+                                                                            __builtin_elementwise_maximum(p12, p0)));
+                    const orbx_h2 B = h2_max3(__builtin_elementwise_minimum(p0, p4), __builtin_elementwise_minimum(p4, p8),
+                                              __builtin_elementwise_maximum(__builtin_elementwise_minimum(p8, p12),
+                                                                            __builtin_elementwise_minimum(p12, p0)));
+                    const orbx_h2 x = __builtin_elementwise_maximum(v - A, B - v) - T1;
+                    okw[hf] = ~__builtin_bit_cast(uint32_t, x) & 0x80008000u;
                 }
                 // pixel j -> bit j (even half: j = 0, 2; odd half: j = 1, 3)
                 mask = (int)(((okw[0] >> 15) & 1) | ((okw[1] >> 14) & 2) | ((okw[0] >> 29) & 4) | ((okw[1] >> 28) & 8));
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             }
             int w = qt + incl - cnt;
             if (mask) {
-    #pragma unroll
+#pragma unroll
                 for (int j = 0; j < 4; j++)
                     if ((mask >> j) & 1) cand[wv][(w++) & (kCandRing - 1)] = (uint32_t)(r * P + 4 * q + j) | (3u << 16);
             }
@@ -664,21 +673,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (qt > qh) score_partial();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    // non-max suppression over the S' map (kept S' written over the tile);
-    // returns this thread's count of kept corners at fastTh
+    // non-max suppression over the S' map: a pixel is kept if its S' beats
+    // all 8 neighbours' S'.  Only dwords whose `nz` bit is set can keep
+    // anything; they are listed (u16 tile dword indices, in windows of
+    // kUnitCap) with one block scan and shared by all 256 threads.
+    // Returns this thread's count of kept corners at fastTh.
     auto nms_pass = [&]() {
-        // non-max suppression: keep S' if it beats all 8 neighbours' S'.
-        // Units whose S' word is zero keep nothing (their tile word is
-        // cleared on the spot); the others are queued per wave in the
-        // candidate ring (tile word index) and suppressed 64 at a time.
         int c1 = 0;
         const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
         auto nms_unit = [&](int idx) {
-            if (idx < 0) return;
             const int q = idx % nq;
             const uint32_t* m = sm32 + idx;
             const uint32_t mid = m[0];
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 if (dr != 1) nb[k++] = mm;
                 nb[k++] = __builtin_amdgcn_alignbyte(hi, mm, 1);   // j+1
             }
-            uint32_t word = 0;
+            uint32_t bits = 0;
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
                 const uint32_t sel = hf ? 0x0c030c01u : 0x0c020c00u;
@@ -703,36 +707,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 for (int i = 1; i < 8; i++) mx = pk_max16(mx, __builtin_amdgcn_perm(0u, nb[i], sel));
                 const uint32_t sv = __builtin_amdgcn_perm(0u, mid, sel);
                 // keep where mx - s < 0 (s > every neighbour)
-                const uint32_t keep = ((pk_sub16(mx, sv) & 0x80008000u) >> 15) * 0xFFu;
-                const uint32_t kept = sv & keep;
-                word |= kept << (8 * hf);
+                const uint32_t keep = pk_sub16(mx, sv) & 0x80008000u;
+                // pixel j -> bit j (even half: j = 0, 2; odd half: j = 1, 3)
+                bits |= ((keep >> 15) & 1) << hf | ((keep >> 31) & 1) << (2 + hf);
                 // corners at fastTh among the kept (kept >= max(fastTh, 1))
-                c1 += __popc(~pk_sub16(kept, FT) & 0x80008000u);
+                const uint32_t kept16 = sv & ((keep >> 15) * 0xFFFFu);
+                c1 += __popc(~pk_sub16(kept16, FT) & keep);
             }
-            tile32[idx] = word;
+            if (bits) atomicOr(&kept[idx >> 3], bits << (4 * (idx & 7)));
         };
-        int qh = 0, qt = 0;
-        RowWalk nw(wv * 64 + lane, kBlock, nqe);
-        for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, nw.next()) {
-            const int u = u0 + lane;
-            const int idx = (3 + nw.r) * nq + q0 + nw.q;
-            const uint32_t mid = u < nunits ? sm32[idx] : 0u;
-            if (u < nunits && !mid) tile32[idx] = 0;
-            const unsigned long long bal = __ballot(mid != 0);
-            if (mid) cand[wv][(qt + __popcll(bal & ((1ull << lane) - 1))) & (kCandRing - 1)] = (uint32_t)idx;
-            qt += __popcll(bal);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            while (qt - qh >= 64) {
-                nms_unit((int)cand[wv][(qh + lane) & (kCandRing - 1)]);
-                qh += 64;
+        const int nw = (hy * nq + 31) >> 5;                  // nz words
+        const int pw = (nw + kBlock - 1) / kBlock;
+        const int w0 = min(tid * pw, nw), w1 = min(w0 + pw, nw);
+        int cnt = 0;
+        for (int w = w0; w < w1; w++) cnt += __popc(nz[w]);
+        int total;
+        const int off0 = block_exclusive_scan(cnt, &total, bs, 1);
+        for (int base = 0; base < total; base += kUnitCap) {
+            if (base > 0) __syncthreads();                   // previous window consumed
+            if (cnt && off0 < base + kUnitCap && off0 + cnt > base) {
+                int off = off0;
+                for (int w = w0; w < w1; w++) {
+                    uint32_t b = nz[w];
+                    while (b) {
+                        const int bit = __builtin_ctz(b);
+                        b &= b - 1;
+                        if (off >= base && off < base + kUnitCap) ulist[off - base] = (uint16_t)(32 * w + bit);
+                        off++;
+                    }
+                }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
+            const int n = min(total - base, kUnitCap);
+            for (int i = tid; i < n; i += kBlock) nms_unit((int)ulist[i]);
         }
-        if (qt > qh) nms_unit(lane < qt - qh ? (int)cand[wv][(qh + lane) & (kCandRing - 1)] : -1);
         return c1;
     };
     // Thresholds (:599-614): FAST(fastTh), and FAST(7) when that finds <= 3
@@ -742,89 +750,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     // rescored at 7 only when it needs the fallback.
     int n1, tmin_final;
     FP_MARK(0);
-    if (a.fast_th > a.fast_th_low) {
-        tmin_final = a.fast_th;
-        score_pass(a.fast_th);
+    tmin_final = a.fast_th;
+    score_pass(a.fast_th);
+    __syncthreads();
+    FP_MARK(1);
+    n1 = block_sum(nms_pass(), bs, 0);
+    FP_MARK(2);
+    if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
+        if (threadIdx.x == 0) FP_ADD(8, 1);
+        clear_maps();
         __syncthreads();
-        FP_MARK(1);
-        n1 = block_sum(nms_pass(), bs, 0);
-        FP_MARK(2);
-        if (n1 <= 3) {   // uniform over the block
-            if (threadIdx.x == 0) FP_ADD(8, 1);
-            __syncthreads();
-            load_tile();
-            __syncthreads();
-            tmin_final = a.fast_th_low;
-            score_pass(a.fast_th_low);
-            __syncthreads();
-            nms_pass();
-            __syncthreads();
-            FP_MARK(3);
-        }
-    } else {
-        tmin_final = a.fast_th;
-        score_pass(a.fast_th);
+        tmin_final = a.fast_th_low;
+        score_pass(a.fast_th_low);
         __syncthreads();
-        n1 = block_sum(nms_pass(), bs, 0);
+        nms_pass();
+        FP_MARK(3);
     }
+    __syncthreads();
     // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
     const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
     uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    // raster-order compaction with one block scan: thread tid owns the
-    // contiguous units [tid * per, (tid + 1) * per)
-    const int per = (nunits + kBlock - 1) / kBlock;
-    const int ua = min(tid * per, nunits), ub = min(ua + per, nunits);
+    // raster-order compaction of the kept bitmap: thread tid owns the
+    // contiguous bitmap words [ka, kb); kept bytes are S' >= tmin of the
+    // final pass, and t == tmin there unless fastTh < 7 fell back to 7
+    // (then each byte is compared)
+    const int nkw = (hy * P + 31) >> 5;
+    const int per = (nkw + kBlock - 1) / kBlock;
+    const int ka = min(tid * per, nkw), kb = min(ka + per, nkw);
+    const bool all_kept = t == tmin_final;
     int cnt = 0;
-    {
-        int r = 3 + ua / nqe, q = q0 + ua - (r - 3) * nqe;
-        // kept bytes are S' >= tmin of the final score pass; t == tmin there
-        // unless fastTh < 7 fell back to 7 (then compare each byte)
-        const bool all_nonzero = t == tmin_final;
-        for (int u = ua; u < ub; u++) {
-            const uint32_t word = tile32[r * nq + q];
-            if (all_nonzero) {
-                uint32_t x = word | (word >> 4);
-                x |= x >> 2;
-                x |= x >> 1;
-                cnt += __popc(x & 0x01010101u);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) cnt += byte_of(word, j) >= t && byte_of(word, j) > 0;
-            }
-            if (++q == q0 + nqe) {
-                q = q0;
-                r++;
+    for (int k = ka; k < kb; k++) {
+        uint32_t b = kept[k];
+        if (all_kept) {
+            cnt += __popc(b);
+        } else {
+            while (b) {
+                const int bit = __builtin_ctz(b);
+                b &= b - 1;
+                cnt += sm[32 * k + bit] >= t;
             }
         }
     }
     int base;
     int off = block_exclusive_scan(cnt, &base, bs, 1);
     if (cnt) {
-        int r = 3 + ua / nqe, q = q0 + ua - (r - 3) * nqe;
-        for (int u = ua; u < ub; u++) {
-            const uint32_t word = tile32[r * nq + q];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int s = byte_of(word, j);
-                if (s >= t && s > 0) {
+        // the list is assembled in the (no longer needed) tile area; list_cap
+        // <= ceil(iw/2) * ceil(ih/2) <= hx * hy / 4 <= the tile's dwords
+        for (int k = ka; k < kb; k++) {
+            uint32_t b = kept[k];
+            while (b) {
+                const int bit = __builtin_ctz(b);
+                b &= b - 1;
+                const int pos = 32 * k + bit;
+                const int s = sm[pos];
+                if (s >= t) {
                     if (off < C.list_cap) {
-                        const int cc = 4 * q + j - sh;   // ROI column
-                        sm32[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                        const int r = pos / P, cc = pos - r * P - sh;   // tile row, ROI column
+                        tile32[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
                     }
                     off++;
                 }
             }
-            if (++q == q0 + nqe) {
-                q = q0;
-                r++;
-            }
         }
     }
-    // the list was assembled in the (no longer needed) S' map area; copy it
-    // out with consecutive lanes on consecutive dwords (list_cap <= the
-    // map's dword capacity: ceil(iw/2) * ceil(ih/2) <= hx * hy / 4)
+    // copy out with consecutive lanes on consecutive dwords
     __syncthreads();
-    for (int i = tid; i < min(base, C.list_cap); i += kBlock) out[i] = sm32[i];
+    for (int i = tid; i < min(base, C.list_cap); i += kBlock) out[i] = tile32[i];
     if (tid == 0) {
         *count_out = base;
         if (base > C.list_cap) atomicOr(a.error_flags, 1);
@@ -1414,16 +1405,16 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             }
             const dim3 grid((int)g.cells.size(), nb);
             auto fast = [&](auto kern, int P) {
-                const int bytes = (hmax * P + 15) & ~15;
-                hipLaunchKernelGGL(kern, grid, dim3(256), 2 * bytes, st, x, bytes);
+                const int bytes = fast_tile_bytes(hmax, P);
+                hipLaunchKernelGGL(kern, grid, dim3(256), fast_lds_bytes(bytes), st, x, bytes);
             };
             if (wmax <= 96) fast(k_fast_cells<96>, 96);
             else if (wmax <= 144) fast(k_fast_cells<144>, 144);
             else if (wmax <= 208) fast(k_fast_cells<208>, 208);
             else if (wmax <= 336) fast(k_fast_cells<336>, 336);
             else {
-                const int pitch = (g.max_tile_bytes + 15) & ~15;
-                hipLaunchKernelGGL(k_fast_cells<0>, grid, dim3(256), 2 * pitch, st, x, pitch);
+                const int bytes = fast_tile_bytes(1, g.max_tile_bytes);
+                hipLaunchKernelGGL(k_fast_cells<0>, grid, dim3(256), fast_lds_bytes(bytes), st, x, bytes);
             }
         }
         timer_end(ctx, "fast", st);
