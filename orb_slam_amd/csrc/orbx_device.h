@@ -82,10 +82,12 @@ __device__ inline int hamming256(const uint4& a0, const uint4& a1, const uint4& 
 // --------------------------------------------------------------------------
 // Block-wide scans / reductions for 256-thread blocks (4 waves).
 // --------------------------------------------------------------------------
-struct BlockScratch {
-    int wave[2][kWaves];
+template <int kW>
+struct BlockScratchN {
+    int wave[2][kW];
     int vars[8];
 };
+using BlockScratch = BlockScratchN<kWaves>;
 
 // Wave64 scans / reductions on DPP row shifts + row broadcasts (gfx9):
 // VALU-only, no ds_bpermute round trips.  All 64 lanes must be active.
@@ -123,7 +125,8 @@ __device__ inline int wave_max(int v)
 }
 
 // Exclusive prefix of v over threadIdx order; *total = block sum.
-__device__ inline int block_exclusive_scan(int v, int* total, BlockScratch& s, int buf)
+template <int kW>
+__device__ inline int block_exclusive_scan(int v, int* total, BlockScratchN<kW>& s, int buf)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int inc = wave_inclusive_scan(v);
@@ -131,7 +134,7 @@ __device__ inline int block_exclusive_scan(int v, int* total, BlockScratch& s, i
     __syncthreads();
     int base = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < kWaves; i++) {
+    for (int i = 0; i < kW; i++) {
         const int x = s.wave[buf][i];
         base += (i < w) ? x : 0;
         tot += x;
@@ -140,7 +143,8 @@ __device__ inline int block_exclusive_scan(int v, int* total, BlockScratch& s, i
     return base + inc - v;
 }
 
-__device__ inline int block_sum(int v, BlockScratch& s, int buf)
+template <int kW>
+__device__ inline int block_sum(int v, BlockScratchN<kW>& s, int buf)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     v = wave_sum(v);
@@ -148,7 +152,7 @@ __device__ inline int block_sum(int v, BlockScratch& s, int buf)
     __syncthreads();
     int t = 0;
 #pragma unroll
-    for (int i = 0; i < kWaves; i++) t += s.wave[buf][i];
+    for (int i = 0; i < kW; i++) t += s.wave[buf][i];
     return t;
 }
 

@@ -457,9 +457,10 @@ __device__ inline void fast_arc2(const uint8_t* t, int pa, int pb, int pitch, in
 }
 
 // One workgroup per (cell, frame).  LDS (dynamic): the cell ROI with
-// 16-byte aligned rows (tile, kept intact for the threshold-7 rescore), its
-// S' map (sm), and two bitmaps: `nz` (one bit per tile dword whose S' word
-// is nonzero) and `kept` (one bit per tile byte that survives NMS).
+// 16-byte aligned rows (tile), its S' map (sm), and two bitmaps: `nz` (one
+// bit per tile dword whose S' word is nonzero) and `kept` (one bit per tile
+// byte that survives NMS), which reuses the tile's first bytes once the
+// score pass is done (the threshold-7 rescore reloads the tile).
 //  1. compass pre-test, 4 pixels per thread: a 9-arc covers two adjacent
 //     compass points, so S >= tmin needs d > tmin (or < -tmin) on both;
 //     survivors are compacted per wave and scored with all lanes busy; a
@@ -489,17 +490,23 @@ __device__ inline orbx_h2 h2_bytes(uint32_t w, uint32_t k64, uint32_t sel)
     return __builtin_bit_cast(orbx_h2, __builtin_amdgcn_perm(k64, w, sel));
 }
 
+constexpr int kFastWideThreads = 256;   // workgroup of the wide-tile FAST instances
 // Dynamic LDS of a FAST workgroup for tiles of `bytes` (host and device).
 __host__ __device__ constexpr int fast_tile_bytes(int hy_max, int pitch) { return (hy_max * pitch + 511) & ~511; }
-__host__ __device__ constexpr int fast_lds_bytes(int tile_bytes) { return 2 * tile_bytes + tile_bytes / 8 + tile_bytes / 32; }
+__host__ __device__ constexpr int fast_lds_bytes(int tile_bytes) { return 2 * tile_bytes + tile_bytes / 32; }
 
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
-template <int kP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_fast_cells(ExtractArgs a, int tile_bytes)
+// kThreads: 256 for cells up to 208-byte rows; the wide tiles of large
+// frames (1920x1080: 336-byte rows, 75 KB of LDS, two workgroups per CU)
+// get more waves per workgroup instead.
+template <int kP, int kThreads = 256>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
+    ExtractArgs a, int tile_bytes)
 {
+    constexpr int kBlock = kThreads, kWaves = kThreads / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ BlockScratch bs;
+    __shared__ BlockScratchN<kWaves> bs;
     constexpr int kCandRing = 256;           // per-wave ring (a full iteration's 256 fit after a drain)
     constexpr int kUnitCap = kWaves * kCandRing * 2;   // u16 NMS unit list aliasing the rings
     __shared__ __attribute__((aligned(16))) uint32_t cand[kWaves][kCandRing];
@@ -521,10 +528,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     uint8_t* sm = smem + tile_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
-    uint32_t* kept = reinterpret_cast<uint32_t*>(sm + tile_bytes);               // bit per tile byte
-    uint32_t* nz = reinterpret_cast<uint32_t*>(sm + tile_bytes + tile_bytes / 8);  // bit per tile dword
+    uint32_t* kept = tile32;                                      // bit per tile byte (after scoring)
+    uint32_t* nz = reinterpret_cast<uint32_t*>(sm + tile_bytes);  // bit per tile dword
     FP_T0();
-    {
+    auto load_tile = [&]() {
         uint4* t16 = reinterpret_cast<uint4*>(tile32);
         const int n = hy * nq16;
         // i / nq16 as a float product: (i + 1/2) / nq16 is at least 1/(2 nq16)
@@ -549,12 +556,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             t16[r2 * (P >> 4) + c2] = v2;
             t16[r3 * (P >> 4) + c3] = v3;
         }
-    }
-    // S' (0 where not scored) and both bitmaps start at zero (they are
-    // contiguous: tile_bytes * (1 + 1/8 + 1/32), a multiple of 16)
-    const int clear16 = (tile_bytes + tile_bytes / 8 + tile_bytes / 32) >> 4;
+    };
+    load_tile();
+    // S' (0 where not scored) and nz start at zero (contiguous: tile_bytes *
+    // (1 + 1/32), a multiple of 16); kept is cleared after the score pass
+    const int clear16 = (tile_bytes + tile_bytes / 32) >> 4;
     auto clear_maps = [&]() {
         for (int i = tid; i < clear16; i += kBlock) reinterpret_cast<uint4*>(sm32)[i] = make_uint4(0, 0, 0, 0);
+    };
+    auto clear_kept = [&]() {
+        for (int i = tid; i < (tile_bytes >> 7); i += kBlock) reinterpret_cast<uint4*>(kept)[i] = make_uint4(0, 0, 0, 0);
     };
     clear_maps();
     __syncthreads();
@@ -753,15 +764,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     tmin_final = a.fast_th;
     score_pass(a.fast_th);
     __syncthreads();
+    clear_kept();   // the tile is dead until a rescore reloads it
+    __syncthreads();
     FP_MARK(1);
     n1 = block_sum(nms_pass(), bs, 0);
     FP_MARK(2);
     if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
         if (threadIdx.x == 0) FP_ADD(8, 1);
+        load_tile();
         clear_maps();
         __syncthreads();
         tmin_final = a.fast_th_low;
         score_pass(a.fast_th_low);
+        __syncthreads();
+        clear_kept();
         __syncthreads();
         nms_pass();
         FP_MARK(3);
@@ -794,8 +810,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     int base;
     int off = block_exclusive_scan(cnt, &base, bs, 1);
     if (cnt) {
-        // the list is assembled in the (no longer needed) tile area; list_cap
-        // <= ceil(iw/2) * ceil(ih/2) <= hx * hy / 4 <= the tile's dwords
+        // entries go straight to the cell's list (each thread's run is
+        // contiguous; the tile area holds the kept bitmap being read)
         for (int k = ka; k < kb; k++) {
             uint32_t b = kept[k];
             while (b) {
@@ -806,16 +822,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 if (s >= t) {
                     if (off < C.list_cap) {
                         const int r = pos / P, cc = pos - r * P - sh;   // tile row, ROI column
-                        tile32[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                        out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
                     }
                     off++;
                 }
             }
         }
     }
-    // copy out with consecutive lanes on consecutive dwords
-    __syncthreads();
-    for (int i = tid; i < min(base, C.list_cap); i += kBlock) out[i] = tile32[i];
     if (tid == 0) {
         *count_out = base;
         if (base > C.list_cap) atomicOr(a.error_flags, 1);
@@ -1404,17 +1417,18 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 hmax = std::max(hmax, c.hy);
             }
             const dim3 grid((int)g.cells.size(), nb);
-            auto fast = [&](auto kern, int P) {
+            auto fast = [&](auto kern, int P, int threads) {
                 const int bytes = fast_tile_bytes(hmax, P);
-                hipLaunchKernelGGL(kern, grid, dim3(256), fast_lds_bytes(bytes), st, x, bytes);
+                hipLaunchKernelGGL(kern, grid, dim3(threads), fast_lds_bytes(bytes), st, x, bytes);
             };
-            if (wmax <= 96) fast(k_fast_cells<96>, 96);
-            else if (wmax <= 144) fast(k_fast_cells<144>, 144);
-            else if (wmax <= 208) fast(k_fast_cells<208>, 208);
-            else if (wmax <= 336) fast(k_fast_cells<336>, 336);
+            if (wmax <= 96) fast(k_fast_cells<96>, 96, 256);
+            else if (wmax <= 144) fast(k_fast_cells<144>, 144, 256);
+            else if (wmax <= 208) fast(k_fast_cells<208>, 208, 256);
+            else if (wmax <= 336) fast(k_fast_cells<336, kFastWideThreads>, 336, kFastWideThreads);
             else {
                 const int bytes = fast_tile_bytes(1, g.max_tile_bytes);
-                hipLaunchKernelGGL(k_fast_cells<0>, grid, dim3(256), fast_lds_bytes(bytes), st, x, bytes);
+                hipLaunchKernelGGL((k_fast_cells<0, kFastWideThreads>), grid, dim3(kFastWideThreads), fast_lds_bytes(bytes),
+                                   st, x, bytes);
             }
         }
         timer_end(ctx, "fast", st);

@@ -1,7 +1,7 @@
 """FAST kernel phase breakdown (diagnostic build): per-phase cycles summed
 over workgroups (s_memtime stamps of thread 0), compass survivors and units.
 Build: python -m orb_slam_amd.build -DORBX_FAST_PROFILE --out=orb_slam_amd/liborbx_fastprof.so
-Run:   ORBX_LIBRARY=orb_slam_amd/liborbx_fastprof.so python3 tools/fast_phases.py"""
+Run:   ORBX_LIBRARY=orb_slam_amd/liborbx_fastprof.so python3 tools/fast_phases.py [W H nfeatures frames]"""
 import ctypes
 import sys
 from pathlib import Path
@@ -10,9 +10,9 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import orb_slam_amd as ox  # noqa: E402
 from orb_slam_amd import synth  # noqa: E402
 
-B = 256
-ctx = ox.Context(nfeatures=1000, max_w=640, max_h=480, slots=B)
-ctx.upload(synth.sequence(640, 480, B, seed=2000))
+W, H, NF, B = (int(v) for v in sys.argv[1:5]) if len(sys.argv) > 4 else (640, 480, 1000, 256)
+ctx = ox.Context(nfeatures=NF, max_w=W, max_h=H, slots=B)
+ctx.upload(synth.sequence(W, H, B, seed=2000))
 ctx.set_split(False)
 ctx.extract(0, B)
 ctx.sync()
