@@ -368,6 +368,27 @@ def pmc_traffic(workload, name):
                                     f"build {meta.get('git_head')}"}
 
 
+# wave64 VALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per 2
+# cycles per SIMD (32 lanes), 2.4 GHz (MI355X_MICROARCH.md constants table)
+VALU_PEAK_TIPS = 256 * 4 * 2.4e9 / 2 / 1e12
+
+
+def pmc_valu(workload, name):
+    """SQ_INSTS_VALU per launch of kernel `name` from the newest committed
+    PMC summary of this bench command, when it profiled the loaded build."""
+    import hashlib
+    cands = sorted((Path(__file__).resolve().parent / "profiles").glob(f"r*_{workload}_pmc_hbm.json"))
+    sym = KERNEL_SYMBOL.get(name)
+    if not cands or not sym:
+        return None
+    summary = json.loads(cands[-1].read_text())
+    meta = summary.pop("_meta", {})
+    hits = [v["SQ_INSTS_VALU"] for k, v in summary.items() if sym in k and "SQ_INSTS_VALU" in v]
+    if not hits or meta.get("liborbx_sha256") != hashlib.sha256(Path(ox.LIB_PATH).read_bytes()).hexdigest():
+        return None
+    return {"insts_per_launch": sum(hits) / len(hits), "source": f"profiles/{cands[-1].name} (SQ_INSTS_VALU per dispatch)"}
+
+
 def timed(args, ctx, step, dist, names, only=None):
     def barrier():
         if dist is not None:
@@ -469,6 +490,16 @@ def main():
                                "traffic": roof.get("traffic"), "kernel": roof["kernel"],
                                "flops_per_frame": check["fp64_flops_per_frame"],
                                "avg_launch_ms": roof["avg_launch_ms"]}
+        valu = pmc_valu(args.workload, roof["kernel"])
+        if valu and roof.get("avg_launch_ms"):
+            # the dominant kernel against its instruction-issue ceiling: wave64
+            # VALU instructions per launch (committed SQ_INSTS_VALU pass of this
+            # build) over the live mean launch duration
+            rate = valu["insts_per_launch"] / (roof["avg_launch_ms"] / 1e3)
+            out["roofline_valu"] = {"bound": "valu-issue", "achieved": round(rate / 1e12, 4), "peak": VALU_PEAK_TIPS,
+                                    "unit": "T wave-instr/s", "frac": round(rate / 1e12 / VALU_PEAK_TIPS, 4),
+                                    "kernel": roof["kernel"], "valu_insts_per_launch": valu["insts_per_launch"],
+                                    "avg_launch_ms": roof["avg_launch_ms"], "source": valu["source"]}
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)

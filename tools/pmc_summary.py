@@ -10,7 +10,9 @@ rows, atomics) the truth lies between the two.
 The summary records the build it profiled (`_meta`: git HEAD and the SHA-256
 of orb_slam_amd/liborbx.so as shipped to the GPU box), so bench.py can refuse
 a stale profile.
-usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv>
+usage: python tools/pmc_summary.py <fetch run_counter_collection.csv> <write csv> [<SQ csv>]
+(the optional third pass adds SQ_INSTS_VALU per dispatch: bench.py's
+roofline_valu)
 """
 import csv
 import hashlib
@@ -46,6 +48,7 @@ def load(path, counter):
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
+    valu = load(sys.argv[3], "SQ_INSTS_VALU") if len(sys.argv) > 3 else {}
     out = {"_meta": build_id()}
     for k in sorted(set(fetch) | set(write)):
         if k.startswith("__amd"):
@@ -53,6 +56,8 @@ def main():
         fk, wk = fetch.get(k, 0.0), write.get(k, 0.0)
         out[k] = {"FETCH_SIZE_KiB": fk, "WRITE_SIZE_KiB": wk,
                   "hbm_bytes_raw": (fk + wk) * 1024, "hbm_bytes_fetch_x2": (2 * fk + wk) * 1024}
+        if k in valu:
+            out[k]["SQ_INSTS_VALU"] = valu[k]
     print(json.dumps(out, indent=1))
 
 
