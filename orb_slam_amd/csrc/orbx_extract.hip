@@ -1406,7 +1406,9 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         }
     };
     // FAST .. describe over nb frames on stream st (after their pyramid).
-    auto run_rest = [&](const ExtractArgs& x, int nb, hipStream_t st) {
+    // parts: 1 = FAST, 2 = retain, 4 = blur + describe
+    auto run_rest = [&](const ExtractArgs& x, int nb, hipStream_t st, int parts) {
+        if (parts & 1) {
         timer_begin(ctx, "fast", st);
         {
             // widest aligned cell row and tallest cell pick the tile pitch
@@ -1432,6 +1434,8 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             }
         }
         timer_end(ctx, "fast", st);
+        }
+        if (parts & 2) {
         timer_begin(ctx, "retain", st);
         {
             // wave-private LDS: cell list + partition scratch (longer lists
@@ -1446,6 +1450,8 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                                (size_t)lwaves * lw * 4, st, x, lwaves, lw);
         }
         timer_end(ctx, "retain", st);
+        }
+        if (!(parts & 4)) return;
         timer_begin(ctx, "blur", st);
         hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
         timer_end(ctx, "blur", st);
@@ -1455,7 +1461,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     };
     auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         run_pyramid(x, nb, st);
-        run_rest(x, nb, st);
+        run_rest(x, nb, st, 7);
     };
     // Work buffers are indexed by batch position (frame f of a pass uses
     // work slot f); the frame store and outputs by slot.  Large batches run
@@ -1501,18 +1507,45 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         ctx->stream_dirty = true;
     }
     if (async) {
-        // Extraction (two concurrent halves, joined on the context stream),
-        // then the batch's matching on mstream, which overlaps the next
-        // call's extraction of other slots.  Measured alternatives, both
-        // no faster because the step is VALU-bound overall: offsetting the
-        // halves (one half's FAST against the other's latency-bound passes),
-        // and running the next batch's pyramid on stream2 during this
-        // batch's FAST .. describe (work buffers are per slot, so that is
-        // safe; it stays possible).
-        const int r = launch_extract(ctx, first, count, nullptr);
-        if (r != ORBX_OK) return r;
-        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream));
-        ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
+        // Extraction, then the batch's matching on mstream, which overlaps
+        // the next call's extraction of other slots.  Batches large enough
+        // to split run as a software pipeline over two streams: the first
+        // half's pyramid + FAST on the context stream, then its retain ..
+        // describe while the second half (stream2, started at that point)
+        // runs its pyramid + FAST; the next call's first half follows on the
+        // context stream during the second half's tail.  The VALU-bound FAST
+        // of one half thus overlaps the latency-bound stages of the other,
+        // in steady state.  mstream's match waits for both halves.
+        if (ctx->split && count >= 2 * kSplitMinFrames && ctx->stream2) {
+            // outputs of [first, first + count) are rewritten: pending matches
+            // reading them finish first (stream2 inherits it through ev_fork)
+            wait_pending_overlap(ctx, first, count, ctx->stream);
+            const int n0 = count / 2, n1 = count - n0;
+            ExtractArgs b = a;
+            b.first_slot = first + n0;
+            b.pyr_raw += (size_t)n0 * a.frame_pyr_bytes;
+            b.pyr_blur += (size_t)n0 * a.frame_pyr_bytes;
+            b.cell_lists += (size_t)n0 * a.list_entries;
+            b.retain_scratch += (size_t)n0 * (a.list_entries + 4 * a.ncells);
+            b.cell_count += (size_t)n0 * a.ncells;
+            b.level_keys += (size_t)n0 * a.level_entries;
+            b.level_count += (size_t)n0 * a.nlevels;
+            run_pyramid(a, n0, ctx->stream);
+            run_rest(a, n0, ctx->stream, 1);
+            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+            run_rest(a, n0, ctx->stream, 6);
+            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream));
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+            run(b, n1, ctx->stream2);
+            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream2));
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_join, 0));
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
+        } else {
+            const int r = launch_extract(ctx, first, count, nullptr);
+            if (r != ORBX_OK) return r;
+            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream));
+            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
+        }
         match_runs(first, first + count, 0, -1, ctx->mstream);
         // the match reads the outputs of the batch's sequences
         const int q = m->seq_len;
