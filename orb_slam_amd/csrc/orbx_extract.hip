@@ -1445,7 +1445,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             hipLaunchKernelGGL(k_retain_cells, dim3(((int)g.cells.size() + cwaves - 1) / cwaves, nb), dim3(64 * cwaves),
                                (size_t)cwaves * cw * 4, st, x, cwaves, cw);
             const int lw = 2 * g.max_level_cap + 8;
-            const int lwaves = std::max(1, std::min(4, (int)(kRetainLds / (4 * (size_t)lw))));
+            const int lwaves = 1;   // one level per block: small LDS blocks fit beside the other stream's kernels
             hipLaunchKernelGGL(k_retain_levels, dim3((g.nlevels + lwaves - 1) / lwaves, nb), dim3(64 * lwaves),
                                (size_t)lwaves * lw * 4, st, x, lwaves, lw);
         }
