@@ -128,3 +128,40 @@ def test_async_extract_match_alternating_slots(mode):
         k, _ = ctx.features(s)
         assert n == got[s][1] and np.array_equal(m[:len(k)], got[s][0][:len(k)]), s
     ctx.close()
+
+
+def test_async_pipeline_reused_slots_odd_batch():
+    """The two-stream extract+match pipeline with an odd batch (halves of 18
+    and 19 frames), the same slot range extracted again while its previous
+    match is pending, and new frames uploaded between pipelined calls: every
+    slot's keypoints, descriptors and matches equal the synchronous path's."""
+    w, h, B = 320, 240, 37
+    seqs = [synth.sequence(w, h, B, seed=s) for s in (41, 42)]
+    ctx = ox.Context(nfeatures=500, max_w=w, max_h=h, slots=B)
+
+    def snapshot():
+        return [(*ctx.features(s), *ctx.matches(s)) for s in range(B)]
+
+    def reference(frames):
+        ctx.set_async_match(False)
+        ctx.upload(frames)
+        ctx.extract(0, B)
+        ctx.match_prev(0, B, B)
+        ctx.sync()
+        return snapshot()
+
+    want = [reference(f) for f in seqs]
+    ctx.set_async_match(True)
+    ctx.upload(seqs[0])
+    ctx.extract_match(0, B, B)
+    ctx.extract_match(0, B, B)      # same slots: waits for the pending match
+    ctx.upload(seqs[1])             # new frames while nothing is pending any more
+    ctx.extract_match(0, B, B)
+    ctx.sync()
+    got = snapshot()
+    for s in range(B):
+        gk, gd, gm, gn = got[s]
+        rk, rd, rm, rn = want[1][s]
+        assert np.array_equal(gk, rk) and np.array_equal(gd, rd), s
+        assert gn == rn and np.array_equal(gm[:len(gk)], rm[:len(rk)]), s
+    ctx.close()
