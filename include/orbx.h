@@ -126,6 +126,18 @@ int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int
  * consecutive batches concurrent).  Any other call on the context, or an
  * extraction into slots the pending match reads, waits for it first. */
 int orbx_dev_set_async_match(orbx_ctx* ctx, int enable);
+/* Pyramid construction mode (both produce identical buffers):
+ * 0 = staged launches (level-0 copy, one resize per level, blur): default;
+ * 1 = one fused launch per batch (orbx_pyramid.hip) that streams each frame
+ *     once and builds every level and its blur from LDS rings, used when the
+ *     frame size fits its plan (otherwise the staged launches run).  It
+ *     holds one 1024-thread workgroup per frame on a CU for the whole frame,
+ *     which the two-stream extraction pipeline cannot overlap: slower at C2
+ *     (DESIGN.md section 3), kept for parity coverage and experiments.
+ * orbx_dev_pyramid_fused reports whether the fused launch applies to the
+ * current frame size and mode (1) or not (0). */
+int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode);
+int orbx_dev_pyramid_fused(orbx_ctx* ctx);
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */

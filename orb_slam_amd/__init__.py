@@ -73,6 +73,8 @@ def _declare(L):
         "orbx_dev_match_bf_prev": ([vp, i, i, i, i, f], i),
         "orbx_dev_set_split": ([vp, i], i),
         "orbx_dev_set_async_match": ([vp, i], i),
+        "orbx_dev_set_pyramid_mode": ([vp, i], i),
+        "orbx_dev_pyramid_fused": ([vp], i),
         "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
         "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
@@ -210,6 +212,15 @@ class Context:
         """Queue extract_match's matching behind the extraction on an internal
         stream; later extract_match calls on other slots overlap it."""
         _check(lib().orbx_dev_set_async_match(self._h, int(enable)), "orbx_dev_set_async_match")
+
+    def set_pyramid_mode(self, mode):
+        """0: staged launches (level-0 copy, per-level resize, blur; default),
+        1: one fused pyramid + blur launch where its plan fits the frame size."""
+        _check(lib().orbx_dev_set_pyramid_mode(self._h, int(mode)), "orbx_dev_set_pyramid_mode")
+
+    def pyramid_fused(self):
+        """True when extraction of the current frame size uses the fused pyramid."""
+        return bool(lib().orbx_dev_pyramid_fused(self._h))
 
     def match_bf_prev(self, first, count, seq_len, th_low=50, nnratio=0.9):
         _check(lib().orbx_dev_match_bf_prev(self._h, first, count, seq_len, th_low, nnratio),

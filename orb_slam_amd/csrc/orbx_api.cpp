@@ -1,6 +1,7 @@
 // C ABI of liborbx (include/orbx.h): context lifetime, device buffers,
 // host <-> HBM transfers, kernel timing, and the drop-in entry points that
 // replace ORBextractor::operator() / ORBmatcher / Optimizer calls.
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -79,7 +80,7 @@ static void free_buffers(orbx_ctx* ctx)
                     ctx->level_keys, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
-                    ctx->scratch, ctx->pose_dev};
+                    ctx->scratch, ctx->pose_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
@@ -151,6 +152,7 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     ORBX_HIP_CHECK(hipMemcpy(ctx->blur_tiles, tiles.data(), tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
     // The retain kernel keeps per-cell state for up to 256 cells per level.
     if (g.max_cells_per_level > 256) return ORBX_ERR_UNSUPPORTED;
+    if ((r = upload_pyramid_plan(ctx)) != ORBX_OK) return r;
     ctx->geom_w = w;
     ctx->geom_h = h;
     return ORBX_OK;
@@ -193,6 +195,7 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     ctx->max_w = max_w;
     ctx->max_h = max_h;
     ctx->slots = max_batch;
+    if (const char* e = getenv("ORBX_PYR_MODE")) ctx->pyr_mode = atoi(e) == 1 ? 1 : 0;   // A/B runs
     init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
     int r = ORBX_OK;
     const int S = max_batch;
@@ -333,6 +336,20 @@ int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
     ctx_enter(ctx);
     ctx->async_match = enable != 0;
     return ORBX_OK;
+}
+
+int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 1) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->pyr_mode = mode;
+    return ORBX_OK;
+}
+
+int orbx_dev_pyramid_fused(orbx_ctx* ctx)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    return ctx->pyr.ok && ctx->pyr_mode == 1 ? 1 : 0;
 }
 
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)

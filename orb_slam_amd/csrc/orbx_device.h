@@ -68,6 +68,33 @@ __device__ inline void cr_sincosf(float x, float* s, float* c)
     *c = fc;
 }
 
+// BORDER_REFLECT_101 index (cv::borderInterpolate).
+__host__ __device__ inline int reflect101(int p, int len)
+{
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+// GaussianBlur 7x7 sigma 2 (OpenCV 2.4 8U fixed point, kernel {18,34,49,55,49,34,18}):
+// Horizontal 7-tap sums of the 4 pixels of dword wc (wl / wr: the dwords to
+// its left / right): taps j-3..j as one v_dot4_u32_u8 with {18,34,49,55},
+// taps j+1..j+3 as a second with {49,34,18,0}.
+__device__ inline void blur_hsum_w(uint32_t wl, uint32_t wc, uint32_t wr, int hs[4])
+{
+    constexpr uint32_t kWA = 0x37312212u, kWB = 0x00122231u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t A = j == 3 ? wc : __builtin_amdgcn_alignbyte(wc, wl, j + 1);   // bytes j-3 .. j
+        const uint32_t B = j == 3 ? wr : __builtin_amdgcn_alignbyte(wr, wc, j + 1);   // bytes j+1 .. j+4
+        hs[j] = (int)__builtin_amdgcn_udot4(B, kWB, __builtin_amdgcn_udot4(A, kWA, 0u, false), false);
+    }
+}
+
 // cvRound of a float (SSE2 cvtsd2si, round half to even).
 __device__ inline int cv_round(float v) { return __float2int_rn(v); }
 

@@ -83,17 +83,6 @@ struct ExtractArgs {
     int max_list_cap, max_level_cap;
 };
 
-__device__ inline int reflect101(int p, int len)
-{
-    if ((unsigned)p < (unsigned)len) return p;
-    if (len == 1) return 0;
-    do {
-        if (p < 0) p = -p;
-        else p = 2 * len - 2 - p;
-    } while ((unsigned)p >= (unsigned)len);
-    return p;
-}
-
 __device__ inline uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
 __device__ inline int sat_s16(int v) { return min(max(v, -32768), 32767); }
 
@@ -985,20 +974,6 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
 // slides a 7-row window of horizontal sums down it in registers: one pass
 // over the input rows it needs, one dword store per output row, no LDS.
 // ---------------------------------------------------------------------------
-// Horizontal 7-tap sums of the 4 pixels of dword wc (wl / wr: the dwords to
-// its left / right): taps j-3..j as one v_dot4_u32_u8 with {18,34,49,55},
-// taps j+1..j+3 as a second with {49,34,18,0}.
-__device__ inline void blur_hsum_w(uint32_t wl, uint32_t wc, uint32_t wr, int hs[4])
-{
-    constexpr uint32_t kWA = 0x37312212u, kWB = 0x00122231u;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t A = j == 3 ? wc : __builtin_amdgcn_alignbyte(wc, wl, j + 1);   // bytes j-3 .. j
-        const uint32_t B = j == 3 ? wr : __builtin_amdgcn_alignbyte(wr, wc, j + 1);   // bytes j+1 .. j+4
-        hs[j] = (int)__builtin_amdgcn_udot4(B, kWB, __builtin_amdgcn_udot4(A, kWA, 0u, false), false);
-    }
-}
-
 __device__ inline void blur_hsum(const uint8_t* row, int x, int hs[4])
 {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(row + x);
@@ -1371,7 +1346,15 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.max_level_cap = g.max_level_cap;
 
     // The pyramid stages over nb frames on stream st.
+    // fused pyramid + blur (orbx_pyramid.hip) when the plan fits this geometry
+    const bool fused = ctx->pyr.ok && ctx->pyr_mode == 1;
     auto run_pyramid = [&](const ExtractArgs& x, int nb, hipStream_t st) {
+        if (fused) {
+            timer_begin(ctx, "pyramid", st);
+            launch_pyramid(ctx, x.first_slot, x.pyr_raw, x.pyr_blur, nb, st);
+            timer_end(ctx, "pyramid", st);
+            return;
+        }
         timer_begin(ctx, "pyr0", st);
         {
             const LevelGeom& L = g.levels[0];
@@ -1452,9 +1435,11 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         timer_end(ctx, "retain", st);
         }
         if (!(parts & 4)) return;
-        timer_begin(ctx, "blur", st);
-        hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
-        timer_end(ctx, "blur", st);
+        if (!fused) {
+            timer_begin(ctx, "blur", st);
+            hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
+            timer_end(ctx, "blur", st);
+        }
         timer_begin(ctx, "describe", st);
         hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), nb), dim3(256), 0, st, x);
         timer_end(ctx, "describe", st);

@@ -78,6 +78,34 @@ struct CellGeom {
 struct ResizeCol { int16_t sx0, sx1, a0, a1; };
 struct ResizeRow { int16_t sy0, sy1, b0, b1; };
 
+// Fused pyramid + blur (k_pyramid, orbx_pyramid.hip): one 1024-thread
+// workgroup per frame streams the frame's rows top to bottom; each level keeps
+// its most recent rows in an LDS ring.  Per level: ring placement and the
+// multiply-shift constant of (row mod ring).
+constexpr int kPyrThreads = 1024;
+constexpr int kPyrWaves = kPyrThreads / 64;
+struct PyrLevel {
+    int ring_off;   // LDS byte offset of the ring
+    int ring;       // rows in the ring
+    int rp;         // ring row pitch (padded row rounded up to 16 bytes)
+    uint32_t mul;   // ceil(2^20 / ring): row mod ring = r - ring * ((r * mul) >> 20)
+};
+// Jobs of one wave (-1: none): the blur of 64 dword columns of a level, the
+// resize of 64 dword columns of a level >= 1, 64 level-0 load items.
+struct PyrWave {
+    int16_t blur_level, blur_q0, res_level, res_q0, l0_base, pad;
+};
+struct PyrPlan {
+    bool ok = false;
+    int T = 0, S = 0;             // level-0 rows per step, steps
+    int l0_items = 0, nq16 = 0;   // level-0 load items per step (rows x 16-byte columns)
+    int rows_first = 0, rows_count = 0;   // res_rows entries staged in LDS (levels >= 1)
+    int rows_lds = 0, sched_lds = 0, lds_bytes = 0;
+    std::vector<PyrLevel> levels;
+    std::vector<int32_t> sched;   // S x nlevels: rows produced | rows blurred << 16, by the end of each step
+    PyrWave waves[kPyrWaves];
+};
+
 // Extractor configuration and per-image-size geometry (host computed, the
 // way OpenCV computes its tables per call).
 struct Geometry {
@@ -174,6 +202,13 @@ struct orbx_ctx {
     int cap_res_cols = 0, cap_res_rows = 0, cap_blur_tiles = 0;
     int4* blur_tiles = nullptr;        // (level, first item, dwords/row, strips) blur blocks
     int blur_tiles_n = 0;
+    // fused pyramid + blur plan for the current geometry (orbx_pyramid.hip)
+    orbx::PyrPlan pyr;
+    int pyr_mode = 0;                  // 0: staged launches, 1: fused when the plan fits
+    orbx::PyrLevel* d_pyr_levels = nullptr;
+    int32_t* d_pyr_sched = nullptr;
+    orbx::PyrWave* d_pyr_waves = nullptr;
+    int cap_pyr_sched = 0;
     int last_first = 0, last_count = 0;   // batch of the most recent extract
     // generic scratch for the one-shot matcher / BA entry points
     void* scratch = nullptr;
@@ -217,6 +252,13 @@ struct MatchSpec {
     float nnratio;
 };
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nullptr);
+// orbx_pyramid.hip: plan of the fused pyramid + blur kernel for geometry g
+// (plan.ok false when it does not apply: tiny levels, LDS or job overflow),
+// its upload, and its launch over nb frames (frame f reads slot first_slot + f
+// and writes the pyramid buffers at f * frame_pyr_bytes).
+void plan_pyramid(const Geometry& g, int T, PyrPlan& p);
+int upload_pyramid_plan(orbx_ctx* ctx);
+int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr_blur, int nb, hipStream_t st);
 // timing helpers (orbx_api.cpp)
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);

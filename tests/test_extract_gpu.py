@@ -115,3 +115,33 @@ def test_large_batch_paths_match_oracle():
         for lvl in (1, 4, 7):
             assert np.array_equal(ctx.level(s, lvl), ref.level(lvl)), (s, lvl)
     ctx.close()
+
+
+@pytest.mark.parametrize("kind,w,h,n,seed", CASES)
+def test_pyramid_modes_identical(kind, w, h, n, seed):
+    """The fused pyramid + blur launch (orbx_pyramid.hip) and the staged
+    launches give byte-identical padded levels, keypoints and descriptors, on
+    a two-frame batch (frame 1 flipped, so the two workgroups differ)."""
+    img = make(kind, w, h, seed)
+    frames = np.stack([img, img[::-1].copy()])
+    res = []
+    for mode in (0, 1):
+        ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=2)
+        ctx.set_pyramid_mode(mode)
+        ctx.upload(frames)
+        ctx.extract(0, 2)
+        ctx.sync()
+        if mode == 1 and (w, h) in ((640, 480), (96, 80), (333, 251)):
+            assert ctx.pyramid_fused(), "fused pyramid plan expected for this size"
+        if mode == 0:
+            assert not ctx.pyramid_fused()
+        res.append([(ctx.level(s, l), ctx.level(s, l, blurred=True)) for s in range(2) for l in range(8)]
+                   + [ctx.features(s) for s in range(2)])
+        ctx.close()
+    a, b = res
+    for i in range(16):
+        assert np.array_equal(a[i][0], b[i][0]), f"raw slot {i // 8} level {i % 8}"
+        assert np.array_equal(a[i][1], b[i][1]), f"blurred slot {i // 8} level {i % 8}"
+    for i in (16, 17):
+        assert_kps_equal(a[i][0], b[i][0])
+        assert np.array_equal(a[i][1], b[i][1])
