@@ -44,7 +44,7 @@ from orb_slam_amd import dist as odist, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 WORKLOADS = {
-    "c2": dict(w=640, h=480, nfeatures=1000, batch=256,
+    "c2": dict(w=640, h=480, nfeatures=1000, batch=1024,
                metric="frames/sec ORB extract+match (640x480, 1000 kp)", unit="frames/s",
                desc="640x480 mono8, 8 levels x1.2, 1000 kp: ORB extract + SearchForInitialization vs previous frame"),
     "c3": dict(w=1920, h=1080, nfeatures=2000, batch=64,
