@@ -101,6 +101,10 @@ __device__ inline unsigned long long lba_stamp()
 constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem
 constexpr int kLbaWaves = kLbaThreads / 64;
 constexpr int kSchurEdges = 8;                 // per-thread LDS edge table of the Schur pass (32 KB)
+#ifndef ORBX_SCHUR_GROUP
+#define ORBX_SCHUR_GROUP 2
+#endif
+constexpr int kSchurGroup = ORBX_SCHUR_GROUP;  // edges whose W_i Dinv share one pass over the later W_j
 
 
 
@@ -379,42 +383,61 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
 #pragma unroll
             for (int i = 0; i < 9; i++) v[i] = src[i];
         };
-        for (int qi = 0; qi < k; qi++) {
-            const int2 ei = edge_at(qi);
-            const int i1 = ei.y;
-            double2 cur[9];
-            load_hpl(ei.x, cur);   // W_i, also the first pair's W_j (qj == qi)
-            double wd[18];         // W_i Dinv (6x3)
+        // The point's edges in groups of kSchurGroup: the group's W_i Dinv
+        // blocks stay in registers while every later edge's W_j is loaded
+        // once for the whole group: k + ~k^2 / (2 G) Hpl reads per point
+        // instead of k (k + 1) / 2 (the pass re-read these blocks from HBM).
+        constexpr int G = kSchurGroup;
+        // S(i1, i2) -= (W_i Dinv) W_j^T over the 6x6 block (upper triangle of
+        // a diagonal block)
+        auto pair_update = [&](const double (&w)[18], int i1, const double2 (&bj2)[9], int i2) {
+            double bj[18];
 #pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double b0 = (r & 1) ? cur[(3 * r) >> 1].y : cur[(3 * r) >> 1].x;
-                const double b1 = (r & 1) ? cur[(3 * r + 1) >> 1].x : cur[(3 * r + 1) >> 1].y;
-                const double b2 = (r & 1) ? cur[(3 * r + 2) >> 1].y : cur[(3 * r + 2) >> 1].x;
-#pragma unroll
-                for (int c = 0; c < 3; c++) wd[r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
-                atomicAdd(&bs[6 * i1 + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
+            for (int i = 0; i < 9; i++) {
+                bj[2 * i] = bj2[i].x;
+                bj[2 * i + 1] = bj2[i].y;
             }
-            for (int qj = qi; qj < k; qj++) {
-                const int i2 = qj == qi ? i1 : edge_at(qj).y;
-                double2 nxt[9];
-                if (qj + 1 < k) load_hpl(edge_at(qj + 1).x, nxt);
-                double bj[18];
 #pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    bj[2 * i] = cur[i].x;
-                    bj[2 * i + 1] = cur[i].y;
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    if (i1 == i2 && c < r) continue;
+                    const double v = w[r * 3] * bj[c * 3] + w[r * 3 + 1] * bj[c * 3 + 1] + w[r * 3 + 2] * bj[c * 3 + 2];
+                    atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
                 }
+        };
+        for (int g = 0; g < k; g += G) {
+            double wd[G][18];   // W_i Dinv (6x3) of the group's edges
+            int pi[G];
+            double2 cur[9];
+            // the group's own W blocks, each loaded once: W_i Dinv, bs, and
+            // the pairs among the group's edges
 #pragma unroll
-                for (int r = 0; r < 6; r++)
+            for (int u = 0; u < G; u++) {
+                pi[u] = -1;
+                if (g + u < k) {
+                    const int2 ei = edge_at(g + u);
+                    pi[u] = ei.y;
+                    load_hpl(ei.x, cur);
 #pragma unroll
-                    for (int c = 0; c < 6; c++) {
-                        if (i1 == i2 && c < r) continue;
-                        const double v = wd[r * 3] * bj[c * 3] + wd[r * 3 + 1] * bj[c * 3 + 1] + wd[r * 3 + 2] * bj[c * 3 + 2];
-                        atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
+                    for (int r = 0; r < 6; r++) {
+                        const double b0 = (r & 1) ? cur[(3 * r) >> 1].y : cur[(3 * r) >> 1].x;
+                        const double b1 = (r & 1) ? cur[(3 * r + 1) >> 1].x : cur[(3 * r + 1) >> 1].y;
+                        const double b2 = (r & 1) ? cur[(3 * r + 2) >> 1].y : cur[(3 * r + 2) >> 1].x;
+#pragma unroll
+                        for (int c = 0; c < 3; c++) wd[u][r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
+                        atomicAdd(&bs[6 * ei.y + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
                     }
-                if (qj + 1 < k)
 #pragma unroll
-                    for (int i = 0; i < 9; i++) cur[i] = nxt[i];
+                    for (int v = 0; v <= u; v++) pair_update(wd[v], pi[v], cur, ei.y);
+                }
+            }
+            // every later edge's W_j, loaded once for the whole group
+            for (int qj = g + G; qj < k; qj++) {
+                const int2 ej = edge_at(qj);
+                load_hpl(ej.x, cur);
+#pragma unroll
+                for (int u = 0; u < G; u++) pair_update(wd[u], pi[u], cur, ej.y);
             }
         }
     }
