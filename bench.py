@@ -202,7 +202,7 @@ def run_pose(args, wl, rank, local, world, dist):
     arr, n_inl, st = ctx.pose_fetch()
     stats = np.array([elapsed, P * args.steps, int(n_inl[0]), st[0].rounds], dtype=np.float64)
     ab = {"pose": n_edges * 25 + 80 + 160}
-    units_per_launch = {"pose": P}
+    units_per_step = {"pose": P}
     flops = float(np.mean([pose_flops(st[i], int(frames[i]["has_mp"].sum())) for i in range(len(uniq))]))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -214,7 +214,7 @@ def run_pose(args, wl, rank, local, world, dist):
            "parallelism": f"dp{world} (independent frames per GPU)",
            "boundary": "frames staged in HBM before the timed region (orbx_pose_stage); results fetched after"}
     ctx.close()
-    return stats, kernels, ab, units_per_launch, cpu, check, cfg
+    return stats, kernels, ab, units_per_step, cpu, check, cfg
 
 
 def run_frames(args, wl, rank, local, world, dist):
@@ -268,7 +268,7 @@ def run_frames(args, wl, rank, local, world, dist):
     _, nm = ctx.matches(B - 1)
     stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
     ab = algorithmic_bytes(w, h, nf, "bf" if bf else "init")
-    units_per_launch = {k: B for k in ab}
+    units_per_step = {k: B for k in ab}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_frames(frames, nf, args.cpu_budget, bf=bf)
@@ -276,7 +276,7 @@ def run_frames(args, wl, rank, local, world, dist):
     cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf, "image": f"{w}x{h}",
            "parallelism": f"dp{world} (one sequence per GPU)"}
     ctx.close()
-    return stats, kernels, ab, units_per_launch, cpu, check, cfg
+    return stats, kernels, ab, units_per_step, cpu, check, cfg
 
 
 def run_lba(args, wl, rank, local, world, dist):
@@ -317,7 +317,10 @@ def run_lba(args, wl, rank, local, world, dist):
     stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
                      dtype=np.float64)
     ab = {"lba_iter": lba_bytes(22, 2000, n_edges), "lba_outliers": n_edges * 16}
-    units_per_launch = {"lba_iter": P, "lba_outliers": P}
+    # lba_bytes is per problem and LM iteration: every lba_iter launch runs one
+    # iteration of all P problems (5 + 10 launches per step), lba_outliers
+    # one pass over all P (2 per step)
+    units_per_step = {"lba_iter": P * 15, "lba_outliers": P * 2}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_lba(probs, args.cpu_budget)
@@ -327,7 +330,7 @@ def run_lba(args, wl, rank, local, world, dist):
            "parallelism": f"dp{world} (independent problems per GPU; replicas)",
            "boundary": "host arrays in/out (H2D/D2H inside the timed region)"}
     ctx.close()
-    return stats, kernels, ab, units_per_launch, cpu, check, cfg
+    return stats, kernels, ab, units_per_step, cpu, check, cfg
 
 
 # bench timer name -> kernel symbol in the rocprofv3 CSVs
@@ -455,8 +458,9 @@ def main():
 
         def roofline_events(kern, steps):
             # dominant kernel: largest total time; its algorithmic bytes per
-            # launch over its mean launch duration (HIP events on the stream
-            # the kernel is launched on)
+            # launch (bytes per unit x units per step / launches per step) over
+            # its mean launch duration (HIP events on the stream the kernel is
+            # launched on)
             timed_k = [k for k in kern if kern[k]["launches"]] or list(kern)
             dom = max(timed_k, key=lambda k: kern[k]["total_ms"])
             launches_per_step = max(1, kern[dom]["launches"] // steps)
