@@ -317,19 +317,26 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
         }
         return;
     }
+    // queries are the F1 octave-0 keypoints: the groups below stop after the
+    // last one (extractor output is level-major, so they are a prefix)
+    int last0 = -1;
     for (int i = tid; i < F1.n; i += kBlock) {
+        const orbx_keypoint k1 = F1.kps[i];
         s.m12[i] = -1;
         s.pushed[i] = -1;
-        s.ang1[i] = F1.kps[i].angle;
+        s.ang1[i] = k1.angle;
+        if (k1.octave == 0) last0 = i;
     }
     if (tid < 36) s.hist[tid] = 0;
+    __syncthreads();   // the staging scans' reads of bs are done
+    const int n1q = block_max(last0, bs, 0) + 1;
     __syncthreads();
     MP_MARK(0);
     const float r = (float)window;
     const int wv = tid >> 6;
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int g0 = 0; g0 < F1.n; g0 += kBlock) {
-        const int gn = min(kBlock, F1.n - g0);
+    for (int g0 = 0; g0 < n1q; g0 += kBlock) {
+        const int gn = min(kBlock, n1q - g0);
         // stage the group's queries (one thread each): position, cell range,
         // descriptor; inactive (octave > 0 or empty area) get an empty range
         {
