@@ -652,6 +652,166 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     if (threadIdx.x == 0) n_out[blockIdx.x] = s_cnt;
 }
 
+// Structures of the second optimize() (src/Optimizer.cc:472-478: the edges
+// the first outlier pass set to level 1 leave the graph) built on the device
+// from the first pass's: g2o's initializeOptimization / buildStructure
+// restated as order-preserving filters of the first pass's sorted lists
+// (active edges keep their original order, free poses / points their id
+// order, every CSR list its edge or pose order), so the result equals the
+// host build_struct on the reduced edge set.  One workgroup per problem;
+// the first pass's Hpl and Hll scratch (dead until the second pass
+// linearises) hold the index maps.  B's pointer fields are set by the host.
+__global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, LbaDev* d1s, const uint8_t* status_all,
+                                                             const long long* offs)
+{
+    __shared__ BlockScratchN<kLbaWaves> bs;
+    const LbaDev& A = d0s[blockIdx.x];
+    LbaDev& B = d1s[blockIdx.x];
+    const uint8_t* st = status_all + offs[3 * blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nE0 = A.nE, nP0 = A.nP, nL0 = A.nL;
+    int* na = reinterpret_cast<int*>(A.ce);     // [nE0] new edge index or -1
+    int* ph1 = reinterpret_cast<int*>(A.hp);    // [nP0] new pose hessian index or -1, then counts
+    int* cp = ph1 + nP0;                        // [nP0] kept edges per pose
+    int* lh1 = reinterpret_cast<int*>(A.hl);    // [nL0] new point index or -1
+    int* cl = lh1 + nL0;                        // [nL0] kept edges per point
+    int* cc = cl + nL0;                         // [nL0] kept Schur-column edges per point
+    auto kept = [&](int a0) { return st[A.e_orig[a0]] == 0; };
+    // 1. edges: new index by a block scan over the kept flags (edge order)
+    int base = 0;
+    for (int c = 0; c < nE0; c += kLbaThreads) {
+        const int a0 = c + tid;
+        const int k = a0 < nE0 && kept(a0) ? 1 : 0;
+        int tot;
+        const int off = block_exclusive_scan<kLbaWaves>(k, &tot, bs, (c / kLbaThreads) & 1);
+        if (a0 < nE0) na[a0] = k ? base + off : -1;
+        base += tot;
+    }
+    const int nE1 = base;
+    __syncthreads();
+    // 2. kept edges per pose (wave per pose) and per point (thread per point)
+    for (int p = wv; p < nP0; p += kLbaWaves) {
+        int cnt = 0;
+        for (int q = A.pe_ptr[p] + lane; q < A.pe_ptr[p + 1]; q += 64) cnt += na[A.pe_idx[q]] >= 0;
+        cnt = wave_sum(cnt);
+        if (lane == 0) cp[p] = cnt;
+    }
+    for (int l = tid; l < nL0; l += kLbaThreads) {
+        int c1 = 0, c2 = 0;
+        for (int q = A.le_ptr[l]; q < A.le_ptr[l + 1]; q++) c1 += na[A.le_idx[q]] >= 0;
+        for (int q = A.lc_ptr[l]; q < A.lc_ptr[l + 1]; q++) c2 += na[A.lc_idx[q]] >= 0;
+        cl[l] = c1;
+        cc[l] = c2;
+    }
+    __syncthreads();
+    // 3. new pose / point indices and list offsets: scans over the active ones
+    int nP1 = 0, pe_base = 0;
+    for (int c = 0; c < nP0; c += kLbaThreads) {
+        const int p = c + tid;
+        const int act = p < nP0 && cp[p] > 0 ? 1 : 0;
+        int tot, tot2;
+        const int idx = block_exclusive_scan<kLbaWaves>(act, &tot, bs, 0);
+        const int eo = block_exclusive_scan<kLbaWaves>(act ? cp[p] : 0, &tot2, bs, 1);
+        if (p < nP0) {
+            const int p1 = act ? nP1 + idx : -1;
+            if (act) {
+                const_cast<int*>(B.iv_pose)[p1] = A.iv_pose[p];
+                const_cast<int*>(B.pe_ptr)[p1] = pe_base + eo;
+            }
+            ph1[p] = p1;
+        }
+        nP1 += tot;
+        pe_base += tot2;
+        __syncthreads();   // bs reads done before the next round's scans
+    }
+    int nL1 = 0, le_base = 0, lc_base = 0;
+    for (int c = 0; c < nL0; c += kLbaThreads) {
+        const int l = c + tid;
+        const int act = l < nL0 && cl[l] > 0 ? 1 : 0;
+        int tot, tot2, tot3;
+        const int idx = block_exclusive_scan<kLbaWaves>(act, &tot, bs, 0);
+        const int eo = block_exclusive_scan<kLbaWaves>(act ? cl[l] : 0, &tot2, bs, 1);
+        const int co = block_exclusive_scan<kLbaWaves>(act ? cc[l] : 0, &tot3, bs, 0);
+        if (l < nL0) {
+            const int l1 = act ? nL1 + idx : -1;
+            if (act) {
+                const_cast<int*>(B.iv_point)[l1] = A.iv_point[l];
+                const_cast<int*>(B.le_ptr)[l1] = le_base + eo;
+                const_cast<int*>(B.lc_ptr)[l1] = lc_base + co;
+            }
+            lh1[l] = l1;
+        }
+        nL1 += tot;
+        le_base += tot2;
+        lc_base += tot3;
+        __syncthreads();   // bs reads done before the next round's scans
+    }
+    if (tid == 0) {
+        const_cast<int*>(B.pe_ptr)[nP1] = pe_base;
+        const_cast<int*>(B.le_ptr)[nL1] = le_base;
+        const_cast<int*>(B.lc_ptr)[nL1] = lc_base;
+    }
+    __syncthreads();
+    // 4. the kept edges' records, remapped
+    for (int a0 = tid; a0 < nE0; a0 += kLbaThreads) {
+        const int a1 = na[a0];
+        if (a1 < 0) continue;
+        const int ph = A.e_ph[a0];
+        const_cast<int*>(B.e_orig)[a1] = A.e_orig[a0];
+        const_cast<int*>(B.e_pose)[a1] = A.e_pose[a0];
+        const_cast<int*>(B.e_point)[a1] = A.e_point[a0];
+        const_cast<int*>(B.e_ph)[a1] = ph >= 0 ? ph1[ph] : -1;
+        const_cast<int*>(B.e_lh)[a1] = lh1[A.e_lh[a0]];
+        const_cast<double*>(B.e_obs)[2 * a1] = A.e_obs[2 * a0];
+        const_cast<double*>(B.e_obs)[2 * a1 + 1] = A.e_obs[2 * a0 + 1];
+        const_cast<double*>(B.e_isig)[a1] = A.e_isig[a0];
+    }
+    // 5. CSR lists: filters of the first pass's lists (wave per pose, with a
+    //    ballot compaction; thread per point)
+    for (int p = wv; p < nP0; p += kLbaWaves) {
+        const int p1 = ph1[p];
+        if (p1 < 0) continue;
+        int w = B.pe_ptr[p1];
+        for (int q0 = A.pe_ptr[p]; q0 < A.pe_ptr[p + 1]; q0 += 64) {
+            const int q = q0 + lane;
+            const int a1 = q < A.pe_ptr[p + 1] ? na[A.pe_idx[q]] : -1;
+            const unsigned long long bal = __ballot(a1 >= 0);
+            if (a1 >= 0) {
+                const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                const_cast<int*>(B.pe_idx)[w + __popcll(bal & lt)] = a1;
+            }
+            w += __popcll(bal);
+        }
+    }
+    for (int l = tid; l < nL0; l += kLbaThreads) {
+        const int l1 = lh1[l];
+        if (l1 < 0) continue;
+        int w = B.le_ptr[l1];
+        for (int q = A.le_ptr[l]; q < A.le_ptr[l + 1]; q++) {
+            const int a1 = na[A.le_idx[q]];
+            if (a1 >= 0) const_cast<int*>(B.le_idx)[w++] = a1;
+        }
+        w = B.lc_ptr[l1];
+        for (int q = A.lc_ptr[l]; q < A.lc_ptr[l + 1]; q++) {
+            const int a1 = na[A.lc_idx[q]];
+            if (a1 >= 0) const_cast<int*>(B.lc_idx)[w++] = a1;
+        }
+    }
+    if (tid == 0) {
+        B.nP = nP1;
+        B.nL = nL1;
+        B.nE = nE1;
+        B.dim_p = 6 * nP1;
+        B.lambda = 0;
+        B.ni = 2;
+        B.current_chi = B.last_chi = B.chi2_initial = 0;
+        B.nBad = 0;
+        B.status = kRunning;
+        B.iterations = B.trials = B.not_posdef = 0;
+        B.abort = A.abort;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Host: structure build (initializeOptimization + buildStructure) and driver
 // ---------------------------------------------------------------------------
@@ -850,7 +1010,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     const size_t o_all_st = at;   at += align256((size_t)eacc);
     const size_t o_all_bad = at;  at += align256((size_t)pacc);
     const size_t o_offs = at;     at += align256(offs.size() * 8);
-    const size_t o_nout = at;     at += align256(4 * (size_t)P);
+    const size_t o_nout = at;     at += align256(8 * (size_t)P);   // outliers per problem, per pass
     const size_t base_bytes = at;
     std::vector<uint8_t> all_st((size_t)eacc, 0);
     std::vector<LbaDev> devs(P);
@@ -862,84 +1022,89 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     if (!ctx->lba_host) ctx->lba_host = std::make_shared<HostCache>();
     std::vector<HostStruct>& hs = static_cast<HostCache*>(ctx->lba_host.get())->hs;
     if ((int)hs.size() < P) hs.resize(P);
-    for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
-        host_parallel(P, [&](int i) {
-            build_struct(probs[i], pass == 0 ? nullptr : all_st.data() + offs[3 * i], hs[i]);
-        });
-        mark("build_struct");
-        // ---- per-pass structures after the persistent block ----
-        constexpr int kArr = 15;
-        std::vector<size_t> so(kArr * (size_t)P);
-        size_t end = base_bytes;
-        for (int i = 0; i < P; i++) {
-            const HostStruct& h = hs[i];
-            const size_t bytes[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
-                                        h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
-                                        h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
-                                        h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
-                                        h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
-            for (int k = 0; k < kArr; k++) {
-                so[kArr * i + k] = end;
-                end += align256(bytes[k]);
-            }
+    // The first pass's structures are built on host threads; the second
+    // pass's are built on the device from them (k_lba_rebuild) right after
+    // the first outlier pass, so both optimize() calls run back to back with
+    // no host round trip.  Layout after the persistent block: the first
+    // pass's staged arrays, both LbaDev arrays (the second one's pointers
+    // staged by the host, its counts written by the rebuild), the second
+    // pass's arrays (device-written, first-pass sizes), the device scratch.
+    host_parallel(P, [&](int i) { build_struct(probs[i], nullptr, hs[i]); });
+    mark("build_struct");
+    constexpr int kArr = 15;
+    std::vector<size_t> so(kArr * (size_t)P), so1(kArr * (size_t)P);
+    auto arr_bytes = [&](const HostStruct& h, size_t (&bytes)[kArr]) {
+        const size_t b[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
+                                h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
+                                h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
+                                h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
+                                h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
+        for (int k = 0; k < kArr; k++) bytes[k] = b[k];
+    };
+    size_t end = base_bytes;
+    for (int i = 0; i < P; i++) {
+        size_t bytes[kArr];
+        arr_bytes(hs[i], bytes);
+        for (int k = 0; k < kArr; k++) {
+            so[kArr * i + k] = end;
+            end += align256(bytes[k]);
         }
-        const size_t o_devs = end;
-        end += align256(sizeof(LbaDev) * P);
-        const size_t staged_end = end;
-        // device-only scratch after the staged block (never copied)
-        std::vector<size_t> sc(8 * (size_t)P);
-        for (int i = 0; i < P; i++) {
-            const HostStruct& h = hs[i];
-            const size_t nE = h.e_orig.size(), n = 6 * (size_t)h.nP;
-            const size_t bytes[7] = {18 * nE * 8, 27 * (size_t)h.nP * 8, 9 * (size_t)h.nL * 8, 12 * (size_t)h.nL * 8,
-                                     n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * (size_t)h.nL) * 8, n * 8 + 8};
-            for (int k = 0; k < 7; k++) {
-                sc[8 * i + k] = end;
-                end += align256(bytes[k]);
-            }
+    }
+    const size_t o_devs = end;
+    end += align256(sizeof(LbaDev) * P);
+    const size_t o_devs1 = end;
+    end += align256(sizeof(LbaDev) * P);
+    const size_t staged_end = end;
+    for (int i = 0; i < P; i++) {
+        size_t bytes[kArr];
+        arr_bytes(hs[i], bytes);
+        for (int k = 0; k < kArr; k++) {
+            so1[kArr * i + k] = end;
+            end += align256(bytes[k]);
         }
-        const size_t dev_end = end;
-        if (dev_end > ctx->scratch_bytes) {
-            if (pass == 1) {   // keep the device-resident state across the reallocation
-                if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) break;
-                ORBX_HIP_CHECK(hipMemcpy(ctx->host_pinned, ctx->scratch, base_bytes, hipMemcpyDeviceToHost));
-            }
-            if ((r = ensure_scratch(ctx, dev_end)) != ORBX_OK) break;
-            if (pass == 1)
-                ORBX_HIP_CHECK(hipMemcpy(ctx->scratch, ctx->host_pinned, base_bytes, hipMemcpyHostToDevice));
+    }
+    // device-only scratch (never copied), sized by the first pass
+    std::vector<size_t> sc(8 * (size_t)P);
+    for (int i = 0; i < P; i++) {
+        const HostStruct& h = hs[i];
+        const size_t nE = h.e_orig.size(), n = 6 * (size_t)h.nP;
+        const size_t bytes[7] = {18 * nE * 8, 27 * (size_t)h.nP * 8, 9 * (size_t)h.nL * 8, 12 * (size_t)h.nL * 8,
+                                 n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * (size_t)h.nL) * 8, n * 8 + 8};
+        for (int k = 0; k < 7; k++) {
+            sc[8 * i + k] = end;
+            end += align256(bytes[k]);
         }
-        if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) break;
-        uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
-        uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
-        // fill the staged bytes on host threads
-        host_parallel(P, [&](int i) {
-            const orbx_ba_problem& p = probs[i];
-            const HostStruct& h = hs[i];
-            if (pass == 0) {
-                double* pose = reinterpret_cast<double*>(hb + pl[i].pose);
-                for (int k = 0; k < p.n_poses; k++) {
-                    for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
-                    for (int j = 0; j < 3; j++) pose[7 * k + 4 + j] = p.pose_t[3 * k + j];
-                }
-                std::memcpy(hb + pl[i].point, p.points, 3 * (size_t)p.n_points * 8);
-                std::memcpy(hb + pl[i].cam, p.pose_cam, 4 * (size_t)p.n_poses * 8);
-                std::memset(hb + pl[i].err, 0, 2 * (size_t)p.n_edges * 8);
-                std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
-                std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
-                std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
-            }
-            const void* src[kArr] = {h.e_orig.data(), h.e_pose.data(), h.e_point.data(), h.e_ph.data(),
-                                     h.e_lh.data(),   h.e_obs.data(),  h.e_isig.data(),  h.iv_pose.data(),
-                                     h.iv_point.data(), h.pe_ptr.data(), h.pe_idx.data(), h.le_ptr.data(),
-                                     h.le_idx.data(), h.lc_ptr.data(), h.lc_idx.data()};
-            const size_t bytes[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
-                                        h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
-                                        h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
-                                        h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
-                                        h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
-            for (int k = 0; k < kArr; k++)
-                if (bytes[k]) std::memcpy(hb + so[kArr * i + k], src[k], bytes[k]);
-            LbaDev& D = devs[i];
+    }
+    const size_t dev_end = end;
+    if (dev_end > ctx->scratch_bytes && (r = ensure_scratch(ctx, dev_end)) != ORBX_OK) return r;
+    if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) return r;
+    uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    std::vector<LbaDev> devs1(P);
+    // fill the staged bytes on host threads
+    host_parallel(P, [&](int i) {
+        const orbx_ba_problem& p = probs[i];
+        const HostStruct& h = hs[i];
+        double* pose = reinterpret_cast<double*>(hb + pl[i].pose);
+        for (int k = 0; k < p.n_poses; k++) {
+            for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
+            for (int j = 0; j < 3; j++) pose[7 * k + 4 + j] = p.pose_t[3 * k + j];
+        }
+        std::memcpy(hb + pl[i].point, p.points, 3 * (size_t)p.n_points * 8);
+        std::memcpy(hb + pl[i].cam, p.pose_cam, 4 * (size_t)p.n_poses * 8);
+        std::memset(hb + pl[i].err, 0, 2 * (size_t)p.n_edges * 8);
+        std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
+        std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
+        std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
+        const void* src[kArr] = {h.e_orig.data(), h.e_pose.data(), h.e_point.data(), h.e_ph.data(),
+                                 h.e_lh.data(),   h.e_obs.data(),  h.e_isig.data(),  h.iv_pose.data(),
+                                 h.iv_point.data(), h.pe_ptr.data(), h.pe_idx.data(), h.le_ptr.data(),
+                                 h.le_idx.data(), h.lc_ptr.data(), h.lc_idx.data()};
+        size_t bytes[kArr];
+        arr_bytes(h, bytes);
+        for (int k = 0; k < kArr; k++)
+            if (bytes[k]) std::memcpy(hb + so[kArr * i + k], src[k], bytes[k]);
+        auto fill = [&](LbaDev& D, const size_t* o) {
             D = LbaDev{};
             D.nP = h.nP;
             D.nL = h.nL;
@@ -954,7 +1119,6 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             D.point_bk = reinterpret_cast<double*>(d + pl[i].pointbk);
             D.cam = reinterpret_cast<const double*>(d + pl[i].cam);
             D.err = reinterpret_cast<double*>(d + pl[i].err);
-            const size_t* o = &so[kArr * i];
             D.e_orig = reinterpret_cast<const int*>(d + o[0]);
             D.e_pose = reinterpret_cast<const int*>(d + o[1]);
             D.e_point = reinterpret_cast<const int*>(d + o[2]);
@@ -981,28 +1145,39 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             D.huber_delta = p.huber_delta;
             D.status = kRunning;
             D.ni = 2;
-        });
-        if (pass == 0) std::memcpy(hb + o_offs, offs.data(), offs.size() * 8);
-        std::memcpy(hb + o_devs, devs.data(), sizeof(LbaDev) * P);
-        mark("pack");
-        // pass 0: everything; pass 1: only the per-pass structures (the
-        // persistent block - poses, points, errors, status - stays on device)
-        const size_t up0 = pass == 0 ? 0 : base_bytes;
-        ORBX_HIP_CHECK(hipMemcpyAsync(d + up0, hb + up0, staged_end - up0, hipMemcpyHostToDevice, ctx->stream));
-        mark("upload");
-        LbaDev* dd = reinterpret_cast<LbaDev*>(d + o_devs);
+        };
+        fill(devs[i], &so[kArr * i]);
+        fill(devs1[i], &so1[kArr * i]);   // counts and contents: k_lba_rebuild
+    });
+    std::memcpy(hb + o_offs, offs.data(), offs.size() * 8);
+    std::memcpy(hb + o_devs, devs.data(), sizeof(LbaDev) * P);
+    std::memcpy(hb + o_devs1, devs1.data(), sizeof(LbaDev) * P);
+    mark("pack");
+    ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, staged_end, hipMemcpyHostToDevice, ctx->stream));
+    mark("upload");
+    size_t max_n2 = 0;
+    for (int i = 0; i < P; i++)
+        max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p + (size_t)devs[i].dim_p);
+    const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
+    const int lds_cap = (int)(lds / 8);
+    for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
+        LbaDev* dd = reinterpret_cast<LbaDev*>(d + (pass == 0 ? o_devs : o_devs1));
+        if (pass == 1) {
+            timer_begin(ctx, "lba_rebuild");
+            hipLaunchKernelGGL(k_lba_rebuild, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
+                               reinterpret_cast<const LbaDev*>(d + o_devs), dd, d + o_all_st,
+                               reinterpret_cast<const long long*>(d + o_offs));
+            timer_end(ctx, "lba_rebuild");
+            ORBX_HIP_CHECK(hipGetLastError());
+        }
         const int iters = pass == 0 ? iters0 : iters1;
-        size_t max_n2 = 0;
-        for (int i = 0; i < P; i++)
-            max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p + (size_t)devs[i].dim_p);
-        const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;
-        const int lds_cap = (int)(lds / 8);
         for (int it = 0; it < iters; it++) {
             if (abort && *abort) {
                 const int one = 1;
                 for (int i = 0; i < P; i++)
-                    ORBX_HIP_CHECK(hipMemcpy(reinterpret_cast<uint8_t*>(dd + i) + offsetof(LbaDev, abort), &one, 4,
-                                             hipMemcpyHostToDevice));
+                    ORBX_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(dd + i) + offsetof(LbaDev, abort), &one, 4,
+                                                  hipMemcpyHostToDevice, ctx->stream));
+                ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
                 break;
             }
             timer_begin(ctx, "lba_iter");
@@ -1014,44 +1189,45 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             // without one, iterations are queued back to back and a
             // terminated problem's later launches return immediately.
             if (abort) {
-                ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+                std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
+                ORBX_HIP_CHECK(hipMemcpyAsync(hv.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
                 ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
                 bool running = false;
-                for (int i = 0; i < P; i++) running |= devs[i].status == kRunning;
+                for (int i = 0; i < P; i++) running |= hv[i].status == kRunning;
                 if (!running) break;
             }
         }
         timer_begin(ctx, "lba_outliers");
         hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(256), 0, ctx->stream, dd,
                            reinterpret_cast<int*>(d + o_all_nobs), d + o_all_st, d + o_all_bad, pass + 1,
-                           probs[0].chi2_threshold, reinterpret_cast<int*>(d + o_nout),
+                           probs[0].chi2_threshold, reinterpret_cast<int*>(d + o_nout) + pass * P,
                            reinterpret_cast<const long long*>(d + o_offs));
         timer_end(ctx, "lba_outliers");
         ORBX_HIP_CHECK(hipGetLastError());
-        std::vector<int> nout(P);
-        ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-        ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
-        ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + o_nout, 4 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
-        ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        mark("iterations+outliers");
-        if (stats)
-            for (int i = 0; i < P; i++) {
-                stats[i].iterations[pass] = devs[i].iterations;
-                stats[i].levenberg_trials[pass] = devs[i].trials;
-                stats[i].chi2_initial[pass] = devs[i].chi2_initial;
-                stats[i].chi2_final[pass] = devs[i].last_chi;
-                stats[i].n_outliers[pass] = nout[i];
-                stats[i].not_posdef += devs[i].not_posdef;
-            }
     }
-    if (r != ORBX_OK) return r;
-    // results: poses and points in one copy, scattered on host threads
-    uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb, ctx->scratch, result_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb + o_all_bad, static_cast<uint8_t*>(ctx->scratch) + o_all_bad, (size_t)pacc,
-                                  hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<int> nout(2 * (size_t)P);
+    ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), d + o_devs, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(devs1.data(), d + o_devs1, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + o_nout, 8 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
+    // results: poses and points in one copy, scattered on host threads below
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, result_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb + o_all_bad, d + o_all_bad, (size_t)pacc, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    mark("results copy");
+    mark("iterations+outliers+results copy");
+    if (stats)
+        for (int pass = 0; pass < 2; pass++) {
+            const std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
+            for (int i = 0; i < P; i++) {
+                stats[i].iterations[pass] = hv[i].iterations;
+                stats[i].levenberg_trials[pass] = hv[i].trials;
+                stats[i].chi2_initial[pass] = hv[i].chi2_initial;
+                stats[i].chi2_final[pass] = hv[i].last_chi;
+                stats[i].n_outliers[pass] = nout[pass * (size_t)P + i];
+                stats[i].not_posdef += hv[i].not_posdef;
+            }
+        }
+
     host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
         const double* pose = reinterpret_cast<const double*>(hb + pl[i].pose);
