@@ -47,7 +47,7 @@ WORKLOADS = {
     "c2": dict(w=640, h=480, nfeatures=1000, batch=1024,
                metric="frames/sec ORB extract+match (640x480, 1000 kp)", unit="frames/s",
                desc="640x480 mono8, 8 levels x1.2, 1000 kp: ORB extract + SearchForInitialization vs previous frame"),
-    "c3": dict(w=1920, h=1080, nfeatures=2000, batch=64,
+    "c3": dict(w=1920, h=1080, nfeatures=2000, batch=128,
                metric="pairs/sec ORB extract + brute-force Hamming match (1920x1080, 2000 kp)", unit="pairs/s",
                desc="1920x1080 mono8, 8 levels x1.2, 2000 kp: ORB extract + brute-force Hamming vs previous frame"),
     "c5": dict(batch=256, metric="local BA problems/sec (20 KF x 2000 MP, 5+10 LM iterations)", unit="problems/s",
