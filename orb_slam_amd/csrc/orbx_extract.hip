@@ -179,6 +179,30 @@ __global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a, int q_lo, int
     const int py = idx / nbord, k = idx - py * nbord;
     const int q = k < q_lo ? k : k + nint, px0 = 16 * q;
     const uint8_t* row = src + (size_t)reflect101(py - kEdge, L.h) * a.w;
+    if (kEdge == 16 && a.w % 16 == 0 && a.w >= 32) {
+        // aligned rows: the left border word is frame bytes 16 .. 1, the word
+        // after the last 16 interior bytes is bytes w-2 .. w-17 (byte permutes
+        // of two aligned loads), the rest of the row is zero
+        const int w16 = a.w >> 4;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (q == 0) {
+            const uint4 A = *reinterpret_cast<const uint4*>(row), B = *reinterpret_cast<const uint4*>(row + 16);
+            v.x = __builtin_amdgcn_perm(B.x, A.w, 0x01020304u);
+            v.y = __builtin_amdgcn_perm(A.w, A.z, 0x01020304u);
+            v.z = __builtin_amdgcn_perm(A.z, A.y, 0x01020304u);
+            v.w = __builtin_amdgcn_perm(A.y, A.x, 0x01020304u);
+        } else if (q <= w16) {
+            v = *reinterpret_cast<const uint4*>(row + 16 * (q - 1));
+        } else if (q == w16 + 1) {
+            const uint4 A = *reinterpret_cast<const uint4*>(row + a.w - 32), B = *reinterpret_cast<const uint4*>(row + a.w - 16);
+            v.x = __builtin_amdgcn_perm(B.w, B.z, 0x03040506u);
+            v.y = __builtin_amdgcn_perm(B.z, B.y, 0x03040506u);
+            v.z = __builtin_amdgcn_perm(B.y, B.x, 0x03040506u);
+            v.w = __builtin_amdgcn_perm(B.x, A.w, 0x03040506u);
+        }
+        *reinterpret_cast<uint4*>(dst + (size_t)py * L.stride + px0) = v;
+        return;
+    }
     uint8_t v[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) v[i] = px0 + i < L.pw ? row[reflect101(px0 + i - kEdge, L.w)] : 0;
