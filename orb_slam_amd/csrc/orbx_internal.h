@@ -226,10 +226,6 @@ struct orbx_ctx {
     std::vector<int32_t> pose_edge_kp;     // edge -> keypoint index (frame-local)
     std::vector<long long> pose_e0;        // first edge of each frame
     bool pose_ran = false;
-    // host-side local-BA structures (orbx_lba.hip), kept between calls so
-    // their capacity is reused: freeing and refaulting ~1 MB per problem cost
-    // more than building them
-    std::shared_ptr<void> lba_host;
     // timing
     bool timing = false;
     std::string timing_only;   // non-empty: only this timer records (orbx_dev_kernel_time_select)

@@ -67,6 +67,14 @@ struct LbaDev {
     double* S;                     // [dim_p][dim_p] (global fallback)
     double* x;                     // [dim_p + 3 nL]
     double* bs;                    // [dim_p]
+    // the caller's problem arrays (staged; read by k_lba_build only)
+    const int* r_edge_pose;
+    const int* r_edge_point;
+    const double* r_edge_obs;
+    const double* r_edge_isig;
+    const uint8_t* r_pose_fixed;
+    const long long* r_pose_id;
+    const long long* r_point_id;
     double huber_delta;
     // LM state
     double lambda, ni, current_chi, last_chi, chi2_initial;
@@ -652,13 +660,193 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     if (threadIdx.x == 0) n_out[blockIdx.x] = s_cnt;
 }
 
+// Structures of the first optimize() built on the device from the caller's
+// arrays: g2o's initializeOptimization + BlockSolver::buildStructure
+// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295) on the subset
+// LocalBundleAdjustment uses.  Every edge is active; the free poses with an
+// edge and the points with an edge are ordered by g2o vertex id (ties by
+// index: a stable sort), which fixes the Hessian block order; per free pose
+// and per point the active edges in edge order (CSR); per point its edges to
+// free poses in pose-block order (the Schur columns).  Ranks come from a
+// scan when the ids are already increasing (the caller's usual order) and
+// from pairwise counts otherwise.  One workgroup per problem; the Hpl
+// scratch (dead until linearisation) holds the index maps.
+__device__ inline void lba_rank(const long long* id, const int* act, int n, int* rank, int* count,
+                                BlockScratchN<kLbaWaves>& bs)
+{
+    const int tid = threadIdx.x;
+    int unsorted = 0;
+    for (int i = tid; i + 1 < n; i += kLbaThreads) unsorted |= !(id[i] < id[i + 1]);
+    unsorted = block_sum<kLbaWaves>(unsorted, bs, 0);
+    __syncthreads();
+    int total = 0;
+    if (!unsorted) {
+        int base = 0;
+        for (int c = 0; c < n; c += kLbaThreads) {
+            const int i = c + tid;
+            const int a = i < n ? act[i] : 0;
+            int tot;
+            const int off = block_exclusive_scan<kLbaWaves>(a, &tot, bs, (c / kLbaThreads) & 1);
+            if (i < n) rank[i] = a ? base + off : -1;
+            base += tot;
+        }
+        total = base;
+    } else {
+        int cnt = 0;
+        for (int i = tid; i < n; i += kLbaThreads) {
+            if (!act[i]) {
+                rank[i] = -1;
+                continue;
+            }
+            cnt++;
+            const long long v = id[i];
+            int r = 0;
+            for (int j = 0; j < n; j++) r += act[j] && (id[j] < v || (id[j] == v && j < i));
+            rank[i] = r;
+        }
+        total = block_sum<kLbaWaves>(cnt, bs, 1);
+    }
+    __syncthreads();
+    *count = total;
+}
+
+__global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
+{
+    __shared__ BlockScratchN<kLbaWaves> bs;
+    LbaDev& A = probs[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int NP = A.nposes_all, NL = A.npoints_all, E = A.nedges_all;
+    int* pflag = reinterpret_cast<int*>(A.ce);   // [NP] pose has an edge and is free
+    int* lflag = pflag + NP;                     // [NL] point has an edge
+    int* ph = lflag + NL;                        // [NP] pose block or -1
+    int* lh = ph + NP;                           // [NL] point block or -1
+    int* cur = lh + NL;                          // [NL] list cursors
+    for (int i = tid; i < NP; i += kLbaThreads) pflag[i] = 0;
+    for (int i = tid; i < NL; i += kLbaThreads) lflag[i] = 0;
+    __syncthreads();
+    for (int a = tid; a < E; a += kLbaThreads) {
+        const int p = A.r_edge_pose[a];
+        if (!A.r_pose_fixed[p]) pflag[p] = 1;
+        lflag[A.r_edge_point[a]] = 1;
+    }
+    __syncthreads();
+    int nP, nL;
+    lba_rank(A.r_pose_id, pflag, NP, ph, &nP, bs);
+    lba_rank(A.r_point_id, lflag, NL, lh, &nL, bs);
+    int* iv_pose = const_cast<int*>(A.iv_pose);
+    int* iv_point = const_cast<int*>(A.iv_point);
+    for (int i = tid; i < NP; i += kLbaThreads)
+        if (ph[i] >= 0) iv_pose[ph[i]] = i;
+    for (int i = tid; i < NL; i += kLbaThreads)
+        if (lh[i] >= 0) iv_point[lh[i]] = i;
+    // edge records (every edge active, original order)
+    int* pe_ptr = const_cast<int*>(A.pe_ptr);
+    int* le_ptr = const_cast<int*>(A.le_ptr);
+    int* lc_ptr = const_cast<int*>(A.lc_ptr);
+    for (int i = tid; i <= nP; i += kLbaThreads) pe_ptr[i] = 0;
+    for (int i = tid; i <= nL; i += kLbaThreads) {
+        le_ptr[i] = 0;
+        lc_ptr[i] = 0;
+    }
+    __syncthreads();
+    for (int a = tid; a < E; a += kLbaThreads) {
+        const int p = A.r_edge_pose[a], l = A.r_edge_point[a];
+        const int eph = ph[p], elh = lh[l];
+        const_cast<int*>(A.e_orig)[a] = a;
+        const_cast<int*>(A.e_pose)[a] = p;
+        const_cast<int*>(A.e_point)[a] = l;
+        const_cast<int*>(A.e_ph)[a] = eph;
+        const_cast<int*>(A.e_lh)[a] = elh;
+        const_cast<double*>(A.e_obs)[2 * a] = A.r_edge_obs[2 * a];
+        const_cast<double*>(A.e_obs)[2 * a + 1] = A.r_edge_obs[2 * a + 1];
+        const_cast<double*>(A.e_isig)[a] = A.r_edge_isig[a];
+        if (eph >= 0) {
+            atomicAdd(&pe_ptr[eph + 1], 1);
+            atomicAdd(&lc_ptr[elh + 1], 1);
+        }
+        atomicAdd(&le_ptr[elh + 1], 1);
+    }
+    __syncthreads();
+    // counts -> offsets (block scans)
+    auto offsets = [&](int* ptr, int n) {
+        int base = 0;
+        for (int c = 0; c < n; c += kLbaThreads) {
+            const int i = c + tid;
+            const int v = i < n ? ptr[i + 1] : 0;
+            int tot;
+            const int inc = block_exclusive_scan<kLbaWaves>(v, &tot, bs, (c / kLbaThreads) & 1) + v;
+            __syncthreads();
+            if (i < n) ptr[i + 1] = base + inc;
+            base += tot;
+            __syncthreads();
+        }
+    };
+    offsets(pe_ptr, nP);
+    offsets(le_ptr, nL);
+    offsets(lc_ptr, nL);
+    __syncthreads();
+    // per free pose, its edges in edge order (wave per pose, ballot compaction)
+    int* pe_idx = const_cast<int*>(A.pe_idx);
+    for (int p1 = wv; p1 < nP; p1 += kLbaWaves) {
+        const int pose = iv_pose[p1];
+        int w = pe_ptr[p1];
+        for (int a0 = 0; a0 < E; a0 += 64) {
+            const int a = a0 + lane;
+            const bool mine = a < E && A.r_edge_pose[a] == pose;
+            const unsigned long long bal = __ballot(mine);
+            if (mine) pe_idx[w + __popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull))] = a;
+            w += __popcll(bal);
+        }
+    }
+    // per point: its edges appended, then put in edge order (few per point);
+    // its Schur columns: the edges to free poses, in pose-block order
+    int* le_idx = const_cast<int*>(A.le_idx);
+    int* lc_idx = const_cast<int*>(A.lc_idx);
+    for (int l1 = tid; l1 < nL; l1 += kLbaThreads) cur[l1] = le_ptr[l1];
+    __syncthreads();
+    for (int a = tid; a < E; a += kLbaThreads) le_idx[atomicAdd(&cur[lh[A.r_edge_point[a]]], 1)] = a;
+    __syncthreads();
+    for (int l1 = tid; l1 < nL; l1 += kLbaThreads) {
+        const int q0 = le_ptr[l1], q1 = le_ptr[l1 + 1];
+        for (int i = q0 + 1; i < q1; i++) {   // insertion sort by edge index
+            const int x = le_idx[i];
+            int j = i - 1;
+            while (j >= q0 && le_idx[j] > x) {
+                le_idx[j + 1] = le_idx[j];
+                j--;
+            }
+            le_idx[j + 1] = x;
+        }
+        int w = lc_ptr[l1];
+        const int c0 = w;
+        for (int q = q0; q < q1; q++) {
+            const int a = le_idx[q];
+            const int eph = ph[A.r_edge_pose[a]];
+            if (eph < 0) continue;
+            int j = w - 1;   // stable insertion by pose block
+            while (j >= c0 && ph[A.r_edge_pose[lc_idx[j]]] > eph) {
+                lc_idx[j + 1] = lc_idx[j];
+                j--;
+            }
+            lc_idx[j + 1] = a;
+            w++;
+        }
+    }
+    if (tid == 0) {
+        A.nP = nP;
+        A.nL = nL;
+        A.nE = E;
+        A.dim_p = 6 * nP;
+    }
+}
+
 // Structures of the second optimize() (src/Optimizer.cc:472-478: the edges
 // the first outlier pass set to level 1 leave the graph) built on the device
 // from the first pass's: g2o's initializeOptimization / buildStructure
 // restated as order-preserving filters of the first pass's sorted lists
 // (active edges keep their original order, free poses / points their id
 // order, every CSR list its edge or pose order), so the result equals the
-// host build_struct on the reduced edge set.  One workgroup per problem;
+// first-pass build (k_lba_build) on the reduced edge set.  One workgroup per problem;
 // the first pass's Hpl and Hll scratch (dead until the second pass
 // linearises) hold the index maps.  B's pointer fields are set by the host.
 __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, LbaDev* d1s, const uint8_t* status_all,
@@ -817,111 +1005,6 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
 // ---------------------------------------------------------------------------
 namespace {
 
-struct HostStruct {
-    std::vector<int> e_orig, e_pose, e_point, e_ph, e_lh;
-    std::vector<double> e_obs, e_isig;
-    std::vector<int> iv_pose, iv_point;
-    std::vector<int> pe_ptr, pe_idx, le_ptr, le_idx, lc_ptr, lc_idx;
-    int nP = 0, nL = 0;
-};
-
-void build_struct(const orbx_ba_problem& p, const uint8_t* removed, HostStruct& s)
-{
-    const int NP = p.n_poses, NL = p.n_points, NE = p.n_edges;
-    std::vector<uint8_t> pact(NP, 0), lact(NL, 0);
-    std::vector<int> act;
-    for (int e = 0; e < NE; e++) {
-        if (removed && removed[e]) continue;
-        act.push_back(e);
-        pact[p.edge_pose[e]] = 1;
-        lact[p.edge_point[e]] = 1;
-    }
-    std::vector<int> ps, ls;
-    for (int i = 0; i < NP; i++)
-        if (pact[i] && !p.pose_fixed[i]) ps.push_back(i);
-    for (int i = 0; i < NL; i++)
-        if (lact[i]) ls.push_back(i);
-    std::stable_sort(ps.begin(), ps.end(), [&](int a, int b) { return p.pose_id[a] < p.pose_id[b]; });
-    std::stable_sort(ls.begin(), ls.end(), [&](int a, int b) { return p.point_id[a] < p.point_id[b]; });
-    std::vector<int> ph(NP, -1), lh(NL, -1);
-    for (size_t i = 0; i < ps.size(); i++) ph[ps[i]] = (int)i;
-    for (size_t i = 0; i < ls.size(); i++) lh[ls[i]] = (int)i;
-    s.nP = (int)ps.size();
-    s.nL = (int)ls.size();
-    s.iv_pose = ps;
-    s.iv_point = ls;
-    const int nE = (int)act.size();
-    s.e_orig = act;
-    s.e_pose.resize(nE);
-    s.e_point.resize(nE);
-    s.e_ph.resize(nE);
-    s.e_lh.resize(nE);
-    s.e_obs.resize(2 * nE);
-    s.e_isig.resize(nE);
-    for (int a = 0; a < nE; a++) {
-        const int e = act[a];
-        s.e_pose[a] = p.edge_pose[e];
-        s.e_point[a] = p.edge_point[e];
-        s.e_ph[a] = ph[p.edge_pose[e]];
-        s.e_lh[a] = lh[p.edge_point[e]];
-        s.e_obs[2 * a] = p.edge_obs[2 * e];
-        s.e_obs[2 * a + 1] = p.edge_obs[2 * e + 1];
-        s.e_isig[a] = p.edge_inv_sigma2[e];
-    }
-    // CSR lists by counting sort (edge order kept within a bucket): no
-    // per-bucket allocations, which contend in malloc across host threads
-    auto csr = [&](int n, auto key, std::vector<int>& ptr, std::vector<int>& idx) {
-        ptr.assign(n + 1, 0);
-        for (int a = 0; a < nE; a++) {
-            const int k = key(a);
-            if (k >= 0) ptr[k + 1]++;
-        }
-        for (int i = 0; i < n; i++) ptr[i + 1] += ptr[i];
-        idx.resize(ptr[n]);
-        std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-        for (int a = 0; a < nE; a++) {
-            const int k = key(a);
-            if (k >= 0) idx[fill[k]++] = a;
-        }
-    };
-    csr(s.nP, [&](int a) { return s.e_ph[a]; }, s.pe_ptr, s.pe_idx);
-    csr(s.nL, [&](int a) { return s.e_lh[a]; }, s.le_ptr, s.le_idx);
-    csr(s.nL, [&](int a) { return s.e_ph[a] >= 0 ? s.e_lh[a] : -1; }, s.lc_ptr, s.lc_idx);
-    // Schur columns of a point in pose order (stable: insertion sort of the
-    // point's few edges by pose hessian index)
-    for (int l = 0; l < s.nL; l++) {
-        int* v = s.lc_idx.data();
-        for (int i = s.lc_ptr[l] + 1; i < s.lc_ptr[l + 1]; i++) {
-            const int x = v[i];
-            int j = i - 1;
-            while (j >= s.lc_ptr[l] && s.e_ph[v[j]] > s.e_ph[x]) {
-                v[j + 1] = v[j];
-                j--;
-            }
-            v[j + 1] = x;
-        }
-    }
-}
-
-// Packs host vectors into one device allocation.
-struct Packer {
-    std::vector<uint8_t> host;
-    template <typename T>
-    size_t add(const std::vector<T>& v)
-    {
-        const size_t off = host.size();
-        host.resize(off + ((v.size() * sizeof(T) + 255) & ~size_t(255)));
-        if (!v.empty()) std::memcpy(host.data() + off, v.data(), v.size() * sizeof(T));
-        return off;
-    }
-    size_t reserve(size_t bytes)
-    {
-        const size_t off = host.size();
-        host.resize(off + ((bytes + 255) & ~size_t(255)));
-        return off;
-    }
-};
-
 // doubles of LDS for the reduced system (160 KB less the Schur edge table)
 constexpr int kLdsSCap = (160 * 1024 - kLbaThreads * kSchurEdges * 8 - 1024) / 8;
 
@@ -1016,37 +1099,39 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     std::vector<LbaDev> devs(P);
     int r = ORBX_OK;
     mark("setup");
-    struct HostCache {
-        std::vector<HostStruct> hs;
+    // Both optimize() calls' structures are built on the device: the first
+    // from the caller's arrays (k_lba_build), the second from the first's
+    // after the first outlier pass (k_lba_rebuild), so the host only stages
+    // the problems, and both passes run back to back after one upload.
+    // Layout after the persistent block: the caller's edge / id arrays, both
+    // LbaDev arrays (pointers from the host, counts from the builds), then
+    // device-only: the two passes' structure arrays (sized by the problem:
+    // every edge, pose and point), the scratch (sized by the free poses).
+    constexpr int kRaw = 7, kArr = 15;
+    std::vector<size_t> so_raw(kRaw * (size_t)P), so(kArr * (size_t)P), so1(kArr * (size_t)P);
+    std::vector<int> nfree(P, 0);
+    host_parallel(P, [&](int i) {
+        int c = 0;
+        for (int k = 0; k < probs[i].n_poses; k++) c += !probs[i].pose_fixed[k];
+        nfree[i] = c;
+    });
+    auto raw_bytes = [&](const orbx_ba_problem& p, size_t (&bytes)[kRaw]) {
+        const size_t E = p.n_edges, NP = p.n_poses, NL = p.n_points;
+        const size_t b[kRaw] = {E * 4, E * 4, E * 16, E * 8, NP, NP * 8, NL * 8};
+        for (int k = 0; k < kRaw; k++) bytes[k] = b[k];
     };
-    if (!ctx->lba_host) ctx->lba_host = std::make_shared<HostCache>();
-    std::vector<HostStruct>& hs = static_cast<HostCache*>(ctx->lba_host.get())->hs;
-    if ((int)hs.size() < P) hs.resize(P);
-    // The first pass's structures are built on host threads; the second
-    // pass's are built on the device from them (k_lba_rebuild) right after
-    // the first outlier pass, so both optimize() calls run back to back with
-    // no host round trip.  Layout after the persistent block: the first
-    // pass's staged arrays, both LbaDev arrays (the second one's pointers
-    // staged by the host, its counts written by the rebuild), the second
-    // pass's arrays (device-written, first-pass sizes), the device scratch.
-    host_parallel(P, [&](int i) { build_struct(probs[i], nullptr, hs[i]); });
-    mark("build_struct");
-    constexpr int kArr = 15;
-    std::vector<size_t> so(kArr * (size_t)P), so1(kArr * (size_t)P);
-    auto arr_bytes = [&](const HostStruct& h, size_t (&bytes)[kArr]) {
-        const size_t b[kArr] = {h.e_orig.size() * 4, h.e_pose.size() * 4, h.e_point.size() * 4,
-                                h.e_ph.size() * 4,   h.e_lh.size() * 4,   h.e_obs.size() * 8,
-                                h.e_isig.size() * 8, h.iv_pose.size() * 4, h.iv_point.size() * 4,
-                                h.pe_ptr.size() * 4, h.pe_idx.size() * 4, h.le_ptr.size() * 4,
-                                h.le_idx.size() * 4, h.lc_ptr.size() * 4, h.lc_idx.size() * 4};
+    auto arr_bytes = [&](const orbx_ba_problem& p, size_t (&bytes)[kArr]) {
+        const size_t E = p.n_edges, NP = nfree[&p - probs], NL = p.n_points;
+        const size_t b[kArr] = {E * 4,  E * 4,        E * 4,  E * 4,        E * 4,  E * 16,       E * 8, NP * 4,
+                                NL * 4, (NP + 1) * 4, E * 4, (NL + 1) * 4, E * 4, (NL + 1) * 4, E * 4};
         for (int k = 0; k < kArr; k++) bytes[k] = b[k];
     };
     size_t end = base_bytes;
     for (int i = 0; i < P; i++) {
-        size_t bytes[kArr];
-        arr_bytes(hs[i], bytes);
-        for (int k = 0; k < kArr; k++) {
-            so[kArr * i + k] = end;
+        size_t bytes[kRaw];
+        raw_bytes(probs[i], bytes);
+        for (int k = 0; k < kRaw; k++) {
+            so_raw[kRaw * i + k] = end;
             end += align256(bytes[k]);
         }
     }
@@ -1055,21 +1140,26 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     const size_t o_devs1 = end;
     end += align256(sizeof(LbaDev) * P);
     const size_t staged_end = end;
-    for (int i = 0; i < P; i++) {
-        size_t bytes[kArr];
-        arr_bytes(hs[i], bytes);
-        for (int k = 0; k < kArr; k++) {
-            so1[kArr * i + k] = end;
-            end += align256(bytes[k]);
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < P; i++) {
+            size_t bytes[kArr];
+            arr_bytes(probs[i], bytes);
+            for (int k = 0; k < kArr; k++) {
+                (pass == 0 ? so : so1)[kArr * i + k] = end;
+                end += align256(bytes[k]);
+            }
         }
-    }
-    // device-only scratch (never copied), sized by the first pass
+    // device-only scratch, sized by the free poses, every point and edge
+    // (the Hpl scratch also holds k_lba_build's and k_lba_rebuild's maps)
     std::vector<size_t> sc(8 * (size_t)P);
+    size_t max_n2 = 0;
     for (int i = 0; i < P; i++) {
-        const HostStruct& h = hs[i];
-        const size_t nE = h.e_orig.size(), n = 6 * (size_t)h.nP;
-        const size_t bytes[7] = {18 * nE * 8, 27 * (size_t)h.nP * 8, 9 * (size_t)h.nL * 8, 12 * (size_t)h.nL * 8,
-                                 n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * (size_t)h.nL) * 8, n * 8 + 8};
+        const orbx_ba_problem& p = probs[i];
+        const size_t nE = p.n_edges, nL = p.n_points, n = 6 * (size_t)nfree[i];
+        max_n2 = std::max(max_n2, n * n + n);
+        const size_t bytes[7] = {std::max(18 * nE * 8, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
+                                 9 * nL * 8, 12 * nL * 8, n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * nL) * 8,
+                                 n * 8 + 8};
         for (int k = 0; k < 7; k++) {
             sc[8 * i + k] = end;
             end += align256(bytes[k]);
@@ -1084,7 +1174,6 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     // fill the staged bytes on host threads
     host_parallel(P, [&](int i) {
         const orbx_ba_problem& p = probs[i];
-        const HostStruct& h = hs[i];
         double* pose = reinterpret_cast<double*>(hb + pl[i].pose);
         for (int k = 0; k < p.n_poses; k++) {
             for (int j = 0; j < 4; j++) pose[7 * k + j] = p.pose_q[4 * k + j];
@@ -1096,23 +1185,17 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
         std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
         std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
-        const void* src[kArr] = {h.e_orig.data(), h.e_pose.data(), h.e_point.data(), h.e_ph.data(),
-                                 h.e_lh.data(),   h.e_obs.data(),  h.e_isig.data(),  h.iv_pose.data(),
-                                 h.iv_point.data(), h.pe_ptr.data(), h.pe_idx.data(), h.le_ptr.data(),
-                                 h.le_idx.data(), h.lc_ptr.data(), h.lc_idx.data()};
-        size_t bytes[kArr];
-        arr_bytes(h, bytes);
-        for (int k = 0; k < kArr; k++)
-            if (bytes[k]) std::memcpy(hb + so[kArr * i + k], src[k], bytes[k]);
+        const void* src[kRaw] = {p.edge_pose, p.edge_point, p.edge_obs, p.edge_inv_sigma2,
+                                 p.pose_fixed, p.pose_id, p.point_id};
+        size_t rb[kRaw];
+        raw_bytes(p, rb);
+        for (int k = 0; k < kRaw; k++)
+            if (rb[k]) std::memcpy(hb + so_raw[kRaw * i + k], src[k], rb[k]);
         auto fill = [&](LbaDev& D, const size_t* o) {
             D = LbaDev{};
-            D.nP = h.nP;
-            D.nL = h.nL;
-            D.nE = (int)h.e_orig.size();
             D.nposes_all = p.n_poses;
             D.npoints_all = p.n_points;
             D.nedges_all = p.n_edges;
-            D.dim_p = 6 * h.nP;
             D.pose = reinterpret_cast<double*>(d + pl[i].pose);
             D.point = reinterpret_cast<double*>(d + pl[i].point);
             D.pose_bk = reinterpret_cast<double*>(d + pl[i].posebk);
@@ -1142,11 +1225,19 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             D.S = reinterpret_cast<double*>(d + c[4]);
             D.x = reinterpret_cast<double*>(d + c[5]);
             D.bs = reinterpret_cast<double*>(d + c[6]);
+            const size_t* q = &so_raw[kRaw * i];
+            D.r_edge_pose = reinterpret_cast<const int*>(d + q[0]);
+            D.r_edge_point = reinterpret_cast<const int*>(d + q[1]);
+            D.r_edge_obs = reinterpret_cast<const double*>(d + q[2]);
+            D.r_edge_isig = reinterpret_cast<const double*>(d + q[3]);
+            D.r_pose_fixed = d + q[4];
+            D.r_pose_id = reinterpret_cast<const long long*>(d + q[5]);
+            D.r_point_id = reinterpret_cast<const long long*>(d + q[6]);
             D.huber_delta = p.huber_delta;
             D.status = kRunning;
             D.ni = 2;
         };
-        fill(devs[i], &so[kArr * i]);
+        fill(devs[i], &so[kArr * i]);     // counts and contents: k_lba_build
         fill(devs1[i], &so1[kArr * i]);   // counts and contents: k_lba_rebuild
     });
     std::memcpy(hb + o_offs, offs.data(), offs.size() * 8);
@@ -1155,9 +1246,10 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     mark("pack");
     ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, staged_end, hipMemcpyHostToDevice, ctx->stream));
     mark("upload");
-    size_t max_n2 = 0;
-    for (int i = 0; i < P; i++)
-        max_n2 = std::max(max_n2, (size_t)devs[i].dim_p * devs[i].dim_p + (size_t)devs[i].dim_p);
+    timer_begin(ctx, "lba_build");
+    hipLaunchKernelGGL(k_lba_build, dim3(P), dim3(kLbaThreads), 0, ctx->stream, reinterpret_cast<LbaDev*>(d + o_devs));
+    timer_end(ctx, "lba_build");
+    ORBX_HIP_CHECK(hipGetLastError());
     const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
     const int lds_cap = (int)(lds / 8);
     for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {

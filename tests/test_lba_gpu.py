@@ -108,3 +108,16 @@ def test_lba_batch_equals_single(ctx):
         # FP64 atomics make the summation order run-dependent: equal up to rounding
         assert np.abs(a["pose_q"] - s[0]["pose_q"]).max() < 1e-10 and np.abs(a["points"] - s[0]["points"]).max() < 1e-9
         assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
+
+
+def test_lba_unsorted_vertex_ids(ctx):
+    """Vertex ids that do not increase with the array index (a caller's
+    keyframe / map-point order differing from mnId order): the Hessian block
+    order follows the ids (g2o sorts its vertices by id), so the device build
+    takes its pairwise-rank path; the result must still equal the oracle's."""
+    prob = sb.make_problem(n_kf=8, n_points=500, seed=11, outlier_frac=0.03)
+    r = np.random.default_rng(5)
+    prob = dict(prob)
+    prob["pose_id"] = r.permutation(prob["pose_id"])
+    prob["point_id"] = r.permutation(prob["point_id"])
+    compare(run_ref(prob), run_gpu(ctx, prob))
