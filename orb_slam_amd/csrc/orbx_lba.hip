@@ -1080,10 +1080,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     const size_t result_bytes = at;
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
-        pl[i].posebk = at;  at += align256(7 * (size_t)p.n_poses * 8);
-        pl[i].pointbk = at; at += align256(3 * (size_t)p.n_points * 8);
         pl[i].cam = at;     at += align256(4 * (size_t)p.n_poses * 8);
-        pl[i].err = at;     at += align256(2 * (size_t)p.n_edges * 8);
         offs[3 * i] = eacc;
         offs[3 * i + 1] = pacc;
         eacc += p.n_edges;
@@ -1140,6 +1137,18 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     const size_t o_devs1 = end;
     end += align256(sizeof(LbaDev) * P);
     const size_t staged_end = end;
+    // device-only: the LM backups and the per-edge errors (zeroed on the device)
+    for (int i = 0; i < P; i++) {
+        const orbx_ba_problem& p = probs[i];
+        pl[i].posebk = end;  end += align256(7 * (size_t)p.n_poses * 8);
+        pl[i].pointbk = end; end += align256(3 * (size_t)p.n_points * 8);
+    }
+    const size_t o_err = end;
+    for (int i = 0; i < P; i++) {
+        pl[i].err = end;
+        end += align256(2 * (size_t)probs[i].n_edges * 8);
+    }
+    const size_t err_bytes = end - o_err;
     for (int pass = 0; pass < 2; pass++)
         for (int i = 0; i < P; i++) {
             size_t bytes[kArr];
@@ -1181,7 +1190,6 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         }
         std::memcpy(hb + pl[i].point, p.points, 3 * (size_t)p.n_points * 8);
         std::memcpy(hb + pl[i].cam, p.pose_cam, 4 * (size_t)p.n_poses * 8);
-        std::memset(hb + pl[i].err, 0, 2 * (size_t)p.n_edges * 8);
         std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
         std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
         std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
@@ -1245,6 +1253,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     std::memcpy(hb + o_devs1, devs1.data(), sizeof(LbaDev) * P);
     mark("pack");
     ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, staged_end, hipMemcpyHostToDevice, ctx->stream));
+    ORBX_HIP_CHECK(hipMemsetAsync(d + o_err, 0, err_bytes, ctx->stream));
     mark("upload");
     timer_begin(ctx, "lba_build");
     hipLaunchKernelGGL(k_lba_build, dim3(P), dim3(kLbaThreads), 0, ctx->stream, reinterpret_cast<LbaDev*>(d + o_devs));
