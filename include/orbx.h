@@ -111,6 +111,9 @@ int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
  * Batches of 32+ frames run as two halves on two internal streams (joined
  * before the call's later work) unless disabled with orbx_dev_set_split. */
 int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
+/* enable: 0 = one stream; 1 = split (default); 2..4 = split, and the
+ * asynchronous extract_match pipeline runs its batch in that many parts on
+ * as many streams, part i released by part i-1's FAST pass (default 3). */
 int orbx_dev_set_split(orbx_ctx* ctx, int enable);
 /* orbx_dev_extract followed by matching every slot of the batch against its
  * predecessor (mode 1: orbx_dev_match_prev with window / nnratio / check_ori;

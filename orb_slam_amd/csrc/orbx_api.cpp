@@ -208,6 +208,13 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
         r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxPending; i++)
         if (hipEventCreateWithFlags(&ctx->ev_match[i], hipEventDisableTiming) != hipSuccess) r = ORBX_ERR_HIP;
+    if (const char* e = getenv("ORBX_SPLIT_WAYS")) ctx->split_ways = std::min(std::max(atoi(e), 2), orbx_ctx::kMaxWays);
+    for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays - 2; i++)
+        if (hipStreamCreateWithFlags(&ctx->xstreams[i], hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays; i++)
+        if (hipEventCreateWithFlags(&ctx->ev_part_fast[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->ev_part_done[i], hipEventDisableTiming) != hipSuccess)
+            r = ORBX_ERR_HIP;
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
     if (r == ORBX_OK) r = realloc_dev(ctx->level_count, (size_t)S * nlevels);
@@ -238,6 +245,8 @@ void orbx_destroy(orbx_ctx* ctx)
     ctx_enter(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+    for (hipStream_t x : ctx->xstreams)
+        if (x) (void)hipStreamSynchronize(x);
     if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
     for (auto& t : ctx->timers) {
         for (auto e : t.start) hipEventDestroy(e);
@@ -251,6 +260,12 @@ void orbx_destroy(orbx_ctx* ctx)
         if (e) (void)hipEventDestroy(e);
     if (ctx->mstream) (void)hipStreamDestroy(ctx->mstream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    for (hipStream_t x : ctx->xstreams)
+        if (x) (void)hipStreamDestroy(x);
+    for (int i = 0; i < orbx_ctx::kMaxWays; i++) {
+        if (ctx->ev_part_fast[i]) (void)hipEventDestroy(ctx->ev_part_fast[i]);
+        if (ctx->ev_part_done[i]) (void)hipEventDestroy(ctx->ev_part_done[i]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -325,8 +340,9 @@ int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int
 
 int orbx_dev_set_split(orbx_ctx* ctx, int enable)
 {
-    if (!ctx) return ORBX_ERR_ARG;
+    if (!ctx || enable < 0 || enable > orbx_ctx::kMaxWays) return ORBX_ERR_ARG;
     ctx->split = enable != 0;
+    if (enable >= 2) ctx->split_ways = enable;
     return ORBX_OK;
 }
 

@@ -1525,30 +1525,33 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         // context stream during the second half's tail.  The VALU-bound FAST
         // of one half thus overlaps the latency-bound stages of the other,
         // in steady state.  mstream's match waits for both halves.
-        if (ctx->split && count >= 2 * kSplitMinFrames && ctx->stream2) {
+        const int ways = std::min(ctx->split_ways, count / kSplitMinFrames);
+        if (ctx->split && ways >= 2 && ctx->stream2) {
             // outputs of [first, first + count) are rewritten: pending matches
-            // reading them finish first (stream2 inherits it through ev_fork)
+            // reading them finish first (the other parts' streams inherit it
+            // through the release chain)
             wait_pending_overlap(ctx, first, count, ctx->stream);
-            const int n0 = count / 2, n1 = count - n0;
-            ExtractArgs b = a;
-            b.first_slot = first + n0;
-            b.pyr_raw += (size_t)n0 * a.frame_pyr_bytes;
-            b.pyr_blur += (size_t)n0 * a.frame_pyr_bytes;
-            b.cell_lists += (size_t)n0 * a.list_entries;
-            b.retain_scratch += (size_t)n0 * (a.list_entries + 4 * a.ncells);
-            b.cell_count += (size_t)n0 * a.ncells;
-            b.level_keys += (size_t)n0 * a.level_entries;
-            b.level_count += (size_t)n0 * a.nlevels;
-            run_pyramid(a, n0, ctx->stream);
-            run_rest(a, n0, ctx->stream, 1);
-            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
-            run_rest(a, n0, ctx->stream, 6);
-            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream));
-            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-            run(b, n1, ctx->stream2);
-            ORBX_HIP_CHECK(hipEventRecord(ctx->ev_extracted, ctx->stream2));
-            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_join, 0));
-            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_extracted, 0));
+            const hipStream_t S[orbx_ctx::kMaxWays] = {ctx->stream, ctx->stream2, ctx->xstreams[0], ctx->xstreams[1]};
+            for (int i = 0; i < ways; i++) {
+                const int lo = count * i / ways, n = count * (i + 1) / ways - lo;
+                ExtractArgs b = a;
+                b.first_slot = first + lo;
+                b.pyr_raw += (size_t)lo * a.frame_pyr_bytes;
+                b.pyr_blur += (size_t)lo * a.frame_pyr_bytes;
+                b.cell_lists += (size_t)lo * a.list_entries;
+                b.retain_scratch += (size_t)lo * (a.list_entries + 4 * a.ncells);
+                b.cell_count += (size_t)lo * a.ncells;
+                b.level_keys += (size_t)lo * a.level_entries;
+                b.level_count += (size_t)lo * a.nlevels;
+                // part i starts once part i - 1 is past its FAST pass
+                if (i > 0) ORBX_HIP_CHECK(hipStreamWaitEvent(S[i], ctx->ev_part_fast[i - 1], 0));
+                run_pyramid(b, n, S[i]);
+                run_rest(b, n, S[i], 1);
+                ORBX_HIP_CHECK(hipEventRecord(ctx->ev_part_fast[i], S[i]));
+                run_rest(b, n, S[i], 6);
+                ORBX_HIP_CHECK(hipEventRecord(ctx->ev_part_done[i], S[i]));
+                ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_part_done[i], 0));
+            }
         } else {
             const int r = launch_extract(ctx, first, count, nullptr);
             if (r != ORBX_OK) return r;

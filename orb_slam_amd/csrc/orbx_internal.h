@@ -157,6 +157,13 @@ struct orbx_ctx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;      // second half of large extraction batches
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // pipelined extraction in split_ways parts (2..kMaxWays): part i on
+    // streams[i] (streams[0] = stream, streams[1] = stream2), released by
+    // part i - 1's FAST (ev_part_fast), joined by the match (ev_part_done)
+    static constexpr int kMaxWays = 4;
+    int split_ways = 3;
+    hipStream_t xstreams[kMaxWays - 2] = {};
+    hipEvent_t ev_part_fast[kMaxWays] = {}, ev_part_done[kMaxWays] = {};
     bool split = true;                  // run large batches as two concurrent halves
     // Asynchronous matching (orbx_dev_set_async_match): the matching of an
     // extract_match call runs on mstream while later calls extract other
