@@ -130,13 +130,15 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
         if ((r = realloc_dev(ctx->dgeom.res_rows, g.res_rows.size())) != ORBX_OK) return r;
         ctx->cap_res_rows = (int)g.res_rows.size();
     }
-    // blur work blocks: per level, items = (row strip, dword column) in
-    // strip-major order; one block = kBlurItems consecutive items of a level.
+    // blur work blocks: per level, wave items = (row strip, chunk of
+    // kBlurChunkCols dword columns) in strip-major order; one block = 4
+    // consecutive wave items of a level.
     std::vector<int4> tiles;
     for (int l = 0; l < g.nlevels; l++) {
         const LevelGeom& L = g.levels[l];
         const int ndw = L.stride / 4, nstrips = (L.ph + kBlurStrip - 1) / kBlurStrip;
-        for (int b = 0; b < ndw * nstrips; b += kBlurItems) tiles.push_back(make_int4(l, b, ndw, nstrips));
+        const int nchunks = (ndw + kBlurChunkCols - 1) / kBlurChunkCols;
+        for (int b = 0; b < nchunks * nstrips; b += kBlurItems / 64) tiles.push_back(make_int4(l, b, nchunks, nstrips));
     }
     if ((int)tiles.size() > ctx->cap_blur_tiles) {
         if ((r = realloc_dev(ctx->blur_tiles, tiles.size())) != ORBX_OK) return r;

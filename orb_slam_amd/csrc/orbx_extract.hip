@@ -1006,26 +1006,38 @@ __device__ inline void blur_hsum(const uint8_t* row, int x, int hs[4])
 
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
 {
+    // One wave per (row strip, chunk of kBlurChunkCols dword columns): lane
+    // l holds dword 62 c - 1 + l of each row, lanes 0 and 63 only as halo.
+    // A row is one dword load per lane; the left / right neighbour dwords of
+    // the horizontal taps come from the adjacent lanes (DPP wave_shr:1 /
+    // wave_shl:1) instead of two more loads.
     const int f = blockIdx.y;
-    const int4 tl = tiles[blockIdx.x];   // level, first item, dwords per row, strips
-    const int item = tl.y + threadIdx.x;
-    if (item >= tl.z * tl.w) return;
+    const int4 tl = tiles[blockIdx.x];   // level, first wave item, chunks per row, strips
+    const int wi = tl.y + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wi >= tl.z * tl.w) return;       // whole waves
     const LevelGeom L = a.levels[tl.x];
-    const int strip = item / tl.z, dw = item - strip * tl.z;
-    const int x = dw * 4;
+    const int strip = wi / tl.z, chunk = wi - strip * tl.z;
+    const int ndw = L.stride >> 2;
+    const int dw = kBlurChunkCols * chunk - 1 + lane;
+    const bool out = lane >= 1 && lane <= kBlurChunkCols && dw < ndw;
+    const int x = 4 * min(max(dw, 0), ndw - 1);
     const int y0 = strip * kBlurStrip, y1 = min(y0 + kBlurStrip, L.ph);
     // uniform level bases + 32-bit per-lane offsets (saddr + voffset loads)
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off;
     uint8_t* dst = a.pyr_blur + (size_t)f * a.frame_pyr_bytes + L.off;
     const uint32_t stride = (uint32_t)L.stride;
-    auto ld = [&](int y, int dx) { return *reinterpret_cast<const uint32_t*>(src + ((uint32_t)y * stride + (uint32_t)x) + dx); };
-    auto st = [&](int y, uint32_t v) { *reinterpret_cast<uint32_t*>(dst + ((uint32_t)y * stride + (uint32_t)x)) = v; };
-    // interior columns / rows of this level in padded coordinates
-    const int ix0 = kEdge, ix1 = kEdge + L.w, iy0 = kEdge, iy1 = kEdge + L.h;
-    const bool col_interior = (x + 3 >= ix0) && (x < ix1);
-    // rows [ya, yb) of this strip are blurred, the rest copied
-    const int ya = col_interior ? max(y0, iy0) : y1;
-    const int yb = col_interior ? min(y1, iy1) : y1;
+    auto ld = [&](int y) { return *reinterpret_cast<const uint32_t*>(src + ((uint32_t)y * stride + (uint32_t)x)); };
+    auto st = [&](int y, uint32_t v) {
+        if (out) *reinterpret_cast<uint32_t*>(dst + ((uint32_t)y * stride + (uint32_t)x)) = v;
+    };
+    // neighbours' words (lane - 1 / lane + 1): the DPP reads need every lane
+    // of the wave active, so all lanes run the same rows
+    auto left = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); };
+    auto right = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false); };
+    // interior rows of this level in padded coordinates: rows [ya, yb) of the
+    // strip are blurred (border columns keep their raw bytes), the rest copied
+    const int iy0 = kEdge, iy1 = kEdge + L.h;
+    const int ya = min(max(y0, iy0), y1), yb = max(min(y1, iy1), ya);
     // bytes beyond the padded width (row pitch padding) are zero
     uint32_t keep_mask = 0;
 #pragma unroll
@@ -1036,13 +1048,13 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
         for (int yc = ylo; yc < yhi; yc += 4) {
             uint32_t v[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = ld(min(yc + k, yhi - 1), 0);
+            for (int k = 0; k < 4; k++) v[k] = ld(min(yc + k, yhi - 1));
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 if (yc + k < yhi) st(yc + k, v[k] & keep_mask);
         }
     };
-    copy_rows(y0, min(ya, y1));
+    copy_rows(y0, ya);
     if (ya < yb) {
         // per column: float path (round half to even) below nvec, else +2^15
         int half_even[4];
@@ -1068,39 +1080,37 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
             any_tail = any_tail || tail_col[j];
         }
         f2 R[7][2];
-        auto hrow = [&](uint32_t l, uint32_t c, uint32_t r, f2 (&out)[2]) {
+        auto hrow = [&](uint32_t c, f2 (&o)[2]) {
             int hs[4];
-            blur_hsum_w(l, c, r, hs);
-            out[0] = f2{(float)hs[0], (float)hs[1]};
-            out[1] = f2{(float)hs[2], (float)hs[3]};
+            blur_hsum_w(left(c), c, right(c), hs);
+            o[0] = f2{(float)hs[0], (float)hs[1]};
+            o[1] = f2{(float)hs[2], (float)hs[3]};
         };
         uint32_t C[3];   // raw centre words of rows y, y+1, y+2 (loaded as rows y'+3 earlier)
+        {
+            uint32_t w0[6];
 #pragma unroll
-        for (int k = 0; k < 6; k++) {
-            const uint32_t wc = ld(ya - 3 + k, 0);
-            hrow(ld(ya - 3 + k, -4), wc, ld(ya - 3 + k, 4), R[k]);
-            if (k >= 3) C[k - 3] = wc;
+            for (int k = 0; k < 6; k++) w0[k] = ld(ya - 3 + k);
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                hrow(w0[k], R[k]);
+                if (k >= 3) C[k - 3] = w0[k];
+            }
         }
         // chunks of 7 output rows (the window's period: the register
         // rotation needs no moves); the chunk's input rows y + 3 are loaded
         // together, then filtered from registers
         constexpr int kBlurChunk = 7;
         for (int yc = ya; yc < yb; yc += kBlurChunk) {
-            uint32_t wl[kBlurChunk], wc[kBlurChunk], wr[kBlurChunk];
+            uint32_t wc[kBlurChunk];
 #pragma unroll
-            for (int k = 0; k < kBlurChunk; k++) {
-                // rows past yb + 2 repeat the last one (never used)
-                const int yy = min(yc + k, yb - 1) + 3;
-                wl[k] = ld(yy, -4);
-                wc[k] = ld(yy, 0);
-                wr[k] = ld(yy, 4);
-            }
+            for (int k = 0; k < kBlurChunk; k++) wc[k] = ld(min(yc + k, yb - 1) + 3);   // rows past yb + 2 repeat
 #pragma unroll
             for (int k = 0; k < kBlurChunk; k++) {
                 // rows past yb are computed on repeated input and not stored:
                 // no early exit, so the window rotation stays straight-line
                 const int y = yc + k;
-                hrow(wl[k], wc[k], wr[k], R[6]);
+                hrow(wc[k], R[6]);
                 float sv[4];
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
@@ -1112,9 +1122,9 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
                     sv[2 * h] = sc.x;
                     sv[2 * h + 1] = sc.y;
                     if (any_tail) {
-                        const f2 tl = (N + 32768.0f) * kInv;
-                        if (tail_col[2 * h]) sv[2 * h] = floorf(tl.x);
-                        if (tail_col[2 * h + 1]) sv[2 * h + 1] = floorf(tl.y);
+                        const f2 tl2 = (N + 32768.0f) * kInv;
+                        if (tail_col[2 * h]) sv[2 * h] = floorf(tl2.x);
+                        if (tail_col[2 * h + 1]) sv[2 * h + 1] = floorf(tl2.y);
                     }
                 }
                 uint32_t word = C[0];   // border columns keep the raw byte
@@ -1132,7 +1142,7 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
             }
         }
     }
-    copy_rows(max(yb, ya), y1);
+    copy_rows(yb, y1);
 }
 
 // ---------------------------------------------------------------------------

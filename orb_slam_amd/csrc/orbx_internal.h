@@ -40,7 +40,8 @@ constexpr int kMaxLevels = 16;
 constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
 constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
 constexpr int kBlurStrip = 28;   // output rows per blur thread (rolling window; 4 chunks of 7)
-constexpr int kBlurItems = 256;  // blur items (strip x dword column) per block
+constexpr int kBlurItems = 256;  // blur threads per block (4 waves, one (strip, column chunk) each)
+constexpr int kBlurChunkCols = 62;   // output dword columns per blur wave (+ one halo lane each side)
 
 constexpr int kResRows = 16;   // output rows per staged resize strip (k_pyr_resize_lds)
 
