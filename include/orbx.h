@@ -57,7 +57,10 @@ typedef struct orbx_ctx orbx_ctx;
  * buffers (frames larger than max_w x max_h are rejected); max_batch is the
  * number of frames one batched launch may carry and also the number of
  * device-resident frame slots available to orbx_dev_* (see below).
- * score_type: 1 = FAST_SCORE (implemented), 0 = HARRIS_SCORE (unsupported). */
+ * score_type: 0 = ORB::HARRIS_SCORE (HarrisResponses re-scores the FAST
+ * corners before retainBest, src/ORBextractor.cc:79-120, :616-620; keypoint
+ * responses are the Harris values), any other value = FAST_SCORE (the FAST
+ * score; the reference tests only == HARRIS_SCORE). */
 int  orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor,
                  int nlevels, int score_type, int fast_th,
                  int max_w, int max_h, int max_batch);

@@ -22,7 +22,7 @@ struct orbx_ref_extractor {
 orbx_ref_extractor* orbx_ref_extractor_create(int nfeatures, float scale, int nlevels,
                                               int score_type, int fast_th)
 {
-    if (nfeatures <= 0 || nlevels <= 0 || nlevels > 32 || !(scale > 1.0f) || score_type != 1)
+    if (nfeatures <= 0 || nlevels <= 0 || nlevels > 32 || !(scale > 1.0f))
         return nullptr;
     auto* r = new orbx_ref_extractor;
     r->ex.reset(new ORBextractorRef(nfeatures, scale, nlevels, score_type, fast_th));

@@ -284,6 +284,35 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
 }
 
 // ---------------------------------------------------------------------------
+// HarrisResponses (src/ORBextractor.cc:79-120): 7x7 block of 3x3 Sobel
+// products around each keypoint of the cell image (pt in cell coordinates;
+// the Sobel taps read one pixel past the block, inside the level buffer).
+// Integer sums, then the float response in the source's evaluation order
+// (no contraction: this file is built with -ffp-contract=off).
+void cv24_harris_responses(const uint8_t* img, int step, std::vector<KeyPoint>& pts, int blockSize, float harris_k)
+{
+    const int r = blockSize / 2;
+    float scale = (1 << 2) * blockSize * 255.0f;
+    scale = 1.0f / scale;
+    const float scale_sq_sq = scale * scale * scale * scale;
+    for (KeyPoint& kp : pts) {
+        const int x0 = cvRound(kp.x - r), y0 = cvRound(kp.y - r);
+        const uint8_t* ptr0 = img + (ptrdiff_t)y0 * step + x0;
+        int a = 0, b = 0, c = 0;
+        for (int i = 0; i < blockSize; i++) {
+            for (int j = 0; j < blockSize; j++) {
+                const uint8_t* p = ptr0 + (ptrdiff_t)i * step + j;
+                const int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
+                const int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
+                a += Ix * Ix;
+                b += Iy * Iy;
+                c += Ix * Iy;
+            }
+        }
+        kp.response = ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+    }
+}
+
 // KeyPointsFilter::retainBest (OpenCV 2.4 features2d/src/keypoint.cpp).
 // Called at src/ORBextractor.cc:683 and :699.  The surviving set and order is
 // the libstdc++ introselect permutation (std::nth_element).
@@ -556,6 +585,8 @@ void ORBextractorRef::computeKeyPoints(std::vector<std::vector<KeyPoint>>& allKe
                     ck.clear();
                     cv24_fast16(cell, L.step(), r1 - r0, c1 - c0, 7, true, ck);
                 }
+                // ORB::HARRIS_SCORE == 0 (:616-620, HARRIS_K = 0.04f :73)
+                if (scoreType == 0) cv24_harris_responses(cell, L.step(), ck, 7, 0.04f);
                 const int nKeys = (int)ck.size();
                 nTotal[i][j] = nKeys;
                 if (nKeys > nfeaturesCell) {

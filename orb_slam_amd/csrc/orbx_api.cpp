@@ -77,7 +77,7 @@ static int realloc_dev(T*& p, size_t count)
 static void free_buffers(orbx_ctx* ctx)
 {
     void* ptrs[] = {ctx->frames, ctx->pyr_raw, ctx->pyr_blur, ctx->cell_lists, ctx->retain_scratch, ctx->cell_count,
-                    ctx->level_keys, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
+                    ctx->level_keys, ctx->cell_keys64, ctx->level_keys64, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
                     ctx->scratch, ctx->pose_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
@@ -111,6 +111,7 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
         const long long e = g.list_entries + 4LL * (long long)g.cells.size();
         if ((r = realloc_dev(ctx->cell_lists, (size_t)S * e)) != ORBX_OK) return r;
         if ((r = realloc_dev(ctx->retain_scratch, (size_t)S * e)) != ORBX_OK) return r;
+        if (ctx->harris && (r = realloc_dev(ctx->cell_keys64, (size_t)S * e)) != ORBX_OK) return r;
         ctx->cap_list_entries = e;
     }
     if ((int)g.cells.size() > ctx->cap_cells) {
@@ -120,6 +121,7 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     }
     if (g.level_entries > ctx->cap_level_entries) {
         if ((r = realloc_dev(ctx->level_keys, (size_t)S * g.level_entries)) != ORBX_OK) return r;
+        if (ctx->harris && (r = realloc_dev(ctx->level_keys64, (size_t)S * g.level_entries)) != ORBX_OK) return r;
         ctx->cap_level_entries = g.level_entries;
     }
     if ((int)g.res_cols.size() > ctx->cap_res_cols) {
@@ -186,7 +188,6 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
         !(scale_factor > 1.0f) || max_w <= 0 || max_h <= 0 || max_w > 4095 || max_h > 4095 ||
         max_batch <= 0 || fast_th < 1 || fast_th > 255)
         return ORBX_ERR_ARG;
-    if (score_type != 1) return ORBX_ERR_UNSUPPORTED;   // HARRIS_SCORE not implemented
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBX_ERR_HIP;
     if (device < 0 || device >= ndev) return ORBX_ERR_ARG;
@@ -197,6 +198,9 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     ctx->max_w = max_w;
     ctx->max_h = max_h;
     ctx->slots = max_batch;
+    // ORB::HARRIS_SCORE == 0 selects Harris responses; any other value is
+    // FAST_SCORE, as in the reference (src/ORBextractor.cc:616)
+    ctx->harris = score_type == 0;
     if (const char* e = getenv("ORBX_PYR_MODE")) ctx->pyr_mode = atoi(e) == 1 ? 1 : 0;   // A/B runs
     init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
     int r = ORBX_OK;

@@ -209,11 +209,33 @@ __device__ inline int block_max(int v, BlockScratch& s, int buf)
 // k = 1..m where m = max_s min(#L before s, #R at/after s), and returns
 // L_1 (m == 0) or min(L_{m+1}, R_m).
 // --------------------------------------------------------------------------
+// Harris entries (scoreType == HARRIS_SCORE) are u64: the order-preserving
+// bit image of the float response (harris_key) in the high word, y<<12 | x
+// in the low word.
 __device__ inline uint32_t kp_key(uint32_t e) { return e >> 24; }
-__device__ inline bool kp_greater(uint32_t a, uint32_t b) { return kp_key(a) > kp_key(b); }
+__device__ inline uint32_t kp_key(uint64_t e) { return (uint32_t)(e >> 32); }
+template <typename E>
+__device__ inline bool kp_greater(E a, E b) { return kp_key(a) > kp_key(b); }
+// float -> u32 with a < b (as floats) <=> key(a) < key(b) for finite values
+// (-0 is folded onto +0, which compares equal to it)
+__host__ __device__ inline uint32_t harris_key(float r)
+{
+    uint32_t u;
+    const float z = r + 0.0f;
+    __builtin_memcpy(&u, &z, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float harris_response(uint32_t k)
+{
+    const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    float r;
+    __builtin_memcpy(&r, &u, 4);
+    return r;
+}
 
 // libstdc++ bits/stl_heap.h helpers (sequential, thread 0 only).
-__device__ inline void heap_push(uint32_t* first, int hole, int top, uint32_t value)
+template <typename E>
+__device__ inline void heap_push(E* first, int hole, int top, E value)
 {
     int parent = (hole - 1) / 2;
     while (hole > top && kp_greater(first[parent], value)) {
@@ -224,7 +246,8 @@ __device__ inline void heap_push(uint32_t* first, int hole, int top, uint32_t va
     first[hole] = value;
 }
 
-__device__ inline void heap_adjust(uint32_t* first, int hole, int len, uint32_t value)
+template <typename E>
+__device__ inline void heap_adjust(E* first, int hole, int len, E value)
 {
     const int top = hole;
     int second = hole;
@@ -242,7 +265,8 @@ __device__ inline void heap_adjust(uint32_t* first, int hole, int len, uint32_t 
     heap_push(first, hole, top, value);
 }
 
-__device__ inline void heap_select(uint32_t* first, int middle, int last)
+template <typename E>
+__device__ inline void heap_select(E* first, int middle, int last)
 {
     // __make_heap(first, first+middle)
     if (middle >= 2) {
@@ -256,18 +280,19 @@ __device__ inline void heap_select(uint32_t* first, int middle, int last)
     for (int i = middle; i < last; ++i) {
         if (kp_greater(first[i], first[0])) {
             // __pop_heap(first, first+middle, first+i)
-            const uint32_t value = first[i];
+            const E value = first[i];
             first[i] = first[0];
             heap_adjust(first, 0, middle, value);
         }
     }
 }
 
-__device__ inline void insertion_sort(uint32_t* a, int first, int last)
+template <typename E>
+__device__ inline void insertion_sort(E* a, int first, int last)
 {
     if (first == last) return;
     for (int i = first + 1; i < last; ++i) {
-        const uint32_t val = a[i];
+        const E val = a[i];
         if (kp_greater(val, a[first])) {
             for (int k = i; k > first; --k) a[k] = a[k - 1];
             a[first] = val;
@@ -282,7 +307,8 @@ __device__ inline void insertion_sort(uint32_t* a, int first, int last)
     }
 }
 
-__device__ inline void move_median_to_first(uint32_t* a, int result, int x, int y, int z)
+template <typename E>
+__device__ inline void move_median_to_first(E* a, int result, int x, int y, int z)
 {
     int t;
     if (kp_greater(a[x], a[y])) {
@@ -296,7 +322,7 @@ __device__ inline void move_median_to_first(uint32_t* a, int result, int x, int 
     } else {
         t = y;
     }
-    const uint32_t tmp = a[result];
+    const E tmp = a[result];
     a[result] = a[t];
     a[t] = tmp;
 }
@@ -437,8 +463,8 @@ __device__ inline int wave_min_int(int v)
     return v;
 }
 
-template <bool kGlobal = false>
-__device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos)
+template <bool kGlobal = false, typename E>
+__device__ inline int wave_hoare_partition(E* a, int lo, int hi, int* pos)
 {
     int* posR = pos;
     int* posL = pos + (hi - lo) / 2 + 1;
@@ -489,7 +515,7 @@ __device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos
     nth_sync<kGlobal>();
     for (int k = lane; k < m; k += 64) {
         const int i = posL[k], j = posR[k];
-        const uint32_t t = a[i];
+        const E t = a[i];
         a[i] = a[j];
         a[j] = t;
     }
@@ -499,8 +525,8 @@ __device__ inline int wave_hoare_partition(uint32_t* a, int lo, int hi, int* pos
 
 // std::nth_element(a, a + nth, a + n, greater-by-response), one wave.
 // kGlobal: list and scratch in global memory (lists too long for LDS).
-template <bool kGlobal = false>
-__device__ inline void wave_nth_element(uint32_t* a, int n, int nth, int* pos)
+template <bool kGlobal = false, typename E>
+__device__ inline void wave_nth_element(E* a, int n, int nth, int* pos)
 {
     if (n == 0 || nth == n) return;
     const int lane = threadIdx.x & 63;
@@ -510,7 +536,7 @@ __device__ inline void wave_nth_element(uint32_t* a, int n, int nth, int* pos)
         if (depth == 0) {
             if (lane == 0) {
                 heap_select(a + first, nth + 1 - first, last - first);
-                const uint32_t t = a[first];
+                const E t = a[first];
                 a[first] = a[nth];
                 a[nth] = t;
             }

@@ -6,6 +6,8 @@
 //   k_fast_cells   FAST-9/16 + cell-local NMS + threshold-7
 //                  fallback + raster-order compaction, one
 //                  workgroup per grid cell                    (:599-614)
+//   k_harris_cells HarrisResponses of every FAST corner (HARRIS_SCORE
+//                  only), u64 entries keyed by the float response (:616-620)
 //   k_retain_cells per-level quota redistribution + cell retainBest,
 //                  one wave per cell (libstdc++ introselect)  (:622-694)
 //   k_retain_levels level retainBest, one wave per level      (:697-701)
@@ -75,6 +77,9 @@ struct ExtractArgs {
     int32_t* out_n;
     int32_t* error_flags;
     int32_t* retain_scratch;        // slots x (list_entries + 4 ncells): global nth_element scratch
+    uint64_t* cell_keys64;          // HARRIS_SCORE: Harris-keyed cell lists (as cell_lists)
+    uint64_t* level_keys64;         // HARRIS_SCORE: Harris-keyed level lists (as level_keys)
+    int harris;                     // scoreType == HARRIS_SCORE
     long long frame_pyr_bytes;
     int first_slot;
     int w, h;
@@ -929,13 +934,89 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
     *level_total = base;
 }
 
+// ---------------------------------------------------------------------------
+// HarrisResponses(cellImage, cellKeyPoints, 7, HARRIS_K) (:79-120, :616-620)
+// on each cell's FAST list, one thread per corner: the 7x7 block of 3x3
+// Sobel products around the corner (9x9 pixels of the unblurred level,
+// three rows live in registers), integer sums, then the float response in
+// the source's evaluation order with every operation rounded on its own
+// (no contraction).  The entry becomes harris_key(response) << 32 | y << 12
+// | x, so the retain kernels compare responses exactly as retainBest does.
+// ---------------------------------------------------------------------------
+constexpr float kHarrisK = 0.04f;                                  // HARRIS_K (:73)
+constexpr float kHarrisScale = 1.0f / ((1 << 2) * 7 * 255.0f);     // 1 / ((1<<2) blockSize 255)  (:90-91)
+constexpr float kHarrisScale4 = kHarrisScale * kHarrisScale * kHarrisScale * kHarrisScale;   // (:92)
+
+__global__ __launch_bounds__(256) void k_harris_cells(ExtractArgs a)
+{
+    const int cell = blockIdx.x, f = blockIdx.y;
+    const CellGeom C = a.cells[cell];
+    if (!C.valid) return;
+    const int n = min(a.cell_count[(size_t)f * a.ncells + cell], C.list_cap);
+    const LevelGeom L = a.levels[C.level];
+    const int stride = L.stride;
+    const uint8_t* img = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)kEdge * stride + kEdge;
+    const uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
+    uint64_t* dst = a.cell_keys64 + (size_t)f * a.list_entries + C.list_off;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t e = src[i];
+        const int y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
+        const uint8_t* p0 = img + (ptrdiff_t)(y - 4) * stride + (x - 4);
+        int r0[9], r1[9], r2[9];
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            r0[j] = p0[j];
+            r1[j] = p0[stride + j];
+        }
+        int sa = 0, sb = 0, sc = 0;
+#pragma unroll
+        for (int rr = 2; rr < 9; rr++) {
+#pragma unroll
+            for (int j = 0; j < 9; j++) r2[j] = p0[(ptrdiff_t)rr * stride + j];
+#pragma unroll
+            for (int j = 1; j < 8; j++) {
+                const int Ix = (r1[j + 1] - r1[j - 1]) * 2 + (r0[j + 1] - r0[j - 1]) + (r2[j + 1] - r2[j - 1]);
+                const int Iy = (r2[j] - r0[j]) * 2 + (r2[j - 1] - r0[j - 1]) + (r2[j + 1] - r0[j + 1]);
+                sa += Ix * Ix;
+                sb += Iy * Iy;
+                sc += Ix * Iy;
+            }
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                r0[j] = r1[j];
+                r1[j] = r2[j];
+            }
+        }
+        const float fa = (float)sa, fb = (float)sb, fc = (float)sc;
+        const float s2 = __fadd_rn(fa, fb);
+        const float t = __fsub_rn(__fsub_rn(__fmul_rn(fa, fb), __fmul_rn(fc, fc)), __fmul_rn(__fmul_rn(kHarrisK, s2), s2));
+        const float resp = __fmul_rn(t, kHarrisScale4);
+        dst[i] = (uint64_t)harris_key(resp) << 32 | (e & 0xFFFFFFu);
+    }
+}
+
+// E = uint32_t (FAST score entries) or uint64_t (Harris-keyed entries)
+template <typename E>
+__device__ inline E* cell_entries(const ExtractArgs& a)
+{
+    if constexpr (sizeof(E) == 8) return a.cell_keys64;
+    else return a.cell_lists;
+}
+template <typename E>
+__device__ inline E* level_entries(const ExtractArgs& a)
+{
+    if constexpr (sizeof(E) == 8) return a.level_keys64;
+    else return a.level_keys;
+}
+
+template <typename E>
 __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_per_block, int wave_words)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cell = blockIdx.x * waves_per_block + wv, f = blockIdx.y;
     if (cell >= a.ncells) return;
-    uint32_t* list = sbuf + (size_t)wv * wave_words;
+    E* list = reinterpret_cast<E*>(sbuf + (size_t)wv * wave_words);
     int* pos = reinterpret_cast<int*>(list + kRetainCellCap);
     const CellGeom C = a.cells[cell];
     const LevelGeom L = a.levels[C.level];
@@ -951,8 +1032,8 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     const int n = counts[c];
     if (n == 0 || k == 0) return;
     const int take = min(n, k);
-    uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    uint32_t* dst = a.level_keys + (size_t)f * a.level_entries + L.level_off + pre;
+    E* src = cell_entries<E>(a) + (size_t)f * a.list_entries + C.list_off;
+    E* dst = level_entries<E>(a) + (size_t)f * a.level_entries + L.level_off + pre;
     if (n > k && n <= kRetainCellCap) {
         stage_to_lds<8>(list, n, lane, 64, [&](int i) { return src[i]; });
         lds_wave_sync();
@@ -968,6 +1049,7 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     }
 }
 
+template <typename E>
 __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_per_block, int wave_words)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t sbuf[];
@@ -978,9 +1060,9 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
     int32_t* cnt = a.level_count + (size_t)f * a.nlevels + level;
     const int nlev = *cnt;
     if (nlev <= L.n_desired) return;
-    uint32_t* list = sbuf + (size_t)wv * wave_words;
+    E* list = reinterpret_cast<E*>(sbuf + (size_t)wv * wave_words);
     int* pos = reinterpret_cast<int*>(list + a.max_level_cap);
-    uint32_t* g = a.level_keys + (size_t)f * a.level_entries + L.level_off;
+    E* g = level_entries<E>(a) + (size_t)f * a.level_entries + L.level_off;
     stage_to_lds<8>(list, nlev, lane, 64, [&](int i) { return g[i]; });
     lds_wave_sync();
     wave_nth_element(list, nlev, L.n_desired, pos);
@@ -1226,8 +1308,17 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
     const int lev_stride = pick(stride_l), lev_loff = pick(loff_l);
     const float lev_scale = __int_as_float(pick(__float_as_int(scale_l)));
     const float lev_psize = __int_as_float(pick(__float_as_int(psize_l)));
-    const uint32_t e = a.level_keys[(size_t)f * a.level_entries + lev_loff + local];
-    const int score = (int)(e >> 24), y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
+    uint32_t e;
+    float response;
+    if (a.harris) {
+        const uint64_t e64 = a.level_keys64[(size_t)f * a.level_entries + lev_loff + local];
+        e = (uint32_t)e64;
+        response = harris_response((uint32_t)(e64 >> 32));
+    } else {
+        e = a.level_keys[(size_t)f * a.level_entries + lev_loff + local];
+        response = (float)(e >> 24);   // FAST score
+    }
+    const int y = (int)((e >> 12) & 0xFFF), x = (int)(e & 0xFFF);
     const int X = kEdge + (valid ? x : kHalfPatch + 8), Y = kEdge + (valid ? y : kHalfPatch + 8);
     uint8_t* ic = s_patch[slot];
     uint8_t* br = ic + kIcRows * kIcPitch;
@@ -1333,7 +1424,7 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
         }
         kp.size = lev_psize;
         kp.angle = angle;
-        kp.response = (float)score;
+        kp.response = response;
         kp.octave = level;
         kp.class_id = -1;
         a.out_kps[(size_t)(a.first_slot + f) * a.nfeatures + k] = kp;
@@ -1366,6 +1457,11 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.out_n = ctx->out_n;
     a.error_flags = ctx->error_flags;
     a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
+    a.harris = ctx->harris;
+    // the level retain holds a whole level list (+ scratch) in one block's LDS
+    if ((size_t)((ctx->harris ? 3 : 2) * g.max_level_cap + 8) * 4 > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
+    a.cell_keys64 = ctx->harris ? ctx->cell_keys64 + (size_t)first * g.list_entries : nullptr;
+    a.level_keys64 = ctx->harris ? ctx->level_keys64 + (size_t)first * g.level_entries : nullptr;
     a.frame_pyr_bytes = g.frame_pyr_bytes;
     a.w = g.w;
     a.h = g.h;
@@ -1455,16 +1551,26 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         if (parts & 2) {
         timer_begin(ctx, "retain", st);
         {
-            // wave-private LDS: cell list + partition scratch (longer lists
-            // are replayed in global memory)
-            const int cw = 2 * kRetainCellCap + 8;
+            // wave-private LDS (u32 words): cell list + partition scratch
+            // (longer lists are replayed in global memory)
+            const int ew = x.harris ? 2 : 1;   // u32 words per entry
+            const int cw = (ew + 1) * kRetainCellCap + 8;
             const int cwaves = 4;
-            hipLaunchKernelGGL(k_retain_cells, dim3(((int)g.cells.size() + cwaves - 1) / cwaves, nb), dim3(64 * cwaves),
-                               (size_t)cwaves * cw * 4, st, x, cwaves, cw);
-            const int lw = 2 * g.max_level_cap + 8;
+            const int lw = (ew + 1) * g.max_level_cap + 8;
             const int lwaves = 1;   // one level per block: small LDS blocks fit beside the other stream's kernels
-            hipLaunchKernelGGL(k_retain_levels, dim3((g.nlevels + lwaves - 1) / lwaves, nb), dim3(64 * lwaves),
-                               (size_t)lwaves * lw * 4, st, x, lwaves, lw);
+            const dim3 cgrid(((int)g.cells.size() + cwaves - 1) / cwaves, nb), lgrid((g.nlevels + lwaves - 1) / lwaves, nb);
+            if (x.harris) {
+                hipLaunchKernelGGL(k_harris_cells, dim3((int)g.cells.size(), nb), dim3(256), 0, st, x);
+                hipLaunchKernelGGL(k_retain_cells<uint64_t>, cgrid, dim3(64 * cwaves), (size_t)cwaves * cw * 4, st, x,
+                                   cwaves, cw);
+                hipLaunchKernelGGL(k_retain_levels<uint64_t>, lgrid, dim3(64 * lwaves), (size_t)lwaves * lw * 4, st, x,
+                                   lwaves, lw);
+            } else {
+                hipLaunchKernelGGL(k_retain_cells<uint32_t>, cgrid, dim3(64 * cwaves), (size_t)cwaves * cw * 4, st, x,
+                                   cwaves, cw);
+                hipLaunchKernelGGL(k_retain_levels<uint32_t>, lgrid, dim3(64 * lwaves), (size_t)lwaves * lw * 4, st, x,
+                                   lwaves, lw);
+            }
         }
         timer_end(ctx, "retain", st);
         }
@@ -1552,6 +1658,10 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 b.retain_scratch += (size_t)lo * (a.list_entries + 4 * a.ncells);
                 b.cell_count += (size_t)lo * a.ncells;
                 b.level_keys += (size_t)lo * a.level_entries;
+                if (a.harris) {
+                    b.cell_keys64 += (size_t)lo * a.list_entries;
+                    b.level_keys64 += (size_t)lo * a.level_entries;
+                }
                 b.level_count += (size_t)lo * a.nlevels;
                 // part i starts once part i - 1 is past its FAST pass
                 if (i > 0) ORBX_HIP_CHECK(hipStreamWaitEvent(S[i], ctx->ev_part_fast[i - 1], 0));
@@ -1604,6 +1714,10 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         b.retain_scratch += (size_t)n0 * (a.list_entries + 4 * a.ncells);
         b.cell_count += (size_t)n0 * a.ncells;
         b.level_keys += (size_t)n0 * a.level_entries;
+        if (a.harris) {
+            b.cell_keys64 += (size_t)n0 * a.list_entries;
+            b.level_keys64 += (size_t)n0 * a.level_entries;
+        }
         b.level_count += (size_t)n0 * a.nlevels;
         ORBX_HIP_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
         ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));

@@ -194,6 +194,10 @@ struct orbx_ctx {
     int32_t* retain_scratch = nullptr;   // slots x (list_entries + 4 cells)
     int32_t* cell_count = nullptr;
     uint32_t* level_keys = nullptr;
+    // HARRIS_SCORE (score_type 0) only: u64 entries, Harris key << 32 | y << 12 | x
+    uint64_t* cell_keys64 = nullptr;    // slots x list_entries
+    uint64_t* level_keys64 = nullptr;   // slots x level_entries
+    int harris = 0;
     int32_t* level_count = nullptr;
     orbx_keypoint* out_kps = nullptr;
     uint8_t* out_desc = nullptr;

@@ -69,9 +69,9 @@ def ptr(a):
 
 
 class RefExtractor:
-    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20):
+    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1):
         self.L = load()
-        self.h = self.L.orbx_ref_extractor_create(nfeatures, scale, nlevels, 1, fast_th)
+        self.h = self.L.orbx_ref_extractor_create(nfeatures, scale, nlevels, score_type, fast_th)
         assert self.h, "oracle rejected the configuration"
         self.nfeatures = nfeatures
         self.nlevels = nlevels

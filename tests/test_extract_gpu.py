@@ -145,3 +145,39 @@ def test_pyramid_modes_identical(kind, w, h, n, seed):
     for i in (16, 17):
         assert_kps_equal(a[i][0], b[i][0])
         assert np.array_equal(a[i][1], b[i][1])
+
+
+@pytest.mark.parametrize("kind,w,h,n,seed", CASES)
+def test_harris_score_matches_oracle(kind, w, h, n, seed):
+    """scoreType == HARRIS_SCORE (src/ORBextractor.cc:616-620): the FAST
+    corners are re-scored by HarrisResponses before both retainBest calls;
+    keypoints (Harris responses included) and descriptors bit-exact."""
+    img = make(kind, w, h, seed)
+    ref = RefExtractor(n, score_type=0)
+    rk, rd = ref(img)
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=1, score_type=0)
+    ctx.upload(img)
+    ctx.extract(0, 1)
+    ctx.sync()
+    gk, gd = ctx.features(0)
+    assert_kps_equal(gk, rk)
+    assert np.array_equal(gd, rd), f"{np.count_nonzero((gd != rd).any(1))} descriptors differ"
+    ctx.close()
+
+
+def test_harris_large_batch_pipeline():
+    """HARRIS_SCORE through the multi-stream batch pipeline (64 frames in
+    parts), spot-checked against the oracle."""
+    w, h, B = 640, 480, 64
+    frames = synth.sequence(w, h, B, seed=98)
+    ctx = ox.Context(nfeatures=1000, max_w=w, max_h=h, slots=B, score_type=0)
+    ctx.upload(frames)
+    ctx.extract(0, B)
+    ctx.sync()
+    ref = RefExtractor(1000, score_type=0)
+    for s in (0, 21, 42, 63):
+        rk, rd = ref(frames[s])
+        gk, gd = ctx.features(s)
+        assert_kps_equal(gk, rk)
+        assert np.array_equal(gd, rd)
+    ctx.close()
