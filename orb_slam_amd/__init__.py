@@ -170,9 +170,11 @@ class Context:
         return out[:n]
 
     def __call__(self, image, mask=None):
-        """ORBextractor::operator()(image, mask, keypoints, descriptors)."""
-        if mask is not None and np.asarray(mask).size:
-            raise OrbxError(-4, "masked extraction (the reference never passes a mask)")
+        """ORBextractor::operator()(image, mask, keypoints, descriptors).
+
+        `mask` is accepted and has no effect, as in the reference: it only
+        feeds mvMaskPyramid (src/ORBextractor.cc:792-812), whose per-cell
+        ROI (:601-603) FAST never reads (:607, :613)."""
         img = np.ascontiguousarray(image, dtype=np.uint8)
         h, w = img.shape if img.ndim == 2 else (0, 0)
         kps = np.zeros(self.nfeatures, KEYPOINT)

@@ -87,6 +87,15 @@ public:
         descriptors.resize((size_t)n * 32);
     }
 
+    // With a mask (any size / content): the reference builds mvMaskPyramid
+    // from it (:792-812) but FAST never reads the cell mask (:601-613), so
+    // the outputs are those of the unmasked call.
+    void operator()(const uint8_t* image, int w, int h, size_t stride, const uint8_t* /*mask*/,
+                    std::vector<KeyPoint>& keypoints, std::vector<uint8_t>& descriptors)
+    {
+        (*this)(image, w, h, stride, keypoints, descriptors);
+    }
+
     int GetLevels() const { return orbx_get_levels(ctx_.get()); }
     float GetScaleFactor() const { return orbx_get_scale_factor(ctx_.get()); }
     std::vector<int> GetFeaturesPerLevel() const

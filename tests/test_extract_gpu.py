@@ -91,6 +91,13 @@ def test_operator_call_and_batch_consistency():
     rk, rd = ref(frames[2])
     assert_kps_equal(k1, rk)
     assert np.array_equal(d1, rd)
+    # a mask does not change the result (the reference never reads the
+    # cell mask, src/ORBextractor.cc:601-613)
+    mask = np.zeros((h, w), np.uint8)
+    mask[:, : w // 2] = 255
+    km, dm = ctx(frames[2], mask)
+    assert_kps_equal(km, rk)
+    assert np.array_equal(dm, rd)
     # empty image: returns without keypoints (src/ORBextractor.cc:721-722)
     k0, d0 = ctx(np.zeros((0, 0), np.uint8))
     assert len(k0) == 0 and len(d0) == 0
