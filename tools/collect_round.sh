@@ -5,13 +5,18 @@
 #           serialised c2 kernel trace (tools/extract_serial.py)
 #   part 2: tools/collect_profiles.sh for c2, c3, c5, pose (kernel trace +
 #           stats, FETCH_SIZE, WRITE_SIZE and one SQ pass each)
-# usage: tools/collect_round.sh 1|2 ; every GPU step has its own time limit
+# usage: tools/collect_round.sh 1|2|bench ; every GPU step has its own time limit
 # and the first failure ends the script.
 set -e -o pipefail
 out=gpurun_out/round
 mkdir -p "$out"
 export TMPDIR=/tmp
-if [ "$1" = 1 ]; then
+if [ "$1" = bench ]; then   # the four bench lines only (after the profiles exist)
+timeout -k 10 300 python3 bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err"
+timeout -k 10 300 python3 bench.py --workload pose --cpu-budget 10 > "$out/bench_pose.json" 2> "$out/bench_pose.err"
+timeout -k 10 300 python3 bench.py --workload c3 --cpu-budget 10 > "$out/bench_c3.json" 2> "$out/bench_c3.err"
+timeout -k 10 300 python3 bench.py --workload c5 --cpu-budget 10 > "$out/bench_c5.json" 2> "$out/bench_c5.err"
+elif [ "$1" = 1 ]; then
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > "$out/gpu_tests.log" 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 timeout -k 10 300 python3 bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err"
