@@ -209,6 +209,24 @@ __device__ inline int block_max(int v, BlockScratch& s, int buf)
 // k = 1..m where m = max_s min(#L before s, #R at/after s), and returns
 // L_1 (m == 0) or min(L_{m+1}, R_m).
 // --------------------------------------------------------------------------
+// XCD-aware block order for a (chunk, frame) grid launched as C x
+// roundup(nframes, 8) blocks.  Blocks are dealt round-robin over the 8 XCDs
+// (blocks p and p + 8 share one L2; MI355X_MICROARCH.md, workgroup
+// dispatch), so frame f's chunks are taken by the blocks p = 8 j + f % 8,
+// j = (f / 8) C .. (f / 8 + 1) C - 1: one frame's chunks share an L2 and the
+// data they have in common (overlapping rows, patches) is fetched once.
+// frame >= nframes marks a padding block (return before any barrier).
+struct XcdBlock {
+    int chunk, frame;
+};
+__device__ inline XcdBlock xcd_block()
+{
+    const int C = gridDim.x;
+    const int p = blockIdx.x + C * blockIdx.y, j = p >> 3, g = j / C;
+    return {j - g * C, 8 * g + (p & 7)};
+}
+__host__ inline int xcd_frames(int nframes) { return (nframes + 7) & ~7; }
+
 // Harris entries (scoreType == HARRIS_SCORE) are u64: the order-preserving
 // bit image of the float response (harris_key) in the high word, y<<12 | x
 // in the low word.

@@ -1259,13 +1259,17 @@ __device__ inline int half_wave_sum(int v)
 // step (fastAtan2, the correctly rounded sin/cos) is shared by two
 // keypoints per instruction, and the pattern's 256 tests map onto 8 rounds
 // of 32 lanes (ballot halves = 32 descriptor bits each).
-__global__ __launch_bounds__(256) void k_describe(ExtractArgs a)
+__global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_patch[2 * kWaves][kDescWaveBytes];
-    const int f = blockIdx.y;
+    // XCD-aware order (xcd_block): a frame's keypoint patches, which overlap,
+    // are fetched into one XCD's L2
+    const XcdBlock xb = xcd_block();
+    const int f = xb.frame, chunk = xb.chunk;
+    if (f >= nframes) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
     const int slot = wv * 2 + half;
-    const int k = blockIdx.x * (2 * kWaves) + slot;
+    const int k = chunk * (2 * kWaves) + slot;
     // tables needed later, loaded up front (independent of the keypoint):
     // umax[0..15] one entry per lane, this lane's 8 pattern pairs
     const int umax_l = a.umax[min(lane, kHalfPatch)];
@@ -1581,7 +1585,8 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_end(ctx, "blur", st);
         }
         timer_begin(ctx, "describe", st);
-        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), nb), dim3(256), 0, st, x);
+        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), xcd_frames(nb)), dim3(256), 0,
+                           st, x, nb);
         timer_end(ctx, "describe", st);
     };
     auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
