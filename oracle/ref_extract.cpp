@@ -74,8 +74,21 @@ void cv24_resize_linear_u8(const uint8_t* src, int sstep, int sw, int sh,
     const int iscale_x = (int)std::lrint(scale_x), iscale_y = (int)std::lrint(scale_y);
     const bool area_fast = std::fabs(scale_x - iscale_x) < 2.220446049250313e-16 &&
                            std::fabs(scale_y - iscale_y) < 2.220446049250313e-16;
-    if (area_fast && iscale_x == 2 && iscale_y == 2)
-        throw std::runtime_error("resize: exact 2x decimation takes the INTER_AREA path (unsupported)");
+    if (area_fast && iscale_x == 2 && iscale_y == 2) {
+        // cv::resize reroutes INTER_LINEAR at exactly 2x to INTER_AREA's fast
+        // path: resizeAreaFast_ with ResizeAreaFastVec<uchar> in fast mode
+        // (scale 2, cn 1): D = (S00 + S01 + S10 + S11 + 2) >> 2 over the
+        // dwidth1 = sw / 2 columns and rows whose two source rows exist --
+        // all of them when sw = 2 dw and sh = 2 dh.
+        for (int dy = 0; dy < dh; dy++) {
+            const uint8_t* S = src + (size_t)(2 * dy) * sstep;
+            const uint8_t* T = S + sstep;
+            uint8_t* D = dst + (size_t)dy * dstep;
+            for (int dx = 0; dx < dw; dx++)
+                D[dx] = (uint8_t)((S[2 * dx] + S[2 * dx + 1] + T[2 * dx] + T[2 * dx + 1] + 2) >> 2);
+        }
+        return;
+    }
 
     const int kScale = 2048;  // INTER_RESIZE_COEF_SCALE
     std::vector<int> xofs(dw);

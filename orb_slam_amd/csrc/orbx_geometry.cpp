@@ -85,7 +85,15 @@ static int resize_tables(Geometry& g, int sw, int sh, int dw, int dh)
     const int isx = (int)std::lrint(sx_scale), isy = (int)std::lrint(sy_scale);
     const bool area_fast = std::fabs(sx_scale - isx) < 2.220446049250313e-16 &&
                            std::fabs(sy_scale - isy) < 2.220446049250313e-16;
-    if (area_fast && isx == 2 && isy == 2) return ORBX_ERR_UNSUPPORTED;  // INTER_AREA path
+    // At exactly 2x cv::resize takes INTER_AREA's fast path, (S00 + S01 +
+    // S10 + S11 + 2) >> 2 (ResizeAreaFastVec<uchar>).  The INTER_LINEAR
+    // tables built below are then fx = fy = 1/2 (weights 1024 / 1024) and
+    // both of its roundings, ((S0 >> 4) * 1024 >> 16) + ... + 2 >> 2 and
+    // (S0 * 1024 + S1 * 1024 + 2^21) >> 22, reduce to that same value, so
+    // the linear kernels compute the area result bit for bit (OpenCV's own
+    // comment at the switch: "INTER_AREA (fast) also is equal to
+    // INTER_LINEAR" there).
+    (void)area_fast;
     int xmax = dw;
     std::vector<int> xofs(dw);
     std::vector<int16_t> a0(dw), a1(dw);

@@ -188,3 +188,55 @@ def test_harris_large_batch_pipeline():
         assert_kps_equal(gk, rk)
         assert np.array_equal(gd, rd)
     ctx.close()
+
+
+# ORBextractor parameters other than Settings.yaml's defaults (nFeatures,
+# scaleFactor, nLevels, fastTh: src/Tracking.cc:105-113); fastTh < 7 makes
+# the threshold-7 fallback the higher threshold (src/ORBextractor.cc:607-614).
+CONFIGS = [
+    (500, 1.5, 4, 20, 1),
+    (2000, 1.1, 12, 10, 1),
+    (1200, 1.3, 6, 35, 1),
+    (1000, 2.0, 3, 5, 1),
+    (800, 1.25, 10, 20, 0),   # HARRIS_SCORE
+]
+
+
+@pytest.mark.parametrize("nf,scale,nlev,fth,score", CONFIGS)
+@pytest.mark.parametrize("kind,w,h,seed", [("texture", 640, 480, 21), ("noise", 333, 251, 22)])
+def test_extractor_configs_match_oracle(nf, scale, nlev, fth, score, kind, w, h, seed):
+    img = make(kind, w, h, seed)
+    ref = RefExtractor(nf, scale=scale, nlevels=nlev, fast_th=fth, score_type=score)
+    rk, rd = ref(img)
+    ctx = ox.Context(nfeatures=nf, scale_factor=scale, nlevels=nlev, score_type=score, fast_th=fth,
+                     max_w=w, max_h=h, slots=1)
+    assert ctx.GetLevels() == nlev
+    ctx.upload(img)
+    ctx.extract(0, 1)
+    ctx.sync()
+    for lvl in range(nlev):
+        assert np.array_equal(ctx.level(0, lvl), ref.level(lvl)), f"raw level {lvl}"
+        assert np.array_equal(ctx.level(0, lvl, blurred=True), ref.level(lvl, blurred=True)), f"blurred level {lvl}"
+    gk, gd = ctx.features(0)
+    assert_kps_equal(gk, rk)
+    assert np.array_equal(gd, rd)
+    ctx.close()
+
+
+@pytest.mark.parametrize("nf,scale,nlev,fth,score", CONFIGS[:2])
+def test_extractor_configs_batch_pipeline(nf, scale, nlev, fth, score):
+    """A non-default configuration through the multi-stream batch path."""
+    w, h, B = 640, 480, 64
+    frames = synth.sequence(w, h, B, seed=31)
+    ctx = ox.Context(nfeatures=nf, scale_factor=scale, nlevels=nlev, score_type=score, fast_th=fth,
+                     max_w=w, max_h=h, slots=B)
+    ctx.upload(frames)
+    ctx.extract(0, B)
+    ctx.sync()
+    ref = RefExtractor(nf, scale=scale, nlevels=nlev, fast_th=fth, score_type=score)
+    for s in (0, 33, 63):
+        rk, rd = ref(frames[s])
+        gk, gd = ctx.features(s)
+        assert_kps_equal(gk, rk)
+        assert np.array_equal(gd, rd)
+    ctx.close()

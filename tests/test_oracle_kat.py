@@ -172,6 +172,20 @@ def test_resize_constant_and_identity(ref):
     assert np.array_equal(same, r)
 
 
+def test_resize_exact_half_is_area_fast(ref):
+    """Exactly 2x: cv::resize reroutes INTER_LINEAR to INTER_AREA's fast path,
+    (S00 + S01 + S10 + S11 + 2) >> 2 (ResizeAreaFastVec<uchar>); a ratio just
+    off 2 stays INTER_LINEAR."""
+    r = np.random.default_rng(4).integers(0, 256, (48, 64), dtype=np.uint8)
+    dst = np.zeros((24, 32), np.uint8)
+    assert ref.orbx_ref_resize(ptr(r), 64, 64, 48, ptr(dst), 32, 32, 24) == 0
+    s = r.astype(np.int32)
+    want = (s[0::2, 0::2] + s[0::2, 1::2] + s[1::2, 0::2] + s[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(dst, want)
+    odd = np.zeros((24, 33), np.uint8)   # 64 -> 33 columns: linear
+    assert ref.orbx_ref_resize(ptr(r), 64, 64, 48, ptr(odd), 33, 33, 24) == 0
+
+
 @pytest.mark.parametrize("n,keep,seed", [(50, 10, 0), (200, 37, 1), (1000, 217, 2), (30, 30, 3), (30, 40, 4),
                                          (500, 1, 5)])
 def test_retain_best_keeps_top_n(ref, n, keep, seed):
