@@ -50,6 +50,52 @@ def test_match_prev_matches_oracle(n, seq_len):
     ctx.close()
 
 
+@pytest.mark.parametrize("window,nnratio,check_ori", [(50, 0.6, True), (150, 0.75, False), (20, 0.9, False)])
+def test_match_prev_parameters(window, nnratio, check_ori):
+    """The batched device path with ORBmatcher(nnratio, checkOri) and window
+    sizes other than Tracking's (src/Tracking.cc:361: 0.9, true, 100)."""
+    w, h, n, seq_len = 640, 480, 1000, 6
+    frames = synth.sequence(w, h, seq_len, seed=40 + window)
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_prev(0, seq_len, seq_len, window=window, nnratio=nnratio, check_ori=check_ori)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        k1, d1 = feats[p]
+        k2, d2 = feats[s]
+        rm, rn = ref_search_init(L, k1, d1, k2, d2, w, h, window, nnratio, check_ori)
+        gm, gn = ctx.matches(s)
+        assert gn == rn, (s, gn, rn)
+        assert np.array_equal(gm[:len(k1)], rm), (s, np.count_nonzero(gm[:len(k1)] != rm))
+    ctx.close()
+
+
+@pytest.mark.parametrize("th_low,nnratio", [(40, 0.8), (80, 0.95)])
+def test_match_bf_prev_parameters(th_low, nnratio):
+    w, h, n, seq_len = 640, 480, 1000, 3
+    frames = synth.sequence(w, h, seq_len, seed=th_low)
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_bf_prev(0, seq_len, seq_len, th_low=th_low, nnratio=nnratio)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        dA, dB = feats[p][1], feats[s][1]
+        bi, b1, b2 = (np.zeros(len(dA), np.int32) for _ in range(3))
+        L.orbx_ref_hamming_bf(ptr(dA), len(dA), ptr(dB), len(dB), ptr(bi), ptr(b1), ptr(b2))
+        want = np.where((b1 <= th_low) & (b1.astype(np.float32) < b2.astype(np.float32) * np.float32(nnratio)), bi, -1)
+        gm, gn = ctx.matches(s)
+        assert np.array_equal(gm[:len(dA)], want)
+    ctx.close()
+
+
 def test_match_bf_prev_matches_oracle():
     """Device-resident brute-force pairs (C3) against the oracle's all-pairs
     best/second + the acceptance rule."""
