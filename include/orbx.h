@@ -461,6 +461,17 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
 int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems,
                          int iters0, int iters1, uint8_t* const* edge_status,
                          uint8_t* const* point_bad, orbx_ba_stats* stats);
+/* Device-resident form of the batch (bench/tests; the pose API's shape):
+ * stage P problems in HBM once (validated as orbx_lba_solve_batch does),
+ * run both optimize() passes from the staged state any number of times
+ * (asynchronous, on the context stream; kernel timers "lba_iter" /
+ * "lba_outliers"), fetch the last run's poses, points, flags and statistics
+ * into problems laid out like the staged ones (ORBX_ERR_ARG before a run or
+ * on a size mismatch). */
+int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems);
+int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1);
+int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edge_status,
+                   uint8_t* const* point_bad, orbx_ba_stats* stats);
 
 /* ------------------------------------------------------------------------ */
 /* D. Motion-only pose optimisation                   */

@@ -151,6 +151,7 @@ struct KernelTimer {
     int used = 0;
 };
 
+struct LbaResident;   // orbx_lba.hip
 }  // namespace orbx
 
 struct orbx_ctx {
@@ -228,6 +229,7 @@ struct orbx_ctx {
     void* host_pinned = nullptr;
     size_t host_pinned_bytes = 0;
     // staged pose-optimisation batch (orbx_pose_stage / run / fetch)
+    orbx::LbaResident* lba_res = nullptr;   // orbx_lba_stage's batch (orbx_lba.hip)
     void* pose_dev = nullptr;
     size_t pose_dev_bytes = 0;
     void* pose_host = nullptr;
@@ -271,6 +273,7 @@ int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 int ensure_scratch(orbx_ctx* ctx, size_t bytes);
+void lba_resident_free(orbx_ctx* ctx);
 int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 }  // namespace orbx
 

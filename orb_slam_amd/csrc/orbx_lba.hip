@@ -1008,11 +1008,6 @@ namespace {
 // doubles of LDS for the reduced system (160 KB less the Schur edge table)
 constexpr int kLdsSCap = (160 * 1024 - kLbaThreads * kSchurEdges * 8 - 1024) / 8;
 
-}  // namespace
-
-// Solves P problems; per problem a workgroup.  The problems' pose/point
-// arrays are updated in place.
-namespace {
 // Runs fn(i) for i in [0, n) on up to 16 host threads (independent problems).
 template <typename Fn>
 void host_parallel(int n, Fn fn)
@@ -1033,21 +1028,34 @@ void host_parallel(int n, Fn fn)
 inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 }  // namespace
 
-// Solves P problems; per problem a workgroup.  The problems' pose/point
-// arrays are updated in place.  Host staging: one planned layout, filled by
-// host threads straight into the context's pinned buffer, one copy each way.
-static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int iters1,
-                   const volatile uint8_t* abort, uint8_t* const* edge_status, uint8_t* const* point_bad,
-                   orbx_ba_stats* stats)
+// Device layout of one batch of P problems (planned on the host from the
+// problems' sizes): the staged block [0, staged_end) that the host fills --
+// the persistent part [0, base_bytes) (poses, points, cameras, per-point
+// observation counts, edge / point flags, offsets, outlier counts; poses
+// and points first, so the results copy reads back a prefix), the callers'
+// raw edge / id arrays, and both passes' LbaDev arrays -- then device-only:
+// the LM backups, the per-edge errors, both passes' structure arrays and the
+// scratch.
+struct LbaPlay {
+    size_t pose, point, posebk, pointbk, cam, err;
+};
+struct LbaPlan {
+    int P = 0;
+    uint8_t* d = nullptr;   // device base the LbaDev pointers were packed against
+    std::vector<LbaPlay> pl;
+    std::vector<long long> offs;   // per problem: first edge, first point (global flag arrays)
+    std::vector<int> n_poses, n_points, n_edges;
+    long long eacc = 0, pacc = 0;
+    size_t result_bytes = 0, base_bytes = 0, o_all_nobs = 0, o_all_st = 0, o_all_bad = 0, o_offs = 0, o_nout = 0;
+    size_t o_devs = 0, o_devs1 = 0, staged_end = 0, o_err = 0, err_bytes = 0, dev_end = 0, max_n2 = 0;
+    double chi2_threshold = 0;
+};
+
+// Plans the layout of P problems at device base d (nullptr: plan only, to
+// learn dev_end) and, with d set, packs the staged block into the pinned
+// buffer and queues its upload on the context stream.
+static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, uint8_t* d, LbaPlan& L)
 {
-    static const bool prof = getenv("ORBX_LBA_PROFILE_HOST") != nullptr;
-    auto tprev = std::chrono::steady_clock::now();
-    auto mark = [&](const char* what) {
-        if (!prof) return;
-        const auto t = std::chrono::steady_clock::now();
-        fprintf(stderr, "[lba host] %-22s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tprev).count());
-        tprev = t;
-    };
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         if (p.n_poses < 0 || p.n_points < 0 || p.n_edges < 0) return ORBX_ERR_ARG;
@@ -1061,49 +1069,44 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     });
     for (int i = 0; i < P; i++)
         if (bad_edge[i]) return ORBX_ERR_ARG;
-    ctx_enter(ctx);
-    // ---- persistent block (device-resident across both passes) ----
-    struct PLay {
-        size_t pose, point, posebk, pointbk, cam, err;
-    };
-    std::vector<PLay> pl(P);
-    std::vector<long long> offs(3 * P);
+    L = LbaPlan{};
+    L.P = P;
+    L.d = d;
+    L.chi2_threshold = P > 0 ? probs[0].chi2_threshold : 0;
+    L.pl.resize(P);
+    L.offs.assign(3 * (size_t)P, 0);
+    L.n_poses.resize(P);
+    L.n_points.resize(P);
+    L.n_edges.resize(P);
+    std::vector<LbaPlay>& pl = L.pl;
     size_t at = 0;
-    long long eacc = 0, pacc = 0;
-    // poses and points of all problems first: the results copy reads back
-    // only that prefix
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
+        L.n_poses[i] = p.n_poses;
+        L.n_points[i] = p.n_points;
+        L.n_edges[i] = p.n_edges;
         pl[i].pose = at;    at += align256(7 * (size_t)p.n_poses * 8);
         pl[i].point = at;   at += align256(3 * (size_t)p.n_points * 8);
     }
-    const size_t result_bytes = at;
+    L.result_bytes = at;
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         pl[i].cam = at;     at += align256(4 * (size_t)p.n_poses * 8);
-        offs[3 * i] = eacc;
-        offs[3 * i + 1] = pacc;
-        eacc += p.n_edges;
-        pacc += p.n_points;
+        L.offs[3 * i] = L.eacc;
+        L.offs[3 * i + 1] = L.pacc;
+        L.eacc += p.n_edges;
+        L.pacc += p.n_points;
     }
-    const size_t o_all_nobs = at; at += align256(4 * (size_t)pacc);
-    const size_t o_all_st = at;   at += align256((size_t)eacc);
-    const size_t o_all_bad = at;  at += align256((size_t)pacc);
-    const size_t o_offs = at;     at += align256(offs.size() * 8);
-    const size_t o_nout = at;     at += align256(8 * (size_t)P);   // outliers per problem, per pass
-    const size_t base_bytes = at;
-    std::vector<uint8_t> all_st((size_t)eacc, 0);
-    std::vector<LbaDev> devs(P);
-    int r = ORBX_OK;
-    mark("setup");
+    L.o_all_nobs = at; at += align256(4 * (size_t)L.pacc);
+    L.o_all_st = at;   at += align256((size_t)L.eacc);
+    L.o_all_bad = at;  at += align256((size_t)L.pacc);
+    L.o_offs = at;     at += align256(L.offs.size() * 8);
+    L.o_nout = at;     at += align256(8 * (size_t)P);   // outliers per problem, per pass
+    L.base_bytes = at;
     // Both optimize() calls' structures are built on the device: the first
     // from the caller's arrays (k_lba_build), the second from the first's
     // after the first outlier pass (k_lba_rebuild), so the host only stages
     // the problems, and both passes run back to back after one upload.
-    // Layout after the persistent block: the caller's edge / id arrays, both
-    // LbaDev arrays (pointers from the host, counts from the builds), then
-    // device-only: the two passes' structure arrays (sized by the problem:
-    // every edge, pose and point), the scratch (sized by the free poses).
     constexpr int kRaw = 7, kArr = 15;
     std::vector<size_t> so_raw(kRaw * (size_t)P), so(kArr * (size_t)P), so1(kArr * (size_t)P);
     std::vector<int> nfree(P, 0);
@@ -1117,13 +1120,14 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         const size_t b[kRaw] = {E * 4, E * 4, E * 16, E * 8, NP, NP * 8, NL * 8};
         for (int k = 0; k < kRaw; k++) bytes[k] = b[k];
     };
-    auto arr_bytes = [&](const orbx_ba_problem& p, size_t (&bytes)[kArr]) {
-        const size_t E = p.n_edges, NP = nfree[&p - probs], NL = p.n_points;
+    auto arr_bytes = [&](int i, size_t (&bytes)[kArr]) {
+        const orbx_ba_problem& p = probs[i];
+        const size_t E = p.n_edges, NP = nfree[i], NL = p.n_points;
         const size_t b[kArr] = {E * 4,  E * 4,        E * 4,  E * 4,        E * 4,  E * 16,       E * 8, NP * 4,
                                 NL * 4, (NP + 1) * 4, E * 4, (NL + 1) * 4, E * 4, (NL + 1) * 4, E * 4};
         for (int k = 0; k < kArr; k++) bytes[k] = b[k];
     };
-    size_t end = base_bytes;
+    size_t end = L.base_bytes;
     for (int i = 0; i < P; i++) {
         size_t bytes[kRaw];
         raw_bytes(probs[i], bytes);
@@ -1132,27 +1136,27 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             end += align256(bytes[k]);
         }
     }
-    const size_t o_devs = end;
+    L.o_devs = end;
     end += align256(sizeof(LbaDev) * P);
-    const size_t o_devs1 = end;
+    L.o_devs1 = end;
     end += align256(sizeof(LbaDev) * P);
-    const size_t staged_end = end;
+    L.staged_end = end;
     // device-only: the LM backups and the per-edge errors (zeroed on the device)
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         pl[i].posebk = end;  end += align256(7 * (size_t)p.n_poses * 8);
         pl[i].pointbk = end; end += align256(3 * (size_t)p.n_points * 8);
     }
-    const size_t o_err = end;
+    L.o_err = end;
     for (int i = 0; i < P; i++) {
         pl[i].err = end;
         end += align256(2 * (size_t)probs[i].n_edges * 8);
     }
-    const size_t err_bytes = end - o_err;
+    L.err_bytes = end - L.o_err;
     for (int pass = 0; pass < 2; pass++)
         for (int i = 0; i < P; i++) {
             size_t bytes[kArr];
-            arr_bytes(probs[i], bytes);
+            arr_bytes(i, bytes);
             for (int k = 0; k < kArr; k++) {
                 (pass == 0 ? so : so1)[kArr * i + k] = end;
                 end += align256(bytes[k]);
@@ -1161,11 +1165,10 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     // device-only scratch, sized by the free poses, every point and edge
     // (the Hpl scratch also holds k_lba_build's and k_lba_rebuild's maps)
     std::vector<size_t> sc(8 * (size_t)P);
-    size_t max_n2 = 0;
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         const size_t nE = p.n_edges, nL = p.n_points, n = 6 * (size_t)nfree[i];
-        max_n2 = std::max(max_n2, n * n + n);
+        L.max_n2 = std::max(L.max_n2, n * n + n);
         const size_t bytes[7] = {std::max(18 * nE * 8, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
                                  9 * nL * 8, 12 * nL * 8, n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * nL) * 8,
                                  n * 8 + 8};
@@ -1174,12 +1177,12 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             end += align256(bytes[k]);
         }
     }
-    const size_t dev_end = end;
-    if (dev_end > ctx->scratch_bytes && (r = ensure_scratch(ctx, dev_end)) != ORBX_OK) return r;
-    if ((r = ensure_pinned(ctx, staged_end)) != ORBX_OK) return r;
+    L.dev_end = end;
+    if (!d) return ORBX_OK;
+    int r;
+    if ((r = ensure_pinned(ctx, L.staged_end)) != ORBX_OK) return r;
     uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
-    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
-    std::vector<LbaDev> devs1(P);
+    std::vector<LbaDev> devs(P), devs1(P);
     // fill the staged bytes on host threads
     host_parallel(P, [&](int i) {
         const orbx_ba_problem& p = probs[i];
@@ -1190,9 +1193,9 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         }
         std::memcpy(hb + pl[i].point, p.points, 3 * (size_t)p.n_points * 8);
         std::memcpy(hb + pl[i].cam, p.pose_cam, 4 * (size_t)p.n_poses * 8);
-        std::memcpy(hb + o_all_nobs + 4 * (size_t)offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
-        std::memset(hb + o_all_st + offs[3 * i], 0, (size_t)p.n_edges);
-        std::memset(hb + o_all_bad + offs[3 * i + 1], 0, (size_t)p.n_points);
+        std::memcpy(hb + L.o_all_nobs + 4 * (size_t)L.offs[3 * i + 1], p.point_nobs, 4 * (size_t)p.n_points);
+        std::memset(hb + L.o_all_st + L.offs[3 * i], 0, (size_t)p.n_edges);
+        std::memset(hb + L.o_all_bad + L.offs[3 * i + 1], 0, (size_t)p.n_points);
         const void* src[kRaw] = {p.edge_pose, p.edge_point, p.edge_obs, p.edge_inv_sigma2,
                                  p.pose_fixed, p.pose_id, p.point_id};
         size_t rb[kRaw];
@@ -1248,26 +1251,36 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         fill(devs[i], &so[kArr * i]);     // counts and contents: k_lba_build
         fill(devs1[i], &so1[kArr * i]);   // counts and contents: k_lba_rebuild
     });
-    std::memcpy(hb + o_offs, offs.data(), offs.size() * 8);
-    std::memcpy(hb + o_devs, devs.data(), sizeof(LbaDev) * P);
-    std::memcpy(hb + o_devs1, devs1.data(), sizeof(LbaDev) * P);
-    mark("pack");
-    ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, staged_end, hipMemcpyHostToDevice, ctx->stream));
-    ORBX_HIP_CHECK(hipMemsetAsync(d + o_err, 0, err_bytes, ctx->stream));
-    mark("upload");
+    std::memcpy(hb + L.o_offs, L.offs.data(), L.offs.size() * 8);
+    std::memcpy(hb + L.o_devs, devs.data(), sizeof(LbaDev) * P);
+    std::memcpy(hb + L.o_devs1, devs1.data(), sizeof(LbaDev) * P);
+    ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, L.staged_end, hipMemcpyHostToDevice, ctx->stream));
+    return ORBX_OK;
+}
+
+// Queues both optimize() passes of a staged batch on the context stream:
+// k_lba_build, iterations, outliers, k_lba_rebuild, iterations, outliers.
+// With an abort flag the host polls it (and the problems' status) between
+// iterations, which synchronises; without one nothing waits.
+static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, const volatile uint8_t* abort)
+{
+    const int P = L.P;
+    uint8_t* d = L.d;
+    ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_err, 0, L.err_bytes, ctx->stream));
     timer_begin(ctx, "lba_build");
-    hipLaunchKernelGGL(k_lba_build, dim3(P), dim3(kLbaThreads), 0, ctx->stream, reinterpret_cast<LbaDev*>(d + o_devs));
+    hipLaunchKernelGGL(k_lba_build, dim3(P), dim3(kLbaThreads), 0, ctx->stream, reinterpret_cast<LbaDev*>(d + L.o_devs));
     timer_end(ctx, "lba_build");
     ORBX_HIP_CHECK(hipGetLastError());
-    const size_t lds = std::min(max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
+    const size_t lds = std::min(L.max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
     const int lds_cap = (int)(lds / 8);
-    for (int pass = 0; pass < 2 && r == ORBX_OK; pass++) {
-        LbaDev* dd = reinterpret_cast<LbaDev*>(d + (pass == 0 ? o_devs : o_devs1));
+    std::vector<LbaDev> hv(abort ? P : 0);
+    for (int pass = 0; pass < 2; pass++) {
+        LbaDev* dd = reinterpret_cast<LbaDev*>(d + (pass == 0 ? L.o_devs : L.o_devs1));
         if (pass == 1) {
             timer_begin(ctx, "lba_rebuild");
             hipLaunchKernelGGL(k_lba_rebuild, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
-                               reinterpret_cast<const LbaDev*>(d + o_devs), dd, d + o_all_st,
-                               reinterpret_cast<const long long*>(d + o_offs));
+                               reinterpret_cast<const LbaDev*>(d + L.o_devs), dd, d + L.o_all_st,
+                               reinterpret_cast<const long long*>(d + L.o_offs));
             timer_end(ctx, "lba_rebuild");
             ORBX_HIP_CHECK(hipGetLastError());
         }
@@ -1290,7 +1303,6 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
             // without one, iterations are queued back to back and a
             // terminated problem's later launches return immediately.
             if (abort) {
-                std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
                 ORBX_HIP_CHECK(hipMemcpyAsync(hv.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
                 ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
                 bool running = false;
@@ -1300,22 +1312,39 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
         }
         timer_begin(ctx, "lba_outliers");
         hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(256), 0, ctx->stream, dd,
-                           reinterpret_cast<int*>(d + o_all_nobs), d + o_all_st, d + o_all_bad, pass + 1,
-                           probs[0].chi2_threshold, reinterpret_cast<int*>(d + o_nout) + pass * P,
-                           reinterpret_cast<const long long*>(d + o_offs));
+                           reinterpret_cast<int*>(d + L.o_all_nobs), d + L.o_all_st, d + L.o_all_bad, pass + 1,
+                           L.chi2_threshold, reinterpret_cast<int*>(d + L.o_nout) + pass * P,
+                           reinterpret_cast<const long long*>(d + L.o_offs));
         timer_end(ctx, "lba_outliers");
         ORBX_HIP_CHECK(hipGetLastError());
     }
+    return ORBX_OK;
+}
+
+// Reads a solved batch back (synchronising the context stream): poses and
+// points into the problems' arrays, edge / point flags, statistics.
+static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs, uint8_t* const* edge_status,
+                        uint8_t* const* point_bad, orbx_ba_stats* stats)
+{
+    const int P = L.P;
+    uint8_t* d = L.d;
+    int r;
+    if ((r = ensure_pinned(ctx, std::max(L.result_bytes, L.o_all_bad + (size_t)L.pacc))) != ORBX_OK) return r;
+    uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
+    std::vector<LbaDev> devs(P), devs1(P);
+    std::vector<uint8_t> all_st((size_t)L.eacc, 0);
     std::vector<int> nout(2 * (size_t)P);
-    ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), d + o_devs, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(devs1.data(), d + o_devs1, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + o_nout, 8 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), d + L.o_devs, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(devs1.data(), d + L.o_devs1, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
+    if (L.eacc)
+        ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + L.o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + L.o_nout, 8 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
     // results: poses and points in one copy, scattered on host threads below
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, result_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb + o_all_bad, d + o_all_bad, (size_t)pacc, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, L.result_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (L.pacc)
+        ORBX_HIP_CHECK(hipMemcpyAsync(hb + L.o_all_bad, d + L.o_all_bad, (size_t)L.pacc, hipMemcpyDeviceToHost,
+                                      ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    mark("iterations+outliers+results copy");
     if (stats)
         for (int pass = 0; pass < 2; pass++) {
             const std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
@@ -1328,20 +1357,106 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
                 stats[i].not_posdef += hv[i].not_posdef;
             }
         }
-
     host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
-        const double* pose = reinterpret_cast<const double*>(hb + pl[i].pose);
+        const double* pose = reinterpret_cast<const double*>(hb + L.pl[i].pose);
         for (int k = 0; k < p.n_poses; k++) {
             for (int j = 0; j < 4; j++) p.pose_q[4 * k + j] = pose[7 * k + j];
             for (int j = 0; j < 3; j++) p.pose_t[3 * k + j] = pose[7 * k + 4 + j];
         }
-        std::memcpy(p.points, hb + pl[i].point, 3 * (size_t)p.n_points * 8);
-        if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st.data() + offs[3 * i], p.n_edges);
-        if (point_bad && point_bad[i]) std::memcpy(point_bad[i], hb + o_all_bad + offs[3 * i + 1], p.n_points);
+        std::memcpy(p.points, hb + L.pl[i].point, 3 * (size_t)p.n_points * 8);
+        if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st.data() + L.offs[3 * i], p.n_edges);
+        if (point_bad && point_bad[i]) std::memcpy(point_bad[i], hb + L.o_all_bad + L.offs[3 * i + 1], p.n_points);
     });
-    mark("results");
     return ORBX_OK;
+}
+
+// Solves P problems from host arrays; per problem a workgroup.  The
+// problems' pose/point arrays are updated in place.  One planned layout in
+// the context scratch, filled by host threads straight into the pinned
+// buffer, one copy each way.
+static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int iters1,
+                   const volatile uint8_t* abort, uint8_t* const* edge_status, uint8_t* const* point_bad,
+                   orbx_ba_stats* stats)
+{
+    ctx_enter(ctx);
+    LbaPlan L;
+    int r = lba_plan_stage(ctx, P, probs, nullptr, L);   // sizes only
+    if (r != ORBX_OK) return r;
+    if (L.dev_end > ctx->scratch_bytes && (r = ensure_scratch(ctx, L.dev_end)) != ORBX_OK) return r;
+    if ((r = lba_plan_stage(ctx, P, probs, static_cast<uint8_t*>(ctx->scratch), L)) != ORBX_OK) return r;
+    if ((r = lba_launch(ctx, L, iters0, iters1, abort)) != ORBX_OK) return r;
+    return lba_readback(ctx, L, probs, edge_status, point_bad, stats);
+}
+
+// Device-resident form (orbx_lba_stage / _run / _fetch): the batch lives in
+// a buffer of its own, with a copy of the staged block's mutable parts
+// (poses, points, counts and flags; both LbaDev arrays) that every run
+// restores first, so each run starts from the staged problems.
+struct LbaResident {
+    LbaPlan plan;
+    void* dev = nullptr;
+    void* image = nullptr;
+    size_t dev_bytes = 0, image_bytes = 0;
+    bool solved = false;
+};
+
+void lba_resident_free(orbx_ctx* ctx)
+{
+    if (!ctx->lba_res) return;
+    if (ctx->lba_res->dev) (void)hipFree(ctx->lba_res->dev);
+    if (ctx->lba_res->image) (void)hipFree(ctx->lba_res->image);
+    delete ctx->lba_res;
+    ctx->lba_res = nullptr;
+}
+
+static int lba_stage_resident(orbx_ctx* ctx, int P, const orbx_ba_problem* probs)
+{
+    ctx_enter(ctx);
+    if (!ctx->lba_res) ctx->lba_res = new (std::nothrow) LbaResident();
+    if (!ctx->lba_res) return ORBX_ERR_NOMEM;
+    LbaResident& R = *ctx->lba_res;
+    R.solved = false;
+    LbaPlan L;
+    int r = lba_plan_stage(ctx, P, probs, nullptr, L);
+    if (r != ORBX_OK) return r;
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (L.dev_end > R.dev_bytes) {
+        if (R.dev) (void)hipFree(R.dev);
+        R.dev = nullptr;
+        R.dev_bytes = 0;
+        if (hipMalloc(&R.dev, L.dev_end) != hipSuccess) return ORBX_ERR_NOMEM;
+        R.dev_bytes = L.dev_end;
+    }
+    if (L.staged_end > R.image_bytes) {
+        if (R.image) (void)hipFree(R.image);
+        R.image = nullptr;
+        R.image_bytes = 0;
+        if (hipMalloc(&R.image, L.staged_end) != hipSuccess) return ORBX_ERR_NOMEM;
+        R.image_bytes = L.staged_end;
+    }
+    if ((r = lba_plan_stage(ctx, P, probs, static_cast<uint8_t*>(R.dev), L)) != ORBX_OK) return r;
+    ORBX_HIP_CHECK(hipMemcpyAsync(R.image, R.dev, L.staged_end, hipMemcpyDeviceToDevice, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    R.plan = std::move(L);
+    return ORBX_OK;
+}
+
+static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1)
+{
+    if (!ctx->lba_res || ctx->lba_res->plan.P == 0) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    LbaResident& R = *ctx->lba_res;
+    const LbaPlan& L = R.plan;
+    uint8_t* d = static_cast<uint8_t*>(R.dev);
+    const uint8_t* img = static_cast<const uint8_t*>(R.image);
+    // mutable parts of the staged block: [0, base_bytes) and the LbaDev
+    // arrays (the raw edge / id arrays between them are only read)
+    ORBX_HIP_CHECK(hipMemcpyAsync(d, img, L.base_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(d + L.o_devs, img + L.o_devs, L.staged_end - L.o_devs, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+    R.solved = true;
+    return lba_launch(ctx, L, iters0, iters1, nullptr);
 }
 
 }  // namespace orbx
@@ -1371,6 +1486,32 @@ int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems, int it
     if (!ctx || P <= 0 || !problems || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
     if (stats) std::memset(stats, 0, sizeof(*stats) * P);
     return orbx::lba_run(ctx, P, problems, iters0, iters1, nullptr, edge_status, point_bad, stats);
+}
+
+int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems)
+{
+    if (!ctx || P <= 0 || !problems) return ORBX_ERR_ARG;
+    return orbx::lba_stage_resident(ctx, P, problems);
+}
+
+int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1)
+{
+    if (!ctx || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
+    return orbx::lba_run_resident(ctx, iters0, iters1);
+}
+
+int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edge_status, uint8_t* const* point_bad,
+                   orbx_ba_stats* stats)
+{
+    if (!ctx || !problems || !ctx->lba_res || !ctx->lba_res->solved) return ORBX_ERR_ARG;
+    const orbx::LbaPlan& L = ctx->lba_res->plan;
+    for (int i = 0; i < L.P; i++)
+        if (problems[i].n_poses != L.n_poses[i] || problems[i].n_points != L.n_points[i] ||
+            problems[i].n_edges != L.n_edges[i])
+            return ORBX_ERR_ARG;
+    if (stats) std::memset(stats, 0, sizeof(*stats) * L.P);
+    ctx_enter(ctx);
+    return orbx::lba_readback(ctx, L, problems, edge_status, point_bad, stats);
 }
 
 }  // extern "C"

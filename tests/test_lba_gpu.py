@@ -110,6 +110,48 @@ def test_lba_batch_equals_single(ctx):
         assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
 
 
+def test_lba_resident_equals_batch(ctx):
+    """orbx_lba_stage / _run / _fetch (problems resident in HBM, every run
+    restarting from the staged state) against orbx_lba_solve_batch on the
+    same problems; two runs in a row give the same results."""
+    probs = [sb.make_problem(n_kf=6 + k, n_points=200 + 50 * k, seed=40 + k, outlier_frac=0.03) for k in range(4)]
+
+    def marshal():
+        cps = [sb.to_ctypes(pr) for pr in probs]
+        arr = (sb.BAProblem * 4)(*[c[0] for c in cps])
+        es = [np.zeros(c[0].n_edges, np.uint8) for c in cps]
+        pb = [np.zeros(c[0].n_points, np.uint8) for c in cps]
+        esp = (ctypes.c_void_p * 4)(*[e.ctypes.data for e in es])
+        pbp = (ctypes.c_void_p * 4)(*[b.ctypes.data for b in pb])
+        return cps, arr, es, pb, esp, pbp, (sb.BAStats * 4)()
+
+    cps, arr, es, pb, esp, pbp, st = marshal()
+    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, esp, pbp, st) == 0
+    L = ox.lib()
+    s_cps, s_arr, _, _, _, _, _ = marshal()
+    assert L.orbx_lba_stage(ctx.handle, 4, s_arr) == 0
+    r_cps, r_arr, r_es, r_pb, r_esp, r_pbp, r_st = marshal()
+    assert L.orbx_lba_fetch(ctx.handle, r_arr, r_esp, r_pbp, r_st) == -1   # nothing run yet
+    runs = []
+    for _ in range(2):
+        assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+        r_cps, r_arr, r_es, r_pb, r_esp, r_pbp, r_st = marshal()
+        assert L.orbx_lba_fetch(ctx.handle, r_arr, r_esp, r_pbp, r_st) == 0
+        runs.append((r_cps, r_es, r_pb, r_st))
+    for r_cps, r_es, r_pb, r_st in runs:
+        for k in range(4):
+            a, b = r_cps[k][1], cps[k][1]
+            # FP64 atomics make the summation order run-dependent: equal up to rounding
+            assert np.abs(a["pose_q"] - b["pose_q"]).max() < 1e-10 and np.abs(a["points"] - b["points"]).max() < 1e-9
+            assert np.array_equal(r_es[k], es[k]) and np.array_equal(r_pb[k], pb[k])
+            assert list(r_st[k].n_outliers) == list(st[k].n_outliers)
+            assert list(r_st[k].iterations) == list(st[k].iterations)
+    # a problem set laid out differently from the staged one is refused
+    bad = [sb.to_ctypes(sb.make_problem(n_kf=5, n_points=100, seed=3))[0]] * 4
+    bad_arr = (sb.BAProblem * 4)(*bad)
+    assert L.orbx_lba_fetch(ctx.handle, bad_arr, None, None, None) == -1
+
+
 def test_lba_unsorted_vertex_ids(ctx):
     """Vertex ids that do not increase with the array index (a caller's
     keyframe / map-point order differing from mnId order): the Hessian block
