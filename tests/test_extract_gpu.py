@@ -240,3 +240,23 @@ def test_extractor_configs_batch_pipeline(nf, scale, nlev, fth, score):
         assert_kps_equal(gk, rk)
         assert np.array_equal(gd, rd)
     ctx.close()
+
+
+@pytest.mark.parametrize("w,h", [(333, 251), (1000, 562)])
+def test_ragged_large_batch_pipeline(w, h):
+    """Frame widths that are not multiples of 16 (gathered level-0 border
+    words, per-pixel resize tails) through the three-part batch pipeline."""
+    B = 48
+    frames = synth.sequence(w, h, B, seed=w)
+    ctx = ox.Context(nfeatures=1000, max_w=w, max_h=h, slots=B)
+    ctx.upload(frames)
+    ctx.extract(0, B)
+    ctx.sync()
+    ref = RefExtractor(1000)
+    for s in (0, 16, 47):
+        rk, rd = ref(frames[s])
+        gk, gd = ctx.features(s)
+        assert_kps_equal(gk, rk)
+        assert np.array_equal(gd, rd)
+        assert np.array_equal(ctx.level(s, 3), ref.level(3))
+    ctx.close()
