@@ -179,6 +179,42 @@ extern "C" {
 
 const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
 
+/* Diagnostics (not in include/orbx.h): the device error flags of the last
+ * batch without clearing them (1: a cell list overflowed its capacity,
+ * 2: a level list overflowed). */
+int orbx_debug_error_flags(orbx_ctx* ctx)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    int32_t flags = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&flags, ctx->error_flags, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_ERR_HIP;
+    return flags;
+}
+
+/* Diagnostics: per cell of slot `slot`'s last extraction, 8 ints: level, i,
+ * j, ini_x, ini_y, hx, hy, FAST corner count (list capacity in the 9th).
+ * Returns the number of cells. */
+int orbx_debug_cells(orbx_ctx* ctx, int slot, int32_t* out, int cap)
+{
+    if (!ctx || slot < 0 || slot >= ctx->slots) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    const Geometry& g = ctx->geom;
+    const int n = (int)g.cells.size();
+    if (cap < 9 * n) return ORBX_ERR_CAPACITY;
+    std::vector<int32_t> cnt(n);
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(cnt.data(), ctx->cell_count + (size_t)slot * n, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+        return ORBX_ERR_HIP;
+    for (int c = 0; c < n; c++) {
+        const CellGeom& C = g.cells[c];
+        const int32_t v[9] = {C.level, C.i, C.j, C.ini_x, C.ini_y, C.hx, C.hy, cnt[c], C.list_cap};
+        for (int k = 0; k < 9; k++) out[9 * c + k] = v[k];
+    }
+    return n;
+}
+
 int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, int nlevels,
                 int score_type, int fast_th, int max_w, int max_h, int max_batch)
 {

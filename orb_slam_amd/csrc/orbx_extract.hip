@@ -588,11 +588,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     clear_maps();
     __syncthreads();
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
-    const int q0 = c_lo >> 2, nqe = (c_hi >> 2) - q0 + 1; // dwords holding them
+    // dwords holding them; none when the ROI has no interior (hx < 7: a
+    // degenerate cell of a tiny level, where c_hi < c_lo and, with a large
+    // alignment shift, (c_hi >> 2) - q0 + 1 would go negative)
+    const int q0 = c_lo >> 2, nqe = c_hi >= c_lo ? (c_hi >> 2) - q0 + 1 : 0;
     const int q_last = q0 + nqe - 1;
     const int m_first = 0xF & ~((1 << (c_lo & 3)) - 1);  // pixels j >= c_lo & 3 of dword q0
     const int m_last = (1 << ((c_hi & 3) + 1)) - 1;      // pixels j <= c_hi & 3 of the last dword
-    const int nunits = (hy - 6) * nqe;
+    const int nunits = max(hy - 6, 0) * nqe;
     const uint32_t k64 = 0x64646464u;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {

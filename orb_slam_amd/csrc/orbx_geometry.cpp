@@ -272,7 +272,15 @@ int compute_geometry(Geometry& g, int w, int h)
         // iniXCol for rows > 0 is read from row 0 (same as the reference);
         // cells of later rows were pushed with iniXCol values already set
         // because row 0 is always processed first.
-        L.level_cap = nDesired + nCells * (nCells + 1) + 64;
+        // Bound on the retained cell lists of a level, Σ_c min(nTotal_c,
+        // nToRetain_c) (src/ORBextractor.cc:622-670): with q the quota of the
+        // cells still distributing and D the surplus to distribute, a round
+        // maps (Σ retained + D) to at most itself + m (1 + nfeaturesCell - q)
+        // over its m open cells (q' <= nfeaturesCell + D / m + 1).  Only the
+        // first round has q = nfeaturesCell; later ones have q >= it + 1.
+        // Start: nCells * nfeaturesCell <= nDesired + nCells - 1.  So the
+        // total stays <= nDesired + 2 nCells - 1 (slack: + 64).
+        L.level_cap = nDesired + 2 * nCells + 64;
         L.level_off = level_off;
         level_off += L.level_cap;   // the cell pass writes up to level_cap entries
         g.max_level_cap = std::max(g.max_level_cap, L.level_cap);

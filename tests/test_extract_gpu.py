@@ -4,12 +4,14 @@ Every comparison is bit-exact: pyramid levels (raw and blurred), keypoints
 (all seven cv::KeyPoint fields, in reference order) and descriptors.
 Reference: ORBextractor::operator() (src/ORBextractor.cc:718-779).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
 import orb_slam_amd as ox
 from orb_slam_amd import synth
-from oracle_lib import RefExtractor
+from oracle_lib import KEYPOINT as KEYPOINT_DT, RefExtractor
 
 pytestmark = pytest.mark.gpu
 
@@ -260,3 +262,46 @@ def test_ragged_large_batch_pipeline(w, h):
         assert np.array_equal(gd, rd)
         assert np.array_equal(ctx.level(s, 3), ref.level(3))
     ctx.close()
+
+
+def _random_configs(n, seed=2026):
+    r = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        w, h = int(r.integers(48, 720)), int(r.integers(48, 560))
+        out.append((w, h, int(r.integers(20, 2500)), float(np.float32(r.uniform(1.05, 1.6))), int(r.integers(1, 13)),
+                    int(r.integers(1, 60)), int(r.integers(0, 2)), ("texture", "noise", "rects")[i % 3], i))
+    return out
+
+
+@pytest.mark.parametrize("w,h,nf,scale,nlev,fth,score,kind,seed", _random_configs(40))
+def test_random_configs_match_oracle(w, h, nf, scale, nlev, fth, score, kind, seed):
+    """Seeded random extractor configurations and frame sizes: where the
+    oracle extracts, the GPU result is bit-exact; where the oracle refuses
+    (a configuration the reference cannot run, e.g. an empty cell grid), the
+    product refuses too."""
+    img = make(kind, w, h, seed)
+    ref = RefExtractor(nf, scale=scale, nlevels=nlev, fast_th=fth, score_type=score)
+    kps = np.zeros(nf, KEYPOINT_DT)
+    desc = np.zeros((nf, 32), np.uint8)
+    n = ctypes.c_int()
+    rc = ref.L.orbx_ref_extract(ref.h, img.ctypes.data_as(ctypes.c_void_p), w, h, w,
+                                kps.ctypes.data_as(ctypes.c_void_p), desc.ctypes.data_as(ctypes.c_void_p), nf,
+                                ctypes.byref(n))
+    try:
+        ctx = ox.Context(nfeatures=nf, scale_factor=scale, nlevels=nlev, score_type=score, fast_th=fth,
+                         max_w=w, max_h=h, slots=1)
+    except ox.OrbxError as e:
+        assert rc != 0, f"product refused a configuration the oracle runs: {e}"
+        return
+    try:
+        gk, gd = ctx(img)
+    except ox.OrbxError as e:
+        assert rc != 0, f"product refused a frame the oracle extracts: {e}"
+        return
+    finally:
+        ctx.close()
+    assert rc == 0, "product extracted a configuration the oracle refuses"
+    rk, rd = kps[:n.value], desc[:n.value]
+    assert_kps_equal(gk, rk)
+    assert np.array_equal(gd, rd)
