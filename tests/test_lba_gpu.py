@@ -163,3 +163,30 @@ def test_lba_unsorted_vertex_ids(ctx):
     prob["pose_id"] = r.permutation(prob["pose_id"])
     prob["point_id"] = r.permutation(prob["point_id"])
     compare(run_ref(prob), run_gpu(ctx, prob))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_lba_random_problems(ctx, seed):
+    """Seeded random local-BA problems against the oracle: keyframe and point
+    counts, extra fixed keyframes, fixed-pose patterns (down to every pose
+    fixed), outlier fractions, initial noise, vertex ids out of index order
+    and LM iteration budgets (including 0)."""
+    r = np.random.default_rng(1000 + seed)
+    nkf = int(r.integers(1, 25))
+    prob = sb.make_problem(n_kf=nkf, n_points=int(r.integers(30, 900)), n_fixed_extra=int(r.integers(0, 4)),
+                           seed=seed, outlier_frac=float(r.choice([0.0, 0.02, 0.1, 0.2])),
+                           pose_noise=(float(r.uniform(0.002, 0.03)), float(r.uniform(0.005, 0.06))),
+                           point_noise=float(r.uniform(0.005, 0.05)))
+    prob = dict(prob)
+    fixed = prob["pose_fixed"].copy()
+    mode = seed % 4
+    if mode == 1:
+        fixed[r.random(len(fixed)) < 0.3] = 1          # scattered fixed keyframes
+    elif mode == 2 and seed % 8 == 2:
+        fixed[:] = 1                                     # nothing to optimise but the points
+    prob["pose_fixed"] = fixed
+    if mode == 3:
+        prob["pose_id"] = r.permutation(prob["pose_id"])
+        prob["point_id"] = r.permutation(prob["point_id"])
+    i0, i1 = int(r.choice([0, 1, 3, 5])), int(r.choice([0, 2, 10]))
+    compare(run_ref(prob, i0, i1), run_gpu(ctx, prob, i0, i1))
