@@ -154,7 +154,8 @@ def test_search_by_projection_local(ctx, frames_feats, th):
     assert np.array_equal(mg, mr)
 
 
-@pytest.mark.parametrize("na,nb", [(1000, 1000), (2000, 1999), (1, 300), (257, 0)])
+@pytest.mark.parametrize("na,nb", [(1000, 1000), (2000, 1999), (1, 300), (257, 0), (0, 100), (65, 63), (3000, 4500),
+                                   (4097, 2)])
 def test_hamming_bf_and_match(ctx, na, nb):
     rng = np.random.default_rng(na + nb)
     dA = rng.integers(0, 256, (na, 32), dtype=np.uint8)
