@@ -211,3 +211,39 @@ def test_async_pipeline_reused_slots_odd_batch():
         assert np.array_equal(gk, rk) and np.array_equal(gd, rd), s
         assert gn == rn and np.array_equal(gm[:len(gk)], rm[:len(rk)]), s
     ctx.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_match_prev_random_sizes(seed):
+    """SearchForInitialization on the device path for random frame sizes and
+    feature counts (the frame grid's cell size follows the image bounds)."""
+    r = np.random.default_rng(300 + seed)
+    w, h = int(r.integers(120, 900)), int(r.integers(100, 700))
+    n, seq_len = int(r.integers(100, 2500)), 4
+    window = int(r.choice([30, 100, 200]))
+    frames = synth.sequence(w, h, seq_len, seed=400 + seed)
+    try:
+        ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    except ox.OrbxError as e:
+        # a level whose cell grid is empty: the reference divides by zero
+        # (src/ORBextractor.cc:533-541); the oracle refuses it as well
+        from oracle_lib import RefExtractor
+        with pytest.raises(AssertionError):
+            RefExtractor(n)(frames[0])
+        assert e.code == -4
+        return
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_prev(0, seq_len, seq_len, window=window, nnratio=0.9, check_ori=True)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        k1, d1 = feats[p]
+        k2, d2 = feats[s]
+        rm, rn = ref_search_init(L, k1, d1, k2, d2, w, h, window)
+        gm, gn = ctx.matches(s)
+        assert gn == rn, (s, gn, rn)
+        assert np.array_equal(gm[:len(k1)], rm)
+    ctx.close()
