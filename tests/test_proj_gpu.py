@@ -30,7 +30,8 @@ def gpu_fuse(ctx, KF, mps, T, sim3, th):
     return bi, bd
 
 
-@pytest.mark.parametrize("sim3,th,seed", [(0, 3.0, 0), (0, 5.0, 1), (1, 3.0, 2), (1, 10.0, 3)])
+@pytest.mark.parametrize("sim3,th,seed", [(0, 3.0, 0), (0, 5.0, 1), (1, 3.0, 2), (1, 10.0, 3), (0, 2.0, 4), (1, 7.5, 5),
+                                          (0, 12.0, 6), (1, 4.0, 7)])
 def test_fuse_candidates_match_oracle(ctx, sim3, th, seed):
     k1, d1, k2, d2, du, dv = pd.keyframes()
     rng = np.random.default_rng(seed)
@@ -49,7 +50,8 @@ def test_fuse_candidates_match_oracle(ctx, sim3, th, seed):
     assert np.array_equal(gb[0], rb[0]) and np.array_equal(gb[1], rb[1])
 
 
-@pytest.mark.parametrize("seed,th,prior", [(0, 7.5, 0.1), (1, 4.0, 0.0), (2, 10.0, 0.4)])
+@pytest.mark.parametrize("seed,th,prior", [(0, 7.5, 0.1), (1, 4.0, 0.0), (2, 10.0, 0.4), (3, 6.0, 0.2), (4, 9.0, 0.0),
+                                           (5, 3.0, 0.3)])
 def test_search_by_sim3_matches_oracle(ctx, seed, th, prior):
     c = sim3_case(seed, prior)
     K1, K2, m1, v1, m2, v2, T1, T2, s12, R12, t12, pr = c[:12]
@@ -64,7 +66,7 @@ def test_search_by_sim3_matches_oracle(ctx, seed, th, prior):
     assert np.array_equal(gn, rn)
 
 
-@pytest.mark.parametrize("seed", [0, 1])
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4])
 def test_distinctive_descriptors_match_oracle(ctx, seed):
     p, d = pd.distinctive_sets(n_mp=600, seed=seed)
     rb = ref_distinctive(p, d)
@@ -73,7 +75,8 @@ def test_distinctive_descriptors_match_oracle(ctx, seed):
     assert np.array_equal(gb, rb)
 
 
-@pytest.mark.parametrize("seed,th,scale", [(0, 10, 1.5), (1, 5, 1.0), (2, 20, 0.8)])
+@pytest.mark.parametrize("seed,th,scale", [(0, 10, 1.5), (1, 5, 1.0), (2, 20, 0.8), (3, 8, 1.2), (4, 12, 0.9),
+                                           (5, 15, 2.0)])
 def test_search_by_projection_kf_sim3_matches_oracle(ctx, seed, th, scale):
     from test_proj_oracle import ref_proj_kf_sim3, seq_case
     k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
@@ -93,7 +96,8 @@ def test_search_by_projection_kf_sim3_matches_oracle(ctx, seed, th, scale):
     assert np.array_equal(go, ro)
 
 
-@pytest.mark.parametrize("seed,th,orb,ori", [(0, 10.0, 100, 1), (1, 5.0, 64, 0), (2, 15.0, 50, 1)])
+@pytest.mark.parametrize("seed,th,orb,ori", [(0, 10.0, 100, 1), (1, 5.0, 64, 0), (2, 15.0, 50, 1), (3, 7.0, 80, 0),
+                                              (4, 20.0, 100, 1), (5, 9.0, 40, 1)])
 def test_search_by_projection_frame_kf_matches_oracle(ctx, seed, th, orb, ori):
     from test_proj_oracle import ref_proj_frame_kf, seq_case
     k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
