@@ -503,6 +503,26 @@ def main():
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
         if roof_iso:
+            # the PMC summary profiled the overlapped launches; the isolated
+            # pass launches each kernel over the whole step, so per-dispatch
+            # counts scale with the launch size (bytes and instructions are
+            # proportional to the frames a launch processes)
+            ratio = (roof_iso["algorithmic_bytes_per_launch"] / roof["algorithmic_bytes_per_launch"]
+                     if roof.get("algorithmic_bytes_per_launch") else None)
+            if ratio and roof_iso.get("traffic") is not None:
+                for key in ("traffic", "traffic_raw"):
+                    if roof_iso.get(key) is not None:
+                        roof_iso[key] = round(roof_iso[key] * ratio)
+                roof_iso["traffic_note"] = (f"PMC bytes per profiled (overlapped) dispatch x {ratio:.4g}, "
+                                            "the isolated launch's size ratio")
+            valu_iso = pmc_valu(args.workload, roof_iso["kernel"])
+            if ratio and valu_iso and roof_iso.get("avg_launch_ms"):
+                rate = valu_iso["insts_per_launch"] * ratio / (roof_iso["avg_launch_ms"] / 1e3)
+                out["roofline_valu_isolated"] = {
+                    "bound": "valu-issue", "achieved": round(rate / 1e12, 4), "peak": VALU_PEAK_TIPS,
+                    "unit": "T wave-instr/s", "frac": round(rate / 1e12 / VALU_PEAK_TIPS, 4), "kernel": roof_iso["kernel"],
+                    "valu_insts_per_launch": valu_iso["insts_per_launch"] * ratio,
+                    "avg_launch_ms": roof_iso["avg_launch_ms"], "source": valu_iso["source"] + " x launch-size ratio"}
             out["roofline_isolated"] = roof_iso
         if args.workload == "pose" and roof.get("avg_launch_ms"):
             # PoseOptimization is FP64-VALU bound (its edges are read from HBM
