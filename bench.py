@@ -127,6 +127,70 @@ def cpu_baseline_frames(frames, nfeatures, budget_s, bf=False):
                       f"oracle/liborbx_ref.so (g++ -O3), 1 thread, {dt:.1f} s"}
 
 
+def cpu_threads():
+    """Host threads for the all-cores CPU baseline: the box's CPU share
+    (OMP_NUM_THREADS is set to it on the GPU box), else the visible cores."""
+    for key in ("ORBX_CPU_THREADS", "OMP_NUM_THREADS"):
+        if os.environ.get(key, "").isdigit() and int(os.environ[key]) > 0:
+            return min(int(os.environ[key]), 64)
+    return min(os.cpu_count() or 1, 64)
+
+
+def run_threads(n_threads, budget_s, worker):
+    """worker(t, deadline) -> units done; the oracle's C calls release the
+    GIL, so the threads run on separate cores.  Returns (units, seconds)."""
+    import threading
+    counts = [0] * n_threads
+    t0 = time.perf_counter()
+    deadline = t0 + budget_s
+
+    def run(t):
+        counts[t] = worker(t, deadline)
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(n_threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return sum(counts), time.perf_counter() - t0
+
+
+def cpu_all_cores_frames(frames, nfeatures, budget_s, bf=False):
+    """the oracle on every host core, one frame stream per
+    thread (extract + match against that stream's previous frame)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    L = oracle_lib.load()
+    h, w = frames.shape[1:]
+    T = cpu_threads()
+
+    def worker(t, deadline):
+        ex = oracle_lib.RefExtractor(nfeatures)
+        n, prev = 0, None
+        while time.perf_counter() < deadline:
+            k, d = ex(frames[(t + n * T) % len(frames)])
+            if prev is not None:
+                if bf:
+                    bi, b1, b2 = (np.zeros(len(prev[1]), np.int32) for _ in range(3))
+                    L.orbx_ref_hamming_bf(oracle_lib.ptr(prev[1]), len(prev[1]), oracle_lib.ptr(d), len(d),
+                                          oracle_lib.ptr(bi), oracle_lib.ptr(b1), oracle_lib.ptr(b2))
+                else:
+                    F1 = ox.frame_view(prev[0], prev[1], w, h)
+                    F2 = ox.frame_view(k, d, w, h)
+                    pm = np.stack([prev[0]["x"], prev[0]["y"]], 1).astype(np.float32).copy()
+                    m = np.zeros(len(prev[0]), np.int32)
+                    nm = ctypes.c_int()
+                    L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), oracle_lib.ptr(pm),
+                                                         oracle_lib.ptr(m), 100, 0.9, 1, ctypes.byref(nm))
+            prev = (k, d)
+            n += 1
+        return n
+
+    n, dt = run_threads(T, budget_s, worker)
+    return {"value": round(n / dt, 3), "unit": "pairs/s" if bf else "frames/s", "cores": T, "kind": "port",
+            "sample": f"{n} frames ({w}x{h}) on {T} threads, one frame stream each, {dt:.1f} s"}
+
+
 def cpu_baseline_lba(probs, budget_s):
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
@@ -160,6 +224,53 @@ def pose_flops(stats, n_edges):
         f += stats.iterations[r] * 215.0 * active + stats.levenberg_trials[r] * 55.0 * active + 55.0 * n_edges
         active = n_edges - stats.n_bad[r]
     return f
+
+
+def cpu_all_cores_lba(probs, budget_s):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_ba as sb
+    L = oracle_lib.load()
+    L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    T = cpu_threads()
+
+    def worker(t, deadline):
+        n = 0
+        while time.perf_counter() < deadline:
+            p, arrs = sb.to_ctypes(probs[(t + n * T) % len(probs)])
+            es = np.zeros(p.n_edges, np.uint8)
+            pb = np.zeros(p.n_points, np.uint8)
+            L.orbx_ref_lba(ctypes.byref(p), 5, 10, es.ctypes.data, pb.ctypes.data, ctypes.byref(sb.BAStats()))
+            n += 1
+        return n
+
+    n, dt = run_threads(T, budget_s, worker)
+    return {"value": round(n / dt, 4), "unit": "problems/s", "cores": T, "kind": "port",
+            "sample": f"{n} problems on {T} threads, {dt:.1f} s"}
+
+
+def cpu_all_cores_pose(frames, budget_s):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_pose as sp
+    L = oracle_lib.load()
+    L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    structs = [sp.to_ctypes(fr) for fr in frames]
+    T = cpu_threads()
+
+    def worker(t, deadline):
+        n = 0
+        while time.perf_counter() < deadline:
+            p, arrs = structs[(t + n * T) % len(structs)]
+            q = sp.PoseFrame.from_buffer_copy(p)
+            L.orbx_ref_pose_optimization(ctypes.byref(q), None, None)
+            n += 1
+        return n
+
+    n, dt = run_threads(T, budget_s, worker)
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": T, "kind": "port",
+            "sample": f"{n} frames on {T} threads, {dt:.1f} s"}
 
 
 def cpu_baseline_pose(frames, budget_s):
@@ -207,6 +318,7 @@ def run_pose(args, wl, rank, local, world, dist):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_pose(uniq, args.cpu_budget)
+        cpu["all_cores"] = cpu_all_cores_pose(uniq, max(3.0, args.cpu_budget / 2))
     check = {"inliers_frame0": int(n_inl[0]), "edges_frame0": int(frames[0]["has_mp"].sum()),
              "rounds_frame0": int(st[0].rounds), "lm_iterations_frame0": list(st[0].iterations),
              "fp64_flops_per_frame": round(flops)}
@@ -272,6 +384,7 @@ def run_frames(args, wl, rank, local, world, dist):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_frames(frames, nf, args.cpu_budget, bf=bf)
+        cpu["all_cores"] = cpu_all_cores_frames(frames, nf, max(3.0, args.cpu_budget / 2), bf=bf)
     check = {"last_frame_keypoints": int(stats[2]), "last_frame_matches": int(stats[3])}
     cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf, "image": f"{w}x{h}",
            "parallelism": f"dp{world} (one sequence per GPU)"}
@@ -345,6 +458,7 @@ def run_lba(args, wl, rank, local, world, dist):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_lba(probs, args.cpu_budget)
+        cpu["all_cores"] = cpu_all_cores_lba(probs, max(3.0, args.cpu_budget / 2))
     check = {"iterations_problem0": int(stats[2]), "outliers_pass1_problem0": int(stats[3]),
              "edges_per_problem": n_edges, "pcie_inclusive": pcie}
     cfg = {"workload": wl["desc"], "problems_per_step_per_gpu": P, "keyframes": 20, "map_points": 2000,
@@ -502,6 +616,10 @@ def main():
             "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py / synth_pose.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
+        if cpu and "all_cores" in cpu:
+            # the same oracle on every host core of the box
+            # (one independent stream per thread), core count stated
+            out["cpu_baseline_all_cores"] = cpu.pop("all_cores")
         if roof_iso:
             # the PMC summary profiled the overlapped launches; the isolated
             # pass launches each kernel over the whole step, so per-dispatch
