@@ -1438,6 +1438,48 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
     }
 }
 
+// Diagnostics: the LDS introselect replay of k_retain_cells on one list of
+// u32 entries (key << 24 | payload), one wavefront; also the global-memory
+// replay of long lists (out_glb).
+__global__ __launch_bounds__(64) void k_debug_nth(const uint32_t* in, int n, int nth, uint32_t* out_glb,
+                                                  uint32_t* out_lds, int* gpos)
+{
+    __shared__ uint32_t list[kRetainCellCap];
+    __shared__ int pos[kRetainCellCap + 8];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < n; i += 64) out_glb[i] = in[i];
+    global_wave_sync();
+    wave_nth_element<true>(out_glb, n, nth, gpos);
+    for (int i = lane; i < n; i += 64) list[i] = in[i];
+    lds_wave_sync();
+    wave_nth_element(list, n, nth, pos);
+    for (int i = lane; i < n; i += 64) out_lds[i] = list[i];
+}
+
+}  // namespace orbx
+
+extern "C" int orbx_debug_nth(const uint32_t* entries, int n, int nth, uint32_t* out_glb, uint32_t* out_lds)
+{
+    using namespace orbx;
+    if (!entries || !out_glb || !out_lds || n < 0 || n > kRetainCellCap || nth < 0 || nth > n) return ORBX_ERR_ARG;
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, 4 * sizeof(uint32_t) * (n + 8)) != hipSuccess) return ORBX_ERR_NOMEM;
+    int r = ORBX_OK;
+    if (hipMemcpy(d, entries, sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK) {
+        hipLaunchKernelGGL(k_debug_nth, dim3(1), dim3(64), 0, 0, d, n, nth, d + (n + 8), d + 2 * (n + 8),
+                           reinterpret_cast<int*>(d + 3 * (n + 8)));
+        if (hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(out_glb, d + (n + 8), sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(out_lds, d + 2 * (n + 8), sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess)
+            r = ORBX_ERR_HIP;
+    }
+    (void)hipFree(d);
+    return r;
+}
+
+namespace orbx {
+
 // ---------------------------------------------------------------------------
 // Host launcher
 // ---------------------------------------------------------------------------
