@@ -497,7 +497,16 @@ __device__ inline int wave_hoare_partition(E* a, int lo, int hi, int* pos)
         nle += (k <= P);
         nge += (k >= P);
     }
-    const int le_incl = wave_inclusive_scan(nle), ge_incl = wave_inclusive_scan(nge);
+    // both prefix counts in one scan (16-bit halves) when they fit
+    int le_incl, ge_incl;
+    if (len < 65536) {
+        const int both = wave_inclusive_scan(nle | (nge << 16));
+        le_incl = both & 0xFFFF;
+        ge_incl = (int)((uint32_t)both >> 16);
+    } else {
+        le_incl = wave_inclusive_scan(nle);
+        ge_incl = wave_inclusive_scan(nge);
+    }
     const int tot_ge = __builtin_amdgcn_readlane(ge_incl, 63);
     const int le_before = le_incl - nle;
     const int ge_after_chunk = tot_ge - ge_incl;
@@ -527,9 +536,15 @@ __device__ inline int wave_hoare_partition(E* a, int lo, int hi, int* pos)
             cr--;
         }
     }
-    lm1 = wave_min_int(lm1);
-    l1 = wave_min_int(l1);
-    rm = wave_max(rm);
+    // L_{m+1}, L_1 and R_m each lie in exactly one lane's chunk (or none):
+    // read them from that lane instead of reducing over the wave
+    auto from_lane = [](int v, bool have, int none) {
+        const unsigned long long b = __ballot(have);
+        return b ? __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(b)) : none;
+    };
+    lm1 = from_lane(lm1, lm1 != 0x7fffffff, 0x7fffffff);
+    l1 = from_lane(l1, l1 != 0x7fffffff, 0x7fffffff);
+    rm = from_lane(rm, rm >= 0, -1);
     nth_sync<kGlobal>();
     for (int k = lane; k < m; k += 64) {
         const int i = posL[k], j = posR[k];
