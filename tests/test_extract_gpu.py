@@ -305,3 +305,28 @@ def test_random_configs_match_oracle(w, h, nf, scale, nlev, fth, score, kind, se
     rk, rd = kps[:n.value], desc[:n.value]
     assert_kps_equal(gk, rk)
     assert np.array_equal(gd, rd)
+
+
+@pytest.mark.parametrize("w,h,nf,scale,nlev,fth,score,kind,seed", _random_configs(10, seed=77))
+def test_random_configs_batch_pipeline(w, h, nf, scale, nlev, fth, score, kind, seed):
+    """Random configurations through the multi-part batch pipeline (48
+    frames: three parts), spot-checked against the oracle."""
+    B = 48
+    frames = synth.sequence(w, h, B, seed=seed + 500)
+    ref = RefExtractor(nf, scale=scale, nlevels=nlev, fast_th=fth, score_type=score)
+    try:
+        ctx = ox.Context(nfeatures=nf, scale_factor=scale, nlevels=nlev, score_type=score, fast_th=fth,
+                         max_w=w, max_h=h, slots=B)
+    except ox.OrbxError:
+        with pytest.raises(AssertionError):
+            ref(frames[0])
+        return
+    ctx.upload(frames)
+    ctx.extract(0, B)
+    ctx.sync()
+    for s in (0, 17, 47):
+        rk, rd = ref(frames[s])
+        gk, gd = ctx.features(s)
+        assert_kps_equal(gk, rk)
+        assert np.array_equal(gd, rd)
+    ctx.close()
