@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.distributed as tdist
 import torch.multiprocessing as mp
 
@@ -32,8 +33,9 @@ def _worker(rank, world, port, q):
     tdist.destroy_process_group()
 
 
-def test_two_rank_gather_and_job_rate():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_rank_gather_and_job_rate(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -46,10 +48,11 @@ def test_two_rank_gather_and_job_rate():
     for r, w, allst, rate, elapsed, work in res:
         assert w == world
         a = np.array(allst)
-        assert a.shape == (2, 4)
-        assert elapsed == 2.0 and work == 30.0 and rate == 15.0
-        assert a[0, 2] != a[1, 2]          # ranks own different sequences
-    assert res[0][2] == res[1][2]
+        assert a.shape == (world, 4)
+        # value = work of all ranks / the slowest rank's time (rank r: 1 + r s, 10 (r + 1) units)
+        assert elapsed == float(world) and work == 5.0 * world * (world + 1) and rate == 5.0 * (world + 1)
+        assert len(set(a[:, 2])) == world   # ranks own different sequences
+    assert all(res[k][2] == res[0][2] for k in range(world))
 
 
 def test_single_process_path():
