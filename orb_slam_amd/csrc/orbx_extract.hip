@@ -877,13 +877,15 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
     int tot[kPer], ret[kPer];
     bool nomore[kPer];
     int toDist = 0, nNoMore = 0;
+    // slots past the level's cells are skipped (a uniform branch): C2's
+    // levels have <= 30 cells, so one slot of 64 does all the work
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         const int c = lane + 64 * k;
         tot[k] = 0;
         ret[k] = 0;
         nomore[k] = false;
-        if (c < nCells) {
+        if (64 * k < nCells && c < nCells) {
             tot[k] = counts[c];
             if (a.cells[L.cell_base + c].valid) {
                 if (tot[k] > nfc) {
@@ -904,6 +906,7 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
         int td = 0, nm = 0;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
+            if (64 * k >= nCells) break;
             const int c = lane + 64 * k;
             if (c < nCells && !nomore[k]) {
                 if (tot[k] > nNew) {
@@ -922,6 +925,7 @@ __device__ inline void level_quota(const ExtractArgs& a, const LevelGeom& L, con
     int base = 0, my_keep = 0, my_pre = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
+        if (64 * k >= nCells) break;
         const int c = lane + 64 * k;
         const int take = (c < nCells && tot[k] > 0 && ret[k] > 0) ? min(tot[k], ret[k]) : 0;
         const int incl = wave_inclusive_scan(take);
