@@ -93,17 +93,65 @@ def lba_bytes(n_kf, n_pts, n_edges):
     return n_edges * (2 * 8 + 4 + 8) + n_edges * 144 + n_kf * 7 * 8 + n_pts * 3 * 8
 
 
-def cpu_baseline_frames(frames, nfeatures, budget_s, bf=False):
-    """Oracle (C++ restatement, 1 core) on a bounded sample of the workload."""
+def native_oracle():
+    """The timed CPU baseline's library: the oracle built on THIS host with
+    the reference's own flags, -O3 -march=native (CMakeLists.txt:12-13;
+    SURVEY.md 8(d)), by `make -C oracle native`, rebuilt when the host CPU
+    differs from the one it was built for.  Falls back to the portable
+    x86-64-v3 parity build (oracle/liborbx_ref.so) if that fails.
+    Returns (ctypes library, description)."""
+    import hashlib
+    import subprocess
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
-    L = oracle_lib.load()
-    ex = oracle_lib.RefExtractor(nfeatures)
+    try:
+        cpu = Path("/proc/cpuinfo").read_text()
+        sig = hashlib.sha256("".join(l for l in cpu.splitlines(True)[:40]
+                                     if l.startswith(("model name", "flags"))).encode()).hexdigest()[:16]
+    except OSError:
+        sig = "unknown"
+    nat = ROOT / "oracle" / "_native"
+    so = nat / "liborbx_ref_native.so"
+    stamp = nat / "HOST"
+    try:
+        if not so.exists() or not stamp.exists() or stamp.read_text() != sig:
+            if nat.exists():
+                subprocess.run(["rm", "-rf", str(nat)], check=True)
+            subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j16", "native"], check=True,
+                           capture_output=True, timeout=240)
+            stamp.write_text(sig)
+        return oracle_lib.load("native"), "oracle/_native/liborbx_ref_native.so (g++ -O3 -march=native, built on this host)"
+    except Exception as e:   # noqa: BLE001 -- a baseline, not the product: say what was timed
+        return oracle_lib.load(), f"oracle/liborbx_ref.so (g++ -O3 -march=x86-64-v3; native build failed: {e!r:.80})"
+
+
+def percentile_summary(times_s, unit_name):
+    t = np.asarray(times_s)
+    med, p90 = float(np.median(t)), float(np.percentile(t, 90))
+    return {"value": round(1.0 / med, 3), "median_ms": round(1e3 * med, 4), "p90_ms": round(1e3 * p90, 4),
+            "mean_rate": round(len(t) / float(t.sum()), 3), "timed_units": len(t), "rate_from": f"1 / median {unit_name} time"}
+
+
+# SURVEY.md 8(d) protocol: warm-up units, then the median (and p90) of the
+# per-unit times of `timed` units.  C3's 1080p frames take ~65 ms each, so
+# its sample is shorter (stated in the line).
+CPU_PROTOCOL = {"c2": (50, 500), "c3": (10, 150), "c5": (50, 500), "pose": (50, 500)}
+
+
+def cpu_baseline_frames(frames, nfeatures, protocol, bf=False, L=None, lib_desc=""):
+    """Oracle on one host core, per frame: extract + match against the
+    previous frame of the same sequence (the bench's unit)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    if L is None:
+        L, lib_desc = native_oracle()
+    ex = oracle_lib.RefExtractor(nfeatures, lib=L)
     h, w = frames.shape[1:]
-    t0 = time.perf_counter()
-    n = 0
+    warm, timed_n = protocol
+    times = []
     prev = None
-    while time.perf_counter() - t0 < budget_s and n < len(frames) * 4:
+    for n in range(warm + timed_n):
+        t0 = time.perf_counter()
         k, d = ex(frames[n % len(frames)])
         if prev is not None:
             if bf:
@@ -118,13 +166,16 @@ def cpu_baseline_frames(frames, nfeatures, budget_s, bf=False):
                 nm = ctypes.c_int()
                 L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), oracle_lib.ptr(pm),
                                                      oracle_lib.ptr(m), 100, 0.9, 1, ctypes.byref(nm))
+        dt = time.perf_counter() - t0
+        if n >= warm:
+            times.append(dt)
         prev = (k, d)
-        n += 1
-    dt = time.perf_counter() - t0
     what = "brute-force Hamming" if bf else "SearchForInitialization"
-    return {"value": round(n / dt, 3), "unit": "pairs/s" if bf else "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames of the same synthetic sequence ({w}x{h}), extract + {what}, "
-                      f"oracle/liborbx_ref.so (g++ -O3), 1 thread, {dt:.1f} s"}
+    out = {"unit": "pairs/s" if bf else "frames/s", "cores": 1, "kind": "port"}
+    out.update(percentile_summary(times, "frame"))
+    out["sample"] = (f"{warm} warm-up + {timed_n} timed frames of the same synthetic sequence ({w}x{h}), extract + "
+                     f"{what} vs the previous frame, 1 thread; {lib_desc}")
+    return out
 
 
 def cpu_threads():
@@ -155,17 +206,18 @@ def run_threads(n_threads, budget_s, worker):
     return sum(counts), time.perf_counter() - t0
 
 
-def cpu_all_cores_frames(frames, nfeatures, budget_s, bf=False):
+def cpu_all_cores_frames(frames, nfeatures, budget_s, bf=False, L=None, lib_desc=""):
     """the oracle on every host core, one frame stream per
     thread (extract + match against that stream's previous frame)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
-    L = oracle_lib.load()
+    if L is None:
+        L, lib_desc = native_oracle()
     h, w = frames.shape[1:]
     T = cpu_threads()
 
     def worker(t, deadline):
-        ex = oracle_lib.RefExtractor(nfeatures)
+        ex = oracle_lib.RefExtractor(nfeatures, lib=L)
         n, prev = 0, None
         while time.perf_counter() < deadline:
             k, d = ex(frames[(t + n * T) % len(frames)])
@@ -188,29 +240,32 @@ def cpu_all_cores_frames(frames, nfeatures, budget_s, bf=False):
 
     n, dt = run_threads(T, budget_s, worker)
     return {"value": round(n / dt, 3), "unit": "pairs/s" if bf else "frames/s", "cores": T, "kind": "port",
-            "sample": f"{n} frames ({w}x{h}) on {T} threads, one frame stream each, {dt:.1f} s"}
+            "sample": f"{n} frames ({w}x{h}) on {T} threads, one frame stream each, {dt:.1f} s; {lib_desc}"}
 
 
-def cpu_baseline_lba(probs, budget_s):
+def cpu_baseline_lba(probs, protocol, L=None, lib_desc=""):
     sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_lib
     from orb_slam_amd import synth_ba as sb
-    L = oracle_lib.load()
+    if L is None:
+        L, lib_desc = native_oracle()
     L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p]
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < budget_s and n < len(probs):
-        p, arrs = sb.to_ctypes(probs[n])
+    warm, timed_n = protocol
+    times = []
+    for n in range(warm + timed_n):
+        p, arrs = sb.to_ctypes(probs[n % len(probs)])
         es = np.zeros(p.n_edges, np.uint8)
         pb = np.zeros(p.n_points, np.uint8)
         st = sb.BAStats()
+        t0 = time.perf_counter()
         L.orbx_ref_lba(ctypes.byref(p), 5, 10, es.ctypes.data, pb.ctypes.data, ctypes.byref(st))
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "problems/s", "cores": 1, "kind": "port",
-            "sample": f"{n} problems (20 KF x 2000 MP), oracle LBA (dense LLT in place of CHOLMOD), "
-                      f"1 thread, {dt:.1f} s"}
+        if n >= warm:
+            times.append(time.perf_counter() - t0)
+    out = {"unit": "problems/s", "cores": 1, "kind": "port"}
+    out.update(percentile_summary(times, "problem"))
+    out["sample"] = (f"{warm} warm-up + {timed_n} timed problems (20 KF x 2000 MP), oracle LBA (dense LLT in place "
+                     f"of CHOLMOD), 1 thread; {lib_desc}")
+    return out
 
 
 def pose_flops(stats, n_edges):
@@ -226,11 +281,11 @@ def pose_flops(stats, n_edges):
     return f
 
 
-def cpu_all_cores_lba(probs, budget_s):
+def cpu_all_cores_lba(probs, budget_s, L=None, lib_desc=""):
     sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_lib
     from orb_slam_amd import synth_ba as sb
-    L = oracle_lib.load()
+    if L is None:
+        L, lib_desc = native_oracle()
     L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p]
     T = cpu_threads()
@@ -247,14 +302,14 @@ def cpu_all_cores_lba(probs, budget_s):
 
     n, dt = run_threads(T, budget_s, worker)
     return {"value": round(n / dt, 4), "unit": "problems/s", "cores": T, "kind": "port",
-            "sample": f"{n} problems on {T} threads, {dt:.1f} s"}
+            "sample": f"{n} problems on {T} threads, {dt:.1f} s; {lib_desc}"}
 
 
-def cpu_all_cores_pose(frames, budget_s):
+def cpu_all_cores_pose(frames, budget_s, L=None, lib_desc=""):
     sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_lib
     from orb_slam_amd import synth_pose as sp
-    L = oracle_lib.load()
+    if L is None:
+        L, lib_desc = native_oracle()
     L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     structs = [sp.to_ctypes(fr) for fr in frames]
     T = cpu_threads()
@@ -270,27 +325,55 @@ def cpu_all_cores_pose(frames, budget_s):
 
     n, dt = run_threads(T, budget_s, worker)
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": T, "kind": "port",
-            "sample": f"{n} frames on {T} threads, {dt:.1f} s"}
+            "sample": f"{n} frames on {T} threads, {dt:.1f} s; {lib_desc}"}
 
 
-def cpu_baseline_pose(frames, budget_s):
+def cpu_baseline_pose(frames, protocol, L=None, lib_desc=""):
+    sys.path.insert(0, str(ROOT / "tests"))
+    from orb_slam_amd import synth_pose as sp
+    if L is None:
+        L, lib_desc = native_oracle()
+    L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    structs = [sp.to_ctypes(fr) for fr in frames]
+    warm, timed_n = protocol
+    times = []
+    for n in range(warm + timed_n):
+        p, arrs = structs[n % len(structs)]
+        q = sp.PoseFrame.from_buffer_copy(p)          # fresh initial pose each time
+        t0 = time.perf_counter()
+        L.orbx_ref_pose_optimization(ctypes.byref(q), None, None)
+        if n >= warm:
+            times.append(time.perf_counter() - t0)
+    out = {"unit": "frames/s", "cores": 1, "kind": "port"}
+    out.update(percentile_summary(times, "frame"))
+    out["sample"] = (f"{warm} warm-up + {timed_n} timed frames of the same synthetic set, oracle PoseOptimization "
+                     f"(Eigen-LDLT restatement), 1 thread; {lib_desc}")
+    return out
+
+
+def parity_pose(uniq, arr, n_inl, sample=(0, 1, 2, 3, 127, 255)):
+    """The last timed step's Tcw of a few frames against the oracle's
+    PoseOptimization from the same initial pose (1e-5, the north_star pose
+    tolerance; identical inlier counts)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from orb_slam_amd import synth_pose as sp
     L = oracle_lib.load()
     L.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-    structs = [sp.to_ctypes(fr) for fr in frames]
-    t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < budget_s and n < 64 * len(frames):
-        p, arrs = structs[n % len(structs)]
-        q = sp.PoseFrame.from_buffer_copy(p)          # fresh initial pose each time
-        L.orbx_ref_pose_optimization(ctypes.byref(q), None, None)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames of the same synthetic set, oracle PoseOptimization (Eigen-LDLT restatement), "
-                      f"1 thread, {dt:.1f} s"}
+    L.orbx_ref_pose_optimization.restype = ctypes.c_int
+    worst, bad = 0.0, []
+    for i in sample:
+        if i >= len(uniq):
+            continue
+        p, arrs = sp.to_ctypes(uniq[i])
+        ni = ctypes.c_int()
+        r = L.orbx_ref_pose_optimization(ctypes.byref(p), ctypes.byref(ni), None)
+        d = float(np.abs(np.ctypeslib.as_array(arr[i].Tcw) - np.ctypeslib.as_array(p.Tcw)).max())
+        worst = max(worst, d)
+        if r != 0 or d > 1e-5 or ni.value != int(n_inl[i]):
+            bad.append(i)
+    return {"within_1e-5": not bad, "max_abs_tcw_diff": worst, "frames": list(sample), "mismatched": bad,
+            "oracle": "oracle/liborbx_ref.so"}
 
 
 def run_pose(args, wl, rank, local, world, dist):
@@ -309,24 +392,70 @@ def run_pose(args, wl, rank, local, world, dist):
     for _ in range(args.warmup):
         step()
     elapsed, kernels = timed(args, ctx, step, dist, ["pose"])
-    kernels = {"overlapped": kernels, "isolated": None}
+    kernels = {"timed": None, "serial": kernels, "serial_steps": args.steps}   # one launch per step
     arr, n_inl, st = ctx.pose_fetch()
     stats = np.array([elapsed, P * args.steps, int(n_inl[0]), st[0].rounds], dtype=np.float64)
     ab = {"pose": n_edges * 25 + 80 + 160}
     units_per_step = {"pose": P}
     flops = float(np.mean([pose_flops(st[i], int(frames[i]["has_mp"].sum())) for i in range(len(uniq))]))
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_pose(uniq, args.cpu_budget)
-        cpu["all_cores"] = cpu_all_cores_pose(uniq, max(3.0, args.cpu_budget / 2))
     check = {"inliers_frame0": int(n_inl[0]), "edges_frame0": int(frames[0]["has_mp"].sum()),
              "rounds_frame0": int(st[0].rounds), "lm_iterations_frame0": list(st[0].iterations),
              "fp64_flops_per_frame": round(flops)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        check["parity_last_step"] = parity_pose(uniq, arr, n_inl)
+        L, desc = native_oracle()
+        cpu = cpu_baseline_pose(uniq, CPU_PROTOCOL["pose"], L=L, lib_desc=desc)
+        cpu["all_cores"] = cpu_all_cores_pose(uniq, max(3.0, args.cpu_budget / 2), L=L, lib_desc=desc)
     cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": P, "keypoints": 1000, "map_point_edges": n_edges,
            "parallelism": f"dp{world} (independent frames per GPU)",
            "boundary": "frames staged in HBM before the timed region (orbx_pose_stage); results fetched after"}
     ctx.close()
     return stats, kernels, ab, units_per_step, cpu, check, cfg
+
+
+def parity_frames(ctx, frames, first, B, nf, w, h, bf):
+    """Bit-exact check of the last timed step's output against the oracle
+    (run after the timed region, with the CPU baseline): the pipeline's part
+    boundaries and a few interior frames of slot range [first, first + B),
+    keypoints + descriptors and the match vector against the predecessor."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    L = oracle_lib.load()
+    ex = oracle_lib.RefExtractor(nf)
+    ways = 3
+    picks = sorted({min(B - 1, max(0, v)) for i in range(ways) for v in (B * i // ways, B * (i + 1) // ways - 1)}
+                   | {B // 2})
+    ref = {}
+    bad = []
+    for f in picks:
+        for g in ((f - 1) % B, f):
+            if g not in ref:
+                ref[g] = ex(frames[g])
+        rk, rd = ref[f]
+        pk, pd = ref[(f - 1) % B]
+        gk, gd = ctx.features(first + f)
+        gm, gn = ctx.matches(first + f)
+        ok = np.array_equal(gk.view(np.uint8), rk.view(np.uint8)) and np.array_equal(gd, rd)
+        if bf:
+            bi, b1, b2 = (np.zeros(len(pd), np.int32) for _ in range(3))
+            L.orbx_ref_hamming_bf(oracle_lib.ptr(pd), len(pd), oracle_lib.ptr(rd), len(rd), oracle_lib.ptr(bi),
+                                  oracle_lib.ptr(b1), oracle_lib.ptr(b2))
+            want = np.where((b1 <= 50) & (b1.astype(np.float32) < b2.astype(np.float32) * np.float32(0.9)), bi, -1)
+            wn = int((want >= 0).sum())
+        else:
+            F1, F2 = ox.frame_view(pk, pd, w, h), ox.frame_view(rk, rd, w, h)
+            pm = np.stack([pk["x"], pk["y"]], 1).astype(np.float32).copy()
+            want = np.zeros(len(pk), np.int32)
+            nm = ctypes.c_int()
+            L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), oracle_lib.ptr(pm),
+                                                 oracle_lib.ptr(want), 100, 0.9, 1, ctypes.byref(nm))
+            wn = nm.value
+        ok = ok and gn == wn and np.array_equal(gm[:len(pk)], want)
+        if not ok:
+            bad.append(first + f)
+    return {"bit_exact": not bad, "slots": [first + f for f in picks], "mismatched_slots": bad,
+            "oracle": "oracle/liborbx_ref.so", "what": "keypoints, descriptors and matches of the last timed step"}
 
 
 def run_frames(args, wl, rank, local, world, dist):
@@ -338,11 +467,23 @@ def run_frames(args, wl, rank, local, world, dist):
     ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=2 * B, device=local if world > 1 else 0)
     ctx.upload(frames, first=0)
     ctx.upload(frames, first=B)
-    ctx.set_async_match(not args.sync_match)
+    if args.split_ways:
+        ctx.set_split(args.split_ways)
+    if args.pyramid_mode:
+        ctx.set_pyramid_mode(args.pyramid_mode)
+    pipelined = not (args.sync_match or args.serial)
+
+    def configure(serial):
+        ctx.set_split(0 if serial else (args.split_ways or 1))
+        ctx.set_async_match(not serial and pipelined)
+
+    configure(args.serial)
     it = [0]
+    last = [0]
 
     def step():
         first = (it[0] % 2) * B
+        last[0] = first
         it[0] += 1
         if args.sync_match:   # extraction, then matching, in order on the context stream
             ctx.extract(first, B)
@@ -358,38 +499,77 @@ def run_frames(args, wl, rank, local, world, dist):
         step()
     ctx.sync()
     names = ["pyr0", "resize", "fast", "retain", "blur", "describe", "match"]
-    # Serialised pass before the timed region (3 steps, halves and matching
-    # in order, every kernel timed): the per-kernel breakdown, and the
-    # dominant kernel, the only one carrying timing events in the timed region.
-    iso = {}
-    dominant = "fast"
-    if not args.no_isolated:
-        ctx.set_split(False)
-        ctx.set_async_match(False)
-        iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
-        _, iso = timed(iso_args, ctx, step, None, names)
-        ctx.set_split(True)
-        ctx.set_async_match(not args.sync_match)
-        dominant = max(iso, key=lambda k: iso[k]["total_ms"])
-        for _ in range(args.warmup):
-            step()
-        ctx.sync()
-    elapsed, kernels = timed(args, ctx, step, dist, [dominant], only=dominant)
-    kernels = {"overlapped": kernels, "isolated": iso}
+    if args.serial:
+        # diagnostic form (PMC collection of the serialised launches): the
+        # timed steps themselves run one launch per kernel over the batch
+        elapsed, kernels = timed(args, ctx, step, dist, names)
+        kernels = {"timed": None, "serial": kernels, "serial_steps": args.steps}
+    else:
+        # Serialised pass before the timed region (3 steps: one launch per
+        # kernel over the whole batch, matching in order, every kernel timed):
+        # the per-kernel breakdown and the headline roofline; then the
+        # pipelined timed steps carry events on the dominant kernel only.
+        iso = {}
+        dominant = "fast"
+        if not args.no_isolated:
+            configure(True)
+            iso_args = argparse.Namespace(**{**vars(args), "steps": 3, "no_kernel_timing": False})
+            _, iso = timed(iso_args, ctx, step, None, names)
+            configure(False)
+            dominant = max(iso, key=lambda k: iso[k]["total_ms"])
+            for _ in range(args.warmup):
+                step()
+            ctx.sync()
+        elapsed, kernels = timed(args, ctx, step, dist, [dominant], only=dominant)
+        kernels = {"timed": kernels, "serial": iso or None, "serial_steps": 3}
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
     stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
     ab = algorithmic_bytes(w, h, nf, "bf" if bf else "init")
     units_per_step = {k: B for k in ab}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_frames(frames, nf, args.cpu_budget, bf=bf)
-        cpu["all_cores"] = cpu_all_cores_frames(frames, nf, max(3.0, args.cpu_budget / 2), bf=bf)
     check = {"last_frame_keypoints": int(stats[2]), "last_frame_matches": int(stats[3])}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        check["parity_last_step"] = parity_frames(ctx, frames, last[0], B, nf, w, h, bf)
+        L, desc = native_oracle()
+        cpu = cpu_baseline_frames(frames, nf, CPU_PROTOCOL[args.workload], bf=bf, L=L, lib_desc=desc)
+        cpu["all_cores"] = cpu_all_cores_frames(frames, nf, max(3.0, args.cpu_budget / 2), bf=bf, L=L, lib_desc=desc)
     cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf, "image": f"{w}x{h}",
-           "parallelism": f"dp{world} (one sequence per GPU)"}
+           "parallelism": f"dp{world} (one sequence per GPU)",
+           "pipeline": ("serialised (diagnostic --serial)" if args.serial else
+                        "sync matching" if args.sync_match else
+                        f"{args.split_ways or 3}-part extraction pipeline, asynchronous matching")}
     ctx.close()
     return stats, kernels, ab, units_per_step, cpu, check, cfg
+
+
+def parity_lba(uniq, work, es, pb, st, sample=(0, 1, 2, 3)):
+    """The last timed run's fetched results of a few problems against the
+    oracle LBA: poses within 1e-5 (north_star), points 1e-4, identical
+    outlier decisions and LM iteration counts."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_ba as sb
+    L = oracle_lib.load()
+    L.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+    worst, bad = 0.0, []
+    for i in sample:
+        p, arrs = sb.to_ctypes(uniq[i])
+        res = np.zeros(p.n_edges, np.uint8)
+        rpb = np.zeros(p.n_points, np.uint8)
+        rst = sb.BAStats()
+        L.orbx_ref_lba(ctypes.byref(p), 5, 10, res.ctypes.data, rpb.ctypes.data, ctypes.byref(rst))
+        g = work[i][1]
+        d = max(float(np.abs(g["pose_q"] - arrs["pose_q"]).max()), float(np.abs(g["pose_t"] - arrs["pose_t"]).max()))
+        worst = max(worst, d)
+        same = (np.array_equal(es[i], res) and np.array_equal(pb[i], rpb)
+                and list(st[i].iterations) == list(rst.iterations)
+                and float(np.abs(g["points"] - arrs["points"]).max()) <= 1e-4)
+        if d > 1e-5 or not same:
+            bad.append(i)
+    return {"within_1e-5": not bad, "max_abs_pose_diff": worst, "problems": list(sample), "mismatched": bad,
+            "oracle": "oracle/liborbx_ref.so"}
 
 
 def run_lba(args, wl, rank, local, world, dist):
@@ -425,9 +605,13 @@ def run_lba(args, wl, rank, local, world, dist):
     for _ in range(args.warmup):
         step()
     elapsed, kernels = timed(args, ctx, step, dist, ["lba_iter", "lba_outliers"])
-    kernels = {"overlapped": kernels, "isolated": None}
+    kernels = {"timed": None, "serial": kernels, "serial_steps": args.steps}   # one stream, in order
     st = (sb.BAStats * P)()
     check_rc(L.orbx_lba_fetch(ctx.handle, arr, esp, pbp, st), "orbx_lba_fetch")
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline
+    # the last timed run's results against the oracle, before the host-array
+    # leg below reuses these arrays
+    parity = parity_lba(uniq, work, es, pb, st) if cpu_leg else None
     stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
                      dtype=np.float64)
     # the host-array boundary (orbx_lba_solve_batch: packing, H2D upload,
@@ -456,11 +640,13 @@ def run_lba(args, wl, rank, local, world, dist):
     # one pass over all P (2 per step)
     units_per_step = {"lba_iter": P * 15, "lba_outliers": P * 2}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_lba(probs, args.cpu_budget)
-        cpu["all_cores"] = cpu_all_cores_lba(probs, max(3.0, args.cpu_budget / 2))
     check = {"iterations_problem0": int(stats[2]), "outliers_pass1_problem0": int(stats[3]),
              "edges_per_problem": n_edges, "pcie_inclusive": pcie}
+    if cpu_leg:
+        check["parity_last_step"] = parity
+        L, desc = native_oracle()
+        cpu = cpu_baseline_lba(probs, CPU_PROTOCOL["c5"], L=L, lib_desc=desc)
+        cpu["all_cores"] = cpu_all_cores_lba(probs, max(3.0, args.cpu_budget / 2), L=L, lib_desc=desc)
     cfg = {"workload": wl["desc"], "problems_per_step_per_gpu": P, "keyframes": 20, "map_points": 2000,
            "parallelism": f"dp{world} (independent problems per GPU; replicas)",
            "boundary": "problems staged in HBM before the timed region (orbx_lba_stage); results fetched after"}
@@ -475,35 +661,38 @@ KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": "k_pyr_resize", "fast": "k_fa
                  "pose": "k_pose_opt"}
 
 
-def pmc_traffic(workload, name):
-    """HBM bytes per launch of kernel `name` from the newest committed PMC
-    summary of this bench command (profiles/rNN_<workload>_pmc_hbm.json,
-    written by tools/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE
-    passes of `bench.py --no-isolated`).  `traffic` = FETCH_SIZE x2 (gfx950
-    wide-read correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE;
-    `traffic_raw` = FETCH_SIZE + WRITE_SIZE as counted.  The profile names the
-    liborbx.so it measured (SHA-256): when that is not the library loaded now,
-    the numbers describe another build and `traffic` is null."""
+def pmc_summary(key):
+    """Newest committed PMC summary of bench command `key`
+    (profiles/rNN_<key>_pmc_hbm.json, tools/pmc_summary.py: separate
+    FETCH_SIZE / WRITE_SIZE / SQ passes).  key = <workload> for the pipelined
+    bench command, <workload>_serial for `bench.py --serial` (one launch per
+    kernel over the whole batch).  Returns (summary, source) only when the
+    profile names the liborbx.so loaded now (SHA-256), else (None, note)."""
     import hashlib
-    cands = sorted((Path(__file__).resolve().parent / "profiles").glob(f"r*_{workload}_pmc_hbm.json"))
-    sym = KERNEL_SYMBOL.get(name)
-    if not cands or not sym:
-        return {"traffic": None}
-    path = cands[-1]
-    summary = json.loads(path.read_text())
+    cands = sorted((ROOT / "profiles").glob(f"r*_{key}_pmc_hbm.json"))
+    if not cands:
+        return None, None
+    summary = json.loads(cands[-1].read_text())
     meta = summary.pop("_meta", {})
+    if meta.get("liborbx_sha256") != hashlib.sha256(Path(ox.LIB_PATH).read_bytes()).hexdigest():
+        return None, f"profiles/{cands[-1].name}: profile of another liborbx.so build (SHA-256 differs), not reported"
+    return summary, f"profiles/{cands[-1].name} (per dispatch, build {meta.get('git_head')})"
+
+
+def pmc_traffic(key, name):
+    """HBM bytes per launch of kernel `name`: FETCH_SIZE x2 (gfx950 wide-read
+    correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE as `traffic`,
+    FETCH_SIZE + WRITE_SIZE as counted as `traffic_raw`."""
+    summary, src = pmc_summary(key)
+    sym = KERNEL_SYMBOL.get(name)
+    if summary is None or not sym:
+        return {"traffic": None, "traffic_source": src}
     hits = [v for k, v in summary.items() if sym in k]
     if not hits:
-        return {"traffic": None}
-    src = f"profiles/{path.name} (per dispatch)"
-    lib_sha = hashlib.sha256(Path(ox.LIB_PATH).read_bytes()).hexdigest()
-    if meta.get("liborbx_sha256") != lib_sha:
-        return {"traffic": None, "traffic_source": src,
-                "traffic_note": "profile snapshot of another liborbx.so build (SHA-256 differs): not reported"}
+        return {"traffic": None, "traffic_source": src}
     return {"traffic": round(sum(h["hbm_bytes_fetch_x2"] for h in hits) / len(hits)),
             "traffic_raw": round(sum(h["hbm_bytes_raw"] for h in hits) / len(hits)),
-            "traffic_source": src + ", FETCH_SIZE x2 + WRITE_SIZE (traffic_raw: FETCH_SIZE + WRITE_SIZE), "
-                                    f"build {meta.get('git_head')}"}
+            "traffic_source": src + ", FETCH_SIZE x2 + WRITE_SIZE (traffic_raw: FETCH_SIZE + WRITE_SIZE)"}
 
 
 # wave64 VALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per 2
@@ -511,20 +700,16 @@ def pmc_traffic(workload, name):
 VALU_PEAK_TIPS = 256 * 4 * 2.4e9 / 2 / 1e12
 
 
-def pmc_valu(workload, name):
-    """SQ_INSTS_VALU per launch of kernel `name` from the newest committed
-    PMC summary of this bench command, when it profiled the loaded build."""
-    import hashlib
-    cands = sorted((Path(__file__).resolve().parent / "profiles").glob(f"r*_{workload}_pmc_hbm.json"))
+def pmc_valu(key, name):
+    """SQ_INSTS_VALU per launch of kernel `name` from the same summary."""
+    summary, src = pmc_summary(key)
     sym = KERNEL_SYMBOL.get(name)
-    if not cands or not sym:
+    if summary is None or not sym:
         return None
-    summary = json.loads(cands[-1].read_text())
-    meta = summary.pop("_meta", {})
     hits = [v["SQ_INSTS_VALU"] for k, v in summary.items() if sym in k and "SQ_INSTS_VALU" in v]
-    if not hits or meta.get("liborbx_sha256") != hashlib.sha256(Path(ox.LIB_PATH).read_bytes()).hexdigest():
+    if not hits:
         return None
-    return {"insts_per_launch": sum(hits) / len(hits), "source": f"profiles/{cands[-1].name} (SQ_INSTS_VALU per dispatch)"}
+    return {"insts_per_launch": sum(hits) / len(hits), "source": src + " SQ_INSTS_VALU"}
 
 
 def timed(args, ctx, step, dist, names, only=None):
@@ -558,7 +743,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="frames (or BA problems) per step per GPU")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--cpu-budget", type=float, default=12.0,
+                    help="seconds of the all-cores CPU baseline x2 (the 1-core baseline follows CPU_PROTOCOL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-isolated", action="store_true",
@@ -566,6 +752,13 @@ def main():
     ap.add_argument("--sync-match", action="store_true",
                     help="match each batch after its extraction on the same stream (no overlap with the next "
                          "batch's extraction)")
+    ap.add_argument("--serial", action="store_true",
+                    help="diagnostic: time serialised steps (one launch per kernel over the batch, matching in "
+                         "order) -- the form the headline roofline's PMC profile is collected from")
+    ap.add_argument("--split-ways", type=int, default=0, choices=[0, 2, 3, 4],
+                    help="extraction pipeline parts (orbx_dev_set_split; 0 = library default, 3)")
+    ap.add_argument("--pyramid-mode", type=int, default=0, choices=[0, 1],
+                    help="orbx_dev_set_pyramid_mode: 0 staged launches (default), 1 fused pyramid + blur")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()
@@ -586,16 +779,12 @@ def main():
     value, elapsed, _ = odist.job_rate(allst)
 
     if rank == 0:
-        def roofline(kern, steps):
-            roof = roofline_events(kern, steps)
-            roof.update(pmc_traffic(args.workload, roof["kernel"]))
-            return roof
+        frames_wl = args.workload in ("c2", "c3")
 
         def roofline_events(kern, steps):
             # dominant kernel: largest total time; its algorithmic bytes per
             # launch (bytes per unit x units per step / launches per step) over
-            # its mean launch duration (HIP events on the stream the kernel is
-            # launched on)
+            # its mean launch duration (HIP events on the stream it is launched on)
             timed_k = [k for k in kern if kern[k]["launches"]] or list(kern)
             dom = max(timed_k, key=lambda k: kern[k]["total_ms"])
             launches_per_step = max(1, kern[dom]["launches"] // steps)
@@ -606,8 +795,49 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
                     "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": kern[dom]["avg_ms"]}
 
-        roof = roofline(kernels["overlapped"], args.steps)
-        roof_iso = roofline(kernels["isolated"], 3) if kernels["isolated"] else None
+        def valu_roof(key, roof):
+            valu = pmc_valu(key, roof["kernel"])
+            if not valu or not roof.get("avg_launch_ms"):
+                return None
+            rate = valu["insts_per_launch"] / (roof["avg_launch_ms"] / 1e3)
+            return {"bound": "valu-issue", "achieved": round(rate / 1e12, 4), "peak": VALU_PEAK_TIPS,
+                    "unit": "T wave-instr/s", "frac": round(rate / 1e12 / VALU_PEAK_TIPS, 4), "kernel": roof["kernel"],
+                    "valu_insts_per_launch": valu["insts_per_launch"],
+                    "valu_insts_per_frame": (valu["insts_per_launch"] / roof["frames_per_launch"]
+                                             if roof.get("frames_per_launch") else None),
+                    "avg_launch_ms": roof["avg_launch_ms"], "source": valu["source"]}
+
+        roof, occ, roof_valu = None, None, None
+        if kernels["serial"]:
+            # the headline roofline: the dominant kernel launched alone over the
+            # whole batch (the serialised pass; PMC of `bench.py --serial`)
+            serial_key = f"{args.workload}_serial" if frames_wl else args.workload
+            roof = roofline_events(kernels["serial"], kernels["serial_steps"])
+            roof.update(pmc_traffic(serial_key, roof["kernel"]))
+            if frames_wl:
+                roof["frames_per_launch"] = units[roof["kernel"]] // max(
+                    1, kernels["serial"][roof["kernel"]]["launches"] // kernels["serial_steps"])
+                roof["launch"] = "serialised: one launch per kernel over the batch (no other kernel running)"
+            roof_valu = valu_roof(serial_key, roof)
+        if kernels["timed"]:
+            # the same kernel inside the pipelined timed steps: its hipEvent
+            # duration includes CU time shared with the other streams' kernels,
+            # so this measures co-scheduling as much as the kernel
+            occ = roofline_events(kernels["timed"], args.steps)
+            occ.update(pmc_traffic(args.workload, occ["kernel"]))
+            occ["launch"] = "overlapped: one pipeline part, concurrent with the other parts' kernels and matching"
+            occ["launches_per_step"] = kernels["timed"][occ["kernel"]]["launches"] // args.steps
+            if roof is None:
+                roof = occ
+        path = None
+        if frames_wl:
+            # the whole path: algorithmic bytes of every stage per step over the
+            # measured step time
+            per_step = sum(ab[k] * units[k] for k in ab)
+            gbs = per_step / (elapsed / args.steps) / 1e9
+            path = {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_step": per_step,
+                    "note": "all stages' algorithmic bytes (SURVEY.md 8(d)) x frames per step / ms_per_step"}
         out = {
             "metric": wl["metric"], "value": round(value, 2), "unit": wl["unit"], "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -616,33 +846,17 @@ def main():
             "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py / synth_pose.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
+        if occ is not None and occ is not roof:
+            out["occupancy"] = occ
+        if path:
+            out["path_roofline"] = path
+        if roof_valu:
+            out["roofline_valu"] = roof_valu
         if cpu and "all_cores" in cpu:
             # the same oracle on every host core of the box
             # (one independent stream per thread), core count stated
             out["cpu_baseline_all_cores"] = cpu.pop("all_cores")
-        if roof_iso:
-            # the PMC summary profiled the overlapped launches; the isolated
-            # pass launches each kernel over the whole step, so per-dispatch
-            # counts scale with the launch size (bytes and instructions are
-            # proportional to the frames a launch processes)
-            ratio = (roof_iso["algorithmic_bytes_per_launch"] / roof["algorithmic_bytes_per_launch"]
-                     if roof.get("algorithmic_bytes_per_launch") else None)
-            if ratio and roof_iso.get("traffic") is not None:
-                for key in ("traffic", "traffic_raw"):
-                    if roof_iso.get(key) is not None:
-                        roof_iso[key] = round(roof_iso[key] * ratio)
-                roof_iso["traffic_note"] = (f"PMC bytes per profiled (overlapped) dispatch x {ratio:.4g}, "
-                                            "the isolated launch's size ratio")
-            valu_iso = pmc_valu(args.workload, roof_iso["kernel"])
-            if ratio and valu_iso and roof_iso.get("avg_launch_ms"):
-                rate = valu_iso["insts_per_launch"] * ratio / (roof_iso["avg_launch_ms"] / 1e3)
-                out["roofline_valu_isolated"] = {
-                    "bound": "valu-issue", "achieved": round(rate / 1e12, 4), "peak": VALU_PEAK_TIPS,
-                    "unit": "T wave-instr/s", "frac": round(rate / 1e12 / VALU_PEAK_TIPS, 4), "kernel": roof_iso["kernel"],
-                    "valu_insts_per_launch": valu_iso["insts_per_launch"] * ratio,
-                    "avg_launch_ms": roof_iso["avg_launch_ms"], "source": valu_iso["source"] + " x launch-size ratio"}
-            out["roofline_isolated"] = roof_iso
-        if args.workload == "pose" and roof.get("avg_launch_ms"):
+        if args.workload == "pose" and roof and roof.get("avg_launch_ms"):
             # PoseOptimization is FP64-VALU bound (its edges are read from HBM
             # once and kept in LDS): the FP64 roofline is the headline one, the
             # HBM figure is kept beside it
@@ -653,16 +867,6 @@ def main():
                                "traffic": roof.get("traffic"), "kernel": roof["kernel"],
                                "flops_per_frame": check["fp64_flops_per_frame"],
                                "avg_launch_ms": roof["avg_launch_ms"]}
-        valu = pmc_valu(args.workload, roof["kernel"])
-        if valu and roof.get("avg_launch_ms"):
-            # the dominant kernel against its instruction-issue ceiling: wave64
-            # VALU instructions per launch (committed SQ_INSTS_VALU pass of this
-            # build) over the live mean launch duration
-            rate = valu["insts_per_launch"] / (roof["avg_launch_ms"] / 1e3)
-            out["roofline_valu"] = {"bound": "valu-issue", "achieved": round(rate / 1e12, 4), "peak": VALU_PEAK_TIPS,
-                                    "unit": "T wave-instr/s", "frac": round(rate / 1e12 / VALU_PEAK_TIPS, 4),
-                                    "kernel": roof["kernel"], "valu_insts_per_launch": valu["insts_per_launch"],
-                                    "avg_launch_ms": roof["avg_launch_ms"], "source": valu["source"]}
         if args.verbose:
             out["kernels"] = kernels
         print(json.dumps(out), flush=True)

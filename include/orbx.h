@@ -114,9 +114,22 @@ int orbx_dev_upload(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
  * Batches of 32+ frames run as two halves on two internal streams (joined
  * before the call's later work) unless disabled with orbx_dev_set_split. */
 int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
-/* enable: 0 = one stream; 1 = split (default); 2..4 = split, and the
- * asynchronous extract_match pipeline runs its batch in that many parts on
- * as many streams, part i released by part i-1's FAST pass (default 3). */
+/* Floating-point evaluation of the expressions that live in the reference's
+ * own source rather than in OpenCV: computeOrbDescriptor's sample coordinates
+ * x*b + y*a, x*a - y*b (src/ORBextractor.cc:165-167) and HarrisResponses'
+ * response (:117-118).  0 (default): each operation rounded as written (ISO
+ * C++, the reference built with -ffp-contract=off or on a host without FMA).
+ * 1: as GCC evaluates them when it builds the reference with its own flags
+ * (-O3 -march=native, CMakeLists.txt:12-13) on an FMA host, where GCC's
+ * default -ffp-contract=fast fuses them: fma(x, b, y*a), fma(x, a, -(y*b));
+ * fma(-(k*(a+b)), a+b, fma(a, b, -(c*c))).  Applies to extractions launched
+ * after the call (DESIGN.md section 4 has the measured effect). */
+int orbx_set_fp_contract(orbx_ctx* ctx, int enable);
+int orbx_get_fp_contract(const orbx_ctx* ctx);
+/* enable: 0 = one stream; 1 = split with the default three parts;
+ * 2..4 = split, and the asynchronous extract_match pipeline runs its batch
+ * in that many parts on as many streams, part i released by part i-1's
+ * FAST pass. */
 int orbx_dev_set_split(orbx_ctx* ctx, int enable);
 /* orbx_dev_extract followed by matching every slot of the batch against its
  * predecessor (mode 1: orbx_dev_match_prev with window / nnratio / check_ori;

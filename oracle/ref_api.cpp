@@ -116,6 +116,9 @@ double orbx_ref_time_extract(orbx_ref_extractor* r, const uint8_t* imgs, int nim
 // ---- primitives ----
 float orbx_ref_fast_atan2(float y, float x) { return fast_atan2_cv24(y, x); }
 float orbx_ref_cosf(float x) { return cr_cosf(x); }
+/* 1 when this library's reference-compiled float sites (ref_orbsites.cpp)
+ * were built with GCC's FMA contraction (liborbx_ref_contract.so) */
+int orbx_ref_fp_contract(void) { return orbsites_contracted(); }
 float orbx_ref_sinf(float x) { return cr_sinf(x); }
 int orbx_ref_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 

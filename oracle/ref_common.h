@@ -78,7 +78,11 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
 int  cv24_corner_score16(const uint8_t* ptr, const int pixel[25], int threshold);
 void cv24_gaussian_blur7_roi(const PaddedImage& src, PaddedImage& dst);
 void cv24_retain_best(std::vector<KeyPoint>& kps, int n_points);
+// ---- reference-compiled float expressions (ref_orbsites.cpp; built with
+//      and without FMA contraction) ----
 void cv24_harris_responses(const uint8_t* img, int step, std::vector<KeyPoint>& pts, int blockSize, float harris_k);
+void orb_descriptor(const KeyPoint& kpt, const PaddedImage& img, uint8_t* desc);
+int orbsites_contracted();
 
 // ---- matching (ref_match.cpp) ----
 int descriptor_distance(const uint8_t* a, const uint8_t* b);

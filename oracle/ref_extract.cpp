@@ -23,9 +23,6 @@ const int kPatchSize = 31;       // PATCH_SIZE      (src/ORBextractor.cc:75)
 const int kHalfPatch = 15;       // HALF_PATCH_SIZE (:76)
 const int kEdge = 16;            // EDGE_THRESHOLD  (:77)
 
-const int kPattern[256 * 4] = {
-#include "ref_pattern.inc"
-};
 
 // cvRound/cvFloor/cvCeil of OpenCV 2.4 on x86-64 (cvtsd2si under the default
 // round-to-nearest-even MXCSR mode).
@@ -296,36 +293,6 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
     }
 }
 
-// ---------------------------------------------------------------------------
-// HarrisResponses (src/ORBextractor.cc:79-120): 7x7 block of 3x3 Sobel
-// products around each keypoint of the cell image (pt in cell coordinates;
-// the Sobel taps read one pixel past the block, inside the level buffer).
-// Integer sums, then the float response in the source's evaluation order
-// (no contraction: this file is built with -ffp-contract=off).
-void cv24_harris_responses(const uint8_t* img, int step, std::vector<KeyPoint>& pts, int blockSize, float harris_k)
-{
-    const int r = blockSize / 2;
-    float scale = (1 << 2) * blockSize * 255.0f;
-    scale = 1.0f / scale;
-    const float scale_sq_sq = scale * scale * scale * scale;
-    for (KeyPoint& kp : pts) {
-        const int x0 = cvRound(kp.x - r), y0 = cvRound(kp.y - r);
-        const uint8_t* ptr0 = img + (ptrdiff_t)y0 * step + x0;
-        int a = 0, b = 0, c = 0;
-        for (int i = 0; i < blockSize; i++) {
-            for (int j = 0; j < blockSize; j++) {
-                const uint8_t* p = ptr0 + (ptrdiff_t)i * step + j;
-                const int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
-                const int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
-                a += Ix * Ix;
-                b += Iy * Iy;
-                c += Ix * Iy;
-            }
-        }
-        kp.response = ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
-    }
-}
-
 // KeyPointsFilter::retainBest (OpenCV 2.4 features2d/src/keypoint.cpp).
 // Called at src/ORBextractor.cc:683 and :699.  The surviving set and order is
 // the libstdc++ introselect permutation (std::nth_element).
@@ -509,32 +476,6 @@ static float ic_angle(const PaddedImage& image, float px, float py, const std::v
         m_01 += v * v_sum;
     }
     return fast_atan2_cv24((float)m_01, (float)m_10);
-}
-
-// computeOrbDescriptor (src/ORBextractor.cc:154-194)
-static void orb_descriptor(const KeyPoint& kpt, const PaddedImage& img, uint8_t* desc)
-{
-    const float factorPI = (float)(M_PI / 180.f);
-    const float angle = (float)kpt.angle * factorPI;
-    const float a = cr_cosf(angle), b = cr_sinf(angle);
-    const uint8_t* center = img.roi(cvRound(kpt.x), cvRound(kpt.y));
-    const int step = img.step();
-    auto value = [&](const int* pt) {
-        const float x = (float)pt[0], y = (float)pt[1];
-        const float fy = x * b + y * a;
-        const float fx = x * a - y * b;
-        return (int)center[cvRound(fy) * step + cvRound(fx)];
-    };
-    const int* pattern = kPattern;
-    for (int i = 0; i < 32; ++i, pattern += 32) {
-        int val = 0;
-        for (int bit = 0; bit < 8; bit++) {
-            const int t0 = value(pattern + 4 * bit);
-            const int t1 = value(pattern + 4 * bit + 2);
-            val |= (t0 < t1) << bit;
-        }
-        desc[i] = (uint8_t)val;
-    }
 }
 
 // ---------------------------------------------------------------------------

@@ -73,6 +73,8 @@ def _declare(L):
         "orbx_dev_match_bf_prev": ([vp, i, i, i, i, f], i),
         "orbx_dev_set_split": ([vp, i], i),
         "orbx_dev_set_async_match": ([vp, i], i),
+        "orbx_set_fp_contract": ([vp, i], i),
+        "orbx_get_fp_contract": ([vp], i),
         "orbx_dev_set_pyramid_mode": ([vp, i], i),
         "orbx_dev_pyramid_fused": ([vp], i),
         "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
@@ -212,6 +214,12 @@ class Context:
     def set_split(self, enable):
         """Two concurrent half-batch streams for large extraction batches."""
         _check(lib().orbx_dev_set_split(self._h, int(enable)), "orbx_dev_set_split")
+
+    def set_fp_contract(self, enable):
+        """Evaluate src/ORBextractor.cc's own float expressions (descriptor
+        sample coordinates, Harris response) as a reference build with GCC's
+        FMA contraction does (orbx_set_fp_contract)."""
+        _check(lib().orbx_set_fp_contract(self._h, int(enable)), "orbx_set_fp_contract")
 
     def set_async_match(self, enable):
         """Queue extract_match's matching behind the extraction on an internal

@@ -105,6 +105,9 @@ public:
         return v;
     }
     orbx_ctx* context() const { return ctx_.get(); }
+    // Match a reference binary built with FMA contraction (GCC -O3
+    // -march=native on an FMA host; orbx_set_fp_contract).
+    void SetFpContract(bool enable) { check(orbx_set_fp_contract(ctx_.get(), enable ? 1 : 0), "SetFpContract"); }
 
 private:
     int nfeatures_;

@@ -156,7 +156,9 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     ORBX_HIP_CHECK(hipMemcpy(ctx->blur_tiles, tiles.data(), tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
     // The retain kernel keeps per-cell state for up to 256 cells per level.
     if (g.max_cells_per_level > 256) return ORBX_ERR_UNSUPPORTED;
-    if ((r = upload_pyramid_plan(ctx)) != ORBX_OK) return r;
+    // the fused-pyramid plan is optional: planned on first use (pyramid mode 1)
+    ctx->pyr = PyrPlan{};
+    ctx->pyr_planned = false;
     ctx->geom_w = w;
     ctx->geom_h = h;
     return ORBX_OK;
@@ -237,7 +239,6 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     // ORB::HARRIS_SCORE == 0 selects Harris responses; any other value is
     // FAST_SCORE, as in the reference (src/ORBextractor.cc:616)
     ctx->harris = score_type == 0;
-    if (const char* e = getenv("ORBX_PYR_MODE")) ctx->pyr_mode = atoi(e) == 1 ? 1 : 0;   // A/B runs
     init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
     int r = ORBX_OK;
     const int S = max_batch;
@@ -250,7 +251,6 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
         r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxPending; i++)
         if (hipEventCreateWithFlags(&ctx->ev_match[i], hipEventDisableTiming) != hipSuccess) r = ORBX_ERR_HIP;
-    if (const char* e = getenv("ORBX_SPLIT_WAYS")) ctx->split_ways = std::min(std::max(atoi(e), 2), orbx_ctx::kMaxWays);
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays - 2; i++)
         if (hipStreamCreateWithFlags(&ctx->xstreams[i], hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays; i++)
@@ -385,9 +385,20 @@ int orbx_dev_set_split(orbx_ctx* ctx, int enable)
 {
     if (!ctx || enable < 0 || enable > orbx_ctx::kMaxWays) return ORBX_ERR_ARG;
     ctx->split = enable != 0;
-    if (enable >= 2) ctx->split_ways = enable;
+    // 1 restores the documented default of three parts
+    if (enable != 0) ctx->split_ways = enable >= 2 ? enable : orbx_ctx::kDefaultWays;
     return ORBX_OK;
 }
+
+int orbx_set_fp_contract(orbx_ctx* ctx, int enable)
+{
+    if (!ctx || enable < 0 || enable > 1) return ORBX_ERR_ARG;
+    ctx_enter(ctx);   // extractions already queued keep the mode they were launched with
+    ctx->fp_contract = enable;
+    return ORBX_OK;
+}
+
+int orbx_get_fp_contract(const orbx_ctx* ctx) { return ctx ? ctx->fp_contract : ORBX_ERR_ARG; }
 
 int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
 {
@@ -408,7 +419,7 @@ int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode)
 int orbx_dev_pyramid_fused(orbx_ctx* ctx)
 {
     if (!ctx) return ORBX_ERR_ARG;
-    return ctx->pyr.ok && ctx->pyr_mode == 1 ? 1 : 0;
+    return ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx) ? 1 : 0;
 }
 
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)

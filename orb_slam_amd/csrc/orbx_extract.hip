@@ -80,6 +80,7 @@ struct ExtractArgs {
     uint64_t* cell_keys64;          // HARRIS_SCORE: Harris-keyed cell lists (as cell_lists)
     uint64_t* level_keys64;         // HARRIS_SCORE: Harris-keyed level lists (as level_keys)
     int harris;                     // scoreType == HARRIS_SCORE
+    int fp_contract;                // orbx_set_fp_contract: FMA-contracted reference build
     long long frame_pyr_bytes;
     int first_slot;
     int w, h;
@@ -996,7 +997,13 @@ __global__ __launch_bounds__(256) void k_harris_cells(ExtractArgs a)
         }
         const float fa = (float)sa, fb = (float)sb, fc = (float)sc;
         const float s2 = __fadd_rn(fa, fb);
-        const float t = __fsub_rn(__fsub_rn(__fmul_rn(fa, fb), __fmul_rn(fc, fc)), __fmul_rn(__fmul_rn(kHarrisK, s2), s2));
+        // (a*b - c*c) - (k*(a+b))*(a+b), each operation rounded (ISO), or as
+        // GCC contracts it on an FMA host: fma(a, b, -(c*c)), then
+        // fma(-(k*(a+b)), a+b, that) (oracle/ref_orbsites.cpp)
+        const float t = a.fp_contract
+                            ? __fmaf_rn(-__fmul_rn(kHarrisK, s2), s2, __fmaf_rn(fa, fb, -__fmul_rn(fc, fc)))
+                            : __fsub_rn(__fsub_rn(__fmul_rn(fa, fb), __fmul_rn(fc, fc)),
+                                        __fmul_rn(__fmul_rn(kHarrisK, s2), s2));
         const float resp = __fmul_rn(t, kHarrisScale4);
         dst[i] = (uint64_t)harris_key(resp) << 32 | (e & 0xFFFFFFu);
     }
@@ -1266,6 +1273,18 @@ __device__ inline int half_wave_sum(int v)
 // step (fastAtan2, the correctly rounded sin/cos) is shared by two
 // keypoints per instruction, and the pattern's 256 tests map onto 8 rounds
 // of 32 lanes (ballot halves = 32 descriptor bits each).
+// GET_VALUE's sample coordinates (src/ORBextractor.cc:165-167): row
+// x*b + y*a and column x*a - y*b.  kFma: as GCC contracts them on an FMA host
+// (-O3 -march=native, CMakeLists.txt:12-13): fma(x, b, y*a), fma(x, a, -(y*b)).
+template <bool kFma>
+__device__ inline int orb_sample_offset(float px, float py, float sa, float ca)
+{
+    const float fy = kFma ? __fmaf_rn(px, sa, __fmul_rn(py, ca)) : __fadd_rn(__fmul_rn(px, sa), __fmul_rn(py, ca));
+    const float fx = kFma ? __fmaf_rn(px, ca, -__fmul_rn(py, sa)) : __fsub_rn(__fmul_rn(px, ca), __fmul_rn(py, sa));
+    return cv_round(fy) * kBrPitch + cv_round(fx);
+}
+
+template <bool kFma>
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_patch[2 * kWaves][kDescWaveBytes];
@@ -1417,10 +1436,8 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
     for (int r = 0; r < 8; r++) {
         const float px1 = (float)(int8_t)(pat[r] & 0xFF), py1 = (float)(int8_t)((pat[r] >> 8) & 0xFF);
         const float px2 = (float)(int8_t)((pat[r] >> 16) & 0xFF), py2 = (float)(int8_t)(pat[r] >> 24);
-        const int t0 = br[cv_round(__fadd_rn(__fmul_rn(px1, sa), __fmul_rn(py1, ca))) * kBrPitch +
-                          cv_round(__fsub_rn(__fmul_rn(px1, ca), __fmul_rn(py1, sa)))];
-        const int t1 = br[cv_round(__fadd_rn(__fmul_rn(px2, sa), __fmul_rn(py2, ca))) * kBrPitch +
-                          cv_round(__fsub_rn(__fmul_rn(px2, ca), __fmul_rn(py2, sa)))];
+        const int t0 = br[orb_sample_offset<kFma>(px1, py1, sa, ca)];
+        const int t1 = br[orb_sample_offset<kFma>(px2, py2, sa, ca)];
         const unsigned long long bits = __ballot(t0 < t1);
         // this half's 32 bits are descriptor bits 32r .. 32r+31 (bytes 4r .. 4r+3)
         if (valid && hl == r) reinterpret_cast<uint32_t*>(desc)[r] = (uint32_t)(bits >> (32 * half));
@@ -1511,6 +1528,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.error_flags = ctx->error_flags;
     a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
     a.harris = ctx->harris;
+    a.fp_contract = ctx->fp_contract;
     // the level retain holds a whole level list (+ scratch) in one block's LDS
     if ((size_t)((ctx->harris ? 3 : 2) * g.max_level_cap + 8) * 4 > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     a.cell_keys64 = ctx->harris ? ctx->cell_keys64 + (size_t)first * g.list_entries : nullptr;
@@ -1530,7 +1548,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
 
     // The pyramid stages over nb frames on stream st.
     // fused pyramid + blur (orbx_pyramid.hip) when the plan fits this geometry
-    const bool fused = ctx->pyr.ok && ctx->pyr_mode == 1;
+    const bool fused = ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx);
     auto run_pyramid = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         if (fused) {
             timer_begin(ctx, "pyramid", st);
@@ -1634,18 +1652,17 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_end(ctx, "blur", st);
         }
         timer_begin(ctx, "describe", st);
-        hipLaunchKernelGGL(k_describe, dim3((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), xcd_frames(nb)), dim3(256), 0,
-                           st, x, nb);
+        const dim3 dgrid((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), xcd_frames(nb));
+        if (x.fp_contract)
+            hipLaunchKernelGGL(k_describe<true>, dgrid, dim3(256), 0, st, x, nb);
+        else
+            hipLaunchKernelGGL(k_describe<false>, dgrid, dim3(256), 0, st, x, nb);
         timer_end(ctx, "describe", st);
     };
     auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         run_pyramid(x, nb, st);
         run_rest(x, nb, st, 7);
     };
-    // Work buffers are indexed by batch position (frame f of a pass uses
-    // work slot f); the frame store and outputs by slot.  Large batches run
-    // as two halves on two streams so that the VALU-bound FAST pass of one
-    // half overlaps the latency-bound passes of the other.
     // Matching of slot s against prev(s) (the rule of orbx_dev_match_prev),
     // for the slots of [lo, hi) whose predecessor lies in [plo, phi) (all of
     // them when phi < 0), launched as contiguous runs on stream st.
@@ -1671,8 +1688,14 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             s0 = s1;
         }
     };
-    // Work buffers are indexed by batch position (frame f of a pass uses
-    // work slot f); the frame store and outputs by slot.  Large batches run
+    // Every buffer is indexed by slot: the frame store and outputs, and the
+    // work buffers too (a.pyr_raw, cell_lists, retain_scratch, the key lists
+    // are offset by `first`, and by a part's first slot below), so calls on
+    // disjoint slot ranges never share scratch.  Parts launched on stream2 /
+    // xstreams are never joined back to ctx->stream: later calls are ordered
+    // after them only through the pending-match events that ctx_enter and
+    // wait_pending_overlap wait on (the match stream waits for every part).
+    // Large batches run
     // as two halves on two streams so that the VALU-bound FAST pass of one
     // half overlaps the latency-bound passes of the other; each half's
     // internal frame pairs are matched on its own stream, the pairs that

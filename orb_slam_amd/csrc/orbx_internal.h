@@ -163,10 +163,11 @@ struct orbx_ctx {
     // streams[i] (streams[0] = stream, streams[1] = stream2), released by
     // part i - 1's FAST (ev_part_fast), joined by the match (ev_part_done)
     static constexpr int kMaxWays = 4;
-    int split_ways = 3;
+    static constexpr int kDefaultWays = 3;
+    int split_ways = kDefaultWays;
     hipStream_t xstreams[kMaxWays - 2] = {};
     hipEvent_t ev_part_fast[kMaxWays] = {}, ev_part_done[kMaxWays] = {};
-    bool split = true;                  // run large batches as two concurrent halves
+    bool split = true;                  // run large batches as concurrent parts (split_ways, or halves)
     // Asynchronous matching (orbx_dev_set_async_match): the matching of an
     // extract_match call runs on mstream while later calls extract other
     // slots.  pend[] lists the matches queued on mstream, oldest first: the
@@ -199,6 +200,7 @@ struct orbx_ctx {
     uint64_t* cell_keys64 = nullptr;    // slots x list_entries
     uint64_t* level_keys64 = nullptr;   // slots x level_entries
     int harris = 0;
+    int fp_contract = 0;               // orbx_set_fp_contract
     int32_t* level_count = nullptr;
     orbx_keypoint* out_kps = nullptr;
     uint8_t* out_desc = nullptr;
@@ -218,6 +220,7 @@ struct orbx_ctx {
     // fused pyramid + blur plan for the current geometry (orbx_pyramid.hip)
     orbx::PyrPlan pyr;
     int pyr_mode = 0;                  // 0: staged launches, 1: fused when the plan fits
+    bool pyr_planned = false;          // pyr holds the plan of the current geometry
     orbx::PyrLevel* d_pyr_levels = nullptr;
     int32_t* d_pyr_sched = nullptr;
     orbx::PyrWave* d_pyr_waves = nullptr;
@@ -268,6 +271,9 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nul
 // and writes the pyramid buffers at f * frame_pyr_bytes).
 void plan_pyramid(const Geometry& g, int T, PyrPlan& p);
 int upload_pyramid_plan(orbx_ctx* ctx);
+// plan + upload the fused pyramid for the current geometry on first use;
+// true when the fused path can run
+bool ensure_pyramid_plan(orbx_ctx* ctx);
 int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr_blur, int nb, hipStream_t st);
 // timing helpers (orbx_api.cpp)
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);

@@ -1416,11 +1416,15 @@ static int lba_stage_resident(orbx_ctx* ctx, int P, const orbx_ba_problem* probs
     if (!ctx->lba_res) ctx->lba_res = new (std::nothrow) LbaResident();
     if (!ctx->lba_res) return ORBX_ERR_NOMEM;
     LbaResident& R = *ctx->lba_res;
+    // the previous staging is dropped before anything is freed: a stage that
+    // fails part-way leaves no plan pointing into released buffers, and
+    // orbx_lba_run / _fetch refuse the context until a stage succeeds
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    R.plan = LbaPlan{};
     R.solved = false;
     LbaPlan L;
     int r = lba_plan_stage(ctx, P, probs, nullptr, L);
     if (r != ORBX_OK) return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (L.dev_end > R.dev_bytes) {
         if (R.dev) (void)hipFree(R.dev);
         R.dev = nullptr;
@@ -1503,7 +1507,7 @@ int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1)
 int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edge_status, uint8_t* const* point_bad,
                    orbx_ba_stats* stats)
 {
-    if (!ctx || !problems || !ctx->lba_res || !ctx->lba_res->solved) return ORBX_ERR_ARG;
+    if (!ctx || !problems || !ctx->lba_res || !ctx->lba_res->solved || ctx->lba_res->plan.P == 0) return ORBX_ERR_ARG;
     const orbx::LbaPlan& L = ctx->lba_res->plan;
     for (int i = 0; i < L.P; i++)
         if (problems[i].n_poses != L.n_poses[i] || problems[i].n_points != L.n_points[i] ||

@@ -589,11 +589,17 @@ static int ensure_dev(T*& ptr, size_t count)
 
 int upload_pyramid_plan(orbx_ctx* ctx)
 {
+#ifdef ORBX_AB_KNOBS   // experiment builds only: step size and plan dump from the environment
     const char* e = getenv("ORBX_PYR_T");
     const int T = e ? std::max(1, atoi(e)) : 8;
+    const bool verbose = getenv("ORBX_PYR_VERBOSE") != nullptr;
+#else
+    const int T = 8;
+    const bool verbose = false;
+#endif
     plan_pyramid(ctx->geom, T, ctx->pyr);
     const PyrPlan& p = ctx->pyr;
-    if (getenv("ORBX_PYR_VERBOSE")) {   // diagnostics: the plan on stderr
+    if (verbose) {   // diagnostics: the plan on stderr
         fprintf(stderr, "pyramid plan %dx%d: ok=%d T=%d S=%d lds=%d rings:", ctx->geom.w, ctx->geom.h, (int)p.ok, p.T,
                 p.S, p.lds_bytes);
         for (const PyrLevel& q : p.levels) fprintf(stderr, " %d", q.ring);
@@ -614,6 +620,16 @@ int upload_pyramid_plan(orbx_ctx* ctx)
     ORBX_HIP_CHECK(hipMemcpy(ctx->d_pyr_waves, p.waves, sizeof(p.waves), hipMemcpyHostToDevice));
     ORBX_HIP_CHECK(hipMemcpy(ctx->d_pyr_sched, p.sched.data(), p.sched.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     return ORBX_OK;
+}
+
+bool ensure_pyramid_plan(orbx_ctx* ctx)
+{
+    if (!ctx->pyr_planned) {
+        ctx->pyr_planned = true;
+        // a failed upload only disables the optional fused path
+        if (upload_pyramid_plan(ctx) != ORBX_OK) ctx->pyr.ok = false;
+    }
+    return ctx->pyr.ok;
 }
 
 int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr_blur, int nb, hipStream_t st)

@@ -10,7 +10,7 @@ README.md:150), so tests and the benchmark use generated frames:
 * flat_frame    -- constant 128 (FAST finds nothing: threshold-7 fallback and
   the empty-level paths).
 * sequence      -- "TUM-style" camera motion: frame k is a w x h window of a
-  larger texture shifted by (2k mod 40, k mod 20) pixels.
+  larger texture; 300 distinct window offsets per period (sequence_offset).
 """
 import numpy as np
 
@@ -51,11 +51,25 @@ def flat_frame(w, h, value=128):
     return np.full((h, w), value, dtype=np.uint8)
 
 
+SEQ_PERIOD = 300     # a 300-frame sequence at 30 Hz
+
+
+def sequence_offset(k):
+    """Window offset (dx, dy) of frame k: a horizontal pan of +-2 px per frame
+    (a triangle wave over 0..40) while the camera drifts down one pixel every
+    five frames.  The 300 offsets of a period are pairwise distinct (within a
+    run of five frames dy is constant and the triangle values differ), so
+    a 300-frame sequence has no repeated frame; longer runs cycle."""
+    k %= SEQ_PERIOD
+    t = k % 40
+    return (2 * t if t < 20 else 2 * (40 - t)), k // 5
+
+
 def sequence(w, h, n_frames, seed):
     """n_frames x h x w uint8 frames of one synthetic camera sequence."""
-    big = texture_frame(w + 40, h + 20, seed, n_rects=260)
+    big = texture_frame(w + 40, h + SEQ_PERIOD // 5, seed, n_rects=260)
     out = np.empty((n_frames, h, w), dtype=np.uint8)
     for k in range(n_frames):
-        dx, dy = (2 * k) % 40, k % 20
+        dx, dy = sequence_offset(k)
         out[k] = big[dy:dy + h, dx:dx + w]
     return out

@@ -13,23 +13,34 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 ORACLE = ROOT / "oracle"
 SO = ORACLE / "liborbx_ref.so"
+# the same oracle with src/ORBextractor.cc's own float expressions built as
+# GCC builds the reference on an FMA host (oracle/ref_orbsites.cpp)
+SO_CONTRACT = ORACLE / "liborbx_ref_contract.so"
 KEYPOINT = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 
 _lib = None
+_libs = {}
 
 
 def build():
     subprocess.run(["make", "-s", "-C", str(ORACLE), "-j8"], check=True)
 
 
-def load():
+def load(variant="iso"):
+    """The oracle library: variant "iso" (liborbx_ref.so, the parity oracle)
+    or "contract" (liborbx_ref_contract.so)."""
     global _lib
-    if _lib is not None:
+    if variant == "iso" and _lib is not None:
         return _lib
-    if not SO.exists():
+    if variant in _libs:
+        return _libs[variant]
+    path = {"iso": SO, "contract": SO_CONTRACT, "native": ORACLE / "_native" / "liborbx_ref_native.so"}[variant]
+    if not path.exists():
+        if variant == "native":   # built on the timing host by bench.native_oracle()
+            raise FileNotFoundError(path)
         build()
-    L = ctypes.CDLL(str(SO))
+    L = ctypes.CDLL(str(path))
     vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
     ip = ctypes.POINTER(ctypes.c_int)
     sigs = {
@@ -55,12 +66,17 @@ def load():
         "orbx_ref_search_by_projection_motion": ([vp, vp, vp, vp, vp, vp, vp, f, i, vp, ip], i),
         "orbx_ref_search_by_projection_local": ([vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, ip], i),
         "orbx_ref_hamming_bf": ([vp, i, vp, i, vp, vp, vp], i),
+        "orbx_ref_fp_contract": ([], i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = L
+    if variant != "native":   # the native build contracts wherever its host has FMA
+        assert L.orbx_ref_fp_contract() == (variant == "contract")
+    _libs[variant] = L
+    if variant == "iso":
+        _lib = L
     return L
 
 
@@ -69,8 +85,8 @@ def ptr(a):
 
 
 class RefExtractor:
-    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1):
-        self.L = load()
+    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1, variant="iso", lib=None):
+        self.L = lib if lib is not None else load(variant)
         self.h = self.L.orbx_ref_extractor_create(nfeatures, scale, nlevels, score_type, fast_th)
         assert self.h, "oracle rejected the configuration"
         self.nfeatures = nfeatures

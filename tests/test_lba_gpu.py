@@ -190,3 +190,25 @@ def test_lba_random_problems(ctx, seed):
         prob["point_id"] = r.permutation(prob["point_id"])
     i0, i1 = int(r.choice([0, 1, 3, 5])), int(r.choice([0, 2, 10]))
     compare(run_ref(prob, i0, i1), run_gpu(ctx, prob, i0, i1))
+
+
+def test_lba_failed_stage_refuses_run(ctx):
+    """a stage that fails must not leave a plan pointing into
+    released buffers.  Stage a small batch, then a larger one whose last
+    problem has an out-of-range edge: the stage fails, and run / fetch are
+    refused until a later stage succeeds."""
+    L = ox.lib()
+    small = [sb.to_ctypes(sb.make_problem(n_kf=4, n_points=100, seed=60 + k)) for k in range(2)]
+    arr = (sb.BAProblem * 2)(*[c[0] for c in small])
+    assert L.orbx_lba_stage(ctx.handle, 2, arr) == 0
+    assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+    big = [sb.to_ctypes(sb.make_problem(n_kf=12, n_points=900, seed=70 + k)) for k in range(6)]
+    big[-1][1]["edge_point"][7] = big[-1][0].n_points + 3          # invalid edge
+    barr = (sb.BAProblem * 6)(*[c[0] for c in big])
+    assert L.orbx_lba_stage(ctx.handle, 6, barr) == -1
+    assert L.orbx_lba_run(ctx.handle, 5, 10) == -1
+    assert L.orbx_lba_fetch(ctx.handle, arr, None, None, None) == -1
+    big[-1][1]["edge_point"][7] = 0
+    assert L.orbx_lba_stage(ctx.handle, 6, barr) == 0
+    assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+    assert L.orbx_lba_fetch(ctx.handle, barr, None, None, None) == 0
