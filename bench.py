@@ -88,6 +88,14 @@ def algorithmic_bytes(w, h, nfeatures, match="init"):
     }
 
 
+def survey_frame_bytes(w, h, nfeatures):
+    """SURVEY.md 8(d) B_frame: sum_{l>=1}(px_l + px_{l-1}) pyramid write + read,
+    sum_l px_l FAST read, 2 sum_l px_l blur read + write, N_kp (32 + 28)
+    outputs (4.48 MB at 640x480 / 1000 kp)."""
+    px = [a * b for a, b in level_sizes(w, h)]
+    return sum(px[l] + px[l - 1] for l in range(1, len(px))) + 3 * sum(px) + nfeatures * (32 + 28)
+
+
 def lba_bytes(n_kf, n_pts, n_edges):
     """Algorithmic bytes of one LM iteration."""
     return n_edges * (2 * 8 + 4 + 8) + n_edges * 144 + n_kf * 7 * 8 + n_pts * 3 * 8
@@ -833,11 +841,20 @@ def main():
         if frames_wl:
             # the whole path: algorithmic bytes of every stage per step over the
             # measured step time
-            per_step = sum(ab[k] * units[k] for k in ab)
-            gbs = per_step / (elapsed / args.steps) / 1e9
+            step_s = elapsed / args.steps
+            per_frame = survey_frame_bytes(wl["w"], wl["h"], wl["nfeatures"])
+            per_step = per_frame * units["fast"]
+            stage_step = sum(ab[k] * units[k] for k in ab)
+            gbs = per_step / step_s / 1e9
             path = {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_step": per_step,
-                    "note": "all stages' algorithmic bytes (SURVEY.md 8(d)) x frames per step / ms_per_step"}
+                    "frac": round(gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_frame": per_frame,
+                    "algorithmic_bytes_per_step": per_step,
+                    "note": "SURVEY.md 8(d) B_frame (pyramid read + write, FAST read, blur read + write, outputs) x "
+                            "frames per step / ms_per_step",
+                    "with_every_stage_bytes": {"bytes_per_step": stage_step,
+                                               "achieved": round(stage_step / step_s / 1e9, 2),
+                                               "note": "also the level-0 copy and describe's patch reads "
+                                                       "(the per-kernel figures of algorithmic_bytes())"}}
         out = {
             "metric": wl["metric"], "value": round(value, 2), "unit": wl["unit"], "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),

@@ -280,6 +280,48 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F,
                                     const uint8_t* f_assigned, float th, float nnratio,
                                     int32_t* matches_f, int* n_matches);
 
+/* Tracking::SearchReferencePointsInFrustum (src/Tracking.cc:701-752) without a
+ * host pass over the local map: Frame::isInFrustum(pMP, view_cos_limit)
+ * (src/Frame.cc:136-197) for every local map point on the device, then
+ * ORBmatcher(nnratio).SearchByProjection(F, mvpLocalMapPoints, th)
+ * (src/ORBmatcher.cc:49-125) over the points found in view.  The frame's
+ * pose matrices are Frame state (UpdatePoseMatrices, src/Frame.cc:129-134)
+ * and are passed as such.  Outputs per point are what isInFrustum writes into
+ * the MapPoint (mbTrackInView, mTrackProjX/Y, mnTrackScaleLevel,
+ * mTrackViewCos); the caller applies IncreaseVisible() to the points in view
+ * and the matches to mvpMapPoints, as the reference's loops do. */
+typedef struct {
+    const orbx_frame_view* frame;   /* F: mvKeysUn, mDescriptors, bounds, scale pyramid   */
+    const float* Rcw;               /* 9, row-major (Frame::mRcw)                          */
+    const float* tcw;               /* 3 (mtcw)                                            */
+    const float* Ow;                /* 3 (mOw, the camera centre)                          */
+    const float* cam;               /* fx, fy, cx, cy                                      */
+    int n_mp;                       /* local map points                                    */
+    const float* mp_pos;            /* n_mp x 3: GetWorldPos()                             */
+    const float* mp_normal;         /* n_mp x 3: GetNormal()                               */
+    const float* mp_dist;           /* n_mp x 2: GetMinDistanceInvariance(), GetMaxDistanceInvariance() */
+    const uint8_t* mp_skip;         /* n_mp or NULL: 1 = not projected (isBad(), or
+                                       mnLastFrameSeen == this frame: already matched)    */
+    const uint8_t* mp_desc;         /* n_mp x 32: GetDescriptor()                          */
+    const uint8_t* f_assigned;      /* F->n: mvpMapPoints non-null                         */
+    float view_cos_limit;           /* 0.5 (src/Tracking.cc:738)                           */
+    float th;                       /* 1, or 5 just after relocalisation (:745-748)        */
+    float nnratio;                  /* 0.8 (:744)                                          */
+    uint8_t* in_view;               /* out, n_mp or NULL: mbTrackInView                    */
+    float* proj_xy;                 /* out, n_mp x 2 or NULL: mTrackProjX/Y                */
+    int32_t* pred_level;            /* out, n_mp or NULL: mnTrackScaleLevel                */
+    float* view_cos;                /* out, n_mp or NULL: mTrackViewCos                    */
+    int32_t* matches_f;             /* out, F->n: map point assigned to each keypoint, or -1 */
+    int n_in_view;                  /* out: points in view (nToMatch)                      */
+    int n_matches;                  /* out: SearchByProjection's return value              */
+} orbx_local_map_query;
+
+int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q);
+/* B independent frames (each with its own local map) in one upload, two
+ * launches (all frustum tests, then one search wavefront per frame) and one
+ * readback. */
+int orbx_search_local_map_batch(orbx_ctx* ctx, int B, orbx_local_map_query* qs);
+
 /* Vocabulary-node searches.  A keyframe or frame as
  * the BoW matchers read it: keypoints (angle; pt and octave for the
  * epipolar test), descriptors, the map-point state of every keypoint and

@@ -240,6 +240,51 @@ int orbx_ref_search_by_projection_local(const orbx_frame_view* Fv, int n_mp, con
     return ORBX_OK;
 }
 
+// Tracking::SearchReferencePointsInFrustum (src/Tracking.cc:701-752):
+// isInFrustum per local map point, in list order, then the local-map
+// SearchByProjection over the points in view.
+int orbx_ref_search_local_map(orbx_local_map_query* q)
+{
+    if (!q || !q->frame) return ORBX_ERR_ARG;
+    static thread_local FrameRef F;
+    to_frame(q->frame, F);
+    const int n = q->n_mp;
+    std::vector<uint8_t> in(n, 0);
+    std::vector<float> xy(2 * (size_t)n, 0.f), vc(n, 0.f);
+    std::vector<int32_t> lv(n, 0);
+    int n_in = 0;
+    for (int m = 0; m < n; m++) {
+        if (q->mp_skip && q->mp_skip[m]) continue;
+        float u, v, c;
+        int l;
+        if (is_in_frustum(F, q->Rcw, q->tcw, q->Ow, q->cam, q->mp_pos + 3 * m, q->mp_normal + 3 * m,
+                          q->mp_dist[2 * m], q->mp_dist[2 * m + 1], q->view_cos_limit, u, v, l, c)) {
+            in[m] = 1;
+            xy[2 * m] = u;
+            xy[2 * m + 1] = v;
+            lv[m] = l;
+            vc[m] = c;
+            n_in++;
+        }
+    }
+    for (int m = 0; m < n; m++) {
+        if (q->in_view) q->in_view[m] = in[m];
+        if (q->proj_xy) {
+            q->proj_xy[2 * m] = xy[2 * m];
+            q->proj_xy[2 * m + 1] = xy[2 * m + 1];
+        }
+        if (q->pred_level) q->pred_level[m] = lv[m];
+        if (q->view_cos) q->view_cos[m] = vc[m];
+    }
+    q->n_in_view = n_in;
+    std::vector<int> mf;
+    q->n_matches = n_in > 0 ? search_by_projection_local(F, n, in.data(), xy.data(), lv.data(), vc.data(), q->mp_desc,
+                                                         q->f_assigned, q->th, q->nnratio, mf)
+                            : 0;
+    for (int i = 0; i < q->frame->n; i++) q->matches_f[i] = n_in > 0 ? mf[i] : -1;
+    return ORBX_OK;
+}
+
 int orbx_ref_hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
                         int32_t* best, int32_t* second)
 {

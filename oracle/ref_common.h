@@ -120,6 +120,9 @@ int search_by_projection_local(const FrameRef& F, int n_mp, const uint8_t* in_vi
                                const float* view_cos, const uint8_t* mp_desc,
                                const uint8_t* f_assigned, float th, float nnratio,
                                std::vector<int>& matchesF);
+bool is_in_frustum(const FrameRef& F, const float* Rcw, const float* tcw, const float* Ow, const float* cam,
+                   const float* P, const float* Pn, float minDistance, float maxDistance, float viewingCosLimit,
+                   float& u_out, float& v_out, int& level_out, float& cos_out);
 void hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB,
                 int32_t* best_idx, int32_t* best, int32_t* second);
 

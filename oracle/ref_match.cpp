@@ -409,6 +409,42 @@ int search_by_projection_local(const FrameRef& F, int n_mp, const uint8_t* in_vi
     return nmatches;
 }
 
+// Frame::isInFrustum (src/Frame.cc:136-197).  cv::Mat arithmetic as OpenCV
+// 2.4 evaluates it (un-vendored, restated; the same conventions as
+// ref_proj.cpp): Pc = mRcw*P + mtcw through gemm's small-matrix path (float
+// products summed left to right, + t); cv::norm and Mat::dot of float
+// vectors accumulate in double.  Rcw / tcw / Ow are the Frame's own members.
+bool is_in_frustum(const FrameRef& F, const float* Rcw, const float* tcw, const float* Ow, const float* cam,
+                   const float* P, const float* Pn, float minDistance, float maxDistance, float viewingCosLimit,
+                   float& u_out, float& v_out, int& level_out, float& cos_out)
+{
+    float Pc[3];
+    for (int r = 0; r < 3; r++) Pc[r] = Rcw[3 * r] * P[0] + Rcw[3 * r + 1] * P[1] + Rcw[3 * r + 2] * P[2] + tcw[r];
+    if (Pc[2] < 0.0) return false;                                   // :150-151
+    const float invz = (float)(1.0 / Pc[2]);                         // :154
+    const float u = cam[0] * Pc[0] * invz + cam[2];
+    const float v = cam[1] * Pc[1] * invz + cam[3];
+    if (u < F.minX || u > F.maxX) return false;                      // :158-161
+    if (v < F.minY || v > F.maxY) return false;
+    const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};   // :166
+    double s = 0;
+    for (int i = 0; i < 3; i++) s += (double)PO[i] * PO[i];
+    const float dist = (float)std::sqrt(s);                          // cv::norm
+    if (dist < minDistance || dist > maxDistance) return false;       // :169-170
+    double d = 0;
+    for (int i = 0; i < 3; i++) d += (double)PO[i] * Pn[i];           // Mat::dot
+    const float viewCos = (float)(d / dist);                         // :175
+    if (viewCos < viewingCosLimit) return false;
+    const float ratio = dist / minDistance;                          // :181
+    int level = (int)(std::lower_bound(F.scaleFactors.begin(), F.scaleFactors.end(), ratio) - F.scaleFactors.begin());
+    if (level >= (int)F.scaleFactors.size()) level = (int)F.scaleFactors.size() - 1;
+    u_out = u;
+    v_out = v;
+    level_out = level;
+    cos_out = viewCos;
+    return true;
+}
+
 // All-pairs best / second (B8 primitive; rule of src/ORBmatcher.cc:640-649).
 void hamming_bf(const uint8_t* dA, int nA, const uint8_t* dB, int nB,
                 int32_t* best_idx, int32_t* best, int32_t* second)

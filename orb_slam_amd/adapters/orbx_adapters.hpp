@@ -210,6 +210,24 @@ public:
         return n;
     }
 
+    // Tracking::SearchReferencePointsInFrustum (src/Tracking.cc:701-752):
+    // Frame::isInFrustum for every local map point, then the local-map search
+    // above, both on the device (no host pass over the local map).  The
+    // per-point frustum results come back for IncreaseVisible() and the
+    // MapPoint tracking fields; q.frame / q.matches_f are set here.
+    int SearchLocalMap(const FrameData& F, orbx_local_map_query& q, std::vector<int>& matches_f)
+    {
+        const orbx_frame_view v = F.view();
+        matches_f.assign(v.n, -1);
+        q.frame = &v;
+        q.matches_f = matches_f.data();
+        q.nnratio = mfNNratio;
+        check(orbx_search_local_map(ctx_, &q), "Tracking::SearchReferencePointsInFrustum");
+        q.frame = nullptr;
+        q.matches_f = nullptr;
+        return q.n_matches;
+    }
+
     // :1507-1620, motion-model tracking.
     int SearchByProjection(const FrameData& Cur, const FrameData& Last, const float* last_mp_xyz,
                            const uint8_t* last_mp_valid, const uint8_t* cur_assigned, const float* Tcw,

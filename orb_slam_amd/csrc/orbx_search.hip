@@ -8,6 +8,8 @@
 // earliest candidate, as the reference's strict `<` comparisons do.  The
 // second-best of a query is the earliest candidate holding the minimum over
 // all admissible candidates except the best one.
+#include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "orbx_match_common.h"
@@ -175,6 +177,18 @@ struct SearchArgs {
     int check_ori;
     int32_t* out;                 // result array
     int32_t* out_n;
+    // Frame::isInFrustum inputs / outputs (local-map search from raw points)
+    const float* mp_normal;       // n x 3
+    const float* mp_dist;         // n x 2: min, max distance invariance
+    const uint8_t* mp_skip;       // n or null
+    float Rcw[9], tcw[3], Ow[3];
+    float view_cos_limit;
+    int nlevels;
+    uint8_t* fr_in_view;          // n
+    float* fr_proj;               // n x 2
+    int32_t* fr_pred;             // n
+    float* fr_cos;                // n
+    int32_t* fr_count;            // points in view
 };
 
 // ORBmatcher::WindowSearch (src/ORBmatcher.cc:409-516)
@@ -307,9 +321,8 @@ __global__ __launch_bounds__(64) void k_proj_motion(SearchArgs a)
 
 // ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, float)
 // (src/ORBmatcher.cc:49-125) with RadiusByViewingCos (:127-133).
-__global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
+__device__ inline void proj_local_wave(const SearchArgs& a, uint8_t* smem)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CandTab t;
     carve_tab(smem, a.F2.n, t);
     fill_tab(a.F2, a.f2_assigned, t);
@@ -343,6 +356,99 @@ __global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
         }
     }
     if (threadIdx.x == 0) *a.out_n = nmatches;
+}
+
+__global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    proj_local_wave(a, smem);
+}
+
+// Frame::isInFrustum (src/Frame.cc:136-197) for map point m of job a:
+// Pc = mRcw*P + mtcw as OpenCV 2.4's small-matrix gemm evaluates it (float
+// products summed left to right, + t); invz = 1.0/PcZ in double; cv::norm
+// and Mat::dot of the float vectors accumulated in double.  Every float
+// operation rounded on its own (ISO evaluation, -ffp-contract=off).
+__device__ inline void frustum_point(const SearchArgs& a, int m)
+{
+    uint8_t in = 0;
+    float u = 0.f, v = 0.f, vc = 0.f;
+    int pred = 0;
+    if (!(a.mp_skip && a.mp_skip[m])) {
+        const float P[3] = {a.q_xyz[3 * m], a.q_xyz[3 * m + 1], a.q_xyz[3 * m + 2]};
+        float Pc[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            Pc[r] = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(a.Rcw[3 * r], P[0]), __fmul_rn(a.Rcw[3 * r + 1], P[1])),
+                                        __fmul_rn(a.Rcw[3 * r + 2], P[2])),
+                              a.tcw[r]);
+        if (!(Pc[2] < 0.0f)) {
+            const float invz = (float)(1.0 / (double)Pc[2]);
+            u = __fadd_rn(__fmul_rn(__fmul_rn(a.cam[0], Pc[0]), invz), a.cam[2]);
+            v = __fadd_rn(__fmul_rn(__fmul_rn(a.cam[1], Pc[1]), invz), a.cam[3]);
+            if (!(u < a.F2.min_x || u > a.F2.max_x || v < a.F2.min_y || v > a.F2.max_y)) {
+                const float minD = a.mp_dist[2 * m], maxD = a.mp_dist[2 * m + 1];
+                const float PO[3] = {__fsub_rn(P[0], a.Ow[0]), __fsub_rn(P[1], a.Ow[1]), __fsub_rn(P[2], a.Ow[2])};
+                double s2 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 3; i++) s2 = __dadd_rn(s2, __dmul_rn((double)PO[i], (double)PO[i]));
+                const float dist = (float)__dsqrt_rn(s2);
+                if (!(dist < minD || dist > maxD)) {
+                    const float* Pn = a.mp_normal + 3 * m;
+                    double d = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 3; i++) d = __dadd_rn(d, __dmul_rn((double)PO[i], (double)Pn[i]));
+                    vc = (float)__ddiv_rn(d, (double)dist);
+                    if (!(vc < a.view_cos_limit)) {
+                        const float ratio = __fdiv_rn(dist, minD);
+                        // lower_bound(mvScaleFactors, ratio), clamped to the last level
+                        pred = 0;
+                        while (pred < a.nlevels && a.scale[pred] < ratio) pred++;
+                        if (pred >= a.nlevels) pred = a.nlevels - 1;
+                        in = 1;
+                    }
+                }
+            }
+        }
+    }
+    a.fr_in_view[m] = in;
+    if (in) {
+        a.fr_proj[2 * m] = u;
+        a.fr_proj[2 * m + 1] = v;
+        a.fr_pred[m] = pred;
+        a.fr_cos[m] = vc;
+    } else {
+        a.fr_proj[2 * m] = 0.f;
+        a.fr_proj[2 * m + 1] = 0.f;
+        a.fr_pred[m] = 0;
+        a.fr_cos[m] = 0.f;
+    }
+    const unsigned long long b = __ballot(in);
+    if (__lane_id() == 0 && b) atomicAdd(a.fr_count, (int)__popcll(b));
+}
+
+// One thread per local map point; grid.y = job (independent frames).
+__global__ __launch_bounds__(256) void k_frustum(const SearchArgs* jobs)
+{
+    const SearchArgs& a = jobs[blockIdx.y];
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    // a wave's lane 0 holds its smallest index, so lane 0 is active
+    // whenever any lane is (the in-view count is added by lane 0)
+    if (m < a.nq) frustum_point(a, m);
+}
+
+// SearchByProjection(F, local map) per job after k_frustum: one wavefront per
+// frame, skipped when no point is in view (`if(nToMatch>0)`,
+// src/Tracking.cc:742).
+__global__ __launch_bounds__(64) void k_proj_local_jobs(const SearchArgs* jobs)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const SearchArgs& a = jobs[blockIdx.x];
+    if (*a.fr_count == 0) {
+        if (threadIdx.x == 0) *a.out_n = 0;
+        return;
+    }
+    proj_local_wave(a, smem);
 }
 
 // SearchForInitialization with host inputs (prev_xy in/out).
@@ -683,6 +789,141 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     return ORBX_OK;
 }
 
+// Tracking::SearchReferencePointsInFrustum for B frames: one packed upload
+// (pinned staging), k_frustum over every job's points, k_proj_local_jobs one
+// wavefront per frame, one packed readback.
+static int search_local_map_impl(orbx_ctx* ctx, int B, orbx_local_map_query* qs)
+{
+    if (!ctx || B <= 0 || !qs) return ORBX_ERR_ARG;
+    int max_n = 1, max_mp = 0;
+    for (int b = 0; b < B; b++) {
+        const orbx_local_map_query& q = qs[b];
+        const orbx_frame_view* F = q.frame;
+        if (!valid_view(F) || q.n_mp < 0 || !q.Rcw || !q.tcw || !q.Ow || !q.cam || !q.f_assigned || !q.matches_f ||
+            (q.n_mp > 0 && (!q.mp_pos || !q.mp_normal || !q.mp_dist || !q.mp_desc)))
+            return ORBX_ERR_ARG;
+        max_n = std::max(max_n, F->n);
+        max_mp = std::max(max_mp, q.n_mp);
+    }
+    ctx_enter(ctx);
+    // layout: [inputs of every job | SearchArgs[B] | outputs of every job]
+    struct Offs {
+        FrameOffs f;
+        size_t assigned, pos, normal, dist, skip, desc;        // inputs
+        size_t in_view, proj, pred, cos, out, out_n, count;    // outputs
+    };
+    std::vector<Offs> o(B);
+    Uploader u{ctx};
+    for (int b = 0; b < B; b++) {
+        const orbx_local_map_query& q = qs[b];
+        const size_t n = q.frame->n, m = q.n_mp;
+        o[b].f = reserve_frame(u, q.frame);
+        o[b].assigned = u.reserve(n);
+        o[b].pos = u.reserve(m * 12);
+        o[b].normal = u.reserve(m * 12);
+        o[b].dist = u.reserve(m * 8);
+        o[b].skip = u.reserve(m);
+        o[b].desc = u.reserve(m * 32);
+    }
+    const size_t o_jobs = u.reserve((size_t)B * sizeof(SearchArgs));
+    const size_t o_outputs = u.total;
+    for (int b = 0; b < B; b++) {
+        const orbx_local_map_query& q = qs[b];
+        const size_t n = q.frame->n, m = q.n_mp;
+        o[b].out = u.reserve(n * 4);
+        o[b].out_n = u.reserve(4);
+        o[b].count = u.reserve(4);
+        o[b].in_view = u.reserve(m);
+        o[b].proj = u.reserve(m * 8);
+        o[b].pred = u.reserve(m * 4);
+        o[b].cos = u.reserve(m * 4);
+    }
+    int r = ensure_scratch(ctx, u.total);
+    if (r == ORBX_OK) r = ensure_pinned(ctx, u.total);
+    if (r != ORBX_OK) return r;
+    uint8_t* h = static_cast<uint8_t*>(ctx->host_pinned);
+    uint8_t* d = u.base();
+    auto cp = [&](size_t off, const void* src, size_t bytes) {
+        if (bytes && src) std::memcpy(h + off, src, bytes);
+    };
+    std::vector<SearchArgs> jobs(B);
+    for (int b = 0; b < B; b++) {
+        const orbx_local_map_query& q = qs[b];
+        const orbx_frame_view* F = q.frame;
+        const size_t n = F->n, m = q.n_mp;
+        cp(o[b].f.kp, F->keys_un, n * sizeof(orbx_keypoint));
+        cp(o[b].f.desc, F->desc, n * 32);
+        cp(o[b].assigned, q.f_assigned, n);
+        cp(o[b].pos, q.mp_pos, m * 12);
+        cp(o[b].normal, q.mp_normal, m * 12);
+        cp(o[b].dist, q.mp_dist, m * 8);
+        if (q.mp_skip) cp(o[b].skip, q.mp_skip, m);
+        else if (m) std::memset(h + o[b].skip, 0, m);
+        cp(o[b].desc, q.mp_desc, m * 32);
+        std::memset(h + o[b].out, 0xFF, n * 4);   // matches_f: -1 unless assigned here
+        std::memset(h + o[b].out_n, 0, 8);        // out_n, count
+        SearchArgs& a = jobs[b];
+        a = SearchArgs{};
+        a.F2 = dev_frame(F, d, o[b].f.kp, o[b].f.desc);
+        a.nq = q.n_mp;
+        a.q_xyz = reinterpret_cast<const float*>(d + o[b].pos);
+        a.mp_normal = reinterpret_cast<const float*>(d + o[b].normal);
+        a.mp_dist = reinterpret_cast<const float*>(d + o[b].dist);
+        a.mp_skip = d + o[b].skip;
+        a.q_desc = d + o[b].desc;
+        a.f2_assigned = d + o[b].assigned;
+        for (int i = 0; i < 9; i++) a.Rcw[i] = q.Rcw[i];
+        for (int i = 0; i < 3; i++) {
+            a.tcw[i] = q.tcw[i];
+            a.Ow[i] = q.Ow[i];
+        }
+        for (int i = 0; i < 4; i++) a.cam[i] = q.cam[i];
+        frame_scales(F, a.scale);
+        a.nlevels = F->nlevels;
+        a.view_cos_limit = q.view_cos_limit;
+        a.th = q.th;
+        a.nnratio = q.nnratio;
+        a.fr_in_view = d + o[b].in_view;
+        a.fr_proj = reinterpret_cast<float*>(d + o[b].proj);
+        a.fr_pred = reinterpret_cast<int32_t*>(d + o[b].pred);
+        a.fr_cos = reinterpret_cast<float*>(d + o[b].cos);
+        a.fr_count = reinterpret_cast<int32_t*>(d + o[b].count);
+        // the search reads the frustum results as its per-point inputs
+        a.q_valid = a.fr_in_view;
+        a.proj_xy = a.fr_proj;
+        a.pred_level = a.fr_pred;
+        a.view_cos = a.fr_cos;
+        a.out = reinterpret_cast<int32_t*>(d + o[b].out);
+        a.out_n = reinterpret_cast<int32_t*>(d + o[b].out_n);
+    }
+    cp(o_jobs, jobs.data(), (size_t)B * sizeof(SearchArgs));
+    // inputs and the job table in one copy, then each job's -1 match vector
+    // and zero counters (contiguous per job)
+    ORBX_HIP_CHECK(hipMemcpyAsync(d, h, o_outputs, hipMemcpyHostToDevice, ctx->stream));
+    for (int b = 0; b < B; b++)
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + o[b].out, h + o[b].out, o[b].count + 4 - o[b].out, hipMemcpyHostToDevice,
+                                      ctx->stream));
+    const SearchArgs* dj = reinterpret_cast<const SearchArgs*>(d + o_jobs);
+    if (max_mp > 0)
+        hipLaunchKernelGGL(k_frustum, dim3((max_mp + 255) / 256, B), dim3(256), 0, ctx->stream, dj);
+    hipLaunchKernelGGL(k_proj_local_jobs, dim3(B), dim3(64), tab_lds(max_n), ctx->stream, dj);
+    ORBX_HIP_CHECK(hipGetLastError());
+    ORBX_HIP_CHECK(hipMemcpyAsync(h + o_outputs, d + o_outputs, u.total - o_outputs, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int b = 0; b < B; b++) {
+        orbx_local_map_query& q = qs[b];
+        const size_t n = q.frame->n, m = q.n_mp;
+        std::memcpy(q.matches_f, h + o[b].out, n * 4);
+        std::memcpy(&q.n_matches, h + o[b].out_n, 4);
+        std::memcpy(&q.n_in_view, h + o[b].count, 4);
+        if (q.in_view) std::memcpy(q.in_view, h + o[b].in_view, m);
+        if (q.proj_xy) std::memcpy(q.proj_xy, h + o[b].proj, m * 8);
+        if (q.pred_level) std::memcpy(q.pred_level, h + o[b].pred, m * 4);
+        if (q.view_cos) std::memcpy(q.view_cos, h + o[b].cos, m * 4);
+    }
+    return ORBX_OK;
+}
+
 static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
                            int32_t* best, int32_t* second, int32_t* m12, int th_low, float nnratio)
 {
@@ -707,6 +948,16 @@ static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8
         return r;
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return ORBX_OK;
+}
+
+int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q)
+{
+    return search_local_map_impl(ctx, 1, q);
+}
+
+int orbx_search_local_map_batch(orbx_ctx* ctx, int B, orbx_local_map_query* qs)
+{
+    return search_local_map_impl(ctx, B, qs);
 }
 
 int orbx_hamming_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, int nB, int32_t* best_idx,
