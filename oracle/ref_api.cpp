@@ -13,6 +13,13 @@
 
 using namespace orbref;
 
+// memcpy that accepts the empty vectors' null data() (n == 0), which
+// std::memcpy does not (UBSan: nonnull arguments)
+static inline void copy_bytes(void* dst, const void* src, size_t n)
+{
+    if (n) std::memcpy(dst, src, n);
+}
+
 extern "C" {
 
 struct orbx_ref_extractor {
@@ -43,8 +50,8 @@ int orbx_ref_extract(orbx_ref_extractor* r, const uint8_t* img, int w, int h, si
         }
         *n_out = (int)k.size();
         if ((int)k.size() > cap) return ORBX_ERR_CAPACITY;
-        std::memcpy(kps, k.data(), k.size() * sizeof(KeyPoint));
-        std::memcpy(desc, d.data(), d.size());
+        copy_bytes(kps, k.data(), k.size() * sizeof(KeyPoint));
+        copy_bytes(desc, d.data(), d.size());
         return ORBX_OK;
     } catch (const std::exception&) {
         return ORBX_ERR_UNSUPPORTED;
@@ -61,7 +68,7 @@ int orbx_ref_level(orbx_ref_extractor* r, int level, int blurred, uint8_t* out, 
     *pw = L.pw;
     *ph = L.ph;
     if ((int)L.buf.size() > cap) return ORBX_ERR_CAPACITY;
-    std::memcpy(out, L.buf.data(), L.buf.size());
+    copy_bytes(out, L.buf.data(), L.buf.size());
     return ORBX_OK;
 }
 
@@ -72,7 +79,7 @@ int orbx_ref_level_keys(orbx_ref_extractor* r, int level, orbx_keypoint* out, in
     const auto& v = r->ex->levelKeys[level];
     *n = (int)v.size();
     if ((int)v.size() > cap) return ORBX_ERR_CAPACITY;
-    std::memcpy(out, v.data(), v.size() * sizeof(KeyPoint));
+    copy_bytes(out, v.data(), v.size() * sizeof(KeyPoint));
     return ORBX_OK;
 }
 
@@ -129,7 +136,7 @@ int orbx_ref_fast_cell(const uint8_t* img, int step, int rows, int cols, int thr
     cv24_fast16(img, step, rows, cols, threshold, true, k);
     *n = (int)k.size();
     if ((int)k.size() > cap) return ORBX_ERR_CAPACITY;
-    std::memcpy(out, k.data(), k.size() * sizeof(KeyPoint));
+    copy_bytes(out, k.data(), k.size() * sizeof(KeyPoint));
     return ORBX_OK;
 }
 
@@ -176,7 +183,7 @@ int orbx_ref_search_for_initialization(const orbx_frame_view* F1v, const orbx_fr
     std::vector<float> pm(prev_matched, prev_matched + 2 * F1v->n);
     std::vector<int> m;
     *n_matches = search_for_initialization(F1, F2, pm, m, window, nnratio, check_ori != 0);
-    std::memcpy(prev_matched, pm.data(), pm.size() * sizeof(float));
+    copy_bytes(prev_matched, pm.data(), pm.size() * sizeof(float));
     for (int i = 0; i < F1v->n; i++) matches12[i] = m[i];
     return ORBX_OK;
 }
@@ -331,9 +338,9 @@ extern "C" int orbx_ref_lba(orbx_ba_problem* p, int iters0, int iters1, uint8_t*
         p->pose_q[4 * i + 3] = in.poses[i].q.w;
         for (int k = 0; k < 3; k++) p->pose_t[3 * i + k] = in.poses[i].t[k];
     }
-    std::memcpy(p->points, in.points.data(), in.points.size() * sizeof(double));
-    std::memcpy(edge_status, es.data(), es.size());
-    std::memcpy(point_bad, pb.data(), pb.size());
+    copy_bytes(p->points, in.points.data(), in.points.size() * sizeof(double));
+    copy_bytes(edge_status, es.data(), es.size());
+    copy_bytes(point_bad, pb.data(), pb.size());
     if (stats) {
         for (int k = 0; k < 2; k++) {
             stats->iterations[k] = st.iterations[k];

@@ -41,13 +41,33 @@ def _needs(obj, src, headers):
     return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
 
 
-def build(verbose=False, jobs=None, defines=(), lib=None):
+ASAN_DIR = PKG / "build_asan"
+ASAN_LIB = ASAN_DIR / "liborbx_asan.so"
+
+
+def asan_runtime():
+    """clang's AddressSanitizer runtime (preloaded to run the ASan build)."""
+    hits = sorted(Path("/opt/rocm/lib/llvm/lib/clang").glob("*/lib/linux/libclang_rt.asan-x86_64.so"))
+    if not hits:
+        raise RuntimeError("libclang_rt.asan-x86_64.so not found under /opt/rocm/lib/llvm")
+    return hits[-1]
+
+
+def build(verbose=False, jobs=None, defines=(), lib=None, sanitize=False):
     """defines: extra -D flags for an instrumented variant (e.g.
     ORBX_MATCH_PROFILE); such a variant is linked to `lib` with its own
-    object directory and loaded through ORBX_LIBRARY."""
+    object directory and loaded through ORBX_LIBRARY.
+    sanitize: the host-code AddressSanitizer build:
+    host code of every file instrumented, device code untouched (-Xarch_host),
+    linked to build_asan/liborbx_asan.so; run it with the runtime of
+    asan_runtime() preloaded (tests/test_sanitizers.py).  GPU-side ASan is
+    not used."""
     cc = hipcc()
-    obj_dir = OBJ if not defines else OBJ.parent / ("build_" + "_".join(d.lower() for d in defines))
-    out = Path(lib) if lib else LIB
+    if sanitize:
+        obj_dir, out = ASAN_DIR, ASAN_LIB
+    else:
+        obj_dir = OBJ if not defines else OBJ.parent / ("build_" + "_".join(d.lower() for d in defines))
+        out = Path(lib) if lib else LIB
     obj_dir.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) + [PKG.parent / "include" / "orbx.h"]
     srcs = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
@@ -58,7 +78,11 @@ def build(verbose=False, jobs=None, defines=(), lib=None):
         objs.append(o)
         if _needs(o, s, headers):
             lang = ["-x", "hip", f"--offload-arch={ARCH}"] if s.suffix == ".hip" else ["-D__HIP_PLATFORM_AMD__"]
-            cmds.append([cc, *lang, *COMMON, *(f"-D{d}" for d in defines), "-c", str(s), "-o", str(o)])
+            san = []
+            if sanitize:
+                san = (["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+                       if s.suffix == ".hip" else ["-fsanitize=address", "-fno-omit-frame-pointer", "-g"])
+            cmds.append([cc, *lang, *COMMON, *san, *(f"-D{d}" for d in defines), "-c", str(s), "-o", str(o)])
 
     def run(cmd):
         if verbose:
@@ -75,7 +99,7 @@ def build(verbose=False, jobs=None, defines=(), lib=None):
     if cmds or not out.exists():
         link = [cc, f"--offload-arch={ARCH}", "-shared", "-pthread", "-o", str(out), *map(str, objs)]
         run(link)
-    if defines:
+    if defines or sanitize:
         return out
     # C++ adapter demo (the reference-style C++ binding)
     demo_src = PKG / "adapters" / "adapter_demo.cpp"
@@ -90,4 +114,4 @@ def build(verbose=False, jobs=None, defines=(), lib=None):
 if __name__ == "__main__":
     defs = [a[2:] for a in sys.argv[1:] if a.startswith("-D")]
     outs = [a[6:] for a in sys.argv[1:] if a.startswith("--out=")]
-    print(build(verbose="-v" in sys.argv, defines=defs, lib=outs[0] if outs else None))
+    print(build(verbose="-v" in sys.argv, defines=defs, lib=outs[0] if outs else None, sanitize="--asan" in sys.argv))

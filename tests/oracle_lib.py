@@ -5,6 +5,7 @@ thing measured or shipped.  Built from oracle/ with make when missing (the
 prebuilt .so travels to GPU boxes with the snapshot).
 """
 import ctypes
+import os
 import subprocess
 from pathlib import Path
 
@@ -36,6 +37,8 @@ def load(variant="iso"):
     if variant in _libs:
         return _libs[variant]
     path = {"iso": SO, "contract": SO_CONTRACT, "native": ORACLE / "_native" / "liborbx_ref_native.so"}[variant]
+    if variant == "iso" and os.environ.get("ORBX_REF_LIBRARY"):   # e.g. the ASan build (test_sanitizers.py)
+        path = Path(os.environ["ORBX_REF_LIBRARY"])
     if not path.exists():
         if variant == "native":   # built on the timing host by bench.native_oracle()
             raise FileNotFoundError(path)

@@ -5,15 +5,21 @@ The reference ships no tests or fixtures for this path (SURVEY.md section
 from the reference's own source and its dependencies' published semantics:
 
 * fastAtan2 exact quadrant values and its documented ~0.3 deg accuracy
-  (OpenCV 2.4 mathfuncs.cpp, used by IC_Angle src/ORBextractor.cc:77);
-* DescriptorDistance popcount identity (src/ORBmatcher.cc:1364-1382);
+  (OpenCV 2.4 mathfuncs.cpp; IC_Angle src/ORBextractor.cc:124-151 returns
+  fastAtan2 at :150);
+* DescriptorDistance popcount identity (src/ORBmatcher.cc:1794-1810);
 * a hand-built FAST-9 patch whose score is known in closed form
-  (cv::FAST with nonmax suppression, src/ORBextractor.cc:623);
-* umax, features per level, level sizes (src/ORBextractor.cc:424-487);
-* retainBest keeps exactly the top-n responses (src/ORBextractor.cc:599);
+  (cv::FAST with nonmax suppression, called per cell at
+  src/ORBextractor.cc:607 and, for <= 3 corners, :613);
+* cosf / sinf of the descriptor angle (computeOrbDescriptor,
+  src/ORBextractor.cc:159-160) against correctly rounded values;
+* umax, features per level, level sizes (src/ORBextractor.cc:457-511:
+  scale factors :462-471, quotas :476-487, umax :495-510);
+* retainBest keeps exactly the top-n responses (src/ORBextractor.cc:683-685,
+  :697-701);
 * SE3 exponential against scipy's matrix exponential, and the analytic
   EdgeSE3ProjectXYZ Jacobians against central finite differences
-  (Thirdparty/g2o/g2o/types/types_six_dof_expmap.cpp:170-207);
+  (Thirdparty/g2o/g2o/types/sba/types_six_dof_expmap.cpp:384-420);
 * a noise-free local BA recovers the ground truth (src/Optimizer.cc:449-535).
 
 The product's own host tables (orbx_describe_levels) are checked against
@@ -52,7 +58,7 @@ def test_fast_atan2_accuracy(ref):
 
 
 def test_sincos_is_correctly_rounded_float(ref):
-    """IC_Angle's cos/sin (src/ORBextractor.cc:113) are evaluated as the
+    """computeOrbDescriptor's cos/sin (src/ORBextractor.cc:159-160) are evaluated as the
     correctly rounded float of the true value (see oracle/ref_math.cpp)."""
     r = np.random.default_rng(1)
     for a in r.uniform(0, 2 * np.pi, 3000).astype(np.float32):
