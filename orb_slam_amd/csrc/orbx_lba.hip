@@ -12,11 +12,17 @@
 //             thread in edge order
 //   trial     Schur point by point (a point's edges are contiguous): Dinv,
 //             db, then bs -= W_i db and S(i,j) -= W_i Dinv W_j^T for every
-//             pair of its edges, FP64 atomics into the reduced camera system
-//             held in LDS (summation order differs from g2o's only by
-//             rounding); dense LLT; one-wave triangular solves;
-//             back-substitution for the points; exp-map update; accept /
-//             reject with g2o's rho rule
+//             pair of its edges.  The W_i = Hpl blocks are rebuilt from the
+//             edge's inputs (pose, point, observation) where they are used
+//             instead of being stored per edge and re-read from HBM.  The
+//             reduced camera system is accumulated in 2^-60 fixed point with
+//             64-bit integer atomics (two limbs per entry, packed lower
+//             triangle in LDS): integer sums do not depend on the order the
+//             points arrive in, so the result is bitwise reproducible
+//             (g2o sums the points sequentially in double; the two differ by
+//             rounding only).  Dense LLT on the packed triangle; one-wave
+//             triangular solves; back-substitution for the points; exp-map
+//             update; accept / reject with g2o's rho rule
 //   Raul stop rule (levenberg.cpp:154-161)
 // Index structures (g2o's initializeOptimization / buildStructure) are built
 // on the host once per optimize() call.
@@ -60,11 +66,11 @@ struct LbaDev {
     const int* le_ptr; const int* le_idx;   // per point: active edges, edge order
     const int* lc_ptr; const int* lc_idx;   // per point: Schur column (free poses, pose order)
     // scratch
-    double* ce;                    // [nE][18]: Hpl = B^T W A per edge (row-major 6x3)
+    double* ce;                    // index maps of k_lba_build / k_lba_rebuild (no Hpl blocks are stored)
     double* hp;                    // [nP][27]: Hpp upper 21 | bp 6
     double* hl;                    // [nL][9]: Hll upper 6 | bl 3
     double* dl;                    // [nL][12]: Dinv 9 | db 3
-    double* S;                     // [dim_p][dim_p] (global fallback)
+    double* S;                     // reduced system, lba_sys_doubles(dim_p) (global fallback of the LDS copy)
     double* x;                     // [dim_p + 3 nL]
     double* bs;                    // [dim_p]
     // the caller's problem arrays (staged; read by k_lba_build only)
@@ -185,6 +191,18 @@ __device__ inline double edge_chi2(const LbaDev& P, int a)
     return e0 * (s * e0) + e1 * (s * e1);
 }
 
+// EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) of
+// active edge a at the current pose / point, with the camera-frame point
+__device__ inline void edge_residual(const LbaDev& P, int a, double (&pc)[3], double& e0, double& e1)
+{
+    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
+    const double* c = P.cam + 4 * P.e_pose[a];
+    const double u = pc[0] / pc[2] * c[0] + c[2];
+    const double v = pc[1] / pc[2] * c[1] + c[3];
+    e0 = P.e_obs[2 * a] - u;
+    e1 = P.e_obs[2 * a + 1] - v;
+}
+
 // computeActiveErrors + activeRobustChi2
 __device__ double compute_errors(LbaDev& P, DScratch& sc)
 {
@@ -192,12 +210,7 @@ __device__ double compute_errors(LbaDev& P, DScratch& sc)
     for (int a = threadIdx.x; a < P.nE; a += kLbaThreads) {
         const int e = P.e_orig[a];
         double pc[3];
-        se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
-        const double* c = P.cam + 4 * P.e_pose[a];
-        const double u = pc[0] / pc[2] * c[0] + c[2];
-        const double v = pc[1] / pc[2] * c[1] + c[3];
-        P.err[2 * e] = P.e_obs[2 * a] - u;
-        P.err[2 * e + 1] = P.e_obs[2 * a + 1] - v;
+        edge_residual(P, a, pc, P.err[2 * e], P.err[2 * e + 1]);
         double r0, r1;
         huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
         part += r0;
@@ -213,11 +226,11 @@ struct EdgeLin {
     double A[6], B[12], w, om0, om1;
 };
 
-__device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
+// (pc: the camera-frame point, e0 / e1 the edge's error, both at the
+// linearisation point)
+__device__ inline void edge_linearize_at(const LbaDev& P, int a, const double (&pc)[3], double e0, double e1, EdgeLin& L)
 {
     const double* T = P.pose + 7 * P.e_pose[a];
-    double pc[3];
-    se3_map(T, P.point + 3 * P.e_point[a], pc);
     const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
     const double* c = P.cam + 4 * P.e_pose[a];
     const double fx = c[0], fy = c[1];
@@ -242,21 +255,45 @@ __device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
     L.B[9] = 0;
     L.B[10] = -1. / z * fy;
     L.B[11] = y / z_2 * fy;
-    const int e = P.e_orig[a];
     const double sg = P.e_isig[a];
     double r0, r1;
-    huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
+    huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
     L.w = r1 * sg;
-    L.om0 = -(sg * P.err[2 * e]) * r1;
-    L.om1 = -(sg * P.err[2 * e + 1]) * r1;
+    L.om0 = -(sg * e0) * r1;
+    L.om1 = -(sg * e1) * r1;
+}
+
+// linearizeOplus at the errors computeActiveErrors left in P.err
+__device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
+{
+    double pc[3];
+    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
+    const int e = P.e_orig[a];
+    edge_linearize_at(P, a, pc, P.err[2 * e], P.err[2 * e + 1], L);
+}
+
+// Hpl = B^T W A (6x3, row-major) of active edge a, rebuilt from the edge's
+// inputs at the current pose / point: inside trial_solve these are the
+// iteration's linearisation point (a rejected trial is undone before the
+// next), so the blocks equal the ones linearize() accumulated, bit for bit.
+__device__ inline void edge_hpl(const LbaDev& P, int a, double (&hpl)[18])
+{
+    double pc[3], e0, e1;
+    edge_residual(P, a, pc, e0, e1);
+    EdgeLin L;
+    edge_linearize_at(P, a, pc, e0, e1, L);
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) hpl[i * 3 + j] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
 }
 
 // constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
 //  - per free pose (one wave, lanes stride the pose's edges in edge order,
 //    fixed butterfly reduction): Hpp += B^T W B, bp += B^T (-Omega e)
 //  - per point (one thread, its edges in order): Hll += A^T W A,
-//    bl += A^T (-Omega e), and the edge's Hpl = B^T W A stored component-major
-//    (hpl[k * nE + a]) for the Schur complement and back-substitution.
+//    bl += A^T (-Omega e).  The edges' Hpl = B^T W A blocks are not stored:
+//    the Schur pass and the back-substitution rebuild them (edge_hpl).
 __device__ void linearize(LbaDev& P)
 {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -296,16 +333,6 @@ __device__ void linearize(LbaDev& P)
                 for (int j = i; j < 3; j++) acc[k++] += (L.A[i] * L.w) * L.A[j] + (L.A[3 + i] * L.w) * L.A[3 + j];
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[6 + i] += L.A[i] * L.om0 + L.A[3 + i] * L.om1;
-            if (P.e_ph[a] >= 0) {   // Hpl row of the edge: 18 contiguous doubles, 16-byte stores
-                double hpl[18];
-#pragma unroll
-                for (int i = 0; i < 6; i++)
-#pragma unroll
-                    for (int j = 0; j < 3; j++) hpl[i * 3 + j] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
-                double2* o = reinterpret_cast<double2*>(P.ce + 18 * (size_t)a);
-#pragma unroll
-                for (int i = 0; i < 9; i++) o[i] = make_double2(hpl[2 * i], hpl[2 * i + 1]);
-            }
         }
 #pragma unroll
         for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
@@ -315,6 +342,62 @@ __device__ void linearize(LbaDev& P)
 
 __device__ inline int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
 __device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
+// packed lower triangle: element (i, j), j <= i
+__device__ inline int pk(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// Fixed-point accumulation of the reduced camera system.  A contribution v
+// is split as v * 2^60 ~= hi * 2^40 + lo with hi = floor(v * 2^20) and
+// 0 <= lo < 2^40 (the fraction's bits below 2^-60 truncated; the split of a
+// given v is always the same), and both limbs are added with 64-bit integer
+// atomics.  Integer addition is associative, so the accumulated limbs, and
+// the double made from them, do not depend on the order in which threads
+// add: the reduced system is bitwise reproducible.  lo sums stay exact for
+// 2^23 contributions per entry; |v| >= 2^41 (or a non-finite v) flags the
+// trial, which is then rejected as CHOLMOD's failure would be.
+constexpr double kFxHi = 1048576.0;                        // 2^20
+constexpr double kFxLo = 1099511627776.0;                  // 2^40
+constexpr double kFxInvHi = 1.0 / 1048576.0;               // 2^-20
+constexpr double kFxInvLo = 1.0 / 1152921504606846976.0;   // 2^-60
+constexpr double kFxMax = 2305843009213693952.0;           // 2^61 (of v * 2^20)
+
+typedef unsigned long long fx_t;
+
+__device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
+{
+    const double t = v * kFxHi;   // exact
+    if (!(fabs(t) < kFxMax)) {
+        bad = 1;
+        hi = lo = 0;
+        return;
+    }
+    const double f = floor(t);
+    hi = (fx_t)(long long)f;
+    lo = (fx_t)(long long)((t - f) * kFxLo);   // t - f exact, in [0, 1)
+}
+
+__device__ inline void fx_add(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
+{
+    fx_t h, l;
+    fx_split(v, h, l, bad);
+    atomicAdd(hi + idx, h);
+    atomicAdd(lo + idx, l);
+}
+
+__device__ inline void fx_set(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
+{
+    fx_split(v, hi[idx], lo[idx], bad);
+}
+
+__device__ inline double fx_value(fx_t hi, fx_t lo)
+{
+    return (double)(long long)hi * kFxInvHi + (double)(long long)lo * kFxInvLo;
+}
+
+// Reduced-system storage of one problem (LDS or its global fallback), in
+// doubles: limbs hi[M] | lo[M] | bhi[n] | blo[n] with M = n (n + 1) / 2;
+// after accumulation hi[] holds the packed lower triangle as doubles and
+// bhi[] the right-hand side.
+__host__ __device__ constexpr long long lba_sys_doubles(long long n) { return n * (n + 1) + 2 * n; }
 
 // One Levenberg trial: Schur complement, LLT, back-substitution, update.
 // Returns false when the reduced system is not positive definite.
@@ -323,31 +406,44 @@ __device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j 
 __shared__ int2 s_edges[kLbaThreads][kSchurEdges];
 
 // kLds: the reduced system lives in the dynamic LDS block (its accesses then
-// compile to ds_* instructions instead of flat ones), else in P.S / P.bs.
+// compile to ds_* instructions instead of flat ones), else in P.S.
 template <bool kLds>
 __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
 {
     extern __shared__ __attribute__((aligned(16))) double s_S[];
+    __shared__ int s_bad;
     LBA_T0();
     const int n = P.dim_p;
-    double* S = kLds ? s_S : P.S;
-    double* bs = kLds ? s_S + (size_t)n * n : P.bs;
-    // S <- 0, then the diagonal blocks Hpp + lambda I (full, symmetric); bs <- bp
-    for (int i = threadIdx.x; i < n * n; i += kLbaThreads) S[i] = 0.0;
-    __syncthreads();
-    for (int item = threadIdx.x; item < P.nP * 36; item += kLbaThreads) {
-        const int p = item / 36, rc = item - p * 36, r = rc / 6, c = rc - r * 6;
-        S[(size_t)(6 * p + r) * n + 6 * p + c] = P.hp[27 * p + (r <= c ? up6(r, c) : up6(c, r))] + (r == c ? lambda : 0.0);
+    const int M = n * (n + 1) / 2;
+    fx_t* hi = reinterpret_cast<fx_t*>(kLds ? s_S : P.S);
+    fx_t* lo = hi + M;
+    fx_t* bhi = lo + M;
+    fx_t* blo = bhi + n;
+    double* S = reinterpret_cast<double*>(hi);     // packed lower triangle, after conversion
+    double* bs = reinterpret_cast<double*>(bhi);
+    int bad = 0;
+    // the diagonal blocks Hpp + lambda I, zero elsewhere; bs <- bp
+    for (int k = threadIdx.x; k < M; k += kLbaThreads) {
+        hi[k] = 0;
+        lo[k] = 0;
     }
-    for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = P.hp[27 * (i / 6) + 21 + (i % 6)];
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
+        const int p = item / 21, u = item - p * 21;
+        int r = 0;
+        while (up6(r, 5) < u) r++;
+        const int c = r + (u - up6(r, r));   // upper element (r, c), c >= r
+        fx_set(hi, lo, pk(6 * p + c, 6 * p + r), P.hp[27 * p + u] + (r == c ? lambda : 0.0), bad);
+    }
+    for (int i = threadIdx.x; i < n; i += kLbaThreads) fx_set(bhi, blo, i, P.hp[27 * (i / 6) + 21 + (i % 6)], bad);
     __syncthreads();
     LBA_MARK(1);
     // Schur complement, point by point (one thread per point, its edges are
     // contiguous): D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse),
     // db; then bs -= W_i db and S(i, j) -= (W_i Dinv) W_j^T for every pair of
     // the point's free-pose edges (upper blocks; diagonal blocks upper
-    // triangle), accumulated with FP64 atomics into the reduced camera system
-    // held in LDS.
+    // triangle), as fixed-point limbs.
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
         double m[9];
@@ -373,11 +469,9 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
 #pragma unroll
         for (int i = 0; i < 12; i++) dl[i] = d[i];
         const int q0 = P.lc_ptr[l], q1 = P.lc_ptr[l + 1], k = q1 - q0;
-        // The point's free-pose edges (edge, pose block) go to this thread's
-        // LDS row first, so the pair loop below waits on one global load per
-        // pair (the edge's Hpl block, prefetched one pair ahead) instead of a
-        // chain of three.  Points with more than kSchurEdges such edges read
-        // the lists from global memory.
+        // the point's free-pose edges (edge, pose block) in this thread's LDS
+        // row; points with more than kSchurEdges such edges read the lists
+        // from global memory
         int2* te = s_edges[threadIdx.x];
         const bool tab = k <= kSchurEdges;
         if (tab)
@@ -386,89 +480,77 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
                 te[j] = make_int2(a, P.e_ph[a]);
             }
         auto edge_at = [&](int j) { return tab ? te[j] : make_int2(P.lc_idx[q0 + j], P.e_ph[P.lc_idx[q0 + j]]); };
-        auto load_hpl = [&](int a, double2 (&v)[9]) {
-            const double2* src = reinterpret_cast<const double2*>(P.ce + 18 * (size_t)a);
-#pragma unroll
-            for (int i = 0; i < 9; i++) v[i] = src[i];
-        };
         // The point's edges in groups of kSchurGroup: the group's W_i Dinv
-        // blocks stay in registers while every later edge's W_j is loaded
-        // once for the whole group: k + ~k^2 / (2 G) Hpl reads per point
-        // instead of k (k + 1) / 2 (the pass re-read these blocks from HBM).
+        // blocks stay in registers while every later edge's W_j is rebuilt
+        // once for the whole group (k + ~k^2 / (2 G) rebuilds per point).
         constexpr int G = kSchurGroup;
         // S(i1, i2) -= (W_i Dinv) W_j^T over the 6x6 block (upper triangle of
-        // a diagonal block)
-        auto pair_update = [&](const double (&w)[18], int i1, const double2 (&bj2)[9], int i2) {
-            double bj[18];
-#pragma unroll
-            for (int i = 0; i < 9; i++) {
-                bj[2 * i] = bj2[i].x;
-                bj[2 * i + 1] = bj2[i].y;
-            }
+        // a diagonal block), stored as the lower element (6 i2 + c, 6 i1 + r)
+        auto pair_update = [&](const double (&w)[18], int i1, const double (&bj)[18], int i2) {
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
                 for (int c = 0; c < 6; c++) {
                     if (i1 == i2 && c < r) continue;
                     const double v = w[r * 3] * bj[c * 3] + w[r * 3 + 1] * bj[c * 3 + 1] + w[r * 3 + 2] * bj[c * 3 + 2];
-                    atomicAdd(&S[(size_t)(6 * i1 + r) * n + 6 * i2 + c], -v);
+                    fx_add(hi, lo, pk(6 * i2 + c, 6 * i1 + r), -v, bad);
                 }
         };
         for (int g = 0; g < k; g += G) {
             double wd[G][18];   // W_i Dinv (6x3) of the group's edges
             int pi[G];
-            double2 cur[9];
-            // the group's own W blocks, each loaded once: W_i Dinv, bs, and
-            // the pairs among the group's edges
+            double cur[18];
+            // the group's own W blocks: W_i Dinv, bs, and the pairs among the
+            // group's edges
 #pragma unroll
             for (int u = 0; u < G; u++) {
                 pi[u] = -1;
                 if (g + u < k) {
                     const int2 ei = edge_at(g + u);
                     pi[u] = ei.y;
-                    load_hpl(ei.x, cur);
+                    edge_hpl(P, ei.x, cur);
 #pragma unroll
                     for (int r = 0; r < 6; r++) {
-                        const double b0 = (r & 1) ? cur[(3 * r) >> 1].y : cur[(3 * r) >> 1].x;
-                        const double b1 = (r & 1) ? cur[(3 * r + 1) >> 1].x : cur[(3 * r + 1) >> 1].y;
-                        const double b2 = (r & 1) ? cur[(3 * r + 2) >> 1].y : cur[(3 * r + 2) >> 1].x;
+                        const double b0 = cur[3 * r], b1 = cur[3 * r + 1], b2 = cur[3 * r + 2];
 #pragma unroll
                         for (int c = 0; c < 3; c++) wd[u][r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
-                        atomicAdd(&bs[6 * ei.y + r], -(b0 * d[9] + b1 * d[10] + b2 * d[11]));
+                        fx_add(bhi, blo, 6 * ei.y + r, -(b0 * d[9] + b1 * d[10] + b2 * d[11]), bad);
                     }
 #pragma unroll
                     for (int v = 0; v <= u; v++) pair_update(wd[v], pi[v], cur, ei.y);
                 }
             }
-            // every later edge's W_j, loaded once for the whole group
+            // every later edge's W_j, rebuilt once for the whole group
             for (int qj = g + G; qj < k; qj++) {
                 const int2 ej = edge_at(qj);
-                load_hpl(ej.x, cur);
+                edge_hpl(P, ej.x, cur);
 #pragma unroll
                 for (int u = 0; u < G; u++) pair_update(wd[u], pi[u], cur, ej.y);
             }
         }
     }
+    if (bad) s_bad = 1;
     __syncthreads();
-    // the factorisation reads the lower triangle: mirror the upper blocks
-    for (int item = threadIdx.x; item < n * n; item += kLbaThreads) {
-        const int r = item / n, c = item - r * n;
-        if (c < r) S[item] = S[(size_t)c * n + r];
-    }
+    if (s_bad) return false;   // uniform
+    // limbs -> doubles in place (element k's double overwrites its own hi)
+    for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(hi[k], lo[k]);
+    for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]);
     __syncthreads();
     LBA_MARK(2);
-    // dense LLT (right-looking), lower triangle; two barriers per column
+    // dense LLT (right-looking) on the packed lower triangle; two barriers
+    // per column
     for (int k = 0; k < n; k++) {
-        const double akk = S[(size_t)k * n + k];
+        const double akk = S[pk(k, k)];
         if (!(akk > 0)) return false;   // same value in every thread
         const double lkk = sqrt(akk);
         __syncthreads();                // everyone has read S[k][k]
-        if (threadIdx.x == 0) S[(size_t)k * n + k] = lkk;
-        for (int i = k + 1 + threadIdx.x; i < n; i += kLbaThreads) S[(size_t)i * n + k] /= lkk;
+        if (threadIdx.x == 0) S[pk(k, k)] = lkk;
+        for (int i = k + 1 + threadIdx.x; i < n; i += kLbaThreads) S[pk(i, k)] /= lkk;
         __syncthreads();
         for (int i = k + 1 + (threadIdx.x >> 5); i < n; i += kLbaThreads / 32) {
-            const double lik = S[(size_t)i * n + k];
-            for (int j = k + 1 + (threadIdx.x & 31); j <= i; j += 32) S[(size_t)i * n + j] -= lik * S[(size_t)j * n + k];
+            const double lik = S[pk(i, k)];
+            double* Si = S + pk(i, 0);
+            for (int j = k + 1 + (threadIdx.x & 31); j <= i; j += 32) Si[j] -= lik * S[pk(j, k)];
         }
         __syncthreads();
     }
@@ -482,16 +564,17 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         for (int k = 0; k < n; k++) {
-            const double xk = xp[k] / S[(size_t)k * n + k];
-            for (int i = k + 1 + lane; i < n; i += 64) xp[i] -= S[(size_t)i * n + k] * xk;
+            const double xk = xp[k] / S[pk(k, k)];
+            for (int i = k + 1 + lane; i < n; i += 64) xp[i] -= S[pk(i, k)] * xk;
             if (lane == 0) xp[k] = xk;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         for (int k = n - 1; k >= 0; k--) {
-            const double xk = xp[k] / S[(size_t)k * n + k];
-            for (int i = lane; i < k; i += 64) xp[i] -= S[(size_t)k * n + i] * xk;
+            const double xk = xp[k] / S[pk(k, k)];
+            const double* Sk = S + pk(k, 0);
+            for (int i = lane; i < k; i += 64) xp[i] -= Sk[i] * xk;
             if (lane == 0) xp[k] = xk;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
@@ -500,16 +583,20 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     }
     __syncthreads();
     LBA_MARK(4);
-    // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i)
+    // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i), the W_i rebuilt
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
         const double* h = P.hl + 9 * l;
         double cl[3] = {h[6], h[7], h[8]};
         for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
             const int a = P.lc_idx[q];
             const int i1 = P.e_ph[a];
+            double w[18];
+            edge_hpl(P, a, w);
+#pragma unroll
             for (int c = 0; c < 3; c++) {
                 double acc = 0;
-                for (int r = 0; r < 6; r++) acc += P.ce[18 * (size_t)a + r * 3 + c] * (-xp[6 * i1 + r]);
+#pragma unroll
+                for (int r = 0; r < 6; r++) acc += w[r * 3 + c] * (-xp[6 * i1 + r]);
                 cl[c] += acc;
             }
         }
@@ -532,7 +619,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         return;
     }
     const int n = P.dim_p;
-    const bool in_lds = n * n + n <= lds_S_cap;
+    const bool in_lds = lba_sys_doubles(n) <= lds_S_cap;
     LBA_T0();
     double currentChi = compute_errors(P, sc);
     const double iniChi = currentChi;
@@ -1168,9 +1255,12 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         const size_t nE = p.n_edges, nL = p.n_points, n = 6 * (size_t)nfree[i];
-        L.max_n2 = std::max(L.max_n2, n * n + n);
-        const size_t bytes[7] = {std::max(18 * nE * 8, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
-                                 9 * nL * 8, 12 * nL * 8, n * n + n > (size_t)kLdsSCap ? n * n * 8 : 8, (n + 3 * nL) * 8,
+        const size_t sys = (size_t)lba_sys_doubles((long long)n);
+        L.max_n2 = std::max(L.max_n2, sys);
+        // ce: index maps of k_lba_build / k_lba_rebuild only (no Hpl blocks
+        // are stored); S: the reduced system when it does not fit LDS
+        const size_t bytes[7] = {std::max(nE * 4, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
+                                 9 * nL * 8, 12 * nL * 8, sys > (size_t)kLdsSCap ? sys * 8 : 8, (n + 3 * nL) * 8,
                                  n * 8 + 8};
         for (int k = 0; k < 7; k++) {
             sc[8 * i + k] = end;
