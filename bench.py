@@ -276,6 +276,22 @@ def cpu_baseline_lba(probs, protocol, L=None, lib_desc=""):
     return out
 
 
+def lba_flops(prob, stats):
+    """FP64 flops of one local-BA solve by SURVEY.md 8(d)'s per-iteration
+    formula: E (~150 linearize + ~250 accumulate) per LM iteration, and per
+    trial the Schur complement sum_points k^2 216 (k = the point's edges to
+    free poses) plus the (6P)^3 / 3 factorisation; both optimize() passes
+    with their iteration / trial counts (the second pass on the edge set
+    left after the first outlier pass, approximated by the full set)."""
+    free = prob["pose_fixed"] == 0
+    ep = np.asarray(prob["edge_pose"])
+    k = np.bincount(np.asarray(prob["edge_point"])[free[ep]], minlength=len(prob["point_id"]))
+    E = len(ep)
+    per_iter = E * 400.0
+    per_trial = float((k.astype(np.float64) ** 2).sum()) * 216.0 + (6.0 * free.sum()) ** 3 / 3.0
+    return sum(stats.iterations[p] * per_iter + stats.levenberg_trials[p] * per_trial for p in range(2))
+
+
 def pose_flops(stats, n_edges):
     """FP64 flops of one PoseOptimization from its LM statistics: ~215 per
     edge per fused error+Jacobian+H pass (one per LM iteration), ~55 per edge
@@ -648,8 +664,9 @@ def run_lba(args, wl, rank, local, world, dist):
     # one pass over all P (2 per step)
     units_per_step = {"lba_iter": P * 15, "lba_outliers": P * 2}
     cpu = None
+    flops = float(sum(lba_flops(probs[i], st[i]) for i in range(P)))
     check = {"iterations_problem0": int(stats[2]), "outliers_pass1_problem0": int(stats[3]),
-             "edges_per_problem": n_edges, "pcie_inclusive": pcie}
+             "edges_per_problem": n_edges, "pcie_inclusive": pcie, "fp64_flops_per_step": flops}
     if cpu_leg:
         check["parity_last_step"] = parity
         L, desc = native_oracle()
@@ -873,6 +890,17 @@ def main():
             # the same oracle on every host core of the box
             # (one independent stream per thread), core count stated
             out["cpu_baseline_all_cores"] = cpu.pop("all_cores")
+        if args.workload == "c5" and kernels["serial"] and kernels["serial"].get("lba_iter", {}).get("total_ms"):
+            # FP64 vector roofline of the LM iterations (SURVEY.md 8(d) flop
+            # formula over the step's iterations and trials) beside the HBM one
+            it_s = kernels["serial"]["lba_iter"]["total_ms"] / 1e3 / kernels["serial_steps"]
+            fl = check["fp64_flops_per_step"] / it_s / 1e12
+            out["roofline_fp64"] = {"bound": "fp64-valu", "achieved": round(fl, 4), "peak": FP64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": round(fl / FP64_PEAK_TFLOPS, 5), "kernel": "lba_iter",
+                                    "flops_per_step": check["fp64_flops_per_step"],
+                                    "lba_iter_ms_per_step": round(it_s * 1e3, 4),
+                                    "note": "algorithmic flops (SURVEY.md 8(d)): the kernel also rebuilds each edge's "
+                                            "Hpl block where it is used instead of storing it"}
         if args.workload == "pose" and roof and roof.get("avg_launch_ms"):
             # PoseOptimization is FP64-VALU bound (its edges are read from HBM
             # once and kept in LDS): the FP64 roofline is the headline one, the

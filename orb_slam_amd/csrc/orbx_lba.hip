@@ -346,33 +346,36 @@ __device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j 
 __device__ inline int pk(int i, int j) { return i * (i + 1) / 2 + j; }
 
 // Fixed-point accumulation of the reduced camera system.  A contribution v
-// is split as v * 2^60 ~= hi * 2^40 + lo with hi = floor(v * 2^20) and
-// 0 <= lo < 2^40 (the fraction's bits below 2^-60 truncated; the split of a
-// given v is always the same), and both limbs are added with 64-bit integer
-// atomics.  Integer addition is associative, so the accumulated limbs, and
-// the double made from them, do not depend on the order in which threads
-// add: the reduced system is bitwise reproducible.  lo sums stay exact for
-// 2^23 contributions per entry; |v| >= 2^41 (or a non-finite v) flags the
-// trial, which is then rejected as CHOLMOD's failure would be.
-constexpr double kFxHi = 1048576.0;                        // 2^20
+// (|v| < 2^40) is split as v * 2^51 ~= hi * 2^40 + lo: hi = round(v * 2^11),
+// lo = round((v * 2^11 - hi) * 2^40), |lo| <= 2^39 (the split of a given v is
+// always the same; bits below 2^-51 are rounded off, far below the double
+// rounding of the entries, whose natural scale is >= 1 here), and both limbs
+// are added with 64-bit integer atomics.  Integer addition is associative,
+// so the accumulated limbs, and the double made from them, do not depend on
+// the order in which threads add: the reduced system is bitwise
+// reproducible.  lo sums stay exact for 2^23 contributions per entry; a
+// contribution with |v| >= 2^40 (or non-finite) flags the trial, which is
+// then rejected as CHOLMOD's failure would be.  Integerisation by the
+// 1.5 * 2^52 magic-number addition (exact round-to-nearest for |x| < 2^51).
+constexpr double kFxHi = 2048.0;                           // 2^11
 constexpr double kFxLo = 1099511627776.0;                  // 2^40
-constexpr double kFxInvHi = 1.0 / 1048576.0;               // 2^-20
-constexpr double kFxInvLo = 1.0 / 1152921504606846976.0;   // 2^-60
-constexpr double kFxMax = 2305843009213693952.0;           // 2^61 (of v * 2^20)
+constexpr double kFxInvHi = 1.0 / 2048.0;                  // 2^-11
+constexpr double kFxInvLo = 1.0 / 2251799813685248.0;      // 2^-51
+constexpr double kFxMax = 2251799813685248.0;              // 2^51 (of v * 2^11)
+constexpr double kFxMagic = 6755399441055744.0;            // 1.5 * 2^52
 
 typedef unsigned long long fx_t;
 
 __device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
 {
     const double t = v * kFxHi;   // exact
-    if (!(fabs(t) < kFxMax)) {
-        bad = 1;
-        hi = lo = 0;
-        return;
-    }
-    const double f = floor(t);
-    hi = (fx_t)(long long)f;
-    lo = (fx_t)(long long)((t - f) * kFxLo);   // t - f exact, in [0, 1)
+    bad |= !(fabs(t) < kFxMax);
+    const double th = t + kFxMagic;                 // round(t) in the low mantissa bits
+    const double r = t - (th - kFxMagic);           // exact, |r| <= 1/2
+    const double tl = __fma_rn(r, kFxLo, kFxMagic); // round(r * 2^40) likewise
+    const long long m = __double_as_longlong(kFxMagic);
+    hi = (fx_t)(__double_as_longlong(th) - m);
+    lo = (fx_t)(__double_as_longlong(tl) - m);
 }
 
 __device__ inline void fx_add(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
@@ -443,8 +446,13 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     // contiguous): D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse),
     // db; then bs -= W_i db and S(i, j) -= (W_i Dinv) W_j^T for every pair of
     // the point's free-pose edges (upper blocks; diagonal blocks upper
-    // triangle), as fixed-point limbs.
-    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+    // triangle), as fixed-point limbs.  Points are taken in the order of
+    // their edge counts (P.ce, point_order): the lanes of a wave run loops of
+    // similar length and every thread gets a similar share; with
+    // order-independent sums this changes no bit of the result.
+    const int* order = reinterpret_cast<const int*>(P.ce);
+    for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
+        const int l = order[t];
         const double* h = P.hl + 9 * l;
         double m[9];
 #pragma unroll
@@ -584,7 +592,8 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     __syncthreads();
     LBA_MARK(4);
     // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i), the W_i rebuilt
-    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+    for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
+        const int l = order[t];
         const double* h = P.hl + 9 * l;
         double cl[3] = {h[6], h[7], h[8]};
         for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
@@ -608,6 +617,30 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     return true;
 }
 
+// The points of a pass by decreasing count of free-pose edges (counting
+// sort; the order within a count is arbitrary and does not matter) into
+// P.ce, which is free scratch once the pass's structure is built.
+__device__ void point_order(LbaDev& P)
+{
+    __shared__ int hist[64], off[64];
+    int* order = reinterpret_cast<int*>(P.ce);
+    for (int b = threadIdx.x; b < 64; b += kLbaThreads) hist[b] = 0;
+    __syncthreads();
+    auto bucket = [&](int l) { return 63 - min(P.lc_ptr[l + 1] - P.lc_ptr[l], 63); };
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) atomicAdd(&hist[bucket(l)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int b = 0; b < 64; b++) {
+            off[b] = acc;
+            acc += hist[b];
+        }
+    }
+    __syncthreads();
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) order[atomicAdd(&off[bucket(l)], 1)] = l;
+    __syncthreads();
+}
+
 // OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
 __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
 {
@@ -620,6 +653,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
     }
     const int n = P.dim_p;
     const bool in_lds = lba_sys_doubles(n) <= lds_S_cap;
+    if (iteration == 0) point_order(P);
     LBA_T0();
     double currentChi = compute_errors(P, sc);
     const double iniChi = currentChi;
