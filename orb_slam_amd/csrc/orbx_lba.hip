@@ -73,6 +73,7 @@ struct LbaDev {
     double* S;                     // reduced system, lba_sys_doubles(dim_p) (global fallback of the LDS copy)
     double* x;                     // [dim_p + 3 nL]
     double* bs;                    // [dim_p]
+    double* ew;                    // [nE] robust weight rho' * invSigma2 of the linearisation
     // the caller's problem arrays (staged; read by k_lba_build only)
     const int* r_edge_pose;
     const int* r_edge_point;
@@ -226,35 +227,44 @@ struct EdgeLin {
     double A[6], B[12], w, om0, om1;
 };
 
-// (pc: the camera-frame point, e0 / e1 the edge's error, both at the
-// linearisation point)
-__device__ inline void edge_linearize_at(const LbaDev& P, int a, const double (&pc)[3], double e0, double e1, EdgeLin& L)
+// The Jacobians of linearizeOplus at camera-frame point pc: the
+// reference's divisions by z and z^2 as products with 1/z (one division per
+// edge; the values differ from g2o's in rounding only).
+__device__ inline void edge_jacobians(const LbaDev& P, int a, const double (&pc)[3], double (&A)[6], double (&B)[12])
 {
     const double* T = P.pose + 7 * P.e_pose[a];
-    const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+    const double x = pc[0], y = pc[1];
+    const double iz = 1. / pc[2], iz2 = iz * iz;
     const double* c = P.cam + 4 * P.e_pose[a];
     const double fx = c[0], fy = c[1];
-    const double tmp[6] = {fx, 0, -x / z * fx, 0, fy, -y / z * fy};
+    const double tmp[6] = {fx, 0, -(x * iz) * fx, 0, fy, -(y * iz) * fy};
     double R[9];
     qmat(Q{T[0], T[1], T[2], T[3]}, R);
-    const double s = -1. / z;
+    const double s = -iz;
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int j = 0; j < 3; j++)
-            L.A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
-    L.B[0] = x * y / z_2 * fx;
-    L.B[1] = -(1 + (x * x / z_2)) * fx;
-    L.B[2] = y / z * fx;
-    L.B[3] = -1. / z * fx;
-    L.B[4] = 0;
-    L.B[5] = x / z_2 * fx;
-    L.B[6] = (1 + y * y / z_2) * fy;
-    L.B[7] = -x * y / z_2 * fy;
-    L.B[8] = -x / z * fy;
-    L.B[9] = 0;
-    L.B[10] = -1. / z * fy;
-    L.B[11] = y / z_2 * fy;
+            A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
+    B[0] = x * y * iz2 * fx;
+    B[1] = -(1 + (x * x * iz2)) * fx;
+    B[2] = y * iz * fx;
+    B[3] = -iz * fx;
+    B[4] = 0;
+    B[5] = x * iz2 * fx;
+    B[6] = (1 + y * y * iz2) * fy;
+    B[7] = -x * y * iz2 * fy;
+    B[8] = -x * iz * fy;
+    B[9] = 0;
+    B[10] = -iz * fy;
+    B[11] = y * iz2 * fy;
+}
+
+// (pc: the camera-frame point, e0 / e1 the edge's error, both at the
+// linearisation point)
+__device__ inline void edge_linearize_at(const LbaDev& P, int a, const double (&pc)[3], double e0, double e1, EdgeLin& L)
+{
+    edge_jacobians(P, a, pc, L.A, L.B);
     const double sg = P.e_isig[a];
     double r0, r1;
     huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
@@ -272,20 +282,23 @@ __device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
     edge_linearize_at(P, a, pc, P.err[2 * e], P.err[2 * e + 1], L);
 }
 
-// Hpl = B^T W A (6x3, row-major) of active edge a, rebuilt from the edge's
-// inputs at the current pose / point: inside trial_solve these are the
-// iteration's linearisation point (a rejected trial is undone before the
-// next), so the blocks equal the ones linearize() accumulated, bit for bit.
+// Hpl = B^T W A (6x3, row-major) of active edge a, rebuilt at the current
+// pose / point with the weight linearize() stored: inside trial_solve these
+// are the iteration's linearisation point (a rejected trial is undone before
+// the next), so the blocks are the ones g2o's linearisation would store.
 __device__ inline void edge_hpl(const LbaDev& P, int a, double (&hpl)[18])
 {
-    double pc[3], e0, e1;
-    edge_residual(P, a, pc, e0, e1);
-    EdgeLin L;
-    edge_linearize_at(P, a, pc, e0, e1, L);
+    double pc[3];
+    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
+    double A[6], B[12];
+    edge_jacobians(P, a, pc, A, B);
+    const double w = P.ew[a];   // the robust weight linearize() used
 #pragma unroll
-    for (int i = 0; i < 6; i++)
+    for (int i = 0; i < 6; i++) {
+        const double b0 = B[i] * w, b1 = B[6 + i] * w;
 #pragma unroll
-        for (int j = 0; j < 3; j++) hpl[i * 3 + j] = (L.B[i] * L.w) * L.A[j] + (L.B[6 + i] * L.w) * L.A[3 + j];
+        for (int j = 0; j < 3; j++) hpl[i * 3 + j] = __fma_rn(b1, A[3 + j], b0 * A[j]);
+    }
 }
 
 // constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
@@ -326,6 +339,7 @@ __device__ void linearize(LbaDev& P)
             const int a = P.le_idx[q];
             EdgeLin L;
             edge_linearize(P, a, L);
+            P.ew[a] = L.w;
             int k = 0;
 #pragma unroll
             for (int i = 0; i < 3; i++)
@@ -366,9 +380,9 @@ constexpr double kFxMagic = 6755399441055744.0;            // 1.5 * 2^52
 
 typedef unsigned long long fx_t;
 
-__device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
+// (t = v * 2^11, already scaled)
+__device__ inline void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
 {
-    const double t = v * kFxHi;   // exact
     bad |= !(fabs(t) < kFxMax);
     const double th = t + kFxMagic;                 // round(t) in the low mantissa bits
     const double r = t - (th - kFxMagic);           // exact, |r| <= 1/2
@@ -378,12 +392,39 @@ __device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
     lo = (fx_t)(__double_as_longlong(tl) - m);
 }
 
-__device__ inline void fx_add(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
+__device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
+{
+    fx_split_scaled(v * kFxHi, hi, lo, bad);   // the scaling is exact
+}
+
+// 64-bit integer atomic add into the reduced system, with the address space
+// explicit (LDS, or global for the kLds = false fallback): on a generic
+// pointer the compiler tests the address space at run time, and that test
+// has tripped its instruction selection here
+template <bool kLds>
+__device__ inline void fx_atomic(fx_t* p, fx_t v)
+{
+    if constexpr (kLds) {
+        atomicAdd(p, v);
+    } else {
+        auto* g = (__attribute__((address_space(1))) fx_t*)p;
+        __hip_atomic_fetch_add(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+template <bool kLds>
+__device__ inline void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int& bad)
 {
     fx_t h, l;
-    fx_split(v, h, l, bad);
-    atomicAdd(hi + idx, h);
-    atomicAdd(lo + idx, l);
+    fx_split_scaled(t, h, l, bad);
+    fx_atomic<kLds>(hi + idx, h);
+    fx_atomic<kLds>(lo + idx, l);
+}
+
+template <bool kLds>
+__device__ inline void fx_add(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
+{
+    fx_add_scaled<kLds>(hi, lo, idx, v * kFxHi, bad);   // the scaling is exact
 }
 
 __device__ inline void fx_set(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
@@ -451,6 +492,9 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     // similar length and every thread gets a similar share; with
     // order-independent sums this changes no bit of the result.
     const int* order = reinterpret_cast<const int*>(P.ce);
+#ifdef ORBX_DIAG_SCHUR
+    double diag_sink = 0;
+#endif
     for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
         const int l = order[t];
         const double* h = P.hl + 9 * l;
@@ -494,14 +538,23 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
         constexpr int G = kSchurGroup;
         // S(i1, i2) -= (W_i Dinv) W_j^T over the 6x6 block (upper triangle of
         // a diagonal block), stored as the lower element (6 i2 + c, 6 i1 + r)
+        // (w = -2^11 W_i Dinv: the element's contribution already negated and
+        // in fixed-point scale; fused multiply-adds)
         auto pair_update = [&](const double (&w)[18], int i1, const double (&bj)[18], int i2) {
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
                 for (int c = 0; c < 6; c++) {
                     if (i1 == i2 && c < r) continue;
-                    const double v = w[r * 3] * bj[c * 3] + w[r * 3 + 1] * bj[c * 3 + 1] + w[r * 3 + 2] * bj[c * 3 + 2];
-                    fx_add(hi, lo, pk(6 * i2 + c, 6 * i1 + r), -v, bad);
+                    const double t =
+                        __fma_rn(w[r * 3 + 2], bj[c * 3 + 2], __fma_rn(w[r * 3 + 1], bj[c * 3 + 1], w[r * 3] * bj[c * 3]));
+#if defined(ORBX_DIAG_SCHUR) && ORBX_DIAG_SCHUR == 1   // timing diagnostics only (wrong results)
+                    diag_sink += t;
+#elif defined(ORBX_DIAG_SCHUR) && ORBX_DIAG_SCHUR == 2
+                    if (r == 0 && c == 0) diag_sink += t;
+#else
+                    fx_add_scaled<kLds>(hi, lo, pk(6 * i2 + c, 6 * i1 + r), t, bad);
+#endif
                 }
         };
         for (int g = 0; g < k; g += G) {
@@ -521,8 +574,9 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
                     for (int r = 0; r < 6; r++) {
                         const double b0 = cur[3 * r], b1 = cur[3 * r + 1], b2 = cur[3 * r + 2];
 #pragma unroll
-                        for (int c = 0; c < 3; c++) wd[u][r * 3 + c] = b0 * d[c] + b1 * d[3 + c] + b2 * d[6 + c];
-                        fx_add(bhi, blo, 6 * ei.y + r, -(b0 * d[9] + b1 * d[10] + b2 * d[11]), bad);
+                        for (int c = 0; c < 3; c++)
+                            wd[u][r * 3 + c] = -kFxHi * __fma_rn(b2, d[6 + c], __fma_rn(b1, d[3 + c], b0 * d[c]));
+                        fx_add<kLds>(bhi, blo, 6 * ei.y + r, -(b0 * d[9] + b1 * d[10] + b2 * d[11]), bad);
                     }
 #pragma unroll
                     for (int v = 0; v <= u; v++) pair_update(wd[v], pi[v], cur, ei.y);
@@ -537,6 +591,9 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
             }
         }
     }
+#ifdef ORBX_DIAG_SCHUR
+    if (diag_sink == 1.2345) bad = 1;
+#endif
     if (bad) s_bad = 1;
     __syncthreads();
     if (s_bad) return false;   // uniform
@@ -545,48 +602,121 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]);
     __syncthreads();
     LBA_MARK(2);
-    // dense LLT (right-looking) on the packed lower triangle; two barriers
-    // per column
-    for (int k = 0; k < n; k++) {
-        const double akk = S[pk(k, k)];
-        if (!(akk > 0)) return false;   // same value in every thread
-        const double lkk = sqrt(akk);
-        __syncthreads();                // everyone has read S[k][k]
-        if (threadIdx.x == 0) S[pk(k, k)] = lkk;
-        for (int i = k + 1 + threadIdx.x; i < n; i += kLbaThreads) S[pk(i, k)] /= lkk;
+    // dense LLT on the packed lower triangle, right-looking in 6x6 blocks
+    // (the pose blocks): per block column one wave factors the diagonal block
+    // in registers (rows on lanes 0..5, shuffles), the panel rows solve
+    // against it, the trailing triangle takes the rank-6 update; three
+    // barriers per block column instead of three per column.
+    const int nb = n / 6;
+    for (int kb = 0; kb < nb; kb++) {
+        const int k0 = 6 * kb;
+        if (threadIdx.x < 64) {
+            const int i = threadIdx.x;
+            const bool row = i < 6;
+            double a[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) a[j] = (row && j <= i) ? S[pk(k0 + i, k0 + j)] : 0.0;
+            int fail = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const double piv = __shfl(a[j], j, 64);   // a_jj after the previous columns
+                fail |= !(piv > 0);
+                const double ljj = sqrt(piv);
+                if (i == j) a[j] = ljj;
+                else if (row && i > j) a[j] = a[j] / ljj;
+#pragma unroll
+                for (int q = j + 1; q < 6; q++) {
+                    const double lqj = __shfl(a[j], q, 64);
+                    if (row && i >= q) a[q] -= a[j] * lqj;
+                }
+            }
+            if (row)
+#pragma unroll
+                for (int j = 0; j < 6; j++)
+                    if (j <= i) S[pk(k0 + i, k0 + j)] = a[j];
+            if (i == 0) s_bad = fail;
+        }
         __syncthreads();
-        for (int i = k + 1 + (threadIdx.x >> 5); i < n; i += kLbaThreads / 32) {
-            const double lik = S[pk(i, k)];
+        if (s_bad) return false;   // not positive definite (uniform)
+        // panel: row r below the block solves x L_kk^T = A(r, block)
+        for (int r = k0 + 6 + threadIdx.x; r < n; r += kLbaThreads) {
+            double x[6];
+            double* Sr = S + pk(r, k0);
+#pragma unroll
+            for (int j = 0; j < 6; j++) x[j] = Sr[j];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const double* Lj = S + pk(k0 + j, k0);
+#pragma unroll
+                for (int q = 0; q < j; q++) x[j] -= x[q] * Lj[q];
+                x[j] = x[j] / Lj[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 6; j++) Sr[j] = x[j];
+        }
+        __syncthreads();
+        // trailing triangle: S(i, j) -= L(i, block) . L(j, block)
+        for (int i = k0 + 6 + (threadIdx.x >> 5); i < n; i += kLbaThreads / 32) {
+            const double* Li = S + pk(i, k0);
+            const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
             double* Si = S + pk(i, 0);
-            for (int j = k + 1 + (threadIdx.x & 31); j <= i; j += 32) Si[j] -= lik * S[pk(j, k)];
+            for (int j = k0 + 6 + (threadIdx.x & 31); j <= i; j += 32) {
+                const double* Lj = S + pk(j, k0);
+                Si[j] -= ((((l0 * Lj[0] + l1 * Lj[1]) + l2 * Lj[2]) + l3 * Lj[3]) + l4 * Lj[4]) + l5 * Lj[5];
+            }
         }
         __syncthreads();
     }
     LBA_MARK(3);
-    // forward / backward substitution by one wave (no block barriers per step)
+    // forward / backward substitution by one wave, in 6-row blocks: the
+    // block's triangle on lanes 0..5 with shuffles, then the other rows
+    // updated with the block's six values; one wave barrier per block
     double* xp = P.x;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         for (int i = lane; i < n; i += 64) xp[i] = bs[i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int k = 0; k < n; k++) {
-            const double xk = xp[k] / S[pk(k, k)];
-            for (int i = k + 1 + lane; i < n; i += 64) xp[i] -= S[pk(i, k)] * xk;
-            if (lane == 0) xp[k] = xk;
+        auto wave_fence = [] {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        };
+        wave_fence();
+        for (int kb = 0; kb < nb; kb++) {   // L y = b
+            const int k0 = 6 * kb;
+            double yi = lane < 6 ? xp[k0 + lane] : 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const double yj = __shfl(yi, j, 64) / S[pk(k0 + j, k0 + j)];
+                if (lane == j) yi = yj;
+                else if (lane > j && lane < 6) yi -= S[pk(k0 + lane, k0 + j)] * yj;
+            }
+            if (lane < 6) xp[k0 + lane] = yi;
+            double y[6];
+#pragma unroll
+            for (int p = 0; p < 6; p++) y[p] = __shfl(yi, p, 64);
+            for (int i = k0 + 6 + lane; i < n; i += 64) {
+                const double* Li = S + pk(i, k0);
+                xp[i] -= ((((Li[0] * y[0] + Li[1] * y[1]) + Li[2] * y[2]) + Li[3] * y[3]) + Li[4] * y[4]) + Li[5] * y[5];
+            }
+            wave_fence();
         }
-        for (int k = n - 1; k >= 0; k--) {
-            const double xk = xp[k] / S[pk(k, k)];
-            const double* Sk = S + pk(k, 0);
-            for (int i = lane; i < k; i += 64) xp[i] -= Sk[i] * xk;
-            if (lane == 0) xp[k] = xk;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int kb = nb - 1; kb >= 0; kb--) {   // L^T x = y
+            const int k0 = 6 * kb;
+            double xi = lane < 6 ? xp[k0 + lane] : 0.0;
+#pragma unroll
+            for (int j = 5; j >= 0; j--) {
+                const double xj = __shfl(xi, j, 64) / S[pk(k0 + j, k0 + j)];
+                if (lane == j) xi = xj;
+                else if (lane < j) xi -= S[pk(k0 + j, k0 + lane)] * xj;
+            }
+            if (lane < 6) xp[k0 + lane] = xi;
+            double x[6];
+#pragma unroll
+            for (int p = 0; p < 6; p++) x[p] = __shfl(xi, p, 64);
+            for (int i = lane; i < k0; i += 64)
+                xp[i] -= ((((S[pk(k0, i)] * x[0] + S[pk(k0 + 1, i)] * x[1]) + S[pk(k0 + 2, i)] * x[2]) +
+                           S[pk(k0 + 3, i)] * x[3]) + S[pk(k0 + 4, i)] * x[4]) + S[pk(k0 + 5, i)] * x[5];
+            wave_fence();
         }
     }
     __syncthreads();
@@ -1293,10 +1423,10 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
         L.max_n2 = std::max(L.max_n2, sys);
         // ce: index maps of k_lba_build / k_lba_rebuild only (no Hpl blocks
         // are stored); S: the reduced system when it does not fit LDS
-        const size_t bytes[7] = {std::max(nE * 4, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
+        const size_t bytes[8] = {std::max(nE * 4, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
                                  9 * nL * 8, 12 * nL * 8, sys > (size_t)kLdsSCap ? sys * 8 : 8, (n + 3 * nL) * 8,
-                                 n * 8 + 8};
-        for (int k = 0; k < 7; k++) {
+                                 n * 8 + 8, nE * 8};
+        for (int k = 0; k < 8; k++) {
             sc[8 * i + k] = end;
             end += align256(bytes[k]);
         }
@@ -1360,6 +1490,7 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
             D.S = reinterpret_cast<double*>(d + c[4]);
             D.x = reinterpret_cast<double*>(d + c[5]);
             D.bs = reinterpret_cast<double*>(d + c[6]);
+            D.ew = reinterpret_cast<double*>(d + c[7]);
             const size_t* q = &so_raw[kRaw * i];
             D.r_edge_pose = reinterpret_cast<const int*>(d + q[0]);
             D.r_edge_point = reinterpret_cast<const int*>(d + q[1]);

@@ -243,3 +243,15 @@ def test_lba_bitwise_reproducible(ctx):
         assert list(s.iterations) == list(s0.iterations) and list(s.levenberg_trials) == list(s0.levenberg_trials)
         assert list(s.chi2_final) == list(s0.chi2_final)
     compare(run_ref(prob), runs[0])
+
+
+def test_lba_reduced_system_in_global_memory(ctx):
+    """26 free keyframes: the reduced camera system (156 x 156) exceeds the
+    LDS budget, so trial_solve runs its global-memory instantiation (the
+    fixed-point limbs in HBM with global 64-bit atomics); same bar against
+    the oracle, and bitwise reproducible."""
+    prob = sb.make_problem(n_kf=26, n_points=1200, seed=19, outlier_frac=0.02)
+    a = run_gpu(ctx, prob)
+    b = run_gpu(ctx, prob)
+    assert np.array_equal(a[0]["pose_q"], b[0]["pose_q"]) and np.array_equal(a[0]["points"], b[0]["points"])
+    compare(run_ref(prob), a)
