@@ -358,6 +358,19 @@ int orbx_search_by_bow_kf(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bo
 int orbx_search_for_triangulation(orbx_ctx* ctx, const orbx_bow_view* KF1, const orbx_bow_view* KF2,
                                   const float* F12, const float* sigma2_2, int nlevels, int check_ori,
                                   int32_t* matches12, int* n_matches);
+/* Batched forms for LocalMapping's per-neighbour loops: one keyframe KF1
+ * against n keyframes KF2s[k] in one upload, one launch (a workgroup per
+ * pair) and one readback; results as n separate calls would give.
+ * SearchForTriangulation: CreateNewMapPoints (src/LocalMapping.cc:220-260,
+ * F12s n x 9, sigma2_2s n x nlevels).  SearchByBoW(KF1, KF2): the loop
+ * candidates of LoopClosing::ComputeSim3 (src/LoopClosing.cc:240).
+ * matches12[k] (out, KF1->n) and n_matches[k] per pair. */
+int orbx_search_for_triangulation_batch(orbx_ctx* ctx, const orbx_bow_view* KF1, int n,
+                                        const orbx_bow_view* KF2s, const float* F12s,
+                                        const float* sigma2_2s, int nlevels, int check_ori,
+                                        int32_t* const* matches12, int* n_matches);
+int orbx_search_by_bow_kf_batch(orbx_ctx* ctx, const orbx_bow_view* KF1, int n, const orbx_bow_view* KF2s,
+                                float nnratio, int check_ori, int32_t* const* matches12, int* n_matches);
 
 /* Keyframe projection searches.  Map points as they
  * read them, one entry per point (SoA). */
@@ -383,6 +396,17 @@ typedef struct {
 int orbx_fuse_candidates(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
                          const orbx_mappoint_view* mps, const float* T, int sim3, float th,
                          int32_t* best_idx, int32_t* best_dist);
+/* Fuse candidates for n keyframes in one upload / launch / readback:
+ * SearchInNeighbors' loop over the target keyframes (src/LocalMapping.cc:
+ * 403-416), KFs[k] with camera cams[4k..], pose Ts[16k..] and map points
+ * *mps[k] (views that are the same object are uploaded once: the loop fuses
+ * the current keyframe's points into every neighbour).  The candidates are
+ * state-free, so computing all of them before the caller replays the graph
+ * updates neighbour by neighbour gives the sequential loop's result (a point
+ * replaced or already in the keyframe is skipped at replay, as there). */
+int orbx_fuse_candidates_batch(orbx_ctx* ctx, int n_kf, const orbx_frame_view* KFs, const float* cams,
+                               const orbx_mappoint_view* const* mps, const float* Ts, int sim3, float th,
+                               int32_t* const* best_idx, int32_t* const* best_dist);
 /* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
  * (src/ORBmatcher.cc:1267-1505).  mp1 / valid1: the map point of each KF1
  * keypoint (valid = pMP && !isBad()); mp2 / valid2 likewise for KF2.  T1w,

@@ -63,7 +63,7 @@ __device__ inline bool epipolar_ok(const orbx_keypoint& k1, const orbx_keypoint&
     return (double)dsqr < 3.84 * (double)sigma2[k2.octave];
 }
 
-__global__ __launch_bounds__(256) void k_bow_match(BowArgs a)
+__device__ void bow_match_block(const BowArgs& a)
 {
     __shared__ int hist[kHistoLength];
     __shared__ int s_acc, s_removed, s_ind[3];
@@ -186,6 +186,11 @@ __global__ __launch_bounds__(256) void k_bow_match(BowArgs a)
     if (tid == 0) *a.out_n = s_acc - s_removed;
 }
 
+__global__ __launch_bounds__(256) void k_bow_match(BowArgs a) { bow_match_block(a); }
+
+// One workgroup per job (one keyframe pair each).
+__global__ __launch_bounds__(256) void k_bow_match_jobs(const BowArgs* jobs) { bow_match_block(jobs[blockIdx.x]); }
+
 namespace {
 
 bool valid_bow(const orbx_bow_view* v, int max_octave)
@@ -301,6 +306,108 @@ int run_bow(orbx_ctx* ctx, const orbx_bow_view* V1, const orbx_bow_view* V2, int
     return ORBX_OK;
 }
 
+// One keyframe against n others (modes 1, 2): KF1 uploaded once, each pair's
+// common nodes, one launch of n workgroups, one readback.
+int run_bow_batch(orbx_ctx* ctx, const orbx_bow_view* V1, int n, const orbx_bow_view* V2s, int mode, float nnratio,
+                  int check_ori, const float* F12s, const float* sigma2s, int nlevels, int32_t* const* outs,
+                  int* n_outs)
+{
+    if (!ctx || n < 0 || (n > 0 && (!V2s || !outs || !n_outs))) return ORBX_ERR_ARG;
+    if (mode == 2 && n > 0 && (!F12s || !sigma2s || nlevels <= 0 || nlevels > kMaxLevels)) return ORBX_ERR_ARG;
+    if (!valid_bow(V1, 0)) return ORBX_ERR_ARG;
+    for (int k = 0; k < n; k++)
+        if (!valid_bow(&V2s[k], mode == 2 ? nlevels : 0) || (V1->n > 0 && !outs[k])) return ORBX_ERR_ARG;
+    if (n == 0) return ORBX_OK;
+    std::vector<std::vector<int4>> nodes(n);
+    for (int k = 0; k < n; k++) {
+        nodes[k] = common_nodes(*V1, V2s[k]);
+        for (const int4& nd : nodes[k])
+            if (nd.w > 64 * kBowMaxChunks) return ORBX_ERR_UNSUPPORTED;
+    }
+    ctx_enter(ctx);
+    const int out_len = V1->n;
+    size_t at = 0;
+    auto res = [&](size_t bytes) {
+        const size_t o = at;
+        at += al256(std::max<size_t>(bytes, 1));
+        return o;
+    };
+    const int nf1 = V1->n_nodes ? V1->node_ptr[V1->n_nodes] : 0;
+    const size_t o_k1 = res((size_t)V1->n * sizeof(orbx_keypoint)), o_d1 = res((size_t)V1->n * 32),
+                 o_m1 = res(V1->n), o_f1 = res((size_t)nf1 * 4);
+    struct Off {
+        size_t k2, d2, m2, f2, nd, out, bin, n;
+    };
+    std::vector<Off> o(n);
+    for (int k = 0; k < n; k++) {
+        const orbx_bow_view& V2 = V2s[k];
+        const int nf2 = V2.n_nodes ? V2.node_ptr[V2.n_nodes] : 0;
+        o[k].k2 = res((size_t)V2.n * sizeof(orbx_keypoint));
+        o[k].d2 = res((size_t)V2.n * 32);
+        o[k].m2 = res(V2.n);
+        o[k].f2 = res((size_t)nf2 * 4);
+        o[k].nd = res(nodes[k].size() * sizeof(int4));
+        o[k].out = res((size_t)out_len * 4);
+        o[k].bin = res(out_len);
+        o[k].n = res(4);
+    }
+    const size_t o_jobs = res(sizeof(BowArgs) * (size_t)n);
+    int r = ensure_scratch(ctx, at);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    auto put = [&](size_t off, const void* src, size_t bytes) -> int {
+        if (bytes == 0 || !src) return ORBX_OK;
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + off, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return ORBX_OK;
+    };
+    if ((r = put(o_k1, V1->keys, (size_t)V1->n * sizeof(orbx_keypoint))) ||
+        (r = put(o_d1, V1->desc, (size_t)V1->n * 32)) || (r = put(o_m1, V1->mp, V1->n)) ||
+        (r = put(o_f1, V1->n_nodes ? V1->feat_idx : nullptr, (size_t)nf1 * 4)))
+        return r;
+    std::vector<BowArgs> jobs(n);
+    for (int k = 0; k < n; k++) {
+        const orbx_bow_view& V2 = V2s[k];
+        const int nf2 = V2.n_nodes ? V2.node_ptr[V2.n_nodes] : 0;
+        if ((r = put(o[k].k2, V2.keys, (size_t)V2.n * sizeof(orbx_keypoint))) ||
+            (r = put(o[k].d2, V2.desc, (size_t)V2.n * 32)) || (r = put(o[k].m2, V2.mp, V2.n)) ||
+            (r = put(o[k].f2, V2.n_nodes ? V2.feat_idx : nullptr, (size_t)nf2 * 4)) ||
+            (r = put(o[k].nd, nodes[k].data(), nodes[k].size() * sizeof(int4))))
+            return r;
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].out, 0xFF, (size_t)out_len * 4, ctx->stream));
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].bin, 0xFF, (size_t)out_len, ctx->stream));
+        BowArgs& a = jobs[k];
+        a = BowArgs{};
+        a.s1 = {reinterpret_cast<const orbx_keypoint*>(d + o_k1), d + o_d1, d + o_m1,
+                reinterpret_cast<const int32_t*>(d + o_f1)};
+        a.s2 = {reinterpret_cast<const orbx_keypoint*>(d + o[k].k2), d + o[k].d2, d + o[k].m2,
+                reinterpret_cast<const int32_t*>(d + o[k].f2)};
+        a.nodes = reinterpret_cast<const int4*>(d + o[k].nd);
+        a.n_common = (int)nodes[k].size();
+        a.mode = mode;
+        a.nnratio = nnratio;
+        a.check_ori = check_ori;
+        if (mode == 2) {
+            for (int c = 0; c < 9; c++) a.F12[c] = F12s[9 * k + c];
+            for (int l = 0; l < nlevels; l++) a.sigma2[l] = sigma2s[(size_t)nlevels * k + l];
+        }
+        a.out = reinterpret_cast<int32_t*>(d + o[k].out);
+        a.out_len = out_len;
+        a.bins = reinterpret_cast<signed char*>(d + o[k].bin);
+        a.out_n = reinterpret_cast<int32_t*>(d + o[k].n);
+    }
+    if ((r = put(o_jobs, jobs.data(), sizeof(BowArgs) * (size_t)n))) return r;
+    hipLaunchKernelGGL(k_bow_match_jobs, dim3(n), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const BowArgs*>(d + o_jobs));
+    ORBX_HIP_CHECK(hipGetLastError());
+    for (int k = 0; k < n; k++) {
+        if (out_len)
+            ORBX_HIP_CHECK(hipMemcpyAsync(outs[k], d + o[k].out, (size_t)out_len * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(&n_outs[k], d + o[k].n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
 }  // namespace
 }  // namespace orbx
 
@@ -323,4 +430,18 @@ extern "C" int orbx_search_for_triangulation(orbx_ctx* ctx, const orbx_bow_view*
                                              int32_t* matches12, int* n_matches)
 {
     return run_bow(ctx, KF1, KF2, 2, 0.f, check_ori, F12, sigma2_2, nlevels, matches12, n_matches);
+}
+
+extern "C" int orbx_search_by_bow_kf_batch(orbx_ctx* ctx, const orbx_bow_view* KF1, int n, const orbx_bow_view* KF2s,
+                                           float nnratio, int check_ori, int32_t* const* matches12, int* n_matches)
+{
+    return run_bow_batch(ctx, KF1, n, KF2s, 1, nnratio, check_ori, nullptr, nullptr, 0, matches12, n_matches);
+}
+
+extern "C" int orbx_search_for_triangulation_batch(orbx_ctx* ctx, const orbx_bow_view* KF1, int n,
+                                                   const orbx_bow_view* KF2s, const float* F12s,
+                                                   const float* sigma2_2s, int nlevels, int check_ori,
+                                                   int32_t* const* matches12, int* n_matches)
+{
+    return run_bow_batch(ctx, KF1, n, KF2s, 2, 0.f, check_ori, F12s, sigma2_2s, nlevels, matches12, n_matches);
 }

@@ -657,13 +657,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
                     const orbx_h2 p0 = h2_bytes(dn, k64, sel), p4 = h2_bytes(p4w, k64, sel);
                     const orbx_h2 p8 = h2_bytes(up, k64, sel), p12 = h2_bytes(p12w, k64, sel);
                     // IEEE maximum / minimum: no canonicalising moves (the
-                    // operands are finite)
-                    const orbx_h2 A = h2_min3(__builtin_elementwise_maximum(p0, p4), __builtin_elementwise_maximum(p4, p8),
-                                              __builtin_elementwise_minimum(__builtin_elementwise_maximum(p8, p12),
-                                                                            __builtin_elementwise_maximum(p12, p0)));
-                    const orbx_h2 B = h2_max3(__builtin_elementwise_minimum(p0, p4), __builtin_elementwise_minimum(p4, p8),
-                                              __builtin_elementwise_maximum(__builtin_elementwise_minimum(p8, p12),
-                                                                            __builtin_elementwise_minimum(p12, p0)));
+                    // operands are finite).  A = min over the adjacent pairs
+                    // (0,4), (4,8), (8,12), (12,0) of the pair maximum; by
+                    // distributivity min(max(a, x), max(b, x)) = max(x, min(a, b))
+                    // that is max(min(p4, p12), min(p0, p8)); likewise
+                    // B = max over the pairs of the pair minimum
+                    // = min(max(p4, p12), max(p0, p8)).
+                    const orbx_h2 A = __builtin_elementwise_maximum(__builtin_elementwise_minimum(p4, p12),
+                                                                    __builtin_elementwise_minimum(p0, p8));
+                    const orbx_h2 B = __builtin_elementwise_minimum(__builtin_elementwise_maximum(p4, p12),
+                                                                    __builtin_elementwise_maximum(p0, p8));
                     const orbx_h2 x = __builtin_elementwise_maximum(v - A, B - v) - T1;
                     okw[hf] = ~__builtin_bit_cast(uint32_t, x) & 0x80008000u;
                 }

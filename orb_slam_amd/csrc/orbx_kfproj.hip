@@ -76,9 +76,8 @@ __device__ inline double dot3_cv(const float* a, const float* b)
     return s;
 }
 
-__global__ __launch_bounds__(256) void k_kf_project(KfProjArgs a)
+__device__ inline void kf_project_block(const KfProjArgs& a, uint8_t* smem, int mblock)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     float* tx = reinterpret_cast<float*>(smem);
     float* ty = tx + a.K.n;
     int* tco = reinterpret_cast<int*>(ty + a.K.n);   // cell | octave << 16
@@ -91,7 +90,7 @@ __global__ __launch_bounds__(256) void k_kf_project(KfProjArgs a)
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int m = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int m = mblock * (kBlock / 64) + (threadIdx.x >> 6);
     if (m >= a.nq) return;
     int best_idx = -1, best_dist = INT_MAX;
     do {
@@ -153,6 +152,22 @@ __global__ __launch_bounds__(256) void k_kf_project(KfProjArgs a)
         a.best_idx[m] = best_idx;
         a.best_dist[m] = best_dist;
     }
+}
+
+__global__ __launch_bounds__(256) void k_kf_project(KfProjArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    kf_project_block(a, smem, blockIdx.x);
+}
+
+// Batched form: grid.y = keyframe job (each with its own keypoint table,
+// pose and map points), grid.x = blocks of four map points.
+__global__ __launch_bounds__(256) void k_kf_project_jobs(const KfProjArgs* jobs)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const KfProjArgs& a = jobs[blockIdx.y];
+    if ((int)blockIdx.x * (kBlock / 64) >= a.nq) return;   // uniform per block
+    kf_project_block(a, smem, blockIdx.x);
 }
 
 // MapPoint::ComputeDistinctiveDescriptors, one wavefront per map point.
@@ -489,6 +504,100 @@ extern "C" int orbx_fuse_candidates(orbx_ctx* ctx, const orbx_frame_view* KF, co
         ORBX_HIP_CHECK(hipMemcpyAsync(best_idx, s.base() + o.bi, (size_t)mps->n * 4, hipMemcpyDeviceToHost, ctx->stream));
         ORBX_HIP_CHECK(hipMemcpyAsync(best_dist, s.base() + o.bd, (size_t)mps->n * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
+// SearchInNeighbors' first loop (src/LocalMapping.cc:403-416: Fuse of the
+// current keyframe's map points into every target keyframe) in one upload,
+// one launch and one readback.  Map-point views that are the same object are
+// uploaded once.
+extern "C" int orbx_fuse_candidates_batch(orbx_ctx* ctx, int n_kf, const orbx_frame_view* KFs, const float* cams,
+                                          const orbx_mappoint_view* const* mps, const float* Ts, int sim3, float th,
+                                          int32_t* const* best_idx, int32_t* const* best_dist)
+{
+    if (!ctx || n_kf < 0 || (n_kf > 0 && (!KFs || !cams || !mps || !Ts || !best_idx || !best_dist))) return ORBX_ERR_ARG;
+    for (int k = 0; k < n_kf; k++)
+        if (!valid_kf(&KFs[k]) || !valid_mps(mps[k], true) || (mps[k]->n > 0 && (!best_idx[k] || !best_dist[k])))
+            return ORBX_ERR_ARG;
+    if (n_kf == 0) return ORBX_OK;
+    ctx_enter(ctx);
+    Staging s{ctx};
+    struct Off {
+        size_t kp, kd, pos, nrm, dmin, dmax, qd, bi, bd;
+    };
+    std::vector<Off> o(n_kf);
+    int max_n = 1, max_q = 0;
+    for (int k = 0; k < n_kf; k++) {
+        const orbx_frame_view* K = &KFs[k];
+        const orbx_mappoint_view* P = mps[k];
+        o[k].kp = s.res((size_t)K->n * sizeof(orbx_keypoint), K->keys_un);
+        o[k].kd = s.res((size_t)K->n * 32, K->desc);
+        int same = -1;
+        for (int j = 0; j < k && same < 0; j++)
+            if (mps[j] == P) same = j;
+        if (same >= 0) {   // the same map points: reuse their upload
+            o[k].pos = o[same].pos;
+            o[k].nrm = o[same].nrm;
+            o[k].dmin = o[same].dmin;
+            o[k].dmax = o[same].dmax;
+            o[k].qd = o[same].qd;
+        } else {
+            o[k].pos = s.res((size_t)P->n * 12, P->pos);
+            o[k].nrm = s.res((size_t)P->n * 12, P->normal);
+            o[k].dmin = s.res((size_t)P->n * 4, P->min_dist);
+            o[k].dmax = s.res((size_t)P->n * 4, P->max_dist);
+            o[k].qd = s.res((size_t)P->n * 32, P->desc);
+        }
+        o[k].bi = s.res((size_t)P->n * 4);
+        o[k].bd = s.res((size_t)P->n * 4);
+        max_n = std::max(max_n, K->n);
+        max_q = std::max(max_q, P->n);
+    }
+    const size_t o_jobs = s.res(sizeof(KfProjArgs) * (size_t)n_kf);
+    std::vector<KfProjArgs> jobs(n_kf);
+    uint8_t* d = nullptr;
+    int r = ensure_scratch(ctx, s.at);
+    if (r != ORBX_OK) return r;
+    d = s.base();
+    for (int k = 0; k < n_kf; k++) {
+        const orbx_frame_view* K = &KFs[k];
+        KfProjArgs& a = jobs[k];
+        a = KfProjArgs{};
+        a.K = kf_dev(K, d, o[k].kp, o[k].kd);
+        a.nlevels = K->nlevels;
+        a.scales[0] = 1.0f;
+        for (int l = 1; l < K->nlevels; l++) a.scales[l] = a.scales[l - 1] * K->scale_factor;   // src/Frame.cc:98-102
+        a.nq = mps[k]->n;
+        a.pos = reinterpret_cast<const float*>(d + o[k].pos);
+        a.normal = reinterpret_cast<const float*>(d + o[k].nrm);
+        a.dmin = reinterpret_cast<const float*>(d + o[k].dmin);
+        a.dmax = reinterpret_cast<const float*>(d + o[k].dmax);
+        a.qdesc = d + o[k].qd;
+        a.qvalid = nullptr;
+        a.best_idx = reinterpret_cast<int32_t*>(d + o[k].bi);
+        a.best_dist = reinterpret_cast<int32_t*>(d + o[k].bd);
+        for (int c = 0; c < 4; c++) a.cam[c] = cams[4 * k + c];
+        pose_parts(Ts + 16 * k, sim3, a.Ra, a.ta, a.Ow);
+        a.two_stage = 0;
+        a.mode = sim3 ? 1 : 0;
+        a.th = th;
+    }
+    s.puts.push_back({o_jobs, {jobs.data(), sizeof(KfProjArgs) * (size_t)n_kf}});
+    if ((r = s.upload()) != ORBX_OK) return r;
+    if (max_q > 0) {
+        const int per = kBlock / 64;
+        hipLaunchKernelGGL(k_kf_project_jobs, dim3((max_q + per - 1) / per, n_kf), dim3(kBlock), (size_t)max_n * 12,
+                           ctx->stream, reinterpret_cast<const KfProjArgs*>(d + o_jobs));
+        ORBX_HIP_CHECK(hipGetLastError());
+    }
+    for (int k = 0; k < n_kf; k++)
+        if (mps[k]->n) {
+            ORBX_HIP_CHECK(hipMemcpyAsync(best_idx[k], d + o[k].bi, (size_t)mps[k]->n * 4, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+            ORBX_HIP_CHECK(hipMemcpyAsync(best_dist[k], d + o[k].bd, (size_t)mps[k]->n * 4, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+        }
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return ORBX_OK;
 }
