@@ -18,6 +18,7 @@
 //
 // All integer / byte work; the bounds are HBM or latency, never MFMA.
 #include <algorithm>
+#include <type_traits>
 
 #include "orbx_device.h"
 #include "orbx_internal.h"
@@ -526,11 +527,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     constexpr int kBlock = kThreads, kWaves = kThreads / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratchN<kWaves> bs;
-    constexpr int kCandRing = 256;           // per-wave ring (a full iteration's 256 fit after a drain)
-    constexpr int kUnitCap = kWaves * kCandRing * 2;   // u16 NMS unit list aliasing the rings
-    __shared__ __attribute__((aligned(16))) uint32_t cand[kWaves][kCandRing];
-    uint16_t* ulist = reinterpret_cast<uint16_t*>(&cand[0][0]);
+    // Per-wave queue of compass survivors (tile positions): u16 for the
+    // templated pitches (the host sends tiles over 64 KB to kP = 0), u32 for
+    // kP = 0.  Linear, not a ring: after each scoring round the < 128 left
+    // over move to the front, so an iteration's <= 256 new entries always fit.
+    using QEntry = typename std::conditional<kP != 0, uint16_t, uint32_t>::type;
+    constexpr int kQueue = 128 + 256;
+    constexpr int kQueueWords = kWaves * kQueue * (int)sizeof(QEntry) / 4;
+    constexpr int kUnitCap = 2 * kQueueWords;   // u16 NMS unit list aliasing the queues
+    __shared__ __attribute__((aligned(16))) uint32_t qbuf[kQueueWords];
+    uint16_t* ulist = reinterpret_cast<uint16_t*>(qbuf);
     const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    QEntry* cand = reinterpret_cast<QEntry*>(qbuf) + wv * kQueue;
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
     if (!C.valid) {
@@ -594,21 +602,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     // alignment shift, (c_hi >> 2) - q0 + 1 would go negative)
     const int q0 = c_lo >> 2, nqe = c_hi >= c_lo ? (c_hi >> 2) - q0 + 1 : 0;
     const int q_last = q0 + nqe - 1;
-    const int m_first = 0xF & ~((1 << (c_lo & 3)) - 1);  // pixels j >= c_lo & 3 of dword q0
-    const int m_last = (1 << ((c_hi & 3) + 1)) - 1;      // pixels j <= c_hi & 3 of the last dword
+    const int j_lo = c_lo & 3, j_hi = c_hi & 3;           // pixels j >= j_lo of dword q0, j <= j_hi of q_last
     const int nunits = max(hy - 6, 0) * nqe;
     const uint32_t k64 = 0x64646464u;
     // S' map at threshold tmin: S' = S where S >= tmin, else 0
     auto score_pass = [&](const int tmin) {
-        // per-wave ring of compass survivors (tile position | 3 << 16),
-        // scored 128 at a time (two per lane) with every lane busy
-        int qh = 0, qt = 0;
+        // per-wave queue cand[0, qt) of compass survivors, scored 128 at a
+        // time (two per lane) with every lane busy
+        int qt = 0;
         auto set_nz = [&](int p) { atomicOr(&nz[p >> 7], 1u << ((p >> 2) & 31)); };
-        // cw = position | flags << 16, flags 0 = no candidate (a is filled before b)
-        auto score_pair = [&](uint32_t ca, uint32_t cb) {
-            if (!(ca >> 16)) return;
-            const int pa = (int)(ca & 0xFFFF);
-            const int pb = (cb >> 16) ? (int)(cb & 0xFFFF) : pa;
+        auto score_pair = [&](int pa, int pb, bool has_a, bool has_b) {
+            if (!has_a) return;
             int Sa, Sb;
             fast_arc2(tile, pa, pb, P, Sa, Sb);
             Sa -= 1;
@@ -617,15 +621,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
                 sm[pa] = (uint8_t)Sa;
                 set_nz(pa);
             }
-            if ((cb >> 16) && Sb >= tmin) {
+            if (has_b && Sb >= tmin) {
                 sm[pb] = (uint8_t)Sb;
                 set_nz(pb);
             }
-        };
-        auto score_partial = [&]() {   // the qt - qh < 128 queued candidates
-            const int nq_ = qt - qh;
-            score_pair(lane < nq_ ? cand[wv][(qh + lane) & (kCandRing - 1)] : 0u,
-                       lane + 64 < nq_ ? cand[wv][(qh + 64 + lane) & (kCandRing - 1)] : 0u);
         };
         // pass <=> max(v - A, B - v) >= tmin + 1 with A = min of the four
         // adjacent compass-pair maxima, B = max of the pair minima (exact
@@ -636,7 +635,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
             const int u = u0 + lane;
             const int r = 3 + cw_.r, q = q0 + cw_.q;
-            int mask = 0;
+            // per pixel j: the sign bit of x_j = max(v - A, B - v) - tmin - 1
+            // is set where the pixel fails (even half: j = 0, 2; odd: 1, 3)
+            uint32_t xw0 = 0xBC00BC00u, xw1 = 0xBC00BC00u;   // -1.0: fails both tests (not -0)
             if (u < nunits) {
                 const uint32_t* row = tile32 + r * nq + q;
                 const uint32_t mid = row[0];
@@ -648,7 +649,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
                 // 4 pixels at once: even / odd bytes as two packed fp16 halves
                 const uint32_t p4w = __builtin_amdgcn_alignbyte(hi, mid, 3);    // bytes j+3
                 const uint32_t p12w = __builtin_amdgcn_alignbyte(mid, lo, 1);   // bytes j-3
-                uint32_t okw[2];   // [half] sign bits of pixels failing both tests
+                uint32_t xw[2];
 #pragma unroll
                 for (int hf = 0; hf < 2; hf++) {
                     const uint32_t sel = hf ? 0x04030401u : 0x04020400u;   // bytes 1,3 or 0,2 | 0x64
@@ -668,47 +669,67 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
                     const orbx_h2 B = __builtin_elementwise_minimum(__builtin_elementwise_maximum(p4, p12),
                                                                     __builtin_elementwise_maximum(p0, p8));
                     const orbx_h2 x = __builtin_elementwise_maximum(v - A, B - v) - T1;
-                    okw[hf] = ~__builtin_bit_cast(uint32_t, x) & 0x80008000u;
+                    xw[hf] = __builtin_bit_cast(uint32_t, x);
                 }
-                // pixel j -> bit j (even half: j = 0, 2; odd half: j = 1, 3)
-                mask = (int)(((okw[0] >> 15) & 1) | ((okw[1] >> 14) & 2) | ((okw[0] >> 29) & 4) | ((okw[1] >> 28) & 8));
-                // interior columns only (q0 and the last dword are partial)
-                mask &= (q == q0 ? m_first : 0xF) & (q == q_last ? m_last : 0xF);
+                xw0 = xw[0];
+                xw1 = xw[1];
             }
-            const int cnt = __popc(mask);
-            const int incl = wave_inclusive_scan(cnt);
-            const int ntot = __builtin_amdgcn_readlane(incl, 63);
+            // pass flags as lane masks (bit 15 / 31 clear: a 16-bit and a
+            // 32-bit signed compare each); the partial dwords q0 and q_last
+            // drop the pixels outside the interior columns (uniform j tests;
+            // bitwise on the lane masks, no short-circuit branches)
+            const bool at_q0 = q == q0, at_ql = q == q_last;
+            const bool cut0 = at_q0 & (j_lo > 0), cut1 = (at_q0 & (j_lo > 1)) | (at_ql & (j_hi < 1));
+            const bool cut2 = (at_q0 & (j_lo > 2)) | (at_ql & (j_hi < 2)), cut3 = at_ql & (j_hi < 3);
+            // (low halves as fp16 >= 0: no -0 or NaN arises from these exact
+            // integer differences)
+            const bool ok0 = (__builtin_bit_cast(orbx_h2, xw0).x >= (_Float16)0) & !cut0;
+            const bool ok1 = (__builtin_bit_cast(orbx_h2, xw1).x >= (_Float16)0) & !cut1;
+            const bool ok2 = ((int32_t)xw0 >= 0) & !cut2, ok3 = ((int32_t)xw1 >= 0) & !cut3;
+            const uint64_t b0 = __builtin_amdgcn_ballot_w64(ok0), b1 = __builtin_amdgcn_ballot_w64(ok1);
+            const uint64_t b2 = __builtin_amdgcn_ballot_w64(ok2), b3 = __builtin_amdgcn_ballot_w64(ok3);
+            const int n0 = __popcll(b0), n1 = __popcll(b1), n2 = __popcll(b2);
+            const int ntot = n0 + n1 + n2 + __popcll(b3);
 #ifdef ORBX_FAST_PROFILE
             if (lane == 0) FP_ADD(10 + (tmin < 10), ntot);
             if (lane == 0) FP_ADD(12, 1);
 #endif
-            if (qt - qh + ntot > kCandRing) {   // rare (> 50 % survivors): drain the partial batch
-                score_partial();
-                qh = qt;
+            // plane-major order: each plane's survivors at their lane rank
+            // (mbcnt, which adds the plane's start) after the earlier planes'
+            const int pbase = r * P + 4 * q;
+            auto slot = [&](uint64_t bm, int start) {
+                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bm, (uint32_t)start));
+            };
+            if (ok0) cand[slot(b0, qt)] = (QEntry)pbase;
+            if (ok1) cand[slot(b1, qt + n0)] = (QEntry)(pbase + 1);
+            if (ok2) cand[slot(b2, qt + n0 + n1)] = (QEntry)(pbase + 2);
+            if (ok3) cand[slot(b3, qt + n0 + n1 + n2)] = (QEntry)(pbase + 3);
+            qt = __builtin_amdgcn_readfirstlane(qt + ntot);   // wave-uniform
+            if (qt >= 128) {   // uniform: score full batches, move the rest to the front
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                int qh = 0;
+                for (; qt - qh >= 128; qh += 128)
+                    score_pair(cand[qh + lane], cand[qh + 64 + lane], true, true);
+                const int rest = qt - qh;   // < 128
+                const QEntry e0 = lane < rest ? cand[qh + lane] : (QEntry)0;
+                const QEntry e1 = lane + 64 < rest ? cand[qh + 64 + lane] : (QEntry)0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < rest) cand[lane] = e0;
+                if (lane + 64 < rest) cand[lane + 64] = e1;
+                qt = __builtin_amdgcn_readfirstlane(rest);
             }
-            int w = qt + incl - cnt;
-            if (mask) {
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if ((mask >> j) & 1) cand[wv][(w++) & (kCandRing - 1)] = (uint32_t)(r * P + 4 * q + j) | (3u << 16);
-            }
-            qt += ntot;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // score only full batches (two per lane); the rest waits in the ring
-            while (qt - qh >= 128) {
-                score_pair(cand[wv][(qh + lane) & (kCandRing - 1)], cand[wv][(qh + 64 + lane) & (kCandRing - 1)]);
-                qh += 128;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // no fence here: the next iteration appends at >= qt (the moved
+            // rest lies below it), and the queue is read only after the
+            // fence above
         }
-        if (qt > qh) score_partial();
+        if (qt > 0)   // the last < 128
+            score_pair(lane < qt ? (int)cand[lane] : 0, lane + 64 < qt ? (int)cand[lane + 64] : 0, lane < qt,
+                       lane + 64 < qt);
     };
     // non-max suppression over the S' map: a pixel is kept if its S' beats
     // all 8 neighbours' S'.  Only dwords whose `nz` bit is set can keep
@@ -1610,10 +1631,13 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 const int bytes = fast_tile_bytes(hmax, P);
                 hipLaunchKernelGGL(kern, grid, dim3(threads), fast_lds_bytes(bytes), st, x, bytes);
             };
-            if (wmax <= 96) fast(k_fast_cells<96>, 96, 256);
-            else if (wmax <= 144) fast(k_fast_cells<144>, 144, 256);
-            else if (wmax <= 208) fast(k_fast_cells<208>, 208, 256);
-            else if (wmax <= 336) fast(k_fast_cells<336, kFastWideThreads>, 336, kFastWideThreads);
+            // the templated instances queue u16 tile positions: tiles of up
+            // to 64 KB (taller ones take the runtime-pitch instance)
+            auto fits = [&](int P) { return wmax <= P && (long)hmax * P <= 65536; };
+            if (fits(96)) fast(k_fast_cells<96>, 96, 256);
+            else if (fits(144)) fast(k_fast_cells<144>, 144, 256);
+            else if (fits(208)) fast(k_fast_cells<208>, 208, 256);
+            else if (fits(336)) fast(k_fast_cells<336, kFastWideThreads>, 336, kFastWideThreads);
             else {
                 const int bytes = fast_tile_bytes(1, g.max_tile_bytes);
                 hipLaunchKernelGGL((k_fast_cells<0, kFastWideThreads>), grid, dim3(kFastWideThreads), fast_lds_bytes(bytes),
