@@ -122,12 +122,12 @@ def native_oracle():
     so = nat / "liborbx_ref_native.so"
     stamp = nat / "HOST"
     try:
-        if not so.exists() or not stamp.exists() or stamp.read_text() != sig:
-            if nat.exists():
-                subprocess.run(["rm", "-rf", str(nat)], check=True)
-            subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j16", "native"], check=True,
-                           capture_output=True, timeout=240)
-            stamp.write_text(sig)
+        if nat.exists() and (not stamp.exists() or stamp.read_text() != sig):   # built for another CPU
+            subprocess.run(["rm", "-rf", str(nat)], check=True)
+        # incremental: also picks up oracle sources newer than the objects
+        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "-j16", "native"], check=True,
+                       capture_output=True, timeout=240)
+        stamp.write_text(sig)
         return oracle_lib.load("native"), "oracle/_native/liborbx_ref_native.so (g++ -O3 -march=native, built on this host)"
     except Exception as e:   # noqa: BLE001 -- a baseline, not the product: say what was timed
         return oracle_lib.load(), f"oracle/liborbx_ref.so (g++ -O3 -march=x86-64-v3; native build failed: {e!r:.80})"

@@ -126,6 +126,19 @@ int orbx_dev_extract(orbx_ctx* ctx, int first, int count);
  * after the call (DESIGN.md section 4 has the measured effect). */
 int orbx_set_fp_contract(orbx_ctx* ctx, int enable);
 int orbx_get_fp_contract(const orbx_ctx* ctx);
+/* libstdc++ era of retainBest's std::nth_element (KeyPointsFilter::retainBest,
+ * called at src/ORBextractor.cc:683, :699).  The surviving keypoints and their
+ * order are nth_element's permutation, and libstdc++ changed its introselect
+ * pivot step in GCC 4.9 (PR libstdc++/58437):
+ *   ORBX_NTH_PIVOT_GCC49 (0, default): median of (first + 1, mid, last - 1)
+ *     swapped into first -- GCC >= 4.9;
+ *   ORBX_NTH_PIVOT_GCC48 (1): median of (first, mid, last - 1) moved to
+ *     first -- GCC 4.6 .. 4.8, the compilers of the reference's era.
+ * Applies to extractions launched after the call (DESIGN.md section 4 has the
+ * measured effect). */
+enum { ORBX_NTH_PIVOT_GCC49 = 0, ORBX_NTH_PIVOT_GCC48 = 1 };
+int orbx_set_nth_pivot(orbx_ctx* ctx, int mode);
+int orbx_get_nth_pivot(const orbx_ctx* ctx);
 /* enable: 0 = one stream; 1 = split with the default three parts;
  * 2..4 = split, and the asynchronous extract_match pipeline runs its batch
  * in that many parts on as many streams, part i released by part i-1's

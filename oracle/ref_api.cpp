@@ -6,6 +6,7 @@
 #include "ref_common.h"
 #include "../include/orbx.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <exception>
@@ -149,6 +150,36 @@ int orbx_ref_resize(const uint8_t* src, int sstep, int sw, int sh, uint8_t* dst,
     } catch (const std::exception&) {
         return ORBX_ERR_UNSUPPORTED;
     }
+}
+
+/* libstdc++ era of retainBest's std::nth_element pivot step
+ * (ref_extract.cpp): 0 = GCC >= 4.9 (this image's), 1 = GCC 4.6 .. 4.8 */
+int orbx_ref_set_nth_pivot(int mode)
+{
+    if (mode != NTH_PIVOT_GCC49 && mode != NTH_PIVOT_GCC48) return ORBX_ERR_ARG;
+    set_nth_pivot(mode);
+    return ORBX_OK;
+}
+int orbx_ref_get_nth_pivot(void) { return get_nth_pivot(); }
+
+/* Permutation nth_element(a, a + nth, a + n, greater) leaves on n float
+ * keys: the restatement with the given pivot era (std_impl = 0), or this
+ * image's std::nth_element (std_impl = 1), for checking the restatement. */
+static bool kp_response_greater(const KeyPoint& a, const KeyPoint& b) { return a.response > b.response; }
+
+int orbx_ref_nth_element_perm(const float* keys, int n, int nth, int mode, int std_impl, int32_t* perm)
+{
+    if (n < 0 || nth < 0 || nth > n) return ORBX_ERR_ARG;
+    std::vector<KeyPoint> v(n);
+    for (int i = 0; i < n; i++) {
+        std::memset(&v[i], 0, sizeof(KeyPoint));
+        v[i].response = keys[i];
+        v[i].class_id = i;
+    }
+    if (std_impl) std::nth_element(v.begin(), v.begin() + nth, v.end(), kp_response_greater);
+    else libstdcxx_nth_element(v.data(), v.data() + nth, v.data() + n, kp_response_greater, mode);
+    for (int i = 0; i < n; i++) perm[i] = v[i].class_id;
+    return ORBX_OK;
 }
 
 // retainBest over a list of responses; writes the surviving original indices.

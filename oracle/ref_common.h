@@ -78,6 +78,12 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
 int  cv24_corner_score16(const uint8_t* ptr, const int pixel[25], int threshold);
 void cv24_gaussian_blur7_roi(const PaddedImage& src, PaddedImage& dst);
 void cv24_retain_best(std::vector<KeyPoint>& kps, int n_points);
+// libstdc++ nth_element restated with either era's pivot step (ref_extract.cpp)
+enum { NTH_PIVOT_GCC49 = 0, NTH_PIVOT_GCC48 = 1 };
+void set_nth_pivot(int mode);
+int get_nth_pivot();
+template <class T, class Less>
+void libstdcxx_nth_element(T* first, T* nth, T* last, Less less, int mode);
 // ---- reference-compiled float expressions (ref_orbsites.cpp; built with
 //      and without FMA contraction) ----
 void cv24_harris_responses(const uint8_t* img, int step, std::vector<KeyPoint>& pts, int blockSize, float harris_k);

@@ -293,9 +293,165 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
     }
 }
 
+// std::nth_element as libstdc++ implements it (bits/stl_algo.h
+// __introselect, __heap_select, __insertion_sort, __unguarded_partition),
+// restated so the pivot step can follow either era of the library:
+//   NTH_PIVOT_GCC49 (default): __move_median_to_first(first, first + 1, mid,
+//       last - 1) -- the median of those three swapped into *first (GCC >= 4.9,
+//       PR libstdc++/58437; the GCC 11.4 of this image);
+//   NTH_PIVOT_GCC48: __move_median_first(first, mid, last - 1) -- the median
+//       of (first, mid, last - 1) moved to *first, *first left in place when
+//       it is the median (GCC 4.6 .. 4.8, the compilers of the reference's
+//       era: Ubuntu 12.04 / 14.04).
+// Everything else (depth limit 2 floor(log2 n), the Hoare partition from
+// first + 1, heap select, insertion sort below 4 elements) is common to both.
+// With NTH_PIVOT_GCC49 it is checked against this image's std::nth_element
+// (orbx_ref_nth_element_check, tests/test_sort_era.py).
+// ---------------------------------------------------------------------------
+static int g_nth_pivot = NTH_PIVOT_GCC49;
+void set_nth_pivot(int mode) { g_nth_pivot = mode; }
+int get_nth_pivot() { return g_nth_pivot; }
+
+namespace {
+template <class T, class Less>
+void adjust_heap(T* first, long hole, long len, T value, Less less)
+{
+    const long top = hole;
+    long child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (less(first[child], first[child - 1])) child--;
+        first[hole] = first[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        first[hole] = first[child - 1];
+        hole = child - 1;
+    }
+    long parent = (hole - 1) / 2;   // __push_heap
+    while (hole > top && less(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+template <class T, class Less>
+void heap_select(T* first, T* middle, T* last, Less less)
+{
+    const long len = middle - first;
+    if (len >= 2)   // __make_heap
+        for (long parent = (len - 2) / 2;; parent--) {
+            adjust_heap(first, parent, len, first[parent], less);
+            if (parent == 0) break;
+        }
+    for (T* i = middle; i < last; ++i)
+        if (less(*i, *first)) {   // __pop_heap(first, middle, i)
+            T value = *i;
+            *i = *first;
+            adjust_heap(first, 0, len, value, less);
+        }
+}
+
+template <class T, class Less>
+void insertion_sort(T* first, T* last, Less less)
+{
+    if (first == last) return;
+    for (T* i = first + 1; i != last; ++i) {
+        T val = *i;
+        if (less(val, *first)) {
+            for (T* k = i; k != first; --k) *k = *(k - 1);
+            *first = val;
+        } else {   // __unguarded_linear_insert
+            T* k = i;
+            while (less(val, *(k - 1))) {
+                *k = *(k - 1);
+                --k;
+            }
+            *k = val;
+        }
+    }
+}
+
+template <class T, class Less>
+T* unguarded_partition(T* first, T* last, T* pivot, Less less)
+{
+    while (true) {
+        while (less(*first, *pivot)) ++first;
+        --last;
+        while (less(*pivot, *last)) --last;
+        if (!(first < last)) return first;
+        std::swap(*first, *last);
+        ++first;
+    }
+}
+
+template <class T, class Less>
+void pivot_to_first(T* first, T* last, Less less, int mode)
+{
+    T* mid = first + (last - first) / 2;
+    if (mode == NTH_PIVOT_GCC48) {   // __move_median_first(first, mid, last - 1)
+        T *a = first, *b = mid, *c = last - 1;
+        if (less(*a, *b)) {
+            if (less(*b, *c)) std::swap(*a, *b);
+            else if (less(*a, *c)) std::swap(*a, *c);
+        } else if (less(*a, *c)) {
+            return;
+        } else if (less(*b, *c)) {
+            std::swap(*a, *c);
+        } else {
+            std::swap(*a, *b);
+        }
+        return;
+    }
+    // __move_median_to_first(first, first + 1, mid, last - 1)
+    T *a = first + 1, *b = mid, *c = last - 1, *t;
+    if (less(*a, *b)) {
+        if (less(*b, *c)) t = b;
+        else if (less(*a, *c)) t = c;
+        else t = a;
+    } else if (less(*a, *c)) {
+        t = a;
+    } else if (less(*b, *c)) {
+        t = c;
+    } else {
+        t = b;
+    }
+    std::swap(*first, *t);
+}
+}  // namespace
+
+template <class T, class Less>
+void libstdcxx_nth_element(T* first, T* nth, T* last, Less less, int mode)
+{
+    if (first == last || nth == last) return;
+    long depth = 0;
+    for (long n = last - first; n > 1; n >>= 1) depth++;   // __lg
+    depth *= 2;
+    while (last - first > 3) {
+        if (depth == 0) {
+            heap_select(first, nth + 1, last, less);
+            std::swap(*first, *nth);
+            return;
+        }
+        --depth;
+        pivot_to_first(first, last, less, mode);
+        T* cut = unguarded_partition(first + 1, last, first, less);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    insertion_sort(first, last, less);
+}
+template void libstdcxx_nth_element<KeyPoint>(KeyPoint*, KeyPoint*, KeyPoint*,
+                                              bool (*)(const KeyPoint&, const KeyPoint&), int);
+
+static bool response_greater(const KeyPoint& a, const KeyPoint& b) { return a.response > b.response; }
+
 // KeyPointsFilter::retainBest (OpenCV 2.4 features2d/src/keypoint.cpp).
 // Called at src/ORBextractor.cc:683 and :699.  The surviving set and order is
-// the libstdc++ introselect permutation (std::nth_element).
+// the libstdc++ introselect permutation (std::nth_element, era as above).
 // ---------------------------------------------------------------------------
 void cv24_retain_best(std::vector<KeyPoint>& kps, int n_points)
 {
@@ -304,8 +460,8 @@ void cv24_retain_best(std::vector<KeyPoint>& kps, int n_points)
             kps.clear();
             return;
         }
-        std::nth_element(kps.begin(), kps.begin() + n_points, kps.end(),
-                         [](const KeyPoint& a, const KeyPoint& b) { return a.response > b.response; });
+        libstdcxx_nth_element(kps.data(), kps.data() + n_points, kps.data() + kps.size(), response_greater,
+                              g_nth_pivot);
         const float ambiguous = kps[n_points - 1].response;
         auto newEnd = std::partition(kps.begin() + n_points, kps.end(),
                                      [ambiguous](const KeyPoint& k) { return k.response >= ambiguous; });

@@ -75,6 +75,8 @@ def _declare(L):
         "orbx_dev_set_async_match": ([vp, i], i),
         "orbx_set_fp_contract": ([vp, i], i),
         "orbx_get_fp_contract": ([vp], i),
+        "orbx_set_nth_pivot": ([vp, i], i),
+        "orbx_get_nth_pivot": ([vp], i),
         "orbx_dev_set_pyramid_mode": ([vp, i], i),
         "orbx_dev_pyramid_fused": ([vp], i),
         "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
@@ -225,6 +227,11 @@ class Context:
         sample coordinates, Harris response) as a reference build with GCC's
         FMA contraction does (orbx_set_fp_contract)."""
         _check(lib().orbx_set_fp_contract(self._h, int(enable)), "orbx_set_fp_contract")
+
+    def set_nth_pivot(self, mode):
+        """retainBest's std::nth_element pivot step as libstdc++ >= 4.9 (0,
+        default) or GCC 4.6 .. 4.8 (1) implements it (orbx_set_nth_pivot)."""
+        _check(lib().orbx_set_nth_pivot(self._h, int(mode)), "orbx_set_nth_pivot")
 
     def set_async_match(self, enable):
         """Queue extract_match's matching behind the extraction on an internal

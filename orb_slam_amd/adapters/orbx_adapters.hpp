@@ -108,6 +108,12 @@ public:
     // Match a reference binary built with FMA contraction (GCC -O3
     // -march=native on an FMA host; orbx_set_fp_contract).
     void SetFpContract(bool enable) { check(orbx_set_fp_contract(ctx_.get(), enable ? 1 : 0), "SetFpContract"); }
+    // retainBest's std::nth_element as the libstdc++ the reference was built
+    // against implements it: gcc48 = GCC 4.6 .. 4.8 (orbx_set_nth_pivot).
+    void SetNthElementEra(bool gcc48)
+    {
+        check(orbx_set_nth_pivot(ctx_.get(), gcc48 ? ORBX_NTH_PIVOT_GCC48 : ORBX_NTH_PIVOT_GCC49), "SetNthElementEra");
+    }
 
 private:
     int nfeatures_;

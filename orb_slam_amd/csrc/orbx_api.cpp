@@ -400,6 +400,16 @@ int orbx_set_fp_contract(orbx_ctx* ctx, int enable)
 
 int orbx_get_fp_contract(const orbx_ctx* ctx) { return ctx ? ctx->fp_contract : ORBX_ERR_ARG; }
 
+int orbx_set_nth_pivot(orbx_ctx* ctx, int mode)
+{
+    if (!ctx || (mode != ORBX_NTH_PIVOT_GCC49 && mode != ORBX_NTH_PIVOT_GCC48)) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->nth_pivot = mode;
+    return ORBX_OK;
+}
+
+int orbx_get_nth_pivot(const orbx_ctx* ctx) { return ctx ? ctx->nth_pivot : ORBX_ERR_ARG; }
+
 int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
 {
     if (!ctx) return ORBX_ERR_ARG;

@@ -345,6 +345,40 @@ __device__ inline void move_median_to_first(E* a, int result, int x, int y, int 
     a[t] = tmp;
 }
 
+// GCC 4.6 .. 4.8's __move_median_first(a, b, c): the median of (a, b, c)
+// moved to a, a left in place when it is the median (before PR
+// libstdc++/58437; the reference's era).
+template <typename E>
+__device__ inline void move_median_first_gcc48(E* a, int x, int y, int z)
+{
+    int t;
+    if (kp_greater(a[x], a[y])) {
+        if (kp_greater(a[y], a[z])) t = y;
+        else if (kp_greater(a[x], a[z])) t = z;
+        else return;
+    } else if (kp_greater(a[x], a[z])) {
+        return;
+    } else if (kp_greater(a[y], a[z])) {
+        t = z;
+    } else {
+        t = y;
+    }
+    const E tmp = a[x];
+    a[x] = a[t];
+    a[t] = tmp;
+}
+
+// introselect's pivot step for [first, last): pivot_mode 0 = libstdc++ >=
+// 4.9 (median of first + 1, mid, last - 1 swapped to first), 1 = GCC 4.6 ..
+// 4.8 (median of first, mid, last - 1 moved to first); orbx_set_nth_pivot.
+template <typename E>
+__device__ inline void nth_pivot_step(E* a, int first, int last, int pivot_mode)
+{
+    const int mid = first + (last - first) / 2;
+    if (pivot_mode == 1) move_median_first_gcc48(a, first, mid, last - 1);
+    else move_median_to_first(a, first, first + 1, mid, last - 1);
+}
+
 // Partition [lo+1, hi) around the pivot key at a[lo]; returns the cut.
 // pos: scratch of 2 * ((hi-lo)/2 + 1) ints.  Must be called by all threads.
 __device__ inline int block_hoare_partition(uint32_t* a, int lo, int hi, int* pos, BlockScratch& s)
@@ -420,7 +454,7 @@ __device__ inline int floor_log2(int n)
 
 // std::nth_element(a, a + nth, a + n, greater-by-response).
 // pos: scratch of n + 4 ints.
-__device__ inline void block_nth_element(uint32_t* a, int n, int nth, int* pos, BlockScratch& s)
+__device__ inline void block_nth_element(uint32_t* a, int n, int nth, int* pos, BlockScratch& s, int pivot_mode = 0)
 {
     if (n == 0 || nth == n) return;
     int first = 0, last = n;
@@ -437,7 +471,7 @@ __device__ inline void block_nth_element(uint32_t* a, int n, int nth, int* pos, 
             return;
         }
         --depth;
-        if (threadIdx.x == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        if (threadIdx.x == 0) nth_pivot_step(a, first, last, pivot_mode);
         __syncthreads();
         const int cut = block_hoare_partition(a, first, last, pos, s);
         if (cut <= nth) first = cut;
@@ -559,7 +593,7 @@ __device__ inline int wave_hoare_partition(E* a, int lo, int hi, int* pos)
 // std::nth_element(a, a + nth, a + n, greater-by-response), one wave.
 // kGlobal: list and scratch in global memory (lists too long for LDS).
 template <bool kGlobal = false, typename E>
-__device__ inline void wave_nth_element(E* a, int n, int nth, int* pos)
+__device__ inline void wave_nth_element(E* a, int n, int nth, int* pos, int pivot_mode = 0)
 {
     if (n == 0 || nth == n) return;
     const int lane = threadIdx.x & 63;
@@ -577,7 +611,7 @@ __device__ inline void wave_nth_element(E* a, int n, int nth, int* pos)
             return;
         }
         --depth;
-        if (lane == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        if (lane == 0) nth_pivot_step(a, first, last, pivot_mode);
         nth_sync<kGlobal>();
         const int cut = wave_hoare_partition<kGlobal>(a, first, last, pos);
         if (cut <= nth) first = cut;

@@ -82,6 +82,7 @@ struct ExtractArgs {
     uint64_t* level_keys64;         // HARRIS_SCORE: Harris-keyed level lists (as level_keys)
     int harris;                     // scoreType == HARRIS_SCORE
     int fp_contract;                // orbx_set_fp_contract: FMA-contracted reference build
+    int nth_pivot;                  // orbx_set_nth_pivot: retainBest's libstdc++ era
     long long frame_pyr_bytes;
     int first_slot;
     int w, h;
@@ -1075,12 +1076,12 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     if (n > k && n <= kRetainCellCap) {
         stage_to_lds<8>(list, n, lane, 64, [&](int i) { return src[i]; });
         lds_wave_sync();
-        wave_nth_element(list, n, k, pos);
+        wave_nth_element(list, n, k, pos, a.nth_pivot);
         for (int i = lane; i < take; i += 64) dst[i] = list[i];
     } else if (n > k) {
         // long list: replay in place in global memory
         int* gpos = a.retain_scratch + (size_t)f * (a.list_entries + 4 * a.ncells) + C.list_off + 4 * cell;
-        wave_nth_element<true>(src, n, k, gpos);
+        wave_nth_element<true>(src, n, k, gpos, a.nth_pivot);
         for (int i = lane; i < take; i += 64) dst[i] = src[i];
     } else {
         for (int i = lane; i < take; i += 64) dst[i] = src[i];
@@ -1103,7 +1104,7 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
     E* g = level_entries<E>(a) + (size_t)f * a.level_entries + L.level_off;
     stage_to_lds<8>(list, nlev, lane, 64, [&](int i) { return g[i]; });
     lds_wave_sync();
-    wave_nth_element(list, nlev, L.n_desired, pos);
+    wave_nth_element(list, nlev, L.n_desired, pos, a.nth_pivot);
     for (int i = lane; i < L.n_desired; i += 64) g[i] = list[i];
     if (lane == 0) *cnt = L.n_desired;
 }
@@ -1487,33 +1488,36 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
 // u32 entries (key << 24 | payload), one wavefront; also the global-memory
 // replay of long lists (out_glb).
 __global__ __launch_bounds__(64) void k_debug_nth(const uint32_t* in, int n, int nth, uint32_t* out_glb,
-                                                  uint32_t* out_lds, int* gpos)
+                                                  uint32_t* out_lds, int* gpos, int pivot_mode)
 {
     __shared__ uint32_t list[kRetainCellCap];
     __shared__ int pos[kRetainCellCap + 8];
     const int lane = threadIdx.x;
     for (int i = lane; i < n; i += 64) out_glb[i] = in[i];
     global_wave_sync();
-    wave_nth_element<true>(out_glb, n, nth, gpos);
+    wave_nth_element<true>(out_glb, n, nth, gpos, pivot_mode);
     for (int i = lane; i < n; i += 64) list[i] = in[i];
     lds_wave_sync();
-    wave_nth_element(list, n, nth, pos);
+    wave_nth_element(list, n, nth, pos, pivot_mode);
     for (int i = lane; i < n; i += 64) out_lds[i] = list[i];
 }
 
 }  // namespace orbx
 
-extern "C" int orbx_debug_nth(const uint32_t* entries, int n, int nth, uint32_t* out_glb, uint32_t* out_lds)
+extern "C" int orbx_debug_nth_pivot(const uint32_t* entries, int n, int nth, int pivot_mode, uint32_t* out_glb,
+                                    uint32_t* out_lds)
 {
     using namespace orbx;
-    if (!entries || !out_glb || !out_lds || n < 0 || n > kRetainCellCap || nth < 0 || nth > n) return ORBX_ERR_ARG;
+    if (!entries || !out_glb || !out_lds || n < 0 || n > kRetainCellCap || nth < 0 || nth > n ||
+        (pivot_mode != 0 && pivot_mode != 1))
+        return ORBX_ERR_ARG;
     uint32_t* d = nullptr;
     if (hipMalloc(&d, 4 * sizeof(uint32_t) * (n + 8)) != hipSuccess) return ORBX_ERR_NOMEM;
     int r = ORBX_OK;
     if (hipMemcpy(d, entries, sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK) {
         hipLaunchKernelGGL(k_debug_nth, dim3(1), dim3(64), 0, 0, d, n, nth, d + (n + 8), d + 2 * (n + 8),
-                           reinterpret_cast<int*>(d + 3 * (n + 8)));
+                           reinterpret_cast<int*>(d + 3 * (n + 8)), pivot_mode);
         if (hipDeviceSynchronize() != hipSuccess ||
             hipMemcpy(out_glb, d + (n + 8), sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(out_lds, d + 2 * (n + 8), sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1521,6 +1525,11 @@ extern "C" int orbx_debug_nth(const uint32_t* entries, int n, int nth, uint32_t*
     }
     (void)hipFree(d);
     return r;
+}
+
+extern "C" int orbx_debug_nth(const uint32_t* entries, int n, int nth, uint32_t* out_glb, uint32_t* out_lds)
+{
+    return orbx_debug_nth_pivot(entries, n, nth, 0, out_glb, out_lds);
 }
 
 namespace orbx {
@@ -1553,6 +1562,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
     a.harris = ctx->harris;
     a.fp_contract = ctx->fp_contract;
+    a.nth_pivot = ctx->nth_pivot;
     // the level retain holds a whole level list (+ scratch) in one block's LDS
     if ((size_t)((ctx->harris ? 3 : 2) * g.max_level_cap + 8) * 4 > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     a.cell_keys64 = ctx->harris ? ctx->cell_keys64 + (size_t)first * g.list_entries : nullptr;

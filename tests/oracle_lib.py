@@ -70,6 +70,9 @@ def load(variant="iso"):
         "orbx_ref_search_by_projection_local": ([vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, ip], i),
         "orbx_ref_hamming_bf": ([vp, i, vp, i, vp, vp, vp], i),
         "orbx_ref_fp_contract": ([], i),
+        "orbx_ref_set_nth_pivot": ([i], i),
+        "orbx_ref_get_nth_pivot": ([], i),
+        "orbx_ref_nth_element_perm": ([vp, i, i, i, i, vp], i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -88,8 +91,10 @@ def ptr(a):
 
 
 class RefExtractor:
-    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1, variant="iso", lib=None):
+    def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1, variant="iso", lib=None,
+                 nth_pivot=0):
         self.L = lib if lib is not None else load(variant)
+        self.nth_pivot = nth_pivot   # retainBest's libstdc++ era (orbx_ref_set_nth_pivot), per call
         self.h = self.L.orbx_ref_extractor_create(nfeatures, scale, nlevels, score_type, fast_th)
         assert self.h, "oracle rejected the configuration"
         self.nfeatures = nfeatures
@@ -107,8 +112,13 @@ class RefExtractor:
         kps = np.zeros(self.nfeatures, KEYPOINT)
         desc = np.zeros((self.nfeatures, 32), np.uint8)
         n = ctypes.c_int()
-        r = self.L.orbx_ref_extract(self.h, ptr(img), w, h, w, ptr(kps), ptr(desc), self.nfeatures,
-                                    ctypes.byref(n))
+        prev = self.L.orbx_ref_get_nth_pivot()
+        assert self.L.orbx_ref_set_nth_pivot(self.nth_pivot) == 0
+        try:
+            r = self.L.orbx_ref_extract(self.h, ptr(img), w, h, w, ptr(kps), ptr(desc), self.nfeatures,
+                                        ctypes.byref(n))
+        finally:
+            self.L.orbx_ref_set_nth_pivot(prev)
         assert r == 0, r
         return kps[:n.value].copy(), desc[:n.value].copy()
 

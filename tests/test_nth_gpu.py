@@ -54,3 +54,28 @@ def test_nth_element_replays(kind, keys):
         m = R.orbx_ref_retain_best(ptr(resp), n, nth, ptr(idx))
         assert m >= nth
         assert np.array_equal(lds[:nth] & 0xFFFFFF, idx[:nth]), (kind, n, nth)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["gcc49", "gcc48"])
+@pytest.mark.parametrize("kind,keys", CASES[::3], ids=[f"{k}-{len(v)}" for k, v in CASES[::3]])
+def test_nth_element_full_permutation_both_eras(kind, keys, mode):
+    """The whole list after the device replay (LDS and global memory) equals
+    the oracle's libstdc++ restatement of the same pivot era entry for entry
+    (orbx_ref_nth_element_perm), not just the retained prefix."""
+    L = ox.lib()
+    L.orbx_debug_nth_pivot.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+    R = load()
+    n = len(keys)
+    entries = ((keys.astype(np.uint32) & 0xFF) << 24 | np.arange(n, dtype=np.uint32)).astype(np.uint32)
+    resp = (entries >> 24).astype(np.float32)
+    for nth in sorted({1, n // 3, n // 2, n - 1}):
+        if not 0 < nth < n:
+            continue
+        glb = np.zeros(n, np.uint32)
+        lds = np.zeros(n, np.uint32)
+        assert L.orbx_debug_nth_pivot(entries.ctypes.data, n, nth, mode, glb.ctypes.data, lds.ctypes.data) == 0
+        perm = np.zeros(n, np.int32)
+        assert R.orbx_ref_nth_element_perm(ptr(resp), n, nth, mode, 0, ptr(perm)) == 0
+        assert np.array_equal(lds & 0xFFFFFF, perm), (kind, n, nth, mode)
+        assert np.array_equal(glb, lds), (kind, n, nth, mode)
