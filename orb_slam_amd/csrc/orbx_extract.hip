@@ -1309,6 +1309,36 @@ __device__ inline int orb_sample_offset(float px, float py, float sa, float ca)
     return cv_round(fy) * kBrPitch + cv_round(fx);
 }
 
+// Both points of a pattern pair at once on packed fp32 (v_pk_mul_f32 /
+// v_pk_add_f32 / v_pk_fma_f32: each lane rounds exactly as the scalar
+// operation).  cvRound (round half to even, OpenCV 2.4's cvtsd2si) is the
+// 1.5 * 2^23 magic-number round trip: |coordinate| <= 18, so fy + M rounds fy
+// to its nearest-even integer and subtracting M again is exact.  The patch
+// offset row * kBrPitch + col (+ base, folded into the column's round trip)
+// is then an exact float fma on integers below 2^24.  Returns the two LDS
+// byte addresses.
+typedef float orbx_f2 __attribute__((ext_vector_type(2)));
+template <bool kFma>
+__device__ inline void orb_sample_addr2(orbx_f2 px, orbx_f2 py, float sa, float ca, float base, uint32_t& a1,
+                                        uint32_t& a2)
+{
+    const orbx_f2 SA = {sa, sa}, CA = {ca, ca};
+    orbx_f2 fy, fx;
+    if constexpr (kFma) {
+        fy = __builtin_elementwise_fma(px, SA, py * CA);
+        fx = __builtin_elementwise_fma(px, CA, -(py * SA));
+    } else {
+        fy = px * SA + py * CA;
+        fx = px * CA - py * SA;
+    }
+    const orbx_f2 M = {12582912.0f, 12582912.0f}, MB = {12582912.0f - base, 12582912.0f - base};
+    const orbx_f2 P = {(float)kBrPitch, (float)kBrPitch};
+    const orbx_f2 ry = (fy + M) - M, rxb = (fx + M) - MB;
+    const orbx_f2 ad = __builtin_elementwise_fma(ry, P, rxb);
+    a1 = (uint32_t)ad.x;
+    a2 = (uint32_t)ad.y;
+}
+
 template <bool kFma>
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
 {
@@ -1457,12 +1487,17 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
     float sa, ca;
     cr_sincosf(__fmul_rn(angle, factorPI), &sa, &ca);
     uint8_t* desc = a.out_desc + ((size_t)(a.first_slot + f) * a.nfeatures + k) * 32;
+    // the blurred patch centre as an offset into the block's LDS (exact in float)
+    const uint8_t* lds_bytes = &s_patch[0][0];
+    const float brf = (float)(int)(br - lds_bytes);
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const float px1 = (float)(int8_t)(pat[r] & 0xFF), py1 = (float)(int8_t)((pat[r] >> 8) & 0xFF);
-        const float px2 = (float)(int8_t)((pat[r] >> 16) & 0xFF), py2 = (float)(int8_t)(pat[r] >> 24);
-        const int t0 = br[orb_sample_offset<kFma>(px1, py1, sa, ca)];
-        const int t1 = br[orb_sample_offset<kFma>(px2, py2, sa, ca)];
+        const orbx_f2 px = {(float)(int8_t)(pat[r] & 0xFF), (float)(int8_t)((pat[r] >> 16) & 0xFF)};
+        const orbx_f2 py = {(float)(int8_t)((pat[r] >> 8) & 0xFF), (float)(int8_t)(pat[r] >> 24)};
+        uint32_t a1, a2;
+        orb_sample_addr2<kFma>(px, py, sa, ca, brf, a1, a2);
+        const int t0 = lds_bytes[a1];
+        const int t1 = lds_bytes[a2];
         const unsigned long long bits = __ballot(t0 < t1);
         // this half's 32 bits are descriptor bits 32r .. 32r+31 (bytes 4r .. 4r+3)
         if (valid && hl == r) reinterpret_cast<uint32_t*>(desc)[r] = (uint32_t)(bits >> (32 * half));
