@@ -15,7 +15,7 @@
 //             pair of its edges.  The W_i = Hpl blocks are rebuilt from the
 //             edge's inputs (pose, point, observation) where they are used
 //             instead of being stored per edge and re-read from HBM.  The
-//             reduced camera system is accumulated in 2^-60 fixed point with
+//             reduced camera system is accumulated in 2^-51 fixed point with
 //             64-bit integer atomics (two limbs per entry, packed lower
 //             triangle in LDS): integer sums do not depend on the order the
 //             points arrive in, so the result is bitwise reproducible

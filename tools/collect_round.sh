@@ -5,7 +5,9 @@
 #           serialised c2 kernel trace (tools/extract_serial.py)
 #   part 2: tools/collect_profiles.sh for c2, c3, c5, pose (kernel trace +
 #           stats, FETCH_SIZE, WRITE_SIZE and one SQ pass each)
-# usage: tools/collect_round.sh 1|2|bench ; every GPU step has its own time limit
+#   serial: the same for `bench.py --serial` at c2 and c3 (one launch per
+#           kernel over the whole batch: the bench line's headline roofline)
+# usage: tools/collect_round.sh 1|2|serial|bench ; every GPU step has its own time limit
 # and the first failure ends the script.
 set -e -o pipefail
 out=gpurun_out/round
@@ -25,6 +27,9 @@ timeout -k 10 300 python3 bench.py --workload c3 --cpu-budget 10 > "$out/bench_c
 timeout -k 10 300 python3 bench.py --workload c5 --cpu-budget 10 > "$out/bench_c5.json" 2> "$out/bench_c5.err"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c2_serial" -o run -- \
     python3 tools/extract_serial.py > "$out/c2_serial.log" 2>&1
+elif [ "$1" = serial ]; then   # PMC of the serialised bench (the headline roofline's launch)
+tools/collect_profiles.sh "$out/c2_serial_prof" --serial
+tools/collect_profiles.sh "$out/c3_serial_prof" --workload c3 --serial
 else
 tools/collect_profiles.sh "$out/c2"
 tools/collect_profiles.sh "$out/c3" --workload c3

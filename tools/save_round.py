@@ -35,4 +35,15 @@ for wl in ("c2", "c3", "c5", "pose"):
     with open(dst / f"{tag}_{wl}_pmc_sq.txt", "w") as f:
         subprocess.run([sys.executable, str(ROOT / "tools/pmc_table.py"), sq], stdout=f, check=True)
 shutil.copy(one("c2_serial/**/*kernel_stats.csv"), dst / f"{tag}_c2_serial_kernel_stats.csv")
+for wl in ("c2", "c3"):   # `bench.py --serial` profiles (tools/collect_round.sh serial), when collected
+    if not (src / f"{wl}_serial_prof").exists():
+        continue
+    shutil.copy(one(f"{wl}_serial_prof/trace/**/*kernel_stats.csv"), dst / f"{tag}_{wl}_serial_bench_kernel_stats.csv")
+    fetch = one(f"{wl}_serial_prof/fetch/**/*counter_collection.csv")
+    write = one(f"{wl}_serial_prof/write/**/*counter_collection.csv")
+    sq = one(f"{wl}_serial_prof/sq/**/*counter_collection.csv")
+    with open(dst / f"{tag}_{wl}_serial_pmc_hbm.json", "w") as f:
+        subprocess.run([sys.executable, str(ROOT / "tools/pmc_summary.py"), fetch, write, sq], stdout=f, check=True)
+    with open(dst / f"{tag}_{wl}_serial_pmc_sq.txt", "w") as f:
+        subprocess.run([sys.executable, str(ROOT / "tools/pmc_table.py"), sq], stdout=f, check=True)
 print("saved", tag)
