@@ -100,6 +100,8 @@ struct RowWalk {
     int r, q, dr, dq, nq;
     __device__ RowWalk(int start, int stride, int n_q) : nq(n_q)
     {
+        // callers never pass n_q == 0 (integer division by zero is undefined
+        // behaviour, which the compiler may assume away)
         r = start / n_q;
         q = start - r * n_q;
         dr = stride / n_q;
@@ -515,15 +517,19 @@ constexpr int kFastWideThreads = 256;   // workgroup of the wide-tile FAST insta
 // Dynamic LDS of a FAST workgroup for tiles of `bytes` (host and device).
 __host__ __device__ constexpr int fast_tile_bytes(int hy_max, int pitch) { return (hy_max * pitch + 511) & ~511; }
 __host__ __device__ constexpr int fast_lds_bytes(int tile_bytes) { return 2 * tile_bytes + tile_bytes / 32; }
+// static LDS of a 256-thread FAST workgroup: 4 survivor queues of 384
+// entries (u16, or u32 for the runtime-pitch instance) + block scratch
+__host__ __device__ constexpr int fast_static_lds(bool u32_entries) { return 4 * 384 * (u32_entries ? 4 : 2) + 64; }
+constexpr int kFastLdsTarget = 40 * 1024;   // 4 workgroups per CU
 
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
 // kThreads: 256 for cells up to 208-byte rows; the wide tiles of large
 // frames (1920x1080: 336-byte rows, 75 KB of LDS, two workgroups per CU)
 // get more waves per workgroup instead.
-template <int kP, int kThreads = 256>
+template <int kP, int kThreads = 256, bool kBanded = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
-    ExtractArgs a, int tile_bytes)
+    ExtractArgs a, int tile_bytes, int band_rows)
 {
     constexpr int kBlock = kThreads, kWaves = kThreads / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -559,9 +565,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     uint32_t* kept = tile32;                                      // bit per tile byte (after scoring)
     uint32_t* nz = reinterpret_cast<uint32_t*>(sm + tile_bytes);  // bit per tile dword
     FP_T0();
-    auto load_tile = [&]() {
+    // the cell's rows [w0, w0 + wh) into tile rows 0 .. wh - 1
+    auto load_tile = [&](int w0, int wh) {
         uint4* t16 = reinterpret_cast<uint4*>(tile32);
-        const int n = hy * nq16;
+        const uint8_t* src_w = src + (size_t)w0 * L.stride;
+        const int n = wh * nq16;
         // i / nq16 as a float product: (i + 1/2) / nq16 is at least 1/(2 nq16)
         // from an integer and the product's error is < 2^-21 (i + 1) for
         // i < 2^16, nq16 < 2^8 -- four integer divisions cost ~80 VALU
@@ -575,17 +583,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
             const int r0 = row_of(i0), r1 = row_of(i1), r2 = row_of(i2), r3 = row_of(i3);
             const int c0 = i0 - r0 * nq16, c1 = i1 - r1 * nq16, c2 = i2 - r2 * nq16, c3 = i3 - r3 * nq16;
             // 32-bit offsets from the uniform tile origin (saddr loads)
-            const uint4 v0 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r0 * L.stride + 16 * c0));
-            const uint4 v1 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r1 * L.stride + 16 * c1));
-            const uint4 v2 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r2 * L.stride + 16 * c2));
-            const uint4 v3 = *reinterpret_cast<const uint4*>(src + (uint32_t)(r3 * L.stride + 16 * c3));
+            const uint4 v0 = *reinterpret_cast<const uint4*>(src_w + (uint32_t)(r0 * L.stride + 16 * c0));
+            const uint4 v1 = *reinterpret_cast<const uint4*>(src_w + (uint32_t)(r1 * L.stride + 16 * c1));
+            const uint4 v2 = *reinterpret_cast<const uint4*>(src_w + (uint32_t)(r2 * L.stride + 16 * c2));
+            const uint4 v3 = *reinterpret_cast<const uint4*>(src_w + (uint32_t)(r3 * L.stride + 16 * c3));
             t16[r0 * (P >> 4) + c0] = v0;
             t16[r1 * (P >> 4) + c1] = v1;
             t16[r2 * (P >> 4) + c2] = v2;
             t16[r3 * (P >> 4) + c3] = v3;
         }
     };
-    load_tile();
     // S' (0 where not scored) and nz start at zero (contiguous: tile_bytes *
     // (1 + 1/32), a multiple of 16); kept is cleared after the score pass
     const int clear16 = (tile_bytes + tile_bytes / 32) >> 4;
@@ -595,8 +602,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     auto clear_kept = [&]() {
         for (int i = tid; i < (tile_bytes >> 7); i += kBlock) reinterpret_cast<uint4*>(kept)[i] = make_uint4(0, 0, 0, 0);
     };
-    clear_maps();
-    __syncthreads();
     const int c_lo = 3 + sh, c_hi = hx - 4 + sh;         // interior tile columns
     // dwords holding them; none when the ROI has no interior (hx < 7: a
     // degenerate cell of a tiny level, where c_hi < c_lo and, with a large
@@ -604,10 +609,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     const int q0 = c_lo >> 2, nqe = c_hi >= c_lo ? (c_hi >> 2) - q0 + 1 : 0;
     const int q_last = q0 + nqe - 1;
     const int j_lo = c_lo & 3, j_hi = c_hi & 3;           // pixels j >= j_lo of dword q0, j <= j_hi of q_last
-    const int nunits = max(hy - 6, 0) * nqe;
     const uint32_t k64 = 0x64646464u;
-    // S' map at threshold tmin: S' = S where S >= tmin, else 0
-    auto score_pass = [&](const int tmin) {
+    // S' map at threshold tmin over the window rows [sr0, sr0 + nrows):
+    // S' = S where S >= tmin, else 0
+    auto score_pass = [&](const int tmin, const int sr0, const int nrows) {
+        const int nunits = max(nrows, 0) * nqe;
+        // no interior dwords (a degenerate cell of a tiny level): nothing to
+        // score, and RowWalk must not divide by nqe == 0
+        if (nunits <= 0) return;
         // per-wave queue cand[0, qt) of compass survivors, scored 128 at a
         // time (two per lane) with every lane busy
         int qt = 0;
@@ -635,7 +644,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         RowWalk cw_(wv * 64 + lane, kBlock, nqe);
         for (int u0 = wv * 64; u0 < nunits; u0 += kBlock, cw_.next()) {
             const int u = u0 + lane;
-            const int r = 3 + cw_.r, q = q0 + cw_.q;
+            const int r = sr0 + cw_.r, q = q0 + cw_.q;
             // per pixel j: the sign bit of x_j = max(v - A, B - v) - tmin - 1
             // is set where the pixel fails (even half: j = 0, 2; odd: 1, 3)
             uint32_t xw0 = 0xBC00BC00u, xw1 = 0xBC00BC00u;   // -1.0: fails both tests (not -0)
@@ -736,12 +745,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     // all 8 neighbours' S'.  Only dwords whose `nz` bit is set can keep
     // anything; they are listed (u16 tile dword indices, in windows of
     // kUnitCap) with one block scan and shared by all 256 threads.
+    // Only the window rows [rb0, rb1) (the band's own rows) keep anything;
+    // the halo rows' S' serve as their neighbours.
     // Returns this thread's count of kept corners at fastTh.
-    auto nms_pass = [&]() {
+    auto nms_pass = [&](const int rb0, const int rb1, const int wh) {
         int c1 = 0;
         const uint32_t FT = (uint32_t)max(a.fast_th, 1) * 0x00010001u;
         auto nms_unit = [&](int idx) {
-            const int q = idx % nq;
+            const int rw = idx / nq, q = idx - rw * nq;
+            if (rw < rb0 || rw >= rb1) return;
             const uint32_t* m = sm32 + idx;
             const uint32_t mid = m[0];
             // the 8 neighbours of the 4 pixels as dwords (bytes j-1, j, j+1 of
@@ -774,7 +786,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
             }
             if (bits) atomicOr(&kept[idx >> 3], bits << (4 * (idx & 7)));
         };
-        const int nw = (hy * nq + 31) >> 5;                  // nz words
+        const int nw = (wh * nq + 31) >> 5;                  // nz words
         const int pw = (nw + kBlock - 1) / kBlock;
         const int w0 = min(tid * pw, nw), w1 = min(w0 + pw, nw);
         int cnt = 0;
@@ -801,84 +813,120 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         }
         return c1;
     };
+    uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
+    // Raster-order compaction of the kept bitmap into the cell's list at
+    // out_base: thread tid owns the contiguous bitmap words [ka, kb); kept
+    // bytes are S' >= tmin of the pass, and t == tmin unless fastTh < 7 fell
+    // back to 7 (then each byte is compared).  Returns the entries written.
+    auto compact = [&](const int t, const int tmin, const int w0, const int wh, const int out_base) {
+        const int nkw = (wh * P + 31) >> 5;
+        const int per = (nkw + kBlock - 1) / kBlock;
+        const int ka = min(tid * per, nkw), kb = min(ka + per, nkw);
+        const bool all_kept = t == tmin;
+        int cnt = 0;
+        for (int k = ka; k < kb; k++) {
+            uint32_t b = kept[k];
+            if (all_kept) {
+                cnt += __popc(b);
+            } else {
+                while (b) {
+                    const int bit = __builtin_ctz(b);
+                    b &= b - 1;
+                    cnt += sm[32 * k + bit] >= t;
+                }
+            }
+        }
+        int total;
+        int off = out_base + block_exclusive_scan(cnt, &total, bs, 1);
+        if (cnt) {
+            // entries go straight to the cell's list (each thread's run is
+            // contiguous; the tile area holds the kept bitmap being read)
+            for (int k = ka; k < kb; k++) {
+                uint32_t b = kept[k];
+                while (b) {
+                    const int bit = __builtin_ctz(b);
+                    b &= b - 1;
+                    const int pos = 32 * k + bit;
+                    const int s = sm[pos];
+                    if (s >= t) {
+                        if (off < C.list_cap) {
+                            const int r = w0 + pos / P, cc = pos % P - sh;   // cell row, ROI column
+                            out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
+                        }
+                        off++;
+                    }
+                }
+            }
+        }
+        return total;
+    };
+    // One band: the cell rows [b0, b1) (interior rows 3 .. hy - 4).  Its
+    // window holds the rows [b0 - 4, b1 + 4) (clipped to the cell): FAST's
+    // 3-pixel radius around the rows b0 - 1 .. b1 whose S' the band's NMS
+    // reads.  Scores, suppresses and (emit) appends the band's kept corners
+    // at out_base; returns the band's kept corners at fastTh.  A whole cell
+    // is one band unless the host splits tall cells (band_rows) so that a
+    // workgroup's LDS stays small (1920x1080: 4 workgroups per CU instead of
+    // 2); S' of a row depends only on the rows within 3 of it, so the split
+    // is exact.
+    auto band = [&](const int b0, const int b1, const int tmin) {
+        const int w0 = max(0, b0 - 4), wh = min(hy, b1 + 4) - w0;
+        const int s0 = max(3, b0 - 1), s1 = min(hy - 4, b1);   // scored rows (inclusive)
+        load_tile(w0, wh);
+        clear_maps();
+        __syncthreads();
+        score_pass(tmin, s0 - w0, s1 - s0 + 1);
+        __syncthreads();
+        clear_kept();   // the tile is dead until the next band reloads it
+        __syncthreads();
+        const int n1 = block_sum(nms_pass(b0 - w0, b1 - w0, wh), bs, 0);
+        __syncthreads();
+        return n1;
+    };
     // Thresholds (:599-614): FAST(fastTh), and FAST(7) when that finds <= 3
     // corners.  The S' map at threshold t gives both answers for t <= min
     // (NMS against S' equals NMS against the t-score map for corners >= t),
     // so a cell is scored at fastTh first (far fewer compass survivors) and
     // rescored at 7 only when it needs the fallback.
-    int n1, tmin_final;
     FP_MARK(0);
-    tmin_final = a.fast_th;
-    score_pass(a.fast_th);
-    __syncthreads();
-    clear_kept();   // the tile is dead until a rescore reloads it
-    __syncthreads();
-    FP_MARK(1);
-    n1 = block_sum(nms_pass(), bs, 0);
-    FP_MARK(2);
-    if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
-        if (threadIdx.x == 0) FP_ADD(8, 1);
-        load_tile();
-        clear_maps();
-        __syncthreads();
-        tmin_final = a.fast_th_low;
-        score_pass(a.fast_th_low);
-        __syncthreads();
-        clear_kept();
-        __syncthreads();
-        nms_pass();
-        FP_MARK(3);
-    }
-    __syncthreads();
-    // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
-    const int t = (n1 <= 3) ? a.fast_th_low : a.fast_th;
-    uint32_t* out = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
-    // raster-order compaction of the kept bitmap: thread tid owns the
-    // contiguous bitmap words [ka, kb); kept bytes are S' >= tmin of the
-    // final pass, and t == tmin there unless fastTh < 7 fell back to 7
-    // (then each byte is compared)
-    const int nkw = (hy * P + 31) >> 5;
-    const int per = (nkw + kBlock - 1) / kBlock;
-    const int ka = min(tid * per, nkw), kb = min(ka + per, nkw);
-    const bool all_kept = t == tmin_final;
-    int cnt = 0;
-    for (int k = ka; k < kb; k++) {
-        uint32_t b = kept[k];
-        if (all_kept) {
-            cnt += __popc(b);
-        } else {
-            while (b) {
-                const int bit = __builtin_ctz(b);
-                b &= b - 1;
-                cnt += sm[32 * k + bit] >= t;
+    int n1 = 0, written = 0;
+    if constexpr (kBanded) {
+        // each band is emitted at fastTh as it is done; a cell whose kept
+        // corners at fastTh number <= 3 is scored again band by band (at 7,
+        // or at fastTh < 7 and filtered to >= 7) and re-emitted
+        const int brows = band_rows > 0 ? band_rows : hy;
+        for (int b0 = 3; b0 < hy - 3; b0 += brows) {
+            const int b1 = min(b0 + brows, hy - 3);
+            n1 += band(b0, b1, a.fast_th);
+            written += compact(a.fast_th, a.fast_th, max(0, b0 - 4), min(hy, b1 + 4) - max(0, b0 - 4), written);
+            __syncthreads();   // kept / S' reused by the next band
+        }
+        if (n1 <= 3) {   // uniform over the block
+            const int tmin2 = a.fast_th > a.fast_th_low ? a.fast_th_low : a.fast_th;
+            written = 0;
+            for (int b0 = 3; b0 < hy - 3; b0 += brows) {
+                const int b1 = min(b0 + brows, hy - 3);
+                band(b0, b1, tmin2);
+                written += compact(a.fast_th_low, tmin2, max(0, b0 - 4), min(hy, b1 + 4) - max(0, b0 - 4), written);
+                __syncthreads();
             }
         }
-    }
-    int base;
-    int off = block_exclusive_scan(cnt, &base, bs, 1);
-    if (cnt) {
-        // entries go straight to the cell's list (each thread's run is
-        // contiguous; the tile area holds the kept bitmap being read)
-        for (int k = ka; k < kb; k++) {
-            uint32_t b = kept[k];
-            while (b) {
-                const int bit = __builtin_ctz(b);
-                b &= b - 1;
-                const int pos = 32 * k + bit;
-                const int s = sm[pos];
-                if (s >= t) {
-                    if (off < C.list_cap) {
-                        const int r = pos / P, cc = pos - r * P - sh;   // tile row, ROI column
-                        out[off] = ((uint32_t)s << 24) | ((uint32_t)(C.ini_y + r) << 12) | (uint32_t)(C.ini_x + cc);
-                    }
-                    off++;
-                }
-            }
+    } else if (hy > 6) {   // the whole cell as one band (the host sends band_rows = 0)
+        int tmin_final = a.fast_th;
+        n1 = band(3, hy - 3, a.fast_th);
+        FP_MARK(2);
+        if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
+            if (threadIdx.x == 0) FP_ADD(8, 1);
+            tmin_final = a.fast_th_low;
+            band(3, hy - 3, a.fast_th_low);
+            FP_MARK(3);
         }
+        // threshold choice: FAST(fastTh); if <= 3 corners, FAST(7) (:607-614)
+        written = compact(n1 <= 3 ? a.fast_th_low : a.fast_th, tmin_final, 0, hy, 0);
     }
     if (tid == 0) {
-        *count_out = base;
-        if (base > C.list_cap) atomicOr(a.error_flags, 1);
+        *count_out = written;
+        if (written > C.list_cap) atomicOr(a.error_flags, 1);
     }
     FP_MARK(4);
     if (tid == 0) FP_ADD(9, 1);
@@ -1672,21 +1720,47 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 hmax = std::max(hmax, c.hy);
             }
             const dim3 grid((int)g.cells.size(), nb);
-            auto fast = [&](auto kern, int P, int threads) {
-                const int bytes = fast_tile_bytes(hmax, P);
-                hipLaunchKernelGGL(kern, grid, dim3(threads), fast_lds_bytes(bytes), st, x, bytes);
+            // Whole cells when a workgroup's LDS (tile + S' + nz + the static
+            // survivor queues) stays within kFastLdsTarget (4 workgroups per
+            // CU); taller cells are split into the fewest equal row bands
+            // whose windows (band + 8 halo rows) fit.
+            auto plan = [&](int P, int static_lds, int& band_rows) {
+                band_rows = 0;
+                const int whole = fast_tile_bytes(hmax, P);
+                if (fast_lds_bytes(whole) + static_lds <= kFastLdsTarget || hmax <= 9) return whole;
+                int wh = hmax;
+                while (wh > 9 && fast_lds_bytes(fast_tile_bytes(wh, P)) + static_lds > kFastLdsTarget) wh--;
+                const int nint = hmax - 6, bmax = wh - 8;
+                const int nbands = (nint + bmax - 1) / bmax;
+                band_rows = (nint + nbands - 1) / nbands;
+                return fast_tile_bytes(std::min(hmax, band_rows + 8), P);
             };
-            // the templated instances queue u16 tile positions: tiles of up
-            // to 64 KB (taller ones take the runtime-pitch instance)
-            auto fits = [&](int P) { return wmax <= P && (long)hmax * P <= 65536; };
-            if (fits(96)) fast(k_fast_cells<96>, 96, 256);
-            else if (fits(144)) fast(k_fast_cells<144>, 144, 256);
-            else if (fits(208)) fast(k_fast_cells<208>, 208, 256);
-            else if (fits(336)) fast(k_fast_cells<336, kFastWideThreads>, 336, kFastWideThreads);
+            auto fast = [&](auto kern, int bytes, int band_rows, int threads) {
+                hipLaunchKernelGGL(kern, grid, dim3(threads), fast_lds_bytes(bytes), st, x, bytes, band_rows);
+            };
+            // the templated instances queue u16 tile positions: windows of up
+            // to 64 KB (larger ones take the runtime-pitch instance)
+            // whole cells at the 96 / 144 / 208 pitches (their tiles fit four
+            // workgroups per CU at the frame sizes of interest), row bands
+            // where needed at 336 (1920x1080) and the runtime pitch
+            int br = 0, bytes = 0;
+            auto fits = [&](int P) {
+                if (wmax > P) return false;
+                bytes = fast_tile_bytes(hmax, P);
+                return bytes <= 65536;
+            };
+            auto fits_banded = [&](int P) {
+                if (wmax > P) return false;
+                bytes = plan(P, fast_static_lds(false), br);
+                return bytes <= 65536;
+            };
+            if (fits(96)) fast(k_fast_cells<96>, bytes, 0, 256);
+            else if (fits(144)) fast(k_fast_cells<144>, bytes, 0, 256);
+            else if (fits(208)) fast(k_fast_cells<208>, bytes, 0, 256);
+            else if (fits_banded(336)) fast(k_fast_cells<336, kFastWideThreads, true>, bytes, br, kFastWideThreads);
             else {
-                const int bytes = fast_tile_bytes(1, g.max_tile_bytes);
-                hipLaunchKernelGGL((k_fast_cells<0, kFastWideThreads>), grid, dim3(kFastWideThreads), fast_lds_bytes(bytes),
-                                   st, x, bytes);
+                bytes = plan(wmax, fast_static_lds(true), br);
+                fast(k_fast_cells<0, kFastWideThreads, true>, bytes, br, kFastWideThreads);
             }
         }
         timer_end(ctx, "fast", st);

@@ -330,3 +330,23 @@ def test_random_configs_batch_pipeline(w, h, nf, scale, nlev, fth, score, kind, 
         assert_kps_equal(gk, rk)
         assert np.array_equal(gd, rd)
     ctx.close()
+
+
+@pytest.mark.parametrize("w,h,nf,kind,fth", [
+    (1920, 1080, 2000, "rects", 20),    # 336-pitch instance, three row bands per level-0 cell, flat cells fall back
+    (1920, 1080, 2000, "noise", 20),    # dense corners in every band
+    (1280, 1600, 400, "texture", 20),   # few huge cells: runtime-pitch instance, many bands
+    (1280, 1600, 400, "rects", 45),     # ... with the threshold-7 fallback band by band
+])
+def test_row_bands_match_oracle(w, h, nf, kind, fth):
+    """Tall FAST cells are scored in row bands (each window = band + 8 halo
+    rows) so a workgroup's LDS stays small; corners, scores and their raster
+    order must equal the whole-cell oracle, including cells whose <= 3
+    corners at fastTh send every band back for the FAST(7) pass."""
+    img = make(kind, w, h, 3)
+    ctx = ox.Context(nfeatures=nf, fast_th=fth, max_w=w, max_h=h, slots=1)
+    gk, gd = ctx(img)
+    ctx.close()
+    rk, rd = RefExtractor(nf, fast_th=fth)(img)
+    assert_kps_equal(gk, rk)
+    assert np.array_equal(gd, rd)
