@@ -520,7 +520,10 @@ __host__ __device__ constexpr int fast_lds_bytes(int tile_bytes) { return 2 * ti
 // static LDS of a 256-thread FAST workgroup: 4 survivor queues of 384
 // entries (u16, or u32 for the runtime-pitch instance) + block scratch
 __host__ __device__ constexpr int fast_static_lds(bool u32_entries) { return 4 * 384 * (u32_entries ? 4 : 2) + 64; }
-constexpr int kFastLdsTarget = 40 * 1024;   // 4 workgroups per CU
+#ifndef ORBX_FAST_LDS_TARGET
+#define ORBX_FAST_LDS_TARGET (40 * 1024)   // 4 workgroups per CU
+#endif
+constexpr int kFastLdsTarget = ORBX_FAST_LDS_TARGET;
 
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
