@@ -1739,7 +1739,8 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 return fast_tile_bytes(std::min(hmax, band_rows + 8), P);
             };
             auto fast = [&](auto kern, int bytes, int band_rows, int threads) {
-                hipLaunchKernelGGL(kern, grid, dim3(threads), fast_lds_bytes(bytes), st, x, bytes, band_rows);
+                const int lds = fast_lds_bytes(bytes);
+                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows);
             };
             // the templated instances queue u16 tile positions: windows of up
             // to 64 KB (larger ones take the runtime-pitch instance)

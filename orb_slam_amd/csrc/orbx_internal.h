@@ -39,7 +39,10 @@ constexpr int kPatch = 31;       // PATCH_SIZE (:75)
 constexpr int kMaxLevels = 16;
 constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
 constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
-constexpr int kBlurStrip = 28;   // output rows per blur thread (rolling window; 4 chunks of 7)
+#ifndef ORBX_BLUR_STRIP
+#define ORBX_BLUR_STRIP 28
+#endif
+constexpr int kBlurStrip = ORBX_BLUR_STRIP;   // output rows per blur thread (rolling window; chunks of 7)
 constexpr int kBlurItems = 256;  // blur threads per block (4 waves, one (strip, column chunk) each)
 constexpr int kBlurChunkCols = 62;   // output dword columns per blur wave (+ one halo lane each side)
 
