@@ -503,6 +503,27 @@ int orbx_vocab_transform(orbx_ctx* ctx, const orbx_vocab* voc, int n, const uint
                          uint32_t* bow_words, double* bow_values, int* n_words,
                          uint32_t* fv_nodes, int32_t* fv_ptr, int32_t* fv_feat, int* n_fv_nodes);
 
+/* Device-resident form for extracted slots: Frame::ComputeBoW (src/Frame.cc:
+ * 279-286) of slots [first, first+count) -- the descent of every extracted
+ * descriptor and the slot's BowVector / FeatureVector built on the device,
+ * kept in HBM until the slot is extracted again (async, context stream).
+ * Frames of up to 4096 features (ORBX_ERR_UNSUPPORTED above). */
+int orbx_dev_compute_bow(orbx_ctx* ctx, const orbx_vocab* voc, int first, int count, int levelsup);
+/* Read one slot's BoW (after orbx_dev_compute_bow; syncs), the arrays of
+ * orbx_vocab_transform with the same meaning.  Any output may be NULL;
+ * cap >= the slot's feature count (ORBX_ERR_CAPACITY otherwise). */
+int orbx_dev_read_bow(orbx_ctx* ctx, int slot, int cap, int32_t* word_id, double* weight, int32_t* node_id,
+                      uint32_t* bow_words, double* bow_values, int* n_words, uint32_t* fv_nodes,
+                      int32_t* fv_ptr, int32_t* fv_feat, int* n_fv_nodes);
+/* Tracking::Relocalisation's matching loop (src/Tracking.cc:904-925):
+ * ORBmatcher::SearchByBoW(pKF, F) (src/ORBmatcher.cc:155-283) of n
+ * candidate keyframes against the frame in `slot`, its keypoints,
+ * descriptors and FeatureVector read where orbx_dev_extract /
+ * orbx_dev_compute_bow left them.  matches_f[k] (cap >= nfeatures entries):
+ * per frame keypoint the KF keypoint index or -1, as orbx_search_by_bow_frame. */
+int orbx_dev_search_by_bow(orbx_ctx* ctx, int slot, int n, const orbx_bow_view* KFs, float nnratio,
+                           int check_ori, int32_t* const* matches_f, int cap, int* n_matches);
+
 /* ------------------------------------------------------------------------ */
 /* C. Local bundle adjustment                                                */
 /* ------------------------------------------------------------------------ */

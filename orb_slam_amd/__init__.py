@@ -116,6 +116,9 @@ def _declare(L):
         "orbx_vocab_destroy": ([vp], None),
         "orbx_vocab_n_words": ([vp], i),
         "orbx_vocab_transform": ([vp, vp, i, vp, i, vp, vp, vp, vp, vp, ip, vp, vp, vp, ip], i),
+        "orbx_dev_compute_bow": ([vp, vp, i, i, i], i),
+        "orbx_dev_read_bow": ([vp, i, i, vp, vp, vp, vp, vp, ip, vp, vp, vp, ip], i),
+        "orbx_dev_search_by_bow": ([vp, i, i, vp, f, i, vp, i, vp], i),
         "orbx_undistort_keypoints": ([vp, i, vp, vp, vp, vp], i),
         "orbx_compute_image_bounds": ([i, i, vp, vp, vp], i),
         "orbx_dev_undistort": ([vp, i, i, vp, vp], i),

@@ -80,7 +80,7 @@ static void free_buffers(orbx_ctx* ctx)
                     ctx->level_keys, ctx->cell_keys64, ctx->level_keys64, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
-                    ctx->scratch, ctx->pose_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
+                    ctx->scratch, ctx->pose_dev, ctx->bow_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);

@@ -191,6 +191,65 @@ __global__ __launch_bounds__(256) void k_bow_match(BowArgs a) { bow_match_block(
 // One workgroup per job (one keyframe pair each).
 __global__ __launch_bounds__(256) void k_bow_match_jobs(const BowArgs* jobs) { bow_match_block(jobs[blockIdx.x]); }
 
+// SearchByBoW(KF, F) against a device-resident frame (orbx_dev_search_by_bow):
+// F's FeatureVector comes from k_bow_build, so the common nodes are found
+// here.  Each KF node binary-searches F's ascending node ids; hits are
+// compacted in KF node order (the reference's merge order), then the job
+// runs as bow_match_block.
+struct BowSlotJob {
+    BowArgs a;                 // s1 = KF, s2 = the slot; nodes / n_common / out_len filled here
+    const uint32_t* kf_node_id;
+    const int32_t* kf_node_ptr;
+    int kf_n_nodes;
+    const uint32_t* f_node_id;
+    const int32_t* f_node_ptr;
+    const int32_t* f_counts;   // (n_words, n_fv_nodes)
+    const int32_t* f_n;        // slot feature count
+    int nf;
+    int4* nodes;               // [kf_n_nodes] scratch
+};
+
+__global__ __launch_bounds__(256) void k_bow_match_slot(const BowSlotJob* jobs)
+{
+    __shared__ BlockScratch bs;
+    __shared__ int s_bad;
+    const BowSlotJob& j = jobs[blockIdx.x];
+    const int tid = threadIdx.x, nfv = j.f_counts[1];
+    if (tid == 0) s_bad = 0;
+    const int per = (j.kf_n_nodes + kBlock - 1) / kBlock, k0 = tid * per, k1 = min(k0 + per, j.kf_n_nodes);
+    auto find = [&](uint32_t id) {
+        int lo = 0, hi = nfv;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (j.f_node_id[mid] < id) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo < nfv && j.f_node_id[lo] == id ? lo : -1;
+    };
+    int hits = 0;
+    for (int k = k0; k < k1; k++) hits += find(j.kf_node_id[k]) >= 0;
+    int total;
+    int at = block_exclusive_scan(hits, &total, bs, 0);
+    for (int k = k0; k < k1; k++) {
+        const int f = find(j.kf_node_id[k]);
+        if (f < 0) continue;
+        const int c2 = j.f_node_ptr[f + 1] - j.f_node_ptr[f];
+        if (c2 > 64 * kBowMaxChunks) s_bad = 1;
+        j.nodes[at++] = make_int4(j.kf_node_ptr[k], j.kf_node_ptr[k + 1] - j.kf_node_ptr[k], j.f_node_ptr[f], c2);
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (s_bad) {
+        if (tid == 0) *j.a.out_n = -1;   // a node wider than the taken-mask covers: ORBX_ERR_UNSUPPORTED
+        return;
+    }
+    BowArgs a = j.a;
+    a.nodes = j.nodes;
+    a.n_common = total;
+    a.out_len = min(*j.f_n, j.nf);
+    bow_match_block(a);
+}
+
 namespace {
 
 bool valid_bow(const orbx_bow_view* v, int max_octave)
@@ -444,4 +503,105 @@ extern "C" int orbx_search_for_triangulation_batch(orbx_ctx* ctx, const orbx_bow
                                                    int32_t* const* matches12, int* n_matches)
 {
     return run_bow_batch(ctx, KF1, n, KF2s, 2, 0.f, check_ori, F12s, sigma2_2s, nlevels, matches12, n_matches);
+}
+
+// Tracking::Relocalisation's loop (src/Tracking.cc:904-925): SearchByBoW(KF,
+// F) of each candidate keyframe against the extracted frame in `slot`, whose
+// BoW orbx_dev_compute_bow left in HBM.  One upload of the n keyframes, one
+// launch of n workgroups, one readback.
+extern "C" int orbx_dev_search_by_bow(orbx_ctx* ctx, int slot, int n, const orbx_bow_view* KFs, float nnratio,
+                                      int check_ori, int32_t* const* matches_f, int cap, int* n_matches)
+{
+    if (!ctx || slot < 0 || slot >= ctx->slots || n < 0 || (n > 0 && (!KFs || !matches_f || !n_matches)))
+        return ORBX_ERR_ARG;
+    if (!ctx->bow_dev || slot >= (int)ctx->bow_ready.size() || !ctx->bow_ready[slot]) return ORBX_ERR_ARG;
+    const int nf = ctx->bow_nf;
+    if (n > 0 && cap < nf) return ORBX_ERR_CAPACITY;
+    for (int k = 0; k < n; k++)
+        if (!valid_bow(&KFs[k], 0) || !matches_f[k]) return ORBX_ERR_ARG;
+    if (n == 0) return ORBX_OK;
+    ctx_enter(ctx);
+    size_t at = 0;
+    auto res = [&](size_t bytes) {
+        const size_t o = at;
+        at += al256(std::max<size_t>(bytes, 1));
+        return o;
+    };
+    struct Off {
+        size_t k1, d1, m1, f1, nid, nptr, nd, out, bin, n;
+    };
+    std::vector<Off> o(n);
+    for (int k = 0; k < n; k++) {
+        const orbx_bow_view& V = KFs[k];
+        const int nf1 = V.n_nodes ? V.node_ptr[V.n_nodes] : 0;
+        o[k].k1 = res((size_t)V.n * sizeof(orbx_keypoint));
+        o[k].d1 = res((size_t)V.n * 32);
+        o[k].m1 = res(V.n);
+        o[k].f1 = res((size_t)nf1 * 4);
+        o[k].nid = res((size_t)V.n_nodes * 4);
+        o[k].nptr = res((size_t)(V.n_nodes + 1) * 4);
+        o[k].nd = res((size_t)V.n_nodes * sizeof(int4));
+        o[k].out = res((size_t)nf * 4);
+        o[k].bin = res(nf);
+        o[k].n = res(4);
+    }
+    const size_t o_jobs = res(sizeof(BowSlotJob) * (size_t)n);
+    int r = ensure_scratch(ctx, at);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    auto put = [&](size_t off, const void* src, size_t bytes) -> int {
+        if (bytes == 0 || !src) return ORBX_OK;
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + off, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return ORBX_OK;
+    };
+    const SlotBowDev& b = ctx->bow;
+    std::vector<BowSlotJob> jobs(n);
+    for (int k = 0; k < n; k++) {
+        const orbx_bow_view& V = KFs[k];
+        const int nf1 = V.n_nodes ? V.node_ptr[V.n_nodes] : 0;
+        if ((r = put(o[k].k1, V.keys, (size_t)V.n * sizeof(orbx_keypoint))) ||
+            (r = put(o[k].d1, V.desc, (size_t)V.n * 32)) || (r = put(o[k].m1, V.mp, V.n)) ||
+            (r = put(o[k].f1, V.n_nodes ? V.feat_idx : nullptr, (size_t)nf1 * 4)) ||
+            (r = put(o[k].nid, V.n_nodes ? V.node_id : nullptr, (size_t)V.n_nodes * 4)) ||
+            (r = put(o[k].nptr, V.n_nodes ? V.node_ptr : nullptr, (size_t)(V.n_nodes + 1) * 4)))
+            return r;
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].out, 0xFF, (size_t)nf * 4, ctx->stream));
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].bin, 0xFF, (size_t)nf, ctx->stream));
+        BowSlotJob& j = jobs[k];
+        j = BowSlotJob{};
+        BowArgs& a = j.a;
+        a.s1 = {reinterpret_cast<const orbx_keypoint*>(d + o[k].k1), d + o[k].d1, d + o[k].m1,
+                reinterpret_cast<const int32_t*>(d + o[k].f1)};
+        a.s2 = {ctx->out_kps + (size_t)slot * nf, ctx->out_desc + (size_t)slot * nf * 32, nullptr,
+                b.fv_feat + (size_t)slot * nf};
+        a.mode = 0;
+        a.nnratio = nnratio;
+        a.check_ori = check_ori;
+        a.out = reinterpret_cast<int32_t*>(d + o[k].out);
+        a.bins = reinterpret_cast<signed char*>(d + o[k].bin);
+        a.out_n = reinterpret_cast<int32_t*>(d + o[k].n);
+        j.kf_node_id = reinterpret_cast<const uint32_t*>(d + o[k].nid);
+        j.kf_node_ptr = reinterpret_cast<const int32_t*>(d + o[k].nptr);
+        j.kf_n_nodes = V.n_nodes;
+        j.f_node_id = b.fv_nodes + (size_t)slot * nf;
+        j.f_node_ptr = b.fv_ptr + (size_t)slot * (nf + 1);
+        j.f_counts = b.counts + 2 * slot;
+        j.f_n = ctx->out_n + slot;
+        j.nf = nf;
+        j.nodes = reinterpret_cast<int4*>(d + o[k].nd);
+    }
+    if ((r = put(o_jobs, jobs.data(), sizeof(BowSlotJob) * (size_t)n))) return r;
+    timer_begin(ctx, "bow_match_slot");
+    hipLaunchKernelGGL(k_bow_match_slot, dim3(n), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const BowSlotJob*>(d + o_jobs));
+    timer_end(ctx, "bow_match_slot");
+    ORBX_HIP_CHECK(hipGetLastError());
+    for (int k = 0; k < n; k++) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(matches_f[k], d + o[k].out, (size_t)nf * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(&n_matches[k], d + o[k].n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < n; k++)
+        if (n_matches[k] < 0) return ORBX_ERR_UNSUPPORTED;
+    return ORBX_OK;
 }

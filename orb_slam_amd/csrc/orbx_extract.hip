@@ -1626,6 +1626,7 @@ namespace orbx {
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
 {
     const Geometry& g = ctx->geom;
+    for (int sl = first; sl < first + count && sl < (int)ctx->bow_ready.size(); sl++) ctx->bow_ready[sl] = 0;
     ExtractArgs a;
     a.levels = ctx->dgeom.levels;
     a.cells = ctx->dgeom.cells;

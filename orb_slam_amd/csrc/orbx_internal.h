@@ -157,6 +157,24 @@ struct KernelTimer {
 struct LbaResident;   // orbx_lba.hip
 }  // namespace orbx
 
+namespace orbx {
+// Per-slot BoW of device-resident frames (orbx_dev_compute_bow), each array
+// slots x nf entries (fv_ptr: slots x (nf + 1); counts: slots x 2 =
+// n_words, n_fv_nodes).
+constexpr int kBowSortMax = 4096;   // features per frame the block sort holds
+struct SlotBowDev {
+    int32_t* word;
+    double* weight;
+    int32_t* node;
+    uint32_t* fv_nodes;
+    int32_t* fv_ptr;
+    int32_t* fv_feat;
+    uint32_t* bow_words;
+    double* bow_values;
+    int32_t* counts;
+};
+}  // namespace orbx
+
 struct orbx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -247,6 +265,12 @@ struct orbx_ctx {
     std::vector<int32_t> pose_edge_kp;     // edge -> keypoint index (frame-local)
     std::vector<long long> pose_e0;        // first edge of each frame
     bool pose_ran = false;
+    // per-slot BoW (orbx_vocab.hip): one allocation carved into bow; a
+    // slot's entry of bow_ready is cleared when the slot is extracted again
+    void* bow_dev = nullptr;
+    int bow_nf = 0;
+    orbx::SlotBowDev bow = {};
+    std::vector<uint8_t> bow_ready;
     // timing
     bool timing = false;
     std::string timing_only;   // non-empty: only this timer records (orbx_dev_kernel_time_select)

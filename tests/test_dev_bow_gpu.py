@@ -1,0 +1,177 @@
+"""Device-resident BoW of extracted frames through the C ABI against the CPU
+restatement: orbx_dev_compute_bow (Frame::ComputeBoW, src/Frame.cc:279-286,
+as TemplatedVocabulary::transform, Thirdparty/DBoW2/DBoW2/
+TemplatedVocabulary.h:1127-1259) must give the oracle transform's
+per-feature results, BowVector (values bit-identical) and FeatureVector;
+orbx_dev_search_by_bow (Tracking::Relocalisation's loop, src/Tracking.cc:
+904-925, over ORBmatcher::SearchByBoW(KF, F), src/ORBmatcher.cc:155-283)
+must give the oracle's match vectors and counts for every candidate."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth
+from bow_data import BowView
+from test_bow_oracle import run_ref as ref_search
+from vocab_data import make_vocab, run_ref as ref_transform
+
+pytestmark = pytest.mark.gpu
+
+W, H = 640, 480
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = ox.Context(nfeatures=1000, max_w=W, max_h=H, slots=4)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def extracted(ctx):
+    frames = synth.sequence(W, H, 3, seed=91)
+    ctx.upload(np.stack(frames), 0)
+    ctx.upload(synth.texture_frame(W, H, seed=5), 3)
+    ctx.extract(0, 4)
+    ctx.sync()
+    return [ctx.features(s) for s in range(4)]
+
+
+def create_vocab(ctx, V):
+    voc = ctypes.c_void_p()
+    assert ox.lib().orbx_vocab_create(ctx.handle, V["k"], V["L"], len(V["parent"]), ox._ptr(V["parent"]),
+                                      ox._ptr(V["is_leaf"]), ox._ptr(V["desc"]), ox._ptr(V["weight"]),
+                                      ctypes.byref(voc)) == 0
+    return voc
+
+
+def read_bow(ctx, slot, n):
+    out = {"word": np.zeros(n, np.int32), "weight": np.zeros(n), "nid": np.zeros(n, np.int32),
+           "bw": np.zeros(n, np.uint32), "bv": np.zeros(n), "fn": np.zeros(n, np.uint32),
+           "fp": np.zeros(n + 1, np.int32), "ff": np.zeros(n, np.int32)}
+    nw, nf = ctypes.c_int(), ctypes.c_int()
+    r = ox.lib().orbx_dev_read_bow(ctx.handle, slot, n, ox._ptr(out["word"]), ox._ptr(out["weight"]),
+                                   ox._ptr(out["nid"]), ox._ptr(out["bw"]), ox._ptr(out["bv"]), ctypes.byref(nw),
+                                   ox._ptr(out["fn"]), ox._ptr(out["fp"]), ox._ptr(out["ff"]), ctypes.byref(nf))
+    assert r == 0, r
+    out["nw"], out["nf"] = nw.value, nf.value
+    return out
+
+
+def view(kps, desc, mp, T):
+    """orbx_bow_view over a frame and its transform result T (FeatureVector CSR)."""
+    nn = T["nf"]
+    arrs = {"kps": np.ascontiguousarray(kps), "desc": np.ascontiguousarray(desc, np.uint8),
+            "mp": np.ascontiguousarray(mp, np.uint8), "ids": T["fn"][:nn].copy(), "ptr": T["fp"][:nn + 1].copy(),
+            "feat": T["ff"][:max(int(T["fp"][nn]), 1)].copy()}
+    v = BowView()
+    v.keys = arrs["kps"].ctypes.data
+    v.desc = arrs["desc"].ctypes.data
+    v.n = len(kps)
+    v.mp = arrs["mp"].ctypes.data
+    v.n_nodes = nn
+    v.node_id = arrs["ids"].ctypes.data if nn else None
+    v.node_ptr = arrs["ptr"].ctypes.data
+    v.feat_idx = arrs["feat"].ctypes.data
+    return v, arrs
+
+
+def search(ctx, slot, KFs, nnratio, check_ori, cap=None):
+    cap = cap or ctx.nfeatures
+    outs = [np.zeros(cap, np.int32) for _ in KFs]
+    ptrs = (ctypes.c_void_p * max(len(KFs), 1))(*[o.ctypes.data for o in outs])
+    arr = (BowView * max(len(KFs), 1))(*KFs)
+    nm = np.zeros(max(len(KFs), 1), np.int32)
+    r = ox.lib().orbx_dev_search_by_bow(ctx.handle, slot, len(KFs), arr, nnratio, check_ori, ptrs, cap,
+                                        ox._ptr(nm))
+    return r, outs, nm[:len(KFs)]
+
+
+# (k, L, levelsup): FeatureVector at level L - levelsup (100 nodes at level
+# 2 as with ORBvoc and levelsup 4; 10 wide nodes at level 1)
+VOCABS = [(10, 5, 3), (10, 5, 4), (6, 5, 2)]
+
+
+@pytest.mark.parametrize("k,L,levelsup", VOCABS)
+def test_dev_compute_bow_matches_oracle(ctx, extracted, k, L, levelsup):
+    V = make_vocab(k=k, L=L, seed=k + L, irregular=k == 6)
+    voc = create_vocab(ctx, V)
+    try:
+        assert ox.lib().orbx_dev_compute_bow(ctx.handle, voc, 0, 4, levelsup) == 0
+        for s in range(4):
+            kps, desc = extracted[s]
+            n = len(kps)
+            assert n > 500
+            r = ref_transform(V, desc, levelsup)
+            g = read_bow(ctx, s, n)
+            for key in ["word", "weight", "nid"]:
+                assert np.array_equal(g[key], r[key]), (s, key)
+            assert g["nw"] == r["nw"] and g["nf"] == r["nf"]
+            assert np.array_equal(g["bw"][:r["nw"]], r["bw"][:r["nw"]])
+            assert np.array_equal(g["bv"][:r["nw"]].view(np.uint64), r["bv"][:r["nw"]].view(np.uint64))
+            assert np.array_equal(g["fn"][:r["nf"]], r["fn"][:r["nf"]])
+            assert np.array_equal(g["fp"][:r["nf"] + 1], r["fp"][:r["nf"] + 1])
+            m = int(r["fp"][r["nf"]])
+            assert np.array_equal(g["ff"][:m], r["ff"][:m])
+    finally:
+        ox.lib().orbx_vocab_destroy(voc)
+
+
+@pytest.mark.parametrize("k,L,levelsup", VOCABS)
+@pytest.mark.parametrize("check_ori,nnratio", [(1, 0.75), (0, 0.9)])
+def test_dev_search_by_bow_matches_oracle(ctx, extracted, k, L, levelsup, check_ori, nnratio):
+    V = make_vocab(k=k, L=L, seed=k + L, irregular=k == 6)
+    voc = create_vocab(ctx, V)
+    try:
+        rng = np.random.default_rng(k * 100 + L * 10 + levelsup)
+        assert ox.lib().orbx_dev_compute_bow(ctx.handle, voc, 0, 1, levelsup) == 0
+        fk, fd = extracted[0]
+        Fv, fa = view(fk, fd, np.zeros(len(fk), np.uint8), ref_transform(V, fd, levelsup))
+        # candidates: the next frames of the sequence, an unrelated frame and
+        # the frame itself, map-point states random
+        KFs, keep = [], []
+        for s in (1, 2, 3, 0):
+            kk, kd = extracted[s]
+            mp = rng.choice(3, len(kk), p=(0.3, 0.6, 0.1)).astype(np.uint8)
+            v, a = view(kk, kd, mp, ref_transform(V, kd, levelsup))
+            KFs.append(v)
+            keep.append(a)
+        r, outs, nm = search(ctx, 0, KFs, nnratio, check_ori)
+        assert r == 0, r
+        for i, KF in enumerate(KFs):
+            ro, rn = ref_search(0, {"V1": KF, "V2": Fv}, nnratio, check_ori)
+            assert nm[i] == rn, (i, nm[i], rn)
+            assert np.array_equal(outs[i][:len(fk)], ro), (i, np.count_nonzero(outs[i][:len(fk)] != ro))
+            assert np.all(outs[i][len(fk):] == -1)
+        assert nm[3] > 100   # the frame against itself
+    finally:
+        ox.lib().orbx_vocab_destroy(voc)
+
+
+def test_dev_bow_state_and_errors(ctx, extracted):
+    V = make_vocab(k=10, L=4, seed=3)
+    voc = create_vocab(ctx, V)
+    try:
+        L = ox.lib()
+        assert L.orbx_dev_compute_bow(ctx.handle, voc, 0, 2, 2) == 0
+        n = len(extracted[1][0])
+        read_bow(ctx, 1, n)
+        assert L.orbx_dev_read_bow(ctx.handle, 1, n - 1, None, None, None, None, None, None, None, None, None,
+                                   None) == -3
+        assert L.orbx_dev_compute_bow(ctx.handle, voc, 3, 2, 2) == -1   # past the slots
+        assert search(ctx, 0, [], 0.75, 1)[0] == 0                                   # no candidates
+        assert search(ctx, 0, [BowView()], 0.75, 1, cap=10)[0] == -3
+        # re-extracting a slot drops its BoW until computed again
+        ctx.extract(1, 1)
+        assert L.orbx_dev_read_bow(ctx.handle, 1, n, None, None, None, None, None, None, None, None, None,
+                                   None) == -1
+        assert search(ctx, 1, [BowView()], 0.75, 1)[0] == -1
+        assert L.orbx_dev_compute_bow(ctx.handle, voc, 1, 1, 2) == 0
+        read_bow(ctx, 1, n)
+        # an empty keyframe matches nothing
+        r, outs, nm = search(ctx, 0, [BowView()], 0.75, 1)
+        assert r == 0 and nm[0] == 0 and np.all(outs[0] == -1)
+    finally:
+        ox.lib().orbx_vocab_destroy(voc)
