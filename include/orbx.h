@@ -523,6 +523,25 @@ int orbx_dev_read_bow(orbx_ctx* ctx, int slot, int cap, int32_t* word_id, double
  * per frame keypoint the KF keypoint index or -1, as orbx_search_by_bow_frame. */
 int orbx_dev_search_by_bow(orbx_ctx* ctx, int slot, int n, const orbx_bow_view* KFs, float nnratio,
                            int check_ori, int32_t* const* matches_f, int cap, int* n_matches);
+/* The keyframe-pair searches between device-resident frames, the keyframe
+ * in slot1 against those in slots2[0, n) (keypoints as the slots hold them,
+ * mvKeysUn after orbx_dev_undistort; FeatureVectors from
+ * orbx_dev_compute_bow on every slot named): SearchByBoW(KF1, KF2)
+ * (src/ORBmatcher.cc:715-850) as LoopClosing::ComputeSim3's candidate loop
+ * (src/LoopClosing.cc:240) runs it, and SearchForTriangulation (:852-1014)
+ * as LocalMapping::CreateNewMapPoints' neighbour loop (src/LocalMapping.cc:
+ * 220-260) does (F12s n x 9, sigma2_2s n x nlevels, nlevels the
+ * extractor's).  Only the map-point states travel: mp1 and mp2s[k] hold one
+ * state per keypoint of the slot (0 none, 1 map point, 2 isBad()).
+ * matches12[k] (cap >= nfeatures entries): per slot1 keypoint the slots2[k]
+ * keypoint or -1, as the host-array forms. */
+int orbx_dev_search_by_bow_kf(orbx_ctx* ctx, int slot1, const uint8_t* mp1, int n, const int* slots2,
+                              const uint8_t* const* mp2s, float nnratio, int check_ori,
+                              int32_t* const* matches12, int cap, int* n_matches);
+int orbx_dev_search_for_triangulation(orbx_ctx* ctx, int slot1, const uint8_t* mp1, int n, const int* slots2,
+                                      const uint8_t* const* mp2s, const float* F12s, const float* sigma2_2s,
+                                      int nlevels, int check_ori, int32_t* const* matches12, int cap,
+                                      int* n_matches);
 
 /* ------------------------------------------------------------------------ */
 /* C. Local bundle adjustment                                                */

@@ -119,6 +119,8 @@ def _declare(L):
         "orbx_dev_compute_bow": ([vp, vp, i, i, i], i),
         "orbx_dev_read_bow": ([vp, i, i, vp, vp, vp, vp, vp, ip, vp, vp, vp, ip], i),
         "orbx_dev_search_by_bow": ([vp, i, i, vp, f, i, vp, i, vp], i),
+        "orbx_dev_search_by_bow_kf": ([vp, i, vp, i, vp, vp, f, i, vp, i, vp], i),
+        "orbx_dev_search_for_triangulation": ([vp, i, vp, i, vp, vp, vp, vp, i, i, vp, i, vp], i),
         "orbx_undistort_keypoints": ([vp, i, vp, vp, vp, vp], i),
         "orbx_compute_image_bounds": ([i, i, vp, vp, vp], i),
         "orbx_dev_undistort": ([vp, i, i, vp, vp], i),

@@ -191,8 +191,10 @@ __global__ __launch_bounds__(256) void k_bow_match(BowArgs a) { bow_match_block(
 // One workgroup per job (one keyframe pair each).
 __global__ __launch_bounds__(256) void k_bow_match_jobs(const BowArgs* jobs) { bow_match_block(jobs[blockIdx.x]); }
 
-// SearchByBoW(KF, F) against a device-resident frame (orbx_dev_search_by_bow):
-// F's FeatureVector comes from k_bow_build, so the common nodes are found
+// SearchByBoW(KF, F) against a device-resident frame (orbx_dev_search_by_bow),
+// and the keyframe-pair searches between device-resident frames
+// (orbx_dev_search_by_bow_kf, orbx_dev_search_for_triangulation): the
+// slots' FeatureVectors come from k_bow_build, so the common nodes are found
 // here.  Each KF node binary-searches F's ascending node ids; hits are
 // compacted in KF node order (the reference's merge order), then the job
 // runs as bow_match_block.
@@ -201,12 +203,13 @@ struct BowSlotJob {
     const uint32_t* kf_node_id;
     const int32_t* kf_node_ptr;
     int kf_n_nodes;
+    const int32_t* kf_counts;  // side 1 a slot too: its (n_words, n_fv_nodes), else null
     const uint32_t* f_node_id;
     const int32_t* f_node_ptr;
     const int32_t* f_counts;   // (n_words, n_fv_nodes)
-    const int32_t* f_n;        // slot feature count
+    const int32_t* out_count;  // feature count of the side the output is indexed by
     int nf;
-    int4* nodes;               // [kf_n_nodes] scratch
+    int4* nodes;               // [side-1 nodes] scratch
 };
 
 __global__ __launch_bounds__(256) void k_bow_match_slot(const BowSlotJob* jobs)
@@ -214,9 +217,9 @@ __global__ __launch_bounds__(256) void k_bow_match_slot(const BowSlotJob* jobs)
     __shared__ BlockScratch bs;
     __shared__ int s_bad;
     const BowSlotJob& j = jobs[blockIdx.x];
-    const int tid = threadIdx.x, nfv = j.f_counts[1];
+    const int tid = threadIdx.x, nfv = j.f_counts[1], nkf = j.kf_counts ? j.kf_counts[1] : j.kf_n_nodes;
     if (tid == 0) s_bad = 0;
-    const int per = (j.kf_n_nodes + kBlock - 1) / kBlock, k0 = tid * per, k1 = min(k0 + per, j.kf_n_nodes);
+    const int per = (nkf + kBlock - 1) / kBlock, k0 = tid * per, k1 = min(k0 + per, nkf);
     auto find = [&](uint32_t id) {
         int lo = 0, hi = nfv;
         while (lo < hi) {
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(256) void k_bow_match_slot(const BowSlotJob* jobs)
     BowArgs a = j.a;
     a.nodes = j.nodes;
     a.n_common = total;
-    a.out_len = min(*j.f_n, j.nf);
+    a.out_len = min(*j.out_count, j.nf);
     bow_match_block(a);
 }
 
@@ -586,7 +589,7 @@ extern "C" int orbx_dev_search_by_bow(orbx_ctx* ctx, int slot, int n, const orbx
         j.f_node_id = b.fv_nodes + (size_t)slot * nf;
         j.f_node_ptr = b.fv_ptr + (size_t)slot * (nf + 1);
         j.f_counts = b.counts + 2 * slot;
-        j.f_n = ctx->out_n + slot;
+        j.out_count = ctx->out_n + slot;
         j.nf = nf;
         j.nodes = reinterpret_cast<int4*>(d + o[k].nd);
     }
@@ -604,4 +607,130 @@ extern "C" int orbx_dev_search_by_bow(orbx_ctx* ctx, int slot, int n, const orbx
     for (int k = 0; k < n; k++)
         if (n_matches[k] < 0) return ORBX_ERR_UNSUPPORTED;
     return ORBX_OK;
+}
+
+namespace {
+
+// SearchByBoW(KF1, KF2) (mode 1) / SearchForTriangulation (mode 2) of the
+// frame in slot1 against the frames in slots2[0, n): keypoints, descriptors
+// and FeatureVectors where orbx_dev_extract / orbx_dev_undistort /
+// orbx_dev_compute_bow left them; only the map-point states travel.
+int run_bow_slots(orbx_ctx* ctx, int mode, int slot1, const uint8_t* mp1, int n, const int* slots2,
+                  const uint8_t* const* mp2s, float nnratio, int check_ori, const float* F12s, const float* sigma2s,
+                  int nlevels, int32_t* const* outs, int cap, int* n_outs)
+{
+    auto ready = [&](int s) {
+        return s >= 0 && s < ctx->slots && ctx->bow_dev && s < (int)ctx->bow_ready.size() && ctx->bow_ready[s];
+    };
+    if (n < 0 || (n > 0 && (!slots2 || !mp2s || !outs || !n_outs || !mp1))) return ORBX_ERR_ARG;
+    if (mode == 2 && n > 0 && (!F12s || !sigma2s || nlevels <= 0 || nlevels > kMaxLevels)) return ORBX_ERR_ARG;
+    if (!ready(slot1)) return ORBX_ERR_ARG;
+    for (int k = 0; k < n; k++)
+        if (!ready(slots2[k]) || !mp2s[k] || !outs[k]) return ORBX_ERR_ARG;
+    const int nf = ctx->bow_nf;
+    if (n > 0 && cap < nf) return ORBX_ERR_CAPACITY;
+    if (n == 0) return ORBX_OK;
+    ctx_enter(ctx);
+    // the slots' feature counts bound the map-point arrays the caller passes
+    std::vector<int32_t> cnt(ctx->slots);
+    ORBX_HIP_CHECK(hipMemcpyAsync(cnt.data(), ctx->out_n, sizeof(int32_t) * ctx->slots, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    auto count = [&](int s) { return std::min<int>(cnt[s], nf); };
+    size_t at = 0;
+    auto res = [&](size_t bytes) {
+        const size_t o = at;
+        at += al256(std::max<size_t>(bytes, 1));
+        return o;
+    };
+    const size_t o_m1 = res(nf);
+    struct Off {
+        size_t m2, nd, out, bin, n;
+    };
+    std::vector<Off> o(n);
+    for (int k = 0; k < n; k++) {
+        o[k].m2 = res(nf);
+        o[k].nd = res((size_t)nf * sizeof(int4));
+        o[k].out = res((size_t)nf * 4);
+        o[k].bin = res(nf);
+        o[k].n = res(4);
+    }
+    const size_t o_jobs = res(sizeof(BowSlotJob) * (size_t)n);
+    int r = ensure_scratch(ctx, at);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = static_cast<uint8_t*>(ctx->scratch);
+    if (count(slot1) > 0)
+        ORBX_HIP_CHECK(hipMemcpyAsync(d + o_m1, mp1, count(slot1), hipMemcpyHostToDevice, ctx->stream));
+    const SlotBowDev& b = ctx->bow;
+    std::vector<BowSlotJob> jobs(n);
+    for (int k = 0; k < n; k++) {
+        const int s2 = slots2[k];
+        if (count(s2) > 0)
+            ORBX_HIP_CHECK(hipMemcpyAsync(d + o[k].m2, mp2s[k], count(s2), hipMemcpyHostToDevice, ctx->stream));
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].out, 0xFF, (size_t)nf * 4, ctx->stream));
+        ORBX_HIP_CHECK(hipMemsetAsync(d + o[k].bin, 0xFF, (size_t)nf, ctx->stream));
+        BowSlotJob& j = jobs[k];
+        j = BowSlotJob{};
+        BowArgs& a = j.a;
+        a.s1 = {ctx->out_kps + (size_t)slot1 * nf, ctx->out_desc + (size_t)slot1 * nf * 32, d + o_m1,
+                b.fv_feat + (size_t)slot1 * nf};
+        a.s2 = {ctx->out_kps + (size_t)s2 * nf, ctx->out_desc + (size_t)s2 * nf * 32, d + o[k].m2,
+                b.fv_feat + (size_t)s2 * nf};
+        a.mode = mode;
+        a.nnratio = nnratio;
+        a.check_ori = check_ori;
+        if (mode == 2) {
+            for (int c = 0; c < 9; c++) a.F12[c] = F12s[9 * k + c];
+            for (int l = 0; l < nlevels; l++) a.sigma2[l] = sigma2s[(size_t)nlevels * k + l];
+        }
+        a.out = reinterpret_cast<int32_t*>(d + o[k].out);
+        a.bins = reinterpret_cast<signed char*>(d + o[k].bin);
+        a.out_n = reinterpret_cast<int32_t*>(d + o[k].n);
+        j.kf_node_id = b.fv_nodes + (size_t)slot1 * nf;
+        j.kf_node_ptr = b.fv_ptr + (size_t)slot1 * (nf + 1);
+        j.kf_counts = b.counts + 2 * slot1;
+        j.f_node_id = b.fv_nodes + (size_t)s2 * nf;
+        j.f_node_ptr = b.fv_ptr + (size_t)s2 * (nf + 1);
+        j.f_counts = b.counts + 2 * s2;
+        j.out_count = ctx->out_n + slot1;
+        j.nf = nf;
+        j.nodes = reinterpret_cast<int4*>(d + o[k].nd);
+    }
+    ORBX_HIP_CHECK(hipMemcpyAsync(d + o_jobs, jobs.data(), sizeof(BowSlotJob) * (size_t)n, hipMemcpyHostToDevice,
+                                  ctx->stream));
+    timer_begin(ctx, "bow_match_slot");
+    hipLaunchKernelGGL(k_bow_match_slot, dim3(n), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const BowSlotJob*>(d + o_jobs));
+    timer_end(ctx, "bow_match_slot");
+    ORBX_HIP_CHECK(hipGetLastError());
+    for (int k = 0; k < n; k++) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(outs[k], d + o[k].out, (size_t)nf * 4, hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipMemcpyAsync(&n_outs[k], d + o[k].n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < n; k++)
+        if (n_outs[k] < 0) return ORBX_ERR_UNSUPPORTED;
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" int orbx_dev_search_by_bow_kf(orbx_ctx* ctx, int slot1, const uint8_t* mp1, int n, const int* slots2,
+                                         const uint8_t* const* mp2s, float nnratio, int check_ori,
+                                         int32_t* const* matches12, int cap, int* n_matches)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    return run_bow_slots(ctx, 1, slot1, mp1, n, slots2, mp2s, nnratio, check_ori, nullptr, nullptr, 0, matches12, cap,
+                         n_matches);
+}
+
+extern "C" int orbx_dev_search_for_triangulation(orbx_ctx* ctx, int slot1, const uint8_t* mp1, int n,
+                                                 const int* slots2, const uint8_t* const* mp2s, const float* F12s,
+                                                 const float* sigma2_2s, int nlevels, int check_ori,
+                                                 int32_t* const* matches12, int cap, int* n_matches)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    if (n > 0 && nlevels != ctx->geom.nlevels) return ORBX_ERR_ARG;   // octaves index sigma2_2
+    return run_bow_slots(ctx, 2, slot1, mp1, n, slots2, mp2s, 0.f, check_ori, F12s, sigma2_2s, nlevels, matches12,
+                         cap, n_matches);
 }

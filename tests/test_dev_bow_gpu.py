@@ -175,3 +175,96 @@ def test_dev_bow_state_and_errors(ctx, extracted):
         assert r == 0 and nm[0] == 0 and np.all(outs[0] == -1)
     finally:
         ox.lib().orbx_vocab_destroy(voc)
+
+
+def search_kf(ctx, mode, slot1, mp1, slots2, mp2s, nnratio=0.75, check_ori=1, F12s=None, sigma2s=None, cap=None):
+    cap = cap or ctx.nfeatures
+    n = len(slots2)
+    outs = [np.zeros(cap, np.int32) for _ in range(n)]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[o.ctypes.data for o in outs])
+    mps = (ctypes.c_void_p * max(n, 1))(*[m.ctypes.data for m in mp2s])
+    s2 = np.ascontiguousarray(slots2, np.int32)
+    nm = np.zeros(max(n, 1), np.int32)
+    L = ox.lib()
+    if mode == 1:
+        r = L.orbx_dev_search_by_bow_kf(ctx.handle, slot1, ox._ptr(mp1), n, ox._ptr(s2), mps, nnratio, check_ori, ptrs,
+                                        cap, ox._ptr(nm))
+    else:
+        r = L.orbx_dev_search_for_triangulation(ctx.handle, slot1, ox._ptr(mp1), n, ox._ptr(s2), mps, ox._ptr(F12s),
+                                                ox._ptr(sigma2s), 8, check_ori, ptrs, cap, ox._ptr(nm))
+    return r, outs, nm[:n]
+
+
+def translation_f12(dx, dy):
+    """F12 of a pure image translation (dx, dy): the epipolar line of kp1 is
+    the line through it along (dx, dy) (a = -dy, b = dx, c = x dy - y dx)."""
+    return np.array([0, 0, dy, 0, 0, -dx, -dy, dx, 0], np.float32)
+
+
+def level_sigma2(nlevels=8, scale=1.2):
+    s, out = np.float32(1.0), []
+    for _ in range(nlevels):
+        out.append(np.float32(s * s))
+        s = np.float32(s * np.float32(scale))
+    return np.array(out, np.float32)
+
+
+@pytest.mark.parametrize("k,L,levelsup", VOCABS[:2])
+@pytest.mark.parametrize("mode", [1, 2], ids=["bow_kf", "triangulation"])
+@pytest.mark.parametrize("check_ori", [1, 0])
+def test_dev_kf_searches_match_oracle(ctx, extracted, k, L, levelsup, mode, check_ori):
+    V = make_vocab(k=k, L=L, seed=k + L, irregular=False)
+    voc = create_vocab(ctx, V)
+    try:
+        rng = np.random.default_rng(7 * k + L + mode)
+        assert ox.lib().orbx_dev_compute_bow(ctx.handle, voc, 0, 4, levelsup) == 0
+        probs = (0.3, 0.6, 0.1) if mode == 1 else (0.6, 0.3, 0.1)
+        views, mps = [], []
+        for s in range(4):
+            kk, kd = extracted[s]
+            mp = rng.choice(3, len(kk), p=probs).astype(np.uint8)
+            views.append(view(kk, kd, mp, ref_transform(V, kd, levelsup)))
+            mps.append(mp)
+        slots2 = [1, 2, 3, 0]
+        F12s = np.concatenate([translation_f12(1.0, 0.3 * s) for s in slots2]).astype(np.float32)
+        sig = level_sigma2()
+        sigma2s = np.tile(sig, len(slots2)).astype(np.float32)
+        r, outs, nm = search_kf(ctx, mode, 0, mps[0], slots2, [mps[s] for s in slots2], 0.75, check_ori, F12s, sigma2s)
+        assert r == 0, r
+        n1 = len(extracted[0][0])
+        for i, s in enumerate(slots2):
+            P = {"V1": views[0][0], "V2": views[s][0], "F12": F12s[9 * i:9 * i + 9].copy(), "sigma2": sig}
+            ro, rn = ref_search(mode, P, 0.75, check_ori)
+            assert nm[i] == rn, (i, nm[i], rn)
+            assert np.array_equal(outs[i][:n1], ro), (i, np.count_nonzero(outs[i][:n1] != ro))
+            assert np.all(outs[i][n1:] == -1)
+        assert nm[3] > 50   # slot 0 against itself
+    finally:
+        ox.lib().orbx_vocab_destroy(voc)
+
+
+def test_dev_kf_search_errors(ctx, extracted):
+    V = make_vocab(k=10, L=4, seed=3)
+    voc = create_vocab(ctx, V)
+    try:
+        L = ox.lib()
+        mp = np.ones(ctx.nfeatures, np.uint8)
+        assert L.orbx_dev_compute_bow(ctx.handle, voc, 0, 2, 2) == 0
+        assert search_kf(ctx, 1, 0, mp, [], [])[0] == 0
+        assert search_kf(ctx, 1, 0, mp, [1], [mp], cap=10)[0] == -3
+        ctx.extract(2, 2)                                   # slots 2, 3: no BoW
+        assert search_kf(ctx, 1, 0, mp, [2], [mp])[0] == -1
+        assert search_kf(ctx, 1, 0, mp, [4], [mp])[0] == -1   # no such slot
+        r, outs, nm = search_kf(ctx, 1, 0, mp, [1], [mp])
+        assert r == 0 and nm[0] > 0
+        F = translation_f12(1.0, 0.0)
+        assert search_kf(ctx, 2, 0, mp, [1], [mp], F12s=F, sigma2s=level_sigma2(9))[0] == 0
+        assert ox.lib().orbx_dev_search_for_triangulation(ctx.handle, 0, ox._ptr(mp), 1,
+                                                          ox._ptr(np.array([1], np.int32)),
+                                                          (ctypes.c_void_p * 1)(mp.ctypes.data), ox._ptr(F),
+                                                          ox._ptr(level_sigma2(7)), 7, 1,
+                                                          (ctypes.c_void_p * 1)(outs[0].ctypes.data), 1000,
+                                                          ox._ptr(nm)) == -1   # nlevels != the extractor's
+        assert L.orbx_dev_compute_bow(ctx.handle, voc, 2, 2, 2) == 0
+    finally:
+        ox.lib().orbx_vocab_destroy(voc)
