@@ -60,28 +60,40 @@ __global__ __launch_bounds__(256) void k_match_prev(MatchPrevArgs a)
 // each keypoint a of the previous frame, the first index of the smallest
 // Hamming distance over all keypoints of frame s and the second smallest
 // value; accept best <= th_low && best < nnratio * second (the B3 rule of
-// src/ORBmatcher.cc:640-654 applied to all pairs).  grid = (query blocks,
-// pairs); candidates stream through LDS 256 descriptors at a time.
-__global__ __launch_bounds__(256) void k_match_bf_prev(MatchPrevArgs a, int th_low)
+// src/ORBmatcher.cc:640-654 applied to all pairs).  grid = (query blocks of
+// 64, pairs); candidates stream through LDS 512 descriptors at a time, each
+// of the 8 waves scanning its own 64 (eight times the waves of one query
+// per thread over all candidates, which left ~1.3 waves per SIMD at 1080p).
+constexpr int kBfWaves = 8;   // candidate splits per query wave (k_match_bf_prev)
+
+__global__ __launch_bounds__(64 * kBfWaves) void k_match_bf_prev(MatchPrevArgs a, int th_low)
 {
-    __shared__ uint4 sb[256][2];
+    // 64 queries per workgroup; wave w scans the candidates [64 w, 64 w + 64)
+    // of every LDS chunk (an increasing subset, first strict minimum kept),
+    // then the waves' (best, index, second) merge in wave order: the two
+    // smallest values of the union are the two smallest of the waves' pairs,
+    // and an equal best keeps the lower index, as the one sequential scan does
+    constexpr int kT = 64 * kBfWaves;
+    __shared__ uint4 sb[kT][2];
+    __shared__ int mb1[kBfWaves][64], mbi[kBfWaves][64], mb2[kBfWaves][64];
     const int s = a.first + blockIdx.y;
     const int prev = (s % a.seq_len == 0) ? s + a.seq_len - 1 : s - 1;
     const int nA = a.nkp[prev], nB = a.nkp[s];
     const uint8_t* dA = a.desc + (size_t)prev * a.nfeatures * 32;
     const uint8_t* dB = a.desc + (size_t)s * a.nfeatures * 32;
-    const int q = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= nA) return;   // block-uniform
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int q = blockIdx.x * 64 + lane;
+    if (blockIdx.x * 64 >= nA) return;   // block-uniform
     uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
     if (q < nA) load_desc(dA + (size_t)q * 32, qa, qb);
     int b1 = 0x7fffffff, b2 = 0x7fffffff, bi = -1;
-    for (int base = 0; base < nB; base += 256) {
+    for (int base = 0; base < nB; base += kT) {
         __syncthreads();
         const int j = base + threadIdx.x;
         if (j < nB) load_desc(dB + (size_t)j * 32, sb[threadIdx.x][0], sb[threadIdx.x][1]);
         __syncthreads();
-        const int cnt = min(256, nB - base);
-        for (int k = 0; k < cnt; k++) {
+        const int k0 = 64 * wv, k1 = min(k0 + 64, nB - base);   // wave-uniform
+        for (int k = k0; k < k1; k++) {
             const int d = hamming256(qa, qb, sb[k][0], sb[k][1]);
             if (d < b1) {
                 b2 = b1;
@@ -92,13 +104,32 @@ __global__ __launch_bounds__(256) void k_match_bf_prev(MatchPrevArgs a, int th_l
             }
         }
     }
+    mb1[wv][lane] = b1;
+    mbi[wv][lane] = bi;
+    mb2[wv][lane] = b2;
+    __syncthreads();
+    if (wv != 0) return;
+    b1 = mb1[0][lane];
+    bi = mbi[0][lane];
+    b2 = mb2[0][lane];
+#pragma unroll
+    for (int w = 1; w < kBfWaves; w++) {
+        const int c1 = mb1[w][lane], ci = mbi[w][lane], c2 = mb2[w][lane];
+        if (c1 < b1 || (c1 == b1 && ci >= 0 && (bi < 0 || ci < bi))) {
+            b2 = min(b1, c2);
+            b1 = c1;
+            bi = ci;
+        } else {
+            b2 = min(b2, c1);
+        }
+    }
     int ok = 0;
     if (q < nA) {
         ok = (b1 <= th_low && (float)b1 < __fmul_rn((float)b2, a.nnratio));
         a.match12[(size_t)s * a.nfeatures + q] = ok ? bi : -1;
     }
     ok = wave_sum(ok);
-    if ((threadIdx.x & 63) == 0 && ok) atomicAdd(a.match_n + s, ok);
+    if (lane == 0 && ok) atomicAdd(a.match_n + s, ok);
 }
 
 #ifdef ORBX_MATCH_PROFILE
@@ -125,7 +156,7 @@ int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int t
     a.nnratio = nnratio;
     ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, st));
     timer_begin(ctx, "match", st);
-    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 255) / 256, count), dim3(256), 0, st, a, th_low);
+    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 63) / 64, count), dim3(64 * kBfWaves), 0, st, a, th_low);
     timer_end(ctx, "match", st);
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
