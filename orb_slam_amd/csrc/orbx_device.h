@@ -100,10 +100,26 @@ __device__ inline int cv_round(float v) { return __float2int_rn(v); }
 
 // ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1794-1810): Hamming
 // distance of two 256-bit descriptors = popcount of XOR.
+// (one chain of v_bcnt_u32_b32 accumulations, which add their second
+// operand; the compiler rebalances a summed form into separate counts and
+// add3s: 11 instead of 8 VALU after the xors)
+__device__ inline uint32_t bcnt_acc(uint32_t x, uint32_t acc)
+{
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 __device__ inline int hamming256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1)
 {
-    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+    uint32_t c = __builtin_popcount(a0.x ^ b0.x);
+    c = bcnt_acc(a0.y ^ b0.y, c);
+    c = bcnt_acc(a0.z ^ b0.z, c);
+    c = bcnt_acc(a0.w ^ b0.w, c);
+    c = bcnt_acc(a1.x ^ b1.x, c);
+    c = bcnt_acc(a1.y ^ b1.y, c);
+    c = bcnt_acc(a1.z ^ b1.z, c);
+    c = bcnt_acc(a1.w ^ b1.w, c);
+    return (int)c;
 }
 
 // --------------------------------------------------------------------------

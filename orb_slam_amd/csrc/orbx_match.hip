@@ -61,32 +61,41 @@ __global__ __launch_bounds__(256) void k_match_prev(MatchPrevArgs a)
 // Hamming distance over all keypoints of frame s and the second smallest
 // value; accept best <= th_low && best < nnratio * second (the B3 rule of
 // src/ORBmatcher.cc:640-654 applied to all pairs).  grid = (query blocks of
-// 64, pairs); candidates stream through LDS 512 descriptors at a time, each
-// of the 8 waves scanning its own 64 (eight times the waves of one query
-// per thread over all candidates, which left ~1.3 waves per SIMD at 1080p).
-constexpr int kBfWaves = 8;   // candidate splits per query wave (k_match_bf_prev)
+// 256, pairs); candidates stream through LDS 512 descriptors at a time, each
+// of the 8 waves scanning its own 64 for 4 queries per lane.
+constexpr int kBfWaves = 8;   // candidate splits (k_match_bf_prev)
+constexpr int kBfQ = 4;       // queries per lane
 
 __global__ __launch_bounds__(64 * kBfWaves) void k_match_bf_prev(MatchPrevArgs a, int th_low)
 {
-    // 64 queries per workgroup; wave w scans the candidates [64 w, 64 w + 64)
-    // of every LDS chunk (an increasing subset, first strict minimum kept),
-    // then the waves' (best, index, second) merge in wave order: the two
-    // smallest values of the union are the two smallest of the waves' pairs,
-    // and an equal best keeps the lower index, as the one sequential scan does
-    constexpr int kT = 64 * kBfWaves;
+    // 64 kBfQ queries per workgroup, kBfQ per lane (one LDS read of a
+    // candidate serves kBfQ distances: the broadcast ds_read_b128 pair per
+    // candidate, not the VALU, bounded the one-query-per-lane form); wave w
+    // scans the candidates [64 w, 64 w + 64) of every LDS chunk (an
+    // increasing subset, first strict minimum kept), then the waves'
+    // (best, index, second) merge in wave order: the two smallest values of
+    // the union are the two smallest of the waves' pairs, and an equal best
+    // keeps the lower index, as the one sequential scan does
+    constexpr int kT = 64 * kBfWaves, kQB = 64 * kBfQ;
     __shared__ uint4 sb[kT][2];
-    __shared__ int mb1[kBfWaves][64], mbi[kBfWaves][64], mb2[kBfWaves][64];
+    __shared__ uint32_t mk1[kBfWaves][kQB], mk2[kBfWaves][kQB];
     const int s = a.first + blockIdx.y;
     const int prev = (s % a.seq_len == 0) ? s + a.seq_len - 1 : s - 1;
     const int nA = a.nkp[prev], nB = a.nkp[s];
     const uint8_t* dA = a.desc + (size_t)prev * a.nfeatures * 32;
     const uint8_t* dB = a.desc + (size_t)s * a.nfeatures * 32;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int q = blockIdx.x * 64 + lane;
-    if (blockIdx.x * 64 >= nA) return;   // block-uniform
-    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
-    if (q < nA) load_desc(dA + (size_t)q * 32, qa, qb);
-    int b1 = 0x7fffffff, b2 = 0x7fffffff, bi = -1;
+    const int q0 = blockIdx.x * kQB;
+    if (q0 >= nA) return;   // block-uniform
+    uint4 qa[kBfQ], qb[kBfQ];
+    uint32_t kb1[kBfQ], kb2[kBfQ];
+#pragma unroll
+    for (int u = 0; u < kBfQ; u++) {
+        const int q = q0 + 64 * u + lane;
+        qa[u] = qb[u] = make_uint4(0, 0, 0, 0);
+        if (q < nA) load_desc(dA + (size_t)q * 32, qa[u], qb[u]);
+        kb1[u] = kb2[u] = 0xFFFFFFFFu;
+    }
     for (int base = 0; base < nB; base += kT) {
         __syncthreads();
         const int j = base + threadIdx.x;
@@ -94,39 +103,45 @@ __global__ __launch_bounds__(64 * kBfWaves) void k_match_bf_prev(MatchPrevArgs a
         __syncthreads();
         const int k0 = 64 * wv, k1 = min(k0 + 64, nB - base);   // wave-uniform
         for (int k = k0; k < k1; k++) {
-            const int d = hamming256(qa, qb, sb[k][0], sb[k][1]);
-            if (d < b1) {
-                b2 = b1;
-                b1 = d;
-                bi = base + k;
-            } else if (d < b2) {
-                b2 = d;
+            const uint4 c0 = sb[k][0], c1 = sb[k][1];
+            const uint32_t idx = (uint32_t)(base + k);
+#pragma unroll
+            for (int u = 0; u < kBfQ; u++) {
+                // (distance << 16 | index) keys: the best is the smallest key
+                // (first index of the smallest distance), the second
+                // smallest distance of the multiset is min(second, max(best,
+                // this)) taken on keys (equal distances differ in the index
+                // only)
+                const uint32_t key = ((uint32_t)hamming256(qa[u], qb[u], c0, c1) << 16) | idx;
+                kb2[u] = min(kb2[u], max(kb1[u], key));
+                kb1[u] = min(kb1[u], key);
             }
         }
     }
-    mb1[wv][lane] = b1;
-    mbi[wv][lane] = bi;
-    mb2[wv][lane] = b2;
-    __syncthreads();
-    if (wv != 0) return;
-    b1 = mb1[0][lane];
-    bi = mbi[0][lane];
-    b2 = mb2[0][lane];
 #pragma unroll
-    for (int w = 1; w < kBfWaves; w++) {
-        const int c1 = mb1[w][lane], ci = mbi[w][lane], c2 = mb2[w][lane];
-        if (c1 < b1 || (c1 == b1 && ci >= 0 && (bi < 0 || ci < bi))) {
-            b2 = min(b1, c2);
-            b1 = c1;
-            bi = ci;
-        } else {
-            b2 = min(b2, c1);
-        }
+    for (int u = 0; u < kBfQ; u++) {
+        mk1[wv][64 * u + lane] = kb1[u];
+        mk2[wv][64 * u + lane] = kb2[u];
     }
+    __syncthreads();
+    // merge: thread t < kQB finalises query q0 + t
     int ok = 0;
-    if (q < nA) {
-        ok = (b1 <= th_low && (float)b1 < __fmul_rn((float)b2, a.nnratio));
-        a.match12[(size_t)s * a.nfeatures + q] = ok ? bi : -1;
+    const int t = threadIdx.x;
+    if (t < kQB) {
+        uint32_t r1 = mk1[0][t], r2 = mk2[0][t];
+#pragma unroll
+        for (int w = 1; w < kBfWaves; w++) {
+            const uint32_t c1 = mk1[w][t], c2 = mk2[w][t];
+            r2 = min(min(r2, c2), max(r1, c1));
+            r1 = min(r1, c1);
+        }
+        const int q = q0 + t;
+        if (q < nA) {
+            // no candidate: key ~0 (distance 0xFFFF, never accepted)
+            const int d1 = (int)(r1 >> 16), d2 = r2 == 0xFFFFFFFFu ? 0x7fffffff : (int)(r2 >> 16);
+            ok = (d1 <= th_low && (float)d1 < __fmul_rn((float)d2, a.nnratio));
+            a.match12[(size_t)s * a.nfeatures + q] = ok ? (int)(r1 & 0xFFFF) : -1;
+        }
     }
     ok = wave_sum(ok);
     if (lane == 0 && ok) atomicAdd(a.match_n + s, ok);
@@ -156,7 +171,8 @@ int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int t
     a.nnratio = nnratio;
     ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, st));
     timer_begin(ctx, "match", st);
-    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 63) / 64, count), dim3(64 * kBfWaves), 0, st, a, th_low);
+    hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 64 * kBfQ - 1) / (64 * kBfQ), count), dim3(64 * kBfWaves), 0,
+                       st, a, th_low);
     timer_end(ctx, "match", st);
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
