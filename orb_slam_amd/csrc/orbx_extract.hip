@@ -524,6 +524,13 @@ __host__ __device__ constexpr int fast_static_lds(bool u32_entries) { return 4 *
 #define ORBX_FAST_LDS_TARGET (40 * 1024)   // 4 workgroups per CU
 #endif
 constexpr int kFastLdsTarget = ORBX_FAST_LDS_TARGET;
+// Diagnostic builds only (-DORBX_DIAG_REPEAT=r,b,d,f): launch resize, blur,
+// describe or FAST that many times (idempotent kernels) to price each
+// stage's marginal cost inside the pipelined bench.
+#ifndef ORBX_DIAG_REPEAT
+#define ORBX_DIAG_REPEAT 1, 1, 1, 1
+#endif
+constexpr int kDiagRepeat[4] = {ORBX_DIAG_REPEAT};
 
 // kP > 0: compile-time tile pitch (>= every cell's aligned row), so ring
 // offsets and row strides are immediates; kP == 0: per-cell pitch.
@@ -1701,8 +1708,9 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 const int threads = std::min(256, ((L.stride / 4) + 63) & ~63);
                 const ResizeLevel rl{L.off, P.off, L.stride, P.stride, L.w, L.h, L.pw, L.ph, P.h, L.nvec_resize,
                                      L.res_span, L.res_strip_off, L.res_row_off, L.res_col_off};
-                hipLaunchKernelGGL(k_pyr_resize_lds, dim3((L.ph + kResRows - 1) / kResRows, nb), dim3(threads), lds, st,
-                                   x, rl, pitch);
+                for (int rep = 0; rep < kDiagRepeat[0]; rep++)
+                    hipLaunchKernelGGL(k_pyr_resize_lds, dim3((L.ph + kResRows - 1) / kResRows, nb), dim3(threads), lds,
+                                       st, x, rl, pitch);
             } else {   // very wide levels: per-pixel gathers from global memory
                 const int items = (L.stride / 4) * ((L.ph + kPyrRows - 1) / kPyrRows);
                 hipLaunchKernelGGL(k_pyr_resize, dim3((items + 255) / 256, nb), dim3(256), 0, st, x, l);
@@ -1760,7 +1768,9 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 return bytes <= 65536;
             };
             if (fits(96)) fast(k_fast_cells<96>, bytes, 0, 256);
-            else if (fits(144)) fast(k_fast_cells<144>, bytes, 0, 256);
+            else if (fits(144)) {
+                for (int rep = 0; rep < kDiagRepeat[3]; rep++) fast(k_fast_cells<144>, bytes, 0, 256);
+            }
             else if (fits(208)) fast(k_fast_cells<208>, bytes, 0, 256);
             else if (fits_banded(336)) fast(k_fast_cells<336, kFastWideThreads, true>, bytes, br, kFastWideThreads);
             else {
@@ -1799,15 +1809,18 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         if (!(parts & 4)) return;
         if (!fused) {
             timer_begin(ctx, "blur", st);
-            hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
+            for (int rep = 0; rep < kDiagRepeat[1]; rep++)
+                hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
             timer_end(ctx, "blur", st);
         }
         timer_begin(ctx, "describe", st);
         const dim3 dgrid((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), xcd_frames(nb));
-        if (x.fp_contract)
-            hipLaunchKernelGGL(k_describe<true>, dgrid, dim3(256), 0, st, x, nb);
-        else
-            hipLaunchKernelGGL(k_describe<false>, dgrid, dim3(256), 0, st, x, nb);
+        for (int rep = 0; rep < kDiagRepeat[2]; rep++) {
+            if (x.fp_contract)
+                hipLaunchKernelGGL(k_describe<true>, dgrid, dim3(256), 0, st, x, nb);
+            else
+                hipLaunchKernelGGL(k_describe<false>, dgrid, dim3(256), 0, st, x, nb);
+        }
         timer_end(ctx, "describe", st);
     };
     auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
