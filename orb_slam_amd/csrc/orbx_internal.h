@@ -46,7 +46,10 @@ constexpr int kBlurStrip = ORBX_BLUR_STRIP;   // output rows per blur thread (ro
 constexpr int kBlurItems = 256;  // blur threads per block (4 waves, one (strip, column chunk) each)
 constexpr int kBlurChunkCols = 62;   // output dword columns per blur wave (+ one halo lane each side)
 
-constexpr int kResRows = 16;   // output rows per staged resize strip (k_pyr_resize_lds)
+#ifndef ORBX_RES_ROWS
+#define ORBX_RES_ROWS 16
+#endif
+constexpr int kResRows = ORBX_RES_ROWS;   // output rows per staged resize strip (k_pyr_resize_lds)
 
 struct LevelGeom {
     int w, h;             // level size
