@@ -345,11 +345,15 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
             for (int b = 0; b < 4; b++) S[b] = base[ca[b]] * a0[b] + base[ca[b] + 1] * a1[b];
         };
         int H0[4], H1[4], c0 = -1, c1 = -1;
+        // the next row's table entry is read while this row is computed
+        // (its LDS round trip then overlaps the source reads of this row)
+        uint2 nxt = reinterpret_cast<const uint2*>(s_rows)[0];
         for (int rr = 0; rr < nrows; rr++) {
-            const int sy0 = __builtin_amdgcn_readfirstlane(s_rows[rr].sy0);
-            const int sy1 = __builtin_amdgcn_readfirstlane(s_rows[rr].sy1);
-            const int b0 = __builtin_amdgcn_readfirstlane(s_rows[rr].b0);
-            const int b1 = __builtin_amdgcn_readfirstlane(s_rows[rr].b1);
+            const uint2 cur = nxt;
+            if (rr + 1 < nrows) nxt = reinterpret_cast<const uint2*>(s_rows)[rr + 1];
+            const uint32_t w0 = __builtin_amdgcn_readfirstlane(cur.x), w1 = __builtin_amdgcn_readfirstlane(cur.y);
+            const int sy0 = (int)(int16_t)(w0 & 0xFFFF), sy1 = (int)(int16_t)(w0 >> 16);
+            const int b0 = (int)(int16_t)(w1 & 0xFFFF), b1 = (int)(int16_t)(w1 >> 16);
             int A[4], B[4];
             if (sy0 == c1) {
 #pragma unroll
