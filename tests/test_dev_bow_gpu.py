@@ -268,3 +268,49 @@ def test_dev_kf_search_errors(ctx, extracted):
         assert L.orbx_dev_compute_bow(ctx.handle, voc, 2, 2, 2) == 0
     finally:
         ox.lib().orbx_vocab_destroy(voc)
+
+
+def test_dev_bow_after_async_pipeline():
+    """orbx_dev_compute_bow right after an asynchronous, three-part
+    extract_match (no sync in between) sees the finished extraction: the BoW
+    of every slot equals the oracle transform of the slot's descriptors, and
+    a Relocalisation search over the batch's frames equals the oracle's."""
+    B = 48   # three pipeline parts
+    c = ox.Context(nfeatures=1000, max_w=W, max_h=H, slots=2 * B)
+    try:
+        V = make_vocab(k=10, L=5, seed=15)
+        voc = create_vocab(c, V)
+        frames = np.stack(synth.sequence(W, H, B, seed=123))
+        c.upload(frames, 0)
+        c.upload(frames[::-1].copy(), B)
+        c.set_async_match(True)
+        c.extract_match(0, B, B)
+        c.extract_match(B, B, B)          # the other range: the first batch's match may still run
+        L = ox.lib()
+        assert L.orbx_dev_compute_bow(c.handle, voc, 0, 2 * B, 4) == 0
+        c.sync()
+        rng = np.random.default_rng(5)
+        for s in (0, 15, 16, 31, 32, 47, B, 2 * B - 1):
+            kps, desc = c.features(s)
+            r = ref_transform(V, desc, 4)
+            g = read_bow(c, s, len(kps))
+            assert np.array_equal(g["word"], r["word"]) and np.array_equal(g["nid"], r["nid"]), s
+            assert g["nf"] == r["nf"] and np.array_equal(g["fn"][:r["nf"]], r["fn"][:r["nf"]]), s
+            assert np.array_equal(g["bv"][:r["nw"]].view(np.uint64), r["bv"][:r["nw"]].view(np.uint64)), s
+        # Relocalisation of slot 20 against three other frames of the batch
+        fk, fd = c.features(20)
+        Fv, fa = view(fk, fd, np.zeros(len(fk), np.uint8), ref_transform(V, fd, 4))
+        KFs, keep = [], []
+        for s in (19, 21, B + 27):
+            kk, kd = c.features(s)
+            v, a = view(kk, kd, rng.choice(3, len(kk), p=(0.3, 0.6, 0.1)).astype(np.uint8), ref_transform(V, kd, 4))
+            KFs.append(v)
+            keep.append(a)
+        r, outs, nm = search(c, 20, KFs, 0.75, 1)
+        assert r == 0
+        for i, KF in enumerate(KFs):
+            ro, rn = ref_search(0, {"V1": KF, "V2": Fv}, 0.75, 1)
+            assert nm[i] == rn and np.array_equal(outs[i][:len(fk)], ro), i
+        L.orbx_vocab_destroy(voc)
+    finally:
+        c.close()
