@@ -325,9 +325,75 @@ class Context:
         _check(lib().orbx_pose_fetch(self._h, arr, _ptr(n), st), "orbx_pose_fetch")
         return arr, n, list(st)
 
+    # --- DBoW2 on device-resident frames -----------------------------------
+    def compute_bow(self, voc, first, count, levelsup=4):
+        """Frame::ComputeBoW of extracted slots [first, first+count) on the
+        device (orbx_dev_compute_bow); `voc` is a Vocabulary."""
+        _check(lib().orbx_dev_compute_bow(self._h, voc.handle, first, count, levelsup), "orbx_dev_compute_bow")
+
+    def read_bow(self, slot):
+        """(BowVector, FeatureVector, per-feature (word, weight, node)) of a
+        slot as numpy arrays: bow = (words, values); fv = (node ids, CSR
+        offsets, feature indices)."""
+        n = self.nfeatures
+        word, weight, node = np.zeros(n, np.int32), np.zeros(n), np.zeros(n, np.int32)
+        bw, bv = np.zeros(n, np.uint32), np.zeros(n)
+        fn, fp, ff = np.zeros(n, np.uint32), np.zeros(n + 1, np.int32), np.zeros(n, np.int32)
+        nw, nf = ctypes.c_int(), ctypes.c_int()
+        _check(lib().orbx_dev_read_bow(self._h, slot, n, _ptr(word), _ptr(weight), _ptr(node), _ptr(bw), _ptr(bv),
+                                       ctypes.byref(nw), _ptr(fn), _ptr(fp), _ptr(ff), ctypes.byref(nf)),
+               "orbx_dev_read_bow")
+        m = int(fp[nf.value])
+        return ((bw[:nw.value].copy(), bv[:nw.value].copy()), (fn[:nf.value].copy(), fp[:nf.value + 1].copy(),
+                                                               ff[:m].copy()), (word, weight, node))
+
+    def search_by_bow(self, slot, kf_views, nnratio=0.75, check_ori=True):
+        """Tracking::Relocalisation's SearchByBoW(pKF, F) loop against the
+        frame in `slot` (orbx_dev_search_by_bow): kf_views are orbx_bow_view
+        ctypes structures.  Returns (matches per keyframe, counts)."""
+        n = len(kf_views)
+        outs = [np.zeros(self.nfeatures, np.int32) for _ in range(n)]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[o.ctypes.data for o in outs])
+        arr = (type(kf_views[0]) * n)(*kf_views) if n else None
+        nm = np.zeros(max(n, 1), np.int32)
+        _check(lib().orbx_dev_search_by_bow(self._h, slot, n, arr, nnratio, int(check_ori), ptrs, self.nfeatures,
+                                            _ptr(nm)), "orbx_dev_search_by_bow")
+        return outs, nm[:n]
+
     @property
     def handle(self):
         return self._h
+
+
+class Vocabulary:
+    """A DBoW2 vocabulary tree in HBM (orbx_vocab_create): nodes as
+    TemplatedVocabulary::loadFromTextFile lists them -- parent id per node
+    (node 0 the root), leaf flags, 32-byte descriptors and weights."""
+
+    def __init__(self, ctx, k, L, parent, is_leaf, desc, weight):
+        self._keep = [np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(is_leaf, np.uint8),
+                      np.ascontiguousarray(desc, np.uint8), np.ascontiguousarray(weight, np.float64)]
+        self._h = ctypes.c_void_p()
+        _check(lib().orbx_vocab_create(ctx.handle, k, L, len(self._keep[0]), *[_ptr(a) for a in self._keep],
+                                       ctypes.byref(self._h)), "orbx_vocab_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def n_words(self):
+        return lib().orbx_vocab_n_words(self._h)
+
+    def close(self):
+        if self._h:
+            lib().orbx_vocab_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def describe_levels(w, h, nfeatures=1000, scale_factor=1.2, nlevels=8, fast_th=20):

@@ -314,3 +314,26 @@ def test_dev_bow_after_async_pipeline():
         L.orbx_vocab_destroy(voc)
     finally:
         c.close()
+
+
+def test_python_wrappers_match_raw_calls(ctx, extracted):
+    """Context.compute_bow / read_bow / search_by_bow and Vocabulary give the
+    raw C-ABI calls' results."""
+    V = make_vocab(k=10, L=5, seed=15)
+    voc = ox.Vocabulary(ctx, V["k"], V["L"], V["parent"], V["is_leaf"], V["desc"], V["weight"])
+    try:
+        assert voc.n_words() == int(V["is_leaf"].sum())
+        ctx.compute_bow(voc, 0, 4, 3)
+        (bw, bv), (fn, fp, ff), (word, weight, node) = ctx.read_bow(1)
+        kps, desc = extracted[1]
+        r = ref_transform(V, desc, 3)
+        assert np.array_equal(bw, r["bw"][:r["nw"]]) and np.array_equal(bv, r["bv"][:r["nw"]])
+        assert np.array_equal(fn, r["fn"][:r["nf"]]) and np.array_equal(fp, r["fp"][:r["nf"] + 1])
+        assert np.array_equal(word[:len(kps)], r["word"])
+        mp = np.ones(len(kps), np.uint8)
+        v, keep = view(kps, desc, mp, r)
+        outs, nm = ctx.search_by_bow(0, [v])
+        raw = search(ctx, 0, [v], 0.75, 1)
+        assert raw[0] == 0 and nm[0] == raw[2][0] and np.array_equal(outs[0], raw[1][0])
+    finally:
+        voc.close()
