@@ -420,6 +420,15 @@ int orbx_fuse_candidates(orbx_ctx* ctx, const orbx_frame_view* KF, const float* 
 int orbx_fuse_candidates_batch(orbx_ctx* ctx, int n_kf, const orbx_frame_view* KFs, const float* cams,
                                const orbx_mappoint_view* const* mps, const float* Ts, int sim3, float th,
                                int32_t* const* best_idx, int32_t* const* best_dist);
+/* orbx_fuse_candidates_batch against keyframes that stay in their extraction
+ * slots: keyframe k is the frame in slots[k] (keypoints as the slot holds
+ * them -- mvKeysUn after orbx_dev_undistort -- descriptors, the extractor's
+ * scale pyramid), with image bounds bounds[4k..4k+3] (min_x, max_x, min_y,
+ * max_y; Frame::ComputeImageBounds) or, bounds NULL, 0..w x 0..h.  Only the
+ * map points, cameras and poses are uploaded; results as the batch form. */
+int orbx_dev_fuse_candidates(orbx_ctx* ctx, int n_kf, const int* slots, const float* bounds, const float* cams,
+                             const orbx_mappoint_view* const* mps, const float* Ts, int sim3, float th,
+                             int32_t* const* best_idx, int32_t* const* best_dist);
 /* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
  * (src/ORBmatcher.cc:1267-1505).  mp1 / valid1: the map point of each KF1
  * keypoint (valid = pMP && !isBad()); mp2 / valid2 likewise for KF2.  T1w,

@@ -602,6 +602,114 @@ extern "C" int orbx_fuse_candidates_batch(orbx_ctx* ctx, int n_kf, const orbx_fr
     return ORBX_OK;
 }
 
+// LocalMapping::SearchInNeighbors' Fuse loop against keyframes that stay in
+// their extraction slots: the keyframes' keypoints (mvKeysUn after
+// orbx_dev_undistort) and descriptors are read where orbx_dev_extract left
+// them; only the map points, poses and cameras travel.
+extern "C" int orbx_dev_fuse_candidates(orbx_ctx* ctx, int n_kf, const int* slots, const float* bounds,
+                                        const float* cams, const orbx_mappoint_view* const* mps, const float* Ts,
+                                        int sim3, float th, int32_t* const* best_idx, int32_t* const* best_dist)
+{
+    if (!ctx || n_kf < 0 || (n_kf > 0 && (!slots || !cams || !mps || !Ts || !best_idx || !best_dist)))
+        return ORBX_ERR_ARG;
+    if (ctx->geom_w <= 0) return ORBX_ERR_ARG;
+    for (int k = 0; k < n_kf; k++) {
+        if (slots[k] < 0 || slots[k] >= ctx->slots || !valid_mps(mps[k], true) ||
+            (mps[k]->n > 0 && (!best_idx[k] || !best_dist[k])))
+            return ORBX_ERR_ARG;
+        if (bounds && !(bounds[4 * k + 1] > bounds[4 * k] && bounds[4 * k + 3] > bounds[4 * k + 2])) return ORBX_ERR_ARG;
+    }
+    if (n_kf == 0) return ORBX_OK;
+    ctx_enter(ctx);
+    // the slots' keypoint counts size the kernel's LDS grid
+    std::vector<int32_t> cnt(ctx->slots);
+    ORBX_HIP_CHECK(hipMemcpyAsync(cnt.data(), ctx->out_n, sizeof(int32_t) * ctx->slots, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const Geometry& g = ctx->geom;
+    const size_t nf = g.nfeatures;
+    Staging s{ctx};
+    struct Off {
+        size_t pos, nrm, dmin, dmax, qd, bi, bd;
+    };
+    std::vector<Off> o(n_kf);
+    int max_n = 1, max_q = 0;
+    for (int k = 0; k < n_kf; k++) {
+        const orbx_mappoint_view* P = mps[k];
+        int same = -1;
+        for (int j = 0; j < k && same < 0; j++)
+            if (mps[j] == P) same = j;
+        if (same >= 0) {
+            o[k] = o[same];
+        } else {
+            o[k].pos = s.res((size_t)P->n * 12, P->pos);
+            o[k].nrm = s.res((size_t)P->n * 12, P->normal);
+            o[k].dmin = s.res((size_t)P->n * 4, P->min_dist);
+            o[k].dmax = s.res((size_t)P->n * 4, P->max_dist);
+            o[k].qd = s.res((size_t)P->n * 32, P->desc);
+        }
+        o[k].bi = s.res((size_t)P->n * 4);
+        o[k].bd = s.res((size_t)P->n * 4);
+        max_n = std::max(max_n, std::min<int>(cnt[slots[k]], (int)nf));
+        max_q = std::max(max_q, P->n);
+    }
+    const size_t o_jobs = s.res(sizeof(KfProjArgs) * (size_t)n_kf);
+    std::vector<KfProjArgs> jobs(n_kf);
+    int r = ensure_scratch(ctx, s.at);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = s.base();
+    for (int k = 0; k < n_kf; k++) {
+        const int sl = slots[k];
+        // the extracted frame as a keyframe view (bounds: the caller's
+        // ComputeImageBounds, or the undistorted image 0..w, 0..h)
+        orbx_frame_view v{};
+        v.n = std::min<int>(cnt[sl], (int)nf);
+        v.min_x = bounds ? bounds[4 * k] : 0.f;
+        v.max_x = bounds ? bounds[4 * k + 1] : (float)g.w;
+        v.min_y = bounds ? bounds[4 * k + 2] : 0.f;
+        v.max_y = bounds ? bounds[4 * k + 3] : (float)g.h;
+        KfProjArgs& a = jobs[k];
+        a = KfProjArgs{};
+        a.K = kf_dev(&v, nullptr, 0, 0);
+        a.K.kps = ctx->out_kps + (size_t)sl * nf;
+        a.K.desc = ctx->out_desc + (size_t)sl * nf * 32;
+        a.nlevels = g.nlevels;
+        a.scales[0] = 1.0f;
+        for (int l = 1; l < g.nlevels; l++) a.scales[l] = a.scales[l - 1] * g.scale_factor;   // src/Frame.cc:98-102
+        a.nq = mps[k]->n;
+        a.pos = reinterpret_cast<const float*>(d + o[k].pos);
+        a.normal = reinterpret_cast<const float*>(d + o[k].nrm);
+        a.dmin = reinterpret_cast<const float*>(d + o[k].dmin);
+        a.dmax = reinterpret_cast<const float*>(d + o[k].dmax);
+        a.qdesc = d + o[k].qd;
+        a.qvalid = nullptr;
+        a.best_idx = reinterpret_cast<int32_t*>(d + o[k].bi);
+        a.best_dist = reinterpret_cast<int32_t*>(d + o[k].bd);
+        for (int c = 0; c < 4; c++) a.cam[c] = cams[4 * k + c];
+        pose_parts(Ts + 16 * k, sim3, a.Ra, a.ta, a.Ow);
+        a.two_stage = 0;
+        a.mode = sim3 ? 1 : 0;
+        a.th = th;
+    }
+    s.puts.push_back({o_jobs, {jobs.data(), sizeof(KfProjArgs) * (size_t)n_kf}});
+    if ((r = s.upload()) != ORBX_OK) return r;
+    if (max_q > 0) {
+        const int per = kBlock / 64;
+        hipLaunchKernelGGL(k_kf_project_jobs, dim3((max_q + per - 1) / per, n_kf), dim3(kBlock), (size_t)max_n * 12,
+                           ctx->stream, reinterpret_cast<const KfProjArgs*>(d + o_jobs));
+        ORBX_HIP_CHECK(hipGetLastError());
+    }
+    for (int k = 0; k < n_kf; k++)
+        if (mps[k]->n) {
+            ORBX_HIP_CHECK(hipMemcpyAsync(best_idx[k], d + o[k].bi, (size_t)mps[k]->n * 4, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+            ORBX_HIP_CHECK(hipMemcpyAsync(best_dist[k], d + o[k].bd, (size_t)mps[k]->n * 4, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+        }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
 extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
                                    const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
                                    const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,

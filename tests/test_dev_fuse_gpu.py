@@ -1,0 +1,90 @@
+"""Fuse against keyframes resident in their extraction slots
+(orbx_dev_fuse_candidates; LocalMapping::SearchInNeighbors' loop,
+src/LocalMapping.cc:403-416, over ORBmatcher::Fuse, src/ORBmatcher.cc:
+1016-1265) through the C ABI against the CPU restatement: best keypoint and
+distance of every map point identical, for several keyframes in one call,
+with and without explicit image bounds, both Fuse overloads."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+import proj_data as pd
+from orb_slam_amd import synth
+from test_proj_oracle import ref_fuse
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def slots():
+    c = ox.Context(nfeatures=1000, max_w=pd.W, max_h=pd.H, slots=3)
+    frames = np.stack(synth.sequence(pd.W, pd.H, 2, seed=31))
+    c.upload(frames, 0)
+    c.upload(synth.texture_frame(pd.W, pd.H, seed=8), 2)
+    c.extract(0, 3)
+    c.sync()
+    yield c, [c.features(s) for s in range(3)]
+    c.close()
+
+
+def dev_fuse(c, slots_, bounds, views, Ts, sim3, th):
+    n = len(slots_)
+    sl = np.ascontiguousarray(slots_ or [0], np.int32)
+    cams = np.ascontiguousarray(np.tile(pd.CAM, n).astype(np.float32))
+    Tall = np.ascontiguousarray(np.concatenate([T.reshape(-1) for T in Ts] or [np.zeros(16)]).astype(np.float32))
+    mpp = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(v) for v in views])
+    bis = [np.zeros(v.n, np.int32) for v in views]
+    bds = [np.zeros(v.n, np.int32) for v in views]
+    bip = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in bis])
+    bdp = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in bds])
+    b = None if bounds is None else np.ascontiguousarray(bounds, np.float32)
+    r = ox.lib().orbx_dev_fuse_candidates(c.handle, n, ox._ptr(sl), ox._ptr(b) if b is not None else None,
+                                          ox._ptr(cams), mpp, ox._ptr(Tall), sim3, th, bip, bdp)
+    return r, bis, bds
+
+
+@pytest.mark.parametrize("sim3,th,with_bounds", [(0, 3.0, False), (1, 5.0, False), (0, 7.5, True), (1, 3.0, True)])
+def test_dev_fuse_matches_oracle(slots, sim3, th, with_bounds):
+    c, feats = slots
+    (k0, d0), (k1, d1), (k2, d2) = feats
+    du = float(np.median(k1["x"])) - float(np.median(k0["x"]))   # rough shift; the oracle decides parity
+    rng = np.random.default_rng(int(10 * th) + sim3)
+    mps = pd.mappoints(k0, d0, pd.pose_T([0, 0, 0]), rng)
+    mps[1]["pos"][:20, 2] *= -1
+    mps[1]["max_dist"][20:40] *= 0.1
+    other = pd.mappoints(k2, d2, pd.pose_T([0, 0, 0]), np.random.default_rng(5))
+    _, _, _, _, sdu, sdv = pd.keyframes()
+    T1 = pd.pose_T([sdu * pd.Z0 / pd.CAM[0], sdv * pd.Z0 / pd.CAM[1], 0.0])
+    Ts = [T1, pd.pose_T([0, 0, 0]), T1 + 0, pd.pose_T([0.01, 0, 0.002])]
+    if sim3:
+        Ts = [T.copy() for T in Ts]
+        for T in Ts:
+            T[:3, :] *= np.float32(1.3)
+    kf_slots = [1, 0, 2, 2]
+    views = [mps[0], mps[0], mps[0], other[0]]
+    sets = [mps, mps, mps, other]
+    bounds = None
+    if with_bounds:
+        bounds = np.array([[2.0, pd.W - 3.0, 1.0, pd.H - 2.0]] * len(kf_slots), np.float32).reshape(-1)
+    r, bis, bds = dev_fuse(c, kf_slots, bounds, views, Ts, sim3, th)
+    assert r == 0, r
+    for k, sl in enumerate(kf_slots):
+        kk, kd = feats[sl]
+        KF = ox.frame_view(kk, kd, pd.W, pd.H)
+        if with_bounds:
+            KF.min_x, KF.max_x, KF.min_y, KF.max_y = bounds[4 * k:4 * k + 4]
+        rb = ref_fuse(KF, sets[k], Ts[k], sim3, th)
+        assert np.array_equal(bis[k], rb[0]) and np.array_equal(bds[k], rb[1]), k
+    assert (bds[1] <= 50).sum() > 100   # the points fused back into their own keyframe
+
+
+def test_dev_fuse_errors(slots):
+    c, feats = slots
+    k0, d0 = feats[0]
+    mps = pd.mappoints(k0, d0, pd.pose_T([0, 0, 0]), np.random.default_rng(1))
+    T = pd.pose_T([0, 0, 0])
+    assert dev_fuse(c, [], None, [], [], 0, 3.0)[0] == 0
+    assert dev_fuse(c, [3], None, [mps[0]], [T], 0, 3.0)[0] == -1                    # no such slot
+    assert dev_fuse(c, [0], [5.0, 5.0, 0.0, 10.0], [mps[0]], [T], 0, 3.0)[0] == -1   # empty bounds
