@@ -451,6 +451,13 @@ int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_fr
 int orbx_search_by_projection_kf_sim3(orbx_ctx* ctx, const orbx_frame_view* KF, const float* cam,
                                       const orbx_mappoint_view* mps, const uint8_t* mp_skip,
                                       const float* Scw, int th, int32_t* matched, int* n_matches);
+/* The same against a keyframe resident in its extraction slot (keypoints as
+ * the slot holds them, mvKeysUn after orbx_dev_undistort; bounds: min_x,
+ * max_x, min_y, max_y, or NULL for 0..w x 0..h).  matched (in / out): cap >=
+ * the slot's keypoint count entries, as above. */
+int orbx_dev_search_by_projection_kf_sim3(orbx_ctx* ctx, int slot, const float* bounds, const float* cam,
+                                          const orbx_mappoint_view* mps, const uint8_t* mp_skip, const float* Scw,
+                                          int th, int32_t* matched, int cap, int* n_matches);
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const
  * set<MapPoint*>& sAlreadyFound, float th, int ORBdist) (src/ORBmatcher.cc:
  * 1622-1746), relocalisation.  KF: pKF's keypoints (mvKeysUn); kf_mps: the

@@ -867,6 +867,68 @@ extern "C" int orbx_search_by_projection_kf_sim3(orbx_ctx* ctx, const orbx_frame
     return ORBX_OK;
 }
 
+// LoopClosing::ComputeSim3 / CorrectLoop's SearchByProjection(pKF, Scw, ...)
+// against a keyframe resident in its extraction slot.
+extern "C" int orbx_dev_search_by_projection_kf_sim3(orbx_ctx* ctx, int slot, const float* bounds, const float* cam,
+                                                     const orbx_mappoint_view* mps, const uint8_t* mp_skip,
+                                                     const float* Scw, int th, int32_t* matched, int cap,
+                                                     int* n_matches)
+{
+    if (!ctx || slot < 0 || slot >= ctx->slots || ctx->geom_w <= 0 || !cam || !valid_mps(mps, true) || !Scw ||
+        !n_matches || (mps->n && !mp_skip) || !matched)
+        return ORBX_ERR_ARG;
+    if (bounds && !(bounds[1] > bounds[0] && bounds[3] > bounds[2])) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    int32_t cnt = 0;
+    ORBX_HIP_CHECK(hipMemcpyAsync(&cnt, ctx->out_n + slot, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const Geometry& g = ctx->geom;
+    const size_t nf = g.nfeatures;
+    const int n = std::min<int>(cnt, (int)nf);
+    if (cap < n) return ORBX_ERR_CAPACITY;
+    Staging s{ctx};
+    const size_t o_pos = s.res((size_t)mps->n * 12, mps->pos), o_nrm = s.res((size_t)mps->n * 12, mps->normal),
+                 o_mn = s.res((size_t)mps->n * 4, mps->min_dist), o_mx = s.res((size_t)mps->n * 4, mps->max_dist),
+                 o_qd = s.res((size_t)mps->n * 32, mps->desc), o_sk = s.res(mps->n, mp_skip),
+                 o_out = s.res((size_t)n * 4, matched), o_n = s.res(4);
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    uint8_t* d = s.base();
+    orbx_frame_view v{};
+    v.n = n;
+    v.min_x = bounds ? bounds[0] : 0.f;
+    v.max_x = bounds ? bounds[1] : (float)g.w;
+    v.min_y = bounds ? bounds[2] : 0.f;
+    v.max_y = bounds ? bounds[3] : (float)g.h;
+    SeqProjArgs a{};
+    a.T = kf_dev(&v, nullptr, 0, 0);
+    a.T.kps = ctx->out_kps + (size_t)slot * nf;
+    a.T.desc = ctx->out_desc + (size_t)slot * nf * 32;
+    a.nlevels = g.nlevels;
+    a.scales[0] = 1.0f;
+    for (int l = 1; l < g.nlevels; l++) a.scales[l] = a.scales[l - 1] * g.scale_factor;
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    pose_parts(Scw, 1, a.R, a.t, a.Ow);
+    a.th = (float)th;
+    a.variant = 0;
+    a.nq = mps->n;
+    a.pos = reinterpret_cast<const float*>(d + o_pos);
+    a.normal = reinterpret_cast<const float*>(d + o_nrm);
+    a.dmin = reinterpret_cast<const float*>(d + o_mn);
+    a.dmax = reinterpret_cast<const float*>(d + o_mx);
+    a.qdesc = d + o_qd;
+    a.qskip = d + o_sk;
+    a.out = reinterpret_cast<int32_t*>(d + o_out);
+    a.out_n = reinterpret_cast<int32_t*>(d + o_n);
+    const size_t lds = (size_t)std::max(n, 1) * 21 + 32 * 4 + 64;
+    hipLaunchKernelGGL(k_proj_seq, dim3(1), dim3(64), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if (n) ORBX_HIP_CHECK(hipMemcpyAsync(matched, d + o_out, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(n_matches, d + o_n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}
+
 extern "C" int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, const orbx_frame_view* KF,
                                                   const float* cam, const orbx_mappoint_view* kf_mps,
                                                   const uint8_t* kf_valid, const uint8_t* f_assigned,

@@ -88,3 +88,39 @@ def test_dev_fuse_errors(slots):
     assert dev_fuse(c, [], None, [], [], 0, 3.0)[0] == 0
     assert dev_fuse(c, [3], None, [mps[0]], [T], 0, 3.0)[0] == -1                    # no such slot
     assert dev_fuse(c, [0], [5.0, 5.0, 0.0, 10.0], [mps[0]], [T], 0, 3.0)[0] == -1   # empty bounds
+
+
+@pytest.mark.parametrize("seed,th,scale,with_bounds", [(0, 10, 1.5, False), (1, 5, 1.0, True), (2, 20, 0.8, False)])
+def test_dev_search_by_projection_kf_sim3_matches_oracle(slots, seed, th, scale, with_bounds):
+    """SearchByProjection(pKF, Scw, ...) against the keyframe in slot 1, map
+    points from slot 0's keypoints: matched vector and count as the oracle."""
+    from test_proj_oracle import ref_proj_kf_sim3
+    c, feats = slots
+    (k0, d0), (k1, d1) = feats[0], feats[1]
+    _, _, _, _, du, dv = pd.keyframes()
+    rng = np.random.default_rng(seed)
+    mps = pd.mappoints(k0, d0, pd.pose_T([0, 0, 0]), rng)
+    S = pd.pose_T([du * pd.Z0 / pd.CAM[0], dv * pd.Z0 / pd.CAM[1], 0.0])
+    S[:3, :] *= np.float32(scale)
+    skip = (rng.random(len(k0)) < 0.1).astype(np.uint8)
+    matched = np.full(len(k1), -1, np.int32)
+    matched[rng.random(len(k1)) < 0.05] = 10 ** 6
+    KF = ox.frame_view(k1, d1, pd.W, pd.H)
+    b = None
+    if with_bounds:
+        b = np.array([1.0, pd.W - 2.0, 3.0, pd.H - 1.0], np.float32)
+        KF.min_x, KF.max_x, KF.min_y, KF.max_y = b
+    ro, rn = ref_proj_kf_sim3(KF, mps, skip, S, th, matched)
+    go = np.full(c.nfeatures, -7, np.int32)
+    go[:len(k1)] = matched
+    gn = ctypes.c_int()
+    assert ox.lib().orbx_dev_search_by_projection_kf_sim3(c.handle, 1, ox._ptr(b) if b is not None else None,
+                                                          ox._ptr(pd.CAM), ctypes.byref(mps[0]), ox._ptr(skip),
+                                                          ox._ptr(S), th, ox._ptr(go), c.nfeatures,
+                                                          ctypes.byref(gn)) == 0
+    assert gn.value == rn and rn > 50
+    assert np.array_equal(go[:len(k1)], ro) and np.all(go[len(k1):] == -7)
+    # capacity below the slot's keypoint count
+    assert ox.lib().orbx_dev_search_by_projection_kf_sim3(c.handle, 1, None, ox._ptr(pd.CAM), ctypes.byref(mps[0]),
+                                                          ox._ptr(skip), ox._ptr(S), th, ox._ptr(go), len(k1) - 1,
+                                                          ctypes.byref(gn)) == -3
