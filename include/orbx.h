@@ -471,6 +471,16 @@ int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_frame_view* F, 
                                        const uint8_t* kf_valid, const uint8_t* f_assigned,
                                        const float* Tcw, float th, int orb_dist, int check_ori,
                                        int32_t* matches_f, int* n_matches);
+/* The same with the current frame in f_slot (bounds: min_x, max_x, min_y,
+ * max_y, or NULL for 0..w x 0..h) and the candidate keyframe in kf_slot
+ * (its keypoints from the slot; kf_mps / kf_valid: one entry per keyframe
+ * keypoint), both as extraction / orbx_dev_undistort left them.
+ * matches_f: cap >= the frame's keypoint count entries. */
+int orbx_dev_search_by_projection_frame_kf(orbx_ctx* ctx, int f_slot, const float* f_bounds, int kf_slot,
+                                           const float* cam, const orbx_mappoint_view* kf_mps,
+                                           const uint8_t* kf_valid, const uint8_t* f_assigned, const float* Tcw,
+                                           float th, int orb_dist, int check_ori, int32_t* matches_f, int cap,
+                                           int* n_matches);
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:185-250) for
  * n_mp map points at once: point m's observed descriptors (non-bad
  * keyframes, observation order) are rows obs_ptr[m] .. obs_ptr[m+1]-1 of

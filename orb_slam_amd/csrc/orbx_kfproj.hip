@@ -980,3 +980,77 @@ extern "C" int orbx_search_by_projection_frame_kf(orbx_ctx* ctx, const orbx_fram
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return ORBX_OK;
 }
+
+// Tracking::Relocalisation's second search, SearchByProjection(CurrentFrame,
+// pKF, sAlreadyFound, th, ORBdist), with the current frame and the candidate
+// keyframe both resident in their extraction slots: the frame's keypoints
+// and descriptors and the keyframe's keypoints are read in HBM; the
+// keyframe's map points and the flags are uploaded.
+extern "C" int orbx_dev_search_by_projection_frame_kf(orbx_ctx* ctx, int f_slot, const float* f_bounds, int kf_slot,
+                                                      const float* cam, const orbx_mappoint_view* kf_mps,
+                                                      const uint8_t* kf_valid, const uint8_t* f_assigned,
+                                                      const float* Tcw, float th, int orb_dist, int check_ori,
+                                                      int32_t* matches_f, int cap, int* n_matches)
+{
+    if (!ctx || f_slot < 0 || f_slot >= ctx->slots || kf_slot < 0 || kf_slot >= ctx->slots || ctx->geom_w <= 0 ||
+        !cam || !valid_mps(kf_mps, false) || !Tcw || !n_matches || !matches_f || !f_assigned ||
+        (kf_mps->n && !kf_valid))
+        return ORBX_ERR_ARG;
+    if (f_bounds && !(f_bounds[1] > f_bounds[0] && f_bounds[3] > f_bounds[2])) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    std::vector<int32_t> cnt(ctx->slots);
+    ORBX_HIP_CHECK(hipMemcpyAsync(cnt.data(), ctx->out_n, sizeof(int32_t) * ctx->slots, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const Geometry& g = ctx->geom;
+    const size_t nf = g.nfeatures;
+    const int nF = std::min<int>(cnt[f_slot], (int)nf), nK = std::min<int>(cnt[kf_slot], (int)nf);
+    if (kf_mps->n != nK) return ORBX_ERR_ARG;   // one map-point entry per keyframe keypoint
+    if (cap < nF) return ORBX_ERR_CAPACITY;
+    Staging s{ctx};
+    const size_t o_pos = s.res((size_t)nK * 12, kf_mps->pos), o_mn = s.res((size_t)nK * 4, kf_mps->min_dist),
+                 o_qd = s.res((size_t)nK * 32, kf_mps->desc), o_sk = s.res(nK), o_as = s.res(nF, f_assigned),
+                 o_out = s.res((size_t)nF * 4), o_n = s.res(4);
+    std::vector<uint8_t> skip(nK);
+    for (int i = 0; i < nK; i++) skip[i] = !kf_valid[i];
+    if (nK) s.puts.push_back({o_sk, {skip.data(), (size_t)nK}});
+    int r = s.upload();
+    if (r != ORBX_OK) return r;
+    uint8_t* d = s.base();
+    ORBX_HIP_CHECK(hipMemsetAsync(d + o_out, 0xFF, (size_t)std::max(nF, 1) * 4, ctx->stream));
+    orbx_frame_view v{};
+    v.n = nF;
+    v.min_x = f_bounds ? f_bounds[0] : 0.f;
+    v.max_x = f_bounds ? f_bounds[1] : (float)g.w;
+    v.min_y = f_bounds ? f_bounds[2] : 0.f;
+    v.max_y = f_bounds ? f_bounds[3] : (float)g.h;
+    SeqProjArgs a{};
+    a.T = kf_dev(&v, nullptr, 0, 0);
+    a.T.kps = ctx->out_kps + (size_t)f_slot * nf;
+    a.T.desc = ctx->out_desc + (size_t)f_slot * nf * 32;
+    a.nlevels = g.nlevels;
+    a.scales[0] = 1.0f;
+    for (int l = 1; l < g.nlevels; l++) a.scales[l] = a.scales[l - 1] * g.scale_factor;
+    for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
+    pose_parts(Tcw, 0, a.R, a.t, a.Ow);
+    a.th = th;
+    a.orb_dist = orb_dist;
+    a.check_ori = check_ori;
+    a.variant = 1;
+    a.nq = nK;
+    a.pos = reinterpret_cast<const float*>(d + o_pos);
+    a.dmin = reinterpret_cast<const float*>(d + o_mn);
+    a.qdesc = d + o_qd;
+    a.qskip = d + o_sk;
+    a.qkps = ctx->out_kps + (size_t)kf_slot * nf;
+    a.assigned = d + o_as;
+    a.out = reinterpret_cast<int32_t*>(d + o_out);
+    a.out_n = reinterpret_cast<int32_t*>(d + o_n);
+    const size_t lds = (size_t)std::max(nF, 1) * 21 + 32 * 4 + 64;
+    hipLaunchKernelGGL(k_proj_seq, dim3(1), dim3(64), lds, ctx->stream, a);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if (nF) ORBX_HIP_CHECK(hipMemcpyAsync(matches_f, d + o_out, (size_t)nF * 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(n_matches, d + o_n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return ORBX_OK;
+}

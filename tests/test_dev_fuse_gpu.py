@@ -124,3 +124,40 @@ def test_dev_search_by_projection_kf_sim3_matches_oracle(slots, seed, th, scale,
     assert ox.lib().orbx_dev_search_by_projection_kf_sim3(c.handle, 1, None, ox._ptr(pd.CAM), ctypes.byref(mps[0]),
                                                           ox._ptr(skip), ox._ptr(S), th, ox._ptr(go), len(k1) - 1,
                                                           ctypes.byref(gn)) == -3
+
+
+@pytest.mark.parametrize("seed,th,orb,ori,with_bounds", [(0, 10.0, 100, 1, False), (1, 5.0, 64, 0, True),
+                                                          (2, 15.0, 50, 1, False)])
+def test_dev_search_by_projection_frame_kf_matches_oracle(slots, seed, th, orb, ori, with_bounds):
+    """Relocalisation's SearchByProjection(CurrentFrame, pKF, sAlreadyFound)
+    with the frame in slot 1 and the keyframe in slot 0 (map points of the
+    keyframe's keypoints): matches and count as the oracle."""
+    from test_proj_oracle import ref_proj_frame_kf
+    c, feats = slots
+    (k0, d0), (k1, d1) = feats[0], feats[1]
+    _, _, _, _, du, dv = pd.keyframes()
+    rng = np.random.default_rng(seed)
+    mps = pd.mappoints(k0, d0, pd.pose_T([0, 0, 0]), rng)
+    T = pd.pose_T([du * pd.Z0 / pd.CAM[0], dv * pd.Z0 / pd.CAM[1], 0.0])
+    valid = (rng.random(len(k0)) < 0.8).astype(np.uint8)
+    assigned = (rng.random(len(k1)) < 0.1).astype(np.uint8)
+    F, KF = ox.frame_view(k1, d1, pd.W, pd.H), ox.frame_view(k0, d0, pd.W, pd.H)
+    b = None
+    if with_bounds:
+        b = np.array([2.0, pd.W - 1.0, 0.0, pd.H - 3.0], np.float32)
+        F.min_x, F.max_x, F.min_y, F.max_y = b
+    ro, rn = ref_proj_frame_kf(F, KF, mps, valid, assigned, T, th, orb, ori)
+    go = np.full(c.nfeatures, -7, np.int32)
+    gn = ctypes.c_int()
+    assert ox.lib().orbx_dev_search_by_projection_frame_kf(c.handle, 1, ox._ptr(b) if b is not None else None, 0,
+                                                           ox._ptr(pd.CAM), ctypes.byref(mps[0]), ox._ptr(valid),
+                                                           ox._ptr(assigned), ox._ptr(T), th, orb, ori, ox._ptr(go),
+                                                           c.nfeatures, ctypes.byref(gn)) == 0
+    assert gn.value == rn and rn > 50
+    assert np.array_equal(go[:len(k1)], ro) and np.all(go[len(k1):] == -7)
+    # the keyframe's map points must be one per keyframe keypoint
+    short = pd.mappoints(k0[:10], d0[:10], pd.pose_T([0, 0, 0]), rng)
+    assert ox.lib().orbx_dev_search_by_projection_frame_kf(c.handle, 1, None, 0, ox._ptr(pd.CAM),
+                                                           ctypes.byref(short[0]), ox._ptr(valid), ox._ptr(assigned),
+                                                           ox._ptr(T), th, orb, ori, ox._ptr(go), c.nfeatures,
+                                                           ctypes.byref(gn)) == -1
