@@ -442,6 +442,15 @@ int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_fr
                         const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
                         const float* T2w, float s12, const float* R12, const float* t12, float th,
                         const int32_t* prior12, int32_t* new12, int* n_found);
+/* The same with both keyframes resident in their extraction slots (keypoints
+ * as the slots hold them; bounds1 / bounds2: min_x, max_x, min_y, max_y, or
+ * NULL for 0..w x 0..h; mp1 / valid1 / prior12 one entry per slot1 keypoint,
+ * mp2 / valid2 per slot2 keypoint).  new12: cap >= slot1's keypoint count. */
+int orbx_dev_search_by_sim3(orbx_ctx* ctx, int slot1, const float* bounds1, int slot2, const float* bounds2,
+                            const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
+                            const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
+                            const float* T2w, float s12, const float* R12, const float* t12, float th,
+                            const int32_t* prior12, int32_t* new12, int cap, int* n_found);
 /* ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const
  * vector<MapPoint*>& vpPoints, vector<MapPoint*>& vpMatched, int th)
  * (src/ORBmatcher.cc:286-407), loop closing.  mps: vpPoints; mp_skip:

@@ -111,6 +111,7 @@ def _declare(L):
         "orbx_dev_fuse_candidates": ([vp, i, vp, vp, vp, vp, vp, i, f, vp, vp], i),
         "orbx_dev_search_by_projection_kf_sim3": ([vp, i, vp, vp, vp, vp, vp, i, vp, i, ip], i),
         "orbx_dev_search_by_projection_frame_kf": ([vp, i, vp, i, vp, vp, vp, vp, vp, f, i, i, vp, i, ip], i),
+        "orbx_dev_search_by_sim3": ([vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, f, vp, vp, f, vp, vp, i, ip], i),
         "orbx_search_by_sim3": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f, vp, vp, f, vp, vp, ip], i),
         "orbx_distinctive_descriptors": ([vp, i, vp, vp, vp], i),
         "orbx_search_by_projection_kf_sim3": ([vp, vp, vp, vp, vp, vp, i, vp, ip], i),

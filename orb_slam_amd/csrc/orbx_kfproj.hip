@@ -710,16 +710,16 @@ extern "C" int orbx_dev_fuse_candidates(orbx_ctx* ctx, int n_kf, const int* slot
     return ORBX_OK;
 }
 
-extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
-                                   const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
-                                   const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
-                                   const float* T2w, float s12, const float* R12, const float* t12, float th,
-                                   const int32_t* prior12, int32_t* new12, int* n_found)
+// SearchBySim3 for keyframe views whose keypoints and descriptors are on
+// the host (dev1 / dev2 null: staged) or already on the device (the slot
+// arrays: the views then carry only counts, bounds and the scale pyramid).
+static int run_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
+                    const orbx_keypoint* dk1, const uint8_t* dd1, const orbx_keypoint* dk2, const uint8_t* dd2,
+                    const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
+                    const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w, const float* T2w,
+                    float s12, const float* R12, const float* t12, float th, const int32_t* prior12, int32_t* new12,
+                    int* n_found)
 {
-    if (!ctx || !valid_kf(KF1) || !valid_kf(KF2) || !cam || !valid_mps(mp1, false) || !valid_mps(mp2, false) ||
-        mp1->n != KF1->n || mp2->n != KF2->n || (KF1->n && (!valid1 || !prior12 || !new12)) ||
-        (KF2->n && !valid2) || !T1w || !T2w || !R12 || !t12 || !n_found)
-        return ORBX_ERR_ARG;
     const int N1 = KF1->n, N2 = KF2->n;
     // vbAlreadyMatched1/2 (:1300-1313) folded into the query masks
     std::vector<uint8_t> q1(N1), q2(N2);
@@ -753,6 +753,10 @@ extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, co
     if (r != ORBX_OK) return r;
     KfProjArgs a{};
     fill_proj(a, s, o1, KF2, mp1, true);
+    if (dk2) {
+        a.K.kps = dk2;
+        a.K.desc = dd2;
+    }
     for (int k = 0; k < 4; k++) a.cam[k] = cam[k];
     std::copy(R1w, R1w + 9, a.Ra);
     std::copy(t1w, t1w + 3, a.ta);
@@ -764,6 +768,10 @@ extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, co
     if ((r = launch_proj(ctx, a)) != ORBX_OK) return r;
     KfProjArgs b{};
     fill_proj(b, s, o2, KF1, mp2, true);
+    if (dk1) {
+        b.K.kps = dk1;
+        b.K.desc = dd1;
+    }
     for (int k = 0; k < 4; k++) b.cam[k] = cam[k];
     std::copy(R2w, R2w + 9, b.Ra);
     std::copy(t2w, t2w + 3, b.ta);
@@ -795,6 +803,61 @@ extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, co
     }
     *n_found = nFound;
     return ORBX_OK;
+}
+
+extern "C" int orbx_search_by_sim3(orbx_ctx* ctx, const orbx_frame_view* KF1, const orbx_frame_view* KF2,
+                                   const float* cam, const orbx_mappoint_view* mp1, const uint8_t* valid1,
+                                   const orbx_mappoint_view* mp2, const uint8_t* valid2, const float* T1w,
+                                   const float* T2w, float s12, const float* R12, const float* t12, float th,
+                                   const int32_t* prior12, int32_t* new12, int* n_found)
+{
+    if (!ctx || !valid_kf(KF1) || !valid_kf(KF2) || !cam || !valid_mps(mp1, false) || !valid_mps(mp2, false) ||
+        mp1->n != KF1->n || mp2->n != KF2->n || (KF1->n && (!valid1 || !prior12 || !new12)) ||
+        (KF2->n && !valid2) || !T1w || !T2w || !R12 || !t12 || !n_found)
+        return ORBX_ERR_ARG;
+    return run_sim3(ctx, KF1, KF2, nullptr, nullptr, nullptr, nullptr, cam, mp1, valid1, mp2, valid2, T1w, T2w, s12,
+                    R12, t12, th, prior12, new12, n_found);
+}
+
+// LoopClosing::ComputeSim3's SearchBySim3 with both keyframes resident in
+// their extraction slots.
+extern "C" int orbx_dev_search_by_sim3(orbx_ctx* ctx, int slot1, const float* bounds1, int slot2,
+                                       const float* bounds2, const float* cam, const orbx_mappoint_view* mp1,
+                                       const uint8_t* valid1, const orbx_mappoint_view* mp2, const uint8_t* valid2,
+                                       const float* T1w, const float* T2w, float s12, const float* R12,
+                                       const float* t12, float th, const int32_t* prior12, int32_t* new12, int cap,
+                                       int* n_found)
+{
+    if (!ctx || slot1 < 0 || slot1 >= ctx->slots || slot2 < 0 || slot2 >= ctx->slots || ctx->geom_w <= 0 || !cam ||
+        !valid_mps(mp1, false) || !valid_mps(mp2, false) || !T1w || !T2w || !R12 || !t12 || !n_found || !new12)
+        return ORBX_ERR_ARG;
+    for (const float* b : {bounds1, bounds2})
+        if (b && !(b[1] > b[0] && b[3] > b[2])) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    std::vector<int32_t> cnt(ctx->slots);
+    ORBX_HIP_CHECK(hipMemcpyAsync(cnt.data(), ctx->out_n, sizeof(int32_t) * ctx->slots, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const Geometry& g = ctx->geom;
+    const size_t nf = g.nfeatures;
+    const int N1 = std::min<int>(cnt[slot1], (int)nf), N2 = std::min<int>(cnt[slot2], (int)nf);
+    if (mp1->n != N1 || mp2->n != N2 || (N1 && (!valid1 || !prior12)) || (N2 && !valid2)) return ORBX_ERR_ARG;
+    if (cap < N1) return ORBX_ERR_CAPACITY;
+    auto view = [&](int n, const float* b) {
+        orbx_frame_view v{};
+        v.n = n;
+        v.min_x = b ? b[0] : 0.f;
+        v.max_x = b ? b[1] : (float)g.w;
+        v.min_y = b ? b[2] : 0.f;
+        v.max_y = b ? b[3] : (float)g.h;
+        v.nlevels = g.nlevels;
+        v.scale_factor = g.scale_factor;
+        return v;
+    };
+    const orbx_frame_view K1 = view(N1, bounds1), K2 = view(N2, bounds2);
+    return run_sim3(ctx, &K1, &K2, ctx->out_kps + (size_t)slot1 * nf, ctx->out_desc + (size_t)slot1 * nf * 32,
+                    ctx->out_kps + (size_t)slot2 * nf, ctx->out_desc + (size_t)slot2 * nf * 32, cam, mp1, valid1, mp2,
+                    valid2, T1w, T2w, s12, R12, t12, th, prior12, new12, n_found);
 }
 
 extern "C" int orbx_distinctive_descriptors(orbx_ctx* ctx, int n_mp, const int32_t* obs_ptr, const uint8_t* desc,

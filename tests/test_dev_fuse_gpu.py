@@ -161,3 +161,42 @@ def test_dev_search_by_projection_frame_kf_matches_oracle(slots, seed, th, orb, 
                                                            ctypes.byref(short[0]), ox._ptr(valid), ox._ptr(assigned),
                                                            ox._ptr(T), th, orb, ori, ox._ptr(go), c.nfeatures,
                                                            ctypes.byref(gn)) == -1
+
+
+@pytest.mark.parametrize("seed,th,prior,with_bounds", [(0, 7.5, 0.1, False), (1, 4.0, 0.0, True), (2, 10.0, 0.4, False)])
+def test_dev_search_by_sim3_matches_oracle(slots, seed, th, prior, with_bounds):
+    """LoopClosing's SearchBySim3 with KF1 in slot 0 and KF2 in slot 1:
+    the agreed matches and their count as the oracle."""
+    from test_proj_oracle import ref_sim3
+    c, feats = slots
+    (k1, d1), (k2, d2) = feats[0], feats[1]
+    _, _, _, _, du, dv = pd.keyframes()
+    rng = np.random.default_rng(seed)
+    t2 = np.array([du * pd.Z0 / pd.CAM[0], dv * pd.Z0 / pd.CAM[1], 0.0], np.float32)
+    T1, T2 = pd.pose_T([0, 0, 0]), pd.pose_T(t2)
+    m1 = pd.mappoints(k1, d1, T1, rng)
+    m2 = pd.mappoints(k2, d2, T2, rng)
+    v1 = (rng.random(len(k1)) < 0.85).astype(np.uint8)
+    v2 = (rng.random(len(k2)) < 0.85).astype(np.uint8)
+    pr = np.full(len(k1), -2, np.int32)
+    sel = rng.random(len(k1)) < prior
+    pr[sel] = rng.integers(-1, len(k2), sel.sum())
+    R12 = np.eye(3, dtype=np.float32)
+    t12 = (-t2).astype(np.float32)
+    K1, K2 = ox.frame_view(k1, d1, pd.W, pd.H), ox.frame_view(k2, d2, pd.W, pd.H)
+    b1 = b2 = None
+    if with_bounds:
+        b1 = np.array([1.0, pd.W - 2.0, 2.0, pd.H - 1.0], np.float32)
+        b2 = np.array([0.0, pd.W - 3.0, 1.0, pd.H - 2.0], np.float32)
+        K1.min_x, K1.max_x, K1.min_y, K1.max_y = b1
+        K2.min_x, K2.max_x, K2.min_y, K2.max_y = b2
+    rn, rc = ref_sim3(K1, K2, m1, v1, m2, v2, T1, T2, np.float32(1.0), R12, t12, pr, th)
+    gn = np.full(c.nfeatures, -7, np.int32)
+    gc = ctypes.c_int()
+    bp = lambda b: ox._ptr(b) if b is not None else None
+    assert ox.lib().orbx_dev_search_by_sim3(c.handle, 0, bp(b1), 1, bp(b2), ox._ptr(pd.CAM), ctypes.byref(m1[0]),
+                                            ox._ptr(v1), ctypes.byref(m2[0]), ox._ptr(v2), ox._ptr(T1), ox._ptr(T2),
+                                            1.0, ox._ptr(R12), ox._ptr(t12), th, ox._ptr(pr), ox._ptr(gn), c.nfeatures,
+                                            ctypes.byref(gc)) == 0
+    assert gc.value == rc and rc > 50
+    assert np.array_equal(gn[:len(k1)], rn) and np.all(gn[len(k1):] == -7)
