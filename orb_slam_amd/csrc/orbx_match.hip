@@ -147,6 +147,151 @@ __global__ __launch_bounds__(64 * kBfWaves) void k_match_bf_prev(MatchPrevArgs a
     if (lane == 0 && ok) atomicAdd(a.match_n + s, ok);
 }
 
+// The same brute-force rule on the i8 matrix cores.  popc(a ^ b) =
+// popc(a) + popc(b) - 2 a.b with the 256 descriptor bits as 0/1 bytes, so a
+// 32x32 block of distances is eight v_mfma_i32_32x32x32_i8 over the bit
+// planes (exact integer sums).  Queries sit on the A rows (bits expanded
+// once into registers), candidates on the B columns (expanded per
+// 128-candidate chunk into LDS, rows padded to 272 B; the next chunk's dwords
+// load into registers while the current one is scored).  Any k order serves
+// as long as A and B share it: 16-bit group 2t + h of a descriptor is k-step t of lane
+// half h, bit j its byte j.  For a fixed query popc(a) is a constant, so
+// the per-lane key is C_col - (a.b << 17) with C_col = (popc(b) + 256) << 16
+// | index: one multiply-add per distance, ordered as (distance, index); an
+// absent candidate has C_col = ~0 and zero bits (key ~0, never chosen).
+constexpr int kBfmWaves = 4;                  // query tiles of 32 per workgroup
+constexpr int kBfmQ = 32 * kBfmWaves;
+constexpr int kBfmChunk = 128;                // candidates per LDS chunk
+constexpr int kBfmPitch = 17;                 // uint4 per expanded candidate row
+
+using orbx_i8x16 = __attribute__((ext_vector_type(16))) signed char;
+using orbx_i32x16 = __attribute__((ext_vector_type(16))) int;
+
+__device__ inline uint32_t nibble_bytes(uint32_t nib)   // bit j of nib -> byte j (0/1)
+{
+    return (nib * 0x00204081u) & 0x01010101u;
+}
+
+__device__ inline uint4 expand_bits16(uint32_t g)
+{
+    return make_uint4(nibble_bytes(g & 15u), nibble_bytes((g >> 4) & 15u), nibble_bytes((g >> 8) & 15u),
+                      nibble_bytes((g >> 12) & 15u));
+}
+
+__device__ inline int popc_desc(const uint4& x, const uint4& y)
+{
+    return __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w) + __popc(y.x) + __popc(y.y) + __popc(y.z) +
+           __popc(y.w);
+}
+
+__global__ __launch_bounds__(64 * kBfmWaves) void k_match_bf_prev_mfma(MatchPrevArgs a, int th_low)
+{
+    __shared__ uint4 bx[kBfmChunk][kBfmPitch];
+    __shared__ uint32_t cval[kBfmChunk];
+    __shared__ uint32_t fk1[kBfmQ], fk2[kBfmQ];
+    const int s = a.first + blockIdx.y;
+    const int prev = (s % a.seq_len == 0) ? s + a.seq_len - 1 : s - 1;
+    const int nA = a.nkp[prev], nB = a.nkp[s];
+    const uint8_t* dA = a.desc + (size_t)prev * a.nfeatures * 32;
+    const uint8_t* dB = a.desc + (size_t)s * a.nfeatures * 32;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int q0 = blockIdx.x * kBfmQ;
+    if (q0 >= nA) return;   // block-uniform
+    // A fragments of query q0 + 32 wv + r: k-step t holds 16-bit group 2t + h
+    orbx_i8x16 af[8];
+    {
+        const int q = q0 + 32 * wv + r;
+        uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+        if (q < nA) load_desc(dA + (size_t)q * 32, x, y);
+        const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int t = 0; t < 8; t++) af[t] = __builtin_bit_cast(orbx_i8x16, expand_bits16(w[t] >> (16 * h) & 0xFFFFu));
+    }
+    uint32_t k1[16], k2[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) k1[i] = k2[i] = 0xFFFFFFFFu;
+    // candidate dwords of a chunk: thread tid holds dword i = tid + kT m
+    // (candidate i >> 3, word i & 7), loaded one chunk ahead
+    constexpr int kT = 64 * kBfmWaves, kPer = kBfmChunk * 8 / kT;
+    const uint32_t* dB32 = reinterpret_cast<const uint32_t*>(dB);
+    uint32_t raw[kPer];
+    auto fetch = [&](int base) {
+#pragma unroll
+        for (int m = 0; m < kPer; m++) {
+            const int i = tid + kT * m, j = base + (i >> 3);
+            raw[m] = j < nB ? dB32[(size_t)j * 8 + (i & 7)] : 0u;
+        }
+    };
+    fetch(0);
+    for (int base = 0; base < nB; base += kBfmChunk) {
+        __syncthreads();   // previous chunk consumed
+#pragma unroll
+        for (int m = 0; m < kPer; m++) {
+            const int i = tid + kT * m, c = i >> 3, w = i & 7, j = base + c;
+            bx[c][2 * w] = expand_bits16(raw[m] & 0xFFFFu);
+            bx[c][2 * w + 1] = expand_bits16(raw[m] >> 16);
+            // popc of the candidate over its 8 consecutive lanes
+            int p = __popc(raw[m]);
+            p += __shfl_xor(p, 1);
+            p += __shfl_xor(p, 2);
+            p += __shfl_xor(p, 4);
+            if (w == 0) cval[c] = j < nB ? ((uint32_t)(p + 256) << 16) | (uint32_t)j : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        if (base + kBfmChunk < nB) fetch(base + kBfmChunk);   // block-uniform; lands during the tiles
+        const int ntiles = min(kBfmChunk / 32, (nB - base + 31) >> 5);   // block-uniform
+        for (int tile = 0; tile < ntiles; tile++) {
+            orbx_i32x16 acc = {};
+            const uint4* brow = bx[32 * tile + r];
+#pragma unroll
+            for (int t = 0; t < 8; t++)
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[t], __builtin_bit_cast(orbx_i8x16, brow[2 * t + h]), acc,
+                                                            0, 0, 0);
+            // D[row][col]: col = lane & 31 (candidate), row = (i & 3) + 8 (i >> 2) + 4 h (query)
+            const uint32_t C = cval[32 * tile + r];
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t key = C - ((uint32_t)acc[i] << 17);
+                k2[i] = min(k2[i], max(k1[i], key));
+                k1[i] = min(k1[i], key);
+            }
+        }
+    }
+    // merge the 32 columns of each lane half (keys are unique: order-free)
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t c1 = (uint32_t)__shfl_xor((int)k1[i], off), c2 = (uint32_t)__shfl_xor((int)k2[i], off);
+            k2[i] = min(min(k2[i], c2), max(k1[i], c1));
+            k1[i] = min(k1[i], c1);
+        }
+    }
+    if (r == 0) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            fk1[32 * wv + row] = k1[i];
+            fk2[32 * wv + row] = k2[i];
+        }
+    }
+    __syncthreads();
+    int ok = 0;
+    const int q = q0 + tid;
+    if (tid < kBfmQ && q < nA) {
+        uint4 x, y;
+        load_desc(dA + (size_t)q * 32, x, y);
+        const int pa = popc_desc(x, y) - 256;
+        const uint32_t r1 = fk1[tid], r2 = fk2[tid];
+        const int d1 = r1 == 0xFFFFFFFFu ? 0x7fffffff : (int)(r1 >> 16) + pa;
+        const int d2 = r2 == 0xFFFFFFFFu ? 0x7fffffff : (int)(r2 >> 16) + pa;
+        ok = (d1 <= th_low && (float)d1 < __fmul_rn((float)d2, a.nnratio));
+        a.match12[(size_t)s * a.nfeatures + q] = ok ? (int)(r1 & 0xFFFF) : -1;
+    }
+    ok = wave_sum(ok);
+    if (lane == 0 && ok) atomicAdd(a.match_n + s, ok);
+}
+
 #ifdef ORBX_MATCH_PROFILE
 extern "C" int orbx_debug_match_prof(unsigned long long* out)
 {
@@ -171,8 +316,13 @@ int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int t
     a.nnratio = nnratio;
     ORBX_HIP_CHECK(hipMemsetAsync(ctx->match_n + first, 0, sizeof(int32_t) * count, st));
     timer_begin(ctx, "match", st);
+#ifdef ORBX_BF_VALU   // A/B builds only: the VALU popcount form
     hipLaunchKernelGGL(k_match_bf_prev, dim3((g.nfeatures + 64 * kBfQ - 1) / (64 * kBfQ), count), dim3(64 * kBfWaves), 0,
                        st, a, th_low);
+#else
+    hipLaunchKernelGGL(k_match_bf_prev_mfma, dim3((g.nfeatures + kBfmQ - 1) / kBfmQ, count), dim3(64 * kBfmWaves), 0,
+                       st, a, th_low);
+#endif
     timer_end(ctx, "match", st);
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;

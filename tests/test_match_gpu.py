@@ -96,6 +96,38 @@ def test_match_bf_prev_parameters(th_low, nnratio):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [150, 300, 1000])
+def test_match_bf_prev_ragged_counts(n):
+    """k_match_bf_prev_mfma at keypoint counts off its 32-wide tiles and
+    128-candidate chunks, and with an empty frame (flat: no FAST corners) on
+    either side of a pair."""
+    w, h, seq_len = 640, 480, 4
+    frames = synth.sequence(w, h, seq_len, seed=11 + n)
+    frames[1][:, 200:] = 128   # texture on a third of the frame: a ragged count
+    frames[2] = 128
+    ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=seq_len)
+    ctx.upload(frames)
+    ctx.extract(0, seq_len)
+    ctx.match_bf_prev(0, seq_len, seq_len, th_low=50, nnratio=0.9)
+    ctx.sync()
+    L = load()
+    feats = [ctx.features(s) for s in range(seq_len)]
+    assert len(feats[2][1]) == 0 and 0 < len(feats[1][1]) <= n
+    for s in range(seq_len):
+        p = s - 1 if s % seq_len else s + seq_len - 1
+        dA, dB = feats[p][1], feats[s][1]
+        gm, gn = ctx.matches(s)
+        if len(dA) == 0 or len(dB) == 0:
+            assert gn == 0
+            continue
+        bi, b1, b2 = (np.zeros(len(dA), np.int32) for _ in range(3))
+        L.orbx_ref_hamming_bf(ptr(dA), len(dA), ptr(dB), len(dB), ptr(bi), ptr(b1), ptr(b2))
+        want = np.where((b1 <= 50) & (b1.astype(np.float32) < b2.astype(np.float32) * np.float32(0.9)), bi, -1)
+        assert np.array_equal(gm[:len(dA)], want)
+        assert gn == int((want >= 0).sum())
+    ctx.close()
+
+
 def test_match_bf_prev_matches_oracle():
     """Device-resident brute-force pairs (C3) against the oracle's all-pairs
     best/second + the acceptance rule."""
