@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * kBfWaves) void k_match_bf_prev(MatchPrevArgs a
 // the per-lane key is C_col - (a.b << 17) with C_col = (popc(b) + 256) << 16
 // | index: one multiply-add per distance, ordered as (distance, index); an
 // absent candidate has C_col = ~0 and zero bits (key ~0, never chosen).
-constexpr int kBfmWaves = 4;                  // query tiles of 32 per workgroup
+constexpr int kBfmWaves = 8;                  // query tiles of 32 per workgroup
 constexpr int kBfmQ = 32 * kBfmWaves;
 constexpr int kBfmChunk = 128;                // candidates per LDS chunk
 constexpr int kBfmPitch = 17;                 // uint4 per expanded candidate row
