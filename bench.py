@@ -19,9 +19,11 @@ Workloads (BASELINE.json configs):
      four-round robust pose optimisation of every frame from its initial
      pose (frames/s).
 
-Multi-GPU: one process per GPU (torchrun); each rank owns its sequence (or
-problems); the only collective is the end-of-run gather of stats (RCCL).
-Weak scaling.
+Multi-GPU: one process per GPU (torchrun, or `--gpus N` alone: bench.py then
+starts the N rank processes itself before any GPU call); each rank owns its
+sequence (or problems); the only collective is the end-of-run gather of stats
+(RCCL when every rank has its own GPU, gloo when ranks share one).  Weak
+scaling: value = units of all ranks / the slowest rank's timed seconds.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 """
@@ -405,7 +407,7 @@ def run_pose(args, wl, rank, local, world, dist):
     P = args.batch or wl["batch"]
     uniq = [sp.make_frame(n_kp=1000, seed=odist.shard_seed(7000, rank) * 1000 + i) for i in range(min(P, 256))]
     frames = [uniq[i % len(uniq)] for i in range(P)]
-    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=args.device)
     keep = [sp.to_ctypes(fr) for fr in frames]
     ctx.pose_stage([k[0] for k in keep])
     n_edges = int(np.mean([fr["has_mp"].sum() for fr in uniq]))
@@ -419,6 +421,7 @@ def run_pose(args, wl, rank, local, world, dist):
     kernels = {"timed": None, "serial": kernels, "serial_steps": args.steps}   # one launch per step
     arr, n_inl, st = ctx.pose_fetch()
     stats = np.array([elapsed, P * args.steps, int(n_inl[0]), st[0].rounds], dtype=np.float64)
+    allst = odist.gather_stats(stats, dist, device=args.gather_device)   # before rank 0's CPU legs
     ab = {"pose": n_edges * 25 + 80 + 160}
     units_per_step = {"pose": P}
     flops = float(np.mean([pose_flops(st[i], int(frames[i]["has_mp"].sum())) for i in range(len(uniq))]))
@@ -426,7 +429,7 @@ def run_pose(args, wl, rank, local, world, dist):
     check = {"inliers_frame0": int(n_inl[0]), "edges_frame0": int(frames[0]["has_mp"].sum()),
              "rounds_frame0": int(st[0].rounds), "lm_iterations_frame0": list(st[0].iterations),
              "fp64_flops_per_frame": round(flops)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         check["parity_last_step"] = parity_pose(uniq, arr, n_inl)
         L, desc = native_oracle()
         cpu = cpu_baseline_pose(uniq, CPU_PROTOCOL["pose"], L=L, lib_desc=desc)
@@ -435,7 +438,7 @@ def run_pose(args, wl, rank, local, world, dist):
            "parallelism": f"dp{world} (independent frames per GPU)",
            "boundary": "frames staged in HBM before the timed region (orbx_pose_stage); results fetched after"}
     ctx.close()
-    return stats, kernels, ab, units_per_step, cpu, check, cfg
+    return allst, kernels, ab, units_per_step, cpu, check, cfg
 
 
 def parity_frames(ctx, frames, first, B, nf, w, h, bf):
@@ -446,7 +449,8 @@ def parity_frames(ctx, frames, first, B, nf, w, h, bf):
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     L = oracle_lib.load()
-    ex = oracle_lib.RefExtractor(nf)
+    era = ctx.nth_pivot()        # retainBest's libstdc++ era the product ran (orbx_get_nth_pivot)
+    ex = oracle_lib.RefExtractor(nf, nth_pivot=era)
     ways = 3
     picks = sorted({min(B - 1, max(0, v)) for i in range(ways) for v in (B * i // ways, B * (i + 1) // ways - 1)}
                    | {B // 2})
@@ -479,7 +483,9 @@ def parity_frames(ctx, frames, first, B, nf, w, h, bf):
         if not ok:
             bad.append(first + f)
     return {"bit_exact": not bad, "slots": [first + f for f in picks], "mismatched_slots": bad,
-            "oracle": "oracle/liborbx_ref.so", "what": "keypoints, descriptors and matches of the last timed step"}
+            "oracle": "oracle/liborbx_ref.so", "what": "keypoints, descriptors and matches of the last timed step",
+            "nth_element_era": {1: "GCC 4.6-4.8 (ORBX_NTH_PIVOT_GCC48, the default)",
+                                0: "GCC >= 4.9 (ORBX_NTH_PIVOT_GCC49)"}[era]}
 
 
 def run_frames(args, wl, rank, local, world, dist):
@@ -488,7 +494,7 @@ def run_frames(args, wl, rank, local, world, dist):
     frames = synth.sequence(w, h, B, seed=odist.shard_seed(2000, rank))
     # two slot ranges: step k extracts range k % 2 while the matching of
     # step k - 1 (the other range) finishes on the context's match stream
-    ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=2 * B, device=local if world > 1 else 0)
+    ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=2 * B, device=args.device)
     ctx.upload(frames, first=0)
     ctx.upload(frames, first=B)
     if args.split_ways:
@@ -549,11 +555,12 @@ def run_frames(args, wl, rank, local, world, dist):
     k0, _ = ctx.features(B - 1)
     _, nm = ctx.matches(B - 1)
     stats = np.array([elapsed, B * args.steps, len(k0), nm], dtype=np.float64)
+    allst = odist.gather_stats(stats, dist, device=args.gather_device)   # before rank 0's CPU legs
     ab = algorithmic_bytes(w, h, nf, "bf" if bf else "init")
     units_per_step = {k: B for k in ab}
     cpu = None
     check = {"last_frame_keypoints": int(stats[2]), "last_frame_matches": int(stats[3])}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         check["parity_last_step"] = parity_frames(ctx, frames, last[0], B, nf, w, h, bf)
         L, desc = native_oracle()
         cpu = cpu_baseline_frames(frames, nf, CPU_PROTOCOL[args.workload], bf=bf, L=L, lib_desc=desc)
@@ -564,7 +571,7 @@ def run_frames(args, wl, rank, local, world, dist):
                         "sync matching" if args.sync_match else
                         f"{args.split_ways or 3}-part extraction pipeline, asynchronous matching")}
     ctx.close()
-    return stats, kernels, ab, units_per_step, cpu, check, cfg
+    return allst, kernels, ab, units_per_step, cpu, check, cfg
 
 
 def parity_lba(uniq, work, es, pb, st, sample=(0, 1, 2, 3)):
@@ -604,7 +611,7 @@ def run_lba(args, wl, rank, local, world, dist):
     uniq = [sb.make_problem(n_kf=20, n_points=2000, seed=odist.shard_seed(5000, rank) * 1000 + i)
             for i in range(min(P, 32))]
     probs = [uniq[i % len(uniq)] for i in range(P)]
-    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=local if world > 1 else 0)
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=args.device)
     L = ox.lib()
     # host-side problem arrays, marshalled once
     work = [sb.to_ctypes(pr) for pr in probs]
@@ -632,12 +639,13 @@ def run_lba(args, wl, rank, local, world, dist):
     kernels = {"timed": None, "serial": kernels, "serial_steps": args.steps}   # one stream, in order
     st = (sb.BAStats * P)()
     check_rc(L.orbx_lba_fetch(ctx.handle, arr, esp, pbp, st), "orbx_lba_fetch")
-    cpu_leg = rank == 0 and world == 1 and not args.no_cpu_baseline
+    cpu_leg = rank == 0 and not args.no_cpu_baseline
     # the last timed run's results against the oracle, before the host-array
     # leg below reuses these arrays
     parity = parity_lba(uniq, work, es, pb, st) if cpu_leg else None
     stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
                      dtype=np.float64)
+    allst = odist.gather_stats(stats, dist, device=args.gather_device)   # before rank 0's CPU legs
     # the host-array boundary (orbx_lba_solve_batch: packing, H2D upload,
     # both passes, D2H readback and unpacking), timed beside it on rank 0;
     # reported in `check`, never as `value`
@@ -676,7 +684,7 @@ def run_lba(args, wl, rank, local, world, dist):
            "parallelism": f"dp{world} (independent problems per GPU; replicas)",
            "boundary": "problems staged in HBM before the timed region (orbx_lba_stage); results fetched after"}
     ctx.close()
-    return stats, kernels, ab, units_per_step, cpu, check, cfg
+    return allst, kernels, ab, units_per_step, cpu, check, cfg
 
 
 # bench timer name -> kernel symbol in the rocprofv3 CSVs
@@ -742,7 +750,8 @@ def timed(args, ctx, step, dist, names, only=None):
         if dist is not None:
             import torch
             dist.barrier()
-            torch.cuda.synchronize()
+            if torch.cuda.device_count():   # the stubbed-context CPU test has no GPU
+                torch.cuda.synchronize()
 
     ctx.timing(not args.no_kernel_timing, only=only)
     barrier()
@@ -761,6 +770,56 @@ def timed(args, ctx, step, dist, names, only=None):
     return elapsed, kernels
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a torchrun environment: start N rank
+    processes of this same script (sys.argv[0], so a wrapper that installs a
+    test context is re-entered too) with RANK / LOCAL_RANK / WORLD_SIZE and a
+    127.0.0.1 rendezvous, before this process makes any GPU call, and return
+    the first non-zero exit code (the others are then terminated by pid)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(sys.argv[0]), *sys.argv[1:]], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def init_ranks(world, local):
+    """Process group for N > 1 ranks: RCCL ("nccl") when every rank has a GPU
+    of its own, gloo otherwise (N ranks sharing one GPU, as on a 1-GPU box,
+    or no GPU at all: the CPU tests).  torch.cuda.device_count() does not
+    initialise the GPU on this image.  Returns (dist, device index for the
+    orbx context, device of the stats gather)."""
+    import torch
+    import torch.distributed as tdist
+    ngpu = odist.visible_gpus()
+    backend = os.environ.get("ORBX_BENCH_BACKEND") or ("nccl" if ngpu >= world else "gloo")
+    device = local % ngpu if ngpu else 0
+    if ngpu:
+        torch.cuda.set_device(device)
+    tdist.init_process_group(backend)
+    return tdist, device, ("cuda" if backend == "nccl" else "cpu")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -771,6 +830,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of the all-cores CPU baseline x2 (the 1-core baseline follows CPU_PROTOCOL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-protocol", default="",
+                    help="W,T: CPU baseline warm-up and timed units (default CPU_PROTOCOL: SURVEY.md 8(d)'s 50,500)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-isolated", action="store_true",
                     help="skip the serialised per-kernel pass after the timed steps (PMC collection)")
@@ -787,20 +848,26 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()
+    if args.cpu_protocol:
+        CPU_PROTOCOL[args.workload] = tuple(int(v) for v in args.cpu_protocol.split(","))
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local = odist.env()
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     dist = None
+    args.device, args.gather_device = 0, "cpu"
     if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
-        dist = tdist
+        dist, args.device, args.gather_device = init_ranks(world, local)
+    args.dist_backend = dist.get_backend() if dist is not None else None
 
     wl = WORKLOADS[args.workload]
     run = {"c5": run_lba, "pose": run_pose}.get(args.workload, run_frames)
-    stats, kernels, ab, units, cpu, check, cfg = run(args, wl, rank, local, world, dist)
-    allst = odist.gather_stats(stats, dist, device="cuda")
+    allst, kernels, ab, units, cpu, check, cfg = run(args, wl, rank, local, world, dist)
     value, elapsed, _ = odist.job_rate(allst)
 
     if rank == 0:
@@ -860,14 +927,14 @@ def main():
             # measured step time
             step_s = elapsed / args.steps
             per_frame = survey_frame_bytes(wl["w"], wl["h"], wl["nfeatures"])
-            per_step = per_frame * units["fast"]
-            stage_step = sum(ab[k] * units[k] for k in ab)
+            per_step = per_frame * units["fast"] * world          # every rank's frames
+            stage_step = sum(ab[k] * units[k] for k in ab) * world
             gbs = per_step / step_s / 1e9
             path = {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_frame": per_frame,
                     "algorithmic_bytes_per_step": per_step,
                     "note": "SURVEY.md 8(d) B_frame (pyramid read + write, FAST read, blur read + write, outputs) x "
-                            "frames per step / ms_per_step",
+                            "frames per step of all ranks / ms_per_step",
                     "with_every_stage_bytes": {"bytes_per_step": stage_step,
                                                "achieved": round(stage_step / step_s / 1e9, 2),
                                                "note": "also the level-0 copy and describe's patch reads "
@@ -880,6 +947,12 @@ def main():
             "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py / synth_pose.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
         }
+        if world > 1:
+            # what `value` is made of: every rank's units and timed seconds
+            # (value = sum of units / max of seconds), and how the ranks met
+            out["ranks"] = {"backend": args.dist_backend, "gpus_visible": odist.visible_gpus(),
+                            "elapsed_s": [round(float(x), 6) for x in allst[:, 0]],
+                            "units": [int(x) for x in allst[:, 1]]}
         if occ is not None and occ is not roof:
             out["occupancy"] = occ
         if path:

@@ -130,10 +130,12 @@ int orbx_get_fp_contract(const orbx_ctx* ctx);
  * called at src/ORBextractor.cc:683, :699).  The surviving keypoints and their
  * order are nth_element's permutation, and libstdc++ changed its introselect
  * pivot step in GCC 4.9 (PR libstdc++/58437):
- *   ORBX_NTH_PIVOT_GCC49 (0, default): median of (first + 1, mid, last - 1)
- *     swapped into first -- GCC >= 4.9;
- *   ORBX_NTH_PIVOT_GCC48 (1): median of (first, mid, last - 1) moved to
- *     first -- GCC 4.6 .. 4.8, the compilers of the reference's era.
+ *   ORBX_NTH_PIVOT_GCC49 (0): median of (first + 1, mid, last - 1) swapped
+ *     into first -- GCC >= 4.9;
+ *   ORBX_NTH_PIVOT_GCC48 (1, default): median of (first, mid, last - 1)
+ *     moved to first -- GCC 4.6 .. 4.8, the compilers of the platforms the
+ *     reference documents (Ubuntu 12.04 / 14.04, README.md:46), whose OpenCV
+ *     2.4 packages instantiate retainBest's nth_element.
  * Applies to extractions launched after the call (DESIGN.md section 4 has the
  * measured effect). */
 enum { ORBX_NTH_PIVOT_GCC49 = 0, ORBX_NTH_PIVOT_GCC48 = 1 };

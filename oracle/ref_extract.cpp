@@ -296,19 +296,19 @@ void cv24_fast16(const uint8_t* img, int step, int rows, int cols, int threshold
 // std::nth_element as libstdc++ implements it (bits/stl_algo.h
 // __introselect, __heap_select, __insertion_sort, __unguarded_partition),
 // restated so the pivot step can follow either era of the library:
-//   NTH_PIVOT_GCC49 (default): __move_median_to_first(first, first + 1, mid,
+//   NTH_PIVOT_GCC49: __move_median_to_first(first, first + 1, mid,
 //       last - 1) -- the median of those three swapped into *first (GCC >= 4.9,
 //       PR libstdc++/58437; the GCC 11.4 of this image);
 //   NTH_PIVOT_GCC48: __move_median_first(first, mid, last - 1) -- the median
 //       of (first, mid, last - 1) moved to *first, *first left in place when
 //       it is the median (GCC 4.6 .. 4.8, the compilers of the reference's
-//       era: Ubuntu 12.04 / 14.04).
+//       era: Ubuntu 12.04 / 14.04, README.md:46) -- the default.
 // Everything else (depth limit 2 floor(log2 n), the Hoare partition from
 // first + 1, heap select, insertion sort below 4 elements) is common to both.
 // With NTH_PIVOT_GCC49 it is checked against this image's std::nth_element
 // (orbx_ref_nth_element_check, tests/test_sort_era.py).
 // ---------------------------------------------------------------------------
-static int g_nth_pivot = NTH_PIVOT_GCC49;
+static int g_nth_pivot = NTH_PIVOT_GCC48;   // the default era, as the product's (include/orbx.h)
 void set_nth_pivot(int mode) { g_nth_pivot = mode; }
 int get_nth_pivot() { return g_nth_pivot; }
 

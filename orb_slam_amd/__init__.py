@@ -238,9 +238,14 @@ class Context:
         _check(lib().orbx_set_fp_contract(self._h, int(enable)), "orbx_set_fp_contract")
 
     def set_nth_pivot(self, mode):
-        """retainBest's std::nth_element pivot step as libstdc++ >= 4.9 (0,
-        default) or GCC 4.6 .. 4.8 (1) implements it (orbx_set_nth_pivot)."""
+        """retainBest's std::nth_element pivot step as libstdc++ >= 4.9 (0) or
+        GCC 4.6 .. 4.8 (1, default: the reference's documented platforms)
+        implements it (orbx_set_nth_pivot)."""
         _check(lib().orbx_set_nth_pivot(self._h, int(mode)), "orbx_set_nth_pivot")
+
+    def nth_pivot(self):
+        """The retainBest era in effect (orbx_get_nth_pivot)."""
+        return lib().orbx_get_nth_pivot(self._h)
 
     def set_async_match(self, enable):
         """Queue extract_match's matching behind the extraction on an internal

@@ -110,6 +110,10 @@ public:
     void SetFpContract(bool enable) { check(orbx_set_fp_contract(ctx_.get(), enable ? 1 : 0), "SetFpContract"); }
     // retainBest's std::nth_element as the libstdc++ the reference was built
     // against implements it: gcc48 = GCC 4.6 .. 4.8 (orbx_set_nth_pivot).
+    // The constructor leaves the default, GCC 4.6 .. 4.8: the reference
+    // documents Ubuntu 12.04 / 14.04 (README.md:46), whose OpenCV 2.4
+    // packages were built with those compilers; SetNthElementEra(false)
+    // matches an OpenCV built with GCC >= 4.9.
     void SetNthElementEra(bool gcc48)
     {
         check(orbx_set_nth_pivot(ctx_.get(), gcc48 ? ORBX_NTH_PIVOT_GCC48 : ORBX_NTH_PIVOT_GCC49), "SetNthElementEra");

@@ -1626,7 +1626,7 @@ extern "C" int orbx_debug_nth_pivot(const uint32_t* entries, int n, int nth, int
 
 extern "C" int orbx_debug_nth(const uint32_t* entries, int n, int nth, uint32_t* out_glb, uint32_t* out_lds)
 {
-    return orbx_debug_nth_pivot(entries, n, nth, 0, out_glb, out_lds);
+    return orbx_debug_nth_pivot(entries, n, nth, ORBX_NTH_PIVOT_GCC48, out_glb, out_lds);   // the default era
 }
 
 namespace orbx {

@@ -225,7 +225,7 @@ struct orbx_ctx {
     uint64_t* level_keys64 = nullptr;   // slots x level_entries
     int harris = 0;
     int fp_contract = 0;               // orbx_set_fp_contract
-    int nth_pivot = 0;                 // orbx_set_nth_pivot
+    int nth_pivot = ORBX_NTH_PIVOT_GCC48;   // orbx_set_nth_pivot (the reference's documented platforms)
     int32_t* level_count = nullptr;
     orbx_keypoint* out_kps = nullptr;
     uint8_t* out_desc = nullptr;

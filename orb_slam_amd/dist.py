@@ -18,6 +18,16 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def visible_gpus():
+    """GPUs this process can see (torch.cuda.device_count() does not
+    initialise the GPU on this image); 0 without torch or GPU."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:   # noqa: BLE001
+        return 0
+
+
 def shard_seed(base, rank):
     """Seed of the sequence a rank owns (weak scaling: fixed work per rank)."""
     return base + rank

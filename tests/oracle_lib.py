@@ -92,9 +92,11 @@ def ptr(a):
 
 class RefExtractor:
     def __init__(self, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1, variant="iso", lib=None,
-                 nth_pivot=0):
+                 nth_pivot=1):
         self.L = lib if lib is not None else load(variant)
-        self.nth_pivot = nth_pivot   # retainBest's libstdc++ era (orbx_ref_set_nth_pivot), per call
+        # retainBest's libstdc++ era (orbx_ref_set_nth_pivot), per call; 1 =
+        # GCC 4.6 .. 4.8, the default of the product and the oracle
+        self.nth_pivot = nth_pivot
         self.h = self.L.orbx_ref_extractor_create(nfeatures, scale, nlevels, score_type, fast_th)
         assert self.h, "oracle rejected the configuration"
         self.nfeatures = nfeatures

@@ -54,11 +54,14 @@ def ref_bf(L, dA, dB, th_low=50, nnratio=0.9):
     return want, int((want >= 0).sum())
 
 
-def run_bench_pipeline(w, h, nf, B, mode, split_ways=None, steps=3, seed=2000):
+def run_bench_pipeline(w, h, nf, B, mode, split_ways=None, steps=3, seed=2000, era=None):
     """bench.py run_frames: slots = 2B, both ranges uploaded with the same
-    sequence, async matching, steps alternating the ranges."""
+    sequence, async matching, steps alternating the ranges.  era: retainBest's
+    libstdc++ era (orbx_set_nth_pivot), None = the library default."""
     frames = synth.sequence(w, h, B, seed=seed)
     ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=2 * B)
+    if era is not None:
+        ctx.set_nth_pivot(era)
     ctx.upload(frames, first=0)
     ctx.upload(frames, first=B)
     if split_ways:
@@ -93,8 +96,8 @@ def check_against_sync(ctx, B, mode, got):
         assert n == gn and np.array_equal(m[:len(k)], gm[:len(gk)]), s
 
 
-def check_against_oracle(frames, got, B, nf, w, h, mode, sample):
-    ex = RefExtractor(nf)
+def check_against_oracle(frames, got, B, nf, w, h, mode, sample, era=1):
+    ex = RefExtractor(nf, nth_pivot=era)
     L = load()
     ref = {}
     for s in sorted(set(sample) | {(s % B - 1) % B for s in sample}):
@@ -117,16 +120,20 @@ def check_against_oracle(frames, got, B, nf, w, h, mode, sample):
         assert rn > 0
 
 
-def test_c2_bench_pipeline_1024_three_parts():
+@pytest.mark.parametrize("era", [None, 0], ids=["default-gcc48", "gcc49"])
+def test_c2_bench_pipeline_1024_three_parts(era):
     """C2 exactly as benched: 1024-frame steps, three parts, async matching,
     three steps alternating the two slot ranges.  Twelve frames (the part
     boundaries 0/340/341/681/682/1023 and six interior ones) against the
-    oracle in both ranges; all 2048 slots against the synchronous path."""
+    oracle in both ranges; all 2048 slots against the synchronous path.  In
+    both libstdc++ eras of retainBest: the default (GCC 4.6 .. 4.8, the
+    bench's) and GCC >= 4.9."""
     w, h, nf, B = 640, 480, 1000, 1024
-    frames, ctx = run_bench_pipeline(w, h, nf, B, "init")
+    frames, ctx = run_bench_pipeline(w, h, nf, B, "init", era=era)
+    assert ox.lib().orbx_get_nth_pivot(ctx.handle) == (1 if era is None else era)
     got = snapshot(ctx, range(2 * B))
     sample = sorted(set(part_bounds(B, 3)) | {1, 170, 299, 300, 511, 900})
-    check_against_oracle(frames, got, B, nf, w, h, "init", sample)
+    check_against_oracle(frames, got, B, nf, w, h, "init", sample, era=1 if era is None else era)
     check_against_sync(ctx, B, "init", got)
     ctx.close()
 
@@ -149,16 +156,17 @@ def test_async_pipeline_parts(B, ways):
     ctx.close()
 
 
-def test_c3_bench_pipeline_1080p_bf():
+@pytest.mark.parametrize("era", [None, 0], ids=["default-gcc48", "gcc49"])
+def test_c3_bench_pipeline_1080p_bf(era):
     """C3 exactly as benched: 1920x1080 / 2000 kp, 128-frame steps, three
     parts, async device brute-force pairs (k_match_bf_prev) at full size,
     alternating ranges; part boundaries and frame 0 (matched against the
-    cyclic predecessor 127) against the oracle."""
+    cyclic predecessor 127) against the oracle, in both retainBest eras."""
     w, h, nf, B = 1920, 1080, 2000, 128
-    frames, ctx = run_bench_pipeline(w, h, nf, B, "bf")
+    frames, ctx = run_bench_pipeline(w, h, nf, B, "bf", era=era)
     got = snapshot(ctx, range(2 * B))
     sample = sorted(set(part_bounds(B, 3)) | {64})
-    check_against_oracle(frames, got, B, nf, w, h, "bf", sample)
+    check_against_oracle(frames, got, B, nf, w, h, "bf", sample, era=1 if era is None else era)
     check_against_sync(ctx, B, "bf", got)
     ctx.close()
 

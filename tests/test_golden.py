@@ -16,7 +16,14 @@ from orb_slam_amd import synth_ba as sb
 from oracle_lib import KEYPOINT, RefExtractor, load, ptr
 
 GOLD = Path(__file__).resolve().parent / "golden"
-EXTRACT = ["extract_texture_320x240", "extract_noise_160x120", "extract_ragged_97x71"]
+# each image in both libstdc++ eras of retainBest: `<name>` GCC 4.6 .. 4.8
+# (the default), `<name>_gcc49` GCC >= 4.9 (tools/gen_golden.py ERAS)
+EXTRACT = [n + s for n in ("extract_texture_320x240", "extract_noise_160x120", "extract_ragged_97x71")
+           for s in ("", "_gcc49")]
+
+
+def era(z):
+    return int(z["nth_pivot"])
 
 
 def g(name):
@@ -38,9 +45,15 @@ def lba_problem(z):
 @pytest.mark.parametrize("name", EXTRACT)
 def test_oracle_extract_golden(name):
     z = g(name)
-    k, d = RefExtractor(int(z["nfeatures"]))(z["image"])
+    k, d = RefExtractor(int(z["nfeatures"]), nth_pivot=era(z))(z["image"])
     assert np.array_equal(k.view(np.uint8).reshape(-1, 28), z["keypoints"])
     assert np.array_equal(d, z["descriptors"])
+
+
+def test_golden_eras_differ():
+    """The two eras' vectors of each image differ (so both are pinned)."""
+    for n in EXTRACT[::2]:
+        assert not np.array_equal(g(n)["keypoints"], g(n + "_gcc49")["keypoints"]), n
 
 
 def test_oracle_search_init_golden():
@@ -102,6 +115,8 @@ def test_gpu_extract_golden(name):
     img = z["image"]
     c = ox.Context(nfeatures=int(z["nfeatures"]), max_w=img.shape[1], max_h=img.shape[0], slots=1)
     try:
+        if era(z) != 1:   # 1 is the default
+            c.set_nth_pivot(era(z))
         k, d = c(img)
     finally:
         c.close()

@@ -40,6 +40,13 @@ def random_lists(seed=3, count=400):
         yield keys, nth
 
 
+def test_default_era_is_gcc48():
+    """The oracle's default pivot rule is GCC 4.6 .. 4.8's (the product's
+    default, include/orbx.h), and RefExtractor uses it unless told."""
+    assert load().orbx_ref_get_nth_pivot() == 1
+    assert RefExtractor(100).nth_pivot == 1
+
+
 def test_restatement_equals_std_nth_element():
     """Pivot rule 0 reproduces this image's std::nth_element permutation
     exactly, on random lists with heavy ties and every size class."""
@@ -97,7 +104,8 @@ def test_product_nth_pivot_modes(score_type):
     """The device path with the GCC 4.6 .. 4.8 pivot rule equals the oracle
     with the same rule bit for bit (single frames, a 1080p frame whose long
     cell lists take the global-memory replay, and a 48-frame three-part
-    batch), and switching back restores the default rule."""
+    batch), and the GCC >= 4.9 rule likewise.  The GCC 4.6 .. 4.8 rule is the
+    default of a new context."""
     import orb_slam_amd as ox
     frames = synth.sequence(640, 480, 3, seed=2000)
     ref1 = RefExtractor(1000, score_type=score_type, nth_pivot=1)
@@ -105,6 +113,10 @@ def test_product_nth_pivot_modes(score_type):
     want = [ref1(f) for f in frames]
     B = 48
     ctx = ox.Context(nfeatures=1000, score_type=score_type, max_w=640, max_h=480, slots=B)
+    assert ox.lib().orbx_get_nth_pivot(ctx.handle) == 1   # the default era
+    for i, f in enumerate(frames):
+        k, d = ctx(f)
+        assert np.array_equal(k.view(np.uint8), want[i][0].view(np.uint8)) and np.array_equal(d, want[i][1]), i
     ctx.set_nth_pivot(1)
     for i, f in enumerate(frames):
         k, d = ctx(f)

@@ -35,13 +35,19 @@ def extract_cases():
     ]
 
 
+# retainBest's libstdc++ era (orbx_ref_set_nth_pivot): 1 = GCC 4.6 .. 4.8,
+# the default (`<name>.npz`); 0 = GCC >= 4.9 (`<name>_gcc49.npz`)
+ERAS = {1: "", 0: "_gcc49"}
+
+
 def gen_extract():
     for name, img, nf in extract_cases():
-        e = RefExtractor(nf, 1.2, 8, 20)
-        k, d = e(img)
-        np.savez_compressed(OUT / f"{name}.npz", image=img, nfeatures=nf, keypoints=k.view(np.uint8).reshape(-1, 28),
-                            descriptors=d)
-        print(name, len(k))
+        for era, suffix in ERAS.items():
+            e = RefExtractor(nf, 1.2, 8, 20, nth_pivot=era)
+            k, d = e(img)
+            np.savez_compressed(OUT / f"{name}{suffix}.npz", image=img, nfeatures=nf, nth_pivot=era,
+                                keypoints=k.view(np.uint8).reshape(-1, 28), descriptors=d)
+            print(name + suffix, len(k))
 
 
 def gen_init_match():
@@ -150,6 +156,9 @@ def gen_vocab():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["extract"]:   # only the extraction vectors (both eras)
+        gen_extract()
+        sys.exit(0)
     OUT.mkdir(parents=True, exist_ok=True)
     gen_extract()
     gen_init_match()
