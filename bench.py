@@ -631,7 +631,7 @@ def run_lba(args, wl, rank, local, world, dist):
     check_rc(L.orbx_lba_stage(ctx.handle, P, arr), "orbx_lba_stage")
 
     def step():
-        check_rc(L.orbx_lba_run(ctx.handle, 5, 10), "orbx_lba_run")
+        check_rc(L.orbx_lba_run(ctx.handle, 5, 10, None), "orbx_lba_run")
 
     for _ in range(args.warmup):
         step()
@@ -656,7 +656,7 @@ def run_lba(args, wl, rank, local, world, dist):
                 np.copyto(a["pose_q"], pr["pose_q"])
                 np.copyto(a["pose_t"], pr["pose_t"])
                 np.copyto(a["points"], pr["points"])
-            check_rc(L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, esp, pbp, (sb.BAStats * P)()),
+            check_rc(L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, None, esp, pbp, (sb.BAStats * P)()),
                      "orbx_lba_solve_batch")
         host_step()
         n_host = max(3, args.steps // 4)
@@ -816,7 +816,16 @@ def init_ranks(world, local):
     device = local % ngpu if ngpu else 0
     if ngpu:
         torch.cuda.set_device(device)
-    tdist.init_process_group(backend)
+    # gloo announces its connections on stdout from C++; stdout carries the
+    # one JSON line, so the process group is set up with fd 1 on stderr
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        tdist.init_process_group(backend)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     return tdist, device, ("cuda" if backend == "nccl" else "cpu")
 
 

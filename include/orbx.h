@@ -626,19 +626,27 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
                    const volatile uint8_t* abort, uint8_t* edge_status,
                    uint8_t* point_bad, orbx_ba_stats* stats);
 
-/* Batched throughput form: P independent problems, one workgroup each. */
+/* Batched throughput form: P independent problems, one workgroup each.
+ * aborts: NULL, or P flags (entries may be NULL), each polled between LM
+ * iterations like orbx_lba_solve's: problem i stops its optimize() calls
+ * when *aborts[i] is set (its own LocalMapping's mbAbortBA,
+ * src/LocalMapping.cc:83, :125), the others continue.  Polling makes the
+ * call wait for each iteration; without flags the iterations are queued
+ * back to back. */
 int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems,
-                         int iters0, int iters1, uint8_t* const* edge_status,
-                         uint8_t* const* point_bad, orbx_ba_stats* stats);
+                         int iters0, int iters1, const volatile uint8_t* const* aborts,
+                         uint8_t* const* edge_status, uint8_t* const* point_bad,
+                         orbx_ba_stats* stats);
 /* Device-resident form of the batch (bench/tests; the pose API's shape):
  * stage P problems in HBM once (validated as orbx_lba_solve_batch does),
  * run both optimize() passes from the staged state any number of times
  * (asynchronous, on the context stream; kernel timers "lba_iter" /
  * "lba_outliers"), fetch the last run's poses, points, flags and statistics
  * into problems laid out like the staged ones (ORBX_ERR_ARG before a run or
- * on a size mismatch). */
+ * on a size mismatch).  orbx_lba_run's aborts are orbx_lba_solve_batch's
+ * (NULL: asynchronous; with flags the call returns when the run is done). */
 int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems);
-int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1);
+int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1, const volatile uint8_t* const* aborts);
 int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edge_status,
                    uint8_t* const* point_bad, orbx_ba_stats* stats);
 

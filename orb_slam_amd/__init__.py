@@ -97,9 +97,9 @@ def _declare(L):
         "orbx_search_local_map": ([vp, vp], i),
         "orbx_search_local_map_batch": ([vp, i, vp], i),
         "orbx_lba_solve": ([vp, vp, i, i, vp, vp, vp, vp], i),
-        "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp], i),
+        "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp, vp], i),
         "orbx_lba_stage": ([vp, i, vp], i),
-        "orbx_lba_run": ([vp, i, i], i),
+        "orbx_lba_run": ([vp, i, i, vp], i),
         "orbx_lba_fetch": ([vp, vp, vp, vp, vp], i),
         "orbx_search_by_bow_frame": ([vp, vp, vp, f, i, vp, ip], i),
         "orbx_search_by_bow_kf": ([vp, vp, vp, f, i, vp, ip], i),

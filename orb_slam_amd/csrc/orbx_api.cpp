@@ -222,7 +222,7 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
 {
     if (!out) return ORBX_ERR_ARG;
     *out = nullptr;
-    if (nfeatures <= 0 || nfeatures > 4096 || nlevels <= 0 || nlevels > kMaxLevels ||
+    if (nfeatures <= 0 || nfeatures > kMaxFeatures || nlevels <= 0 || nlevels > kMaxLevels ||
         !(scale_factor > 1.0f) || max_w <= 0 || max_h <= 0 || max_w > 4095 || max_h > 4095 ||
         max_batch <= 0 || fast_th < 1 || fast_th > 255)
         return ORBX_ERR_ARG;

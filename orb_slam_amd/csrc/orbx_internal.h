@@ -37,6 +37,14 @@ constexpr int kEdge = 16;        // EDGE_THRESHOLD (src/ORBextractor.cc:77)
 constexpr int kHalfPatch = 15;   // HALF_PATCH_SIZE (:76)
 constexpr int kPatch = 31;       // PATCH_SIZE (:75)
 constexpr int kMaxLevels = 16;
+// Largest nfeatures of a context.  The reference's constructor has no bound
+// (src/ORBextractor.cc:457-487); its callers use Settings.yaml's nFeatures
+// (1000, Data/Settings.yaml) and twice that for the initialisation extractor
+// (src/Tracking.cc:128), so 4096 covers nFeatures up to 2048.  Kernels that
+// pack a keypoint index into a key field depend on it: the brute-force keys
+// (16 bits, orbx_match.hip), the matcher frame views (orbx_search.hip,
+// orbx_kfproj.hip); each checks it where it packs.
+constexpr int kMaxFeatures = 4096;
 constexpr int kGridCols = 64;    // FRAME_GRID_COLS (include/Frame.h:35)
 constexpr int kGridRows = 48;    // FRAME_GRID_ROWS (include/Frame.h:36)
 #ifndef ORBX_BLUR_STRIP

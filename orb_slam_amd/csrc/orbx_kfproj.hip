@@ -355,7 +355,7 @@ inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 bool valid_kf(const orbx_frame_view* v)
 {
-    return v && v->n >= 0 && v->n <= 4096 && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
+    return v && v->n >= 0 && v->n <= kMaxFeatures && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
            v->max_y > v->min_y && v->nlevels > 0 && v->nlevels <= kMaxLevels;
 }
 

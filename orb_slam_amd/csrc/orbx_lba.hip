@@ -1515,9 +1515,12 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
 
 // Queues both optimize() passes of a staged batch on the context stream:
 // k_lba_build, iterations, outliers, k_lba_rebuild, iterations, outliers.
-// With an abort flag the host polls it (and the problems' status) between
-// iterations, which synchronises; without one nothing waits.
-static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, const volatile uint8_t* abort)
+// With abort flags (per problem, entries may be null) the host polls them
+// (and the problems' status) between iterations, which synchronises; an
+// aborted problem's later iterations return at once (g2o's force-stop flag,
+// sparse_optimizer.cpp:394-396); without flags nothing waits.
+static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
+                      const volatile uint8_t* const* aborts)
 {
     const int P = L.P;
     uint8_t* d = L.d;
@@ -1528,7 +1531,10 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, c
     ORBX_HIP_CHECK(hipGetLastError());
     const size_t lds = std::min(L.max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
     const int lds_cap = (int)(lds / 8);
-    std::vector<LbaDev> hv(abort ? P : 0);
+    bool polled = false;
+    for (int i = 0; aborts && i < P; i++) polled |= aborts[i] != nullptr;
+    std::vector<LbaDev> hv(polled ? P : 0);
+    std::vector<uint8_t> stopped(P, 0);   // abort written to the device
     for (int pass = 0; pass < 2; pass++) {
         LbaDev* dd = reinterpret_cast<LbaDev*>(d + (pass == 0 ? L.o_devs : L.o_devs1));
         if (pass == 1) {
@@ -1540,14 +1546,24 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, c
             ORBX_HIP_CHECK(hipGetLastError());
         }
         const int iters = pass == 0 ? iters0 : iters1;
+        if (pass == 1)   // k_lba_rebuild carries each problem's abort into the second pass
+            for (int i = 0; i < P; i++) stopped[i] = 0;
         for (int it = 0; it < iters; it++) {
-            if (abort && *abort) {
+            if (polled) {
                 const int one = 1;
-                for (int i = 0; i < P; i++)
-                    ORBX_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(dd + i) + offsetof(LbaDev, abort), &one, 4,
-                                                  hipMemcpyHostToDevice, ctx->stream));
-                ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-                break;
+                bool any = false, all = true;
+                for (int i = 0; i < P; i++) {
+                    const bool stop = aborts[i] && *aborts[i];
+                    if (stop && !stopped[i]) {
+                        ORBX_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(dd + i) + offsetof(LbaDev, abort),
+                                                      &one, 4, hipMemcpyHostToDevice, ctx->stream));
+                        stopped[i] = 1;
+                        any = true;
+                    }
+                    all &= stop;
+                }
+                if (any) ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));   // &one outlives the copy
+                if (all) break;
             }
             timer_begin(ctx, "lba_iter");
             hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, lds_cap);
@@ -1557,11 +1573,11 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, c
             // g2o polls its force-stop flag), which needs the device state;
             // without one, iterations are queued back to back and a
             // terminated problem's later launches return immediately.
-            if (abort) {
+            if (polled) {
                 ORBX_HIP_CHECK(hipMemcpyAsync(hv.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
                 ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
                 bool running = false;
-                for (int i = 0; i < P; i++) running |= hv[i].status == kRunning;
+                for (int i = 0; i < P; i++) running |= hv[i].status == kRunning && !hv[i].abort;
                 if (!running) break;
             }
         }
@@ -1631,7 +1647,7 @@ static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs,
 // the context scratch, filled by host threads straight into the pinned
 // buffer, one copy each way.
 static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int iters1,
-                   const volatile uint8_t* abort, uint8_t* const* edge_status, uint8_t* const* point_bad,
+                   const volatile uint8_t* const* aborts, uint8_t* const* edge_status, uint8_t* const* point_bad,
                    orbx_ba_stats* stats)
 {
     ctx_enter(ctx);
@@ -1640,7 +1656,7 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     if (r != ORBX_OK) return r;
     if (L.dev_end > ctx->scratch_bytes && (r = ensure_scratch(ctx, L.dev_end)) != ORBX_OK) return r;
     if ((r = lba_plan_stage(ctx, P, probs, static_cast<uint8_t*>(ctx->scratch), L)) != ORBX_OK) return r;
-    if ((r = lba_launch(ctx, L, iters0, iters1, abort)) != ORBX_OK) return r;
+    if ((r = lba_launch(ctx, L, iters0, iters1, aborts)) != ORBX_OK) return r;
     return lba_readback(ctx, L, probs, edge_status, point_bad, stats);
 }
 
@@ -1701,7 +1717,7 @@ static int lba_stage_resident(orbx_ctx* ctx, int P, const orbx_ba_problem* probs
     return ORBX_OK;
 }
 
-static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1)
+static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1, const volatile uint8_t* const* aborts)
 {
     if (!ctx->lba_res || ctx->lba_res->plan.P == 0) return ORBX_ERR_ARG;
     ctx_enter(ctx);
@@ -1715,7 +1731,7 @@ static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1)
     ORBX_HIP_CHECK(hipMemcpyAsync(d + L.o_devs, img + L.o_devs, L.staged_end - L.o_devs, hipMemcpyDeviceToDevice,
                                   ctx->stream));
     R.solved = true;
-    return lba_launch(ctx, L, iters0, iters1, nullptr);
+    return lba_launch(ctx, L, iters0, iters1, aborts);
 }
 
 }  // namespace orbx
@@ -1736,15 +1752,17 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1, co
     if (stats) std::memset(stats, 0, sizeof(*stats));
     uint8_t* es[1] = {edge_status};
     uint8_t* pb[1] = {point_bad};
-    return orbx::lba_run(ctx, 1, p, iters0, iters1, abort, es, pb, stats);
+    const volatile uint8_t* ab[1] = {abort};
+    return orbx::lba_run(ctx, 1, p, iters0, iters1, ab, es, pb, stats);
 }
 
 int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems, int iters0, int iters1,
-                         uint8_t* const* edge_status, uint8_t* const* point_bad, orbx_ba_stats* stats)
+                         const volatile uint8_t* const* aborts, uint8_t* const* edge_status,
+                         uint8_t* const* point_bad, orbx_ba_stats* stats)
 {
     if (!ctx || P <= 0 || !problems || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
     if (stats) std::memset(stats, 0, sizeof(*stats) * P);
-    return orbx::lba_run(ctx, P, problems, iters0, iters1, nullptr, edge_status, point_bad, stats);
+    return orbx::lba_run(ctx, P, problems, iters0, iters1, aborts, edge_status, point_bad, stats);
 }
 
 int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems)
@@ -1753,10 +1771,10 @@ int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems)
     return orbx::lba_stage_resident(ctx, P, problems);
 }
 
-int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1)
+int orbx_lba_run(orbx_ctx* ctx, int iters0, int iters1, const volatile uint8_t* const* aborts)
 {
     if (!ctx || iters0 < 0 || iters1 < 0) return ORBX_ERR_ARG;
-    return orbx::lba_run_resident(ctx, iters0, iters1);
+    return orbx::lba_run_resident(ctx, iters0, iters1, aborts);
 }
 
 int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edge_status, uint8_t* const* point_bad,

@@ -299,11 +299,16 @@ extern "C" int orbx_debug_match_prof(unsigned long long* out)
 }
 #endif
 
+// Both brute-force kernels pack the candidate index into the low 16 bits of
+// their (distance, index) keys.
+static_assert(kMaxFeatures <= 0xFFFF, "brute-force keys hold the candidate index in 16 bits");
+
 int launch_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio,
                          hipStream_t st)
 {
     if (!st) st = ctx->stream;
     const Geometry& g = ctx->geom;
+    if (g.nfeatures > 0xFFFF) return ORBX_ERR_UNSUPPORTED;   // the 16-bit index field of the keys
     MatchPrevArgs a{};
     a.kps = ctx->out_kps;
     a.desc = ctx->out_desc;

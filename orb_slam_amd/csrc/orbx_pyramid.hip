@@ -589,25 +589,9 @@ static int ensure_dev(T*& ptr, size_t count)
 
 int upload_pyramid_plan(orbx_ctx* ctx)
 {
-#ifdef ORBX_AB_KNOBS   // experiment builds only: step size and plan dump from the environment
-    const char* e = getenv("ORBX_PYR_T");
-    const int T = e ? std::max(1, atoi(e)) : 8;
-    const bool verbose = getenv("ORBX_PYR_VERBOSE") != nullptr;
-#else
-    const int T = 8;
-    const bool verbose = false;
-#endif
+    constexpr int T = 8;   // level-0 rows per step (4 / 8 / 16 measured equal)
     plan_pyramid(ctx->geom, T, ctx->pyr);
     const PyrPlan& p = ctx->pyr;
-    if (verbose) {   // diagnostics: the plan on stderr
-        fprintf(stderr, "pyramid plan %dx%d: ok=%d T=%d S=%d lds=%d rings:", ctx->geom.w, ctx->geom.h, (int)p.ok, p.T,
-                p.S, p.lds_bytes);
-        for (const PyrLevel& q : p.levels) fprintf(stderr, " %d", q.ring);
-        fprintf(stderr, "\n");
-        for (int wv = 0; wv < kPyrWaves && p.ok; wv++)
-            fprintf(stderr, "  wave %2d: blur L%d q%d  resize L%d q%d  l0 %d\n", wv, p.waves[wv].blur_level,
-                    p.waves[wv].blur_q0, p.waves[wv].res_level, p.waves[wv].res_q0, p.waves[wv].l0_base);
-    }
     if (!p.ok) return ORBX_OK;
     int r;
     if (!ctx->d_pyr_levels && (r = ensure_dev(ctx->d_pyr_levels, kMaxLevels)) != ORBX_OK) return r;

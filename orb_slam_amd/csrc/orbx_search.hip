@@ -537,7 +537,7 @@ int get(orbx_ctx* ctx, void* dst, size_t off, size_t bytes)
 
 bool valid_view(const orbx_frame_view* v)
 {
-    return v && v->n >= 0 && v->n <= 4096 && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
+    return v && v->n >= 0 && v->n <= kMaxFeatures && (v->n == 0 || (v->keys_un && v->desc)) && v->max_x > v->min_x &&
            v->max_y > v->min_y && v->nlevels > 0 && v->nlevels <= kMaxLevels;
 }
 

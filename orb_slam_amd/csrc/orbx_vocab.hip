@@ -138,9 +138,12 @@ __global__ __launch_bounds__(kBowBuildThreads) void k_bow_build(const int32_t* n
         // pass 0: (node, feature) -> FeatureVector; pass 1: (word, feature) -> BowVector
         int valid = 0;
         for (int p = tid; p < N; p += kBowBuildThreads) {
+            // entries past n (the power-of-two padding) belong to the next
+            // slot or past the array: only p < n is read
             const bool ok = p < n && b.weight[o + p] > 0.0;
-            const uint32_t id = (uint32_t)(pass == 0 ? b.node[o + p] : b.word[o + p]);
-            keys[p] = ok ? ((uint64_t)id << 32 | (uint32_t)p) : ~0ull;
+            uint64_t key = ~0ull;
+            if (ok) key = (uint64_t)(uint32_t)(pass == 0 ? b.node[o + p] : b.word[o + p]) << 32 | (uint32_t)p;
+            keys[p] = key;
             valid += ok;
         }
         const int m = block_sum(valid, bs, 0);   // includes the barrier after the fill

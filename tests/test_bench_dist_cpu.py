@@ -27,8 +27,8 @@ def _run(args, env_extra=None, timeout=300):
 
 def _line(p):
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout   # rank 0 only
+    lines = p.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout   # rank 0's JSON line, nothing else
     return json.loads(lines[0])
 
 

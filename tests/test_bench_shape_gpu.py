@@ -187,7 +187,7 @@ def test_c5_resident_batch_256_vs_oracle():
     arr = (sb.BAProblem * P)(*[c[0] for c in work])
     assert L.orbx_lba_stage(ctx.handle, P, arr) == 0
     for _ in range(2):
-        assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+        assert L.orbx_lba_run(ctx.handle, 5, 10, None) == 0
     es = [np.zeros(c[0].n_edges, np.uint8) for c in work]
     pb = [np.zeros(c[0].n_points, np.uint8) for c in work]
     esp = (ctypes.c_void_p * P)(*[e.ctypes.data for e in es])

@@ -101,7 +101,7 @@ def test_lba_batch_equals_single(ctx):
     esp = (ctypes.c_void_p * 4)(*[e.ctypes.data for e in es])
     pbp = (ctypes.c_void_p * 4)(*[b.ctypes.data for b in pb])
     st = (sb.BAStats * 4)()
-    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, esp, pbp, st) == 0
+    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, None, esp, pbp, st) == 0
     for k in range(4):
         a = cps[k][1]
         s = singles[k]
@@ -110,6 +110,43 @@ def test_lba_batch_equals_single(ctx):
         assert np.array_equal(a["pose_q"], s[0]["pose_q"]) and np.array_equal(a["pose_t"], s[0]["pose_t"])
         assert np.array_equal(a["points"], s[0]["points"])
         assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
+
+
+def test_lba_batch_per_problem_abort(ctx):
+    """orbx_lba_solve_batch / orbx_lba_run with per-problem abort flags
+    (each problem's LocalMapping mbAbortBA, src/LocalMapping.cc:83, :125): a
+    flagged problem runs no LM iteration in either optimize() call and keeps
+    its poses; the others (flag NULL or 0) equal their single solves."""
+    probs = [sb.make_problem(n_kf=6 + k, n_points=200 + 50 * k, seed=60 + k) for k in range(4)]
+    singles = [run_gpu(ctx, pr) for pr in probs]
+    flags = [ctypes.c_uint8(v) for v in (0, 1, 0, 1)]
+    ab = (ctypes.c_void_p * 4)(ctypes.addressof(flags[0]), ctypes.addressof(flags[1]), None,
+                               ctypes.addressof(flags[3]))
+    L = ox.lib()
+    for resident in (False, True):
+        cps = [sb.to_ctypes(pr) for pr in probs]
+        arr = (sb.BAProblem * 4)(*[c[0] for c in cps])
+        es = [np.zeros(c[0].n_edges, np.uint8) for c in cps]
+        pb = [np.zeros(c[0].n_points, np.uint8) for c in cps]
+        esp = (ctypes.c_void_p * 4)(*[e.ctypes.data for e in es])
+        pbp = (ctypes.c_void_p * 4)(*[b.ctypes.data for b in pb])
+        st = (sb.BAStats * 4)()
+        if resident:
+            assert L.orbx_lba_stage(ctx.handle, 4, arr) == 0
+            assert L.orbx_lba_run(ctx.handle, 5, 10, ab) == 0
+            assert L.orbx_lba_fetch(ctx.handle, arr, esp, pbp, st) == 0
+        else:
+            assert L.orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, ab, esp, pbp, st) == 0
+        for k in range(4):
+            a = cps[k][1]
+            if k in (1, 3):
+                assert list(st[k].iterations) == [0, 0], (resident, k)
+                assert np.array_equal(a["pose_q"], probs[k]["pose_q"]) and np.array_equal(a["points"], probs[k]["points"])
+            else:
+                s = singles[k]
+                assert list(st[k].iterations) == list(s[3].iterations), (resident, k)
+                assert np.array_equal(a["pose_q"], s[0]["pose_q"]) and np.array_equal(a["points"], s[0]["points"])
+                assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
 
 
 def test_lba_resident_equals_batch(ctx):
@@ -128,7 +165,7 @@ def test_lba_resident_equals_batch(ctx):
         return cps, arr, es, pb, esp, pbp, (sb.BAStats * 4)()
 
     cps, arr, es, pb, esp, pbp, st = marshal()
-    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, esp, pbp, st) == 0
+    assert ox.lib().orbx_lba_solve_batch(ctx.handle, 4, arr, 5, 10, None, esp, pbp, st) == 0
     L = ox.lib()
     s_cps, s_arr, _, _, _, _, _ = marshal()
     assert L.orbx_lba_stage(ctx.handle, 4, s_arr) == 0
@@ -136,7 +173,7 @@ def test_lba_resident_equals_batch(ctx):
     assert L.orbx_lba_fetch(ctx.handle, r_arr, r_esp, r_pbp, r_st) == -1   # nothing run yet
     runs = []
     for _ in range(2):
-        assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+        assert L.orbx_lba_run(ctx.handle, 5, 10, None) == 0
         r_cps, r_arr, r_es, r_pb, r_esp, r_pbp, r_st = marshal()
         assert L.orbx_lba_fetch(ctx.handle, r_arr, r_esp, r_pbp, r_st) == 0
         runs.append((r_cps, r_es, r_pb, r_st))
@@ -204,16 +241,16 @@ def test_lba_failed_stage_refuses_run(ctx):
     small = [sb.to_ctypes(sb.make_problem(n_kf=4, n_points=100, seed=60 + k)) for k in range(2)]
     arr = (sb.BAProblem * 2)(*[c[0] for c in small])
     assert L.orbx_lba_stage(ctx.handle, 2, arr) == 0
-    assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+    assert L.orbx_lba_run(ctx.handle, 5, 10, None) == 0
     big = [sb.to_ctypes(sb.make_problem(n_kf=12, n_points=900, seed=70 + k)) for k in range(6)]
     big[-1][1]["edge_point"][7] = big[-1][0].n_points + 3          # invalid edge
     barr = (sb.BAProblem * 6)(*[c[0] for c in big])
     assert L.orbx_lba_stage(ctx.handle, 6, barr) == -1
-    assert L.orbx_lba_run(ctx.handle, 5, 10) == -1
+    assert L.orbx_lba_run(ctx.handle, 5, 10, None) == -1
     assert L.orbx_lba_fetch(ctx.handle, arr, None, None, None) == -1
     big[-1][1]["edge_point"][7] = 0
     assert L.orbx_lba_stage(ctx.handle, 6, barr) == 0
-    assert L.orbx_lba_run(ctx.handle, 5, 10) == 0
+    assert L.orbx_lba_run(ctx.handle, 5, 10, None) == 0
     assert L.orbx_lba_fetch(ctx.handle, barr, None, None, None) == 0
 
 
@@ -233,7 +270,7 @@ def test_lba_bitwise_reproducible(ctx):
         esp = (ctypes.c_void_p * len(batch))(*[e.ctypes.data for e in es])
         pbp = (ctypes.c_void_p * len(batch))(*[b.ctypes.data for b in pb])
         st = (sb.BAStats * len(batch))()
-        assert ox.lib().orbx_lba_solve_batch(ctx.handle, len(batch), arr, 5, 10, esp, pbp, st) == 0
+        assert ox.lib().orbx_lba_solve_batch(ctx.handle, len(batch), arr, 5, 10, None, esp, pbp, st) == 0
         runs.append((cps[pos][1], es[pos], pb[pos], st[pos]))
     a0, e0, p0, s0 = runs[0]
     for a, e, p, s in runs[1:]:

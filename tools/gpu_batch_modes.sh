@@ -5,6 +5,6 @@ out=gpurun_out/$1
 mkdir -p "$out"
 export TMPDIR=/tmp
 for m in 0 1; do for b in 256 512 1024; do
-ORBX_PYR_MODE=$m timeout -k 10 200 python3 bench.py --batch $b --no-cpu-baseline --no-isolated > "$out/m${m}_b$b.json" 2>&1
+timeout -k 10 200 python3 bench.py --pyramid-mode $m --batch $b --no-cpu-baseline --no-isolated > "$out/m${m}_b$b.json" 2>&1
 done; done
 echo ok

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q -k "extract or match or pipeline or smoke" --timeout 120 --timeout-method thread > "$out/tests.log" 2>&1
 for rep in 1 2; do
 timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-isolated > "$out/w3_r$rep.json" 2>&1
-ORBX_SPLIT_WAYS=2 timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-isolated > "$out/w2_r$rep.json" 2>&1
+timeout -k 10 200 python3 bench.py --split-ways 2 --no-cpu-baseline --no-isolated > "$out/w2_r$rep.json" 2>&1
 done
 timeout -k 10 200 python3 bench.py --batch 1536 --no-cpu-baseline --no-isolated > "$out/w3_b1536.json" 2>&1
 echo ok

@@ -26,7 +26,7 @@ L.orbx_debug_lba_prof.argtypes = [ctypes.c_void_p]
 before = (ctypes.c_ulonglong * 16)()
 L.orbx_debug_lba_prof(before)
 st = (sb.BAStats * P)()
-assert L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, esp, pbp, st) == 0
+assert L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, None, esp, pbp, st) == 0
 after = (ctypes.c_ulonglong * 16)()
 L.orbx_debug_lba_prof(after)
 d = [a - b for a, b in zip(after, before)]
