@@ -2,37 +2,48 @@
 // Optimizer::LocalBundleAdjustment (src/Optimizer.cc:287-536) on the g2o
 // subset it uses (BlockSolverX + Schur over the points, Levenberg).
 //
+// Layout.  A problem's active edges are stored point-major: each active
+// point's edges contiguous, in the caller's edge order, as 16-byte records
+// (observation and information as the floats the reference has --
+// cv::KeyPoint::pt, KeyFrame::mvInvLevelSigma2 -- whenever every value of the
+// batch is a float, else 32-byte double records), so the passes that walk a
+// point's edges (errors, linearisation, Schur complement, back-substitution)
+// stream them; a per-free-pose list of (record, point) pairs serves the pose
+// blocks of the linearisation.  The poses (quaternion, translation, rotation
+// matrix, camera) of the problem live in LDS for the whole launch.
+//
 // Device work per LM iteration (one 512-thread workgroup per problem, one
 // launch per iteration so the caller's abort flag is polled between
 // iterations exactly where SparseOptimizer::optimize polls terminate()):
-//   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2
-//   linearize EdgeSE3ProjectXYZ::linearizeOplus + constructQuadraticForm per
-//             edge into component-major (SoA) rows; per pose (Hpp, bp) one
-//             wave with a fixed butterfly reduction, per point (Hll, bl) one
-//             thread in edge order
-//   trial     Schur point by point (a point's edges are contiguous): Dinv,
-//             db, then bs -= W_i db and S(i,j) -= W_i Dinv W_j^T for every
-//             pair of its edges.  The W_i = Hpl blocks are rebuilt from the
-//             edge's inputs (pose, point, observation) where they are used
-//             instead of being stored per edge and re-read from HBM.  The
-//             reduced camera system is accumulated in 2^-51 fixed point with
-//             64-bit integer atomics (two limbs per entry, packed lower
-//             triangle in LDS): integer sums do not depend on the order the
-//             points arrive in, so the result is bitwise reproducible
-//             (g2o sums the points sequentially in double; the two differ by
-//             rounding only).  Dense LLT on the packed triangle; one-wave
-//             triangular solves; back-substitution for the points; exp-map
-//             update; accept / reject with g2o's rho rule
+//   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2 --
+//             only in an optimize() call's first iteration: every later
+//             iteration starts at the state the previous iteration's accepted
+//             trial just evaluated, bit for bit
+//   linearize EdgeSE3ProjectXYZ::linearizeOplus + constructQuadraticForm: per
+//             point (Hll, bl) one thread in edge order; per pose (Hpp, bp)
+//             one wave with a fixed butterfly reduction
+//   trial     Schur point by point (thread per point, its free-pose edges):
+//             Dinv, db, then bs -= W_i db and S(i,j) -= W_i Dinv W_j^T for
+//             every pair, W_i = B_i^T w A_i never formed (the pair's 6x6
+//             block as (w B_i)^T [(A_i Dinv) A_j^T] (w B_j)).  The reduced
+//             camera system is accumulated in scaled fixed point with 64-bit
+//             integer atomics (two limbs per entry, packed lower triangle in
+//             LDS): integer sums do not depend on the order the points arrive
+//             in, so the result is bitwise reproducible (g2o sums the points
+//             sequentially in double; the two differ by rounding only).
+//             Dense LLT on the packed triangle; one-wave triangular solves;
+//             exp-map update of the poses; then one pass per point does the
+//             back-substitution, the point update and the trial's errors
+//             (computeActiveErrors) together; accept / reject with g2o's rho
+//             rule
 //   Raul stop rule (levenberg.cpp:154-161)
 // Index structures (g2o's initializeOptimization / buildStructure) are built
-// on the host once per optimize() call.
+// on the device: k_lba_build for the first optimize() call, k_lba_rebuild
+// (order-preserving filters) for the second.
 #include <algorithm>
 #include <cmath>
 #include <cstddef>
 #include <cstring>
-#include <chrono>
-#include <cstdio>
-#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -42,38 +53,45 @@
 
 namespace orbx {
 
+// Active edge, point-major.  pose: index into the problem's poses; ph: its
+// pose block (free poses in g2o id order) or -1 for a fixed pose.
+struct EdgeRecF {
+    float ox, oy, isig;
+    uint16_t pose;
+    int16_t ph;
+};
+struct EdgeRecD {
+    double ox, oy, isig;
+    uint16_t pose;
+    int16_t ph;
+    int32_t pad;
+};
+static_assert(sizeof(EdgeRecF) == 16 && sizeof(EdgeRecD) == 32, "edge record layout");
+
 struct LbaDev {
     int nP, nL, nE;                // free poses, active points, active edges
     int nposes_all, npoints_all, nedges_all;
     int dim_p;                     // 6 * nP
     double* pose;                  // [nposes_all][7]: qx qy qz qw tx ty tz
     double* point;                 // [npoints_all][3]
-    double* pose_bk;
-    double* point_bk;
+    double* point_bk;              // [nL][3] active points before the trial
     const double* cam;             // [nposes_all][4]
-    // active edges in g2o order (SoA over active index)
-    const int* e_orig;             // original edge index
-    const int* e_pose;             // pose index
-    const int* e_point;            // point index
-    const int* e_ph;               // pose hessian index or -1 (fixed)
-    const int* e_lh;               // point hessian index
-    const double* e_obs;           // [nE][2]
-    const double* e_isig;          // [nE]
-    double* err;                   // [nedges_all][2] last computed errors (original index)
-    const int* iv_pose;            // [nP]
-    const int* iv_point;           // [nL]
-    const int* pe_ptr; const int* pe_idx;   // per free pose: active edges, edge order
-    const int* le_ptr; const int* le_idx;   // per point: active edges, edge order
-    const int* lc_ptr; const int* lc_idx;   // per point: Schur column (free poses, pose order)
+    // active edges, point-major (active point l's edges: le_ptr[l] .. le_ptr[l + 1])
+    const void* rec;               // EdgeRecF / EdgeRecD [nE]
+    const int* e_orig;             // [nE] caller's edge index
+    const int* iv_pose;            // [nP] pose index of each free pose block
+    const int* iv_point;           // [nL] point index of each active point (g2o id order)
+    const int* le_ptr;             // [nL + 1]
+    const int* pe_ptr;             // [nP + 1]
+    const int2* pe_idx;            // per free pose, its edges in edge order: (record, point index)
+    double* err;                   // [nedges_all][2] last computed errors (caller's index)
+    double* ew;                    // [nE] robust weight rho' * invSigma2 of the linearisation
     // scratch
-    double* ce;                    // index maps of k_lba_build / k_lba_rebuild (no Hpl blocks are stored)
+    int* ce;                       // points by edge count (iteration kernel); build / rebuild maps
     double* hp;                    // [nP][27]: Hpp upper 21 | bp 6
     double* hl;                    // [nL][9]: Hll upper 6 | bl 3
-    double* dl;                    // [nL][12]: Dinv 9 | db 3
+    double* dl;                    // [nL][12]: Dinv | db of the trial
     double* S;                     // reduced system, lba_sys_doubles(dim_p) (global fallback of the LDS copy)
-    double* x;                     // [dim_p + 3 nL]
-    double* bs;                    // [dim_p]
-    double* ew;                    // [nE] robust weight rho' * invSigma2 of the linearisation
     // the caller's problem arrays (staged; read by k_lba_build only)
     const int* r_edge_pose;
     const int* r_edge_point;
@@ -85,6 +103,7 @@ struct LbaDev {
     double huber_delta;
     // LM state
     double lambda, ni, current_chi, last_chi, chi2_initial;
+    double hmax, bmax;             // this linearisation's max Hpp diagonal and max |b| (fixed-point scales)
     int nBad, status, iterations, trials, not_posdef;
     int abort;
 };
@@ -94,7 +113,7 @@ enum { kRunning = 0, kTerminated = 1 };
 // Phase timing of block 0 (diagnostic build only: -DORBX_LBA_PROFILE).
 #ifdef ORBX_LBA_PROFILE
 __device__ unsigned long long g_lba_prof[16];
-__device__ inline unsigned long long lba_stamp()
+__device__ __forceinline__ unsigned long long lba_stamp()
 {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -113,40 +132,33 @@ __device__ inline unsigned long long lba_stamp()
 #define LBA_MARK(k)
 #endif
 
-constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem
+constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem: the phases need up to 255 VGPRs
 constexpr int kLbaWaves = kLbaThreads / 64;
-constexpr int kSchurEdges = 8;                 // per-thread LDS edge table of the Schur pass (32 KB)
-#ifndef ORBX_SCHUR_GROUP
-#define ORBX_SCHUR_GROUP 2
-#endif
-constexpr int kSchurGroup = ORBX_SCHUR_GROUP;  // edges whose W_i Dinv share one pass over the later W_j
-
-
+constexpr int kPz = 20;                        // LDS doubles per pose: q(4) t(3) R(9) cam(4)
+constexpr int kPbk = 16;                       // LDS doubles per free-pose backup: q(4) t(3) R(9)
 
 // ---------------------------------------------------------------------------
 // Block reductions in double
 // ---------------------------------------------------------------------------
 struct DScratch {
     double w[kLbaWaves];
-    double v[4];
-    int iv[4];
 };
 
-__device__ inline double wave_sum_d(double v)
+__device__ __forceinline__ double wave_sum_d(double v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-__device__ inline double wave_max_d(double v)
+__device__ __forceinline__ double wave_max_d(double v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
 
-__device__ inline double block_sum_d(double v, DScratch& s)
+__device__ __forceinline__ double block_sum_d(double v, DScratch& s)
 {
     v = wave_sum_d(v);
     __syncthreads();
@@ -157,7 +169,7 @@ __device__ inline double block_sum_d(double v, DScratch& s)
     return t;
 }
 
-__device__ inline double block_max_d(double v, DScratch& s)
+__device__ __forceinline__ double block_max_d(double v, DScratch& s)
 {
     v = wave_max_d(v);
     __syncthreads();
@@ -169,9 +181,10 @@ __device__ inline double block_max_d(double v, DScratch& s)
 }
 
 // ---------------------------------------------------------------------------
-// Phases
+// Edge algebra (pose z in the LDS layout: q at z[0..3], t at z[4..6], the
+// rotation matrix at z[7..15], fx fy cx cy at z[16..19])
 // ---------------------------------------------------------------------------
-__device__ inline void huber(double e2, double delta, double* rho0, double* rho1)
+__device__ __forceinline__ void huber(double e2, double delta, double* rho0, double* rho1)
 {
     const double dsqr = delta * delta;
     if (e2 <= dsqr) {
@@ -184,68 +197,37 @@ __device__ inline void huber(double e2, double delta, double* rho0, double* rho1
     }
 }
 
-__device__ inline double edge_chi2(const LbaDev& P, int a)
+// EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) with
+// cam_project (.cpp:422-428): e = obs - (fx X / Z + cx, fy Y / Z + cy)
+__device__ __forceinline__ void residual(const double* c, const double (&pc)[3], double ox, double oy, double& e0, double& e1)
 {
-    const int e = P.e_orig[a];
-    const double s = P.e_isig[a];
-    const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
-    return e0 * (s * e0) + e1 * (s * e1);
+    e0 = ox - (pc[0] / pc[2] * c[0] + c[2]);
+    e1 = oy - (pc[1] / pc[2] * c[1] + c[3]);
 }
 
-// EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) of
-// active edge a at the current pose / point, with the camera-frame point
-__device__ inline void edge_residual(const LbaDev& P, int a, double (&pc)[3], double& e0, double& e1)
+// EdgeSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:384-420) at
+// camera-frame point pc: A = d e / d point (2x3) with the pose's rotation R,
+// the reference's divisions by z and z^2 as products with 1/z (one division
+// per edge; the values differ from g2o's in rounding only).
+__device__ __forceinline__ void jac_point(const double* c, const double* R, const double (&pc)[3], double (&A)[6])
 {
-    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
-    const double* c = P.cam + 4 * P.e_pose[a];
-    const double u = pc[0] / pc[2] * c[0] + c[2];
-    const double v = pc[1] / pc[2] * c[1] + c[3];
-    e0 = P.e_obs[2 * a] - u;
-    e1 = P.e_obs[2 * a + 1] - v;
-}
-
-// computeActiveErrors + activeRobustChi2
-__device__ double compute_errors(LbaDev& P, DScratch& sc)
-{
-    double part = 0;
-    for (int a = threadIdx.x; a < P.nE; a += kLbaThreads) {
-        const int e = P.e_orig[a];
-        double pc[3];
-        edge_residual(P, a, pc, P.err[2 * e], P.err[2 * e + 1]);
-        double r0, r1;
-        huber(edge_chi2(P, a), P.huber_delta, &r0, &r1);
-        part += r0;
+    const double iz = 1. / pc[2];
+    const double fx = c[0], fy = c[1];
+    const double s = -iz;
+    const double t0 = s * fx, t2 = s * (-(pc[0] * iz) * fx), t4 = s * fy, t5 = s * (-(pc[1] * iz) * fy);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        A[j] = t0 * R[j] + t2 * R[6 + j];
+        A[3 + j] = t4 * R[3 + j] + t5 * R[6 + j];
     }
-    __syncthreads();
-    return block_sum_d(part, sc);
 }
 
-// EdgeSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:384-420) for
-// active edge a: A = d e / d point (2x3), B = d e / d pose (2x6); plus the
-// robust weight w = rho' * invSigma2 and the weighted error -Omega e rho'.
-struct EdgeLin {
-    double A[6], B[12], w, om0, om1;
-};
-
-// The Jacobians of linearizeOplus at camera-frame point pc: the
-// reference's divisions by z and z^2 as products with 1/z (one division per
-// edge; the values differ from g2o's in rounding only).
-__device__ inline void edge_jacobians(const LbaDev& P, int a, const double (&pc)[3], double (&A)[6], double (&B)[12])
+// B = d e / d pose (2x6), update order [omega(3), upsilon(3)]
+__device__ __forceinline__ void jac_pose(const double* c, const double (&pc)[3], double (&B)[12])
 {
-    const double* T = P.pose + 7 * P.e_pose[a];
     const double x = pc[0], y = pc[1];
     const double iz = 1. / pc[2], iz2 = iz * iz;
-    const double* c = P.cam + 4 * P.e_pose[a];
     const double fx = c[0], fy = c[1];
-    const double tmp[6] = {fx, 0, -(x * iz) * fx, 0, fy, -(y * iz) * fy};
-    double R[9];
-    qmat(Q{T[0], T[1], T[2], T[3]}, R);
-    const double s = -iz;
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-            A[i * 3 + j] = (s * tmp[i * 3]) * R[j] + (s * tmp[i * 3 + 1]) * R[3 + j] + (s * tmp[i * 3 + 2]) * R[6 + j];
     B[0] = x * y * iz2 * fx;
     B[1] = -(1 + (x * x * iz2)) * fx;
     B[2] = y * iz * fx;
@@ -260,128 +242,192 @@ __device__ inline void edge_jacobians(const LbaDev& P, int a, const double (&pc)
     B[11] = y * iz2 * fy;
 }
 
-// (pc: the camera-frame point, e0 / e1 the edge's error, both at the
-// linearisation point)
-__device__ inline void edge_linearize_at(const LbaDev& P, int a, const double (&pc)[3], double e0, double e1, EdgeLin& L)
+template <class Rec>
+__device__ __forceinline__ Rec load_rec(const LbaDev& P, int j)
 {
-    edge_jacobians(P, a, pc, L.A, L.B);
-    const double sg = P.e_isig[a];
-    double r0, r1;
-    huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
-    L.w = r1 * sg;
-    L.om0 = -(sg * e0) * r1;
-    L.om1 = -(sg * e1) * r1;
+    return reinterpret_cast<const Rec*>(P.rec)[j];
 }
 
-// linearizeOplus at the errors computeActiveErrors left in P.err
-__device__ inline void edge_linearize(const LbaDev& P, int a, EdgeLin& L)
+__device__ __forceinline__ void load_point(const double* p, double (&v)[3])
 {
-    double pc[3];
-    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
-    const int e = P.e_orig[a];
-    edge_linearize_at(P, a, pc, P.err[2 * e], P.err[2 * e + 1], L);
+    v[0] = p[0];
+    v[1] = p[1];
+    v[2] = p[2];
 }
 
-// Hpl = B^T W A (6x3, row-major) of active edge a, rebuilt at the current
-// pose / point with the weight linearize() stored: inside trial_solve these
-// are the iteration's linearisation point (a rejected trial is undone before
-// the next), so the blocks are the ones g2o's linearisation would store.
-__device__ inline void edge_hpl(const LbaDev& P, int a, double (&hpl)[18])
+__device__ __forceinline__ void map_point(const double* z, const double (&p)[3], double (&pc)[3])
 {
-    double pc[3];
-    se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * P.e_point[a], pc);
-    double A[6], B[12];
-    edge_jacobians(P, a, pc, A, B);
-    const double w = P.ew[a];   // the robust weight linearize() used
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        const double b0 = B[i] * w, b1 = B[6 + i] * w;
-#pragma unroll
-        for (int j = 0; j < 3; j++) hpl[i * 3 + j] = __fma_rn(b1, A[3 + j], b0 * A[j]);
+    se3_map(z, p, pc);   // SE3Quat::map: q p + t
+}
+
+// Errors of point l's edges at the current poses (LDS) and the point value
+// pt; writes P.err, returns the summed robust chi2 (computeActiveErrors +
+// activeRobustChi2 of these edges)
+template <class Rec>
+__device__ __forceinline__ double point_errors(LbaDev& P, const double* pz, int l, const double (&pt)[3])
+{
+    double part = 0;
+    for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
+        const Rec r = load_rec<Rec>(P, j);
+        const double* z = pz + kPz * r.pose;
+        double pc[3], e0, e1;
+        map_point(z, pt, pc);
+        residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+        const int e = P.e_orig[j];
+        P.err[2 * e] = e0;
+        P.err[2 * e + 1] = e1;
+        const double s = (double)r.isig;
+        double r0, r1;
+        huber(e0 * (s * e0) + e1 * (s * e1), P.huber_delta, &r0, &r1);
+        part += r0;
     }
+    return part;
 }
+
+// computeActiveErrors + activeRobustChi2 over every active point.  Points
+// in index order, a fixed share per thread: the double sum is the same on
+// every run (the count-sorted order of the Schur pass is not fixed within a
+// count).
+template <class Rec>
+__device__ __forceinline__ double compute_errors(LbaDev& P, const double* pz, DScratch& sc)
+{
+    double part = 0;
+    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+        double pt[3];
+        load_point(P.point + 3 * P.iv_point[l], pt);
+        part += point_errors<Rec>(P, pz, l, pt);
+    }
+    return block_sum_d(part, sc);
+}
+
+__device__ __forceinline__ int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
+__device__ __forceinline__ int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
+// packed lower triangle: element (i, j), j <= i
+__device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
 
 // constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
+//  - per point (one thread, its edges in edge order): Hll += A^T W A,
+//    bl += A^T (-Omega e); the robust weight W = rho' Omega kept per edge for
+//    the trial (ew)
 //  - per free pose (one wave, lanes stride the pose's edges in edge order,
-//    fixed butterfly reduction): Hpp += B^T W B, bp += B^T (-Omega e)
-//  - per point (one thread, its edges in order): Hll += A^T W A,
-//    bl += A^T (-Omega e).  The edges' Hpl = B^T W A blocks are not stored:
-//    the Schur pass and the back-substitution rebuild them (edge_hpl).
-__device__ void linearize(LbaDev& P)
+//    fixed butterfly reduction): Hpp += B^T W B, bp += B^T (-Omega e).
+// The errors are recomputed from the state (the values compute_errors left
+// in P.err, bit for bit).  Also the largest |Hpp| diagonal and |b| entry
+// (the fixed-point scales of the trials).
+template <class Rec>
+__device__ __forceinline__ void linearize(LbaDev& P, const double* pz, DScratch& sc)
 {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double hm = 0, bm = 0;
+    const int* order = P.ce;
+    for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
+        const int l = order[t];
+        double pt[3];
+        load_point(P.point + 3 * P.iv_point[l], pt);
+        double acc[9];
+#pragma unroll
+        for (int v = 0; v < 9; v++) acc[v] = 0.0;
+        for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
+            const Rec r = load_rec<Rec>(P, j);
+            const double* z = pz + kPz * r.pose;
+            double pc[3], e0, e1, A[6];
+            map_point(z, pt, pc);
+            residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+            jac_point(z + 16, z + 7, pc, A);
+            const double sg = (double)r.isig;
+            double r0, r1;
+            huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
+            const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
+            P.ew[j] = w;
+            int k = 0;
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int c = i; c < 3; c++) acc[k++] += (A[i] * w) * A[c] + (A[3 + i] * w) * A[3 + c];
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[6 + i] += A[i] * om0 + A[3 + i] * om1;
+        }
+#pragma unroll
+        for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
+        bm = fmax(bm, fmax(fabs(acc[6]), fmax(fabs(acc[7]), fabs(acc[8]))));
+    }
     for (int p = wv; p < P.nP; p += kLbaWaves) {
+        const double* z = pz + kPz * P.iv_pose[p];
         double acc[27];
 #pragma unroll
         for (int v = 0; v < 27; v++) acc[v] = 0.0;
         for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
-            EdgeLin L;
-            edge_linearize(P, P.pe_idx[q], L);
+            const int2 ent = P.pe_idx[q];
+            const Rec r = load_rec<Rec>(P, ent.x);
+            double pt[3];
+            load_point(P.point + 3 * ent.y, pt);
+            double pc[3], e0, e1, B[12];
+            map_point(z, pt, pc);
+            residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+            jac_pose(z + 16, pc, B);
+            const double sg = (double)r.isig;
+            double r0, r1;
+            huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
+            const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
             int k = 0;
 #pragma unroll
             for (int i = 0; i < 6; i++)
 #pragma unroll
-                for (int j = i; j < 6; j++) acc[k++] += (L.B[i] * L.w) * L.B[j] + (L.B[6 + i] * L.w) * L.B[6 + j];
+                for (int c = i; c < 6; c++) acc[k++] += (B[i] * w) * B[c] + (B[6 + i] * w) * B[6 + c];
 #pragma unroll
-            for (int i = 0; i < 6; i++) acc[21 + i] += L.B[i] * L.om0 + L.B[6 + i] * L.om1;
+            for (int i = 0; i < 6; i++) acc[21 + i] += B[i] * om0 + B[6 + i] * om1;
         }
 #pragma unroll
         for (int v = 0; v < 27; v++) {
             const double t = wave_sum_d(acc[v]);
             if (lane == 0) P.hp[27 * p + v] = t;
+            // diagonal of the packed upper 6x6 (row-major): 0, 6, 11, 15, 18, 20
+            if (v == 0 || v == 6 || v == 11 || v == 15 || v == 18 || v == 20) hm = fmax(hm, fabs(t));
+            else if (v >= 21) bm = fmax(bm, fabs(t));
         }
     }
-    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
-        double acc[9];
-#pragma unroll
-        for (int v = 0; v < 9; v++) acc[v] = 0.0;
-        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) {
-            const int a = P.le_idx[q];
-            EdgeLin L;
-            edge_linearize(P, a, L);
-            P.ew[a] = L.w;
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 3; i++)
-#pragma unroll
-                for (int j = i; j < 3; j++) acc[k++] += (L.A[i] * L.w) * L.A[j] + (L.A[3 + i] * L.w) * L.A[3 + j];
-#pragma unroll
-            for (int i = 0; i < 3; i++) acc[6 + i] += L.A[i] * L.om0 + L.A[3 + i] * L.om1;
-        }
-#pragma unroll
-        for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
+    hm = block_max_d(hm, sc);
+    bm = block_max_d(bm, sc);
+    if (threadIdx.x == 0) {
+        P.hmax = hm;
+        P.bmax = bm;
     }
     __syncthreads();
 }
 
-__device__ inline int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
-__device__ inline int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
-// packed lower triangle: element (i, j), j <= i
-__device__ inline int pk(int i, int j) { return i * (i + 1) / 2 + j; }
-
-// Fixed-point accumulation of the reduced camera system.  A contribution v
-// (|v| < 2^40) is split as v * 2^51 ~= hi * 2^40 + lo: hi = round(v * 2^11),
-// lo = round((v * 2^11 - hi) * 2^40), |lo| <= 2^39 (the split of a given v is
-// always the same; bits below 2^-51 are rounded off, far below the double
-// rounding of the entries, whose natural scale is >= 1 here), and both limbs
-// are added with 64-bit integer atomics.  Integer addition is associative,
-// so the accumulated limbs, and the double made from them, do not depend on
-// the order in which threads add: the reduced system is bitwise
-// reproducible.  lo sums stay exact for 2^23 contributions per entry; a
-// contribution with |v| >= 2^40 (or non-finite) flags the trial, which is
-// then rejected as CHOLMOD's failure would be.  Integerisation by the
+// Fixed-point accumulation of the reduced camera system.  Every value v is
+// first scaled by a power of two s chosen per problem and trial (exact), so
+// that the largest diagonal entry of Hpp + lambda I lands in [2^29, 2^30)
+// (and the largest |b| entry in [2^23, 2^24) for the right-hand side).  The
+// scaled value x = v s is split as x * 2^51 ~= hi * 2^40 + lo:
+// hi = round(x * 2^11), lo = round((x * 2^11 - hi) * 2^40), |lo| <= 2^39 (the
+// split of a given x is always the same; bits below 2^-51 of x, i.e. 2^-80 of
+// the largest diagonal, are rounded off, far below the double rounding of
+// the entries), and both limbs are added with 64-bit integer atomics.
+// Integer addition is associative, so the accumulated limbs, and the double
+// made from them, do not depend on the order in which threads add: the
+// reduced system is bitwise reproducible.  Every Schur contribution
+// (W_i Dinv W_j^T)_rc is bounded by sqrt(S_rr S_cc) <= the largest diagonal
+// of Hpp + lambda I (a point's block [Hpp_l W; W^T Hll] is positive
+// semi-definite), so the scaled contributions stay below 2^30 whatever the
+// camera model or information weights (pixels, normalised coordinates,
+// huge or tiny weights: tests/test_lba_gpu.py).  The limb sums stay exact for
+// 2^22 contributions per entry (the host refuses problems with more points);
+// a contribution with |x| >= 2^40 (possible only for b, whose bound involves
+// 1/lambda) makes the trial retry at a 2^-24 smaller scale, and a non-finite
+// one rejects the trial, as CHOLMOD's failure would.  Integerisation by the
 // 1.5 * 2^52 magic-number addition (exact round-to-nearest for |x| < 2^51).
 constexpr double kFxHi = 2048.0;                           // 2^11
 constexpr double kFxLo = 1099511627776.0;                  // 2^40
 constexpr double kFxInvHi = 1.0 / 2048.0;                  // 2^-11
 constexpr double kFxInvLo = 1.0 / 2251799813685248.0;      // 2^-51
-constexpr double kFxMax = 2251799813685248.0;              // 2^51 (of v * 2^11)
+constexpr double kFxMax = 2251799813685248.0;              // 2^51 (of x * 2^11)
 constexpr double kFxMagic = 6755399441055744.0;            // 1.5 * 2^52
 
 typedef unsigned long long fx_t;
 
-// (t = v * 2^11, already scaled)
-__device__ inline void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
+// (t = x * 2^11, already scaled)
+__device__ __forceinline__ void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
 {
     bad |= !(fabs(t) < kFxMax);
     const double th = t + kFxMagic;                 // round(t) in the low mantissa bits
@@ -392,17 +438,12 @@ __device__ inline void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
     lo = (fx_t)(__double_as_longlong(tl) - m);
 }
 
-__device__ inline void fx_split(double v, fx_t& hi, fx_t& lo, int& bad)
-{
-    fx_split_scaled(v * kFxHi, hi, lo, bad);   // the scaling is exact
-}
-
 // 64-bit integer atomic add into the reduced system, with the address space
 // explicit (LDS, or global for the kLds = false fallback): on a generic
 // pointer the compiler tests the address space at run time, and that test
 // has tripped its instruction selection here
 template <bool kLds>
-__device__ inline void fx_atomic(fx_t* p, fx_t v)
+__device__ __forceinline__ void fx_atomic(fx_t* p, fx_t v)
 {
     if constexpr (kLds) {
         atomicAdd(p, v);
@@ -413,7 +454,7 @@ __device__ inline void fx_atomic(fx_t* p, fx_t v)
 }
 
 template <bool kLds>
-__device__ inline void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int& bad)
+__device__ __forceinline__ void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int& bad)
 {
     fx_t h, l;
     fx_split_scaled(t, h, l, bad);
@@ -421,18 +462,7 @@ __device__ inline void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int&
     fx_atomic<kLds>(lo + idx, l);
 }
 
-template <bool kLds>
-__device__ inline void fx_add(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
-{
-    fx_add_scaled<kLds>(hi, lo, idx, v * kFxHi, bad);   // the scaling is exact
-}
-
-__device__ inline void fx_set(fx_t* hi, fx_t* lo, int idx, double v, int& bad)
-{
-    fx_split(v, hi[idx], lo[idx], bad);
-}
-
-__device__ inline double fx_value(fx_t hi, fx_t lo)
+__device__ __forceinline__ double fx_value(fx_t hi, fx_t lo)
 {
     return (double)(long long)hi * kFxInvHi + (double)(long long)lo * kFxInvLo;
 }
@@ -443,163 +473,209 @@ __device__ inline double fx_value(fx_t hi, fx_t lo)
 // bhi[] the right-hand side.
 __host__ __device__ constexpr long long lba_sys_doubles(long long n) { return n * (n + 1) + 2 * n; }
 
-// One Levenberg trial: Schur complement, LLT, back-substitution, update.
-// Returns false when the reduced system is not positive definite.
-// per-thread edge table of the Schur pass (one allocation for both
-// instantiations below)
-__shared__ int2 s_edges[kLbaThreads][kSchurEdges];
+// Dinv = (Hll + lambda I)^-1 of a point (Eigen's 3x3 cofactor inverse:
+// d[i*3+j] = cof(j, i) / det)
+__device__ __forceinline__ void point_dinv(const double* h, double lambda, double (&d)[9])
+{
+    double m[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) m[i * 3 + j] = h[i <= j ? up3(i, j) : up3(j, i)] + (i == j ? lambda : 0.0);
+    const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
+    const double c01 = m[5] * m[6] - m[3] * m[8], c11 = m[8] * m[0] - m[6] * m[2], c21 = m[2] * m[3] - m[0] * m[5];
+    const double c02 = m[3] * m[7] - m[4] * m[6], c12 = m[6] * m[1] - m[7] * m[0], c22 = m[0] * m[4] - m[1] * m[3];
+    const double det = c00 * m[0] + c10 * m[3] + c20 * m[6];
+    const double inv = 1.0 / det;
+    d[0] = c00 * inv; d[1] = c10 * inv; d[2] = c20 * inv;
+    d[3] = c01 * inv; d[4] = c11 * inv; d[5] = c21 * inv;
+    d[6] = c02 * inv; d[7] = c12 * inv; d[8] = c22 * inv;
+}
 
+// One point's Schur contributions (thread per point, its edges contiguous):
+// D = Hll + lambda I, Dinv, db = Dinv bl; for each free-pose edge u:
+// bs -= W_u db and, for every later edge v of the point (and v = u),
+// S(p_u, p_v) -= W_u Dinv W_v^T as fixed-point limbs.  With W = (w B)^T A
+// the 6x6 block is (w B_u)^T G (w B_v), G = (A_u Dinv) A_v^T 2x2: W is never
+// formed.  Register budget (128 VGPRs at 1024 threads): Dinv and db are
+// re-read from dl per edge u, and only A_u Dinv and w B_u stay live across
+// the loop over v.
+template <bool kLds>
+__device__ __forceinline__ void schur_block(const double (&AD)[6], const double (&wBu)[12], const double (&Av)[6],
+                                   const double (&wBv)[12], int pu, int pv, bool diag, double kS, fx_t* hi, fx_t* lo,
+                                   int& bad)
+{
+    // G = AD Av^T (2x2); Q = -kS (w B_u)^T G (6x2): element (r, c) of the
+    // block is Q[r] . (w B_v)[:, c]
+    double G[4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+            G[2 * a + b] = __fma_rn(AD[3 * a + 2], Av[3 * b + 2], __fma_rn(AD[3 * a + 1], Av[3 * b + 1], AD[3 * a] * Av[3 * b]));
+    double Q0[6], Q1[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        Q0[r] = -kS * __fma_rn(wBu[6 + r], G[2], wBu[r] * G[0]);
+        Q1[r] = -kS * __fma_rn(wBu[6 + r], G[3], wBu[r] * G[1]);
+    }
+    // element (r, c) belongs at S(6 pu + r, 6 pv + c): stored at the packed
+    // lower index of that position or of its mirror
+    const bool upper = pu < pv;
+    const int ihi = upper ? pv : pu, ilo = upper ? pu : pv;
+    const int base = pk(6 * ihi, 0) + 6 * ilo;
+    if (pu != pv) {
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                const double t = __fma_rn(Q1[r], wBv[6 + c], Q0[r] * wBv[c]);
+                const int rr = upper ? c : r, cc = upper ? r : c;
+                fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * rr + rr * (rr + 1) / 2 + cc, t, bad);
+            }
+    } else {
+        // one edge (diag): the lower triangle of its own block; two edges of
+        // one point on the same pose (not made by LocalBundleAdjustment,
+        // handled for completeness): the block plus its transpose
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c <= r; c++) {
+                double t = __fma_rn(Q1[r], wBv[6 + c], Q0[r] * wBv[c]);
+                if (!diag) t += __fma_rn(Q1[c], wBv[6 + r], Q0[c] * wBv[r]);
+                fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * r + r * (r + 1) / 2 + c, t, bad);
+            }
+    }
+}
+
+// the edge's A (2x3) and w B (2x6) at point pt (pose z in LDS)
+__device__ __forceinline__ void edge_aw(const LbaDev& P, const double* z, int j, const double (&pt)[3], double (&A)[6],
+                               double (&wB)[12])
+{
+    double pc[3], B[12];
+    map_point(z, pt, pc);
+    jac_point(z + 16, z + 7, pc, A);
+    jac_pose(z + 16, pc, B);
+    const double w = P.ew[j];
+#pragma unroll
+    for (int i = 0; i < 12; i++) wB[i] = B[i] * w;
+}
+
+template <class Rec, bool kLds>
+__device__ __forceinline__ void schur_point(LbaDev& P, const double* pz, int l, double lambda, double kS, double kB, fx_t* hi,
+                                   fx_t* lo, fx_t* bhi, fx_t* blo, int& bad)
+{
+    double* dlo = P.dl + 12 * l;
+    {
+        const double* h = P.hl + 9 * l;
+        double d[9];
+        point_dinv(h, lambda, d);
+#pragma unroll
+        for (int i = 0; i < 9; i++) dlo[i] = d[i];
+        dlo[9] = d[0] * h[6] + d[1] * h[7] + d[2] * h[8];
+        dlo[10] = d[3] * h[6] + d[4] * h[7] + d[5] * h[8];
+        dlo[11] = d[6] * h[6] + d[7] * h[7] + d[8] * h[8];
+    }
+    double pt[3];
+    load_point(P.point + 3 * P.iv_point[l], pt);
+    const int j0 = P.le_ptr[l], j1 = P.le_ptr[l + 1];
+    for (int ju = j0; ju < j1; ju++) {
+        const Rec ru = load_rec<Rec>(P, ju);
+        if (ru.ph < 0) continue;
+        const int pu = ru.ph;
+        double AD[6], wBu[12];
+        {
+            double Au[6];
+            edge_aw(P, pz + kPz * ru.pose, ju, pt, Au, wBu);
+            // AD = A_u Dinv (2x3); bs -= W_u db = (w B_u)^T (A_u db)
+            const double* d = dlo;
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    AD[3 * a + k] = __fma_rn(Au[3 * a + 2], d[6 + k], __fma_rn(Au[3 * a + 1], d[3 + k], Au[3 * a] * d[k]));
+            const double adb0 = __fma_rn(Au[2], d[11], __fma_rn(Au[1], d[10], Au[0] * d[9]));
+            const double adb1 = __fma_rn(Au[5], d[11], __fma_rn(Au[4], d[10], Au[3] * d[9]));
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+                fx_add_scaled<kLds>(bhi, blo, 6 * pu + r, -__fma_rn(wBu[6 + r], adb1, wBu[r] * adb0) * kB, bad);
+            schur_block<kLds>(AD, wBu, Au, wBu, pu, pu, true, kS, hi, lo, bad);   // v = u
+        }
+        for (int jv = ju + 1; jv < j1; jv++) {
+            const Rec rv = load_rec<Rec>(P, jv);
+            if (rv.ph < 0) continue;
+            double Av[6], wBv[12];
+            edge_aw(P, pz + kPz * rv.pose, jv, pt, Av, wBv);
+            schur_block<kLds>(AD, wBu, Av, wBv, pu, rv.ph, false, kS, hi, lo, bad);
+        }
+    }
+}
+
+// One Levenberg trial's linear algebra: Schur complement, LLT, the pose
+// solve into xp (LDS).  Returns false when the reduced system is not
+// positive definite (or its accumulation not finite).
 // kLds: the reduced system lives in the dynamic LDS block (its accesses then
 // compile to ds_* instructions instead of flat ones), else in P.S.
-template <bool kLds>
-__device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
+template <class Rec, bool kLds>
+__device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double* pz, double* xp, double lambda)
 {
-    extern __shared__ __attribute__((aligned(16))) double s_S[];
     __shared__ int s_bad;
     LBA_T0();
     const int n = P.dim_p;
     const int M = n * (n + 1) / 2;
-    fx_t* hi = reinterpret_cast<fx_t*>(kLds ? s_S : P.S);
+    fx_t* hi = reinterpret_cast<fx_t*>(kLds ? lds : P.S);
     fx_t* lo = hi + M;
     fx_t* bhi = lo + M;
     fx_t* blo = bhi + n;
     double* S = reinterpret_cast<double*>(hi);     // packed lower triangle, after conversion
     double* bs = reinterpret_cast<double*>(bhi);
-    int bad = 0;
-    // the diagonal blocks Hpp + lambda I, zero elsewhere; bs <- bp
-    for (int k = threadIdx.x; k < M; k += kLbaThreads) {
-        hi[k] = 0;
-        lo[k] = 0;
-    }
-    if (threadIdx.x == 0) s_bad = 0;
-    __syncthreads();
-    for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
-        const int p = item / 21, u = item - p * 21;
-        int r = 0;
-        while (up6(r, 5) < u) r++;
-        const int c = r + (u - up6(r, r));   // upper element (r, c), c >= r
-        fx_set(hi, lo, pk(6 * p + c, 6 * p + r), P.hp[27 * p + u] + (r == c ? lambda : 0.0), bad);
-    }
-    for (int i = threadIdx.x; i < n; i += kLbaThreads) fx_set(bhi, blo, i, P.hp[27 * (i / 6) + 21 + (i % 6)], bad);
-    __syncthreads();
-    LBA_MARK(1);
-    // Schur complement, point by point (one thread per point, its edges are
-    // contiguous): D = Hll + lambda I, Dinv (Eigen 3x3 cofactor inverse),
-    // db; then bs -= W_i db and S(i, j) -= (W_i Dinv) W_j^T for every pair of
-    // the point's free-pose edges (upper blocks; diagonal blocks upper
-    // triangle), as fixed-point limbs.  Points are taken in the order of
-    // their edge counts (P.ce, point_order): the lanes of a wave run loops of
-    // similar length and every thread gets a similar share; with
-    // order-independent sums this changes no bit of the result.
-    const int* order = reinterpret_cast<const int*>(P.ce);
-#ifdef ORBX_DIAG_SCHUR
-    double diag_sink = 0;
-#endif
-    for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
-        const int l = order[t];
-        const double* h = P.hl + 9 * l;
-        double m[9];
-#pragma unroll
-        for (int i = 0; i < 3; i++)
-#pragma unroll
-            for (int j = 0; j < 3; j++) m[i * 3 + j] = h[i <= j ? up3(i, j) : up3(j, i)] + (i == j ? lambda : 0.0);
-        double d[12];
-        {
-            const double c00 = m[4] * m[8] - m[5] * m[7], c10 = m[7] * m[2] - m[8] * m[1], c20 = m[1] * m[5] - m[2] * m[4];
-            const double c01 = m[5] * m[6] - m[3] * m[8], c11 = m[8] * m[0] - m[6] * m[2], c21 = m[2] * m[3] - m[0] * m[5];
-            const double c02 = m[3] * m[7] - m[4] * m[6], c12 = m[6] * m[1] - m[7] * m[0], c22 = m[0] * m[4] - m[1] * m[3];
-            const double det = c00 * m[0] + c10 * m[3] + c20 * m[6];
-            const double inv = 1.0 / det;
-            d[0] = c00 * inv; d[1] = c10 * inv; d[2] = c20 * inv;   // d[i*3+j] = cof(j, i) / det
-            d[3] = c01 * inv; d[4] = c11 * inv; d[5] = c21 * inv;
-            d[6] = c02 * inv; d[7] = c12 * inv; d[8] = c22 * inv;
+    // the power-of-two scales of the fixed point (see fx_split_scaled):
+    // largest diagonal of Hpp + lambda I into [2^29, 2^30), largest |b| into
+    // [2^23, 2^24); exact, and the same on every thread
+    const double hmax = P.hmax + lambda, bmax = P.bmax;
+    double sS = (hmax > 0 && isfinite(hmax)) ? ldexp(1.0, 29 - ilogb(hmax)) : 1.0;
+    double sB = (bmax > 0 && isfinite(bmax)) ? ldexp(1.0, 23 - ilogb(bmax)) : 1.0;
+    const int* order = P.ce;
+    for (int attempt = 0;; attempt++) {
+        const double kS = sS * kFxHi, kB = sB * kFxHi;   // value -> fixed-point scale (x 2^11)
+        int bad = 0;
+        // the diagonal blocks Hpp + lambda I, zero elsewhere; bs <- bp
+        for (int k = threadIdx.x; k < M; k += kLbaThreads) {
+            hi[k] = 0;
+            lo[k] = 0;
         }
-        const double* bl = h + 6;
-#pragma unroll
-        for (int i = 0; i < 3; i++) d[9 + i] = d[3 * i] * bl[0] + d[3 * i + 1] * bl[1] + d[3 * i + 2] * bl[2];
-        double* dl = P.dl + 12 * l;
-#pragma unroll
-        for (int i = 0; i < 12; i++) dl[i] = d[i];
-        const int q0 = P.lc_ptr[l], q1 = P.lc_ptr[l + 1], k = q1 - q0;
-        // the point's free-pose edges (edge, pose block) in this thread's LDS
-        // row; points with more than kSchurEdges such edges read the lists
-        // from global memory
-        int2* te = s_edges[threadIdx.x];
-        const bool tab = k <= kSchurEdges;
-        if (tab)
-            for (int j = 0; j < k; j++) {
-                const int a = P.lc_idx[q0 + j];
-                te[j] = make_int2(a, P.e_ph[a]);
-            }
-        auto edge_at = [&](int j) { return tab ? te[j] : make_int2(P.lc_idx[q0 + j], P.e_ph[P.lc_idx[q0 + j]]); };
-        // The point's edges in groups of kSchurGroup: the group's W_i Dinv
-        // blocks stay in registers while every later edge's W_j is rebuilt
-        // once for the whole group (k + ~k^2 / (2 G) rebuilds per point).
-        constexpr int G = kSchurGroup;
-        // S(i1, i2) -= (W_i Dinv) W_j^T over the 6x6 block (upper triangle of
-        // a diagonal block), stored as the lower element (6 i2 + c, 6 i1 + r)
-        // (w = -2^11 W_i Dinv: the element's contribution already negated and
-        // in fixed-point scale; fused multiply-adds)
-        auto pair_update = [&](const double (&w)[18], int i1, const double (&bj)[18], int i2) {
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int c = 0; c < 6; c++) {
-                    if (i1 == i2 && c < r) continue;
-                    const double t =
-                        __fma_rn(w[r * 3 + 2], bj[c * 3 + 2], __fma_rn(w[r * 3 + 1], bj[c * 3 + 1], w[r * 3] * bj[c * 3]));
-#if defined(ORBX_DIAG_SCHUR) && ORBX_DIAG_SCHUR == 1   // timing diagnostics only (wrong results)
-                    diag_sink += t;
-#elif defined(ORBX_DIAG_SCHUR) && ORBX_DIAG_SCHUR == 2
-                    if (r == 0 && c == 0) diag_sink += t;
-#else
-                    fx_add_scaled<kLds>(hi, lo, pk(6 * i2 + c, 6 * i1 + r), t, bad);
-#endif
-                }
-        };
-        for (int g = 0; g < k; g += G) {
-            double wd[G][18];   // W_i Dinv (6x3) of the group's edges
-            int pi[G];
-            double cur[18];
-            // the group's own W blocks: W_i Dinv, bs, and the pairs among the
-            // group's edges
-#pragma unroll
-            for (int u = 0; u < G; u++) {
-                pi[u] = -1;
-                if (g + u < k) {
-                    const int2 ei = edge_at(g + u);
-                    pi[u] = ei.y;
-                    edge_hpl(P, ei.x, cur);
-#pragma unroll
-                    for (int r = 0; r < 6; r++) {
-                        const double b0 = cur[3 * r], b1 = cur[3 * r + 1], b2 = cur[3 * r + 2];
-#pragma unroll
-                        for (int c = 0; c < 3; c++)
-                            wd[u][r * 3 + c] = -kFxHi * __fma_rn(b2, d[6 + c], __fma_rn(b1, d[3 + c], b0 * d[c]));
-                        fx_add<kLds>(bhi, blo, 6 * ei.y + r, -(b0 * d[9] + b1 * d[10] + b2 * d[11]), bad);
-                    }
-#pragma unroll
-                    for (int v = 0; v <= u; v++) pair_update(wd[v], pi[v], cur, ei.y);
-                }
-            }
-            // every later edge's W_j, rebuilt once for the whole group
-            for (int qj = g + G; qj < k; qj++) {
-                const int2 ej = edge_at(qj);
-                edge_hpl(P, ej.x, cur);
-#pragma unroll
-                for (int u = 0; u < G; u++) pair_update(wd[u], pi[u], cur, ej.y);
-            }
+        if (threadIdx.x == 0) s_bad = 0;
+        __syncthreads();
+        for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
+            const int p = item / 21, u = item - p * 21;
+            int r = 0;
+            while (up6(r, 5) < u) r++;
+            const int c = r + (u - up6(r, r));   // upper element (r, c), c >= r
+            const int idx = pk(6 * p + c, 6 * p + r);
+            fx_split_scaled((P.hp[27 * p + u] + (r == c ? lambda : 0.0)) * kS, hi[idx], lo[idx], bad);
         }
+        for (int i = threadIdx.x; i < n; i += kLbaThreads)
+            fx_split_scaled(P.hp[27 * (i / 6) + 21 + (i % 6)] * kB, bhi[i], blo[i], bad);
+        __syncthreads();
+        LBA_MARK(1);
+        // points in the order of their edge counts: the lanes of a wave run
+        // loops of similar length; with order-independent sums this changes
+        // no bit of the result
+        for (int t = threadIdx.x; t < P.nL; t += kLbaThreads)
+            schur_point<Rec, kLds>(P, pz, order[t], lambda, kS, kB, hi, lo, bhi, blo, bad);
+        if (bad) s_bad = 1;
+        __syncthreads();
+        if (!s_bad) break;                  // uniform
+        if (attempt == 1) return false;     // still out of range (or non-finite): rejected
+        sS *= 0x1p-24;                      // a contribution reached 2^40: once more at a smaller scale
+        sB *= 0x1p-24;
+        __syncthreads();                    // every thread has read s_bad before it is reset
     }
-#ifdef ORBX_DIAG_SCHUR
-    if (diag_sink == 1.2345) bad = 1;
-#endif
-    if (bad) s_bad = 1;
-    __syncthreads();
-    if (s_bad) return false;   // uniform
-    // limbs -> doubles in place (element k's double overwrites its own hi)
-    for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(hi[k], lo[k]);
-    for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]);
+    // limbs -> doubles in place (element k's double overwrites its own hi),
+    // scaled back (exact)
+    const double iS = 1.0 / sS, iB = 1.0 / sB;
+    for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(hi[k], lo[k]) * iS;
+    for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]) * iB;
     __syncthreads();
     LBA_MARK(2);
     // dense LLT on the packed lower triangle, right-looking in 6x6 blocks
@@ -671,7 +747,6 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     // forward / backward substitution by one wave, in 6-row blocks: the
     // block's triangle on lanes 0..5 with shuffles, then the other rows
     // updated with the block's six values; one wave barrier per block
-    double* xp = P.x;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         for (int i = lane; i < n; i += 64) xp[i] = bs[i];
@@ -721,42 +796,18 @@ __device__ bool trial_solve(LbaDev& P, double lambda, DScratch& sc)
     }
     __syncthreads();
     LBA_MARK(4);
-    // landmarks: xl = Dinv (bl - sum_i B_i^T xp_i), the W_i rebuilt
-    for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
-        const int l = order[t];
-        const double* h = P.hl + 9 * l;
-        double cl[3] = {h[6], h[7], h[8]};
-        for (int q = P.lc_ptr[l]; q < P.lc_ptr[l + 1]; q++) {
-            const int a = P.lc_idx[q];
-            const int i1 = P.e_ph[a];
-            double w[18];
-            edge_hpl(P, a, w);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                double acc = 0;
-#pragma unroll
-                for (int r = 0; r < 6; r++) acc += w[r * 3 + c] * (-xp[6 * i1 + r]);
-                cl[c] += acc;
-            }
-        }
-        const double* d = P.dl + 12 * l;
-        for (int i = 0; i < 3; i++) P.x[n + 3 * l + i] = d[3 * i] * cl[0] + d[3 * i + 1] * cl[1] + d[3 * i + 2] * cl[2];
-    }
-    __syncthreads();
-    LBA_MARK(5);
     return true;
 }
 
-// The points of a pass by decreasing count of free-pose edges (counting
-// sort; the order within a count is arbitrary and does not matter) into
-// P.ce, which is free scratch once the pass's structure is built.
-__device__ void point_order(LbaDev& P)
+// The points of a pass by decreasing count of edges (counting sort; the
+// order within a count is arbitrary and does not matter) into P.ce.
+__device__ __forceinline__ void point_order(LbaDev& P)
 {
     __shared__ int hist[64], off[64];
-    int* order = reinterpret_cast<int*>(P.ce);
+    int* order = P.ce;
     for (int b = threadIdx.x; b < 64; b += kLbaThreads) hist[b] = 0;
     __syncthreads();
-    auto bucket = [&](int l) { return 63 - min(P.lc_ptr[l + 1] - P.lc_ptr[l], 63); };
+    auto bucket = [&](int l) { return 63 - min(P.le_ptr[l + 1] - P.le_ptr[l], 63); };
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) atomicAdd(&hist[bucket(l)], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -771,9 +822,56 @@ __device__ void point_order(LbaDev& P)
     __syncthreads();
 }
 
-// OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
-__global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int lds_S_cap)
+// rotation matrix of pose z (q at z[0..3]) into z[7..15] (Eigen's
+// toRotationMatrix, the R of linearizeOplus)
+__device__ __forceinline__ void pz_rot(double* z) { qmat(Q{z[0], z[1], z[2], z[3]}, z + 7); }
+
+// Back-substitution of point l with the W_i of the linearisation state (the
+// saved poses pbk, the point before its update pt): xl = Dinv (bl - sum_i
+// W_i^T xp_i) (block_solver.hpp:461-486)
+template <class Rec>
+__device__ __forceinline__ void point_backsub(const LbaDev& P, const double* pz, const double* pbk, const double* xp, int l,
+                                     const double (&pt)[3], double (&xl)[3])
 {
+    const double* h = P.hl + 9 * l;
+    double cl[3] = {h[6], h[7], h[8]};
+    for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
+        const Rec r = load_rec<Rec>(P, j);
+        if (r.ph < 0) continue;
+        const double* zo = pbk + kPbk * r.ph;          // the pose (and rotation) before the update
+        const double* cam = pz + kPz * r.pose + 16;
+        double pc[3], A[6], B[12];
+        map_point(zo, pt, pc);
+        jac_point(cam, zo + 7, pc, A);
+        jac_pose(cam, pc, B);
+        const double w = P.ew[j];
+        const double* x6 = xp + 6 * r.ph;
+        double bx0 = 0, bx1 = 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            bx0 += B[k] * x6[k];
+            bx1 += B[6 + k] * x6[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) cl[k] -= w * (A[k] * bx0 + A[3 + k] * bx1);
+    }
+    const double* d = P.dl + 12 * l;
+#pragma unroll
+    for (int i = 0; i < 3; i++) xl[i] = d[3 * i] * cl[0] + d[3 * i + 1] * cl[1] + d[3 * i + 2] * cl[2];
+}
+
+// Dynamic LDS layout of k_lba_iteration (doubles): [S region][poses][pose
+// backups][xp]; the S region is empty when the batch's systems live in
+// global memory.
+struct LbaLds {
+    int s_doubles, pz_off, pbk_off, xp_off;
+};
+
+// OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
+template <class Rec>
+__global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, LbaLds lay)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ DScratch sc;
     LbaDev& P = probs[blockIdx.x];
     if (P.status != kRunning || P.abort) return;
@@ -782,14 +880,28 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         return;
     }
     const int n = P.dim_p;
-    const bool in_lds = lba_sys_doubles(n) <= lds_S_cap;
+    const bool in_lds = lba_sys_doubles(n) <= lay.s_doubles;
+    double* pz = lds + lay.pz_off;
+    double* pbk = lds + lay.pbk_off;
+    double* xp = lds + lay.xp_off;
+    // the problem's poses and cameras into LDS, rotation matrices beside them
+    for (int i = threadIdx.x; i < P.nposes_all * 11; i += kLbaThreads) {
+        const int p = i / 11, k = i - 11 * p;
+        pz[kPz * p + (k < 7 ? k : 9 + k)] = k < 7 ? P.pose[7 * p + k] : P.cam[4 * p + (k - 7)];
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P.nposes_all; p += kLbaThreads) pz_rot(pz + kPz * p);
     if (iteration == 0) point_order(P);
+    __syncthreads();
     LBA_T0();
-    double currentChi = compute_errors(P, sc);
+    // computeActiveErrors at the start of the iteration: after the first
+    // iteration the state is the previous iteration's accepted trial state,
+    // whose errors (P.err) and robust chi2 that trial computed, bit for bit
+    double currentChi = iteration == 0 ? compute_errors<Rec>(P, pz, sc) : P.current_chi;
     const double iniChi = currentChi;
     if (iteration == 0 && threadIdx.x == 0) P.chi2_initial = currentChi;
     LBA_MARK(6);
-    linearize(P);
+    linearize<Rec>(P, pz, sc);
     LBA_MARK(7);
     double lambda = P.lambda, ni = P.ni;
     if (iteration == 0) {
@@ -803,37 +915,63 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         ni = 2;
         if (threadIdx.x == 0) P.nBad = 0;
     }
-    const int nx = n + 3 * P.nL;
     double rho = 0;
     int qmax = 0;
     do {
-        // push
-        for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose_bk[i] = P.pose[i];
-        for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point_bk[i] = P.point[i];
-        __syncthreads();
-        const bool ok2 = in_lds ? trial_solve<true>(P, lambda, sc) : trial_solve<false>(P, lambda, sc);
-        if (ok2) {
-            for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) se3_oplus(P.pose + 7 * P.iv_pose[p], P.x + 6 * p);
-            for (int item = threadIdx.x; item < P.nL * 3; item += kLbaThreads) {
-                const int l = item / 3, i = item - l * 3;
-                P.point[3 * P.iv_point[l] + i] += P.x[n + item];
-            }
-        } else {
-            for (int i = threadIdx.x; i < nx; i += kLbaThreads) P.x[i] = 0.0;
-            if (threadIdx.x == 0) P.not_posdef++;
+        // push: the free poses (with their rotation matrices) into LDS; the
+        // points are saved by the update pass below
+        for (int i = threadIdx.x; i < P.nP * kPbk; i += kLbaThreads) {
+            const int p = i / kPbk, k = i - kPbk * p;
+            pbk[i] = pz[kPz * P.iv_pose[p] + k];
         }
+        __syncthreads();
+        const bool ok2 = in_lds ? trial_solve<Rec, true>(P, lds, pz, xp, lambda)
+                                : trial_solve<Rec, false>(P, lds, pz, xp, lambda);
+        if (ok2)
+            for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) {
+                double* z = pz + kPz * P.iv_pose[p];
+                se3_oplus(z, xp + 6 * p);
+                pz_rot(z);
+            }
         __syncthreads();
         LBA_T0();
-        double tempChi = compute_errors(P, sc);
-        LBA_MARK(8);
-        if (!ok2) tempChi = 1.79769313486231570815e+308;
-        // computeScale: sum_j x_j (lambda x_j + b_j)
-        double part = 0;
-        for (int j = threadIdx.x; j < nx; j += kLbaThreads) {
-            const double bj = j < n ? P.hp[27 * (j / 6) + 21 + (j % 6)] : P.hl[9 * ((j - n) / 3) + 6 + ((j - n) % 3)];
-            part += P.x[j] * (lambda * P.x[j] + bj);
+        // per point: back-substitution, the update (VertexSBAPointXYZ::
+        // oplusImpl) and the errors of its edges at the new state;
+        // computeScale's sum_j x_j (lambda x_j + b_j) beside it.  A failed
+        // solve leaves the state as it was (x = 0) and only evaluates the
+        // errors.
+        // (points in index order: a fixed share per thread, so the double
+        // sums are the same on every run)
+        double chi_part = 0, scale_part = 0;
+        for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+            double* pw = P.point + 3 * P.iv_point[l];
+            double pt[3];
+            load_point(pw, pt);
+            if (ok2) {
+                double xl[3];
+                point_backsub<Rec>(P, pz, pbk, xp, l, pt, xl);
+                const double* h = P.hl + 9 * l;
+                double* bk = P.point_bk + 3 * l;
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    bk[i] = pt[i];
+                    scale_part += xl[i] * (lambda * xl[i] + h[6 + i]);
+                    pt[i] += xl[i];
+                    pw[i] = pt[i];
+                }
+            }
+            chi_part += point_errors<Rec>(P, pz, l, pt);
         }
-        double scale = block_sum_d(part, sc);
+        if (ok2)
+            for (int j = threadIdx.x; j < n; j += kLbaThreads)
+                scale_part += xp[j] * (lambda * xp[j] + P.hp[27 * (j / 6) + 21 + (j % 6)]);
+        double tempChi = block_sum_d(chi_part, sc);
+        LBA_MARK(8);
+        if (!ok2) {
+            tempChi = 1.79769313486231570815e+308;
+            if (threadIdx.x == 0) P.not_posdef++;
+        }
+        double scale = block_sum_d(scale_part, sc);
         scale += 1e-3;
         rho = (currentChi - tempChi) / scale;
         const bool accept = rho > 0 && isfinite(tempChi);
@@ -846,18 +984,33 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         } else {
             lambda *= ni;
             ni *= 2;
-            for (int i = threadIdx.x; i < P.nposes_all * 7; i += kLbaThreads) P.pose[i] = P.pose_bk[i];
-            for (int i = threadIdx.x; i < P.npoints_all * 3; i += kLbaThreads) P.point[i] = P.point_bk[i];
+            if (ok2) {   // pop: the saved poses and points
+                for (int i = threadIdx.x; i < P.nP * kPbk; i += kLbaThreads) {
+                    const int p = i / kPbk, k = i - kPbk * p;
+                    pz[kPz * P.iv_pose[p] + k] = pbk[i];
+                }
+                for (int i = threadIdx.x; i < P.nL * 3; i += kLbaThreads) {
+                    const int l = i / 3, k = i - 3 * l;
+                    P.point[3 * P.iv_point[l] + k] = P.point_bk[i];
+                }
+            }
         }
         __syncthreads();
         qmax++;
     } while (rho < 0 && qmax < 10 && !P.abort);
+    // the free poses back to global memory (the next launch and the outlier
+    // pass read them there)
+    for (int i = threadIdx.x; i < P.nP * 7; i += kLbaThreads) {
+        const int p = i / 7, k = i - 7 * p;
+        P.pose[7 * P.iv_pose[p] + k] = pz[kPz * P.iv_pose[p] + k];
+    }
     if (threadIdx.x == 0) {
         P.lambda = lambda;
         P.ni = ni;
         P.trials += qmax;
         P.iterations++;
         P.last_chi = currentChi;
+        P.current_chi = currentChi;
         int status = kRunning;
         if (qmax == 10 || rho == 0) {
             status = kTerminated;
@@ -874,7 +1027,9 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
 // :497-515).  The reference walks the edges in order; an edge's outcome
 // depends only on earlier edges of the same map point (EraseObservation ->
 // SetBadFlag), so each point's active edges are walked in edge order by one
-// thread, points in parallel.
+// thread, points in parallel.  chi2() reads the errors of the last
+// computeActiveErrors (P.err: the last trial's, accepted or not).
+template <class Rec>
 __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_all, uint8_t* status_all,
                                                       uint8_t* bad_all, int pass, double thr, int* n_out,
                                                       const long long* offs)
@@ -890,15 +1045,17 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     int cnt = 0;
     for (int l = threadIdx.x; l < P.nL; l += blockDim.x) {
         const int p = P.iv_point[l];
-        for (int q = P.le_ptr[l]; q < P.le_ptr[l + 1]; q++) {
+        double pt[3];
+        load_point(P.point + 3 * p, pt);
+        for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
             if (bad[p]) break;
-            const int a = P.le_idx[q];
-            const int e = P.e_orig[a];
-            const double s = P.e_isig[a];
+            const Rec r = load_rec<Rec>(P, j);
+            const int e = P.e_orig[j];
+            const double s = (double)r.isig;
             const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
             const double chi2 = e0 * (s * e0) + e1 * (s * e1);
             double pc[3];
-            se3_map(P.pose + 7 * P.e_pose[a], P.point + 3 * p, pc);
+            map_point(P.pose + 7 * r.pose, pt, pc);
             if (chi2 > thr || !(pc[2] > 0.0)) {
                 if (--nobs[p] <= 2) bad[p] = 1;
                 st[e] = (uint8_t)pass;
@@ -916,13 +1073,13 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
 // (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295) on the subset
 // LocalBundleAdjustment uses.  Every edge is active; the free poses with an
 // edge and the points with an edge are ordered by g2o vertex id (ties by
-// index: a stable sort), which fixes the Hessian block order; per free pose
-// and per point the active edges in edge order (CSR); per point its edges to
-// free poses in pose-block order (the Schur columns).  Ranks come from a
-// scan when the ids are already increasing (the caller's usual order) and
-// from pairwise counts otherwise.  One workgroup per problem; the Hpl
-// scratch (dead until linearisation) holds the index maps.
-__device__ inline void lba_rank(const long long* id, const int* act, int n, int* rank, int* count,
+// index: a stable sort), which fixes the Hessian block order.  The edges are
+// laid out point-major (each point's edges in edge order) as records; per
+// free pose the (record, point) list of its edges in edge order.  Ranks come
+// from a scan when the ids are already increasing (the caller's usual order)
+// and from pairwise counts otherwise.  One workgroup per problem; the maps
+// live in the ce scratch.
+__device__ __forceinline__ void lba_rank(const long long* id, const int* act, int n, int* rank, int* count,
                                 BlockScratchN<kLbaWaves>& bs)
 {
     const int tid = threadIdx.x;
@@ -961,17 +1118,38 @@ __device__ inline void lba_rank(const long long* id, const int* act, int n, int*
     *count = total;
 }
 
+// counts in ptr[1 .. n] -> offsets (block scans); ptr[0] = 0
+__device__ __forceinline__ void lba_offsets(int* ptr, int n, BlockScratchN<kLbaWaves>& bs)
+{
+    const int tid = threadIdx.x;
+    int base = 0;
+    for (int c = 0; c < n; c += kLbaThreads) {
+        const int i = c + tid;
+        const int v = i < n ? ptr[i + 1] : 0;
+        int tot;
+        const int inc = block_exclusive_scan<kLbaWaves>(v, &tot, bs, (c / kLbaThreads) & 1) + v;
+        __syncthreads();
+        if (i < n) ptr[i + 1] = base + inc;
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) ptr[0] = 0;
+    __syncthreads();
+}
+
+template <class Rec>
 __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
 {
     __shared__ BlockScratchN<kLbaWaves> bs;
     LbaDev& A = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int NP = A.nposes_all, NL = A.npoints_all, E = A.nedges_all;
-    int* pflag = reinterpret_cast<int*>(A.ce);   // [NP] pose has an edge and is free
-    int* lflag = pflag + NP;                     // [NL] point has an edge
-    int* ph = lflag + NL;                        // [NP] pose block or -1
-    int* lh = ph + NP;                           // [NL] point block or -1
-    int* cur = lh + NL;                          // [NL] list cursors
+    int* pflag = A.ce;           // [NP] pose has an edge and is free
+    int* lflag = pflag + NP;     // [NL] point has an edge
+    int* ph = lflag + NL;        // [NP] pose block or -1
+    int* lh = ph + NP;           // [NL] point block or -1
+    int* cur = lh + NL;          // [NL] list cursors
+    int* pos = cur + NL;         // [E] point-major position of each edge
     for (int i = tid; i < NP; i += kLbaThreads) pflag[i] = 0;
     for (int i = tid; i < NL; i += kLbaThreads) lflag[i] = 0;
     __syncthreads();
@@ -990,54 +1168,55 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         if (ph[i] >= 0) iv_pose[ph[i]] = i;
     for (int i = tid; i < NL; i += kLbaThreads)
         if (lh[i] >= 0) iv_point[lh[i]] = i;
-    // edge records (every edge active, original order)
     int* pe_ptr = const_cast<int*>(A.pe_ptr);
     int* le_ptr = const_cast<int*>(A.le_ptr);
-    int* lc_ptr = const_cast<int*>(A.lc_ptr);
     for (int i = tid; i <= nP; i += kLbaThreads) pe_ptr[i] = 0;
-    for (int i = tid; i <= nL; i += kLbaThreads) {
-        le_ptr[i] = 0;
-        lc_ptr[i] = 0;
-    }
+    for (int i = tid; i <= nL; i += kLbaThreads) le_ptr[i] = 0;
     __syncthreads();
     for (int a = tid; a < E; a += kLbaThreads) {
-        const int p = A.r_edge_pose[a], l = A.r_edge_point[a];
-        const int eph = ph[p], elh = lh[l];
-        const_cast<int*>(A.e_orig)[a] = a;
-        const_cast<int*>(A.e_pose)[a] = p;
-        const_cast<int*>(A.e_point)[a] = l;
-        const_cast<int*>(A.e_ph)[a] = eph;
-        const_cast<int*>(A.e_lh)[a] = elh;
-        const_cast<double*>(A.e_obs)[2 * a] = A.r_edge_obs[2 * a];
-        const_cast<double*>(A.e_obs)[2 * a + 1] = A.r_edge_obs[2 * a + 1];
-        const_cast<double*>(A.e_isig)[a] = A.r_edge_isig[a];
-        if (eph >= 0) {
-            atomicAdd(&pe_ptr[eph + 1], 1);
-            atomicAdd(&lc_ptr[elh + 1], 1);
-        }
-        atomicAdd(&le_ptr[elh + 1], 1);
+        const int eph = ph[A.r_edge_pose[a]];
+        if (eph >= 0) atomicAdd(&pe_ptr[eph + 1], 1);
+        atomicAdd(&le_ptr[lh[A.r_edge_point[a]] + 1], 1);
     }
     __syncthreads();
-    // counts -> offsets (block scans)
-    auto offsets = [&](int* ptr, int n) {
-        int base = 0;
-        for (int c = 0; c < n; c += kLbaThreads) {
-            const int i = c + tid;
-            const int v = i < n ? ptr[i + 1] : 0;
-            int tot;
-            const int inc = block_exclusive_scan<kLbaWaves>(v, &tot, bs, (c / kLbaThreads) & 1) + v;
-            __syncthreads();
-            if (i < n) ptr[i + 1] = base + inc;
-            base += tot;
-            __syncthreads();
+    lba_offsets(pe_ptr, nP, bs);
+    lba_offsets(le_ptr, nL, bs);
+    // point-major slots, then each point's edges put in edge order (few)
+    int* e_orig = const_cast<int*>(A.e_orig);
+    for (int l = tid; l < nL; l += kLbaThreads) cur[l] = le_ptr[l];
+    __syncthreads();
+    for (int a = tid; a < E; a += kLbaThreads) e_orig[atomicAdd(&cur[lh[A.r_edge_point[a]]], 1)] = a;
+    __syncthreads();
+    for (int l = tid; l < nL; l += kLbaThreads) {
+        const int q0 = le_ptr[l], q1 = le_ptr[l + 1];
+        for (int i = q0 + 1; i < q1; i++) {   // insertion sort by edge index
+            const int x = e_orig[i];
+            int j = i - 1;
+            while (j >= q0 && e_orig[j] > x) {
+                e_orig[j + 1] = e_orig[j];
+                j--;
+            }
+            e_orig[j + 1] = x;
         }
-    };
-    offsets(pe_ptr, nP);
-    offsets(le_ptr, nL);
-    offsets(lc_ptr, nL);
+    }
+    __syncthreads();
+    // the records (float fields only when the host found every value exact)
+    Rec* rec = reinterpret_cast<Rec*>(const_cast<void*>(A.rec));
+    for (int j = tid; j < E; j += kLbaThreads) {
+        const int a = e_orig[j];
+        const int p = A.r_edge_pose[a];
+        Rec r{};
+        r.ox = A.r_edge_obs[2 * a];
+        r.oy = A.r_edge_obs[2 * a + 1];
+        r.isig = A.r_edge_isig[a];
+        r.pose = (uint16_t)p;
+        r.ph = (int16_t)ph[p];
+        rec[j] = r;
+        pos[a] = j;
+    }
     __syncthreads();
     // per free pose, its edges in edge order (wave per pose, ballot compaction)
-    int* pe_idx = const_cast<int*>(A.pe_idx);
+    int2* pe_idx = const_cast<int2*>(A.pe_idx);
     for (int p1 = wv; p1 < nP; p1 += kLbaWaves) {
         const int pose = iv_pose[p1];
         int w = pe_ptr[p1];
@@ -1045,42 +1224,9 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
             const int a = a0 + lane;
             const bool mine = a < E && A.r_edge_pose[a] == pose;
             const unsigned long long bal = __ballot(mine);
-            if (mine) pe_idx[w + __popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull))] = a;
+            if (mine)
+                pe_idx[w + __popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull))] = make_int2(pos[a], A.r_edge_point[a]);
             w += __popcll(bal);
-        }
-    }
-    // per point: its edges appended, then put in edge order (few per point);
-    // its Schur columns: the edges to free poses, in pose-block order
-    int* le_idx = const_cast<int*>(A.le_idx);
-    int* lc_idx = const_cast<int*>(A.lc_idx);
-    for (int l1 = tid; l1 < nL; l1 += kLbaThreads) cur[l1] = le_ptr[l1];
-    __syncthreads();
-    for (int a = tid; a < E; a += kLbaThreads) le_idx[atomicAdd(&cur[lh[A.r_edge_point[a]]], 1)] = a;
-    __syncthreads();
-    for (int l1 = tid; l1 < nL; l1 += kLbaThreads) {
-        const int q0 = le_ptr[l1], q1 = le_ptr[l1 + 1];
-        for (int i = q0 + 1; i < q1; i++) {   // insertion sort by edge index
-            const int x = le_idx[i];
-            int j = i - 1;
-            while (j >= q0 && le_idx[j] > x) {
-                le_idx[j + 1] = le_idx[j];
-                j--;
-            }
-            le_idx[j + 1] = x;
-        }
-        int w = lc_ptr[l1];
-        const int c0 = w;
-        for (int q = q0; q < q1; q++) {
-            const int a = le_idx[q];
-            const int eph = ph[A.r_edge_pose[a]];
-            if (eph < 0) continue;
-            int j = w - 1;   // stable insertion by pose block
-            while (j >= c0 && ph[A.r_edge_pose[lc_idx[j]]] > eph) {
-                lc_idx[j + 1] = lc_idx[j];
-                j--;
-            }
-            lc_idx[j + 1] = a;
-            w++;
         }
     }
     if (tid == 0) {
@@ -1094,12 +1240,13 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
 // Structures of the second optimize() (src/Optimizer.cc:472-478: the edges
 // the first outlier pass set to level 1 leave the graph) built on the device
 // from the first pass's: g2o's initializeOptimization / buildStructure
-// restated as order-preserving filters of the first pass's sorted lists
-// (active edges keep their original order, free poses / points their id
-// order, every CSR list its edge or pose order), so the result equals the
-// first-pass build (k_lba_build) on the reduced edge set.  One workgroup per problem;
-// the first pass's Hpl and Hll scratch (dead until the second pass
-// linearises) hold the index maps.  B's pointer fields are set by the host.
+// restated as order-preserving filters of the first pass's lists (the kept
+// records keep their point-major order, free poses / points their id order,
+// the pose lists their edge order), so the result equals the first-pass
+// build (k_lba_build) on the reduced edge set.  One workgroup per problem;
+// the maps live in the shared ce scratch (the first pass's point order is
+// dead by then).  B's pointer fields are set by the host.
+template <class Rec>
 __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, LbaDev* d1s, const uint8_t* status_all,
                                                              const long long* offs)
 {
@@ -1109,21 +1256,20 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
     const uint8_t* st = status_all + offs[3 * blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nE0 = A.nE, nP0 = A.nP, nL0 = A.nL;
-    int* na = reinterpret_cast<int*>(A.ce);     // [nE0] new edge index or -1
-    int* ph1 = reinterpret_cast<int*>(A.hp);    // [nP0] new pose hessian index or -1, then counts
-    int* cp = ph1 + nP0;                        // [nP0] kept edges per pose
-    int* lh1 = reinterpret_cast<int*>(A.hl);    // [nL0] new point index or -1
-    int* cl = lh1 + nL0;                        // [nL0] kept edges per point
-    int* cc = cl + nL0;                         // [nL0] kept Schur-column edges per point
-    auto kept = [&](int a0) { return st[A.e_orig[a0]] == 0; };
-    // 1. edges: new index by a block scan over the kept flags (edge order)
+    int* nj = A.ce;              // [nE0] new record index or -1
+    int* ph1 = nj + nE0;         // [nP0] new pose block or -1
+    int* cp = ph1 + nP0;         // [nP0] kept edges per free pose
+    int* lh1 = cp + nP0;         // [nL0] new point index or -1
+    int* cl = lh1 + nL0;         // [nL0] kept edges per point
+    auto kept = [&](int j) { return st[A.e_orig[j]] == 0; };
+    // 1. records: new index by a block scan over the kept flags (point-major order)
     int base = 0;
     for (int c = 0; c < nE0; c += kLbaThreads) {
-        const int a0 = c + tid;
-        const int k = a0 < nE0 && kept(a0) ? 1 : 0;
+        const int j = c + tid;
+        const int k = j < nE0 && kept(j) ? 1 : 0;
         int tot;
         const int off = block_exclusive_scan<kLbaWaves>(k, &tot, bs, (c / kLbaThreads) & 1);
-        if (a0 < nE0) na[a0] = k ? base + off : -1;
+        if (j < nE0) nj[j] = k ? base + off : -1;
         base += tot;
     }
     const int nE1 = base;
@@ -1131,16 +1277,14 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
     // 2. kept edges per pose (wave per pose) and per point (thread per point)
     for (int p = wv; p < nP0; p += kLbaWaves) {
         int cnt = 0;
-        for (int q = A.pe_ptr[p] + lane; q < A.pe_ptr[p + 1]; q += 64) cnt += na[A.pe_idx[q]] >= 0;
+        for (int q = A.pe_ptr[p] + lane; q < A.pe_ptr[p + 1]; q += 64) cnt += nj[A.pe_idx[q].x] >= 0;
         cnt = wave_sum(cnt);
         if (lane == 0) cp[p] = cnt;
     }
     for (int l = tid; l < nL0; l += kLbaThreads) {
-        int c1 = 0, c2 = 0;
-        for (int q = A.le_ptr[l]; q < A.le_ptr[l + 1]; q++) c1 += na[A.le_idx[q]] >= 0;
-        for (int q = A.lc_ptr[l]; q < A.lc_ptr[l + 1]; q++) c2 += na[A.lc_idx[q]] >= 0;
+        int c1 = 0;
+        for (int j = A.le_ptr[l]; j < A.le_ptr[l + 1]; j++) c1 += nj[j] >= 0;
         cl[l] = c1;
-        cc[l] = c2;
     }
     __syncthreads();
     // 3. new pose / point indices and list offsets: scans over the active ones
@@ -1163,77 +1307,59 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
         pe_base += tot2;
         __syncthreads();   // bs reads done before the next round's scans
     }
-    int nL1 = 0, le_base = 0, lc_base = 0;
+    int nL1 = 0, le_base = 0;
     for (int c = 0; c < nL0; c += kLbaThreads) {
         const int l = c + tid;
         const int act = l < nL0 && cl[l] > 0 ? 1 : 0;
-        int tot, tot2, tot3;
+        int tot, tot2;
         const int idx = block_exclusive_scan<kLbaWaves>(act, &tot, bs, 0);
         const int eo = block_exclusive_scan<kLbaWaves>(act ? cl[l] : 0, &tot2, bs, 1);
-        const int co = block_exclusive_scan<kLbaWaves>(act ? cc[l] : 0, &tot3, bs, 0);
         if (l < nL0) {
             const int l1 = act ? nL1 + idx : -1;
             if (act) {
                 const_cast<int*>(B.iv_point)[l1] = A.iv_point[l];
                 const_cast<int*>(B.le_ptr)[l1] = le_base + eo;
-                const_cast<int*>(B.lc_ptr)[l1] = lc_base + co;
             }
             lh1[l] = l1;
         }
         nL1 += tot;
         le_base += tot2;
-        lc_base += tot3;
         __syncthreads();   // bs reads done before the next round's scans
     }
     if (tid == 0) {
         const_cast<int*>(B.pe_ptr)[nP1] = pe_base;
         const_cast<int*>(B.le_ptr)[nL1] = le_base;
-        const_cast<int*>(B.lc_ptr)[nL1] = lc_base;
     }
     __syncthreads();
-    // 4. the kept edges' records, remapped
-    for (int a0 = tid; a0 < nE0; a0 += kLbaThreads) {
-        const int a1 = na[a0];
-        if (a1 < 0) continue;
-        const int ph = A.e_ph[a0];
-        const_cast<int*>(B.e_orig)[a1] = A.e_orig[a0];
-        const_cast<int*>(B.e_pose)[a1] = A.e_pose[a0];
-        const_cast<int*>(B.e_point)[a1] = A.e_point[a0];
-        const_cast<int*>(B.e_ph)[a1] = ph >= 0 ? ph1[ph] : -1;
-        const_cast<int*>(B.e_lh)[a1] = lh1[A.e_lh[a0]];
-        const_cast<double*>(B.e_obs)[2 * a1] = A.e_obs[2 * a0];
-        const_cast<double*>(B.e_obs)[2 * a1 + 1] = A.e_obs[2 * a0 + 1];
-        const_cast<double*>(B.e_isig)[a1] = A.e_isig[a0];
+    // 4. the kept records, pose blocks remapped
+    const Rec* ra = reinterpret_cast<const Rec*>(A.rec);
+    Rec* rb = reinterpret_cast<Rec*>(const_cast<void*>(B.rec));
+    for (int j = tid; j < nE0; j += kLbaThreads) {
+        const int j1 = nj[j];
+        if (j1 < 0) continue;
+        Rec r = ra[j];
+        r.ph = (int16_t)(r.ph >= 0 ? ph1[r.ph] : -1);
+        rb[j1] = r;
+        const_cast<int*>(B.e_orig)[j1] = A.e_orig[j];
     }
-    // 5. CSR lists: filters of the first pass's lists (wave per pose, with a
-    //    ballot compaction; thread per point)
+    // 5. pose lists: filters of the first pass's lists (wave per pose, ballot compaction)
     for (int p = wv; p < nP0; p += kLbaWaves) {
         const int p1 = ph1[p];
         if (p1 < 0) continue;
         int w = B.pe_ptr[p1];
         for (int q0 = A.pe_ptr[p]; q0 < A.pe_ptr[p + 1]; q0 += 64) {
             const int q = q0 + lane;
-            const int a1 = q < A.pe_ptr[p + 1] ? na[A.pe_idx[q]] : -1;
-            const unsigned long long bal = __ballot(a1 >= 0);
-            if (a1 >= 0) {
+            int2 ent = make_int2(-1, 0);
+            if (q < A.pe_ptr[p + 1]) {
+                ent = A.pe_idx[q];
+                ent.x = nj[ent.x];
+            }
+            const unsigned long long bal = __ballot(ent.x >= 0);
+            if (ent.x >= 0) {
                 const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-                const_cast<int*>(B.pe_idx)[w + __popcll(bal & lt)] = a1;
+                const_cast<int2*>(B.pe_idx)[w + __popcll(bal & lt)] = ent;
             }
             w += __popcll(bal);
-        }
-    }
-    for (int l = tid; l < nL0; l += kLbaThreads) {
-        const int l1 = lh1[l];
-        if (l1 < 0) continue;
-        int w = B.le_ptr[l1];
-        for (int q = A.le_ptr[l]; q < A.le_ptr[l + 1]; q++) {
-            const int a1 = na[A.le_idx[q]];
-            if (a1 >= 0) const_cast<int*>(B.le_idx)[w++] = a1;
-        }
-        w = B.lc_ptr[l1];
-        for (int q = A.lc_ptr[l]; q < A.lc_ptr[l + 1]; q++) {
-            const int a1 = na[A.lc_idx[q]];
-            if (a1 >= 0) const_cast<int*>(B.lc_idx)[w++] = a1;
         }
     }
     if (tid == 0) {
@@ -1256,8 +1382,8 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
 // ---------------------------------------------------------------------------
 namespace {
 
-// doubles of LDS for the reduced system (160 KB less the Schur edge table)
-constexpr int kLdsSCap = (160 * 1024 - kLbaThreads * kSchurEdges * 8 - 1024) / 8;
+// doubles of dynamic LDS for k_lba_iteration (160 KB less its static LDS)
+constexpr int kLdsCap = (160 * 1024 - 2048) / 8;
 
 // Runs fn(i) for i in [0, n) on up to 16 host threads (independent problems).
 template <typename Fn>
@@ -1288,17 +1414,20 @@ inline size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 // the LM backups, the per-edge errors, both passes' structure arrays and the
 // scratch.
 struct LbaPlay {
-    size_t pose, point, posebk, pointbk, cam, err;
+    size_t pose, point, pointbk, cam, err;
 };
 struct LbaPlan {
     int P = 0;
     uint8_t* d = nullptr;   // device base the LbaDev pointers were packed against
+    bool float_rec = true;  // every observation / information is a float: 16-byte edge records
+    LbaLds lay{};           // k_lba_iteration's dynamic LDS
+    size_t lds_bytes = 0;
     std::vector<LbaPlay> pl;
     std::vector<long long> offs;   // per problem: first edge, first point (global flag arrays)
     std::vector<int> n_poses, n_points, n_edges;
     long long eacc = 0, pacc = 0;
     size_t result_bytes = 0, base_bytes = 0, o_all_nobs = 0, o_all_st = 0, o_all_bad = 0, o_offs = 0, o_nout = 0;
-    size_t o_devs = 0, o_devs1 = 0, staged_end = 0, o_err = 0, err_bytes = 0, dev_end = 0, max_n2 = 0;
+    size_t o_devs = 0, o_devs1 = 0, staged_end = 0, o_err = 0, err_bytes = 0, dev_end = 0;
     double chi2_threshold = 0;
 };
 
@@ -1310,17 +1439,31 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         if (p.n_poses < 0 || p.n_points < 0 || p.n_edges < 0) return ORBX_ERR_ARG;
+        // the fixed-point limb sums are exact for < 2^22 contributions per
+        // entry of the reduced system (one per point); edge records hold the
+        // pose index in 16 bits and its block in 15
+        if (p.n_points >= (1 << 22) || p.n_poses > 32767) return ORBX_ERR_UNSUPPORTED;
     }
-    std::vector<uint8_t> bad_edge(P, 0);
+    std::vector<uint8_t> bad_edge(P, 0), not_float(P, 0);
     host_parallel(P, [&](int i) {
         const orbx_ba_problem& p = probs[i];
-        for (int e = 0; e < p.n_edges; e++)
+        for (int e = 0; e < p.n_edges; e++) {
             if (p.edge_point[e] < 0 || p.edge_point[e] >= p.n_points || p.edge_pose[e] < 0 || p.edge_pose[e] >= p.n_poses)
                 bad_edge[i] = 1;
+            // the reference's observations (cv::KeyPoint::pt) and information
+            // (mvInvLevelSigma2) are floats: stored as such when exact
+            const double v[3] = {p.edge_obs[2 * e], p.edge_obs[2 * e + 1], p.edge_inv_sigma2[e]};
+            for (double x : v) not_float[i] |= (double)(float)x != x;
+        }
     });
-    for (int i = 0; i < P; i++)
+    bool float_rec = true;
+    for (int i = 0; i < P; i++) {
         if (bad_edge[i]) return ORBX_ERR_ARG;
+        float_rec = float_rec && !not_float[i];
+    }
     L = LbaPlan{};
+    L.float_rec = float_rec;
+    const size_t rec_bytes = float_rec ? sizeof(EdgeRecF) : sizeof(EdgeRecD);
     L.P = P;
     L.d = d;
     L.chi2_threshold = P > 0 ? probs[0].chi2_threshold : 0;
@@ -1358,7 +1501,7 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     // from the caller's arrays (k_lba_build), the second from the first's
     // after the first outlier pass (k_lba_rebuild), so the host only stages
     // the problems, and both passes run back to back after one upload.
-    constexpr int kRaw = 7, kArr = 15;
+    constexpr int kRaw = 7, kArr = 7;
     std::vector<size_t> so_raw(kRaw * (size_t)P), so(kArr * (size_t)P), so1(kArr * (size_t)P);
     std::vector<int> nfree(P, 0);
     host_parallel(P, [&](int i) {
@@ -1371,11 +1514,11 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
         const size_t b[kRaw] = {E * 4, E * 4, E * 16, E * 8, NP, NP * 8, NL * 8};
         for (int k = 0; k < kRaw; k++) bytes[k] = b[k];
     };
+    // per pass: records, e_orig, iv_pose, iv_point, le_ptr, pe_ptr, pe_idx
     auto arr_bytes = [&](int i, size_t (&bytes)[kArr]) {
         const orbx_ba_problem& p = probs[i];
         const size_t E = p.n_edges, NP = nfree[i], NL = p.n_points;
-        const size_t b[kArr] = {E * 4,  E * 4,        E * 4,  E * 4,        E * 4,  E * 16,       E * 8, NP * 4,
-                                NL * 4, (NP + 1) * 4, E * 4, (NL + 1) * 4, E * 4, (NL + 1) * 4, E * 4};
+        const size_t b[kArr] = {E * rec_bytes, E * 4, NP * 4, NL * 4, (NL + 1) * 4, (NP + 1) * 4, E * 8};
         for (int k = 0; k < kArr; k++) bytes[k] = b[k];
     };
     size_t end = L.base_bytes;
@@ -1392,10 +1535,10 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     L.o_devs1 = end;
     end += align256(sizeof(LbaDev) * P);
     L.staged_end = end;
-    // device-only: the LM backups and the per-edge errors (zeroed on the device)
+    // device-only: the points' LM backups and the per-edge errors (zeroed
+    // on the device); the poses' backups live in LDS
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
-        pl[i].posebk = end;  end += align256(7 * (size_t)p.n_poses * 8);
         pl[i].pointbk = end; end += align256(3 * (size_t)p.n_points * 8);
     }
     L.o_err = end;
@@ -1413,21 +1556,36 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
                 end += align256(bytes[k]);
             }
         }
-    // device-only scratch, sized by the free poses, every point and edge
-    // (the Hpl scratch also holds k_lba_build's and k_lba_rebuild's maps)
-    std::vector<size_t> sc(8 * (size_t)P);
+    // k_lba_iteration's dynamic LDS for the batch: the poses (q, t, R,
+    // camera), the free poses' backups and the pose solution, and the reduced
+    // system in front of them when the largest one fits beside them
+    int np_max = 0, nf_max = 0;
+    for (int i = 0; i < P; i++) {
+        np_max = std::max(np_max, probs[i].n_poses);
+        nf_max = std::max(nf_max, nfree[i]);
+    }
+    const long long non_s = (long long)np_max * kPz + (long long)nf_max * kPbk + 6LL * nf_max;
+    if (non_s > kLdsCap) return ORBX_ERR_UNSUPPORTED;   // hundreds of keyframes: not a local BA
+    const long long sys_max = lba_sys_doubles(6LL * nf_max);
+    const bool s_in_lds = sys_max + non_s <= kLdsCap;
+    L.lay.s_doubles = s_in_lds ? (int)sys_max : 0;
+    L.lay.pz_off = L.lay.s_doubles;
+    L.lay.pbk_off = L.lay.pz_off + np_max * kPz;
+    L.lay.xp_off = L.lay.pbk_off + nf_max * kPbk;
+    L.lds_bytes = (size_t)(L.lay.xp_off + 6 * nf_max + 1) * 8;
+    // device-only scratch, sized by the free poses, every point and edge:
+    // ce (k_lba_build / k_lba_rebuild maps, then the point order), hp, hl,
+    // dl, S (the reduced system when it lives in global memory), ew
+    constexpr int kSc = 6;
+    std::vector<size_t> sc(kSc * (size_t)P);
     for (int i = 0; i < P; i++) {
         const orbx_ba_problem& p = probs[i];
         const size_t nE = p.n_edges, nL = p.n_points, n = 6 * (size_t)nfree[i];
         const size_t sys = (size_t)lba_sys_doubles((long long)n);
-        L.max_n2 = std::max(L.max_n2, sys);
-        // ce: index maps of k_lba_build / k_lba_rebuild only (no Hpl blocks
-        // are stored); S: the reduced system when it does not fit LDS
-        const size_t bytes[8] = {std::max(nE * 4, (2 * (size_t)p.n_poses + 3 * nL) * 4), 27 * (size_t)nfree[i] * 8,
-                                 9 * nL * 8, 12 * nL * 8, sys > (size_t)kLdsSCap ? sys * 8 : 8, (n + 3 * nL) * 8,
-                                 n * 8 + 8, nE * 8};
-        for (int k = 0; k < 8; k++) {
-            sc[8 * i + k] = end;
+        const size_t bytes[kSc] = {(nE + 2 * (size_t)p.n_poses + 3 * nL + 8) * 4, 27 * (size_t)nfree[i] * 8,
+                                   9 * nL * 8, 12 * nL * 8, s_in_lds ? 8 : sys * 8, nE * 8};
+        for (int k = 0; k < kSc; k++) {
+            sc[kSc * i + k] = end;
             end += align256(bytes[k]);
         }
     }
@@ -1463,34 +1621,23 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
             D.nedges_all = p.n_edges;
             D.pose = reinterpret_cast<double*>(d + pl[i].pose);
             D.point = reinterpret_cast<double*>(d + pl[i].point);
-            D.pose_bk = reinterpret_cast<double*>(d + pl[i].posebk);
             D.point_bk = reinterpret_cast<double*>(d + pl[i].pointbk);
             D.cam = reinterpret_cast<const double*>(d + pl[i].cam);
             D.err = reinterpret_cast<double*>(d + pl[i].err);
-            D.e_orig = reinterpret_cast<const int*>(d + o[0]);
-            D.e_pose = reinterpret_cast<const int*>(d + o[1]);
-            D.e_point = reinterpret_cast<const int*>(d + o[2]);
-            D.e_ph = reinterpret_cast<const int*>(d + o[3]);
-            D.e_lh = reinterpret_cast<const int*>(d + o[4]);
-            D.e_obs = reinterpret_cast<const double*>(d + o[5]);
-            D.e_isig = reinterpret_cast<const double*>(d + o[6]);
-            D.iv_pose = reinterpret_cast<const int*>(d + o[7]);
-            D.iv_point = reinterpret_cast<const int*>(d + o[8]);
-            D.pe_ptr = reinterpret_cast<const int*>(d + o[9]);
-            D.pe_idx = reinterpret_cast<const int*>(d + o[10]);
-            D.le_ptr = reinterpret_cast<const int*>(d + o[11]);
-            D.le_idx = reinterpret_cast<const int*>(d + o[12]);
-            D.lc_ptr = reinterpret_cast<const int*>(d + o[13]);
-            D.lc_idx = reinterpret_cast<const int*>(d + o[14]);
-            const size_t* c = &sc[8 * i];
-            D.ce = reinterpret_cast<double*>(d + c[0]);
+            D.rec = d + o[0];
+            D.e_orig = reinterpret_cast<const int*>(d + o[1]);
+            D.iv_pose = reinterpret_cast<const int*>(d + o[2]);
+            D.iv_point = reinterpret_cast<const int*>(d + o[3]);
+            D.le_ptr = reinterpret_cast<const int*>(d + o[4]);
+            D.pe_ptr = reinterpret_cast<const int*>(d + o[5]);
+            D.pe_idx = reinterpret_cast<const int2*>(d + o[6]);
+            const size_t* c = &sc[kSc * i];
+            D.ce = reinterpret_cast<int*>(d + c[0]);
             D.hp = reinterpret_cast<double*>(d + c[1]);
             D.hl = reinterpret_cast<double*>(d + c[2]);
             D.dl = reinterpret_cast<double*>(d + c[3]);
             D.S = reinterpret_cast<double*>(d + c[4]);
-            D.x = reinterpret_cast<double*>(d + c[5]);
-            D.bs = reinterpret_cast<double*>(d + c[6]);
-            D.ew = reinterpret_cast<double*>(d + c[7]);
+            D.ew = reinterpret_cast<double*>(d + c[5]);
             const size_t* q = &so_raw[kRaw * i];
             D.r_edge_pose = reinterpret_cast<const int*>(d + q[0]);
             D.r_edge_point = reinterpret_cast<const int*>(d + q[1]);
@@ -1519,18 +1666,20 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
 // (and the problems' status) between iterations, which synchronises; an
 // aborted problem's later iterations return at once (g2o's force-stop flag,
 // sparse_optimizer.cpp:394-396); without flags nothing waits.
-static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
-                      const volatile uint8_t* const* aborts)
+template <class Rec>
+static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
+                        const volatile uint8_t* const* aborts)
 {
     const int P = L.P;
     uint8_t* d = L.d;
     ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_err, 0, L.err_bytes, ctx->stream));
     timer_begin(ctx, "lba_build");
-    hipLaunchKernelGGL(k_lba_build, dim3(P), dim3(kLbaThreads), 0, ctx->stream, reinterpret_cast<LbaDev*>(d + L.o_devs));
+    hipLaunchKernelGGL(k_lba_build<Rec>, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
+                       reinterpret_cast<LbaDev*>(d + L.o_devs));
     timer_end(ctx, "lba_build");
     ORBX_HIP_CHECK(hipGetLastError());
-    const size_t lds = std::min(L.max_n2, (size_t)kLdsSCap) * 8;   // the second pass's systems are no larger
-    const int lds_cap = (int)(lds / 8);
+    // one layout for both passes: the second pass's systems are no larger
+    const size_t lds = L.lds_bytes;
     bool polled = false;
     for (int i = 0; aborts && i < P; i++) polled |= aborts[i] != nullptr;
     std::vector<LbaDev> hv(polled ? P : 0);
@@ -1539,7 +1688,7 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
         LbaDev* dd = reinterpret_cast<LbaDev*>(d + (pass == 0 ? L.o_devs : L.o_devs1));
         if (pass == 1) {
             timer_begin(ctx, "lba_rebuild");
-            hipLaunchKernelGGL(k_lba_rebuild, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
+            hipLaunchKernelGGL(k_lba_rebuild<Rec>, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
                                reinterpret_cast<const LbaDev*>(d + L.o_devs), dd, d + L.o_all_st,
                                reinterpret_cast<const long long*>(d + L.o_offs));
             timer_end(ctx, "lba_rebuild");
@@ -1566,7 +1715,7 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
                 if (all) break;
             }
             timer_begin(ctx, "lba_iter");
-            hipLaunchKernelGGL(k_lba_iteration, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, lds_cap);
+            hipLaunchKernelGGL(k_lba_iteration<Rec>, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, L.lay);
             timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
             // With an abort flag the host polls it between iterations (where
@@ -1582,7 +1731,7 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             }
         }
         timer_begin(ctx, "lba_outliers");
-        hipLaunchKernelGGL(k_lba_outliers, dim3(P), dim3(256), 0, ctx->stream, dd,
+        hipLaunchKernelGGL(k_lba_outliers<Rec>, dim3(P), dim3(256), 0, ctx->stream, dd,
                            reinterpret_cast<int*>(d + L.o_all_nobs), d + L.o_all_st, d + L.o_all_bad, pass + 1,
                            L.chi2_threshold, reinterpret_cast<int*>(d + L.o_nout) + pass * P,
                            reinterpret_cast<const long long*>(d + L.o_offs));
@@ -1590,6 +1739,12 @@ static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
         ORBX_HIP_CHECK(hipGetLastError());
     }
     return ORBX_OK;
+}
+
+static int lba_launch(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1, const volatile uint8_t* const* aborts)
+{
+    return L.float_rec ? lba_launch_t<EdgeRecF>(ctx, L, iters0, iters1, aborts)
+                       : lba_launch_t<EdgeRecD>(ctx, L, iters0, iters1, aborts);
 }
 
 // Reads a solved batch back (synchronising the context stream): poses and

@@ -66,7 +66,15 @@ def inv_sigma2_table(nlevels=8, scale=1.2):
 
 def make_problem(n_kf=20, n_points=2000, n_fixed_extra=2, seed=0, outlier_frac=0.01,
                  w=640, h=480, fx=500.0, fy=500.0, cx=320.0, cy=240.0,
-                 pose_noise=(0.01, 0.02), point_noise=0.02, pix_noise=1.0):
+                 pose_noise=(0.01, 0.02), point_noise=0.02, pix_noise=1.0,
+                 normalized=False, info_scale=1.0, near_points=0):
+    """normalized: observations and camera in normalised image coordinates
+    ((u - cx) / fx, (v - cy) / fy, camera fx = fy = 1, cx = cy = 0) instead
+    of pixels; info_scale multiplies every edge's information (with a
+    normalised camera, fx^2 keeps the chi2 of the pixel problem);
+    near_points: that many points moved to 2-8 cm in front of keyframe 1
+    (large Jacobians).  These exercise the reduced system outside the pixel
+    regime."""
     rng = np.random.default_rng(seed)
     n_poses = n_kf + n_fixed_extra
     center = np.array([0.0, 0.0, 4.0])
@@ -83,6 +91,11 @@ def make_problem(n_kf=20, n_points=2000, n_fixed_extra=2, seed=0, outlier_frac=0
         Rcw = Rwc.T
         poses_true.append((Rcw, -Rcw @ c))
     pts = center + rng.uniform([-2.0, -1.5, -2.0], [2.0, 1.5, 2.0], size=(n_points, 3))
+    if near_points:
+        R1, t1 = poses_true[1]
+        for i in range(near_points):   # camera-frame point 2-8 cm ahead, back to world
+            pc = np.array([rng.uniform(-0.01, 0.01), rng.uniform(-0.01, 0.01), rng.uniform(0.02, 0.08)])
+            pts[i] = R1.T @ (pc - t1)
     isig = inv_sigma2_table()
     e_point, e_pose, e_obs, e_isig = [], [], [], []
     nobs = np.zeros(n_points, np.int32)
@@ -90,12 +103,12 @@ def make_problem(n_kf=20, n_points=2000, n_fixed_extra=2, seed=0, outlier_frac=0
         vis = []
         for k, (R, t) in enumerate(poses_true):
             pc = R @ pts[p] + t
-            if pc[2] <= 0.5:
+            if pc[2] <= (0.01 if near_points else 0.5):
                 continue
             u, v = fx * pc[0] / pc[2] + cx, fy * pc[1] / pc[2] + cy
             if 0 <= u < w and 0 <= v < h:
                 vis.append((k, u, v))
-        if len(vis) < 3:
+        if len(vis) < (2 if p < near_points else 3):
             continue
         m = int(rng.integers(3, min(10, len(vis)) + 1))
         chosen = sorted(rng.choice(len(vis), m, replace=False))
@@ -109,8 +122,10 @@ def make_problem(n_kf=20, n_points=2000, n_fixed_extra=2, seed=0, outlier_frac=0
                 ov += rng.choice([-1, 1]) * rng.uniform(20, 60)
             e_point.append(p)
             e_pose.append(k)
+            if normalized:
+                ou, ov = (ou - cx) / fx, (ov - cy) / fy
             e_obs.append((np.float32(ou), np.float32(ov)))   # cv::KeyPoint coords are float
-            e_isig.append(isig[octave])
+            e_isig.append(isig[octave] * info_scale)
             nobs[p] += 1
     # keep only observed points, re-index
     used = np.nonzero(nobs)[0]
@@ -138,7 +153,7 @@ def make_problem(n_kf=20, n_points=2000, n_fixed_extra=2, seed=0, outlier_frac=0
     prob = {
         "pose_q": q, "pose_t": t, "pose_fixed": fixed,
         "pose_id": np.arange(n_poses, dtype=np.int64),
-        "pose_cam": np.tile([fx, fy, cx, cy], (n_poses, 1)).astype(np.float64),
+        "pose_cam": np.tile([1.0, 1.0, 0.0, 0.0] if normalized else [fx, fy, cx, cy], (n_poses, 1)).astype(np.float64),
         "points": pts0, "point_id": (np.arange(len(pts0)) + maxkf + 1).astype(np.int64),
         "point_nobs": nobs.astype(np.int32),
         "edge_point": e_point, "edge_pose": np.array(e_pose, np.int32),

@@ -79,6 +79,27 @@ def test_lba_matches_oracle(ctx, nkf, npts, seed, outl):
     assert gpu[3].chi2_final[0] < gpu[3].chi2_initial[0]
 
 
+@pytest.mark.parametrize("kw", [dict(normalized=True), dict(normalized=True, info_scale=250000.0),
+                                dict(info_scale=1e8), dict(info_scale=1e-8), dict(near_points=40),
+                                dict(normalized=True, info_scale=1e-4)],
+                         ids=["normalized", "normalized-fx2-info", "info-1e8", "info-1e-8", "near-points",
+                              "normalized-tiny-info"])
+def test_lba_outside_pixel_regime(ctx, kw):
+    """the fixed-point reduced system outside the pixel-camera
+    regime -- a normalised camera (fx = fy = 1, cx = cy = 0), very large and
+    very small information weights, points a few centimetres from a
+    keyframe -- against the oracle at the same bar (poses 1e-5, identical
+    outlier decisions and LM trajectories).  The accumulation is scaled per
+    problem and trial by a power of two derived from the reduced system's
+    largest diagonal (block_solver.hpp:381-432 accumulates in double)."""
+    prob = sb.make_problem(n_kf=8, n_points=400, seed=3, **kw)
+    ref = run_ref(prob)
+    gpu = run_gpu(ctx, prob)
+    compare(ref, gpu)
+    assert gpu[3].not_posdef == ref[3].not_posdef
+    assert sum(gpu[3].iterations) > 0
+
+
 def test_lba_without_extra_fixed_keyframes(ctx):
     prob = sb.make_problem(n_kf=8, n_points=400, n_fixed_extra=0, seed=7)
     compare(run_ref(prob), run_gpu(ctx, prob))

@@ -12,7 +12,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import orb_slam_amd as ox  # noqa: E402
 from orb_slam_amd import synth_ba as sb  # noqa: E402
 
-P = 64
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 uniq = [sb.make_problem(n_kf=20, n_points=2000, seed=5000 + i) for i in range(8)]
 cps = [sb.to_ctypes(uniq[i % 8]) for i in range(P)]
 arr = (sb.BAProblem * P)(*[c[0] for c in cps])
@@ -30,8 +30,8 @@ assert L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, None, esp, pbp, st) == 
 after = (ctypes.c_ulonglong * 16)()
 L.orbx_debug_lba_prof(after)
 d = [a - b for a, b in zip(after, before)]
-names = {6: "errors (iteration start)", 7: "linearize", 1: "S init", 2: "Schur complement", 3: "dense LLT",
-         4: "substitution", 5: "landmark back-subst", 8: "errors (trial)"}
+names = {6: "errors (first iteration)", 7: "linearize", 1: "S init", 2: "Schur complement", 3: "dense LLT",
+         4: "substitution", 8: "back-subst + update + errors"}
 tot = sum(d[k] for k in names)
 for k, nm in names.items():
     print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / max(tot, 1):5.1f} %)")
