@@ -501,6 +501,8 @@ def run_frames(args, wl, rank, local, world, dist):
         ctx.set_split(args.split_ways)
     if args.pyramid_mode:
         ctx.set_pyramid_mode(args.pyramid_mode)
+    if args.fast_chunk:
+        ctx.set_fast_chunk(args.fast_chunk)
     pipelined = not (args.sync_match or args.serial)
 
     def configure(serial):
@@ -688,7 +690,7 @@ def run_lba(args, wl, rank, local, world, dist):
 
 
 # bench timer name -> kernel symbol in the rocprofv3 CSVs
-KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": "k_pyr_resize", "fast": "k_fast_cells",
+KERNEL_SYMBOL = {"pyr0": "k_pyr_level0", "resize": ("k_pyr_resize", "k_pyr_cascade"), "fast": "k_fast_cells",
                  "retain": "k_retain_cells", "blur": "k_blur", "describe": "k_describe",
                  "match": "k_match_", "lba_iter": "k_lba_iteration", "lba_outliers": "k_lba_outliers",
                  "pose": "k_pose_opt"}
@@ -720,7 +722,8 @@ def pmc_traffic(key, name):
     sym = KERNEL_SYMBOL.get(name)
     if summary is None or not sym:
         return {"traffic": None, "traffic_source": src}
-    hits = [v for k, v in summary.items() if sym in k]
+    syms = sym if isinstance(sym, tuple) else (sym,)
+    hits = [v for k, v in summary.items() if any(s in k for s in syms)]
     if not hits:
         return {"traffic": None, "traffic_source": src}
     return {"traffic": round(sum(h["hbm_bytes_fetch_x2"] for h in hits) / len(hits)),
@@ -739,7 +742,8 @@ def pmc_valu(key, name):
     sym = KERNEL_SYMBOL.get(name)
     if summary is None or not sym:
         return None
-    hits = [v["SQ_INSTS_VALU"] for k, v in summary.items() if sym in k and "SQ_INSTS_VALU" in v]
+    syms = sym if isinstance(sym, tuple) else (sym,)
+    hits = [v["SQ_INSTS_VALU"] for k, v in summary.items() if any(s in k for s in syms) and "SQ_INSTS_VALU" in v]
     if not hits:
         return None
     return {"insts_per_launch": sum(hits) / len(hits), "source": src + " SQ_INSTS_VALU"}
@@ -852,8 +856,10 @@ def main():
                          "order) -- the form the headline roofline's PMC profile is collected from")
     ap.add_argument("--split-ways", type=int, default=0, choices=[0, 2, 3, 4],
                     help="extraction pipeline parts (orbx_dev_set_split; 0 = library default, 3)")
-    ap.add_argument("--pyramid-mode", type=int, default=0, choices=[0, 1],
-                    help="orbx_dev_set_pyramid_mode: 0 staged launches (default), 1 fused pyramid + blur")
+    ap.add_argument("--pyramid-mode", type=int, default=0, choices=[0, 1, 2],
+                    help="orbx_dev_set_pyramid_mode: 0 staged launches (default), 1 fused pyramid + blur, 2 band cascade")
+    ap.add_argument("--fast-chunk", type=int, default=0,
+                    help="orbx_dev_set_fast_chunk: cells per FAST workgroup (0 = library default)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()

@@ -160,8 +160,14 @@ int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int
  * consecutive batches concurrent).  Any other call on the context, or an
  * extraction into slots the pending match reads, waits for it first. */
 int orbx_dev_set_async_match(orbx_ctx* ctx, int enable);
-/* Pyramid construction mode (both produce identical buffers):
- * 0 = staged launches (level-0 copy, one resize per level, blur): default;
+/* Pyramid construction mode (all produce identical buffers):
+ * 0 = default: staged launches (level-0 copy, one resize per level, blur);
+ * 2 = the raw pyramid as a band cascade in one launch (one workgroup per row
+ *     band and frame derives every level from the previous level's rows in
+ *     LDS), then the blur; frames whose width is not a multiple of 16 take the
+ *     staged launches.  Slower than the staged launches at C2 (1.77 vs 1.03 ms
+ *     serialised per 1024 frames), kept for parity
+ *     coverage and experiments;
  * 1 = one fused launch per batch (orbx_pyramid.hip) that streams each frame
  *     once and builds every level and its blur from LDS rings, used when the
  *     frame size fits its plan (otherwise the staged launches run).  It
@@ -172,6 +178,16 @@ int orbx_dev_set_async_match(orbx_ctx* ctx, int enable);
  * current frame size and mode (1) or not (0). */
 int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode);
 int orbx_dev_pyramid_fused(orbx_ctx* ctx);
+/* The construction the current frame size and mode run: 0 staged launches,
+ * 1 fused, 2 band cascade. */
+int orbx_dev_pyramid_kind(orbx_ctx* ctx);
+/* Cells per FAST workgroup (k_fast_cells, src/ORBextractor.cc:599-614 per
+ * cell): 1 = one workgroup per cell; n > 1 = each workgroup scores n
+ * consecutive cells of a frame and copies the next cell's tile into a second
+ * LDS buffer while it scores the current one.  Outputs are identical; cells
+ * too wide for two buffers take one per workgroup.  Range 1..64. */
+int orbx_dev_set_fast_chunk(orbx_ctx* ctx, int cells);
+int orbx_dev_get_fast_chunk(const orbx_ctx* ctx);
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */

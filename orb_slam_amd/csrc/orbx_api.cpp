@@ -79,7 +79,7 @@ static void free_buffers(orbx_ctx* ctx)
     void* ptrs[] = {ctx->frames, ctx->pyr_raw, ctx->pyr_blur, ctx->cell_lists, ctx->retain_scratch, ctx->cell_count,
                     ctx->level_keys, ctx->cell_keys64, ctx->level_keys64, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
-                    ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles,
+                    ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles, ctx->cascade,
                     ctx->scratch, ctx->pose_dev, ctx->bow_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -96,6 +96,7 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     Geometry& g = ctx->geom;
     int r = compute_geometry(g, w, h);
     if (r != ORBX_OK) return r;
+    plan_cascade(g, kCascadeLds);
     const int S = ctx->slots;
     // per-slot buffers depend on the frame size / config only
     if ((long long)w * h > (long long)ctx->cap_frame_px) {
@@ -154,6 +155,12 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     if (!g.res_rows.empty())
         ORBX_HIP_CHECK(hipMemcpy(ctx->dgeom.res_rows, g.res_rows.data(), g.res_rows.size() * sizeof(ResizeRow), hipMemcpyHostToDevice));
     ORBX_HIP_CHECK(hipMemcpy(ctx->blur_tiles, tiles.data(), tiles.size() * sizeof(int4), hipMemcpyHostToDevice));
+    if ((int)g.cascade.size() > ctx->cap_cascade) {
+        if ((r = realloc_dev(ctx->cascade, g.cascade.size())) != ORBX_OK) return r;
+        ctx->cap_cascade = (int)g.cascade.size();
+    }
+    if (!g.cascade.empty())
+        ORBX_HIP_CHECK(hipMemcpy(ctx->cascade, g.cascade.data(), g.cascade.size() * sizeof(int4), hipMemcpyHostToDevice));
     // The retain kernel keeps per-cell state for up to 256 cells per level.
     if (g.max_cells_per_level > 256) return ORBX_ERR_UNSUPPORTED;
     // the fused-pyramid plan is optional: planned on first use (pyramid mode 1)
@@ -420,16 +427,34 @@ int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
 
 int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode)
 {
-    if (!ctx || mode < 0 || mode > 1) return ORBX_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 2) return ORBX_ERR_ARG;
     ctx_enter(ctx);
     ctx->pyr_mode = mode;
     return ORBX_OK;
 }
 
+int orbx_dev_set_fast_chunk(orbx_ctx* ctx, int cells)
+{
+    if (!ctx || cells < 1 || cells > 64) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->fast_chunk = cells;
+    return ORBX_OK;
+}
+
+int orbx_dev_get_fast_chunk(const orbx_ctx* ctx) { return ctx ? ctx->fast_chunk : ORBX_ERR_ARG; }
+
 int orbx_dev_pyramid_fused(orbx_ctx* ctx)
 {
     if (!ctx) return ORBX_ERR_ARG;
     return ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx) ? 1 : 0;
+}
+
+int orbx_dev_pyramid_kind(orbx_ctx* ctx)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    if (ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx)) return 1;
+    if (ctx->pyr_mode == 2 && ctx->geom.cascade_bands > 0) return 2;
+    return 0;
 }
 
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)

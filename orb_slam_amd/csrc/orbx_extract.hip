@@ -406,6 +406,176 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
 }
 
 // ---------------------------------------------------------------------------
+// The whole raw pyramid in one launch: ComputePyramid (src/ORBextractor.cc:
+// 781-822) as a cascade of row bands.  One workgroup per (band, frame) walks
+// the levels: level 0's rows come from the frame, level l's from level
+// l - 1's rows in LDS (ping-pong buffers, each row in the padded layout), so
+// no level waits for another launch.  Per (band, level) the host plan gives
+// the padded rows the band writes (a partition of the level) and the ROI
+// rows it computes: those rows' sources plus every ROI row the band's share
+// of the next level reads (a few halo rows are computed by two bands, with
+// the same arithmetic).  Each ROI pixel is the staged resize's (the row /
+// column tables, the SSE2 column path and the scalar tail), the border
+// pixels copyMakeBorder's REFLECT_101 copies of it, bytes past the padded
+// width zero: the buffers equal the staged launches', byte for byte.
+// plan[band * nlevels + l] = (first owned ROI row, end, first computed ROI
+// row, last computed ROI row); a band writes its owned rows' padded rows and
+// the border rows that reflect to them.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pyr_cascade(ExtractArgs a, const int4* plan, int buf_x)
+{
+    extern __shared__ uint4 s_dyn[];
+    uint8_t* const lds = reinterpret_cast<uint8_t*>(s_dyn);   // buffers: [0, buf_x) even levels, then odd
+    const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    constexpr int T = 256;
+    uint8_t* pyr = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
+    const uint8_t* img = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
+    int sc0 = 0, sstride = 0;   // the previous level's first computed ROI row and row pitch
+    for (int l = 0; l < a.nlevels; l++) {
+        const int4 pl = plan[band * a.nlevels + l];
+        const LevelGeom L = a.levels[l];
+        const int stride = L.stride, c0 = pl.z, nrows = pl.w - pl.z + 1;
+        uint8_t* dst = lds + (l & 1) * buf_x;
+        // 1. the ROI rows [c0, c0 + nrows) into dst at byte kEdge of each row
+        if (l == 0) {
+            // the frame's rows, 16-byte loads (w % 16 == 0: host), four in
+            // flight per thread before the first store
+            const int n16 = a.w >> 4, n = nrows * n16;
+            for (int u0 = 0; u0 < n; u0 += 4 * T) {
+                uint4 v[4];
+                int o[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int u = min(u0 + k * T + tid, n - 1), r = u / n16, q = u - r * n16;
+                    v[k] = *reinterpret_cast<const uint4*>(img + (size_t)(c0 + r) * a.w + 16 * q);
+                    o[k] = r * stride + kEdge + 16 * q;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) *reinterpret_cast<uint4*>(dst + o[k]) = v[k];
+            }
+        } else if (nrows > 0) {
+            const uint8_t* src = lds + ((l - 1) & 1) * buf_x;
+            // one thread per 4-pixel word and group of rows (G groups when the
+            // row is at most T / G words wide; wider rows loop over words)
+            const int nw = (L.w + 3) >> 2;
+            const int G = max(1, T / nw), g = tid / nw;
+            for (int q = tid - min(g, G - 1) * nw; g < G && q < nw; q += T) {
+                const int r_lo = g * nrows / G, r_hi = (g + 1) * nrows / G;
+                const int px0 = 4 * q;
+                int ca[4], a0[4], a1[4];
+                bool vb[4], vec = true;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const bool on = px0 + b < L.w;
+                    const ResizeCol c = a.res_cols[L.res_col_off + (on ? px0 + b : 0)];
+                    ca[b] = kEdge + c.sx0;
+                    a0[b] = on ? c.a0 : 0;
+                    a1[b] = on ? c.a1 : 0;
+                    vb[b] = px0 + b < L.nvec_resize;
+                    vec = vec && (!on || vb[b]);
+                }
+                auto hrow = [&](int sy, int (&S)[4]) {
+                    const uint8_t* base = src + (sy - sc0) * sstride;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) S[b] = base[ca[b]] * a0[b] + base[ca[b] + 1] * a1[b];
+                };
+                int H0[4], H1[4], cs0 = -1, cs1 = -1;
+                for (int r = r_lo; r < r_hi; r++) {
+                    const ResizeRow rw = a.res_rows[L.res_row_off + c0 + r];
+                    const int sy0 = rw.sy0, sy1 = rw.sy1, b0 = rw.b0, b1 = rw.b1;
+                    int A[4], B[4];
+                    if (sy0 == cs1) {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) A[b] = H1[b];
+                    } else if (sy0 == cs0) {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) A[b] = H0[b];
+                    } else {
+                        hrow(sy0, A);
+                    }
+                    if (sy1 == sy0) {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) B[b] = A[b];
+                    } else if (sy1 == cs1) {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) B[b] = H1[b];
+                    } else {
+                        hrow(sy1, B);
+                    }
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        H0[b] = A[b];
+                        H1[b] = B[b];
+                    }
+                    cs0 = sy0;
+                    cs1 = sy1;
+                    uint32_t word = 0;
+                    if (vec) {
+                        // VResizeLinearVec_32s8u (its 16-bit saturations cannot trigger
+                        // for 11-bit weights, k_pyr_resize_lds)
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            const int v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
+                            word |= (uint32_t)min(v, 255) << (8 * b);
+                        }
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) {
+                            int v;
+                            if (vb[b])
+                                v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
+                            else   // FixedPtCast<int, uchar, 22>
+                                v = (A[b] * b0 + B[b] * b1 + (1 << 21)) >> 22;
+                            word |= (uint32_t)sat_u8(v) << (8 * b);
+                        }
+                    }
+                    // bytes past the ROI (the last word) are overwritten by the border pass
+                    *reinterpret_cast<uint32_t*>(dst + r * stride + kEdge + px0) = word;
+                }
+            }
+        }
+        __syncthreads();
+        // 2. border columns (REFLECT_101 of the row's own pixels) and the zero
+        //    tail past the padded width, per computed row
+        const int tail = stride - L.pw;
+        for (int i = tid; i < nrows * (2 * kEdge + tail); i += T) {
+            const int r = i / (2 * kEdge + tail), k = i - r * (2 * kEdge + tail);
+            uint8_t* row = dst + r * stride;
+            if (k < 2 * kEdge) {
+                const int px = k < kEdge ? k : L.w + k;   // 0 .. 15, then kEdge + w .. kEdge + w + 15
+                row[px] = row[kEdge + reflect101(px - kEdge, L.w)];
+            } else {
+                row[L.pw + (k - 2 * kEdge)] = 0;
+            }
+        }
+        __syncthreads();
+        // 3. the band's rows to the pyramid, 16-byte stores: its owned ROI
+        //    rows, then the border rows whose reflection it owns
+        {
+            const int n16 = stride >> 4, nown = pl.y - pl.x;
+            uint8_t* out = pyr + L.off;
+            for (int i = tid; i < nown * n16; i += T) {
+                const int rr = i / n16, q = i - rr * n16, r = pl.x + rr;
+                *reinterpret_cast<uint4*>(out + (size_t)(kEdge + r) * stride + 16 * q) =
+                    *reinterpret_cast<const uint4*>(dst + (r - c0) * stride + 16 * q);
+            }
+            for (int i = tid; i < 2 * kEdge * n16; i += T) {
+                const int k = i / n16, q = i - k * n16;
+                const int py = k < kEdge ? k : L.h + k;   // 0 .. 15, then kEdge + h .. kEdge + h + 15
+                const int r = reflect101(py - kEdge, L.h);
+                if (r >= pl.x && r < pl.y)
+                    *reinterpret_cast<uint4*>(out + (size_t)py * stride + 16 * q) =
+                        *reinterpret_cast<const uint4*>(dst + (r - c0) * stride + 16 * q);
+            }
+        }
+        // the next level reads dst's ROI bytes (final since the first barrier)
+        // and writes the other buffer, which nobody reads any more
+        sc0 = c0;
+        sstride = stride;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // FAST-9/16 score map.  For a pixel with value v and ring d_k = v - p_k
 // (k = 0..15, OpenCV offsets), S = max(M_dark, M_bright) - 1 where M_dark is
 // the best 9-arc minimum of d and M_bright that of -d.  FAST at threshold t
@@ -541,10 +711,16 @@ constexpr int kDiagRepeat[4] = {ORBX_DIAG_REPEAT};
 // kThreads: 256 for cells up to 208-byte rows; the wide tiles of large
 // frames (1920x1080: 336-byte rows, 75 KB of LDS, two workgroups per CU)
 // get more waves per workgroup instead.
-template <int kP, int kThreads = 256, bool kBanded = false>
+// kChunk (whole-cell instances only): each workgroup takes `chunk`
+// consecutive cells of its frame with two tile buffers; the next cell's tile
+// is copied HBM -> LDS by global_load_lds (no VGPR staging) while the current
+// cell is scored, so its load latency hides behind the compass and scoring
+// work instead of stalling the workgroup at the start of every cell.
+template <int kP, int kThreads = 256, bool kBanded = false, bool kChunk = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
-    ExtractArgs a, int tile_bytes, int band_rows)
+    ExtractArgs a, int tile_bytes, int band_rows, int chunk)
 {
+    static_assert(!kChunk || (kP > 0 && !kBanded), "chunked FAST takes whole cells at a template pitch");
     constexpr int kBlock = kThreads, kWaves = kThreads / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratchN<kWaves> bs;
@@ -558,8 +734,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     constexpr int kUnitCap = 2 * kQueueWords;   // u16 NMS unit list aliasing the queues
     __shared__ __attribute__((aligned(16))) uint32_t qbuf[kQueueWords];
     uint16_t* ulist = reinterpret_cast<uint16_t*>(qbuf);
-    const int cell = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     QEntry* cand = reinterpret_cast<QEntry*>(qbuf) + wv * kQueue;
+    // S' (0 where not scored) and nz start at zero (contiguous: tile_bytes *
+    // (1 + 1/32), a multiple of 16); kept is cleared after the score pass
+    const int clear16 = (tile_bytes + tile_bytes / 32) >> 4;
+    auto clear_maps_at = [&](uint8_t* sm) {
+        for (int i = tid; i < clear16; i += kBlock) reinterpret_cast<uint4*>(sm)[i] = make_uint4(0, 0, 0, 0);
+    };
+    // One cell.  tile / sm: its tile buffer and the S' map (nz follows sm);
+    // ready: the tile already holds the cell's rows and S' / nz are clear
+    // (chunked instances), so the first band neither loads nor clears.
+    auto process = [&](const int cell, uint8_t* const tile, uint8_t* const sm, const bool ready) {
     const CellGeom C = a.cells[cell];
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
     if (!C.valid) {
@@ -572,8 +758,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     const int nq16 = (sh + hx + 15) >> 4;               // 16-byte words loaded per row
     const int P = kP ? kP : 16 * nq16, nq = P >> 2;     // tile pitch, dwords per row
     const uint8_t* src = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
-    uint8_t* tile = smem;
-    uint8_t* sm = smem + tile_bytes;
     uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
     uint32_t* sm32 = reinterpret_cast<uint32_t*>(sm);
     uint32_t* kept = tile32;                                      // bit per tile byte (after scoring)
@@ -607,12 +791,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
             t16[r3 * (P >> 4) + c3] = v3;
         }
     };
-    // S' (0 where not scored) and nz start at zero (contiguous: tile_bytes *
-    // (1 + 1/32), a multiple of 16); kept is cleared after the score pass
-    const int clear16 = (tile_bytes + tile_bytes / 32) >> 4;
-    auto clear_maps = [&]() {
-        for (int i = tid; i < clear16; i += kBlock) reinterpret_cast<uint4*>(sm32)[i] = make_uint4(0, 0, 0, 0);
-    };
+    auto clear_maps = [&]() { clear_maps_at(sm); };
     auto clear_kept = [&]() {
         for (int i = tid; i < (tile_bytes >> 7); i += kBlock) reinterpret_cast<uint4*>(kept)[i] = make_uint4(0, 0, 0, 0);
     };
@@ -883,14 +1062,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     // workgroup's LDS stays small (1920x1080: 4 workgroups per CU instead of
     // 2); S' of a row depends only on the rows within 3 of it, so the split
     // is exact.
-    auto band = [&](const int b0, const int b1, const int tmin) {
+    auto band = [&](const int b0, const int b1, const int tmin, const bool loaded = false) {
         const int w0 = max(0, b0 - 4), wh = min(hy, b1 + 4) - w0;
         const int s0 = max(3, b0 - 1), s1 = min(hy - 4, b1);   // scored rows (inclusive)
-        load_tile(w0, wh);
-        clear_maps();
-        __syncthreads();
+        if (!loaded) {
+            load_tile(w0, wh);
+            clear_maps();
+            __syncthreads();
+        }
+        FP_MARK(0);
         score_pass(tmin, s0 - w0, s1 - s0 + 1);
         __syncthreads();
+        FP_MARK(1);
         clear_kept();   // the tile is dead until the next band reloads it
         __syncthreads();
         const int n1 = block_sum(nms_pass(b0 - w0, b1 - w0, wh), bs, 0);
@@ -902,7 +1085,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     // (NMS against S' equals NMS against the t-score map for corners >= t),
     // so a cell is scored at fastTh first (far fewer compass survivors) and
     // rescored at 7 only when it needs the fallback.
-    FP_MARK(0);
     int n1 = 0, written = 0;
     if constexpr (kBanded) {
         // each band is emitted at fastTh as it is done; a cell whose kept
@@ -927,7 +1109,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         }
     } else if (hy > 6) {   // the whole cell as one band (the host sends band_rows = 0)
         int tmin_final = a.fast_th;
-        n1 = band(3, hy - 3, a.fast_th);
+        n1 = band(3, hy - 3, a.fast_th, ready);
         FP_MARK(2);
         if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
             if (threadIdx.x == 0) FP_ADD(8, 1);
@@ -944,6 +1126,51 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     }
     FP_MARK(4);
     if (tid == 0) FP_ADD(9, 1);
+    };
+    if constexpr (!kChunk) {
+        process(blockIdx.x, smem, smem + tile_bytes, false);
+    } else {
+        // LDS: tile buffers 0 and 1, then S' and nz
+        uint8_t* const sm = smem + 2 * tile_bytes;
+        constexpr int kW = kP >> 4;   // 16-byte words per tile row
+        // Copy a whole cell (rows 0 .. hy - 1, kW words each) into dst with
+        // global_load_lds: lane-linear LDS destinations, so every word of
+        // a row is loaded (columns past the ROI repeat its last word and are
+        // never read as pixels).  Cells process() does not score get none.
+        auto prefetch = [&](const int cell, uint8_t* dst) {
+            const CellGeom C = a.cells[cell];
+            if (!C.valid || C.hy <= 6) return;
+            const LevelGeom L = a.levels[C.level];
+            const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15;
+            const int last = ((roi_x - x_al + C.hx + 15) >> 4) - 1;
+            const uint8_t* src =
+                a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
+            const int n = C.hy * kW;
+            for (int base = wv * 64; base < n; base += kBlock) {
+                const int i = base + lane;
+                if (i < n) {
+                    const int r = i / kW, c = min(i - r * kW, last);
+                    __builtin_amdgcn_global_load_lds(src + (uint32_t)(r * L.stride + 16 * c),
+                                                     (__attribute__((address_space(3))) void*)(dst + 16 * base), 16, 0,
+                                                     0);
+                }
+            }
+        };
+        const int c0 = blockIdx.x * chunk, c1 = min(c0 + chunk, a.ncells);
+        clear_maps_at(sm);
+        prefetch(c0, smem);
+        for (int cell = c0; cell < c1; cell++) {
+            const int k = cell - c0;
+            // this cell's tile landed (the barrier waits for the copies), S'
+            // and nz are clear, and the previous cell is done with the other
+            // buffer; the next cell's copy then runs under this cell's scoring
+            __syncthreads();
+            if (cell + 1 < c1) prefetch(cell + 1, smem + ((k + 1) & 1) * tile_bytes);
+            process(cell, smem + (k & 1) * tile_bytes, sm, true);
+            __syncthreads();
+            clear_maps_at(sm);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1688,6 +1915,14 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_end(ctx, "pyramid", st);
             return;
         }
+        if (ctx->pyr_mode == 2 && g.cascade_bands > 0) {   // the whole raw pyramid in one launch
+            timer_begin(ctx, "resize", st);
+            for (int rep = 0; rep < kDiagRepeat[0]; rep++)
+                hipLaunchKernelGGL(k_pyr_cascade, dim3(g.cascade_bands, nb), dim3(256), g.cascade_lds, st, x, ctx->cascade,
+                                   g.cascade_buf_x);
+            timer_end(ctx, "resize", st);
+            return;
+        }
         timer_begin(ctx, "pyr0", st);
         {
             const LevelGeom& L = g.levels[0];
@@ -1753,7 +1988,15 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             };
             auto fast = [&](auto kern, int bytes, int band_rows, int threads) {
                 const int lds = fast_lds_bytes(bytes);
-                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows);
+                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows, 1);
+            };
+            // whole cells, `chunk` per workgroup, next tile prefetched (a
+            // second tile buffer)
+            int chunk = ctx->fast_chunk;
+            auto fast_chunked = [&](auto kern, int bytes) {
+                const int lds = fast_lds_bytes(bytes) + bytes;
+                const dim3 cgrid(((int)g.cells.size() + chunk - 1) / chunk, nb);
+                hipLaunchKernelGGL(kern, cgrid, dim3(256), lds, st, x, bytes, 0, chunk);
             };
             // the templated instances queue u16 tile positions: windows of up
             // to 64 KB (larger ones take the runtime-pitch instance)
@@ -1771,11 +2014,20 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 bytes = plan(P, fast_static_lds(false), br);
                 return bytes <= 65536;
             };
-            if (fits(96)) fast(k_fast_cells<96>, bytes, 0, 256);
-            else if (fits(144)) {
-                for (int rep = 0; rep < kDiagRepeat[3]; rep++) fast(k_fast_cells<144>, bytes, 0, 256);
+            // two tile buffers must fit the CU's LDS with the static queues
+            auto chunk_fits = [&](int b) { return fast_lds_bytes(b) + b + fast_static_lds(false) <= 160 * 1024; };
+            if (fits(96)) {
+                if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<96, 256, false, true>, bytes);
+                else fast(k_fast_cells<96>, bytes, 0, 256);
+            } else if (fits(144)) {
+                for (int rep = 0; rep < kDiagRepeat[3]; rep++) {
+                    if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<144, 256, false, true>, bytes);
+                    else fast(k_fast_cells<144>, bytes, 0, 256);
+                }
+            } else if (fits(208)) {
+                if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<208, 256, false, true>, bytes);
+                else fast(k_fast_cells<208>, bytes, 0, 256);
             }
-            else if (fits(208)) fast(k_fast_cells<208>, bytes, 0, 256);
             else if (fits_banded(336)) fast(k_fast_cells<336, kFastWideThreads, true>, bytes, br, kFastWideThreads);
             else {
                 bytes = plan(wmax, fast_static_lds(true), br);

@@ -291,4 +291,61 @@ int compute_geometry(Geometry& g, int w, int h)
     return ORBX_OK;
 }
 
+// k_pyr_cascade's bands: band j owns ROI rows [h j / B, h (j + 1) / B) of
+// every level (and the border rows that reflect to them) and computes those
+// rows plus every ROI row the next level's computed rows read (their
+// row-table sources), so each level's rows are derived from the previous
+// level's in LDS and the bands of consecutive levels stay aligned.  The
+// smallest band count whose two ping-pong buffers (rows x stride of the even
+// and of the odd levels) fit lds_target.
+void plan_cascade(Geometry& g, int lds_target)
+{
+    g.cascade.clear();
+    g.cascade_bands = g.cascade_buf_x = g.cascade_lds = 0;
+    const int nl = g.nlevels;
+    if (g.w % 16 != 0 || nl < 1) return;
+    std::vector<int4> tab;
+    for (int B = 1; B <= 512; B++) {
+        tab.assign((size_t)B * nl, make_int4(0, 0, 0, -1));
+        int bx = 0, by = 0;
+        for (int j = 0; j < B; j++) {
+            int need_lo = 1 << 30, need_hi = -1;
+            for (int l = nl - 1; l >= 0; l--) {
+                const LevelGeom& L = g.levels[l];
+                const int o0 = (int)((long long)L.h * j / B), o1 = (int)((long long)L.h * (j + 1) / B);
+                int lo = std::min(need_lo, o0), hi = std::max(need_hi, o1 - 1);
+                if (o0 >= o1) lo = need_lo, hi = need_hi;
+                if (lo > hi) lo = 0, hi = -1;
+                tab[(size_t)j * nl + l] = make_int4(o0, o1, lo, hi);
+                const int bytes = (hi - lo + 1) * L.stride;
+                (l % 2 == 0 ? bx : by) = std::max(l % 2 == 0 ? bx : by, bytes);
+                need_lo = 1 << 30;
+                need_hi = -1;
+                if (l > 0)
+                    for (int r = lo; r <= hi; r++) {
+                        const ResizeRow& rr = g.res_rows[L.res_row_off + r];
+                        need_lo = std::min(need_lo, (int)std::min(rr.sy0, rr.sy1));
+                        need_hi = std::max(need_hi, (int)std::max(rr.sy0, rr.sy1));
+                    }
+            }
+        }
+        bx = (bx + 15) & ~15;
+        if (bx + by <= lds_target) {
+            // the halo rows computed twice: a plan that would recompute more
+            // than half again of the resized levels' pixels is not taken
+            long long comp = 0, roi = 0;
+            for (int l = 1; l < nl; l++) {
+                roi += (long long)g.levels[l].w * g.levels[l].h;
+                for (int j = 0; j < B; j++) comp += (long long)g.levels[l].w * (tab[(size_t)j * nl + l].w - tab[(size_t)j * nl + l].z + 1);
+            }
+            if (comp * 2 > roi * 3) return;
+            g.cascade = tab;
+            g.cascade_bands = B;
+            g.cascade_buf_x = bx;
+            g.cascade_lds = bx + by;
+            return;
+        }
+    }
+}
+
 }  // namespace orbx

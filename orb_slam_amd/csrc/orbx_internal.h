@@ -141,6 +141,11 @@ struct Geometry {
     int max_list_cap = 0;     // max list_cap over cells
     int max_level_cap = 0;
     int max_cells_per_level = 0;
+    // band cascade of the raw pyramid (k_pyr_cascade): per (band, level) the
+    // owned padded rows [x, y) and the computed ROI rows [z, w]; 0 bands when
+    // the geometry does not take it (the staged launches run instead)
+    std::vector<int4> cascade;
+    int cascade_bands = 0, cascade_buf_x = 0, cascade_lds = 0;
 };
 
 // ORBextractor constructor tables (src/ORBextractor.cc:457-511).
@@ -149,6 +154,14 @@ void init_extractor_tables(Geometry& g, int nfeatures, float scale_factor, int n
 // Returns ORBX_OK or ORBX_ERR_UNSUPPORTED for sizes the reference cannot
 // handle (empty cell grid, 2x INTER_AREA decimation).
 int compute_geometry(Geometry& g, int w, int h);
+// The band plan of k_pyr_cascade for the current geometry (fills
+// g.cascade*; leaves 0 bands when the frame width is not a multiple of 16 or
+// no band count fits lds_target bytes of LDS).
+void plan_cascade(Geometry& g, int lds_target);
+#ifndef ORBX_CASCADE_LDS
+#define ORBX_CASCADE_LDS (40 * 1024)   // 4 workgroups per CU
+#endif
+constexpr int kCascadeLds = ORBX_CASCADE_LDS;
 
 // Device copies of the geometry tables.
 struct DeviceGeometry {
@@ -249,10 +262,13 @@ struct orbx_ctx {
     int cap_cells = 0;
     int cap_res_cols = 0, cap_res_rows = 0, cap_blur_tiles = 0;
     int4* blur_tiles = nullptr;        // (level, first item, dwords/row, strips) blur blocks
+    int4* cascade = nullptr;           // k_pyr_cascade band plan (Geometry::cascade)
+    int cap_cascade = 0;
     int blur_tiles_n = 0;
     // fused pyramid + blur plan for the current geometry (orbx_pyramid.hip)
     orbx::PyrPlan pyr;
-    int pyr_mode = 0;                  // 0: staged launches, 1: fused when the plan fits
+    int pyr_mode = 0;                  // 0: staged launches, 1: fused, 2: band cascade (staged when it does not fit)
+    int fast_chunk = 1;                // cells per FAST workgroup (> 1: next tile prefetched by global_load_lds)
     bool pyr_planned = false;          // pyr holds the plan of the current geometry
     orbx::PyrLevel* d_pyr_levels = nullptr;
     int32_t* d_pyr_sched = nullptr;
