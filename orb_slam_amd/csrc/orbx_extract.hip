@@ -91,6 +91,21 @@ struct ExtractArgs {
     int max_list_cap, max_level_cap;
 };
 
+// The geometry tables (cells, levels, ...) are never written by a kernel:
+// read through the constant address space, a wave-uniform read is a scalar
+// load (scalar cache hit once warm) instead of a vector load + readfirstlane,
+// so the dependent table reads in front of a workgroup's first data loads
+// cost cache hits rather than L2 round trips.
+template <class T>
+__device__ __forceinline__ T cget(const T* p, int i)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(4))) T*)p)[i];
+#else
+    return p[i];   // host pass: parsed, never called
+#endif
+}
+
 __device__ inline uint8_t sat_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
 __device__ inline int sat_s16(int v) { return min(max(v, -32768), 32767); }
 
@@ -151,7 +166,7 @@ constexpr int kPyr0Shift = (16 - kEdge % 16) % 16;   // (16q - kEdge) mod 16
 __global__ __launch_bounds__(256) void k_pyr_level0(ExtractArgs a, int q_lo, int nint)
 {
     const int f = blockIdx.y;
-    const LevelGeom L = a.levels[0];
+    const LevelGeom L = cget(a.levels, 0);
     const int qpr = L.stride >> 4, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
     const int nbord = qpr - nint;
     int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -248,8 +263,8 @@ __device__ inline uint8_t resize_pixel(const uint8_t* prev, int pstride, const R
 __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 {
     const int f = blockIdx.y;
-    const LevelGeom L = a.levels[level];
-    const LevelGeom P = a.levels[level - 1];
+    const LevelGeom L = cget(a.levels, level);
+    const LevelGeom P = cget(a.levels, level - 1);
     const int wpr = L.stride >> 2, nstrips = (L.ph + kPyrRows - 1) / kPyrRows;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= wpr * nstrips) return;
@@ -433,7 +448,7 @@ __global__ __launch_bounds__(256) void k_pyr_cascade(ExtractArgs a, const int4* 
     int sc0 = 0, sstride = 0;   // the previous level's first computed ROI row and row pitch
     for (int l = 0; l < a.nlevels; l++) {
         const int4 pl = plan[band * a.nlevels + l];
-        const LevelGeom L = a.levels[l];
+        const LevelGeom L = cget(a.levels, l);
         const int stride = L.stride, c0 = pl.z, nrows = pl.w - pl.z + 1;
         uint8_t* dst = lds + (l & 1) * buf_x;
         // 1. the ROI rows [c0, c0 + nrows) into dst at byte kEdge of each row
@@ -746,13 +761,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     // ready: the tile already holds the cell's rows and S' / nz are clear
     // (chunked instances), so the first band neither loads nor clears.
     auto process = [&](const int cell, uint8_t* const tile, uint8_t* const sm, const bool ready) {
-    const CellGeom C = a.cells[cell];
+    const CellGeom C = cget(a.cells, cell);
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
     if (!C.valid) {
         if (tid == 0) *count_out = 0;
         return;
     }
-    const LevelGeom L = a.levels[C.level];
+    const LevelGeom L = cget(a.levels, C.level);
     const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15, sh = roi_x - x_al;
     const int hx = C.hx, hy = C.hy;
     const int nq16 = (sh + hx + 15) >> 4;               // 16-byte words loaded per row
@@ -1138,9 +1153,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         // a row is loaded (columns past the ROI repeat its last word and are
         // never read as pixels).  Cells process() does not score get none.
         auto prefetch = [&](const int cell, uint8_t* dst) {
-            const CellGeom C = a.cells[cell];
+            const CellGeom C = cget(a.cells, cell);
             if (!C.valid || C.hy <= 6) return;
-            const LevelGeom L = a.levels[C.level];
+            const LevelGeom L = cget(a.levels, C.level);
             const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15;
             const int last = ((roi_x - x_al + C.hx + 15) >> 4) - 1;
             const uint8_t* src =
@@ -1272,10 +1287,10 @@ constexpr float kHarrisScale4 = kHarrisScale * kHarrisScale * kHarrisScale * kHa
 __global__ __launch_bounds__(256) void k_harris_cells(ExtractArgs a)
 {
     const int cell = blockIdx.x, f = blockIdx.y;
-    const CellGeom C = a.cells[cell];
+    const CellGeom C = cget(a.cells, cell);
     if (!C.valid) return;
     const int n = min(a.cell_count[(size_t)f * a.ncells + cell], C.list_cap);
-    const LevelGeom L = a.levels[C.level];
+    const LevelGeom L = cget(a.levels, C.level);
     const int stride = L.stride;
     const uint8_t* img = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)kEdge * stride + kEdge;
     const uint32_t* src = a.cell_lists + (size_t)f * a.list_entries + C.list_off;
@@ -1346,8 +1361,8 @@ __global__ __launch_bounds__(256) void k_retain_cells(ExtractArgs a, int waves_p
     if (cell >= a.ncells) return;
     E* list = reinterpret_cast<E*>(sbuf + (size_t)wv * wave_words);
     int* pos = reinterpret_cast<int*>(list + kRetainCellCap);
-    const CellGeom C = a.cells[cell];
-    const LevelGeom L = a.levels[C.level];
+    const CellGeom C = cget(a.cells, cell);
+    const LevelGeom L = cget(a.levels, C.level);
     const int c = cell - L.cell_base;
     const int32_t* counts = a.cell_count + (size_t)f * a.ncells + L.cell_base;
     int k, pre, level_total;
@@ -1384,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_retain_levels(ExtractArgs a, int waves_
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int level = blockIdx.x * waves_per_block + wv, f = blockIdx.y;
     if (level >= a.nlevels) return;
-    const LevelGeom L = a.levels[level];
+    const LevelGeom L = cget(a.levels, level);
     int32_t* cnt = a.level_count + (size_t)f * a.nlevels + level;
     const int nlev = *cnt;
     if (nlev <= L.n_desired) return;
@@ -1422,10 +1437,10 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
     // the horizontal taps come from the adjacent lanes (DPP wave_shr:1 /
     // wave_shl:1) instead of two more loads.
     const int f = blockIdx.y;
-    const int4 tl = tiles[blockIdx.x];   // level, first wave item, chunks per row, strips
+    const int4 tl = cget(tiles, (int)blockIdx.x);   // level, first wave item, chunks per row, strips
     const int wi = tl.y + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wi >= tl.z * tl.w) return;       // whole waves
-    const LevelGeom L = a.levels[tl.x];
+    const LevelGeom L = cget(a.levels, tl.x);
     const int strip = wi / tl.z, chunk = wi - strip * tl.z;
     const int ndw = L.stride >> 2;
     const int dw = kBlurChunkCols * chunk - 1 + lane;
