@@ -43,3 +43,24 @@ def test_descriptor_distance_host_entry():
     a = (ctypes.c_uint8 * 32)(*([0xFF] * 32))
     b = (ctypes.c_uint8 * 32)(*([0x0F] * 32))
     assert ox.lib().orbx_descriptor_distance(a, b) == 128
+
+
+def test_context_setters_refuse_null_context():
+    """The mode setters / getters validate their arguments before touching
+    a device: a null context is ORBX_ERR_ARG (runs without a GPU)."""
+    lib = ox.lib()
+    err_arg = -1
+    calls = [
+        ("orbx_dev_set_pyramid_mode", (None, 0)),
+        ("orbx_dev_pyramid_kind", (None,)),
+        ("orbx_dev_pyramid_fused", (None,)),
+        ("orbx_dev_set_fast_chunk", (None, 2)),
+        ("orbx_dev_get_fast_chunk", (None,)),
+        ("orbx_set_nth_pivot", (None, 1)),
+        ("orbx_get_nth_pivot", (None,)),
+        ("orbx_dev_set_split", (None, 3)),
+        ("orbx_dev_set_async_match", (None, 1)),
+        ("orbx_lba_run", (None, 5, 10, None)),
+    ]
+    for name, args in calls:
+        assert getattr(lib, name)(*args) == err_arg, name
