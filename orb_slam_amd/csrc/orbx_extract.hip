@@ -1081,8 +1081,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         const int w0 = max(0, b0 - 4), wh = min(hy, b1 + 4) - w0;
         const int s0 = max(3, b0 - 1), s1 = min(hy - 4, b1);   // scored rows (inclusive)
         if (!loaded) {
+            FP_MARK(7);
             load_tile(w0, wh);
+            FP_MARK(5);
             clear_maps();
+            FP_MARK(6);
             __syncthreads();
         }
         FP_MARK(0);

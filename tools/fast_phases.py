@@ -25,10 +25,12 @@ ctx.sync()
 after = (ctypes.c_ulonglong * 16)()
 L.orbx_debug_fast_prof(after)
 d = [a - b for a, b in zip(after, before)]
-names = {0: "load+clear", 1: "score@th", 2: "nms@th", 3: "fallback(score+nms@7)", 4: "compact+store",
+names = {7: "start..tile load (geometry)", 5: "tile loads + LDS stores", 6: "clear S'/nz",
+         0: "first barrier wait", 1: "score@th", 2: "nms@th", 3: "fallback(score+nms@7)", 4: "compact+store",
          8: "fallback cells", 9: "cells", 10: "survivors@th", 11: "survivors@7", 12: "unit batches"}
-tot = sum(d[k] for k in range(5))
+stamped = (0, 1, 2, 3, 4, 5, 6, 7)
+tot = sum(d[k] for k in stamped)
 for k, n in names.items():
     v = d[k]
-    extra = f" ({100.0 * v / tot:.1f} % of stamped cycles)" if k < 5 and tot else ""
+    extra = f" ({100.0 * v / tot:.1f} % of stamped cycles)" if k in stamped and tot else ""
     print(f"{n:24s} {v:16d}{extra}")
