@@ -669,9 +669,10 @@ def run_lba(args, wl, rank, local, world, dist):
         pcie = {"problems_per_s": round(P * n_host / dt, 2), "ms_per_step": round(1e3 * dt / n_host, 3),
                 "steps": n_host, "boundary": "orbx_lba_solve_batch: host arrays in / out (packing, H2D, D2H)"}
     ab = {"lba_iter": lba_bytes(22, 2000, n_edges), "lba_outliers": n_edges * 16}
-    # lba_bytes is per problem and LM iteration: every lba_iter launch runs one
-    # iteration of all P problems (5 + 10 launches per step), lba_outliers
-    # one pass over all P (2 per step)
+    # lba_bytes is per problem and LM iteration: the two lba_iter launches of
+    # a step run the 5 and the 10 iterations of all P problems (one launch per
+    # optimize() pass without abort flags), lba_outliers one pass over all P
+    # (2 per step)
     units_per_step = {"lba_iter": P * 15, "lba_outliers": P * 2}
     cpu = None
     flops = float(sum(lba_flops(probs[i], st[i]) for i in range(P)))

@@ -12,9 +12,10 @@
 // blocks of the linearisation.  The poses (quaternion, translation, rotation
 // matrix, camera) of the problem live in LDS for the whole launch.
 //
-// Device work per LM iteration (one 512-thread workgroup per problem, one
-// launch per iteration so the caller's abort flag is polled between
-// iterations exactly where SparseOptimizer::optimize polls terminate()):
+// Device work per LM iteration (one 512-thread workgroup per problem; one
+// launch per iteration when the caller passes abort flags, polled between
+// iterations exactly where SparseOptimizer::optimize polls terminate(), else
+// one launch per optimize() pass):
 //   errors    EdgeSE3ProjectXYZ::computeError per edge, Huber robust chi2 --
 //             only in an optimize() call's first iteration: every later
 //             iteration starts at the state the previous iteration's accepted
@@ -492,14 +493,23 @@ __device__ __forceinline__ void point_dinv(const double* h, double lambda, doubl
     d[6] = c02 * inv; d[7] = c12 * inv; d[8] = c22 * inv;
 }
 
-// One point's Schur contributions (thread per point, its edges contiguous):
-// D = Hll + lambda I, Dinv, db = Dinv bl; for each free-pose edge u:
-// bs -= W_u db and, for every later edge v of the point (and v = u),
-// S(p_u, p_v) -= W_u Dinv W_v^T as fixed-point limbs.  With W = (w B)^T A
-// the 6x6 block is (w B_u)^T G (w B_v), G = (A_u Dinv) A_v^T 2x2: W is never
-// formed.  Register budget (128 VGPRs at 1024 threads): Dinv and db are
-// re-read from dl per edge u, and only A_u Dinv and w B_u stay live across
-// the loop over v.
+// One point's Schur contributions: D = Hll + lambda I, Dinv, db = Dinv bl;
+// for each free-pose edge u: bs -= W_u db and, for every later edge v of the
+// point (and v = u), S(p_u, p_v) -= W_u Dinv W_v^T as fixed-point limbs.
+// With W = (w B)^T A the 6x6 block is (w B_u)^T G (w B_v), G = (A_u Dinv)
+// A_v^T 2x2: W is never formed.
+// (w B)(0, k) a0 + (w B)(1, k) a1 as fma((w B)(1, k), a1, (w B)(0, k) a0),
+// with jac_pose's structural zeros B(0, 4) = B(1, 3) = 0 left out: the fused
+// form's zero product adds only a signed zero, so the value is the same (a
+// non-finite a0 / a1 still reaches the other columns, which reject the
+// trial as before).
+__device__ __forceinline__ double wb_dot(const double (&wB)[12], int k, double a0, double a1)
+{
+    if (k == 3) return wB[3] * a0;
+    if (k == 4) return wB[10] * a1;
+    return __fma_rn(wB[6 + k], a1, wB[k] * a0);
+}
+
 template <bool kLds>
 __device__ __forceinline__ void schur_block(const double (&AD)[6], const double (&wBu)[12], const double (&Av)[6],
                                    const double (&wBv)[12], int pu, int pv, bool diag, double kS, fx_t* hi, fx_t* lo,
@@ -516,8 +526,8 @@ __device__ __forceinline__ void schur_block(const double (&AD)[6], const double 
     double Q0[6], Q1[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) {
-        Q0[r] = -kS * __fma_rn(wBu[6 + r], G[2], wBu[r] * G[0]);
-        Q1[r] = -kS * __fma_rn(wBu[6 + r], G[3], wBu[r] * G[1]);
+        Q0[r] = -kS * wb_dot(wBu, r, G[0], G[2]);
+        Q1[r] = -kS * wb_dot(wBu, r, G[1], G[3]);
     }
     // element (r, c) belongs at S(6 pu + r, 6 pv + c): stored at the packed
     // lower index of that position or of its mirror
@@ -529,7 +539,7 @@ __device__ __forceinline__ void schur_block(const double (&AD)[6], const double 
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int c = 0; c < 6; c++) {
-                const double t = __fma_rn(Q1[r], wBv[6 + c], Q0[r] * wBv[c]);
+                const double t = wb_dot(wBv, c, Q0[r], Q1[r]);
                 const int rr = upper ? c : r, cc = upper ? r : c;
                 fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * rr + rr * (rr + 1) / 2 + cc, t, bad);
             }
@@ -541,8 +551,8 @@ __device__ __forceinline__ void schur_block(const double (&AD)[6], const double 
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int c = 0; c <= r; c++) {
-                double t = __fma_rn(Q1[r], wBv[6 + c], Q0[r] * wBv[c]);
-                if (!diag) t += __fma_rn(Q1[c], wBv[6 + r], Q0[c] * wBv[r]);
+                double t = wb_dot(wBv, c, Q0[r], Q1[r]);
+                if (!diag) t += wb_dot(wBv, r, Q0[c], Q1[c]);
                 fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * r + r * (r + 1) / 2 + c, t, bad);
             }
     }
@@ -558,7 +568,7 @@ __device__ __forceinline__ void edge_aw(const LbaDev& P, const double* z, int j,
     jac_pose(z + 16, pc, B);
     const double w = P.ew[j];
 #pragma unroll
-    for (int i = 0; i < 12; i++) wB[i] = B[i] * w;
+    for (int i = 0; i < 12; i++) wB[i] = (i == 4 || i == 9) ? 0.0 : B[i] * w;   // wb_dot skips them
 }
 
 template <class Rec, bool kLds>
@@ -598,7 +608,7 @@ __device__ __forceinline__ void schur_point(LbaDev& P, const double* pz, int l, 
             const double adb1 = __fma_rn(Au[5], d[11], __fma_rn(Au[4], d[10], Au[3] * d[9]));
 #pragma unroll
             for (int r = 0; r < 6; r++)
-                fx_add_scaled<kLds>(bhi, blo, 6 * pu + r, -__fma_rn(wBu[6 + r], adb1, wBu[r] * adb0) * kB, bad);
+                fx_add_scaled<kLds>(bhi, blo, 6 * pu + r, -wb_dot(wBu, r, adb0, adb1) * kB, bad);
             schur_block<kLds>(AD, wBu, Au, wBu, pu, pu, true, kS, hi, lo, bad);   // v = u
         }
         for (int jv = ju + 1; jv < j1; jv++) {
@@ -867,9 +877,16 @@ struct LbaLds {
     int s_doubles, pz_off, pbk_off, xp_off;
 };
 
-// OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164)
+// OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164),
+// iterations [iteration, iteration + iters) of SparseOptimizer::optimize
+// (sparse_optimizer.cpp:380-402): one launch per iteration when the caller
+// polls an abort flag between iterations, else all of a pass's iterations in
+// one launch, so a problem whose trials take longer does not hold the others
+// at every iteration.  The LM state (lambda, ni, chi2, the Raul counter) is
+// the same on every thread (it follows block sums) and stays in registers
+// across the iterations of a launch.
 template <class Rec>
-__global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, LbaLds lay)
+__global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int iters, LbaLds lay)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     __shared__ DScratch sc;
@@ -893,18 +910,35 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
     for (int p = threadIdx.x; p < P.nposes_all; p += kLbaThreads) pz_rot(pz + kPz * p);
     if (iteration == 0) point_order(P);
     __syncthreads();
+    // the LM state carried from iteration to iteration of this launch, in
+    // LDS: kept in registers across the iteration loop it spilled the Schur
+    // pass (every thread computes the same values; thread 0 stores them)
+    __shared__ double s_lm[3];   // lambda, ni, currentChi
+    __shared__ int s_it[4];      // nBad, status, iterations done, trials
+    if (threadIdx.x == 0) {
+        s_lm[0] = P.lambda;
+        s_lm[1] = P.ni;
+        s_lm[2] = P.current_chi;
+        s_it[0] = P.nBad;
+        s_it[1] = kRunning;
+        s_it[2] = 0;
+        s_it[3] = 0;
+    }
+    __syncthreads();
+    for (int it = iteration; it < iteration + iters && s_it[1] == kRunning; it++) {
+    double lambda = s_lm[0], ni = s_lm[1], currentChi = s_lm[2];
+    int nBad = s_it[0];
     LBA_T0();
     // computeActiveErrors at the start of the iteration: after the first
     // iteration the state is the previous iteration's accepted trial state,
     // whose errors (P.err) and robust chi2 that trial computed, bit for bit
-    double currentChi = iteration == 0 ? compute_errors<Rec>(P, pz, sc) : P.current_chi;
+    if (it == 0) currentChi = compute_errors<Rec>(P, pz, sc);
     const double iniChi = currentChi;
-    if (iteration == 0 && threadIdx.x == 0) P.chi2_initial = currentChi;
+    if (it == 0 && threadIdx.x == 0) P.chi2_initial = currentChi;
     LBA_MARK(6);
     linearize<Rec>(P, pz, sc);
     LBA_MARK(7);
-    double lambda = P.lambda, ni = P.ni;
-    if (iteration == 0) {
+    if (it == 0) {
         double m = 0;
         for (int item = threadIdx.x; item < P.nP * 6; item += kLbaThreads)
             m = fmax(m, fabs(P.hp[27 * (item / 6) + up6(item % 6, item % 6)]));
@@ -913,7 +947,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         m = block_max_d(m, sc);
         lambda = 1e-5 * m;
         ni = 2;
-        if (threadIdx.x == 0) P.nBad = 0;
+        nBad = 0;
     }
     double rho = 0;
     int qmax = 0;
@@ -998,6 +1032,25 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         __syncthreads();
         qmax++;
     } while (rho < 0 && qmax < 10 && !P.abort);
+    int status = kRunning;
+    if (qmax == 10 || rho == 0) {
+        status = kTerminated;
+    } else {
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+        else nBad = 0;
+        if (nBad >= 3) status = kTerminated;
+    }
+    if (threadIdx.x == 0) {
+        s_lm[0] = lambda;
+        s_lm[1] = ni;
+        s_lm[2] = currentChi;
+        s_it[0] = nBad;
+        s_it[1] = status;
+        s_it[2]++;
+        s_it[3] += qmax;
+    }
+    __syncthreads();
+    }
     // the free poses back to global memory (the next launch and the outlier
     // pass read them there)
     for (int i = threadIdx.x; i < P.nP * 7; i += kLbaThreads) {
@@ -1005,21 +1058,14 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         P.pose[7 * P.iv_pose[p] + k] = pz[kPz * P.iv_pose[p] + k];
     }
     if (threadIdx.x == 0) {
-        P.lambda = lambda;
-        P.ni = ni;
-        P.trials += qmax;
-        P.iterations++;
-        P.last_chi = currentChi;
-        P.current_chi = currentChi;
-        int status = kRunning;
-        if (qmax == 10 || rho == 0) {
-            status = kTerminated;
-        } else {
-            if ((iniChi - currentChi) * 1e3 < iniChi) P.nBad++;
-            else P.nBad = 0;
-            if (P.nBad >= 3) status = kTerminated;
-        }
-        P.status = status;
+        P.lambda = s_lm[0];
+        P.ni = s_lm[1];
+        P.trials += s_it[3];
+        P.iterations += s_it[2];
+        P.last_chi = s_lm[2];
+        P.current_chi = s_lm[2];
+        P.nBad = s_it[0];
+        P.status = s_it[1];
     }
 }
 
@@ -1662,10 +1708,11 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
 
 // Queues both optimize() passes of a staged batch on the context stream:
 // k_lba_build, iterations, outliers, k_lba_rebuild, iterations, outliers.
-// With abort flags (per problem, entries may be null) the host polls them
-// (and the problems' status) between iterations, which synchronises; an
-// aborted problem's later iterations return at once (g2o's force-stop flag,
-// sparse_optimizer.cpp:394-396); without flags nothing waits.
+// With abort flags (per problem, entries may be null) each iteration is a
+// launch and the host polls the flags (and the problems' status) between
+// them, which synchronises; an aborted problem's later iterations return at
+// once (g2o's force-stop flag, sparse_optimizer.cpp:394-396).  Without flags
+// each pass is one launch of all its iterations and nothing waits.
 template <class Rec>
 static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
                         const volatile uint8_t* const* aborts)
@@ -1715,14 +1762,16 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
                 if (all) break;
             }
             timer_begin(ctx, "lba_iter");
-            hipLaunchKernelGGL(k_lba_iteration<Rec>, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, L.lay);
+            // without abort flags a pass's iterations run in one launch
+            const int n_it = polled ? 1 : iters;
+            hipLaunchKernelGGL(k_lba_iteration<Rec>, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
             timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
             // With an abort flag the host polls it between iterations (where
             // g2o polls its force-stop flag), which needs the device state;
-            // without one, iterations are queued back to back and a
-            // terminated problem's later launches return immediately.
-            if (polled) {
+            // without one, the launch above ran the whole pass.
+            if (!polled) break;
+            {
                 ORBX_HIP_CHECK(hipMemcpyAsync(hv.data(), dd, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
                 ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
                 bool running = false;
