@@ -646,9 +646,10 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
  * aborts: NULL, or P flags (entries may be NULL), each polled between LM
  * iterations like orbx_lba_solve's: problem i stops its optimize() calls
  * when *aborts[i] is set (its own LocalMapping's mbAbortBA,
- * src/LocalMapping.cc:83, :125), the others continue.  Polling makes the
- * call wait for each iteration; without flags the iterations are queued
- * back to back. */
+ * src/LocalMapping.cc:83, :125), the others continue.  With flags each
+ * iteration is a launch and the call waits for it to poll; without flags
+ * each optimize() pass is one launch of all its iterations and nothing
+ * waits.  Results are the same bits either way. */
 int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems,
                          int iters0, int iters1, const volatile uint8_t* const* aborts,
                          uint8_t* const* edge_status, uint8_t* const* point_bad,
