@@ -231,7 +231,9 @@ class Context:
                                             th_low, nnratio, int(check_ori)), "orbx_dev_extract_match")
 
     def set_split(self, enable):
-        """Two concurrent half-batch streams for large extraction batches."""
+        """Extraction pipeline parts for a batch (orbx_dev_set_split): 0 one
+        stream, 1 the default three parts, 2-4 that many parts on their own
+        streams."""
         _check(lib().orbx_dev_set_split(self._h, int(enable)), "orbx_dev_set_split")
 
     def set_fp_contract(self, enable):
