@@ -1,0 +1,178 @@
+"""An independent restatement of ORBmatcher::SearchForInitialization (B3,
+src/ORBmatcher.cc:598-713) with the Frame grid it reads (B2: Frame::
+PosInGrid / GetFeaturesInArea, src/Frame.cc:199-276; 64 x 48 cells) and
+DescriptorDistance (B1), written from the reference's code paths in numpy
+/ Python and compared with the oracle's restatement (oracle/ref_match.cpp)
+on consecutive frames of the bench sequence.
+
+Per F1 keypoint at level 0: the candidates are the grid cells' keypoints
+(cells ix-major, iy-minor, each cell in keypoint order) at level 0 within
+|dx| <= r and |dy| <= r (float abs) of its previous
+match; candidates whose best distance so far (vMatchedDistance) is <= the
+distance drop out; best = the first minimum, second = the second smallest of
+the multiset; accept at best <= 50 and best < 0.9 second, stealing the F2
+keypoint from an earlier F1 keypoint; then the rotation histogram (30 bins,
+bin = round(rot / 30) as the reference writes it) keeps the three largest
+bins (ComputeThreeMaxima's 10 % rule).  All float steps in float32.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth
+from oracle_lib import RefExtractor, load, ptr
+
+F32 = np.float32
+COLS, ROWS = 64, 48          # FRAME_GRID_COLS / ROWS (include/Frame.h)
+TH_LOW, HISTO = 50, 30       # ORBmatcher::TH_LOW, HISTO_LENGTH (src/ORBmatcher.cc:41-42)
+
+
+def popcount8():
+    return np.array([bin(i).count("1") for i in range(256)], np.int64)
+
+
+POP = popcount8()
+
+
+def hamming(a, B):
+    return POP[np.bitwise_xor(a[None, :], B)].sum(axis=1)
+
+
+class Grid:
+    """Frame's grid over keys_un (no distortion: bounds 0..w, 0..h)."""
+
+    def __init__(self, kps, w, h):
+        self.kps = kps
+        self.minx, self.miny = F32(0), F32(0)
+        self.winv = F32(F32(COLS) / F32(F32(w) - self.minx))
+        self.hinv = F32(F32(ROWS) / F32(F32(h) - self.miny))
+        self.cells = [[[] for _ in range(ROWS)] for _ in range(COLS)]
+
+        def c_round(v):   # C round(): half away from zero
+            return int(np.floor(v + 0.5)) if v >= 0 else -int(np.floor(-v + 0.5))
+
+        for i, k in enumerate(kps):
+            px = c_round(F32(F32(k["x"] - self.minx) * self.winv))
+            py = c_round(F32(F32(k["y"] - self.miny) * self.hinv))
+            if 0 <= px < COLS and 0 <= py < ROWS:
+                self.cells[px][py].append(i)
+
+    def area(self, x, y, r, level):
+        x, y, r = F32(x), F32(y), F32(r)
+        x0 = max(0, int(np.floor(F32(F32(F32(x - self.minx) - r) * self.winv))))
+        if x0 >= COLS:
+            return []
+        x1 = min(COLS - 1, int(np.ceil(F32(F32(F32(x - self.minx) + r) * self.winv))))
+        if x1 < 0:
+            return []
+        y0 = max(0, int(np.floor(F32(F32(F32(y - self.miny) - r) * self.hinv))))
+        if y0 >= ROWS:
+            return []
+        y1 = min(ROWS - 1, int(np.ceil(F32(F32(F32(y - self.miny) + r) * self.hinv))))
+        if y1 < 0:
+            return []
+        out = []
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                for j in self.cells[ix][iy]:
+                    k = self.kps[j]
+                    if k["octave"] != level:
+                        continue
+                    if abs(F32(k["x"] - x)) > r or abs(F32(k["y"] - y)) > r:
+                        continue
+                    out.append(j)
+        return out
+
+
+def three_maxima(hist):
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for i, h in enumerate(hist):
+        s = len(h)
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, i
+        elif s > m3:
+            m3, i3 = s, i
+    if m2 < F32(0.1) * F32(m1):
+        i2 = i3 = -1
+    elif m3 < F32(0.1) * F32(m1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def search_for_initialization(k1, d1, k2, d2, prev, w, h, window=100, nnratio=0.9):
+    g2 = Grid(k2, w, h)
+    int_max = 2147483647
+    m12 = np.full(len(k1), -1, np.int64)
+    m21 = np.full(len(k2), -1, np.int64)
+    mdist = np.full(len(k2), int_max, np.int64)
+    hist = [[] for _ in range(HISTO)]
+    factor = F32(F32(1.0) / F32(HISTO))
+    n = 0
+    for i1 in range(len(k1)):
+        if k1["octave"][i1] > 0:
+            continue
+        cand = g2.area(prev[i1, 0], prev[i1, 1], window, 0)
+        if not cand:
+            continue
+        cand = np.array(cand, np.int64)
+        dist = hamming(d1[i1], d2[cand])
+        live = mdist[cand] > dist
+        cand, dist = cand[live], dist[live]
+        if len(dist) == 0:
+            continue
+        b = int(np.argmin(dist))          # the first minimum
+        best, idx = int(dist[b]), int(cand[b])
+        best2 = int(np.sort(dist)[1]) if len(dist) > 1 else int_max
+        if best <= TH_LOW and F32(best) < F32(F32(best2) * F32(nnratio)):
+            if m21[idx] >= 0:
+                m12[m21[idx]] = -1
+                n -= 1
+            m12[i1] = idx
+            m21[idx] = i1
+            mdist[idx] = best
+            n += 1
+            rot = F32(k1["angle"][i1] - k2["angle"][idx])
+            if rot < 0:
+                rot = F32(rot + F32(360.0))
+            bn = int(np.floor(F32(rot * factor) + 0.5))   # round(), rot >= 0
+            if bn == HISTO:
+                bn = 0
+            hist[bn].append(i1)
+    a, b_, c = three_maxima(hist)
+    for i in range(HISTO):
+        if i in (a, b_, c):
+            continue
+        for i1 in hist[i]:
+            if m12[i1] >= 0:
+                m12[i1] = -1
+                n -= 1
+    prev = prev.copy()
+    for i1 in range(len(k1)):
+        if m12[i1] >= 0:
+            prev[i1] = (k2["x"][m12[i1]], k2["y"][m12[i1]])
+    return m12, n, prev
+
+
+@pytest.mark.parametrize("w,h,nf,pair", [(640, 480, 1000, 0), (640, 480, 1000, 7), (320, 240, 500, 3)])
+def test_search_for_initialization_matches_oracle(w, h, nf, pair):
+    frames = synth.sequence(w, h, pair + 2, seed=2000)
+    ex = RefExtractor(nf)
+    k1, d1 = ex(frames[pair])
+    k2, d2 = ex(frames[pair + 1])
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(F32)
+    m_np, n_np, prev_np = search_for_initialization(k1, d1, k2, d2, prev, w, h)
+    L = load()
+    F1, F2 = ox.frame_view(k1, d1, w, h), ox.frame_view(k2, d2, w, h)
+    pm = prev.copy()
+    mm = np.zeros(len(k1), np.int32)
+    c = ctypes.c_int()
+    assert L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), ptr(pm), ptr(mm), 100,
+                                                0.9, 1, ctypes.byref(c)) == 0
+    assert n_np == c.value and n_np > 20
+    assert np.array_equal(m_np, mm.astype(np.int64))
+    assert np.array_equal(prev_np, pm)
