@@ -1,5 +1,6 @@
-"""An independent restatement of ORBmatcher::SearchForInitialization (B3,
-src/ORBmatcher.cc:598-713) with the Frame grid it reads (B2: Frame::
+"""Independent restatements of ORBmatcher::SearchForInitialization (B3,
+src/ORBmatcher.cc:598-713) and WindowSearch (B4, :409-516) with the Frame
+grid they read (B2: Frame::
 PosInGrid / GetFeaturesInArea, src/Frame.cc:199-276; 64 x 48 cells) and
 DescriptorDistance (B1), written from the reference's code paths in numpy
 / Python and compared with the oracle's restatement (oracle/ref_match.cpp)
@@ -176,3 +177,74 @@ def test_search_for_initialization_matches_oracle(w, h, nf, pair):
     assert n_np == c.value and n_np > 20
     assert np.array_equal(m_np, mm.astype(np.int64))
     assert np.array_equal(prev_np, pm)
+
+
+def window_search(k1, d1, k2, d2, f1_mp, w, h, window, min_level, max_level, nnratio, check_ori):
+    """ORBmatcher::WindowSearch (src/ORBmatcher.cc:409-516): F1 keypoints with
+    a map point, at their own level within the level range, against F2's
+    unmatched keypoints in the window; accept at best <= 0.9 second (<=, in
+    float) and best <= TH_HIGH; the rotation histogram holds F2 indices."""
+    g2 = Grid(k2, w, h)
+    int_max = 2147483647
+    matched2 = np.zeros(len(k2), bool)
+    m21 = np.full(len(k2), -1, np.int64)
+    hist = [[] for _ in range(HISTO)]
+    factor = F32(F32(1.0) / F32(HISTO))
+    bmin, bmax = min_level > 0, max_level < int_max
+    n = 0
+    for i1 in range(len(k1)):
+        if not f1_mp[i1]:
+            continue
+        level = int(k1["octave"][i1])
+        if (bmin and level < min_level) or (bmax and level > max_level):
+            continue
+        cand = g2.area(k1["x"][i1], k1["y"][i1], window, level)
+        cand = np.array([c for c in cand if not matched2[c]], np.int64)
+        if len(cand) == 0:
+            continue
+        dist = hamming(d1[i1], d2[cand])
+        b = int(np.argmin(dist))
+        best, idx = int(dist[b]), int(cand[b])
+        best2 = int(np.sort(dist)[1]) if len(dist) > 1 else int_max
+        if F32(best) <= F32(F32(best2) * F32(nnratio)) and best <= 100:   # TH_HIGH
+            matched2[idx] = True
+            m21[idx] = i1
+            n += 1
+            rot = F32(k1["angle"][i1] - k2["angle"][idx])
+            if rot < 0:
+                rot = F32(rot + F32(360.0))
+            bn = int(np.floor(F32(rot * factor) + 0.5))
+            if bn == HISTO:
+                bn = 0
+            hist[bn].append(idx)
+    if check_ori:
+        a, b_, c = three_maxima(hist)
+        for i in range(HISTO):
+            if i in (a, b_, c):
+                continue
+            for idx in hist[i]:
+                matched2[idx] = False
+                m21[idx] = -1
+                n -= 1
+    return m21, n
+
+
+@pytest.mark.parametrize("levels,nnratio,check_ori", [((0, -1), 0.9, 1), ((1, 3), 0.8, 1), ((0, -1), 0.9, 0)])
+def test_window_search_matches_oracle(levels, nnratio, check_ori):
+    w, h, nf = 640, 480, 1000
+    frames = synth.sequence(w, h, 3, seed=2000)
+    ex = RefExtractor(nf)
+    k1, d1 = ex(frames[1])
+    k2, d2 = ex(frames[2])
+    f1_mp = (np.random.default_rng(5).random(len(k1)) < 0.8).astype(np.uint8)
+    lo, hi = levels
+    m_np, n_np = window_search(k1, d1, k2, d2, f1_mp, w, h, 100, lo, 2147483647 if hi < 0 else hi, nnratio,
+                               check_ori)
+    L = load()
+    F1, F2 = ox.frame_view(k1, d1, w, h), ox.frame_view(k2, d2, w, h)
+    m21 = np.zeros(len(k2), np.int32)
+    c = ctypes.c_int()
+    assert L.orbx_ref_window_search(ctypes.byref(F1), ctypes.byref(F2), ptr(f1_mp), 100, lo, hi, F32(nnratio),
+                                    check_ori, ptr(m21), ctypes.byref(c)) == 0
+    assert n_np == c.value and n_np > 20
+    assert np.array_equal(m_np, m21.astype(np.int64))
