@@ -1,10 +1,10 @@
 """Independent restatements of ORBmatcher::SearchForInitialization (B3,
 src/ORBmatcher.cc:598-713) and WindowSearch (B4, :409-516) with the Frame
-grid they read (B2: Frame::
-PosInGrid / GetFeaturesInArea, src/Frame.cc:199-276; 64 x 48 cells) and
-DescriptorDistance (B1), written from the reference's code paths in numpy
-/ Python and compared with the oracle's restatement (oracle/ref_match.cpp)
-on consecutive frames of the bench sequence.
+grid they read (B2: Frame::PosInGrid / GetFeaturesInArea, src/Frame.cc:
+199-276; 64 x 48 cells) and DescriptorDistance (B1), written from the
+reference's code paths in numpy / Python and compared with the oracle's
+restatement (oracle/ref_match.cpp) on consecutive frames of the bench
+sequence.
 
 Per F1 keypoint at level 0: the candidates are the grid cells' keypoints
 (cells ix-major, iy-minor, each cell in keypoint order) at level 0 within
