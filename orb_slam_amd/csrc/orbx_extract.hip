@@ -726,11 +726,13 @@ constexpr int kDiagRepeat[4] = {ORBX_DIAG_REPEAT};
 // kThreads: 256 for cells up to 208-byte rows; the wide tiles of large
 // frames (1920x1080: 336-byte rows, 75 KB of LDS, two workgroups per CU)
 // get more waves per workgroup instead.
-// kChunk (whole-cell instances only): each workgroup takes `chunk`
-// consecutive cells of its frame with two tile buffers; the next cell's tile
-// is copied HBM -> LDS by global_load_lds (no VGPR staging) while the current
-// cell is scored, so its load latency hides behind the compass and scoring
-// work instead of stalling the workgroup at the start of every cell.
+// kChunk (whole-cell instances only; orbx_dev_set_fast_chunk, measured
+// slower than one cell per workgroup): each workgroup
+// takes `chunk` consecutive cells of its frame with two tile buffers; the
+// next cell's tile is copied HBM -> LDS by global_load_lds (no VGPR staging)
+// before the current cell is scored.  The compiler waits for that copy at the
+// scoring's first LDS atomic (the `nz` bits), so the copy overlaps only the
+// compass work before the first survivor batch.
 template <int kP, int kThreads = 256, bool kBanded = false, bool kChunk = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
     ExtractArgs a, int tile_bytes, int band_rows, int chunk)
@@ -1181,7 +1183,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
             const int k = cell - c0;
             // this cell's tile landed (the barrier waits for the copies), S'
             // and nz are clear, and the previous cell is done with the other
-            // buffer; the next cell's copy then runs under this cell's scoring
+            // buffer; the next cell's copy is issued before this cell's scoring
             __syncthreads();
             if (cell + 1 < c1) prefetch(cell + 1, smem + ((k + 1) & 1) * tile_bytes);
             process(cell, smem + (k & 1) * tile_bytes, sm, true);
