@@ -1183,10 +1183,64 @@ __device__ __forceinline__ void lba_offsets(int* ptr, int n, BlockScratchN<kLbaW
     __syncthreads();
 }
 
+// The edges of each free pose in edge order, as a stable counting scatter:
+// the block walks the edges in chunks of kLbaThreads; in each chunk every
+// wave ranks its lanes among the lanes of the same pose block (one ballot per
+// distinct pose block of the wave) and stores its per-pose counts, then a
+// prefix over the waves (in wave order) and the running per-pose base give
+// each edge its place.  counts != nullptr: only count (the totals land in
+// counts[q]); else write pe_idx[ptr[q] + place] = (point-major record, point).
+constexpr int kBuildPoses = 128;   // free poses the LDS tables hold (else the per-pose scan)
+constexpr int kBuildPoints = 8192; // active points whose counts / cursors k_lba_build keeps in LDS
+
+__device__ __forceinline__ void pose_chunks(const LbaDev& A, const int* ph, int nP, int (*wcnt)[kBuildPoses],
+                                            int* base, int* ptr, const int* pos, int2* pe_idx)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, E = A.nedges_all;
+    const bool count_only = pe_idx == nullptr;
+    for (int q = tid; q < nP; q += kLbaThreads) base[q] = 0;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int a0 = 0; a0 < E; a0 += kLbaThreads) {
+        for (int q = lane; q < nP; q += 64) wcnt[wv][q] = 0;
+        __syncthreads();
+        const int a = a0 + tid;
+        const int q = a < E ? ph[A.r_edge_pose[a]] : -1;
+        int rank = 0;
+        uint64_t act = __builtin_amdgcn_ballot_w64(q >= 0);
+        while (act) {
+            const int lead = (int)__builtin_ctzll(act);
+            const int qq = __builtin_amdgcn_readlane(q, lead);
+            const uint64_t m = __builtin_amdgcn_ballot_w64(q == qq);
+            if (q == qq) rank = (int)__popcll(m & lt);
+            if (lane == lead) wcnt[wv][qq] = (int)__popcll(m);
+            act &= ~m;
+        }
+        __syncthreads();
+        for (int qq = tid; qq < nP; qq += kLbaThreads) {   // wave-order prefix per pose
+            int sum = base[qq];
+#pragma unroll
+            for (int w = 0; w < kLbaWaves; w++) {
+                const int c = wcnt[w][qq];
+                wcnt[w][qq] = sum;
+                sum += c;
+            }
+            base[qq] = sum;
+        }
+        __syncthreads();
+        if (!count_only && q >= 0) pe_idx[ptr[q] + wcnt[wv][q] + rank] = make_int2(pos[a], A.r_edge_point[a]);
+    }
+    __syncthreads();
+    if (count_only)
+        for (int qq = tid; qq < nP; qq += kLbaThreads) ptr[qq] = base[qq];
+    __syncthreads();
+}
+
 template <class Rec>
 __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
 {
     __shared__ BlockScratchN<kLbaWaves> bs;
+    __shared__ int s_wcnt[kLbaWaves][kBuildPoses], s_base[kBuildPoses];
+    __shared__ int s_pt[kBuildPoints];   // per active point: edge counts, then list cursors
     LbaDev& A = probs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int NP = A.nposes_all, NL = A.npoints_all, E = A.nedges_all;
@@ -1196,6 +1250,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     int* lh = ph + NP;           // [NL] point block or -1
     int* cur = lh + NL;          // [NL] list cursors
     int* pos = cur + NL;         // [E] point-major position of each edge
+    LBA_T0();
     for (int i = tid; i < NP; i += kLbaThreads) pflag[i] = 0;
     for (int i = tid; i < NL; i += kLbaThreads) lflag[i] = 0;
     __syncthreads();
@@ -1205,9 +1260,11 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         lflag[A.r_edge_point[a]] = 1;
     }
     __syncthreads();
+    LBA_MARK(9);
     int nP, nL;
     lba_rank(A.r_pose_id, pflag, NP, ph, &nP, bs);
     lba_rank(A.r_point_id, lflag, NL, lh, &nL, bs);
+    LBA_MARK(10);
     int* iv_pose = const_cast<int*>(A.iv_pose);
     int* iv_point = const_cast<int*>(A.iv_point);
     for (int i = tid; i < NP; i += kLbaThreads)
@@ -1219,20 +1276,40 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     for (int i = tid; i <= nP; i += kLbaThreads) pe_ptr[i] = 0;
     for (int i = tid; i <= nL; i += kLbaThreads) le_ptr[i] = 0;
     __syncthreads();
+    // the free poses' edge counts come from the chunked pass below when the
+    // batch's free poses fit its LDS tables (kBuildPoses), else from atomics
+    const bool chunked = nP <= kBuildPoses;
+    if (chunked) pose_chunks(A, ph, nP, s_wcnt, s_base, pe_ptr + 1, nullptr, nullptr);
+    // the points' edge counts and list cursors in LDS when they fit
+    const bool pts_lds = nL <= kBuildPoints;
+    if (pts_lds) {
+        for (int l = tid; l < nL; l += kLbaThreads) s_pt[l] = 0;
+        __syncthreads();
+    }
     for (int a = tid; a < E; a += kLbaThreads) {
-        const int eph = ph[A.r_edge_pose[a]];
-        if (eph >= 0) atomicAdd(&pe_ptr[eph + 1], 1);
-        atomicAdd(&le_ptr[lh[A.r_edge_point[a]] + 1], 1);
+        if (!chunked) {
+            const int eph = ph[A.r_edge_pose[a]];
+            if (eph >= 0) atomicAdd(&pe_ptr[eph + 1], 1);
+        }
+        const int l = lh[A.r_edge_point[a]];
+        if (pts_lds) atomicAdd(&s_pt[l], 1);
+        else atomicAdd(&le_ptr[l + 1], 1);
     }
     __syncthreads();
+    if (pts_lds)
+        for (int l = tid; l < nL; l += kLbaThreads) le_ptr[l + 1] = s_pt[l];
+    __syncthreads();
+    LBA_MARK(11);
     lba_offsets(pe_ptr, nP, bs);
     lba_offsets(le_ptr, nL, bs);
     // point-major slots, then each point's edges put in edge order (few)
     int* e_orig = const_cast<int*>(A.e_orig);
-    for (int l = tid; l < nL; l += kLbaThreads) cur[l] = le_ptr[l];
+    int* cursor = pts_lds ? s_pt : cur;
+    for (int l = tid; l < nL; l += kLbaThreads) cursor[l] = le_ptr[l];
     __syncthreads();
-    for (int a = tid; a < E; a += kLbaThreads) e_orig[atomicAdd(&cur[lh[A.r_edge_point[a]]], 1)] = a;
+    for (int a = tid; a < E; a += kLbaThreads) e_orig[atomicAdd(&cursor[lh[A.r_edge_point[a]]], 1)] = a;
     __syncthreads();
+    LBA_MARK(12);
     for (int l = tid; l < nL; l += kLbaThreads) {
         const int q0 = le_ptr[l], q1 = le_ptr[l + 1];
         for (int i = q0 + 1; i < q1; i++) {   // insertion sort by edge index
@@ -1246,6 +1323,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         }
     }
     __syncthreads();
+    LBA_MARK(13);
     // the records (float fields only when the host found every value exact)
     Rec* rec = reinterpret_cast<Rec*>(const_cast<void*>(A.rec));
     for (int j = tid; j < E; j += kLbaThreads) {
@@ -1261,8 +1339,12 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         pos[a] = j;
     }
     __syncthreads();
-    // per free pose, its edges in edge order (wave per pose, ballot compaction)
+    LBA_MARK(14);
+    // per free pose, its edges in edge order: the chunked stable scatter, or
+    // (more free poses than its tables) a wave per pose with ballot compaction
     int2* pe_idx = const_cast<int2*>(A.pe_idx);
+    if (chunked) pose_chunks(A, ph, nP, s_wcnt, s_base, pe_ptr, pos, pe_idx);
+    else
     for (int p1 = wv; p1 < nP; p1 += kLbaWaves) {
         const int pose = iv_pose[p1];
         int w = pe_ptr[p1];
@@ -1275,6 +1357,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
             w += __popcll(bal);
         }
     }
+    LBA_MARK(15);
     if (tid == 0) {
         A.nP = nP;
         A.nL = nL;

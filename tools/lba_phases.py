@@ -35,4 +35,10 @@ names = {6: "errors (first iteration)", 7: "linearize", 1: "S init", 2: "Schur c
 tot = sum(d[k] for k in names)
 for k, nm in names.items():
     print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / max(tot, 1):5.1f} %)")
+# k_lba_build (the first optimize() call's structures), block 0
+build = {9: "build: flags", 10: "build: rank ids", 11: "build: count atomics", 12: "build: offsets + scatter",
+         13: "build: per-point sort", 14: "build: records", 15: "build: per-pose lists"}
+btot = sum(d[k] for k in build)
+for k, nm in build.items():
+    print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / max(btot, 1):5.1f} % of the build)")
 print("iterations", list(st[0].iterations), "trials", list(st[0].levenberg_trials), "n_edges", cps[0][0].n_edges)
