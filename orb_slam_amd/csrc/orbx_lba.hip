@@ -885,7 +885,7 @@ struct LbaLds {
 // at every iteration.  The LM state (lambda, ni, chi2, the Raul counter) is
 // the same on every thread (it follows block sums) and stays in registers
 // across the iterations of a launch.
-template <class Rec>
+template <class Rec, bool kLds>
 __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, int iteration, int iters, LbaLds lay)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -897,7 +897,6 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         return;
     }
     const int n = P.dim_p;
-    const bool in_lds = lba_sys_doubles(n) <= lay.s_doubles;
     double* pz = lds + lay.pz_off;
     double* pbk = lds + lay.pbk_off;
     double* xp = lds + lay.xp_off;
@@ -959,8 +958,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
             pbk[i] = pz[kPz * P.iv_pose[p] + k];
         }
         __syncthreads();
-        const bool ok2 = in_lds ? trial_solve<Rec, true>(P, lds, pz, xp, lambda)
-                                : trial_solve<Rec, false>(P, lds, pz, xp, lambda);
+        const bool ok2 = trial_solve<Rec, kLds>(P, lds, pz, xp, lambda);
         if (ok2)
             for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) {
                 double* z = pz + kPz * P.iv_pose[p];
@@ -1810,6 +1808,8 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
     ORBX_HIP_CHECK(hipGetLastError());
     // one layout for both passes: the second pass's systems are no larger
     const size_t lds = L.lds_bytes;
+    // the reduced systems in LDS (when the batch's largest fits) or in global memory
+    auto kern = L.lay.s_doubles > 0 ? k_lba_iteration<Rec, true> : k_lba_iteration<Rec, false>;
     bool polled = false;
     for (int i = 0; aborts && i < P; i++) polled |= aborts[i] != nullptr;
     std::vector<LbaDev> hv(polled ? P : 0);
@@ -1847,7 +1847,7 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             timer_begin(ctx, "lba_iter");
             // without abort flags a pass's iterations run in one launch
             const int n_it = polled ? 1 : iters;
-            hipLaunchKernelGGL(k_lba_iteration<Rec>, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
+            hipLaunchKernelGGL(kern, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
             timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
             // With an abort flag the host polls it between iterations (where
