@@ -1,0 +1,215 @@
+"""Independent numpy restatements of ORBmatcher's motion-model and frame-pair
+projection searches (B5 SearchByProjection(Frame&, const Frame&, float),
+src/ORBmatcher.cc:1507-1620; B7 SearchByProjection(Frame&, Frame&, int,
+vector<MapPoint*>&), :519-594) with Frame::GetFeaturesInArea's level range
+(src/Frame.cc:199-276), against the oracle's restatement
+(oracle/ref_match.cpp) on consecutive bench-sequence frames.
+
+* projection: x3Dc = Rcw x3Dw + tcw in float32 (products summed left to
+  right, then + t, as the oracle evaluates the cv::Mat expression -- OpenCV
+  2.4's small-matrix gemm order is the one choice shared with the oracle),
+  invzc = (float)(1.0 / zc), u = fx xc invzc + cx in float32;
+* B5: map points of the last frame that are not outliers; the current
+  frame's image bounds; radius th * mvScaleFactors[octave] (the float table
+  ORBextractor builds from its double scaleFactor); candidates at octaves
+  octave - 1 .. octave + 1 that hold no map point yet (including those taken
+  earlier in this call); the first minimum distance, kept at <= TH_HIGH; the
+  rotation histogram's three maxima (HISTO_LENGTH 30, bin = round(rot / 30));
+* B7: F1's map points, F2's candidates at F1's octave within the window that
+  hold no map point; best / second distance, accept at best <= 0.9 second (in
+  float) and best <= TH_HIGH; no rotation check.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth
+from oracle_lib import RefExtractor, load, ptr
+from test_match_numpy import COLS, HISTO, ROWS, Grid, hamming, three_maxima
+
+F32 = np.float32
+W, H = 640, 480
+CAM = np.array([500.0, 500.0, 320.0, 240.0], np.float32)
+TH_HIGH = 100
+
+
+def scale_factors(nlevels=8, scale=1.2):
+    sf = float(F32(scale))        # ORBextractor::scaleFactor is a double holding the float argument
+    s = [F32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(F32(float(s[-1]) * sf))
+    return s
+
+
+def area_levels(g, x, y, r, min_level, max_level):
+    """GetFeaturesInArea with its level test (-1 / -1: any level; equal: that level)."""
+    x, y, r = F32(x), F32(y), F32(r)
+    x0 = max(0, int(np.floor(F32(F32(F32(x - g.minx) - r) * g.winv))))
+    if x0 >= COLS:
+        return []
+    x1 = min(COLS - 1, int(np.ceil(F32(F32(F32(x - g.minx) + r) * g.winv))))
+    if x1 < 0:
+        return []
+    y0 = max(0, int(np.floor(F32(F32(F32(y - g.miny) - r) * g.hinv))))
+    if y0 >= ROWS:
+        return []
+    y1 = min(ROWS - 1, int(np.ceil(F32(F32(F32(y - g.miny) + r) * g.hinv))))
+    if y1 < 0:
+        return []
+    check = not (min_level == -1 and max_level == -1)
+    same = check and min_level == max_level
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for j in g.cells[ix][iy]:
+                k = g.kps[j]
+                if check and not same and (k["octave"] < min_level or k["octave"] > max_level):
+                    continue
+                if same and k["octave"] != min_level:
+                    continue
+                if abs(F32(k["x"] - x)) > r or abs(F32(k["y"] - y)) > r:
+                    continue
+                out.append(j)
+    return out
+
+
+def project(T, X):
+    T = T.reshape(3, 4)
+    xc = [F32(F32(F32(F32(T[r, 0] * X[0]) + F32(T[r, 1] * X[1])) + F32(T[r, 2] * X[2])) + T[r, 3]) for r in range(3)]
+    inv = F32(1.0 / float(xc[2]))
+    u = F32(F32(F32(CAM[0] * xc[0]) * inv) + CAM[2])
+    v = F32(F32(F32(CAM[1] * xc[1]) * inv) + CAM[3])
+    return u, v
+
+
+def rot_bin(a1, a2):
+    rot = F32(F32(a1) - F32(a2))
+    if rot < 0:
+        rot = F32(rot + F32(360.0))
+    b = int(np.floor(F32(rot * F32(F32(1.0) / F32(HISTO))) + 0.5))
+    return 0 if b == HISTO else b
+
+
+def motion_search(kc, dc, kl, dl, xyz, valid, assigned, T, th, check_ori):
+    g = Grid(kc, W, H)
+    sf = scale_factors()
+    taken = assigned.astype(bool).copy()
+    m = np.full(len(kc), -1, np.int64)
+    hist = [[] for _ in range(HISTO)]
+    n = 0
+    for i in range(len(kl)):
+        if not valid[i]:
+            continue
+        u, v = project(T, xyz[i])
+        if u < 0 or u > W or v < 0 or v > H:
+            continue
+        oct_ = int(kl["octave"][i])
+        cand = [c for c in area_levels(g, u, v, F32(F32(th) * sf[oct_]), oct_ - 1, oct_ + 1) if not taken[c]]
+        if not cand:
+            continue
+        dist = hamming(dl[i], dc[np.array(cand)])
+        b = int(np.argmin(dist))
+        if dist[b] <= TH_HIGH:
+            taken[cand[b]] = True
+            m[cand[b]] = i
+            n += 1
+            if check_ori:
+                hist[rot_bin(kl["angle"][i], kc["angle"][cand[b]])].append(cand[b])
+    if check_ori:
+        keep = three_maxima(hist)
+        for bi in range(HISTO):
+            if bi in keep:
+                continue
+            for c in hist[bi]:
+                m[c] = -1
+                n -= 1
+    return m, n
+
+
+def pair_search(k1, d1, k2, d2, xyz, valid, assigned, T, window, nnratio):
+    g = Grid(k2, W, H)
+    taken = assigned.astype(bool).copy()
+    m = np.full(len(k2), -1, np.int64)
+    n = 0
+    for i in range(len(k1)):
+        if not valid[i]:
+            continue
+        u, v = project(T, xyz[i])
+        lvl = int(k1["octave"][i])
+        cand = [c for c in area_levels(g, u, v, F32(window), lvl, lvl) if not taken[c]]
+        if not cand:
+            continue
+        dist = hamming(d1[i], d2[np.array(cand)])
+        b = int(np.argmin(dist))
+        best2 = int(np.sort(dist)[1]) if len(dist) > 1 else 2147483647
+        if F32(dist[b]) <= F32(F32(best2) * F32(nnratio)) and dist[b] <= TH_HIGH:
+            taken[cand[b]] = True
+            m[cand[b]] = i
+            n += 1
+    return m, n
+
+
+@pytest.fixture(scope="module")
+def feats():
+    frames = synth.sequence(W, H, 3, seed=77)
+    ex = RefExtractor(1000)
+    return [ex(f) for f in frames]
+
+
+def backproject(k, rng):
+    z = rng.uniform(2.0, 6.0, len(k)).astype(np.float32)
+    x = (k["x"] - CAM[2]) / CAM[0] * z
+    y = (k["y"] - CAM[3]) / CAM[1] * z
+    return np.ascontiguousarray(np.stack([x, y, z], 1).astype(np.float32))
+
+
+def pose(tx=-0.008, ty=-0.004, yaw=0.002):
+    c, s = np.cos(yaw), np.sin(yaw)
+    return np.array([[c, 0, s, tx], [0, 1, 0, ty], [-s, 0, c, 0.0]], np.float32).reshape(-1).copy()
+
+
+@pytest.mark.parametrize("th,ori", [(15.0, 1), (7.0, 0), (3.0, 1)])
+def test_motion_search_matches_oracle(feats, th, ori):
+    (kl, dl), (kc, dc) = feats[1], feats[2]
+    rng = np.random.default_rng(int(th))
+    xyz = backproject(kl, rng)
+    valid = (rng.random(len(kl)) < 0.85).astype(np.uint8)
+    assigned = (rng.random(len(kc)) < 0.05).astype(np.uint8)
+    T = pose()
+    m_np, n_np = motion_search(kc, dc, kl, dl, xyz, valid, assigned, T, th, ori)
+    C, Lv = ox.frame_view(kc, dc, W, H), ox.frame_view(kl, dl, W, H)
+    mr = np.zeros(len(kc), np.int32)
+    nr = ctypes.c_int()
+    assert load().orbx_ref_search_by_projection_motion(ctypes.byref(C), ctypes.byref(Lv), ptr(xyz), ptr(valid),
+                                                       ptr(assigned), ptr(T), ptr(CAM), th, ori, ptr(mr),
+                                                       ctypes.byref(nr)) == 0
+    assert n_np == nr.value and n_np > 50
+    assert np.array_equal(m_np, mr.astype(np.int64))
+
+
+@pytest.mark.parametrize("window", [15, 50])
+def test_pair_search_matches_oracle(feats, window):
+    (k1, d1), (k2, d2) = feats[0], feats[1]
+    rng = np.random.default_rng(window)
+    xyz = backproject(k1, rng)
+    valid = (rng.random(len(k1)) < 0.8).astype(np.uint8)
+    assigned = (rng.random(len(k2)) < 0.1).astype(np.uint8)
+    T = pose()
+    m_np, n_np = pair_search(k1, d1, k2, d2, xyz, valid, assigned, T, window, 0.9)
+    F1, F2 = ox.frame_view(k1, d1, W, H), ox.frame_view(k2, d2, W, H)
+    mr = np.zeros(len(k2), np.int32)
+    nr = ctypes.c_int()
+    assert load().orbx_ref_search_by_projection_pair(ctypes.byref(F1), ctypes.byref(F2), ptr(xyz), ptr(valid),
+                                                     ptr(assigned), ptr(T), ptr(CAM), window, 0.9, ptr(mr),
+                                                     ctypes.byref(nr)) == 0
+    assert n_np == nr.value and n_np > 50
+    assert np.array_equal(m_np, mr.astype(np.int64))
+
+
+def test_scale_factors_match_extractor():
+    e = RefExtractor(1000)
+    s, inv = np.zeros(8, np.float32), np.zeros(8, np.float32)
+    assert e.L.orbx_ref_scale_factors(e.h, ptr(s), ptr(inv), 8) == 8
+    assert np.array_equal(np.array(scale_factors(), np.float32), s)
