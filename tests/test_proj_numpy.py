@@ -1,7 +1,9 @@
 """Independent numpy restatements of ORBmatcher's motion-model and frame-pair
 projection searches (B5 SearchByProjection(Frame&, const Frame&, float),
 src/ORBmatcher.cc:1507-1620; B7 SearchByProjection(Frame&, Frame&, int,
-vector<MapPoint*>&), :519-594) with Frame::GetFeaturesInArea's level range
+vector<MapPoint*>&), :519-594; the relocalisation search
+SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int),
+:1622-1746) with Frame::GetFeaturesInArea's level range
 (src/Frame.cc:199-276), against the oracle's restatement
 (oracle/ref_match.cpp) on consecutive bench-sequence frames.
 
@@ -213,3 +215,70 @@ def test_scale_factors_match_extractor():
     s, inv = np.zeros(8, np.float32), np.zeros(8, np.float32)
     assert e.L.orbx_ref_scale_factors(e.h, ptr(s), ptr(inv), 8) == 8
     assert np.array_equal(np.array(scale_factors(), np.float32), s)
+
+
+def frame_kf_search(kf, kf_desc, fk, fd, pos, dmin, valid, assigned, T, th, orb_dist, check_ori):
+    """SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int)
+    (src/ORBmatcher.cc:1622-1746): the KF's map points (valid = not bad and
+    not already found) projected into the frame; predicted level from
+    |X - Ow| / GetMinDistanceInvariance() by lower_bound over the float scale
+    table; radius th * scale; the frame's keypoints at levels pred - 1 ..
+    pred + 1 without a map point; first minimum <= ORBdist; rotation check
+    with the KF keypoint's angle.  Ow = -Rcw^T tcw in float (left to right,
+    the oracle's evaluation of the cv::Mat expression); cv::norm accumulates
+    the squares in double."""
+    g = Grid(fk, W, H)
+    sf = scale_factors()
+    Tm = T.reshape(4, 4)[:3] if T.size == 16 else T.reshape(3, 4)
+    R, t = Tm[:, :3], Tm[:, 3]
+    Ow = [F32(-F32(F32(F32(R[0, c] * t[0]) + F32(R[1, c] * t[1])) + F32(R[2, c] * t[2]))) for c in range(3)]
+    taken = assigned.astype(bool).copy()
+    m = np.full(len(fk), -1, np.int64)
+    hist = [[] for _ in range(HISTO)]
+    n = 0
+    for i in range(len(kf)):
+        if not valid[i]:
+            continue
+        X = pos[i]
+        u, v = project(np.concatenate([Tm[r] for r in range(3)]).astype(np.float32), X)
+        if u < 0 or u > W or v < 0 or v > H:
+            continue
+        PO = [F32(X[c] - Ow[c]) for c in range(3)]
+        dist3 = F32(np.sqrt(sum(float(p) * float(p) for p in PO)))
+        ratio = F32(dist3 / F32(dmin[i]))
+        pred = min(int(np.searchsorted(np.array(sf, np.float32), ratio, side="left")), len(sf) - 1)
+        cand = [c for c in area_levels(g, u, v, F32(F32(th) * sf[pred]), pred - 1, pred + 1) if not taken[c]]
+        if not cand:
+            continue
+        dist = hamming(kf_desc[i], fd[np.array(cand)])
+        b = int(np.argmin(dist))
+        if dist[b] <= orb_dist:
+            taken[cand[b]] = True
+            m[cand[b]] = i
+            n += 1
+            if check_ori:
+                hist[rot_bin(kf["angle"][i], fk["angle"][cand[b]])].append(cand[b])
+    if check_ori:
+        keep = three_maxima(hist)
+        for bi in range(HISTO):
+            if bi in keep:
+                continue
+            for c in hist[bi]:
+                m[c] = -1
+                n -= 1
+    return m, n
+
+
+@pytest.mark.parametrize("seed,th,orb_dist,ori", [(1, 10.0, 100, 1), (2, 5.0, 64, 0)])
+def test_frame_kf_search_matches_oracle(seed, th, orb_dist, ori):
+    import proj_data as pd
+    from test_proj_oracle import ref_proj_frame_kf, seq_case
+    k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
+    valid = (rng.random(len(k1)) < 0.8).astype(np.uint8)
+    assigned = (rng.random(len(k2)) < 0.1).astype(np.uint8)
+    a = mps[1]
+    got, n = frame_kf_search(k1, a["desc"], k2, d2, a["pos"], a["min_dist"], valid, assigned,
+                             np.ascontiguousarray(T2, np.float32), th, orb_dist, ori)
+    want, nw = ref_proj_frame_kf(pd.view(k2, d2), pd.view(k1, d1), mps, valid, assigned, T2, th, orb_dist, ori)
+    assert n == nw and n > 100
+    assert np.array_equal(got, want.astype(np.int64))
