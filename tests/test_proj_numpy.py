@@ -3,7 +3,8 @@ projection searches (B5 SearchByProjection(Frame&, const Frame&, float),
 src/ORBmatcher.cc:1507-1620; B7 SearchByProjection(Frame&, Frame&, int,
 vector<MapPoint*>&), :519-594; the relocalisation search
 SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int),
-:1622-1746) with Frame::GetFeaturesInArea's level range
+:1622-1746; the candidates of both Fuse overloads, :1016-1263) with
+Frame::GetFeaturesInArea's level range
 (src/Frame.cc:199-276), against the oracle's restatement
 (oracle/ref_match.cpp) on consecutive bench-sequence frames.
 
@@ -282,3 +283,70 @@ def test_frame_kf_search_matches_oracle(seed, th, orb_dist, ori):
     want, nw = ref_proj_frame_kf(pd.view(k2, d2), pd.view(k1, d1), mps, valid, assigned, T2, th, orb_dist, ori)
     assert n == nw and n > 100
     assert np.array_equal(got, want.astype(np.int64))
+
+
+def fuse_candidates(k, d, pos, normal, dmin, dmax, mdesc, T, sim3, th):
+    """The state-free part of ORBmatcher::Fuse (KF, vpMapPoints) (src/
+    ORBmatcher.cc:1016-1134) and Fuse (KF, Scw, vpPoints) (:1136-1263) per
+    map point: camera frame (Scw decomposed as scw = sqrt(row0 . row0) in
+    double, Rcw = sRcw / scw and tcw / scw through a double reciprocal),
+    positive depth, 1/z in float (KF overload) or 1.0/z in double (Scw
+    overload), KeyFrame::IsInImage (half-open), the scale-invariance distance
+    range, the 60-degree viewing test PO . Pn >= 0.5 |PO| in double, the
+    predicted level, and the first minimum over the keypoints in the radius
+    whose octave lies in [pred - 1, pred]."""
+    g = Grid(k, W, H)
+    sf = scale_factors()
+    T = T.reshape(4, 4)
+    if sim3:
+        scw = F32(np.sqrt(sum(float(T[0, c]) * float(T[0, c]) for c in range(3))))
+        inv = 1.0 / float(scw)
+        R = np.array([[F32(float(T[r, c]) * inv) for c in range(3)] for r in range(3)], np.float32)
+        t = np.array([F32(float(T[r, 3]) * inv) for r in range(3)], np.float32)
+    else:
+        R, t = T[:3, :3], T[:3, 3]
+    Ow = [F32(-F32(F32(F32(R[0, c] * t[0]) + F32(R[1, c] * t[1])) + F32(R[2, c] * t[2]))) for c in range(3)]
+    n = len(pos)
+    bi = np.full(n, -1, np.int64)
+    bd = np.full(n, 2147483647, np.int64)
+    for m in range(n):
+        X = pos[m]
+        pc = [F32(F32(F32(F32(R[r, 0] * X[0]) + F32(R[r, 1] * X[1])) + F32(R[r, 2] * X[2])) + t[r]) for r in range(3)]
+        if pc[2] < 0:
+            continue
+        invz = F32(1.0 / float(pc[2])) if sim3 else F32(F32(1.0) / pc[2])
+        u = F32(F32(CAM[0] * F32(pc[0] * invz)) + CAM[2])
+        v = F32(F32(CAM[1] * F32(pc[1] * invz)) + CAM[3])
+        if not (0 <= u < W and 0 <= v < H):
+            continue
+        PO = [F32(X[c] - Ow[c]) for c in range(3)]
+        dist3 = F32(np.sqrt(sum(float(p) * float(p) for p in PO)))
+        if dist3 < dmin[m] or dist3 > dmax[m]:
+            continue
+        if sum(float(PO[c]) * float(normal[m, c]) for c in range(3)) < 0.5 * float(dist3):
+            continue
+        pred = min(int(np.searchsorted(np.array(sf, np.float32), F32(dist3 / F32(dmin[m])), side="left")), len(sf) - 1)
+        cand = [c for c in area_levels(g, u, v, F32(F32(th) * sf[pred]), -1, -1)
+                if pred - 1 <= k["octave"][c] <= pred]
+        if not cand:
+            continue
+        dist = hamming(mdesc[m], d[np.array(cand)])
+        b = int(np.argmin(dist))
+        bi[m], bd[m] = cand[b], int(dist[b])
+    return bi, bd
+
+
+@pytest.mark.parametrize("sim3,scale,th", [(0, 1.0, 3.0), (1, 1.5, 3.0), (1, 0.7, 6.0)])
+def test_fuse_candidates_match_oracle(sim3, scale, th):
+    from test_proj_oracle import ref_fuse, seq_case
+    import proj_data as pd
+    k1, d1, k2, d2, T2, mps, rng = seq_case(3)
+    S = np.ascontiguousarray(T2, np.float32).copy()
+    if sim3:
+        S[:3, :] *= np.float32(scale)
+    a = mps[1]
+    got_i, got_d = fuse_candidates(k2, d2, a["pos"], a["normal"], a["min_dist"], a["max_dist"], a["desc"], S, sim3, th)
+    want_i, want_d = ref_fuse(pd.view(k2, d2), mps, S, sim3, th)
+    assert np.count_nonzero(want_i >= 0) > 100
+    assert np.array_equal(got_i, want_i.astype(np.int64))
+    assert np.array_equal(got_d[got_i >= 0], want_d[want_i >= 0].astype(np.int64))
