@@ -3,7 +3,8 @@ projection searches (B5 SearchByProjection(Frame&, const Frame&, float),
 src/ORBmatcher.cc:1507-1620; B7 SearchByProjection(Frame&, Frame&, int,
 vector<MapPoint*>&), :519-594; the relocalisation search
 SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int),
-:1622-1746; the candidates of both Fuse overloads, :1016-1263) with
+:1622-1746; the candidates of both Fuse overloads, :1016-1263;
+SearchBySim3, :1267-1505) with
 Frame::GetFeaturesInArea's level range
 (src/Frame.cc:199-276), against the oracle's restatement
 (oracle/ref_match.cpp) on consecutive bench-sequence frames.
@@ -350,3 +351,74 @@ def test_fuse_candidates_match_oracle(sim3, scale, th):
     assert np.count_nonzero(want_i >= 0) > 100
     assert np.array_equal(got_i, want_i.astype(np.int64))
     assert np.array_equal(got_d[got_i >= 0], want_d[want_i >= 0].astype(np.int64))
+
+
+def search_by_sim3(k1, d1, k2, d2, m1, v1, m2, v2, T1, T2, s12, R12, t12, prior, th):
+    """ORBmatcher::SearchBySim3 (src/ORBmatcher.cc:1267-1505): KF1's map
+    points through R1w, t1w then sR21 = (1.0 / s12) R12^T (double scale),
+    t21 = -sR21 t12 into KF2, and KF2's through R2w, t2w then sR12 = s12 R12
+    into KF1; positive depth, 1.0/z in double, IsInImage, the distance range
+    on |p3Dc| (no viewing test), predicted level, best keypoint in the radius
+    at octaves [pred - 1, pred] with distance <= TH_HIGH; kept when the two
+    directions agree.  prior: -2 no match yet, -1 a match whose point is not
+    in KF2, >= 0 its KF2 index (vbAlreadyMatched1 / 2)."""
+    sf = scale_factors()
+    R12 = R12.reshape(3, 3)
+    sR12 = np.array([[F32(float(s12) * float(R12[r, c])) for c in range(3)] for r in range(3)], np.float32)
+    inv = 1.0 / float(s12)
+    sR21 = np.array([[F32(inv * float(R12[c, r])) for c in range(3)] for r in range(3)], np.float32)
+    t21 = np.array([F32(-F32(F32(F32(sR21[r, 0] * t12[0]) + F32(sR21[r, 1] * t12[1])) + F32(sR21[r, 2] * t12[2])))
+                    for r in range(3)], np.float32)
+    already1 = prior != -2
+    already2 = np.zeros(len(k2), bool)
+    for i in range(len(k1)):
+        if prior[i] >= 0:
+            already2[prior[i]] = True
+
+    def xf(R, t, X):
+        return [F32(F32(F32(F32(R[r, 0] * X[0]) + F32(R[r, 1] * X[1])) + F32(R[r, 2] * X[2])) + t[r]) for r in range(3)]
+
+    grids = {id(k1): Grid(k1, W, H), id(k2): Grid(k2, W, H)}
+
+    def one(kd, dd, mp, i, Rw, tw, sR, tt):
+        pc = xf(sR, tt, np.array(xf(Rw, tw, mp["pos"][i]), np.float32))
+        if pc[2] < 0:
+            return -1
+        invz = F32(1.0 / float(pc[2]))
+        u = F32(F32(CAM[0] * F32(pc[0] * invz)) + CAM[2])
+        v = F32(F32(CAM[1] * F32(pc[1] * invz)) + CAM[3])
+        if not (0 <= u < W and 0 <= v < H):
+            return -1
+        dist3 = F32(np.sqrt(sum(float(p) * float(p) for p in pc)))
+        if dist3 < mp["min_dist"][i] or dist3 > mp["max_dist"][i]:
+            return -1
+        pred = min(int(np.searchsorted(np.array(sf, np.float32), F32(dist3 / F32(mp["min_dist"][i])), side="left")),
+                   len(sf) - 1)
+        cand = [c for c in area_levels(grids[id(kd)], u, v, F32(F32(th) * sf[pred]), -1, -1)
+                if pred - 1 <= kd["octave"][c] <= pred]
+        if not cand:
+            return -1
+        dist = hamming(mp["desc"][i], dd[np.array(cand)])
+        b = int(np.argmin(dist))
+        return cand[b] if dist[b] <= TH_HIGH else -1
+
+    T1, T2 = T1.reshape(4, 4), T2.reshape(4, 4)
+    match1 = [one(k2, d2, m1, i, T1[:3, :3], T1[:3, 3], sR21, t21) if v1[i] and not already1[i] else -1
+              for i in range(len(k1))]
+    match2 = [one(k1, d1, m2, i, T2[:3, :3], T2[:3, 3], sR12, t12) if v2[i] and not already2[i] else -1
+              for i in range(len(k2))]
+    new = np.full(len(k1), -1, np.int64)
+    for i1, i2 in enumerate(match1):
+        if i2 >= 0 and match2[i2] == i1:
+            new[i1] = i2
+    return new, int((new >= 0).sum())
+
+
+@pytest.mark.parametrize("seed,prior_frac,th", [(0, 0.1, 7.5), (2, 0.3, 4.0)])
+def test_search_by_sim3_matches_oracle(seed, prior_frac, th):
+    from test_proj_oracle import ref_sim3, sim3_case
+    K1, K2, m1, v1, m2, v2, T1, T2, s12, R12, t12, prior, (k1, d1, k2, d2) = sim3_case(seed, prior_frac)
+    got, n = search_by_sim3(k1, d1, k2, d2, m1[1], v1, m2[1], v2, T1, T2, s12, R12, t12, prior, th)
+    want, nw = ref_sim3(K1, K2, m1, v1, m2, v2, T1, T2, s12, R12, t12, prior, th)
+    assert n == nw and n > 100
+    assert np.array_equal(got, want.astype(np.int64))
