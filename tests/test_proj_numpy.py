@@ -4,7 +4,8 @@ src/ORBmatcher.cc:1507-1620; B7 SearchByProjection(Frame&, Frame&, int,
 vector<MapPoint*>&), :519-594; the relocalisation search
 SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, float, int),
 :1622-1746; the candidates of both Fuse overloads, :1016-1263;
-SearchBySim3, :1267-1505) with
+SearchBySim3, :1267-1505; SearchByProjection(KeyFrame*, Scw, ...),
+:286-407) with
 Frame::GetFeaturesInArea's level range
 (src/Frame.cc:199-276), against the oracle's restatement
 (oracle/ref_match.cpp) on consecutive bench-sequence frames.
@@ -420,5 +421,69 @@ def test_search_by_sim3_matches_oracle(seed, prior_frac, th):
     K1, K2, m1, v1, m2, v2, T1, T2, s12, R12, t12, prior, (k1, d1, k2, d2) = sim3_case(seed, prior_frac)
     got, n = search_by_sim3(k1, d1, k2, d2, m1[1], v1, m2[1], v2, T1, T2, s12, R12, t12, prior, th)
     want, nw = ref_sim3(K1, K2, m1, v1, m2, v2, T1, T2, s12, R12, t12, prior, th)
+    assert n == nw and n > 100
+    assert np.array_equal(got, want.astype(np.int64))
+
+
+def kf_scw_search(k, d, mp, skip, Scw, th, matched):
+    """SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) (src/
+    ORBmatcher.cc:286-407): Fuse (KF, Scw)'s geometry with 1/z in float,
+    radius th * scale, candidates in the radius at octaves [pred - 1, pred]
+    whose vpMatched entry is empty (including entries set earlier in this
+    call), first minimum <= TH_LOW assigned."""
+    g = Grid(k, W, H)
+    sf = scale_factors()
+    T = Scw.reshape(4, 4)
+    scw = F32(np.sqrt(sum(float(T[0, c]) * float(T[0, c]) for c in range(3))))
+    inv = 1.0 / float(scw)
+    R = np.array([[F32(float(T[r, c]) * inv) for c in range(3)] for r in range(3)], np.float32)
+    t = np.array([F32(float(T[r, 3]) * inv) for r in range(3)], np.float32)
+    Ow = [F32(-F32(F32(F32(R[0, c] * t[0]) + F32(R[1, c] * t[1])) + F32(R[2, c] * t[2]))) for c in range(3)]
+    out = matched.astype(np.int64).copy()
+    n = 0
+    for m in range(len(mp["pos"])):
+        if skip[m]:
+            continue
+        X = mp["pos"][m]
+        pc = [F32(F32(F32(F32(R[r, 0] * X[0]) + F32(R[r, 1] * X[1])) + F32(R[r, 2] * X[2])) + t[r]) for r in range(3)]
+        if pc[2] < 0:
+            continue
+        invz = F32(F32(1.0) / pc[2])
+        u = F32(F32(CAM[0] * F32(pc[0] * invz)) + CAM[2])
+        v = F32(F32(CAM[1] * F32(pc[1] * invz)) + CAM[3])
+        if not (0 <= u < W and 0 <= v < H):
+            continue
+        PO = [F32(X[c] - Ow[c]) for c in range(3)]
+        dist3 = F32(np.sqrt(sum(float(p) * float(p) for p in PO)))
+        if dist3 < mp["min_dist"][m] or dist3 > mp["max_dist"][m]:
+            continue
+        if sum(float(PO[c]) * float(mp["normal"][m, c]) for c in range(3)) < 0.5 * float(dist3):
+            continue
+        pred = min(int(np.searchsorted(np.array(sf, np.float32), F32(dist3 / F32(mp["min_dist"][m])), side="left")),
+                   len(sf) - 1)
+        cand = [c for c in area_levels(g, u, v, F32(F32(th) * sf[pred]), -1, -1)
+                if out[c] < 0 and pred - 1 <= k["octave"][c] <= pred]
+        if not cand:
+            continue
+        dist = hamming(mp["desc"][m], d[np.array(cand)])
+        b = int(np.argmin(dist))
+        if dist[b] <= 50:
+            out[cand[b]] = m
+            n += 1
+    return out, n
+
+
+@pytest.mark.parametrize("seed,scale,th", [(0, 1.5, 10), (4, 0.8, 5)])
+def test_kf_scw_search_matches_oracle(seed, scale, th):
+    import proj_data as pd
+    from test_proj_oracle import ref_proj_kf_sim3, seq_case
+    k1, d1, k2, d2, T2, mps, rng = seq_case(seed)
+    S = np.ascontiguousarray(T2, np.float32).copy()
+    S[:3, :] *= np.float32(scale)
+    skip = (rng.random(len(k1)) < 0.1).astype(np.uint8)
+    matched = np.full(len(k2), -1, np.int32)
+    matched[rng.random(len(k2)) < 0.05] = 10 ** 6
+    got, n = kf_scw_search(k2, d2, mps[1], skip, S, th, matched)
+    want, nw = ref_proj_kf_sim3(pd.view(k2, d2), mps, skip, S, th, matched)
     assert n == nw and n > 100
     assert np.array_equal(got, want.astype(np.int64))
