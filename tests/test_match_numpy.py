@@ -248,3 +248,22 @@ def test_window_search_matches_oracle(levels, nnratio, check_ori):
                                     check_ori, ptr(m21), ctypes.byref(c)) == 0
     assert n_np == c.value and n_np > 20
     assert np.array_equal(m_np, m21.astype(np.int64))
+
+
+def test_hamming_bf_matches_oracle():
+    """B8, the C3 brute force: per query descriptor the first
+    minimum of DescriptorDistance over every train descriptor, and the second
+    smallest distance of the multiset; queries and trains from two bench
+    frames plus exact duplicates (ties)."""
+    frames = synth.sequence(640, 480, 2, seed=2000)
+    ex = RefExtractor(500)
+    _, dA = ex(frames[0])
+    _, dB = ex(frames[1])
+    dB = np.ascontiguousarray(np.concatenate([dB, dB[:40], dA[:25]]))
+    L = load()
+    bi, b1, b2 = (np.zeros(len(dA), np.int32) for _ in range(3))
+    assert L.orbx_ref_hamming_bf(ptr(dA), len(dA), ptr(dB), len(dB), ptr(bi), ptr(b1), ptr(b2)) == 0
+    for i in range(len(dA)):
+        dist = hamming(dA[i], dB)
+        s = np.sort(dist)
+        assert (bi[i], b1[i], b2[i]) == (int(np.argmin(dist)), int(s[0]), int(s[1])), i
