@@ -4,8 +4,9 @@ SearchReferencePointsInFrustum runs them (src/Tracking.cc:701-752), on the
 device with no host pass over the local map (orbx_search_local_map,
 orbx_search_local_map_batch).
 
-CPU: the oracle's isInFrustum against an independent numpy float32/float64
-restatement of the same OpenCV 2.4 Mat semantics.  GPU: the device path
+CPU: the oracle's isInFrustum and local-map SearchByProjection against
+independent numpy float32/float64 restatements of the same OpenCV 2.4 Mat
+semantics.  GPU: the device path
 against the oracle, bit-exact on every per-point output (in view, projection,
 predicted level, viewing cosine) and on the match vector and counts.
 """
@@ -91,6 +92,60 @@ def numpy_in_frustum(a, nlevels=8, scale=1.2):
         lvl = int(np.searchsorted(np.array(sf, np.float32), ratio, side="left"))
         out.append((u, v, min(lvl, nlevels - 1), vc))
     return out
+
+
+def numpy_search_local(a, want, th, nnratio=0.8):
+    """ORBmatcher::SearchByProjection(Frame&, vpMapPoints, th) (src/
+    ORBmatcher.cc:49-125) over the points in view: radius RadiusByViewingCos
+    (2.5 above a 0.998 cosine, else 4.0; times th unless th == 1) times the
+    predicted level's scale; candidates at octaves pred - 1 .. pred without a
+    map point (assigned, or matched earlier in this call); best / second with
+    their octaves; kept at best <= TH_HIGH unless best and second share an
+    octave and best > nnratio * second (float)."""
+    from test_match_numpy import Grid, hamming
+    from test_proj_numpy import area_levels, scale_factors
+    g = Grid(a["kf"], W, H)
+    sf = scale_factors()
+    taken = a["assigned"].astype(bool).copy()
+    out = np.full(len(a["kf"]), -1, np.int64)
+    n = 0
+    for m, w in enumerate(want):
+        if w is None:
+            continue
+        u, v, lvl, vc = w
+        r = f32(2.5) if float(vc) > 0.998 else f32(4.0)
+        if th != 1.0:
+            r = f32(r * f32(th))
+        cand = [c for c in area_levels(g, u, v, f32(r * sf[lvl]), lvl - 1, lvl) if not taken[c]]
+        if not cand:
+            continue
+        dist = hamming(a["desc"][m], a["df"][np.array(cand)])
+        best = best2 = 2147483647
+        bl = bl2 = -1
+        bi = -1
+        for c, d in zip(cand, dist):
+            d = int(d)
+            if d < best:
+                best2, best, bl2, bl, bi = best, d, bl, int(a["kf"]["octave"][c]), c
+            elif d < best2:
+                bl2, best2 = int(a["kf"]["octave"][c]), d
+        if best <= 100:
+            if bl == bl2 and f32(best) > f32(f32(nnratio) * f32(best2)):
+                continue
+            taken[bi] = True
+            out[bi] = m
+            n += 1
+    return out, n
+
+
+@pytest.mark.parametrize("seed,th", [(1, 1.0), (2, 1.0), (3, 5.0)])
+def test_oracle_search_local_matches_numpy(feats, seed, th):
+    (km, dm), (kf, df) = feats
+    a, q = make_case(km, dm, kf, df, W, H, seed, th=th)
+    assert ref_lib().orbx_ref_search_local_map(ctypes.byref(q)) == 0
+    got, n = numpy_search_local(a, numpy_in_frustum(a), th)
+    assert n == q.n_matches > 50
+    assert np.array_equal(got, a["matches"].astype(np.int64))
 
 
 @pytest.mark.parametrize("seed", [1, 2])
