@@ -637,8 +637,11 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
     fx_t* lo = hi + M;
     fx_t* bhi = lo + M;
     fx_t* blo = bhi + n;
-    double* S = reinterpret_cast<double*>(hi);     // packed lower triangle, after conversion
-    double* bs = reinterpret_cast<double*>(bhi);
+    // after conversion: the packed lower triangle S, and the right-hand side
+    // as its row n (S + M, over the dead lo limbs), which the factorisation
+    // below carries through the forward substitution
+    double* S = reinterpret_cast<double*>(hi);
+    double* bs = S + M;
     // the power-of-two scales of the fixed point (see fx_split_scaled):
     // largest diagonal of Hpp + lambda I into [2^29, 2^30), largest |b| into
     // [2^23, 2^24); exact, and the same on every thread
@@ -685,6 +688,7 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
     // scaled back (exact)
     const double iS = 1.0 / sS, iB = 1.0 / sB;
     for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(hi[k], lo[k]) * iS;
+    __syncthreads();   // the lo limbs are read before row n overwrites them
     for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]) * iB;
     __syncthreads();
     LBA_MARK(2);
@@ -725,7 +729,7 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
         __syncthreads();
         if (s_bad) return false;   // not positive definite (uniform)
         // panel: row r below the block solves x L_kk^T = A(r, block)
-        for (int r = k0 + 6 + threadIdx.x; r < n; r += kLbaThreads) {
+        for (int r = k0 + 6 + threadIdx.x; r <= n; r += kLbaThreads) {   // row n: the forward solve of b
             double x[6];
             double* Sr = S + pk(r, k0);
 #pragma unroll
@@ -742,11 +746,11 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
         }
         __syncthreads();
         // trailing triangle: S(i, j) -= L(i, block) . L(j, block)
-        for (int i = k0 + 6 + (threadIdx.x >> 5); i < n; i += kLbaThreads / 32) {
+        for (int i = k0 + 6 + (threadIdx.x >> 5); i <= n; i += kLbaThreads / 32) {
             const double* Li = S + pk(i, k0);
             const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
             double* Si = S + pk(i, 0);
-            for (int j = k0 + 6 + (threadIdx.x & 31); j <= i; j += 32) {
+            for (int j = k0 + 6 + (threadIdx.x & 31); j <= min(i, n - 1); j += 32) {
                 const double* Lj = S + pk(j, k0);
                 Si[j] -= ((((l0 * Lj[0] + l1 * Lj[1]) + l2 * Lj[2]) + l3 * Lj[3]) + l4 * Lj[4]) + l5 * Lj[5];
             }
@@ -754,9 +758,12 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
         __syncthreads();
     }
     LBA_MARK(3);
-    // forward / backward substitution by one wave, in 6-row blocks: the
-    // block's triangle on lanes 0..5 with shuffles, then the other rows
-    // updated with the block's six values; one wave barrier per block
+    // the factorisation above solved L y = b in its row n (the panel step is
+    // the forward substitution's block solve, the trailing update its update
+    // of the later rows, in the same operation order); backward substitution
+    // by one wave, in 6-row blocks: the block's triangle on lanes 0..5 with
+    // shuffles, then the earlier rows updated with the block's six values;
+    // one wave barrier per block
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         for (int i = lane; i < n; i += 64) xp[i] = bs[i];
@@ -766,25 +773,6 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         };
         wave_fence();
-        for (int kb = 0; kb < nb; kb++) {   // L y = b
-            const int k0 = 6 * kb;
-            double yi = lane < 6 ? xp[k0 + lane] : 0.0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const double yj = __shfl(yi, j, 64) / S[pk(k0 + j, k0 + j)];
-                if (lane == j) yi = yj;
-                else if (lane > j && lane < 6) yi -= S[pk(k0 + lane, k0 + j)] * yj;
-            }
-            if (lane < 6) xp[k0 + lane] = yi;
-            double y[6];
-#pragma unroll
-            for (int p = 0; p < 6; p++) y[p] = __shfl(yi, p, 64);
-            for (int i = k0 + 6 + lane; i < n; i += 64) {
-                const double* Li = S + pk(i, k0);
-                xp[i] -= ((((Li[0] * y[0] + Li[1] * y[1]) + Li[2] * y[2]) + Li[3] * y[3]) + Li[4] * y[4]) + Li[5] * y[5];
-            }
-            wave_fence();
-        }
         for (int kb = nb - 1; kb >= 0; kb--) {   // L^T x = y
             const int k0 = 6 * kb;
             double xi = lane < 6 ? xp[k0 + lane] : 0.0;
