@@ -693,43 +693,56 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
     __syncthreads();
     LBA_MARK(2);
     // dense LLT on the packed lower triangle, right-looking in 6x6 blocks
-    // (the pose blocks): per block column one wave factors the diagonal block
-    // in registers (rows on lanes 0..5, shuffles), the panel rows solve
-    // against it, the trailing triangle takes the rank-6 update; three
-    // barriers per block column instead of three per column.
+    // (the pose blocks): wave 0 factors a diagonal block in registers (rows on
+    // lanes 0..5, shuffles), the panel rows solve against it, the trailing
+    // triangle takes the rank-6 update.  Look-ahead: during block column kb's
+    // trailing update wave 0 first updates the next diagonal block itself and
+    // factors it at once, so each block column costs two barriers and the
+    // factorisations hide behind the trailing updates (every element sees the
+    // same operations in the same order as without the look-ahead).
     const int nb = n / 6;
-    for (int kb = 0; kb < nb; kb++) {
-        const int k0 = 6 * kb;
-        if (threadIdx.x < 64) {
-            const int i = threadIdx.x;
-            const bool row = i < 6;
-            double a[6];
+    auto factor_diag = [&](int k0) {   // wave 0
+        const int i = threadIdx.x;
+        const bool row = i < 6;
+        double a[6];
 #pragma unroll
-            for (int j = 0; j < 6; j++) a[j] = (row && j <= i) ? S[pk(k0 + i, k0 + j)] : 0.0;
-            int fail = 0;
+        for (int j = 0; j < 6; j++) a[j] = (row && j <= i) ? S[pk(k0 + i, k0 + j)] : 0.0;
+        int fail = 0;
 #pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const double piv = __shfl(a[j], j, 64);   // a_jj after the previous columns
-                fail |= !(piv > 0);
-                const double ljj = sqrt(piv);
-                if (i == j) a[j] = ljj;
-                else if (row && i > j) a[j] = a[j] / ljj;
+        for (int j = 0; j < 6; j++) {
+            const double piv = __shfl(a[j], j, 64);   // a_jj after the previous columns
+            fail |= !(piv > 0);
+            const double ljj = sqrt(piv);
+            if (i == j) a[j] = ljj;
+            else if (row && i > j) a[j] = a[j] / ljj;
 #pragma unroll
-                for (int q = j + 1; q < 6; q++) {
-                    const double lqj = __shfl(a[j], q, 64);
-                    if (row && i >= q) a[q] -= a[j] * lqj;
-                }
+            for (int q = j + 1; q < 6; q++) {
+                const double lqj = __shfl(a[j], q, 64);
+                if (row && i >= q) a[q] -= a[j] * lqj;
             }
-            if (row)
-#pragma unroll
-                for (int j = 0; j < 6; j++)
-                    if (j <= i) S[pk(k0 + i, k0 + j)] = a[j];
-            if (i == 0) s_bad = fail;
         }
+        if (row)
+#pragma unroll
+            for (int j = 0; j < 6; j++)
+                if (j <= i) S[pk(k0 + i, k0 + j)] = a[j];
+        if (i == 0) s_bad = fail;
+    };
+    // S(i, j) -= L(i, block) . L(j, block) of block column k0
+    auto trail = [&](int k0, int i, int j) {
+        const double* Li = S + pk(i, k0);
+        const double* Lj = S + pk(j, k0);
+        S[pk(i, j)] -= ((((Li[0] * Lj[0] + Li[1] * Lj[1]) + Li[2] * Lj[2]) + Li[3] * Lj[3]) + Li[4] * Lj[4]) +
+                       Li[5] * Lj[5];
+    };
+    if (nb > 0) {
+        if (threadIdx.x < 64) factor_diag(0);
         __syncthreads();
         if (s_bad) return false;   // not positive definite (uniform)
+    }
+    for (int kb = 0; kb < nb; kb++) {
+        const int k0 = 6 * kb, k1 = k0 + 6;
         // panel: row r below the block solves x L_kk^T = A(r, block)
-        for (int r = k0 + 6 + threadIdx.x; r <= n; r += kLbaThreads) {   // row n: the forward solve of b
+        for (int r = k1 + threadIdx.x; r <= n; r += kLbaThreads) {   // row n: the forward solve of b
             double x[6];
             double* Sr = S + pk(r, k0);
 #pragma unroll
@@ -745,17 +758,36 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
             for (int j = 0; j < 6; j++) Sr[j] = x[j];
         }
         __syncthreads();
-        // trailing triangle: S(i, j) -= L(i, block) . L(j, block)
-        for (int i = k0 + 6 + (threadIdx.x >> 5); i <= n; i += kLbaThreads / 32) {
-            const double* Li = S + pk(i, k0);
-            const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
-            double* Si = S + pk(i, 0);
-            for (int j = k0 + 6 + (threadIdx.x & 31); j <= min(i, n - 1); j += 32) {
-                const double* Lj = S + pk(j, k0);
-                Si[j] -= ((((l0 * Lj[0] + l1 * Lj[1]) + l2 * Lj[2]) + l3 * Lj[3]) + l4 * Lj[4]) + l5 * Lj[5];
+        const bool ahead = kb + 1 < nb;
+        if (ahead && threadIdx.x < 64) {
+            // the next diagonal block's 21 elements, then its factorisation
+            const int t = threadIdx.x;
+            if (t < 21) {
+                int r = 0;
+                while ((r + 1) * (r + 2) / 2 <= t) r++;
+                trail(k0, k1 + r, k1 + (t - r * (r + 1) / 2));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            factor_diag(k1);
+        } else {
+            // the rest of the trailing triangle (and the b row), half-wave per row
+            const int t = ahead ? threadIdx.x - 64 : threadIdx.x;
+            const int nhw = (ahead ? kLbaThreads - 64 : kLbaThreads) / 32;
+            for (int i = k1 + (t >> 5); i <= n; i += nhw) {
+                const double* Li = S + pk(i, k0);
+                const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
+                double* Si = S + pk(i, 0);
+                const int j0 = (ahead && i < k1 + 6) ? k1 + 6 : k1;   // the next diagonal block is wave 0's
+                for (int j = j0 + (t & 31); j <= min(i, n - 1); j += 32) {
+                    const double* Lj = S + pk(j, k0);
+                    Si[j] -= ((((l0 * Lj[0] + l1 * Lj[1]) + l2 * Lj[2]) + l3 * Lj[3]) + l4 * Lj[4]) + l5 * Lj[5];
+                }
             }
         }
         __syncthreads();
+        if (s_bad) return false;
     }
     LBA_MARK(3);
     // the factorisation above solved L y = b in its row n (the panel step is
