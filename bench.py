@@ -441,6 +441,251 @@ def run_pose(args, wl, rank, local, world, dist):
     return allst, kernels, ab, units_per_step, cpu, check, cfg
 
 
+# Single-call legs (VERDICT r04 "Next" #1): the reference calls the hot path
+# one unit at a time, synchronously -- the extractor once per frame
+# (src/Frame.cc:59 from src/Tracking.cc:206), SearchForInitialization per
+# initialisation attempt (src/Tracking.cc:361), PoseOptimization 2-4 times per
+# frame (src/Tracking.cc:533,556,593,627), LocalBundleAdjustment once per
+# keyframe (src/LocalMapping.cc:83).  Each leg times the same C-ABI call the
+# C++ adapter makes (orb_slam_amd/adapters/orbx_adapters.hpp), host arrays in
+# and out, one call at a time: 50 warm-up calls, then the median (and p90) of
+# 500; the oracle's single-thread call on the same inputs beside it.
+SINGLE_PROTOCOL = (50, 500)
+
+
+def time_calls(fn, n_items, protocol, reset=None):
+    """Per-call wall times of fn(i) (reset(i) runs before each call, untimed)."""
+    warm, timed_n = protocol
+    times = []
+    for k in range(warm + timed_n):
+        if reset is not None:
+            reset(k % n_items)
+        t0 = time.perf_counter()
+        fn(k % n_items)
+        dt = time.perf_counter() - t0
+        if k >= warm:
+            times.append(dt)
+    t = np.asarray(times)
+    return {"median_ms": round(1e3 * float(np.median(t)), 4), "p90_ms": round(1e3 * float(np.percentile(t, 90)), 4),
+            "calls": len(t)}
+
+
+def single_call_legs(args, frames, nf, w, h):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from orb_slam_amd import synth_ba as sb, synth_pose as sp
+    L = ox.lib()
+    R, rdesc = native_oracle()
+    proto = SINGLE_PROTOCOL
+    out = {"protocol": f"{proto[0]} warm-up calls, then the median / p90 of {proto[1]}; one call at a time, "
+                       "host arrays in and out (the adapter's C-ABI call); cpu = the oracle on one core "
+                       f"({rdesc})"}
+
+    def check_rc(r, where):
+        if r != 0:
+            raise ox.OrbxError(r, where)
+
+    # --- ORBextractor::operator() on one 640x480 frame --------------------
+    imgs = [np.ascontiguousarray(f) for f in frames[:64]]
+    ctx1 = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=1, device=args.device)
+    kps = np.zeros(nf, ox.KEYPOINT)
+    desc = np.zeros((nf, 32), np.uint8)
+    n = ctypes.c_int()
+
+    def ext(i):
+        check_rc(L.orbx_extract(ctx1.handle, imgs[i].ctypes.data, w, h, w, kps.ctypes.data, desc.ctypes.data, nf,
+                                ctypes.byref(n)), "orbx_extract")
+
+    ex = {}
+    for mode, name in ((1, "graph"), (2, "graph_frame_in_place"), (0, "stream_launches")):
+        ctx1.set_launch_mode(mode)
+        ex[name] = time_calls(ext, len(imgs), proto)
+    ctx1.set_launch_mode(1)
+    rex = oracle_lib.RefExtractor(nf, lib=R, nth_pivot=ctx1.nth_pivot())          # timed (reference flags)
+    rpar = oracle_lib.RefExtractor(nf, nth_pivot=ctx1.nth_pivot())                # parity oracle
+    bad = []
+    for i in (0, 1, 63):                      # graph-path outputs against the oracle
+        ext(i)
+        rk, rd = rpar(imgs[i])
+        if not (n.value == len(rk) and np.array_equal(kps[:n.value].view(np.uint8), rk.view(np.uint8))
+                and np.array_equal(desc[:n.value], rd)):
+            bad.append(i)
+    ex["cpu"] = time_calls(lambda i: rex(imgs[i]), len(imgs), proto)
+    ex["speedup_vs_cpu"] = round(ex["cpu"]["median_ms"] / ex["graph"]["median_ms"], 2)
+    ex["graph_vs_stream_launches"] = round(ex["stream_launches"]["median_ms"] / ex["graph"]["median_ms"], 2)
+    ex["bit_exact"] = not bad
+    ex["call"] = (f"orbx_extract: one {w}x{h} mono8 host image in, {nf}-keypoint records + descriptors out "
+                  "(ORBextractor::operator(), src/ORBextractor.cc:718-779)")
+    out["extract"] = ex
+
+    # --- SearchForInitialization on consecutive frames (host views) --------
+    feats = [rex(imgs[i]) for i in range(8)]
+    views = [(ox.frame_view(k, d, w, h), k, d) for k, d in feats]
+    m12 = np.zeros(nf, np.int32)
+    pm = np.zeros((nf, 2), np.float32)
+    nm = ctypes.c_int()
+
+    def prev_reset(i):
+        k = views[i][1]
+        pm[:len(k)] = np.stack([k["x"], k["y"]], 1)
+
+    def sfi(i, lib_call):
+        F1, F2 = views[i][0], views[(i + 1) % len(views)][0]
+        lib_call(F1, F2)
+
+    def gpu_sfi(F1, F2):
+        check_rc(L.orbx_search_for_initialization(ctx1.handle, ctypes.byref(F1), ctypes.byref(F2), pm.ctypes.data,
+                                                  m12.ctypes.data, 100, 0.9, 1, ctypes.byref(nm)),
+                 "orbx_search_for_initialization")
+
+    def cpu_sfi(F1, F2):
+        R.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), pm.ctypes.data, m12.ctypes.data,
+                                             100, 0.9, 1, ctypes.byref(nm))
+
+    mt = {"gpu": time_calls(lambda i: sfi(i, gpu_sfi), len(views), proto, reset=prev_reset),
+          "cpu": time_calls(lambda i: sfi(i, cpu_sfi), len(views), proto, reset=prev_reset)}
+    mt["speedup_vs_cpu"] = round(mt["cpu"]["median_ms"] / mt["gpu"]["median_ms"], 2)
+    mt["call"] = ("orbx_search_for_initialization: two host frame views (1000 keypoints each), window 100, nnratio "
+                  "0.9, orientation check (ORBmatcher::SearchForInitialization, src/ORBmatcher.cc:598-713)")
+    out["search_for_initialization"] = mt
+    ctx1.close()
+
+    # --- Optimizer::PoseOptimization on one frame ------------------------
+    ctxp = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=args.device)
+    pframes = [sp.make_frame(n_kp=1000, seed=7000 * 1000 + i) for i in range(16)]
+    pstructs = [sp.to_ctypes(fr) for fr in pframes]
+    work = [sp.PoseFrame.from_buffer_copy(p) for p, _ in pstructs]
+    ninl = ctypes.c_int()
+    R.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+
+    def pose_reset(i):
+        ctypes.memmove(ctypes.addressof(work[i]), ctypes.addressof(pstructs[i][0]), ctypes.sizeof(work[i]))
+
+    po = {"gpu": time_calls(lambda i: check_rc(L.orbx_pose_optimization(ctxp.handle, ctypes.byref(work[i]),
+                                                                        ctypes.byref(ninl), None),
+                                               "orbx_pose_optimization"), len(work), proto, reset=pose_reset)}
+    gpu_tcw = [np.ctypeslib.as_array(work[i].Tcw).copy() for i in range(len(work))]
+    po["cpu"] = time_calls(lambda i: R.orbx_ref_pose_optimization(ctypes.byref(work[i]), None, None), len(work), proto,
+                           reset=pose_reset)
+    P = oracle_lib.load()                     # the parity oracle for the comparison
+    P.orbx_ref_pose_optimization.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    cpu_tcw = []
+    for i in range(len(work)):
+        pose_reset(i)
+        P.orbx_ref_pose_optimization(ctypes.byref(work[i]), None, None)
+        cpu_tcw.append(np.ctypeslib.as_array(work[i].Tcw).copy())
+    po["max_abs_tcw_diff_vs_oracle"] = float(max(np.abs(a - b).max() for a, b in zip(gpu_tcw, cpu_tcw)))
+    po["speedup_vs_cpu"] = round(po["cpu"]["median_ms"] / po["gpu"]["median_ms"], 2)
+    po["call"] = ("orbx_pose_optimization: one frame, 1000 keypoints, ~700 map-point edges, ~10 % outliers "
+                  "(Optimizer::PoseOptimization, src/Optimizer.cc:154-285)")
+    out["pose_optimization"] = po
+    ctxp.close()
+
+    # --- Optimizer::LocalBundleAdjustment on one problem -------------------
+    ctxb = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=args.device)
+    probs = [sb.make_problem(n_kf=20, n_points=2000, seed=5000 * 1000 + i) for i in range(4)]
+    bwork = [sb.to_ctypes(pr) for pr in probs]
+    es = [np.zeros(p.n_edges, np.uint8) for p, _ in bwork]
+    pb = [np.zeros(p.n_points, np.uint8) for p, _ in bwork]
+    R.orbx_ref_lba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]
+
+    def lba_reset(i):
+        a, pr = bwork[i][1], probs[i]
+        np.copyto(a["pose_q"], pr["pose_q"])
+        np.copyto(a["pose_t"], pr["pose_t"])
+        np.copyto(a["points"], pr["points"])
+
+    st = sb.BAStats()
+    ba = {"gpu": time_calls(lambda i: check_rc(L.orbx_lba_solve(ctxb.handle, ctypes.byref(bwork[i][0]), 5, 10, None,
+                                                                es[i].ctypes.data, pb[i].ctypes.data,
+                                                                ctypes.byref(st)), "orbx_lba_solve"),
+                            len(bwork), proto, reset=lba_reset)}
+    gq = [bwork[i][1]["pose_q"].copy() for i in range(len(bwork))]
+    ba["cpu"] = time_calls(lambda i: R.orbx_ref_lba(ctypes.byref(bwork[i][0]), 5, 10, es[i].ctypes.data,
+                                                    pb[i].ctypes.data, ctypes.byref(st)),
+                           len(bwork), proto, reset=lba_reset)
+    P.orbx_ref_lba.argtypes = R.orbx_ref_lba.argtypes
+    worst = 0.0
+    for i in range(len(bwork)):
+        lba_reset(i)
+        P.orbx_ref_lba(ctypes.byref(bwork[i][0]), 5, 10, es[i].ctypes.data, pb[i].ctypes.data, ctypes.byref(st))
+        worst = max(worst, float(np.abs(gq[i] - bwork[i][1]["pose_q"]).max()))
+    ba["max_abs_pose_q_diff_vs_oracle"] = worst
+    ba["speedup_vs_cpu"] = round(ba["cpu"]["median_ms"] / ba["gpu"]["median_ms"], 2)
+    ba["call"] = ("orbx_lba_solve: one 20 KF (+2 fixed) x 2000 MP problem, optimize(5), outlier pass, optimize(10), "
+                  "outlier pass (Optimizer::LocalBundleAdjustment, src/Optimizer.cc:287-536)")
+    out["lba_solve"] = ba
+    ctxb.close()
+    return out
+
+
+def host_inclusive_frames(args, ctx, frames, B, bf, configure):
+    """c2 with the host boundary inside the timed region: each step uploads
+    its B frames from page-locked host memory (orbx_dev_upload_async, the next
+    step's frames while this step extracts), extracts + matches them, and
+    reads keypoints, descriptors, counts and match vectors back into
+    page-locked host memory (orbx_dev_download_async).  Reported beside
+    `value`, never as it (the task's contract keeps inputs resident there)."""
+    h, w = frames.shape[1:]
+    nf = ctx.nfeatures
+    src = ox.HostArray((B, h, w), np.uint8)
+    src.array[:] = frames
+    outs = [dict(kps=ox.HostArray((B * nf,), ox.KEYPOINT), desc=ox.HostArray((B * nf, 32), np.uint8),
+                 n=ox.HostArray((B,), np.int32), m12=ox.HostArray((B * nf,), np.int32),
+                 nm=ox.HostArray((B,), np.int32)) for _ in range(2)]
+    configure(False)
+    it = [0]
+
+    def step():
+        k = it[0]
+        it[0] += 1
+        first, nxt = (k % 2) * B, ((k + 1) % 2) * B
+        ctx.upload_async(src.array, first=nxt)       # next step's frames, behind this step's extraction
+        ctx.extract_match(first, B, B, mode="bf" if bf else "init", window=100, th_low=50, nnratio=0.9,
+                          check_ori=True)
+        o = outs[k % 2]
+        ctx.download_async(first, B, o["kps"].array, o["desc"].array, o["n"].array, o["m12"].array, o["nm"].array)
+
+    ctx.upload_async(src.array, first=0)
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    steps = max(5, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    dt = time.perf_counter() - t0
+    # the last step's host buffers against the device-resident outputs (which
+    # parity_frames checks against the oracle)
+    k = it[0] - 1
+    first, o = (k % 2) * B, outs[k % 2]
+    bad = []
+    for f in (0, B // 2, B - 1):
+        gk, gd = ctx.features(first + f)
+        gm, gn = ctx.matches(first + f)
+        hk = o["kps"].array[f * nf:f * nf + len(gk)]
+        ok = (int(o["n"].array[f]) == len(gk) and np.array_equal(hk.view(np.uint8), gk.view(np.uint8))
+              and np.array_equal(o["desc"].array[f * nf:f * nf + len(gk)], gd)
+              and int(o["nm"].array[f]) == gn and np.array_equal(o["m12"].array[f * nf:(f + 1) * nf], gm))
+        if not ok:
+            bad.append(first + f)
+    in_b = B * h * w
+    out_b = B * (nf * (28 + 32 + 4) + 8)
+    res = {"frames_per_s": round(B * steps / dt, 2), "ms_per_step": round(1e3 * dt / steps, 4), "steps": steps,
+           "h2d_GBps": round(in_b * steps / dt / 1e9, 2), "d2h_GBps": round(out_b * steps / dt / 1e9, 2),
+           "host_buffers_equal_device_outputs": not bad,
+           "boundary": "images uploaded from page-locked host memory and keypoints / descriptors / counts / match "
+                       "vectors read back into it inside the timed region (orbx_dev_upload_async, "
+                       "orbx_dev_download_async)"}
+    for o in outs:
+        for v in o.values():
+            v.close()
+    src.close()
+    return res
+
+
 def parity_frames(ctx, frames, first, B, nf, w, h, bf):
     """Bit-exact check of the last timed step's output against the oracle
     (run after the timed region, with the CPU baseline): the pipeline's part
@@ -567,6 +812,10 @@ def run_frames(args, wl, rank, local, world, dist):
         L, desc = native_oracle()
         cpu = cpu_baseline_frames(frames, nf, CPU_PROTOCOL[args.workload], bf=bf, L=L, lib_desc=desc)
         cpu["all_cores"] = cpu_all_cores_frames(frames, nf, max(3.0, args.cpu_budget / 2), bf=bf, L=L, lib_desc=desc)
+    if rank == 0 and not args.no_host_inclusive and not args.serial:
+        check["host_inclusive"] = host_inclusive_frames(args, ctx, frames, B, bf, configure)
+    if rank == 0 and world == 1 and args.workload == "c2" and not (args.no_single_call or args.no_cpu_baseline):
+        check["single_call"] = single_call_legs(args, frames, nf, w, h)
     cfg = {"workload": wl["desc"], "frames_per_step_per_gpu": B, "nfeatures": nf, "image": f"{w}x{h}",
            "parallelism": f"dp{world} (one sequence per GPU)",
            "pipeline": ("serialised (diagnostic --serial)" if args.serial else
@@ -861,6 +1110,10 @@ def main():
                     help="orbx_dev_set_pyramid_mode: 0 staged launches (default), 1 fused pyramid + blur, 2 band cascade")
     ap.add_argument("--fast-chunk", type=int, default=0,
                     help="orbx_dev_set_fast_chunk: cells per FAST workgroup (0 = library default)")
+    ap.add_argument("--no-single-call", action="store_true",
+                    help="skip the single-call latency legs of the c2 line (check.single_call)")
+    ap.add_argument("--no-host-inclusive", action="store_true",
+                    help="skip the host-fed throughput leg of c2 / c3 (check.host_inclusive)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel hipEvents in the timed region (roofline then unavailable)")
     args = ap.parse_args()

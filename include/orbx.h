@@ -27,6 +27,20 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header.  A caller compares orbx_abi_version() with the
+ * ORBX_ABI_VERSION it was compiled against before its first call (the C++
+ * adapter does, in every constructor) and refuses a library of another
+ * revision instead of calling through a changed signature.
+ *   1: rounds 1-3.
+ *   2: orbx_lba_solve_batch / orbx_lba_run take per-problem abort flags
+ *      (the `aborts` argument after iters1).
+ *   3: single-frame graph path (orbx_set_launch_mode), host-fed pipeline
+ *      (orbx_host_alloc, orbx_dev_upload_async, orbx_dev_download_async),
+ *      image bounds of device-resident frames (orbx_dev_set_image_bounds);
+ *      additions only. */
+#define ORBX_ABI_VERSION 3
+int orbx_abi_version(void);
+
 #define ORBX_OK               0
 #define ORBX_ERR_ARG         -1  /* invalid argument / shape                      */
 #define ORBX_ERR_HIP         -2  /* HIP runtime failure (device missing, launch)  */
@@ -92,6 +106,24 @@ int orbx_describe_levels(int nfeatures, float scale_factor, int nlevels, int fas
  * reference returns without touching its outputs (:721-722). */
 int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
                  orbx_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+/* How orbx_extract issues its work (Frame::Frame calls the extractor once per
+ * frame, synchronously: src/Frame.cc:59, src/Tracking.cc:206).
+ *   1 (default): the call is one hipGraph launch -- the image copied through a
+ *     page-locked staging buffer into its slot, the extraction kernels (the
+ *     blur on a branch beside FAST and retainBest), then one kernel that
+ *     stores the count, error flags, keypoints and descriptors into a
+ *     page-locked buffer -- and one synchronisation.  The graph is captured
+ *     on the first call of a configuration (frame size, launch mode,
+ *     fp-contract mode, nth_element era, pyramid mode, FAST chunking) and
+ *     replayed after that.
+ *   2: as 1, but the pyramid kernels read the frame from the page-locked
+ *     staging buffer directly (no copy).
+ *   0: the kernels launched one by one on the context stream, with pageable
+ *     copies (rounds 1-4).
+ * Both produce identical outputs; kernel timing (orbx_dev_kernel_time_enable)
+ * takes the stream launches. */
+int orbx_set_launch_mode(orbx_ctx* ctx, int mode);
+int orbx_get_launch_mode(const orbx_ctx* ctx);
 
 /* Batched form: B frames of identical size, host in / host out.
  * kps: B*cap records, desc: B*cap*32 bytes, n_out: B counts. */
@@ -193,6 +225,13 @@ int orbx_dev_get_fast_chunk(const orbx_ctx* ctx);
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */
 int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len,
                         int window, float nnratio, int check_ori);
+/* Image bounds of the slots' keypoints for the device-resident matchers
+ * (orbx_dev_match_prev and the extract_match pipeline): Frame's static
+ * mnMinX, mnMaxX, mnMinY, mnMaxY (src/Frame.cc:320-348), which also scale its
+ * 64x48 grid (:76-77).  After orbx_dev_undistort with a distorting camera,
+ * pass orbx_compute_image_bounds' result; NULL (the default) is 0..w x 0..h,
+ * the reference's bounds without distortion (:341-347). */
+int orbx_dev_set_image_bounds(orbx_ctx* ctx, const float* bounds);
 /* Brute-force matching (config C3) of slots [first, first+count) against
  * their predecessors, same slot pairing as orbx_dev_match_prev: every
  * keypoint of s-1 against every keypoint of s, accepted when best <= th_low
@@ -201,6 +240,28 @@ int orbx_dev_match_prev(orbx_ctx* ctx, int first, int count, int seq_len,
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len,
                            int th_low, float nnratio);
 int orbx_dev_sync(orbx_ctx* ctx);
+/* Host-fed pipeline: frames that arrive in host memory and results that must
+ * leave it, overlapped with the extraction of other slots.
+ * orbx_host_alloc / orbx_host_free: page-locked host memory (the copies below
+ * overlap device work only from such memory).
+ * orbx_dev_upload_async: like orbx_dev_upload, but queued on an internal copy
+ * stream and returning at once; the copy waits for the extractions queued
+ * before the call (which may still read the slots' previous frames), and a
+ * later extraction of these slots waits for the copy.  The frame size must be
+ * the context's current one (otherwise the call is orbx_dev_upload).
+ * orbx_dev_download_async: queue read-backs of slots [first, first+count)
+ * after their queued extraction and match: keypoints (count x nfeatures
+ * records, slot-major), descriptors (count x nfeatures x 32), keypoint counts
+ * (count), match vectors (count x nfeatures) and match counts (count); any
+ * pointer may be NULL.  A later extraction of these slots waits for the
+ * copies; the host buffers are complete after orbx_dev_sync. */
+int  orbx_host_alloc(size_t bytes, void** out);
+void orbx_host_free(void* p);
+int  orbx_dev_upload_async(orbx_ctx* ctx, int first, int count, const uint8_t* imgs,
+                           int w, int h, size_t stride);
+int  orbx_dev_download_async(orbx_ctx* ctx, int first, int count, orbx_keypoint* kps,
+                             uint8_t* desc, int32_t* n_kps, int32_t* matches12,
+                             int32_t* n_matches);
 /* Read back one slot's features / its match result (after sync). */
 int orbx_dev_read_features(orbx_ctx* ctx, int slot, orbx_keypoint* kps,
                            uint8_t* desc, int cap, int* n_out);

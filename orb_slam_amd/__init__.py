@@ -137,6 +137,14 @@ def _declare(L):
         "orbx_pose_run": ([vp], i),
         "orbx_pose_fetch": ([vp, vp, vp, vp], i),
         "orbx_version": ([], ctypes.c_char_p),
+        "orbx_abi_version": ([], i),
+        "orbx_dev_set_image_bounds": ([vp, vp], i),
+        "orbx_set_launch_mode": ([vp, i], i),
+        "orbx_get_launch_mode": ([vp], i),
+        "orbx_host_alloc": ([sz, ctypes.POINTER(vp)], i),
+        "orbx_host_free": ([vp], None),
+        "orbx_dev_upload_async": ([vp, i, i, vp, i, i, sz], i),
+        "orbx_dev_download_async": ([vp, i, i, vp, vp, vp, vp, vp], i),
         "orbx_describe_levels": ([i, f, i, i, i, i, vp, i], i),
     }
     for name, (args, res) in sigs.items():
@@ -208,6 +216,20 @@ class Context:
                                   _ptr(desc), self.nfeatures, ctypes.byref(n)), "orbx_extract")
         return kps[:n.value].copy(), desc[:n.value].copy()
 
+    def set_image_bounds(self, bounds=None):
+        """orbx_dev_set_image_bounds: (min_x, max_x, min_y, max_y) of the
+        slots' undistorted keypoints for the device matchers, None = image."""
+        b = None if bounds is None else np.ascontiguousarray(bounds, np.float32)
+        _check(lib().orbx_dev_set_image_bounds(self._h, _ptr(b)), "orbx_dev_set_image_bounds")
+
+    def set_launch_mode(self, mode):
+        """orbx_extract's launches: 1 one captured hipGraph per call (default),
+        0 stream launches (orbx_set_launch_mode)."""
+        _check(lib().orbx_set_launch_mode(self._h, int(mode)), "orbx_set_launch_mode")
+
+    def launch_mode(self):
+        return lib().orbx_get_launch_mode(self._h)
+
     # --- device-resident pipeline ------------------------------------------
     def upload(self, frames, first=0):
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
@@ -215,6 +237,19 @@ class Context:
             frames = frames[None]
         cnt, h, w = frames.shape
         _check(lib().orbx_dev_upload(self._h, first, cnt, _ptr(frames), w, h, w), "orbx_dev_upload")
+
+    def upload_async(self, frames, first=0):
+        """orbx_dev_upload_async: `frames` should be page-locked (HostArray)
+        for the copy to overlap device work."""
+        cnt, h, w = frames.shape
+        _check(lib().orbx_dev_upload_async(self._h, first, cnt, _ptr(frames), w, h, w), "orbx_dev_upload_async")
+
+    def download_async(self, first, count, kps=None, desc=None, n_kps=None, m12=None, n_m=None):
+        """orbx_dev_download_async into (preferably page-locked) arrays:
+        kps count*nfeatures KEYPOINT, desc (count*nfeatures, 32) u8, n_kps
+        count i32, m12 count*nfeatures i32, n_m count i32."""
+        _check(lib().orbx_dev_download_async(self._h, first, count, _ptr(kps), _ptr(desc), _ptr(n_kps), _ptr(m12),
+                                             _ptr(n_m)), "orbx_dev_download_async")
 
     def extract(self, first, count):
         _check(lib().orbx_dev_extract(self._h, first, count), "orbx_dev_extract")
@@ -392,6 +427,31 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+
+class HostArray:
+    """Page-locked host memory from orbx_host_alloc viewed as a numpy array
+    (freed with the object)."""
+
+    def __init__(self, shape, dtype):
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        self._p = ctypes.c_void_p()
+        _check(lib().orbx_host_alloc(max(n, 1), ctypes.byref(self._p)), "orbx_host_alloc")
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(self._p.value)
+        self.array = np.frombuffer(buf, np.uint8, count=n).view(dtype).reshape(shape)
+
+    def close(self):
+        if self._p:
+            self.array = None
+            lib().orbx_host_free(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Vocabulary:

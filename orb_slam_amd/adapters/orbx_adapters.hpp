@@ -47,6 +47,9 @@ public:
     Context(int nfeatures, float scale_factor, int nlevels, int score_type, int fast_th, int max_w, int max_h,
             int max_batch = 1, int device = 0)
     {
+        // a library of another ABI revision may have changed a signature this
+        // header calls through (include/orbx.h, ORBX_ABI_VERSION)
+        if (orbx_abi_version() != ORBX_ABI_VERSION) throw orbx_error(ORBX_ERR_UNSUPPORTED, "orbx_abi_version");
         check(orbx_create(&ctx_, device, nfeatures, scale_factor, nlevels, score_type, fast_th, max_w, max_h, max_batch),
               "orbx_create");
     }

@@ -168,7 +168,30 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
     ctx->pyr_planned = false;
     ctx->geom_w = w;
     ctx->geom_h = h;
+    ctx->geom_gen++;   // a captured single-frame graph holds the old tables and buffers
     return ORBX_OK;
+}
+
+// Make stream dst wait for everything queued so far on the extraction streams
+// (the context stream, stream2 and the pipeline part streams).
+static int order_after_extraction(orbx_ctx* ctx, hipStream_t dst)
+{
+    const hipStream_t S[orbx_ctx::kMaxWays] = {ctx->stream, ctx->stream2, ctx->xstreams[0], ctx->xstreams[1]};
+    for (int i = 0; i < orbx_ctx::kMaxWays; i++) {
+        if (!S[i] || S[i] == dst) continue;
+        ORBX_HIP_CHECK(hipEventRecord(ctx->ev_now[i], S[i]));
+        ORBX_HIP_CHECK(hipStreamWaitEvent(dst, ctx->ev_now[i], 0));
+    }
+    return ORBX_OK;
+}
+
+static void drop_single_graph(orbx_ctx* ctx)
+{
+    if (ctx->one_exec) (void)hipGraphExecDestroy(ctx->one_exec);
+    if (ctx->one_graph) (void)hipGraphDestroy(ctx->one_graph);
+    ctx->one_exec = nullptr;
+    ctx->one_graph = nullptr;
+    ctx->one_key = 0;
 }
 
 static int check_errors(orbx_ctx* ctx)
@@ -187,6 +210,8 @@ static int check_errors(orbx_ctx* ctx)
 extern "C" {
 
 const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+
+int orbx_abi_version(void) { return ORBX_ABI_VERSION; }
 
 /* Diagnostics (not in include/orbx.h): the device error flags of the last
  * batch without clearing them (1: a cell list overflowed its capacity,
@@ -262,8 +287,11 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
         if (hipStreamCreateWithFlags(&ctx->xstreams[i], hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays; i++)
         if (hipEventCreateWithFlags(&ctx->ev_part_fast[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ctx->ev_part_done[i], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&ctx->ev_part_done[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->ev_now[i], hipEventDisableTiming) != hipSuccess)
             r = ORBX_ERR_HIP;
+    for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxUploads; i++)
+        if (hipEventCreateWithFlags(&ctx->ev_upload[i], hipEventDisableTiming) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.levels, kMaxLevels);
     if (r == ORBX_OK) r = realloc_dev(ctx->dgeom.umax, kHalfPatch + 1);
     if (r == ORBX_OK) r = realloc_dev(ctx->level_count, (size_t)S * nlevels);
@@ -297,6 +325,15 @@ void orbx_destroy(orbx_ctx* ctx)
     for (hipStream_t x : ctx->xstreams)
         if (x) (void)hipStreamSynchronize(x);
     if (ctx->mstream) (void)hipStreamSynchronize(ctx->mstream);
+    if (ctx->ustream) (void)hipStreamSynchronize(ctx->ustream);
+    drop_single_graph(ctx);
+    if (ctx->one_in) (void)hipHostFree(ctx->one_in);
+    if (ctx->one_out) (void)hipHostFree(ctx->one_out);
+    for (auto e : ctx->ev_now)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev_upload)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->ustream) (void)hipStreamDestroy(ctx->ustream);
     for (auto& t : ctx->timers) {
         for (auto e : t.start) hipEventDestroy(e);
         for (auto e : t.stop) hipEventDestroy(e);
@@ -572,12 +609,201 @@ int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
         *n_out = 0;
         return ORBX_OK;
     }
-    if (w < 0 || h < 0) return ORBX_ERR_ARG;
-    int r = orbx_dev_upload(ctx, 0, 1, img, w, h, stride);
+    if (w < 0 || h < 0 || stride < (size_t)w) return ORBX_ERR_ARG;
+    if (ctx->launch_mode == 0 || ctx->timing) {
+        // stream launches: pageable upload, the extraction chain, read-backs
+        int r = orbx_dev_upload(ctx, 0, 1, img, w, h, stride);
+        if (r != ORBX_OK) return r;
+        if ((r = orbx_dev_extract(ctx, 0, 1)) != ORBX_OK) return r;
+        if ((r = orbx_dev_sync(ctx)) != ORBX_OK) return r;
+        return orbx_dev_read_features(ctx, 0, kps, desc, cap, n_out);
+    }
+    // One graph launch per call: the image goes through a page-locked staging
+    // buffer, the outputs come back into another (count, error flags,
+    // nfeatures keypoint records and descriptors), one synchronisation.
+    ctx_enter(ctx);
+    int r = set_geometry(ctx, w, h);
     if (r != ORBX_OK) return r;
-    if ((r = orbx_dev_extract(ctx, 0, 1)) != ORBX_OK) return r;
-    if ((r = orbx_dev_sync(ctx)) != ORBX_OK) return r;
-    return orbx_dev_read_features(ctx, 0, kps, desc, cap, n_out);
+    const size_t nf = ctx->geom.nfeatures, in_bytes = (size_t)w * h;
+    const size_t o_kps = 64, o_desc = o_kps + nf * sizeof(orbx_keypoint), out_bytes = o_desc + nf * 32;
+    if (in_bytes > ctx->one_in_bytes) {
+        drop_single_graph(ctx);
+        if (ctx->one_in) (void)hipHostFree(ctx->one_in);
+        ctx->one_in = nullptr;
+        ctx->one_in_bytes = 0;
+        if (hipHostMalloc(&ctx->one_in, in_bytes, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_NOMEM;
+        ctx->one_in_bytes = in_bytes;
+    }
+    if (out_bytes > ctx->one_out_bytes) {
+        drop_single_graph(ctx);
+        if (ctx->one_out) (void)hipHostFree(ctx->one_out);
+        ctx->one_out = nullptr;
+        ctx->one_out_bytes = 0;
+        if (hipHostMalloc(&ctx->one_out, out_bytes, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_NOMEM;
+        ctx->one_out_bytes = out_bytes;
+    }
+    // everything a captured launch sequence depends on
+    const unsigned long long key = (unsigned long long)ctx->launch_mode | (unsigned long long)ctx->geom_gen << 2 |
+                                   (unsigned long long)ctx->fp_contract << 33 |
+                                   (unsigned long long)ctx->nth_pivot << 34 | (unsigned long long)ctx->pyr_mode << 35 |
+                                   (unsigned long long)ctx->fast_chunk << 37;
+    // the call's device work on the context stream: the frame into slot 0
+    // (modes 1 and 3; mode 2 reads the staging buffer in place), the
+    // single-frame extraction launches, the read-back kernel
+    uint8_t* out_host = static_cast<uint8_t*>(ctx->one_out);
+    auto enqueue = [&]() -> int {
+        int cr = ORBX_OK;
+        if (ctx->launch_mode != 2 &&
+            hipMemcpyAsync(ctx->frames, ctx->one_in, in_bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            cr = ORBX_ERR_HIP;
+        ctx->frames_src = ctx->launch_mode == 2 ? static_cast<const uint8_t*>(ctx->one_in) : nullptr;
+        ctx->single_frame = true;
+        if (cr == ORBX_OK) cr = launch_extract(ctx, 0, 1);
+        ctx->frames_src = nullptr;
+        ctx->single_frame = false;
+        if (cr == ORBX_OK) cr = launch_pack_single(ctx, out_host, ctx->stream);
+        return cr;
+    };
+    if (ctx->launch_mode != 3 && (!ctx->one_exec || ctx->one_key != key)) {
+        drop_single_graph(ctx);
+        if (ctx->pyr_mode == 1) ensure_pyramid_plan(ctx);   // plans and uploads synchronously: not inside a capture
+        ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        ORBX_HIP_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        const int cr = enqueue();
+        hipGraph_t graph = nullptr;
+        const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+        if (cr != ORBX_OK || ec != hipSuccess || !graph) {
+            if (graph) (void)hipGraphDestroy(graph);
+            (void)hipGetLastError();
+            return cr != ORBX_OK ? cr : ORBX_ERR_HIP;
+        }
+        ctx->one_graph = graph;
+        if (hipGraphInstantiate(&ctx->one_exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+            drop_single_graph(ctx);
+            return ORBX_ERR_HIP;
+        }
+        ctx->one_key = key;
+    }
+    uint8_t* in = static_cast<uint8_t*>(ctx->one_in);
+    if (stride == (size_t)w) {
+        std::memcpy(in, img, in_bytes);
+    } else {
+        for (int y = 0; y < h; y++) std::memcpy(in + (size_t)y * w, img + (size_t)y * stride, (size_t)w);
+    }
+    if (ctx->launch_mode == 3) {
+        const int cr = enqueue();
+        if (cr != ORBX_OK) return cr;
+    } else {
+        // host-side effects of launch_extract that a graph replay does not repeat
+        if (!ctx->bow_ready.empty()) ctx->bow_ready[0] = 0;
+        ctx->last_first = 0;
+        ctx->last_count = 1;
+        ORBX_HIP_CHECK(hipGraphLaunch(ctx->one_exec, ctx->stream));
+    }
+    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const uint8_t* out = static_cast<const uint8_t*>(ctx->one_out);
+    int32_t n = 0, flags = 0;
+    std::memcpy(&n, out, 4);
+    std::memcpy(&flags, out + 4, 4);
+    if (flags) {
+        (void)hipMemset(ctx->error_flags, 0, sizeof(int32_t));
+        return ORBX_ERR_CAPACITY;
+    }
+    *n_out = n;
+    if (n > cap) return ORBX_ERR_CAPACITY;
+    if (n > 0 && kps) std::memcpy(kps, out + o_kps, (size_t)n * sizeof(orbx_keypoint));
+    if (n > 0 && desc) std::memcpy(desc, out + o_desc, (size_t)n * 32);
+    return ORBX_OK;
+}
+
+int orbx_dev_set_image_bounds(orbx_ctx* ctx, const float* bounds)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    if (bounds && !(bounds[1] > bounds[0] && bounds[3] > bounds[2])) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->has_bounds = bounds != nullptr;
+    for (int i = 0; i < 4; i++) ctx->bounds[i] = bounds ? bounds[i] : 0.f;
+    return ORBX_OK;
+}
+
+int orbx_set_launch_mode(orbx_ctx* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 3) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->launch_mode = mode;
+    return ORBX_OK;
+}
+
+int orbx_get_launch_mode(const orbx_ctx* ctx) { return ctx ? ctx->launch_mode : ORBX_ERR_ARG; }
+
+int orbx_host_alloc(size_t bytes, void** out)
+{
+    if (!out || bytes == 0) return ORBX_ERR_ARG;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return ORBX_ERR_NOMEM;
+    }
+    return ORBX_OK;
+}
+
+void orbx_host_free(void* p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
+int orbx_dev_upload_async(orbx_ctx* ctx, int first, int count, const uint8_t* imgs, int w, int h, size_t stride)
+{
+    if (!ctx || !imgs || count <= 0 || first < 0 || first + count > ctx->slots || stride < (size_t)w) return ORBX_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    if (w != ctx->geom_w || h != ctx->geom_h) return orbx_dev_upload(ctx, first, count, imgs, w, h, stride);
+    if (!ctx->ustream && hipStreamCreateWithFlags(&ctx->ustream, hipStreamNonBlocking) != hipSuccess) {
+        ctx->ustream = nullptr;
+        return ORBX_ERR_HIP;
+    }
+    // the slots' previous frames are read by extractions queued before this
+    // call: the copy starts after them
+    int r = order_after_extraction(ctx, ctx->ustream);
+    if (r != ORBX_OK) return r;
+    uint8_t* dst = ctx->frames + (size_t)first * w * h;
+    if (stride == (size_t)w)   // one linear copy (a 2-D copy of w-byte rows is much slower)
+        ORBX_HIP_CHECK(hipMemcpyAsync(dst, imgs, (size_t)w * h * count, hipMemcpyHostToDevice, ctx->ustream));
+    else
+        ORBX_HIP_CHECK(hipMemcpy2DAsync(dst, (size_t)w, imgs, stride, (size_t)w, (size_t)h * count, hipMemcpyHostToDevice,
+                                        ctx->ustream));
+    if (ctx->n_uploads == orbx_ctx::kMaxUploads) {   // table full: the context stream takes the oldest
+        ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->uploads[0].done, 0));
+        for (int i = 1; i < ctx->n_uploads; i++) ctx->uploads[i - 1] = ctx->uploads[i];
+        ctx->n_uploads--;
+    }
+    hipEvent_t ev = ctx->ev_upload[ctx->next_upload];
+    ctx->next_upload = (ctx->next_upload + 1) % orbx_ctx::kMaxUploads;
+    ORBX_HIP_CHECK(hipEventRecord(ev, ctx->ustream));
+    ctx->uploads[ctx->n_uploads++] = orbx_ctx::PendingMatch{first, first + count, ev};
+    return ORBX_OK;
+}
+
+int orbx_dev_download_async(orbx_ctx* ctx, int first, int count, orbx_keypoint* kps, uint8_t* desc, int32_t* n_kps,
+                            int32_t* matches12, int32_t* n_matches)
+{
+    if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots) return ORBX_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    // after the extraction of the slots (every stream it may run on) and, mstream
+    // being in order, after their queued match
+    int r = order_after_extraction(ctx, ctx->mstream);
+    if (r != ORBX_OK) return r;
+    const size_t nf = ctx->geom.nfeatures, s0 = first, n = count;
+    const hipStream_t st = ctx->mstream;
+    if (kps)
+        ORBX_HIP_CHECK(hipMemcpyAsync(kps, ctx->out_kps + s0 * nf, n * nf * sizeof(orbx_keypoint), hipMemcpyDeviceToHost, st));
+    if (desc) ORBX_HIP_CHECK(hipMemcpyAsync(desc, ctx->out_desc + s0 * nf * 32, n * nf * 32, hipMemcpyDeviceToHost, st));
+    if (n_kps) ORBX_HIP_CHECK(hipMemcpyAsync(n_kps, ctx->out_n + s0, n * 4, hipMemcpyDeviceToHost, st));
+    if (matches12)
+        ORBX_HIP_CHECK(hipMemcpyAsync(matches12, ctx->match12 + s0 * nf, n * nf * 4, hipMemcpyDeviceToHost, st));
+    if (n_matches) ORBX_HIP_CHECK(hipMemcpyAsync(n_matches, ctx->match_n + s0, n * 4, hipMemcpyDeviceToHost, st));
+    // a later extraction of these slots waits for the copies
+    ORBX_HIP_CHECK(push_pending(ctx, first, first + count));
+    return ORBX_OK;
 }
 
 int orbx_extract_batch(orbx_ctx* ctx, int B, const uint8_t* const* imgs, int w, int h, size_t stride,

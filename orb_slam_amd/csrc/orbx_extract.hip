@@ -78,6 +78,7 @@ struct ExtractArgs {
     int32_t* out_n;
     int32_t* error_flags;
     int32_t* retain_scratch;        // slots x (list_entries + 4 ncells): global nth_element scratch
+    const int4* blur_tiles;         // k_blur work blocks (also the blur tail of k_fast_cells<..., true>)
     uint64_t* cell_keys64;          // HARRIS_SCORE: Harris-keyed cell lists (as cell_lists)
     uint64_t* level_keys64;         // HARRIS_SCORE: Harris-keyed level lists (as level_keys)
     int harris;                     // scoreType == HARRIS_SCORE
@@ -437,12 +438,18 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
 // row, last computed ROI row); a band writes its owned rows' padded rows and
 // the border rows that reflect to them.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pyr_cascade(ExtractArgs a, const int4* plan, int buf_x)
+// T threads per workgroup: 256 in batches (several bands per CU), 1024 for
+// orbx_extract's single frame, whose ~23 bands leave most CUs idle: more
+// threads per band shorten each level's row loop.
+#ifndef ORBX_CASCADE_SINGLE_THREADS
+#define ORBX_CASCADE_SINGLE_THREADS 1024
+#endif
+template <int T>
+__global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* plan, int buf_x)
 {
     extern __shared__ uint4 s_dyn[];
     uint8_t* const lds = reinterpret_cast<uint8_t*>(s_dyn);   // buffers: [0, buf_x) even levels, then odd
     const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-    constexpr int T = 256;
     uint8_t* pyr = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
     const uint8_t* img = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
     int sc0 = 0, sstride = 0;   // the previous level's first computed ROI row and row pitch
@@ -733,11 +740,23 @@ constexpr int kDiagRepeat[4] = {ORBX_DIAG_REPEAT};
 // before the current cell is scored.  The compiler waits for that copy at the
 // scoring's first LDS atomic (the `nz` bits), so the copy overlaps only the
 // compass work before the first survivor batch.
-template <int kP, int kThreads = 256, bool kBanded = false, bool kChunk = false>
+__device__ __forceinline__ void blur_block(const ExtractArgs& a, const int4* tiles, int bx, int f);
+
+// kBlurTail (orbx_extract's single-frame graph): the grid carries the blur's
+// work blocks after the cells (blockIdx.x >= ncells), so FAST and the blur,
+// which both read only the raw pyramid, are one launch.
+template <int kP, int kThreads = 256, bool kBanded = false, bool kChunk = false, bool kBlurTail = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
     ExtractArgs a, int tile_bytes, int band_rows, int chunk)
 {
     static_assert(!kChunk || (kP > 0 && !kBanded), "chunked FAST takes whole cells at a template pitch");
+    static_assert(!kBlurTail || (!kChunk && kThreads == kBlurItems), "the blur tail runs 256-thread blur blocks");
+    if constexpr (kBlurTail) {
+        if ((int)blockIdx.x >= a.ncells) {
+            blur_block(a, a.blur_tiles, (int)blockIdx.x - a.ncells, (int)blockIdx.y);
+            return;
+        }
+    }
     constexpr int kBlock = kThreads, kWaves = kThreads / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratchN<kWaves> bs;
@@ -1181,9 +1200,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         prefetch(c0, smem);
         for (int cell = c0; cell < c1; cell++) {
             const int k = cell - c0;
-            // this cell's tile landed (the barrier waits for the copies), S'
-            // and nz are clear, and the previous cell is done with the other
-            // buffer; the next cell's copy is issued before this cell's scoring
+            // this cell's tile landed, S' and nz are clear, and the previous
+            // cell is done with the other buffer; the next cell's copy is
+            // issued before this cell's scoring.  A workgroup barrier does not
+            // wait for vector-memory counters: each wave drains its own
+            // global_load_lds copies (vmcnt) first, then the barrier makes
+            // every wave's part of the tile visible to all.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (cell + 1 < c1) prefetch(cell + 1, smem + ((k + 1) & 1) * tile_bytes);
             process(cell, smem + (k & 1) * tile_bytes, sm, true);
@@ -1434,15 +1457,15 @@ __device__ inline void blur_hsum(const uint8_t* row, int x, int hs[4])
     blur_hsum_w(w[-1], w[0], w[1], hs);
 }
 
-__global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
+// One blur work block (bx) of frame f.
+__device__ __forceinline__ void blur_block(const ExtractArgs& a, const int4* tiles, const int bx, const int f)
 {
     // One wave per (row strip, chunk of kBlurChunkCols dword columns): lane
     // l holds dword 62 c - 1 + l of each row, lanes 0 and 63 only as halo.
     // A row is one dword load per lane; the left / right neighbour dwords of
     // the horizontal taps come from the adjacent lanes (DPP wave_shr:1 /
     // wave_shl:1) instead of two more loads.
-    const int f = blockIdx.y;
-    const int4 tl = cget(tiles, (int)blockIdx.x);   // level, first wave item, chunks per row, strips
+    const int4 tl = cget(tiles, bx);   // level, first wave item, chunks per row, strips
     const int wi = tl.y + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wi >= tl.z * tl.w) return;       // whole waves
     const LevelGeom L = cget(a.levels, tl.x);
@@ -1573,6 +1596,11 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
         }
     }
     copy_rows(yb, y1);
+}
+
+__global__ __launch_bounds__(256) void k_blur(ExtractArgs a, const int4* tiles)
+{
+    blur_block(a, tiles, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -1885,13 +1913,18 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
 {
     const Geometry& g = ctx->geom;
     for (int sl = first; sl < first + count && sl < (int)ctx->bow_ready.size(); sl++) ctx->bow_ready[sl] = 0;
+    // frames still being uploaded (orbx_dev_upload_async): every part and
+    // half below starts on, or is released from, the context stream
+    wait_uploads_overlap(ctx, first, count, ctx->stream);
     ExtractArgs a;
     a.levels = ctx->dgeom.levels;
     a.cells = ctx->dgeom.cells;
     a.res_cols = ctx->dgeom.res_cols;
     a.res_rows = ctx->dgeom.res_rows;
     a.umax = ctx->dgeom.umax;
-    a.frames = ctx->frames;
+    // the single-frame graph may read its frame where the host staged it
+    // (page-locked, device-mapped: orbx_extract's zero-copy launch mode)
+    a.frames = ctx->frames_src ? ctx->frames_src : ctx->frames;
     // work buffers are per slot (frame f of this pass uses slot first + f):
     // batches on disjoint slots can be in flight at the same time
     a.pyr_raw = ctx->pyr_raw + (size_t)first * g.frame_pyr_bytes;
@@ -1905,6 +1938,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.out_n = ctx->out_n;
     a.error_flags = ctx->error_flags;
     a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
+    a.blur_tiles = ctx->blur_tiles;
     a.harris = ctx->harris;
     a.fp_contract = ctx->fp_contract;
     a.nth_pivot = ctx->nth_pivot;
@@ -1935,11 +1969,19 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_end(ctx, "pyramid", st);
             return;
         }
-        if (ctx->pyr_mode == 2 && g.cascade_bands > 0) {   // the whole raw pyramid in one launch
+        // the whole raw pyramid in one launch: pyramid mode 2, and the
+        // default of orbx_extract's single-frame graph (its lowest latency)
+        if ((ctx->pyr_mode == 2 || (ctx->single_frame && ctx->pyr_mode == 0)) && g.cascade_bands > 0) {
             timer_begin(ctx, "resize", st);
-            for (int rep = 0; rep < kDiagRepeat[0]; rep++)
-                hipLaunchKernelGGL(k_pyr_cascade, dim3(g.cascade_bands, nb), dim3(256), g.cascade_lds, st, x, ctx->cascade,
-                                   g.cascade_buf_x);
+            for (int rep = 0; rep < kDiagRepeat[0]; rep++) {
+                if (ctx->single_frame)
+                    hipLaunchKernelGGL(k_pyr_cascade<ORBX_CASCADE_SINGLE_THREADS>, dim3(g.cascade_bands, nb),
+                                       dim3(ORBX_CASCADE_SINGLE_THREADS), g.cascade_lds, st, x, ctx->cascade,
+                                       g.cascade_buf_x);
+                else
+                    hipLaunchKernelGGL(k_pyr_cascade<256>, dim3(g.cascade_bands, nb), dim3(256), g.cascade_lds, st, x,
+                                       ctx->cascade, g.cascade_buf_x);
+            }
             timer_end(ctx, "resize", st);
             return;
         }
@@ -1978,9 +2020,13 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         }
     };
     // FAST .. describe over nb frames on stream st (after their pyramid).
-    // parts: 1 = FAST, 2 = retain, 4 = blur + describe
+    // parts: 1 = FAST, 2 = retain, 4 = blur, 8 = describe
+    // 16 = FAST with the blur's blocks in the same launch where the FAST
+    // instance takes them (whole cells at a template pitch), else FAST then blur
     auto run_rest = [&](const ExtractArgs& x, int nb, hipStream_t st, int parts) {
-        if (parts & 1) {
+        const bool tail = (parts & 16) && !fused;
+        bool tail_done = false;
+        if (parts & (1 | 16)) {
         timer_begin(ctx, "fast", st);
         {
             // widest aligned cell row and tallest cell pick the tile pitch
@@ -2010,6 +2056,12 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 const int lds = fast_lds_bytes(bytes);
                 hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows, 1);
             };
+            auto fast_tail = [&](auto kern, int bytes) {
+                const int lds = fast_lds_bytes(bytes);
+                hipLaunchKernelGGL(kern, dim3((int)g.cells.size() + ctx->blur_tiles_n, nb), dim3(256), lds, st, x, bytes,
+                                   0, 1);
+                tail_done = true;
+            };
             // whole cells, `chunk` per workgroup, next tile prefetched (a
             // second tile buffer)
             int chunk = ctx->fast_chunk;
@@ -2037,15 +2089,19 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             // two tile buffers must fit the CU's LDS with the static queues
             auto chunk_fits = [&](int b) { return fast_lds_bytes(b) + b + fast_static_lds(false) <= 160 * 1024; };
             if (fits(96)) {
-                if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<96, 256, false, true>, bytes);
+                if (tail) fast_tail(k_fast_cells<96, 256, false, false, true>, bytes);
+                else if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<96, 256, false, true>, bytes);
                 else fast(k_fast_cells<96>, bytes, 0, 256);
             } else if (fits(144)) {
+                if (tail) fast_tail(k_fast_cells<144, 256, false, false, true>, bytes);
+                else
                 for (int rep = 0; rep < kDiagRepeat[3]; rep++) {
                     if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<144, 256, false, true>, bytes);
                     else fast(k_fast_cells<144>, bytes, 0, 256);
                 }
             } else if (fits(208)) {
-                if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<208, 256, false, true>, bytes);
+                if (tail) fast_tail(k_fast_cells<208, 256, false, false, true>, bytes);
+                else if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<208, 256, false, true>, bytes);
                 else fast(k_fast_cells<208>, bytes, 0, 256);
             }
             else if (fits_banded(336)) fast(k_fast_cells<336, kFastWideThreads, true>, bytes, br, kFastWideThreads);
@@ -2082,13 +2138,13 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         }
         timer_end(ctx, "retain", st);
         }
-        if (!(parts & 4)) return;
-        if (!fused) {
+        if ((parts & 4 || (tail && !tail_done)) && !fused) {
             timer_begin(ctx, "blur", st);
             for (int rep = 0; rep < kDiagRepeat[1]; rep++)
                 hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);
             timer_end(ctx, "blur", st);
         }
+        if (!(parts & 8)) return;
         timer_begin(ctx, "describe", st);
         const dim3 dgrid((g.nfeatures + 2 * kWaves - 1) / (2 * kWaves), xcd_frames(nb));
         for (int rep = 0; rep < kDiagRepeat[2]; rep++) {
@@ -2101,7 +2157,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     };
     auto run = [&](const ExtractArgs& x, int nb, hipStream_t st) {
         run_pyramid(x, nb, st);
-        run_rest(x, nb, st, 7);
+        run_rest(x, nb, st, 15);
     };
     // Matching of slot s against prev(s) (the rule of orbx_dev_match_prev),
     // for the slots of [lo, hi) whose predecessor lies in [plo, phi) (all of
@@ -2185,7 +2241,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 run_pyramid(b, n, S[i]);
                 run_rest(b, n, S[i], 1);
                 ORBX_HIP_CHECK(hipEventRecord(ctx->ev_part_fast[i], S[i]));
-                run_rest(b, n, S[i], 6);
+                run_rest(b, n, S[i], 14);
                 ORBX_HIP_CHECK(hipEventRecord(ctx->ev_part_done[i], S[i]));
                 ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->mstream, ctx->ev_part_done[i], 0));
             }
@@ -2199,24 +2255,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         // the match reads the outputs of the batch's sequences
         const int q = m->seq_len;
         const int lo = (first / q) * q, hi = ((first + count + q - 1) / q) * q;
-        if (ctx->n_pend == orbx_ctx::kMaxPending) {   // table full: retire the oldest
-            ORBX_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->pend[0].done, 0));
-            for (int i = 1; i < ctx->n_pend; i++) ctx->pend[i - 1] = ctx->pend[i];
-            ctx->n_pend--;
-        }
-        // an event not referenced by any pending entry
-        hipEvent_t ev = nullptr;
-        for (int t = 0; t < orbx_ctx::kMaxPending && !ev; t++) {
-            hipEvent_t c = ctx->ev_match[(ctx->next_ev + t) % orbx_ctx::kMaxPending];
-            bool used = false;
-            for (int i = 0; i < ctx->n_pend; i++) used = used || ctx->pend[i].done == c;
-            if (!used) {
-                ev = c;
-                ctx->next_ev = (ctx->next_ev + t + 1) % orbx_ctx::kMaxPending;
-            }
-        }
-        ORBX_HIP_CHECK(hipEventRecord(ev, ctx->mstream));
-        ctx->pend[ctx->n_pend++] = orbx_ctx::PendingMatch{lo, hi, ev};
+        ORBX_HIP_CHECK(push_pending(ctx, lo, hi));
         if (err != ORBX_OK) return err;
         if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
         return ORBX_OK;
@@ -2250,6 +2289,14 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         match_runs(first + n0, first + count, first, first + n0, ctx->stream);
         match_runs(first + n0, first + count, first + count, 0x7fffffff, ctx->stream);
         match_runs(first + n0, first + count, -0x7fffffff, first, ctx->stream);
+    } else if (ctx->single_frame && count == 1) {
+        // one frame (orbx_extract's captured graph), for latency: the raw
+        // pyramid as one cascade launch, FAST with the blur's blocks in its
+        // grid (a branch for the blur measured slower: the cross-queue join
+        // cost more than the blur), then retain and describe
+        run_pyramid(a, 1, ctx->stream);
+        run_rest(a, 1, ctx->stream, 16 | 2 | 8);
+        match_runs(first, first + count, 0, -1, ctx->stream);
     } else {
         run(a, count, ctx->stream);
         match_runs(first, first + count, 0, -1, ctx->stream);
@@ -2257,6 +2304,34 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     if (err != ORBX_OK) return err;
     if (hipGetLastError() != hipSuccess) return ORBX_ERR_HIP;
     return ORBX_OK;
+}
+
+// Single-frame read-back (orbx_extract's graph): slot 0's keypoint count,
+// the device error flags, then its keypoint records and descriptors, stored
+// straight into the page-locked host buffer (header 64 bytes; records at 64;
+// descriptors at 64 + nfeatures * 28).  One launch in place of four copies.
+__global__ __launch_bounds__(1024) void k_pack_single(const int32_t* out_n, const int32_t* flags,
+                                                     const orbx_keypoint* kps, const uint8_t* desc, int nf,
+                                                     uint8_t* host)
+{
+    const int n = min(max(out_n[0], 0), nf);
+    if (threadIdx.x == 0) {
+        reinterpret_cast<int32_t*>(host)[0] = out_n[0];
+        reinterpret_cast<int32_t*>(host)[1] = flags[0];
+    }
+    const uint32_t* ks = reinterpret_cast<const uint32_t*>(kps);
+    uint32_t* kd = reinterpret_cast<uint32_t*>(host + 64);
+    for (int i = threadIdx.x; i < n * 7; i += blockDim.x) kd[i] = ks[i];
+    const uint4* ds = reinterpret_cast<const uint4*>(desc);
+    uint4* dd = reinterpret_cast<uint4*>(host + 64 + (size_t)nf * sizeof(orbx_keypoint));
+    for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dd[i] = ds[i];
+}
+
+int launch_pack_single(orbx_ctx* ctx, uint8_t* host, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_pack_single, dim3(1), dim3(1024), 0, st, ctx->out_n, ctx->error_flags, ctx->out_kps,
+                       ctx->out_desc, ctx->geom.nfeatures, host);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
 }
 
 }  // namespace orbx

@@ -217,7 +217,9 @@ struct orbx_ctx {
     // extract_match call runs on mstream while later calls extract other
     // slots.  pend[] lists the matches queued on mstream, oldest first: the
     // slots each reads and the event recorded after it.
-    static constexpr int kMaxPending = 4;
+    // pend[] also lists the asynchronous read-backs of orbx_dev_download_async
+    // (queued on mstream too): an extraction rewriting those slots waits.
+    static constexpr int kMaxPending = 8;
     struct PendingMatch {
         int lo, hi;
         hipEvent_t done;
@@ -228,6 +230,30 @@ struct orbx_ctx {
     PendingMatch pend[kMaxPending] = {};
     int n_pend = 0, next_ev = 0;
     bool async_match = false;
+    // Host-fed pipeline (orbx_dev_upload_async): frame uploads queued on
+    // ustream (created on first use), each ordered after every extraction
+    // queued before it; an extraction of slots an upload writes waits for it.
+    static constexpr int kMaxUploads = 4;
+    hipStream_t ustream = nullptr;
+    hipEvent_t ev_now[kMaxWays] = {};          // "extraction streams so far" marks
+    hipEvent_t ev_upload[kMaxUploads] = {};
+    PendingMatch uploads[kMaxUploads] = {};
+    int n_uploads = 0, next_upload = 0;
+    // Single-frame host path (orbx_extract): page-locked staging for the
+    // image and the outputs, and the whole call (upload, extraction launches,
+    // read-back) captured once per configuration as a hipGraph
+    // (orbx_set_launch_mode).
+    int launch_mode = 1;                       // 0: stream launches, 1: graph, 2: graph reading the staged frame in place
+    const uint8_t* frames_src = nullptr;       // launch_extract's frame source override (graph capture of mode 2)
+    bool single_frame = false;                // launch_extract: one frame, latency-first launches (graph capture)
+    void* one_in = nullptr;
+    size_t one_in_bytes = 0;
+    void* one_out = nullptr;
+    size_t one_out_bytes = 0;
+    hipGraph_t one_graph = nullptr;
+    hipGraphExec_t one_exec = nullptr;
+    unsigned long long one_key = 0;            // configuration the graph was captured for
+    unsigned geom_gen = 0;                     // bumped whenever set_geometry changes the buffers
     bool stream_dirty = true;   // the context stream got work outside the async pipeline
     orbx::Geometry geom;
     orbx::DeviceGeometry dgeom;
@@ -275,6 +301,10 @@ struct orbx_ctx {
     orbx::PyrWave* d_pyr_waves = nullptr;
     int cap_pyr_sched = 0;
     int last_first = 0, last_count = 0;   // batch of the most recent extract
+    // Frame::ComputeImageBounds of the slots' keypoints (orbx_dev_set_image_bounds;
+    // has_bounds 0: 0..w x 0..h, the undistorted case) for the device matchers
+    int has_bounds = 0;
+    float bounds[4] = {0.f, 0.f, 0.f, 0.f};
     // generic scratch for the one-shot matcher / BA entry points
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -320,6 +350,9 @@ struct MatchSpec {
     float nnratio;
 };
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nullptr);
+// orbx_extract's read-back kernel: slot 0's count, error flags, keypoints and
+// descriptors into the page-locked buffer `host` (layout in orbx_extract.hip)
+int launch_pack_single(orbx_ctx* ctx, uint8_t* host, hipStream_t st);
 // orbx_pyramid.hip: plan of the fused pyramid + blur kernel for geometry g
 // (plan.ok false when it does not apply: tiny levels, LDS or job overflow),
 // its upload, and its launch over nb frames (frame f reads slot first_slot + f
@@ -354,6 +387,50 @@ inline void ctx_enter(orbx_ctx* ctx)
         (void)hipStreamWaitEvent(ctx->stream, ctx->pend[ctx->n_pend - 1].done, 0);
         ctx->n_pend = 0;
     }
+    if (ctx->n_uploads > 0) {   // ustream is in order too
+        (void)hipStreamWaitEvent(ctx->stream, ctx->uploads[ctx->n_uploads - 1].done, 0);
+        ctx->n_uploads = 0;
+    }
+}
+
+// Record the end of the work just queued on mstream as a pending entry that
+// reads slots [lo, hi) (a match or an asynchronous read-back).
+inline hipError_t push_pending(orbx_ctx* ctx, int lo, int hi)
+{
+    if (ctx->n_pend == orbx_ctx::kMaxPending) {   // table full: retire the oldest
+        hipError_t e = hipStreamWaitEvent(ctx->stream, ctx->pend[0].done, 0);
+        if (e != hipSuccess) return e;
+        for (int i = 1; i < ctx->n_pend; i++) ctx->pend[i - 1] = ctx->pend[i];
+        ctx->n_pend--;
+    }
+    // an event not referenced by any pending entry
+    hipEvent_t ev = nullptr;
+    for (int t = 0; t < orbx_ctx::kMaxPending && !ev; t++) {
+        hipEvent_t c = ctx->ev_match[(ctx->next_ev + t) % orbx_ctx::kMaxPending];
+        bool used = false;
+        for (int i = 0; i < ctx->n_pend; i++) used = used || ctx->pend[i].done == c;
+        if (!used) {
+            ev = c;
+            ctx->next_ev = (ctx->next_ev + t + 1) % orbx_ctx::kMaxPending;
+        }
+    }
+    hipError_t e = hipEventRecord(ev, ctx->mstream);
+    if (e != hipSuccess) return e;
+    ctx->pend[ctx->n_pend++] = orbx_ctx::PendingMatch{lo, hi, ev};
+    return hipSuccess;
+}
+
+// Order stream st after the queued uploads that write a slot of
+// [first, first + count) (orbx_dev_upload_async), and forget them.
+inline void wait_uploads_overlap(orbx_ctx* ctx, int first, int count, hipStream_t st)
+{
+    int last = -1;
+    for (int i = 0; i < ctx->n_uploads; i++)
+        if (first < ctx->uploads[i].hi && first + count > ctx->uploads[i].lo) last = i;
+    if (last < 0) return;
+    (void)hipStreamWaitEvent(st, ctx->uploads[last].done, 0);
+    for (int i = last + 1; i < ctx->n_uploads; i++) ctx->uploads[i - last - 1] = ctx->uploads[i];
+    ctx->n_uploads -= last + 1;
 }
 
 // Order ctx->stream after every pending match that reads a slot of

@@ -350,13 +350,15 @@ int launch_match_prev(orbx_ctx* ctx, int first, int count, int seq_len, int wind
     a.window = window;
     a.nnratio = nnratio;
     a.check_ori = check_ori;
-    // Frame::ComputeImageBounds without distortion (src/Frame.cc:341-347)
-    a.min_x = 0.f;
-    a.max_x = (float)g.w;
-    a.min_y = 0.f;
-    a.max_y = (float)g.h;
-    a.gw_inv = static_cast<float>(kGridCols) / static_cast<float>(g.w - 0);
-    a.gh_inv = static_cast<float>(kGridRows) / static_cast<float>(g.h - 0);
+    // Frame::ComputeImageBounds (src/Frame.cc:320-348): the context's bounds
+    // of undistorted keypoints (orbx_dev_set_image_bounds), else the image
+    // (:341-347); the grid cell scales of src/Frame.cc:76-77
+    a.min_x = ctx->has_bounds ? ctx->bounds[0] : 0.f;
+    a.max_x = ctx->has_bounds ? ctx->bounds[1] : (float)g.w;
+    a.min_y = ctx->has_bounds ? ctx->bounds[2] : 0.f;
+    a.max_y = ctx->has_bounds ? ctx->bounds[3] : (float)g.h;
+    a.gw_inv = static_cast<float>(kGridCols) / (a.max_x - a.min_x);
+    a.gh_inv = static_cast<float>(kGridRows) / (a.max_y - a.min_y);
     // candidates = keypoints of octave 0, at most the level-0 quota
     a.cap_c = std::min(g.levels[0].n_desired, g.nfeatures);
     if (a.cap_c > kInitMaxCand) return ORBX_ERR_UNSUPPORTED;

@@ -621,7 +621,7 @@ int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr
     const Geometry& g = ctx->geom;
     const PyrPlan& p = ctx->pyr;
     PyrArgs a;
-    a.frames = ctx->frames;
+    a.frames = ctx->frames_src ? ctx->frames_src : ctx->frames;
     a.pyr_raw = pyr_raw;
     a.pyr_blur = pyr_blur;
     a.levels = ctx->dgeom.levels;

@@ -44,6 +44,20 @@ class StubContext:
         for i, f in enumerate(np.asarray(frames, np.uint8)):
             self.frames[first + i] = f.copy()
 
+    def upload_async(self, frames, first=0):
+        self.upload(frames, first)
+
+    def download_async(self, first, count, kps=None, desc=None, n_kps=None, m12=None, n_m=None):
+        nf = self.nfeatures
+        for i in range(count):
+            k, d = self.out[first + i]
+            m, nm = self.match[first + i]
+            kps[i * nf:i * nf + len(k)] = k
+            desc[i * nf:i * nf + len(k)] = d
+            n_kps[i] = len(k)
+            m12[i * nf:(i + 1) * nf] = m
+            n_m[i] = nm
+
     def set_split(self, n):
         pass
 
@@ -123,6 +137,17 @@ class StubContext:
         pass
 
 
+class StubHostArray:
+    """orb_slam_amd.HostArray without page-locking (no device here)."""
+
+    def __init__(self, shape, dtype):
+        self.array = np.zeros(shape, dtype)
+
+    def close(self):
+        self.array = None
+
+
 if __name__ == "__main__":
     bench.ox.Context = StubContext
+    bench.ox.HostArray = StubHostArray
     bench.main()

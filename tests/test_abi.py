@@ -61,6 +61,26 @@ def test_context_setters_refuse_null_context():
         ("orbx_dev_set_split", (None, 3)),
         ("orbx_dev_set_async_match", (None, 1)),
         ("orbx_lba_run", (None, 5, 10, None)),
+        ("orbx_set_launch_mode", (None, 1)),
+        ("orbx_get_launch_mode", (None,)),
+        ("orbx_dev_upload_async", (None, 0, 1, None, 640, 480, 640)),
+        ("orbx_dev_download_async", (None, 0, 1, None, None, None, None, None)),
     ]
     for name, args in calls:
         assert getattr(lib, name)(*args) == err_arg, name
+
+
+def test_abi_version_matches_header():
+    """orbx_abi_version() equals the header's ORBX_ABI_VERSION (the adapter
+    refuses a library of another revision)."""
+    text = (ROOT / "include" / "orbx.h").read_text()
+    want = int(re.search(r"#define ORBX_ABI_VERSION (\d+)", text).group(1))
+    assert ox.lib().orbx_abi_version() == want
+
+
+def test_host_alloc_refuses_bad_arguments():
+    lib = ox.lib()
+    out = ctypes.c_void_p()
+    assert lib.orbx_host_alloc(0, ctypes.byref(out)) == -1
+    assert lib.orbx_host_alloc(16, None) == -1
+    lib.orbx_host_free(None)   # no-op

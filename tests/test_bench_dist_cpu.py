@@ -50,6 +50,9 @@ def test_bench_gpus_n_end_to_end(world, workload, batch):
     assert out["check"]["parity_last_step"]["bit_exact"] is True
     assert out["check"]["parity_last_step"]["nth_element_era"].startswith("GCC 4.6-4.8")
     assert out["roofline"]["kernel"] == "fast"
+    # the host-fed leg's read-back equals the device outputs (stubbed here)
+    hi = out["check"]["host_inclusive"]
+    assert hi["host_buffers_equal_device_outputs"] is True and hi["frames_per_s"] > 0
     # the whole-path figure counts every rank's frames
     per = out["path_roofline"]["algorithmic_bytes_per_frame"]
     assert out["path_roofline"]["algorithmic_bytes_per_step"] == per * batch * world

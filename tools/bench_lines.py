@@ -1,5 +1,5 @@
 """Summarise bench JSON lines of one GPU A/B directory: value, ms per step and
-the serialised per-kernel times (python3 tools/ab_show_r04.py gpurun_out/<dir>)."""
+the serialised per-kernel times (python3 tools/bench_lines.py gpurun_out/<dir>)."""
 import json
 import sys
 from pathlib import Path

@@ -1,0 +1,110 @@
+"""Single-call workloads for kernel traces of the drop-in path (run from the
+repo root on the GPU box, under `rocprofv3 --kernel-trace --memory-copy-trace
+--stats`): N calls each of
+
+  extract   orbx_extract on one 640x480 frame (graph launch mode, then stream
+            launches): ORBextractor::operator() as Frame::Frame calls it
+  sfi       orbx_search_for_initialization on two host frame views
+  pose      orbx_pose_optimization on one frame
+  lba       orbx_lba_solve on one 20 KF x 2000 MP problem
+
+usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N]
+"""
+import ctypes
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+import orb_slam_amd as ox  # noqa: E402
+from orb_slam_amd import synth  # noqa: E402
+
+args = sys.argv[1:]
+n = int(args[args.index("--n") + 1]) if "--n" in args else 100
+what = [a for a in args if a in ("extract", "sfi", "pose", "lba")] or ["extract"]
+pyr = [int(v) for v in args[args.index("--pyr") + 1].split(",")] if "--pyr" in args else [0]
+L = ox.lib()
+
+
+def med(fn, k):
+    t = []
+    for i in range(k):
+        t0 = time.perf_counter()
+        fn(i)
+        t.append(time.perf_counter() - t0)
+    return 1e3 * float(np.median(t))
+
+
+if "extract" in what or "sfi" in what:
+    frames = synth.sequence(640, 480, 16, seed=2000)
+    ctx = ox.Context(nfeatures=1000, max_w=640, max_h=480, slots=1)
+    kps = np.zeros(1000, ox.KEYPOINT)
+    desc = np.zeros((1000, 32), np.uint8)
+    nk = ctypes.c_int()
+
+    def ext(i):
+        assert L.orbx_extract(ctx.handle, frames[i % 16].ctypes.data, 640, 480, 640, kps.ctypes.data,
+                              desc.ctypes.data, 1000, ctypes.byref(nk)) == 0
+
+    if "extract" in what:
+        for pm in pyr:
+            ctx.set_pyramid_mode(pm)
+            for mode in (1, 2, 3, 0):
+                ctx.set_launch_mode(mode)
+                print(f"extract pyramid mode {pm} launch mode {mode}: {med(ext, n):.4f} ms median", flush=True)
+        ctx.set_pyramid_mode(0)
+        ctx.set_launch_mode(1)
+    if "sfi" in what:
+        feats = [ctx(frames[i]) for i in range(2)]
+        F1 = ox.frame_view(*feats[0], 640, 480)
+        F2 = ox.frame_view(*feats[1], 640, 480)
+        k1 = feats[0][0]
+        pm = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+        m = np.zeros(len(k1), np.int32)
+        nm = ctypes.c_int()
+
+        def sfi(i):
+            pm[:] = np.stack([k1["x"], k1["y"]], 1)
+            assert L.orbx_search_for_initialization(ctx.handle, ctypes.byref(F1), ctypes.byref(F2), pm.ctypes.data,
+                                                    m.ctypes.data, 100, 0.9, 1, ctypes.byref(nm)) == 0
+
+        print(f"sfi: {med(sfi, n):.4f} ms median", flush=True)
+    ctx.close()
+
+if "pose" in what:
+    from orb_slam_amd import synth_pose as sp
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
+    p, arrs = sp.to_ctypes(sp.make_frame(n_kp=1000, seed=7))
+    w = sp.PoseFrame.from_buffer_copy(p)
+    ni = ctypes.c_int()
+
+    def pose(i):
+        ctypes.memmove(ctypes.addressof(w), ctypes.addressof(p), ctypes.sizeof(w))
+        assert L.orbx_pose_optimization(ctx.handle, ctypes.byref(w), ctypes.byref(ni), None) == 0
+
+    print(f"pose: {med(pose, n):.4f} ms median", flush=True)
+    ctx.close()
+
+if "lba" in what:
+    from orb_slam_amd import synth_ba as sb
+    ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
+    pr = sb.make_problem(n_kf=20, n_points=2000, seed=5)
+    p, arrs = sb.to_ctypes(pr)
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    st = sb.BAStats()
+
+    def lba(i):
+        np.copyto(arrs["pose_q"], pr["pose_q"])
+        np.copyto(arrs["pose_t"], pr["pose_t"])
+        np.copyto(arrs["points"], pr["points"])
+        assert L.orbx_lba_solve(ctx.handle, ctypes.byref(p), 5, 10, None, es.ctypes.data, pb.ctypes.data,
+                                ctypes.byref(st)) == 0
+
+    print(f"lba: {med(lba, max(5, n // 10)):.4f} ms median", flush=True)
+    ctx.close()
+print("ok")
