@@ -36,7 +36,8 @@ extern "C" {
  *      (the `aborts` argument after iters1).
  *   3: single-frame graph path (orbx_set_launch_mode), host-fed pipeline
  *      (orbx_host_alloc, orbx_dev_upload_async, orbx_dev_download_async),
- *      image bounds of device-resident frames (orbx_dev_set_image_bounds);
+ *      image bounds of device-resident frames (orbx_dev_set_image_bounds),
+ *      multi-workgroup single local-BA problems (orbx_lba_set_workgroups);
  *      additions only. */
 #define ORBX_ABI_VERSION 3
 int orbx_abi_version(void);
@@ -702,6 +703,15 @@ typedef struct {
 int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
                    const volatile uint8_t* abort, uint8_t* edge_status,
                    uint8_t* point_bad, orbx_ba_stats* stats);
+
+/* Workgroups that share one problem (orbx_lba_solve, and batches of one):
+ * 0 (default) = automatic (one per 32 points, at most 64, when the reduced
+ * system fits a workgroup's LDS); 1 = one workgroup, as in a batch; n > 1 =
+ * n workgroups.  Every setting gives the same bits (k_lba_split sums in the
+ * single-workgroup kernel's order); more workgroups cut the latency of the
+ * call LocalMapping makes once per keyframe (src/LocalMapping.cc:83). */
+int orbx_lba_set_workgroups(orbx_ctx* ctx, int n);
+int orbx_lba_get_workgroups(const orbx_ctx* ctx);
 
 /* Batched throughput form: P independent problems, one workgroup each.
  * aborts: NULL, or P flags (entries may be NULL), each polled between LM

@@ -138,6 +138,8 @@ def _declare(L):
         "orbx_pose_fetch": ([vp, vp, vp, vp], i),
         "orbx_version": ([], ctypes.c_char_p),
         "orbx_abi_version": ([], i),
+        "orbx_lba_set_workgroups": ([vp, i], i),
+        "orbx_lba_get_workgroups": ([vp], i),
         "orbx_dev_set_image_bounds": ([vp, vp], i),
         "orbx_set_launch_mode": ([vp, i], i),
         "orbx_get_launch_mode": ([vp], i),

@@ -340,6 +340,7 @@ void orbx_destroy(orbx_ctx* ctx)
     }
     free_buffers(ctx);
     lba_resident_free(ctx);
+    if (ctx->lba_split) (void)hipFree(ctx->lba_split);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->ev_extracted) (void)hipEventDestroy(ctx->ev_extracted);

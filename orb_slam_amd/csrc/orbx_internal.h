@@ -312,6 +312,13 @@ struct orbx_ctx {
     size_t host_pinned_bytes = 0;
     // staged pose-optimisation batch (orbx_pose_stage / run / fetch)
     orbx::LbaResident* lba_res = nullptr;   // orbx_lba_stage's batch (orbx_lba.hip)
+    // single-problem local BA over several workgroups (k_lba_split): the
+    // setting (orbx_lba_set_workgroups; 0 automatic), its device buffers, and
+    // the failed flag of the last solve
+    int lba_workgroups = 0;
+    void* lba_split = nullptr;
+    size_t lba_split_bytes = 0;
+    const unsigned* lba_split_failed = nullptr;
     void* pose_dev = nullptr;
     size_t pose_dev_bytes = 0;
     void* pose_host = nullptr;

@@ -113,7 +113,7 @@ enum { kRunning = 0, kTerminated = 1 };
 
 // Phase timing of block 0 (diagnostic build only: -DORBX_LBA_PROFILE).
 #ifdef ORBX_LBA_PROFILE
-__device__ unsigned long long g_lba_prof[16];
+__device__ unsigned long long g_lba_prof[32];
 __device__ __forceinline__ unsigned long long lba_stamp()
 {
     unsigned long long t;
@@ -315,78 +315,102 @@ __device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
 // The errors are recomputed from the state (the values compute_errors left
 // in P.err, bit for bit).  Also the largest |Hpp| diagonal and |b| entry
 // (the fixed-point scales of the trials).
+// One point's share (thread per point, its edges in edge order): Hll, bl
+// into P.hl, the robust weights into P.ew; returns max |bl|.
+template <class Rec>
+__device__ __forceinline__ double point_linearize(LbaDev& P, const double* pz, int l, double (&acc)[9])
+{
+    double pt[3];
+    load_point(P.point + 3 * P.iv_point[l], pt);
+#pragma unroll
+    for (int v = 0; v < 9; v++) acc[v] = 0.0;
+    for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
+        const Rec r = load_rec<Rec>(P, j);
+        const double* z = pz + kPz * r.pose;
+        double pc[3], e0, e1, A[6];
+        map_point(z, pt, pc);
+        residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+        jac_point(z + 16, z + 7, pc, A);
+        const double sg = (double)r.isig;
+        double r0, r1;
+        huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
+        const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
+        P.ew[j] = w;
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int c = i; c < 3; c++) acc[k++] += (A[i] * w) * A[c] + (A[3 + i] * w) * A[3 + c];
+#pragma unroll
+        for (int i = 0; i < 3; i++) acc[6 + i] += A[i] * om0 + A[3 + i] * om1;
+    }
+#pragma unroll
+    for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
+    return fmax(fabs(acc[6]), fmax(fabs(acc[7]), fabs(acc[8])));
+}
+
+// One free pose's share (one wave, lanes stride the pose's edges in edge
+// order, fixed butterfly reduction): Hpp, bp into P.hp.  hm / bm take the
+// largest |diagonal| and |bp|; every lane ends with the same values.
+template <class Rec>
+__device__ __forceinline__ void pose_linearize(LbaDev& P, const double* pz, int p, double& hm, double& bm)
+{
+    const int lane = threadIdx.x & 63;
+    const double* z = pz + kPz * P.iv_pose[p];
+    double acc[27];
+#pragma unroll
+    for (int v = 0; v < 27; v++) acc[v] = 0.0;
+    for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
+        const int2 ent = P.pe_idx[q];
+        const Rec r = load_rec<Rec>(P, ent.x);
+        double pt[3];
+        load_point(P.point + 3 * ent.y, pt);
+        double pc[3], e0, e1, B[12];
+        map_point(z, pt, pc);
+        residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+        jac_pose(z + 16, pc, B);
+        const double sg = (double)r.isig;
+        double r0, r1;
+        huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
+        const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int c = i; c < 6; c++) acc[k++] += (B[i] * w) * B[c] + (B[6 + i] * w) * B[6 + c];
+#pragma unroll
+        for (int i = 0; i < 6; i++) acc[21 + i] += B[i] * om0 + B[6 + i] * om1;
+    }
+#pragma unroll
+    for (int v = 0; v < 27; v++) {
+        const double t = wave_sum_d(acc[v]);
+        if (lane == 0) P.hp[27 * p + v] = t;
+        // diagonal of the packed upper 6x6 (row-major): 0, 6, 11, 15, 18, 20
+        if (v == 0 || v == 6 || v == 11 || v == 15 || v == 18 || v == 20) hm = fmax(hm, fabs(t));
+        else if (v >= 21) bm = fmax(bm, fabs(t));
+    }
+}
+
+// constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
+//  - per point (one thread, its edges in edge order): Hll += A^T W A,
+//    bl += A^T (-Omega e); the robust weight W = rho' Omega kept per edge for
+//    the trial (ew)
+//  - per free pose (one wave, lanes stride the pose's edges in edge order,
+//    fixed butterfly reduction): Hpp += B^T W B, bp += B^T (-Omega e).
+// The errors are recomputed from the state (the values compute_errors left
+// in P.err, bit for bit).  Also the largest |Hpp| diagonal and |b| entry
+// (the fixed-point scales of the trials).
 template <class Rec>
 __device__ __forceinline__ void linearize(LbaDev& P, const double* pz, DScratch& sc)
 {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
     double hm = 0, bm = 0;
     const int* order = P.ce;
     for (int t = threadIdx.x; t < P.nL; t += kLbaThreads) {
-        const int l = order[t];
-        double pt[3];
-        load_point(P.point + 3 * P.iv_point[l], pt);
         double acc[9];
-#pragma unroll
-        for (int v = 0; v < 9; v++) acc[v] = 0.0;
-        for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
-            const Rec r = load_rec<Rec>(P, j);
-            const double* z = pz + kPz * r.pose;
-            double pc[3], e0, e1, A[6];
-            map_point(z, pt, pc);
-            residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
-            jac_point(z + 16, z + 7, pc, A);
-            const double sg = (double)r.isig;
-            double r0, r1;
-            huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
-            const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
-            P.ew[j] = w;
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 3; i++)
-#pragma unroll
-                for (int c = i; c < 3; c++) acc[k++] += (A[i] * w) * A[c] + (A[3 + i] * w) * A[3 + c];
-#pragma unroll
-            for (int i = 0; i < 3; i++) acc[6 + i] += A[i] * om0 + A[3 + i] * om1;
-        }
-#pragma unroll
-        for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
-        bm = fmax(bm, fmax(fabs(acc[6]), fmax(fabs(acc[7]), fabs(acc[8]))));
+        bm = fmax(bm, point_linearize<Rec>(P, pz, order[t], acc));
     }
-    for (int p = wv; p < P.nP; p += kLbaWaves) {
-        const double* z = pz + kPz * P.iv_pose[p];
-        double acc[27];
-#pragma unroll
-        for (int v = 0; v < 27; v++) acc[v] = 0.0;
-        for (int q = P.pe_ptr[p] + lane; q < P.pe_ptr[p + 1]; q += 64) {
-            const int2 ent = P.pe_idx[q];
-            const Rec r = load_rec<Rec>(P, ent.x);
-            double pt[3];
-            load_point(P.point + 3 * ent.y, pt);
-            double pc[3], e0, e1, B[12];
-            map_point(z, pt, pc);
-            residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
-            jac_pose(z + 16, pc, B);
-            const double sg = (double)r.isig;
-            double r0, r1;
-            huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
-            const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int c = i; c < 6; c++) acc[k++] += (B[i] * w) * B[c] + (B[6 + i] * w) * B[6 + c];
-#pragma unroll
-            for (int i = 0; i < 6; i++) acc[21 + i] += B[i] * om0 + B[6 + i] * om1;
-        }
-#pragma unroll
-        for (int v = 0; v < 27; v++) {
-            const double t = wave_sum_d(acc[v]);
-            if (lane == 0) P.hp[27 * p + v] = t;
-            // diagonal of the packed upper 6x6 (row-major): 0, 6, 11, 15, 18, 20
-            if (v == 0 || v == 6 || v == 11 || v == 15 || v == 18 || v == 20) hm = fmax(hm, fabs(t));
-            else if (v >= 21) bm = fmax(bm, fabs(t));
-        }
-    }
+    for (int p = wv; p < P.nP; p += kLbaWaves) pose_linearize<Rec>(P, pz, p, hm, bm);
     hm = block_max_d(hm, sc);
     bm = block_max_d(bm, sc);
     if (threadIdx.x == 0) {
@@ -621,6 +645,189 @@ __device__ __forceinline__ void schur_point(LbaDev& P, const double* pz, int l, 
     }
 }
 
+// 1 / sqrt(x) for x > 0: the hardware estimate (v_rsq_f64) refined by two
+// Newton steps, r <- r (3/2 - x/2 r^2), to within a few ulps.  The LLT below
+// scales by it instead of dividing by sqrt(x): a dependent double sqrt and
+// division cost several times its latency on the pivot chain.
+__device__ __forceinline__ double rsqrt_nr(double x)
+{
+    double r = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    r = r * __fma_rn(-h * r, r, 1.5);
+    r = r * __fma_rn(-h * r, r, 1.5);
+    return r;
+}
+
+// Dense LLT of the reduced system S (packed lower triangle, n x n, with the
+// right-hand side as its row n: bs = S + n (n + 1) / 2) and the pose solve
+// into xp; every thread of the workgroup takes part.  Returns false when S
+// is not positive definite (uniform).  The reciprocals 1 / L_jj live at
+// S + M + n (the free half of the limb region).
+__device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
+{
+    __shared__ int s_fail;
+    LBA_T0();
+    const int M = n * (n + 1) / 2;
+    double* bs = S + M;
+    double* inv = bs + n;
+    // dense LLT on the packed lower triangle, right-looking in 6x6 blocks
+    // (the pose blocks): one lane factors a diagonal block in registers, the
+    // panel rows solve against it (multiplying by the pivots' reciprocals),
+    // the trailing triangle takes the rank-6 update.  Look-ahead: during block
+    // column kb's trailing update wave 0 first updates the next diagonal block
+    // itself and factors it at once, so each block column costs two barriers
+    // and the factorisations hide behind the trailing updates.
+    const int nb = n / 6;
+    auto factor_diag = [&](int k0) {   // lane 0 of wave 0
+        double a[21];                  // packed lower 6x6, a[i (i + 1) / 2 + j]
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = 0; j <= i; j++) a[i * (i + 1) / 2 + j] = S[pk(k0 + i, k0 + j)];
+        int fail = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const double piv = a[j * (j + 1) / 2 + j];
+            fail |= !(piv > 0);
+            const double r = rsqrt_nr(piv);
+            a[j * (j + 1) / 2 + j] = piv * r;   // L_jj = sqrt(piv)
+            inv[k0 + j] = r;
+#pragma unroll
+            for (int i = j + 1; i < 6; i++) a[i * (i + 1) / 2 + j] *= r;
+#pragma unroll
+            for (int i = j + 1; i < 6; i++)
+#pragma unroll
+                for (int q = j + 1; q <= i; q++) a[i * (i + 1) / 2 + q] -= a[i * (i + 1) / 2 + j] * a[q * (q + 1) / 2 + j];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = 0; j <= i; j++) S[pk(k0 + i, k0 + j)] = a[i * (i + 1) / 2 + j];
+        s_fail = fail;
+    };
+    // S(i, j) -= L(i, block) . L(j, block) of block column k0
+    auto trail = [&](int k0, int i, int j) {
+        const double* Li = S + pk(i, k0);
+        const double* Lj = S + pk(j, k0);
+        S[pk(i, j)] -= ((((Li[0] * Lj[0] + Li[1] * Lj[1]) + Li[2] * Lj[2]) + Li[3] * Lj[3]) + Li[4] * Lj[4]) +
+                       Li[5] * Lj[5];
+    };
+    if (nb > 0) {
+        if (threadIdx.x == 0) factor_diag(0);
+        __syncthreads();
+        if (s_fail) return false;   // not positive definite (uniform)
+    }
+    for (int kb = 0; kb < nb; kb++) {
+        const int k0 = 6 * kb, k1 = k0 + 6;
+        // panel: row r below the block solves x L_kk^T = A(r, block)
+        for (int r = k1 + threadIdx.x; r <= n; r += kLbaThreads) {   // row n: the forward solve of b
+            double x[6];
+            double* Sr = S + pk(r, k0);
+#pragma unroll
+            for (int j = 0; j < 6; j++) x[j] = Sr[j];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const double* Lj = S + pk(k0 + j, k0);
+#pragma unroll
+                for (int q = 0; q < j; q++) x[j] -= x[q] * Lj[q];
+                x[j] = x[j] * inv[k0 + j];
+            }
+#pragma unroll
+            for (int j = 0; j < 6; j++) Sr[j] = x[j];
+        }
+        LBA_MARK(26);
+        const bool ahead = kb + 1 < nb;
+        if (ahead && threadIdx.x < 64) {
+            // the next diagonal block's 21 elements, then its factorisation
+            const int t = threadIdx.x;
+            if (t < 21) {
+                int r = 0;
+                while ((r + 1) * (r + 2) / 2 <= t) r++;
+                trail(k0, k1 + r, k1 + (t - r * (r + 1) / 2));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (t == 0) factor_diag(k1);
+        } else {
+            // the rest of the trailing triangle (and the b row): a half-wave
+            // per pair of rows, each L(j, block) loaded once for both rows
+            // (the next diagonal block, rows k1 .. k1 + 5, is wave 0's)
+            const int t = ahead ? threadIdx.x - 64 : threadIdx.x;
+            const int nhw = (ahead ? kLbaThreads - 64 : kLbaThreads) / 32;
+            const int r0 = ahead ? k1 + 6 : k1;
+            for (int i = r0 + 2 * (t >> 5); i <= n; i += 2 * nhw) {
+                const bool two = i + 1 <= n;
+                const double* Li = S + pk(i, k0);
+                const double* Lk = S + pk(two ? i + 1 : i, k0);
+                const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
+                const double m0 = Lk[0], m1 = Lk[1], m2 = Lk[2], m3 = Lk[3], m4 = Lk[4], m5 = Lk[5];
+                double* Si = S + pk(i, 0);
+                double* Sk = S + pk(i + 1, 0);
+                const int ji = min(i, n - 1), jk = two ? min(i + 1, n - 1) : ji;
+                for (int j = k1 + (t & 31); j <= jk; j += 32) {
+                    const double* Lj = S + pk(j, k0);
+                    const double a0 = Lj[0], a1 = Lj[1], a2 = Lj[2], a3 = Lj[3], a4 = Lj[4], a5 = Lj[5];
+                    if (j <= ji) Si[j] -= ((((l0 * a0 + l1 * a1) + l2 * a2) + l3 * a3) + l4 * a4) + l5 * a5;
+                    if (two) Sk[j] -= ((((m0 * a0 + m1 * a1) + m2 * a2) + m3 * a3) + m4 * a4) + m5 * a5;
+                }
+            }
+        }
+        LBA_MARK(27);
+        if (s_fail) return false;
+    }
+    LBA_MARK(3);
+    // the factorisation above solved L y = b in its row n (the panel step is
+    // the forward substitution's block solve, the trailing update its update
+    // of the later rows, in the same operation order); backward substitution
+    // by one wave, in 6-row blocks: lane 0 solves the block's triangle in
+    // registers, then every lane updates the earlier rows with its six values
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        for (int i = lane; i < n; i += 64) xp[i] = bs[i];
+        auto wave_fence = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        };
+        wave_fence();
+        for (int kb = nb - 1; kb >= 0; kb--) {   // L^T x = y
+            const int k0 = 6 * kb;
+            if (lane == 0) {
+                double y[6], iv[6], Lb[21];   // the block's values loaded before the chain
+#pragma unroll
+                for (int p = 0; p < 6; p++) {
+                    y[p] = xp[k0 + p];
+                    iv[p] = inv[k0 + p];
+                }
+#pragma unroll
+                for (int j = 1; j < 6; j++)
+#pragma unroll
+                    for (int p = 0; p < j; p++) Lb[j * (j + 1) / 2 + p] = S[pk(k0 + j, k0 + p)];
+#pragma unroll
+                for (int j = 5; j >= 0; j--) {
+                    y[j] = y[j] * iv[j];
+#pragma unroll
+                    for (int p = 0; p < j; p++) y[p] -= Lb[j * (j + 1) / 2 + p] * y[j];
+                }
+#pragma unroll
+                for (int p = 0; p < 6; p++) xp[k0 + p] = y[p];
+            }
+            wave_fence();
+            double x[6];
+#pragma unroll
+            for (int p = 0; p < 6; p++) x[p] = xp[k0 + p];
+            for (int i = lane; i < k0; i += 64)
+                xp[i] -= ((((S[pk(k0, i)] * x[0] + S[pk(k0 + 1, i)] * x[1]) + S[pk(k0 + 2, i)] * x[2]) +
+                           S[pk(k0 + 3, i)] * x[3]) + S[pk(k0 + 4, i)] * x[4]) + S[pk(k0 + 5, i)] * x[5];
+            wave_fence();
+        }
+    }
+    __syncthreads();
+    LBA_MARK(4);
+    return true;
+}
+
 // One Levenberg trial's linear algebra: Schur complement, LLT, the pose
 // solve into xp (LDS).  Returns false when the reduced system is not
 // positive definite (or its accumulation not finite).
@@ -692,141 +899,7 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
     for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]) * iB;
     __syncthreads();
     LBA_MARK(2);
-    // dense LLT on the packed lower triangle, right-looking in 6x6 blocks
-    // (the pose blocks): wave 0 factors a diagonal block in registers (rows on
-    // lanes 0..5, shuffles), the panel rows solve against it, the trailing
-    // triangle takes the rank-6 update.  Look-ahead: during block column kb's
-    // trailing update wave 0 first updates the next diagonal block itself and
-    // factors it at once, so each block column costs two barriers and the
-    // factorisations hide behind the trailing updates (every element sees the
-    // same operations in the same order as without the look-ahead).
-    const int nb = n / 6;
-    auto factor_diag = [&](int k0) {   // wave 0
-        const int i = threadIdx.x;
-        const bool row = i < 6;
-        double a[6];
-#pragma unroll
-        for (int j = 0; j < 6; j++) a[j] = (row && j <= i) ? S[pk(k0 + i, k0 + j)] : 0.0;
-        int fail = 0;
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const double piv = __shfl(a[j], j, 64);   // a_jj after the previous columns
-            fail |= !(piv > 0);
-            const double ljj = sqrt(piv);
-            if (i == j) a[j] = ljj;
-            else if (row && i > j) a[j] = a[j] / ljj;
-#pragma unroll
-            for (int q = j + 1; q < 6; q++) {
-                const double lqj = __shfl(a[j], q, 64);
-                if (row && i >= q) a[q] -= a[j] * lqj;
-            }
-        }
-        if (row)
-#pragma unroll
-            for (int j = 0; j < 6; j++)
-                if (j <= i) S[pk(k0 + i, k0 + j)] = a[j];
-        if (i == 0) s_bad = fail;
-    };
-    // S(i, j) -= L(i, block) . L(j, block) of block column k0
-    auto trail = [&](int k0, int i, int j) {
-        const double* Li = S + pk(i, k0);
-        const double* Lj = S + pk(j, k0);
-        S[pk(i, j)] -= ((((Li[0] * Lj[0] + Li[1] * Lj[1]) + Li[2] * Lj[2]) + Li[3] * Lj[3]) + Li[4] * Lj[4]) +
-                       Li[5] * Lj[5];
-    };
-    if (nb > 0) {
-        if (threadIdx.x < 64) factor_diag(0);
-        __syncthreads();
-        if (s_bad) return false;   // not positive definite (uniform)
-    }
-    for (int kb = 0; kb < nb; kb++) {
-        const int k0 = 6 * kb, k1 = k0 + 6;
-        // panel: row r below the block solves x L_kk^T = A(r, block)
-        for (int r = k1 + threadIdx.x; r <= n; r += kLbaThreads) {   // row n: the forward solve of b
-            double x[6];
-            double* Sr = S + pk(r, k0);
-#pragma unroll
-            for (int j = 0; j < 6; j++) x[j] = Sr[j];
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const double* Lj = S + pk(k0 + j, k0);
-#pragma unroll
-                for (int q = 0; q < j; q++) x[j] -= x[q] * Lj[q];
-                x[j] = x[j] / Lj[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 6; j++) Sr[j] = x[j];
-        }
-        __syncthreads();
-        const bool ahead = kb + 1 < nb;
-        if (ahead && threadIdx.x < 64) {
-            // the next diagonal block's 21 elements, then its factorisation
-            const int t = threadIdx.x;
-            if (t < 21) {
-                int r = 0;
-                while ((r + 1) * (r + 2) / 2 <= t) r++;
-                trail(k0, k1 + r, k1 + (t - r * (r + 1) / 2));
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            factor_diag(k1);
-        } else {
-            // the rest of the trailing triangle (and the b row), half-wave per row
-            const int t = ahead ? threadIdx.x - 64 : threadIdx.x;
-            const int nhw = (ahead ? kLbaThreads - 64 : kLbaThreads) / 32;
-            for (int i = k1 + (t >> 5); i <= n; i += nhw) {
-                const double* Li = S + pk(i, k0);
-                const double l0 = Li[0], l1 = Li[1], l2 = Li[2], l3 = Li[3], l4 = Li[4], l5 = Li[5];
-                double* Si = S + pk(i, 0);
-                const int j0 = (ahead && i < k1 + 6) ? k1 + 6 : k1;   // the next diagonal block is wave 0's
-                for (int j = j0 + (t & 31); j <= min(i, n - 1); j += 32) {
-                    const double* Lj = S + pk(j, k0);
-                    Si[j] -= ((((l0 * Lj[0] + l1 * Lj[1]) + l2 * Lj[2]) + l3 * Lj[3]) + l4 * Lj[4]) + l5 * Lj[5];
-                }
-            }
-        }
-        __syncthreads();
-        if (s_bad) return false;
-    }
-    LBA_MARK(3);
-    // the factorisation above solved L y = b in its row n (the panel step is
-    // the forward substitution's block solve, the trailing update its update
-    // of the later rows, in the same operation order); backward substitution
-    // by one wave, in 6-row blocks: the block's triangle on lanes 0..5 with
-    // shuffles, then the earlier rows updated with the block's six values;
-    // one wave barrier per block
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        for (int i = lane; i < n; i += 64) xp[i] = bs[i];
-        auto wave_fence = [] {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        };
-        wave_fence();
-        for (int kb = nb - 1; kb >= 0; kb--) {   // L^T x = y
-            const int k0 = 6 * kb;
-            double xi = lane < 6 ? xp[k0 + lane] : 0.0;
-#pragma unroll
-            for (int j = 5; j >= 0; j--) {
-                const double xj = __shfl(xi, j, 64) / S[pk(k0 + j, k0 + j)];
-                if (lane == j) xi = xj;
-                else if (lane < j) xi -= S[pk(k0 + j, k0 + lane)] * xj;
-            }
-            if (lane < 6) xp[k0 + lane] = xi;
-            double x[6];
-#pragma unroll
-            for (int p = 0; p < 6; p++) x[p] = __shfl(xi, p, 64);
-            for (int i = lane; i < k0; i += 64)
-                xp[i] -= ((((S[pk(k0, i)] * x[0] + S[pk(k0 + 1, i)] * x[1]) + S[pk(k0 + 2, i)] * x[2]) +
-                           S[pk(k0 + 3, i)] * x[3]) + S[pk(k0 + 4, i)] * x[4]) + S[pk(k0 + 5, i)] * x[5];
-            wave_fence();
-        }
-    }
-    __syncthreads();
-    LBA_MARK(4);
-    return true;
+    return llt_solve(S, xp, n);
 }
 
 // The points of a pass by decreasing count of edges (counting sort; the
@@ -895,6 +968,8 @@ __device__ __forceinline__ void point_backsub(const LbaDev& P, const double* pz,
 // global memory.
 struct LbaLds {
     int s_doubles, pz_off, pbk_off, xp_off;
+    int bp_off;     // k_lba_split only: bp of the current linearisation (n doubles after xp)
+    int stage_off;  // k_lba_split only: the staged Schur's slots (lba_staged_bytes())
 };
 
 // OptimizationAlgorithmLevenberg::solve for one problem (levenberg.cpp:61-164),
@@ -1087,6 +1162,592 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
     }
 }
 
+// ---------------------------------------------------------------------------
+// One problem over G workgroups (orbx_lba_solve, and batches of one): the
+// latency form of k_lba_iteration for the LocalMapping thread's single call
+// (src/LocalMapping.cc:83).  Point l belongs to workgroup l mod G, free pose
+// p's wave to workgroup p mod G; every workgroup keeps all the poses in its
+// own LDS and applies the identical updates.  Per trial:
+//   Schur     each workgroup accumulates its points' contributions (and
+//             workgroup 0 the diagonal blocks Hpp + lambda I and bp) into its
+//             own fixed-point limbs in LDS, stores them as its slab;
+//             barrier; workgroup g sums slice g of the limbs over all slabs
+//             (integer sums: the same total as k_lba_iteration's atomics);
+//             barrier
+//   solve     every workgroup converts the total and runs the same dense
+//             LLT and solve (llt_solve) on its own copy: identical pose steps
+//             everywhere, no broadcast
+//   update    poses in every workgroup's LDS; back-substitution, point update
+//             and errors per point, their robust chi2 and computeScale terms
+//             stored per point; barrier; every workgroup sums them in
+//             k_lba_iteration's thread order (thread t takes points t, t +
+//             512, ..., then a block sum): the same bits, the same LM decision
+//             everywhere
+// and per iteration the linearisation (points and pose waves spread over the
+// workgroups) with one barrier before its maxima are combined.  Results are
+// bit-identical to k_lba_iteration (tests/test_lba_gpu.py compares the single
+// call with the batch bit for bit).  Barriers: one monotonic arrival counter
+// (zeroed before each launch) polled with relaxed agent-scope loads, an
+// agent-scope release before the arrival and an acquire after it
+// (MI355X_MICROARCH.md, inter-workgroup visibility); a barrier that waits
+// past its bound marks the run failed instead of hanging, and the host
+// reports ORBX_ERR_HIP.
+// ---------------------------------------------------------------------------
+// The Schur contributions of one workgroup's points (l = g + G k) in three
+// stages, so that a point's work spreads over lanes instead of one thread
+// (the split kernel has ~32 points per workgroup: thread per point left one
+// point's ~1500 dependent contributions on the critical path).  Per chunk of
+// up to kSP points whose free edges fit kSE slots:
+//   points  Dinv and db (schur_point's arithmetic, into P.dl and LDS), the
+//           free records into consecutive edge slots
+//   edges   A, w B and A Dinv of each free edge, its bs contribution
+//   pairs   one (u <= v) edge pair of a point per thread: schur_block
+// The values are schur_point's, bit for bit; the limbs are integer sums, so
+// the order of the atomics does not matter.
+constexpr int kSP = 64;    // points per chunk (one wave's scan)
+constexpr int kSE = 128;   // free-edge slots per chunk
+constexpr int kSEd = 24;   // doubles per slot: A (6), w B (12), A Dinv (6)
+// LDS bytes of the staged Schur (after k_lba_split's layout)
+__host__ __device__ constexpr int lba_staged_bytes() { return kSE * kSEd * 8 + kSP * 12 * 8 + (3 * kSE + 3 * kSP + 2) * 4; }
+
+template <class Rec>
+__device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const int g, const int G, const double lambda,
+                                             const double kS, const double kB, fx_t* hi, fx_t* lo, fx_t* bhi,
+                                             fx_t* blo, int& bad, double* eA, double* pD, int* tab)
+{
+    __shared__ int s_m, s_ne, s_np;
+    int* f = tab;               // [kSP] free edges per chunk point
+    int* eb = f + kSP;          // [kSP + 1] first slot of each point
+    int* pb = eb + kSP + 1;     // [kSP + 1] first pair of each point
+    int* erec = pb + kSP + 1;   // [kSE] record of each slot
+    int* epnt = erec + kSE;     // [kSE] chunk point of each slot
+    int* eph = epnt + kSE;      // [kSE] pose block of each slot
+    const int t = threadIdx.x;
+    const int nk = g < P.nL ? (P.nL - g + G - 1) / G : 0;
+    for (int k0 = 0; k0 < nk;) {
+        if (t < kSP) {
+            int c = 0;
+            if (k0 + t < nk) {
+                const int l = g + G * (k0 + t);
+                for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) c += load_rec<Rec>(P, j).ph >= 0;
+            }
+            f[t] = c;
+        }
+        __syncthreads();
+        if (t < 64) {
+            const int c = f[t];
+            const int inc = wave_inclusive_scan(c), pinc = wave_inclusive_scan(c * (c + 1) / 2);
+            eb[t + 1] = inc;
+            pb[t + 1] = pinc;
+            if (t == 0) eb[0] = pb[0] = 0;
+            // the slot counts grow with t: the chunk is the prefix that fits
+            const unsigned long long fit = __ballot(inc <= kSE && k0 + t < nk);
+            const int m = __popcll(fit);
+            if (t == 0) s_m = m;
+            if (m > 0 && t == m - 1) {
+                s_ne = inc;
+                s_np = pinc;
+            }
+        }
+        __syncthreads();
+        const int m = s_m;
+        if (m == 0) {   // a point with more than kSE edges: the host does not split such problems
+            bad = 1;
+            break;
+        }
+        const int ne = s_ne, np = s_np;
+        if (t < m) {
+            const int l = g + G * (k0 + t);
+            double* dlo = P.dl + 12 * l;
+            double* pd = pD + 12 * t;
+            const double* h = P.hl + 9 * l;
+            double d[9];
+            point_dinv(h, lambda, d);
+#pragma unroll
+            for (int i = 0; i < 9; i++) dlo[i] = pd[i] = d[i];
+            dlo[9] = pd[9] = d[0] * h[6] + d[1] * h[7] + d[2] * h[8];
+            dlo[10] = pd[10] = d[3] * h[6] + d[4] * h[7] + d[5] * h[8];
+            dlo[11] = pd[11] = d[6] * h[6] + d[7] * h[7] + d[8] * h[8];
+            int sl = eb[t];
+            for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
+                const int ph = load_rec<Rec>(P, j).ph;
+                if (ph < 0) continue;
+                erec[sl] = j;
+                epnt[sl] = t;
+                eph[sl] = ph;
+                sl++;
+            }
+        }
+        __syncthreads();
+        for (int e = t; e < ne; e += kLbaThreads) {
+            const int j = erec[e], i = epnt[e];
+            const int l = g + G * (k0 + i);
+            double pt[3];
+            load_point(P.point + 3 * P.iv_point[l], pt);
+            const Rec ru = load_rec<Rec>(P, j);
+            double Au[6], wBu[12], AD[6];
+            edge_aw(P, pz + kPz * ru.pose, j, pt, Au, wBu);
+            const double* d = pD + 12 * i;
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    AD[3 * a + k] = __fma_rn(Au[3 * a + 2], d[6 + k], __fma_rn(Au[3 * a + 1], d[3 + k], Au[3 * a] * d[k]));
+            const double adb0 = __fma_rn(Au[2], d[11], __fma_rn(Au[1], d[10], Au[0] * d[9]));
+            const double adb1 = __fma_rn(Au[5], d[11], __fma_rn(Au[4], d[10], Au[3] * d[9]));
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+                fx_add_scaled<true>(bhi, blo, 6 * ru.ph + r, -wb_dot(wBu, r, adb0, adb1) * kB, bad);
+            double* o = eA + kSEd * e;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                o[k] = Au[k];
+                o[18 + k] = AD[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 12; k++) o[6 + k] = wBu[k];
+        }
+        __syncthreads();
+        for (int q = t; q < np; q += kLbaThreads) {
+            int i = 0;
+            while (pb[i + 1] <= q) i++;          // the chunk point of pair q
+            const int fi = f[i];
+            int r = q - pb[i], u = 0;
+            while (r >= fi - u) {                // pairs (u, v), v = u .. fi - 1, u ascending
+                r -= fi - u;
+                u++;
+            }
+            const int eu = eb[i] + u, ev = eu + r;
+            const double* ou = eA + kSEd * eu;
+            const double* ov = eA + kSEd * ev;
+            double ADu[6], wBu[12], Av[6], wBv[12];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                ADu[k] = ou[18 + k];
+                Av[k] = ov[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                wBu[k] = ou[6 + k];
+                wBv[k] = ov[6 + k];
+            }
+            schur_block<true>(ADu, wBu, Av, wBv, eph[eu], eph[ev], eu == ev, kS, hi, lo, bad);
+        }
+        __syncthreads();
+        k0 += m;
+    }
+}
+
+struct LbaSplit {
+    unsigned* bar;    // [0] arrivals, [1] failed (zeroed before each launch)
+    fx_t* slabs;      // G x limbs
+    fx_t* total;      // limbs
+    double* chi_pt;   // nL: robust chi2 of each point's edges (last error pass)
+    double* sc_pt;    // 3 nL: computeScale terms of each point's update
+    double* wmax;     // G x 4: per-workgroup maxima (|Hpp| diagonal, |b|, lambda-init)
+    int* wbad;        // 2 G: per-workgroup fixed-point range flags, per attempt
+    int G, limbs;     // limbs = lba_sys_doubles(dim_p): hi M | lo M | bhi n | blo n
+};
+
+__device__ __forceinline__ bool grid_sync(const LbaSplit& X, unsigned& epoch)
+{
+    __shared__ int s_ok;
+    epoch++;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores drained
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        auto* bar = (__attribute__((address_space(1))) unsigned*)X.bar;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = epoch * (unsigned)X.G;
+        int ok = 1;
+        for (unsigned spins = 0;; spins++) {
+            if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || spins > (1u << 22)) {
+                __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// sum over l of v[l] in k_lba_iteration's order (thread t: l = t, t + 512,
+// ... sequentially, then the block sum); every workgroup gets the same bits
+__device__ __forceinline__ double canon_sum(const double* v, int nL, DScratch& sc)
+{
+    double part = 0;
+    for (int l = threadIdx.x; l < nL; l += kLbaThreads) part += v[l];
+    return block_sum_d(part, sc);
+}
+
+// The LM state of k_lba_split, identical in every workgroup: in LDS, so that
+// no register holds it across the Schur, solve and update stages (kept in
+// registers it spilled them).  Every thread computes the same values; thread
+// 0 stores them before a barrier.
+struct SplitLM {
+    double lambda, ni, currentChi, chi2_ini, iniChi, hm, bm, sS, sB, rho;
+    int nBad, status, done, trials, not_posdef, ok, ok2, qmax;
+};
+
+template <class Rec>
+__global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int iteration, int iters, LbaLds lay,
+                                                           LbaSplit X)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    __shared__ DScratch sc;
+    __shared__ int s_bad;
+    __shared__ SplitLM st;
+    LbaDev& P = probs[0];
+    const int g = blockIdx.x, G = X.G;
+    if (P.status != kRunning || P.abort) return;   // uniform: P is rewritten only after the last barrier
+    if (P.nE == 0 || P.nP + P.nL == 0) {
+        unsigned e = 0;
+        grid_sync(X, e);                           // every workgroup has read P.status
+        if (g == 0 && threadIdx.x == 0) P.status = kTerminated;
+        return;
+    }
+    unsigned epoch = 0;
+    const int n = P.dim_p, M = n * (n + 1) / 2;
+    const int wv = threadIdx.x >> 6;
+    double* pz = lds + lay.pz_off;
+    double* pbk = lds + lay.pbk_off;
+    double* xp = lds + lay.xp_off;
+    double* bpl = lds + lay.bp_off;
+    fx_t* hi = reinterpret_cast<fx_t*>(lds);
+    fx_t* lo = hi + M;
+    fx_t* bhi = lo + M;
+    fx_t* blo = bhi + n;
+    double* S = lds;
+    double* bs = S + M;
+    // the staged Schur's LDS after the layout (lay.stage_off doubles)
+    double* eA = lds + lay.stage_off;
+    double* pD = eA + kSE * kSEd;
+    int* etab = reinterpret_cast<int*>(pD + kSP * 12);
+    for (int i = threadIdx.x; i < P.nposes_all * 11; i += kLbaThreads) {
+        const int p = i / 11, k = i - 11 * p;
+        pz[kPz * p + (k < 7 ? k : 9 + k)] = k < 7 ? P.pose[7 * p + k] : P.cam[4 * p + (k - 7)];
+    }
+    if (threadIdx.x == 0) {
+        st.lambda = P.lambda;
+        st.ni = P.ni;
+        st.currentChi = P.current_chi;
+        st.chi2_ini = P.chi2_initial;
+        st.nBad = P.nBad;
+        st.status = kRunning;
+        st.done = st.trials = st.not_posdef = 0;
+        st.ok = 1;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P.nposes_all; p += kLbaThreads) pz_rot(pz + kPz * p);
+    __syncthreads();
+    for (int it = iteration; it < iteration + iters && st.status == kRunning && st.ok; it++) {
+        LBA_T0();
+        {   // linearisation (and, in a pass's first iteration, computeActiveErrors)
+            double hm = 0, bm = 0, hlm = 0;
+            for (int t = threadIdx.x;; t += kLbaThreads) {
+                const int l = g + G * t;
+                if (l >= P.nL) break;
+                if (it == 0) {
+                    double pt[3];
+                    load_point(P.point + 3 * P.iv_point[l], pt);
+                    X.chi_pt[l] = point_errors<Rec>(P, pz, l, pt);
+                }
+                double acc[9];
+                bm = fmax(bm, point_linearize<Rec>(P, pz, l, acc));
+                hlm = fmax(hlm, fmax(fabs(acc[0]), fmax(fabs(acc[3]), fabs(acc[5]))));
+            }
+            for (int p = g + G * wv; p < P.nP; p += G * kLbaWaves) pose_linearize<Rec>(P, pz, p, hm, bm);
+            hm = block_max_d(hm, sc);
+            bm = block_max_d(bm, sc);
+            hlm = block_max_d(hlm, sc);
+            LBA_MARK(16);
+            if (threadIdx.x == 0) {
+                X.wmax[4 * g] = hm;
+                X.wmax[4 * g + 1] = bm;
+                X.wmax[4 * g + 2] = hlm;
+            }
+        }
+        const bool ok1 = grid_sync(X, epoch);
+        {
+            double a = 0, b = 0, c = 0;
+            for (int q = threadIdx.x; q < G; q += kLbaThreads) {
+                a = fmax(a, X.wmax[4 * q]);
+                b = fmax(b, X.wmax[4 * q + 1]);
+                c = fmax(c, X.wmax[4 * q + 2]);
+            }
+            a = block_max_d(a, sc);
+            b = block_max_d(b, sc);
+            c = block_max_d(c, sc);
+            // bp for computeScale: a copy, since a workgroup that is done with
+            // this iteration's last trial may already write the next linearisation
+            for (int j = threadIdx.x; j < n; j += kLbaThreads) bpl[j] = P.hp[27 * (j / 6) + 21 + (j % 6)];
+            const double chi0 = it == 0 ? canon_sum(X.chi_pt, P.nL, sc) : 0.0;
+            if (threadIdx.x == 0) {
+                st.ok = st.ok && ok1;
+                st.hm = a;
+                st.bm = b;
+                if (it == 0) {
+                    st.currentChi = chi0;
+                    st.chi2_ini = chi0;
+                    st.lambda = 1e-5 * fmax(a, c);
+                    st.ni = 2;
+                    st.nBad = 0;
+                }
+                st.iniChi = st.currentChi;
+                st.rho = 0;
+                st.qmax = 0;
+            }
+            __syncthreads();
+        }
+        LBA_MARK(17);
+        do {
+            for (int i = threadIdx.x; i < P.nP * kPbk; i += kLbaThreads) {
+                const int p = i / kPbk, k = i - kPbk * p;
+                pbk[i] = pz[kPz * P.iv_pose[p] + k];
+            }
+            // --- Schur complement, summed over the workgroups
+            if (threadIdx.x == 0) {
+                const double hmax = st.hm + st.lambda, bmax = st.bm;
+                st.sS = (hmax > 0 && isfinite(hmax)) ? ldexp(1.0, 29 - ilogb(hmax)) : 1.0;
+                st.sB = (bmax > 0 && isfinite(bmax)) ? ldexp(1.0, 23 - ilogb(bmax)) : 1.0;
+                st.ok2 = 1;
+            }
+            for (int attempt = 0;; attempt++) {
+                int bad = 0;
+                for (int k = threadIdx.x; k < X.limbs; k += kLbaThreads) hi[k] = 0;
+                if (threadIdx.x == 0) s_bad = 0;
+                __syncthreads();
+                const double lambda = st.lambda, kS = st.sS * kFxHi, kB = st.sB * kFxHi;
+                if (g == 0) {
+                    for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
+                        const int p = item / 21, u = item - p * 21;
+                        int r = 0;
+                        while (up6(r, 5) < u) r++;
+                        const int c = r + (u - up6(r, r));
+                        const int idx = pk(6 * p + c, 6 * p + r);
+                        fx_split_scaled((P.hp[27 * p + u] + (r == c ? lambda : 0.0)) * kS, hi[idx], lo[idx], bad);
+                    }
+                    for (int i = threadIdx.x; i < n; i += kLbaThreads)
+                        fx_split_scaled(P.hp[27 * (i / 6) + 21 + (i % 6)] * kB, bhi[i], blo[i], bad);
+                }
+                __syncthreads();
+                schur_staged<Rec>(P, pz, g, G, lambda, kS, kB, hi, lo, bhi, blo, bad, eA, pD, etab);
+                if (bad) s_bad = 1;
+                __syncthreads();
+                LBA_MARK(18);
+                fx_t* slab = X.slabs + (size_t)g * X.limbs;
+                for (int k = threadIdx.x; k < X.limbs; k += kLbaThreads) slab[k] = hi[k];
+                if (threadIdx.x == 0) X.wbad[attempt * G + g] = s_bad;
+                const bool oka = grid_sync(X, epoch);
+                LBA_MARK(19);
+                int anyb = 0;
+                for (int q = threadIdx.x; q < G; q += kLbaThreads) anyb |= X.wbad[attempt * G + q];
+                anyb = __syncthreads_or(anyb);
+                if (threadIdx.x == 0) st.ok = st.ok && oka;
+                if (anyb) {
+                    __syncthreads();   // every thread has read st before thread 0 updates it
+                    if (threadIdx.x == 0) {
+                        if (attempt == 1) st.ok2 = 0;   // still out of range (or non-finite): rejected
+                        st.sS *= 0x1p-24;
+                        st.sB *= 0x1p-24;
+                    }
+                    __syncthreads();
+                    if (attempt == 1) break;
+                    continue;
+                }
+                // slice g of the limbs summed over the slabs: 16-byte units
+                // (two limbs), the slabs split into groups so that every
+                // thread keeps several independent loads in flight; group sums
+                // meet in LDS (integer adds: any order)
+                {
+                    const int u0 = (int)((long long)(X.limbs / 2) * g / G), u1 = (int)((long long)(X.limbs / 2) * (g + 1) / G);
+                    const int nu = u1 - u0, t = threadIdx.x;
+                    const ulonglong2* sl = reinterpret_cast<const ulonglong2*>(X.slabs);
+                    const size_t ustride = (size_t)(X.limbs / 2);
+                    if (nu >= kLbaThreads / 2) {   // few workgroups: a thread per unit, every slab
+                        for (int k = t; k < nu; k += kLbaThreads) {
+                            fx_t a = 0, b = 0;
+                            for (int q = 0; q < G; q++) {
+                                const ulonglong2 v = sl[(size_t)q * ustride + u0 + k];
+                                a += v.x;
+                                b += v.y;
+                            }
+                            reinterpret_cast<ulonglong2*>(X.total)[u0 + k] = make_ulonglong2(a, b);
+                        }
+                    } else if (nu > 0) {
+                        const int ngrp = min(kLbaThreads / nu, G);
+                        fx_t* part = reinterpret_cast<fx_t*>(eA);   // the staged Schur's slots are free here
+                        const int grp = t / nu, u = u0 + (t - grp * nu);
+                        if (grp < ngrp) {
+                            fx_t a = 0, b = 0;
+                            for (int q = grp; q < G; q += ngrp) {
+                                const ulonglong2 v = sl[(size_t)q * ustride + u];
+                                a += v.x;
+                                b += v.y;
+                            }
+                            part[2 * t] = a;
+                            part[2 * t + 1] = b;
+                        }
+                        __syncthreads();
+                        for (int k = t; k < nu; k += kLbaThreads) {
+                            fx_t a = 0, b = 0;
+                            for (int q = 0; q < ngrp; q++) {
+                                a += part[2 * (q * nu + k)];
+                                b += part[2 * (q * nu + k) + 1];
+                            }
+                            reinterpret_cast<ulonglong2*>(X.total)[u0 + k] = make_ulonglong2(a, b);
+                        }
+                    }
+                }
+                const bool okb = grid_sync(X, epoch);
+                LBA_MARK(20);
+                const double iS = 1.0 / st.sS, iB = 1.0 / st.sB;
+                const fx_t* T = X.total;
+                for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(T[k], T[M + k]) * iS;
+                for (int i = threadIdx.x; i < n; i += kLbaThreads)
+                    bs[i] = fx_value(T[2 * M + i], T[2 * M + n + i]) * iB;
+                if (threadIdx.x == 0) st.ok = st.ok && okb;
+                __syncthreads();
+                break;
+            }
+            LBA_MARK(21);
+            {
+                const bool ok2 = st.ok2 && llt_solve(S, xp, n);
+                LBA_MARK(22);
+                if (ok2)
+                    for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) {
+                        double* z = pz + kPz * P.iv_pose[p];
+                        se3_oplus(z, xp + 6 * p);
+                        pz_rot(z);
+                    }
+                __syncthreads();
+                if (threadIdx.x == 0) st.ok2 = ok2;
+            }
+            {   // --- back-substitution, point update, errors of this workgroup's points
+                const bool ok2 = st.ok2;
+                const double lambda = st.lambda;
+                for (int t = threadIdx.x;; t += kLbaThreads) {
+                    const int l = g + G * t;
+                    if (l >= P.nL) break;
+                    double* pw = P.point + 3 * P.iv_point[l];
+                    double pt[3];
+                    load_point(pw, pt);
+                    double s3[3] = {0.0, 0.0, 0.0};
+                    if (ok2) {
+                        double xl[3];
+                        point_backsub<Rec>(P, pz, pbk, xp, l, pt, xl);
+                        const double* h = P.hl + 9 * l;
+                        double* bk = P.point_bk + 3 * l;
+#pragma unroll
+                        for (int i = 0; i < 3; i++) {
+                            bk[i] = pt[i];
+                            s3[i] = xl[i] * (lambda * xl[i] + h[6 + i]);
+                            pt[i] += xl[i];
+                            pw[i] = pt[i];
+                        }
+                    }
+                    X.chi_pt[l] = point_errors<Rec>(P, pz, l, pt);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) X.sc_pt[3 * l + i] = s3[i];
+                }
+            }
+            LBA_MARK(23);
+            const bool ok3 = grid_sync(X, epoch);
+            LBA_MARK(24);
+            {   // k_lba_iteration's sums, in its order, and its LM decision
+                const bool ok2 = st.ok2;
+                const double lambda = st.lambda, ni = st.ni, currentChi = st.currentChi;
+                double tempChi = canon_sum(X.chi_pt, P.nL, sc);
+                double scale_part = 0;
+                if (ok2) {
+                    for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
+                        scale_part += X.sc_pt[3 * l];
+                        scale_part += X.sc_pt[3 * l + 1];
+                        scale_part += X.sc_pt[3 * l + 2];
+                    }
+                    for (int j = threadIdx.x; j < n; j += kLbaThreads) scale_part += xp[j] * (lambda * xp[j] + bpl[j]);
+                }
+                if (!ok2) tempChi = 1.79769313486231570815e+308;
+                double scale = block_sum_d(scale_part, sc);
+                scale += 1e-3;
+                const double rho = (currentChi - tempChi) / scale;
+                const bool accept = rho > 0 && isfinite(tempChi);
+                if (!accept && ok2) {   // pop: the saved poses (every workgroup) and this workgroup's points
+                    for (int i = threadIdx.x; i < P.nP * kPbk; i += kLbaThreads) {
+                        const int p = i / kPbk, k = i - kPbk * p;
+                        pz[kPz * P.iv_pose[p] + k] = pbk[i];
+                    }
+                    for (int t = threadIdx.x;; t += kLbaThreads) {
+                        const int l = g + G * t;
+                        if (l >= P.nL) break;
+#pragma unroll
+                        for (int k = 0; k < 3; k++) P.point[3 * P.iv_point[l] + k] = P.point_bk[3 * l + k];
+                    }
+                }
+                __syncthreads();   // every thread has read st
+                if (threadIdx.x == 0) {
+                    if (accept) {
+                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        alpha = fmin(alpha, 2. / 3.);
+                        st.lambda = lambda * fmax(1. / 3., alpha);
+                        st.ni = 2;
+                        st.currentChi = tempChi;
+                    } else {
+                        st.lambda = lambda * ni;
+                        st.ni = ni * 2;
+                    }
+                    if (!ok2) st.not_posdef++;
+                    st.rho = rho;
+                    st.qmax++;
+                    st.ok = st.ok && ok3;
+                }
+                __syncthreads();
+            }
+            LBA_MARK(25);
+        } while (st.rho < 0 && st.qmax < 10 && !P.abort && st.ok);
+        __syncthreads();   // every thread has evaluated the loop condition
+        if (threadIdx.x == 0) {
+            if (st.qmax == 10 || st.rho == 0) {
+                st.status = kTerminated;
+            } else {
+                if ((st.iniChi - st.currentChi) * 1e3 < st.iniChi) st.nBad++;
+                else st.nBad = 0;
+                if (st.nBad >= 3) st.status = kTerminated;
+            }
+            st.done++;
+            st.trials += st.qmax;
+        }
+        __syncthreads();
+    }
+    // every workgroup is past its last read of P and of the shared buffers
+    const bool okf = grid_sync(X, epoch);
+    if (g != 0) return;
+    for (int i = threadIdx.x; i < P.nP * 7; i += kLbaThreads) {
+        const int p = i / 7, k = i - 7 * p;
+        P.pose[7 * P.iv_pose[p] + k] = pz[kPz * P.iv_pose[p] + k];
+    }
+    if (threadIdx.x == 0) {
+        if (iteration == 0) P.chi2_initial = st.chi2_ini;
+        P.lambda = st.lambda;
+        P.ni = st.ni;
+        P.trials += st.trials;
+        P.iterations += st.done;
+        P.last_chi = st.currentChi;
+        P.current_chi = st.currentChi;
+        P.nBad = st.nBad;
+        P.status = (st.ok && okf) ? st.status : kTerminated;
+        P.not_posdef += st.not_posdef;
+    }
+}
+
 // Outlier passes of LocalBundleAdjustment (src/Optimizer.cc:452-470,
 // :497-515).  The reference walks the edges in order; an edge's outcome
 // depends only on earlier edges of the same map point (EraseObservation ->
@@ -1107,7 +1768,9 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     int cnt = 0;
-    for (int l = threadIdx.x; l < P.nL; l += blockDim.x) {
+    // points spread over gridDim.y workgroups (a single problem's call:
+    // several; a batch: one per problem)
+    for (int l = threadIdx.x + blockDim.x * blockIdx.y; l < P.nL; l += blockDim.x * gridDim.y) {
         const int p = P.iv_point[l];
         double pt[3];
         load_point(P.point + 3 * p, pt);
@@ -1129,7 +1792,7 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     }
     atomicAdd(&s_cnt, cnt);
     __syncthreads();
-    if (threadIdx.x == 0) n_out[blockIdx.x] = s_cnt;
+    if (threadIdx.x == 0) atomicAdd(&n_out[blockIdx.x], s_cnt);   // zeroed before the solve
 }
 
 // Structures of the first optimize() built on the device from the caller's
@@ -1569,6 +2232,9 @@ struct LbaPlan {
     bool float_rec = true;  // every observation / information is a float: 16-byte edge records
     LbaLds lay{};           // k_lba_iteration's dynamic LDS
     size_t lds_bytes = 0;
+    size_t lds_split_bytes = 0;   // k_lba_split's (the layout plus bp)
+    int nfree0 = 0;               // free poses of problem 0 (k_lba_split's reduced system)
+    int max_obs0 = 0;             // most edges on one point of problem 0 (k_lba_split stages <= kSE)
     std::vector<LbaPlay> pl;
     std::vector<long long> offs;   // per problem: first edge, first point (global flag arrays)
     std::vector<int> n_poses, n_points, n_edges;
@@ -1720,6 +2386,14 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     L.lay.pbk_off = L.lay.pz_off + np_max * kPz;
     L.lay.xp_off = L.lay.pbk_off + nf_max * kPbk;
     L.lds_bytes = (size_t)(L.lay.xp_off + 6 * nf_max + 1) * 8;
+    L.lay.bp_off = L.lay.xp_off + 6 * nf_max;
+    L.lay.stage_off = L.lay.bp_off + 6 * nf_max + 1;
+    L.lds_split_bytes = (size_t)L.lay.stage_off * 8 + lba_staged_bytes();
+    L.nfree0 = P > 0 ? nfree[0] : 0;
+    if (P == 1) {
+        std::vector<int> obs(probs[0].n_points, 0);
+        for (int e = 0; e < probs[0].n_edges; e++) L.max_obs0 = std::max(L.max_obs0, ++obs[probs[0].edge_point[e]]);
+    }
     // device-only scratch, sized by the free poses, every point and edge:
     // ce (k_lba_build / k_lba_rebuild maps, then the point order), hp, hl,
     // dl, S (the reduced system when it lives in global memory), ew
@@ -1807,6 +2481,22 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     return ORBX_OK;
 }
 
+// Workgroups for a batch of one problem (orbx_lba_set_workgroups): 1 for
+// batches, for reduced systems too large for LDS, for a point seen by more
+// than kSE keyframes (schur_staged's chunk) and for problems with few
+// points; else the context's setting, or by default one workgroup per 32
+// points, at most 64 (each workgroup's share of the Schur complement then
+// costs less than the solve every workgroup repeats).
+static int lba_split_workgroups(const orbx_ctx* ctx, const LbaPlan& L)
+{
+    if (L.P != 1 || L.lay.s_doubles == 0 || ctx->lba_workgroups == 1) return 1;
+    if (L.lds_split_bytes + 2048 > 160 * 1024 || L.max_obs0 > kSE) return 1;
+    const int nL = L.n_points[0];
+    if (ctx->lba_workgroups > 1) return std::min(ctx->lba_workgroups, 256);
+    if (nL < 128) return 1;
+    return std::min(64, (nL + 31) / 32);
+}
+
 // Queues both optimize() passes of a staged batch on the context stream:
 // k_lba_build, iterations, outliers, k_lba_rebuild, iterations, outliers.
 // With abort flags (per problem, entries may be null) each iteration is a
@@ -1821,6 +2511,7 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
     const int P = L.P;
     uint8_t* d = L.d;
     ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_err, 0, L.err_bytes, ctx->stream));
+    ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_nout, 0, 8 * (size_t)P, ctx->stream));   // outlier counts (atomic adds)
     timer_begin(ctx, "lba_build");
     hipLaunchKernelGGL(k_lba_build<Rec>, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
                        reinterpret_cast<LbaDev*>(d + L.o_devs));
@@ -1830,6 +2521,44 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
     const size_t lds = L.lds_bytes;
     // the reduced systems in LDS (when the batch's largest fits) or in global memory
     auto kern = L.lay.s_doubles > 0 ? k_lba_iteration<Rec, true> : k_lba_iteration<Rec, false>;
+    // a single problem runs over G workgroups (k_lba_split) when its reduced
+    // system fits LDS and it has enough points to share out
+    LbaSplit X{};
+    const int G = lba_split_workgroups(ctx, L);
+    if (G > 1) {
+        const long long nL = L.n_points[0], limbs = lba_sys_doubles(6LL * L.nfree0);
+        size_t o = 0;
+        auto take = [&](size_t bytes) {
+            const size_t at = o;
+            o += align256(bytes);
+            return at;
+        };
+        const size_t o_bar = take(64), o_wmax = take(32 * (size_t)G), o_wbad = take(8 * (size_t)G),
+                     o_chi = take(8 * (size_t)nL), o_sc = take(24 * (size_t)nL), o_tot = take(8 * (size_t)limbs),
+                     o_slabs = take(8 * (size_t)limbs * G);
+        if (o > ctx->lba_split_bytes) {
+            if (ctx->lba_split) (void)hipFree(ctx->lba_split);
+            ctx->lba_split = nullptr;
+            ctx->lba_split_bytes = 0;
+            if (hipMalloc(&ctx->lba_split, o) != hipSuccess) return ORBX_ERR_NOMEM;
+            ctx->lba_split_bytes = o;
+        }
+        uint8_t* b = static_cast<uint8_t*>(ctx->lba_split);
+        X.bar = reinterpret_cast<unsigned*>(b + o_bar);
+        X.wmax = reinterpret_cast<double*>(b + o_wmax);
+        X.wbad = reinterpret_cast<int*>(b + o_wbad);
+        X.chi_pt = reinterpret_cast<double*>(b + o_chi);
+        X.sc_pt = reinterpret_cast<double*>(b + o_sc);
+        X.total = reinterpret_cast<fx_t*>(b + o_tot);
+        X.slabs = reinterpret_cast<fx_t*>(b + o_slabs);
+        X.G = G;
+        X.limbs = (int)limbs;
+        // the failed flag (bar[1]) once per solve, the arrival counter per launch
+        ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 64, ctx->stream));
+        ctx->lba_split_failed = reinterpret_cast<const unsigned*>(X.bar + 1);
+    } else {
+        ctx->lba_split_failed = nullptr;
+    }
     bool polled = false;
     for (int i = 0; aborts && i < P; i++) polled |= aborts[i] != nullptr;
     std::vector<LbaDev> hv(polled ? P : 0);
@@ -1867,7 +2596,13 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             timer_begin(ctx, "lba_iter");
             // without abort flags a pass's iterations run in one launch
             const int n_it = polled ? 1 : iters;
-            hipLaunchKernelGGL(kern, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
+            if (G > 1) {
+                ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 4, ctx->stream));
+                hipLaunchKernelGGL(k_lba_split<Rec>, dim3(G), dim3(kLbaThreads), L.lds_split_bytes, ctx->stream, dd, it,
+                                   n_it, L.lay, X);
+            } else {
+                hipLaunchKernelGGL(kern, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
+            }
             timer_end(ctx, "lba_iter");
             ORBX_HIP_CHECK(hipGetLastError());
             // With an abort flag the host polls it between iterations (where
@@ -1883,7 +2618,7 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             }
         }
         timer_begin(ctx, "lba_outliers");
-        hipLaunchKernelGGL(k_lba_outliers<Rec>, dim3(P), dim3(256), 0, ctx->stream, dd,
+        hipLaunchKernelGGL(k_lba_outliers<Rec>, dim3(P, G > 1 ? 16 : 1), dim3(256), 0, ctx->stream, dd,
                            reinterpret_cast<int*>(d + L.o_all_nobs), d + L.o_all_st, d + L.o_all_bad, pass + 1,
                            L.chi2_threshold, reinterpret_cast<int*>(d + L.o_nout) + pass * P,
                            reinterpret_cast<const long long*>(d + L.o_offs));
@@ -1917,12 +2652,16 @@ static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs,
     if (L.eacc)
         ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + L.o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + L.o_nout, 8 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned split_failed = 0;
+    if (ctx->lba_split_failed)
+        ORBX_HIP_CHECK(hipMemcpyAsync(&split_failed, ctx->lba_split_failed, 4, hipMemcpyDeviceToHost, ctx->stream));
     // results: poses and points in one copy, scattered on host threads below
     ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, L.result_bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (L.pacc)
         ORBX_HIP_CHECK(hipMemcpyAsync(hb + L.o_all_bad, d + L.o_all_bad, (size_t)L.pacc, hipMemcpyDeviceToHost,
                                       ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (split_failed) return ORBX_ERR_HIP;   // a k_lba_split barrier timed out (workgroups not co-resident)
     if (stats)
         for (int pass = 0; pass < 2; pass++) {
             const std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
@@ -2048,7 +2787,7 @@ extern "C" {
 #ifdef ORBX_LBA_PROFILE
 int orbx_debug_lba_prof(unsigned long long* out)
 {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_lba_prof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_lba_prof), sizeof(unsigned long long) * 32) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -2071,6 +2810,16 @@ int orbx_lba_solve_batch(orbx_ctx* ctx, int P, orbx_ba_problem* problems, int it
     if (stats) std::memset(stats, 0, sizeof(*stats) * P);
     return orbx::lba_run(ctx, P, problems, iters0, iters1, aborts, edge_status, point_bad, stats);
 }
+
+int orbx_lba_set_workgroups(orbx_ctx* ctx, int n)
+{
+    if (!ctx || n < 0 || n > 256) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    ctx->lba_workgroups = n;
+    return ORBX_OK;
+}
+
+int orbx_lba_get_workgroups(const orbx_ctx* ctx) { return ctx ? ctx->lba_workgroups : ORBX_ERR_ARG; }
 
 int orbx_lba_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* problems)
 {

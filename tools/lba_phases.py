@@ -23,11 +23,11 @@ pbp = (ctypes.c_void_p * P)(*[b.ctypes.data for b in pb])
 ctx = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
 L = ox.lib()
 L.orbx_debug_lba_prof.argtypes = [ctypes.c_void_p]
-before = (ctypes.c_ulonglong * 16)()
+before = (ctypes.c_ulonglong * 32)()
 L.orbx_debug_lba_prof(before)
 st = (sb.BAStats * P)()
 assert L.orbx_lba_solve_batch(ctx.handle, P, arr, 5, 10, None, esp, pbp, st) == 0
-after = (ctypes.c_ulonglong * 16)()
+after = (ctypes.c_ulonglong * 32)()
 L.orbx_debug_lba_prof(after)
 d = [a - b for a, b in zip(after, before)]
 names = {6: "errors (first iteration)", 7: "linearize", 1: "S init", 2: "Schur complement", 3: "dense LLT",
@@ -41,4 +41,14 @@ build = {9: "build: flags", 10: "build: rank ids", 11: "build: count atomics", 1
 btot = sum(d[k] for k in build)
 for k, nm in build.items():
     print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / max(btot, 1):5.1f} % of the build)")
+# k_lba_split (a batch of one over several workgroups), workgroup 0
+split = {16: "split: errors + linearize", 17: "split: barrier + maxima", 18: "split: Schur (LDS)",
+         19: "split: slab + barrier", 20: "split: slice sums + barrier", 21: "split: convert", 22: "split: LLT + solve",
+         23: "split: back-subst + errors", 24: "split: barrier", 25: "split: sums + decision"}
+stot = sum(d[k] for k in split)
+for k, nm in split.items():
+    if stot:
+        print(f"{nm:28s} {d[k]:14d} ({100.0 * d[k] / stot:5.1f} %)")
+print(f"{'LLT: panel steps':28s} {d[26]:14d}")
+print(f"{'LLT: trailing steps':28s} {d[27]:14d}")
 print("iterations", list(st[0].iterations), "trials", list(st[0].levenberg_trials), "n_edges", cps[0][0].n_edges)

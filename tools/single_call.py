@@ -8,7 +8,7 @@ repo root on the GPU box, under `rocprofv3 --kernel-trace --memory-copy-trace
   pose      orbx_pose_optimization on one frame
   lba       orbx_lba_solve on one 20 KF x 2000 MP problem
 
-usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N]
+usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N] [--pyr m,...] [--lbawg g,...]
 """
 import ctypes
 import sys
@@ -27,6 +27,7 @@ args = sys.argv[1:]
 n = int(args[args.index("--n") + 1]) if "--n" in args else 100
 what = [a for a in args if a in ("extract", "sfi", "pose", "lba")] or ["extract"]
 pyr = [int(v) for v in args[args.index("--pyr") + 1].split(",")] if "--pyr" in args else [0]
+lbawg = [int(v) for v in args[args.index("--lbawg") + 1].split(",")] if "--lbawg" in args else [0]
 L = ox.lib()
 
 
@@ -105,6 +106,8 @@ if "lba" in what:
         assert L.orbx_lba_solve(ctx.handle, ctypes.byref(p), 5, 10, None, es.ctypes.data, pb.ctypes.data,
                                 ctypes.byref(st)) == 0
 
-    print(f"lba: {med(lba, max(5, n // 10)):.4f} ms median", flush=True)
+    for wg in lbawg:
+        assert L.orbx_lba_set_workgroups(ctx.handle, wg) == 0
+        print(f"lba workgroups {wg}: {med(lba, max(5, n // 10)):.4f} ms median", flush=True)
     ctx.close()
 print("ok")
