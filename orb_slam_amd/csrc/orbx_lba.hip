@@ -735,6 +735,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
 #pragma unroll
             for (int j = 0; j < 6; j++) Sr[j] = x[j];
         }
+        __syncthreads();
         LBA_MARK(26);
         const bool ahead = kb + 1 < nb;
         if (ahead && threadIdx.x < 64) {
@@ -773,6 +774,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
                 }
             }
         }
+        __syncthreads();
         LBA_MARK(27);
         if (s_fail) return false;
     }
