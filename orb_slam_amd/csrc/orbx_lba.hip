@@ -120,17 +120,34 @@ __device__ __forceinline__ unsigned long long lba_stamp()
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+// per-wave phase stamps of llt_solve (k_llt_bench, block 0): work / barrier
+// wait of the panel phase, work / wait of the trailing phase
+__device__ unsigned long long g_llt_wave[8][4];
+#define LLT_W0() unsigned long long _w = lba_stamp()
+#define LLT_W(k)                                                                                \
+    do {                                                                                        \
+        const unsigned long long _n = lba_stamp();                                              \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_llt_wave[threadIdx.x >> 6][k], _n - _w); \
+        _w = _n;                                                                                \
+    } while (0)
+#ifdef ORBX_LBA_NOMARKS   // the microbenchmarks without the phase marks
+#define LBA_T0()
+#define LBA_MARK(k)
+#else
 #define LBA_T0() unsigned long long _t = lba_stamp()
 #define LBA_MARK(k)                                                         \
     do {                                                                    \
         __syncthreads();                                                    \
         const unsigned long long _n = lba_stamp();                          \
-        if (blockIdx.x == 0 && threadIdx.x == 0) g_lba_prof[k] += _n - _t;  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_lba_prof[k], _n - _t); \
         _t = _n;                                                            \
     } while (0)
+#endif
 #else
 #define LBA_T0()
 #define LBA_MARK(k)
+#define LLT_W0()
+#define LLT_W(k)
 #endif
 
 constexpr int kLbaThreads = 512;               // one workgroup (8 waves) per problem: the phases need up to 255 VGPRs
@@ -717,6 +734,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
         __syncthreads();
         if (s_fail) return false;   // not positive definite (uniform)
     }
+    LLT_W0();
     for (int kb = 0; kb < nb; kb++) {
         const int k0 = 6 * kb, k1 = k0 + 6;
         // panel: row r below the block solves x L_kk^T = A(r, block)
@@ -735,7 +753,9 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
 #pragma unroll
             for (int j = 0; j < 6; j++) Sr[j] = x[j];
         }
+        LLT_W(0);
         __syncthreads();
+        LLT_W(1);
         LBA_MARK(26);
         const bool ahead = kb + 1 < nb;
         if (ahead && threadIdx.x < 64) {
@@ -774,7 +794,9 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
                 }
             }
         }
+        LLT_W(2);
         __syncthreads();
+        LLT_W(3);
         LBA_MARK(27);
         if (s_fail) return false;
     }
@@ -2782,14 +2804,98 @@ static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1, const volatil
     return lba_launch(ctx, L, iters0, iters1, aborts);
 }
 
+#ifdef ORBX_LBA_PROFILE
+// llt_solve alone (diagnostic build): reps factorisations of the packed
+// system Sin (n x n plus the right-hand-side row) in LDS, cycles summed
+__global__ void __launch_bounds__(kLbaThreads) k_llt_bench(const double* Sin, int n, int reps, double* xout,
+                                                            unsigned long long* cyc, int mode)
+{
+    extern __shared__ double lds[];
+    const int M = n * (n + 1) / 2;
+    double* S = lds;
+    double* xp = lds + M + 2 * n;
+    unsigned long long tot = 0;
+    if (mode >= 2) {   // latency probes: 1000 dependent f64 multiplies (2) or rsqrt_nr (3); raw v_rsq_f64 (4)
+        if (mode == 4) {
+            for (int k = threadIdx.x; k < n; k += kLbaThreads) xout[k] = __builtin_amdgcn_rsq(Sin[k]);
+            return;
+        }
+        double v = Sin[threadIdx.x], a = Sin[n + threadIdx.x];
+        if (mode == 5 || mode == 6) {   // 1000 workgroup barriers (5); 1000 dependent LDS loads (6)
+            int* q = reinterpret_cast<int*>(lds);
+            for (int k = threadIdx.x; k < 1024; k += kLbaThreads) q[k] = (k + 1) & 1023;
+            __syncthreads();
+            int j = threadIdx.x & 63;
+            const unsigned long long t0 = lba_stamp();
+            if (mode == 5)
+                for (int i = 0; i < 1000; i++) __syncthreads();
+            else
+                for (int i = 0; i < 1000; i++) j = q[j];
+            const unsigned long long t1 = lba_stamp();
+            if (threadIdx.x == 0) {
+                *cyc = t1 - t0;
+                xout[0] = j;
+            }
+            return;
+        }
+        const unsigned long long t0 = lba_stamp();
+        if (mode == 2)
+            for (int i = 0; i < 1000; i++) v = v * a;
+        else
+            for (int i = 0; i < 1000; i++) v = rsqrt_nr(v);
+        const unsigned long long t1 = lba_stamp();
+        if (threadIdx.x == 0) {
+            *cyc = t1 - t0;
+            xout[0] = v;
+        }
+        return;
+    }
+    for (int r = 0; r < reps; r++) {
+        for (int k = threadIdx.x; k < M + n; k += kLbaThreads) S[k] = Sin[k];
+        __syncthreads();
+        const unsigned long long t0 = lba_stamp();
+        const bool ok = llt_solve(S, xp, n);
+        const unsigned long long t1 = lba_stamp();
+        tot += t1 - t0;
+        if (!ok) break;
+    }
+    for (int k = threadIdx.x; k < n; k += kLbaThreads) xout[k] = xp[k];
+    if (threadIdx.x == 0) *cyc = tot;
+}
+#endif
+
 }  // namespace orbx
 
 extern "C" {
 
 #ifdef ORBX_LBA_PROFILE
+int orbx_debug_llt_waves(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_llt_wave), sizeof(unsigned long long) * 32) == hipSuccess ? 0 : -2;
+}
+
 int orbx_debug_lba_prof(unsigned long long* out)
 {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_lba_prof), sizeof(unsigned long long) * 32) == hipSuccess ? 0 : -2;
+}
+
+int orbx_debug_llt_bench(const double* Sin_host, int n, int reps, double* x_host, unsigned long long* cycles, int mode)
+{
+    const int M = n * (n + 1) / 2;
+    double *dS = nullptr, *dx = nullptr;
+    unsigned long long* dc = nullptr;
+    if (hipMalloc(&dS, (M + n) * 8) != hipSuccess || hipMalloc(&dx, n * 8) != hipSuccess || hipMalloc(&dc, 8) != hipSuccess)
+        return -2;
+    (void)hipMemcpy(dS, Sin_host, (M + n) * 8, hipMemcpyHostToDevice);
+    const size_t lds = (size_t)(M + 3 * n) * 8;
+    hipLaunchKernelGGL(orbx::k_llt_bench, dim3(1), dim3(orbx::kLbaThreads), lds, 0, dS, n, reps, dx, dc, mode);
+    const bool ok = hipDeviceSynchronize() == hipSuccess;
+    (void)hipMemcpy(x_host, dx, n * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(cycles, dc, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(dS);
+    (void)hipFree(dx);
+    (void)hipFree(dc);
+    return ok ? 0 : -2;
 }
 #endif
 
