@@ -38,8 +38,9 @@ extern "C" {
  *      (orbx_host_alloc, orbx_dev_upload_async, orbx_dev_download_async),
  *      image bounds of device-resident frames (orbx_dev_set_image_bounds),
  *      multi-workgroup single local-BA problems (orbx_lba_set_workgroups);
- *      additions only. */
-#define ORBX_ABI_VERSION 3
+ *      additions only.
+ *   4: orbx_pose_set_exact / orbx_pose_get_exact; additions only. */
+#define ORBX_ABI_VERSION 4
 int orbx_abi_version(void);
 
 #define ORBX_OK               0
@@ -788,6 +789,19 @@ int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames);
 int orbx_pose_run(orbx_ctx* ctx);
 int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* n_inliers,
                     orbx_pose_stats* stats);
+/* Summation mode of the pose optimisation (default 0).  0: each wavefront
+ * sums its edges' chi2 / H / b terms lane-strided and then through a fixed
+ * DPP tree -- deterministic, but in another order than g2o, so LM steps
+ * decided on rounding noise (a converged pose restarted in a later robust
+ * round) may count differently.  1: every sum runs sequentially in g2o's
+ * active-edge order (the edge terms are computed in parallel, accumulated
+ * edge by edge), so the whole LM trajectory -- accept / reject of every
+ * trial, lambda, iterations -- follows the sequential reference; about 2x the
+ * kernel time (the dependent chain of additions).  Takes effect at the next
+ * orbx_pose_run.  Returns ORBX_ERR_ARG for a null context or a mode outside
+ * 0..1; orbx_pose_get_exact returns the mode (ORBX_ERR_ARG for NULL). */
+int orbx_pose_set_exact(orbx_ctx* ctx, int exact);
+int orbx_pose_get_exact(const orbx_ctx* ctx);
 
 /* Library identification. */
 const char* orbx_version(void);

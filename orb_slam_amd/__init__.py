@@ -140,6 +140,8 @@ def _declare(L):
         "orbx_abi_version": ([], i),
         "orbx_lba_set_workgroups": ([vp, i], i),
         "orbx_lba_get_workgroups": ([vp], i),
+        "orbx_pose_set_exact": ([vp, i], i),
+        "orbx_pose_get_exact": ([vp], i),
         "orbx_dev_set_image_bounds": ([vp, vp], i),
         "orbx_set_launch_mode": ([vp, i], i),
         "orbx_get_launch_mode": ([vp], i),

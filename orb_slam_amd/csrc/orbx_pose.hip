@@ -264,6 +264,57 @@ __device__ inline void huber2(double e2, double delta, double& rho0, double& rho
     }
 }
 
+// The per-edge terms of one LM linearisation (computeActiveErrors +
+// buildSystem): c[0] the robust chi2, c[1..21] the lower entries of
+// J^T W J, c[22..27] b -- each the value g2o adds for this edge.
+__device__ inline void pose_edge_terms(const double* pose, const Cam& cam, double delta, float fo0, float fo1, float fis,
+                                       float fx_, float fy_, float fz_, double (&c)[28])
+{
+    const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
+    const double s = (double)fis;
+    double pc[3], er0, er1;
+    pose_edge_error(pose, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
+    double rho0, rho1;
+    huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
+    c[0] = rho0;
+    const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+    const double fx = cam.fx, fy = cam.fy;
+    double B[12];
+    B[0] = x * y / z_2 * fx;
+    B[1] = -(1 + (x * x / z_2)) * fx;
+    B[2] = y / z * fx;
+    B[3] = -1. / z * fx;
+    B[4] = 0;
+    B[5] = x / z_2 * fx;
+    B[6] = (1 + y * y / z_2) * fy;
+    B[7] = -x * y / z_2 * fy;
+    B[8] = -x / z * fy;
+    B[9] = 0;
+    B[10] = -1. / z * fy;
+    B[11] = y / z_2 * fy;
+    const double w = rho1 * s;
+    const double om0 = -(s * er0) * rho1, om1 = -(s * er1) * rho1;
+    int k = 1;
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++, k++) c[k] = (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
+#pragma unroll
+    for (int i = 0; i < 6; i++) c[22 + i] = B[i] * om0 + B[6 + i] * om1;
+}
+
+// kExact: every chi2, H and b sum is accumulated sequentially in g2o's
+// active-edge order (OptimizationAlgorithmLevenberg / BlockSolver add edge
+// by edge in insertion order): per group of 64 edges each lane writes its
+// edge's terms to an LDS row, then lane q adds column q over the rows in
+// edge order.  The sums -- and so every accept / reject decision and the
+// whole LM trajectory -- are then those of the sequential restatement
+// (oracle/ref_pose.cpp), at the cost of a 64-step dependent chain per group
+// (orbx_pose_set_exact; off by default).  An inactive edge contributes
+// +0.0: the sum starts at +0.0 and round-to-nearest never yields -0.0 from
+// it, so adding +0.0 leaves every bit as skipping the edge would.  The term
+// rows (57 KB per workgroup) sit beside the edge cache: one workgroup per CU.
+template <bool kExact>
 __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __restrict__ hdrs, PoseEdgeArrays ed,
                                                           uint8_t* __restrict__ eflag, PoseOut* __restrict__ outs,
                                                           int P, double delta)
@@ -300,6 +351,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
     uint8_t* flag = eflag + e0;
     __shared__ float s_e[kPoseThreads / 64][6][kPoseLdsEdges];
     __shared__ uint8_t s_f[kPoseThreads / 64][kPoseLdsEdges];
+    __shared__ double s_rows[kExact ? kPoseThreads / 64 : 1][kExact ? 64 : 1][28];   // per-edge terms
     const int wq = threadIdx.x >> 6;
     const int nL = min(nE, kPoseLdsEdges);
     float* lox = s_e[wq][0];
@@ -334,6 +386,39 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
             if (!flag[a]) body(ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
     };
 
+    // kExact: the sequential sums of Q per-edge terms over the active edges
+    // in edge order; lane q < Q returns sum q
+    auto seq_sums = [&](int Q, auto&& terms) -> double {
+        double acc = 0;
+        double(*rows)[28] = s_rows[kExact ? wq : 0];
+#pragma unroll 1
+        for (int g = 0; g < nE; g += 64) {
+            const int a = g + lane;
+            double c[28];
+            bool act = false;
+            if (a < nL) {
+                act = !lfl[a];
+                if (act) terms(lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a], c);
+            } else if (a < nE) {
+                act = !flag[a];
+                if (act) terms(ox[a], oy[a], isg[a], px[a], py[a], pz[a], c);
+            }
+            for (int q = 0; q < Q; q++) rows[lane][q] = act ? c[q] : 0.0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < Q) {
+                const int ne = min(64, nE - g);
+#pragma unroll 8
+                for (int e = 0; e < ne; e++) acc += rows[e][lane];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        return acc;
+    };
+
     PoseOut& out = outs[prob];
     int not_posdef = 0, rounds = 0;
     int n_active = nE;
@@ -357,6 +442,18 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                 for (int k = 0; k < 21; k++) h[k] = 0;
 #pragma unroll
                 for (int k = 0; k < 6; k++) bv[k] = 0;
+                double currentChi;
+                if constexpr (kExact) {
+                    const double sum = seq_sums(28, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
+                                                        double (&c)[28]) {
+                        pose_edge_terms(pose, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                    });
+                    currentChi = lane_f64(sum, 0);
+#pragma unroll
+                    for (int k = 0; k < 21; k++) h[k] = lane_f64(sum, 1 + k);
+#pragma unroll
+                    for (int k = 0; k < 6; k++) bv[k] = lane_f64(sum, 22 + k);
+                } else {
                 for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
                     const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
                     const double s = (double)fis;
@@ -395,12 +492,13 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
 #pragma unroll
                         for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
                 });
-                double currentChi = wave_sum_uniform(chi);
-                const double iniChi = currentChi;
+                currentChi = wave_sum_uniform(chi);
 #pragma unroll
                 for (int k = 0; k < 21; k++) h[k] = wave_sum_uniform(h[k]);
 #pragma unroll
                 for (int k = 0; k < 6; k++) bv[k] = wave_sum_uniform(bv[k]);
+                }
+                const double iniChi = currentChi;
                 if (iter == 0) {   // computeLambdaInit (levenberg.cpp:166-180)
                     double mx = 0;
 #pragma unroll
@@ -428,17 +526,29 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                         for (int i = 0; i < 6; i++) xs[i] = 0.0;
                     }
                     // computeActiveErrors at the trial estimate
-                    double tchi = 0;
-                    for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
+                    auto trial_chi = [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
                         const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
                         const double s = (double)fis;
                         double pc[3], er0, er1;
                         pose_edge_error(tp, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
                         double rho0, rho1;
                         huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
-                        tchi += rho0;
-                    });
-                    double tempChi = wave_sum_uniform(tchi);
+                        return rho0;
+                    };
+                    double tempChi;
+                    if constexpr (kExact) {
+                        tempChi = lane_f64(seq_sums(1, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
+                                                           double (&c)[28]) {
+                                               c[0] = trial_chi(fo0, fo1, fis, fx_, fy_, fz_);
+                                           }),
+                                           0);
+                    } else {
+                        double tchi = 0;
+                        for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
+                            tchi += trial_chi(fo0, fo1, fis, fx_, fy_, fz_);
+                        });
+                        tempChi = wave_sum_uniform(tchi);
+                    }
 #pragma unroll
                     for (int i = 0; i < 7; i++) errpose[i] = tp[i];
                     if (!ok2) tempChi = 1.79769313486231570815e+308;
@@ -651,7 +761,8 @@ extern "C" int orbx_pose_run(orbx_ctx* ctx)
     const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
     const int per = kPoseThreads / 64;
     timer_begin(ctx, "pose");
-    k_pose_opt<<<(P + per - 1) / per, kPoseThreads, 0, ctx->stream>>>(
+    auto kern = ctx->pose_exact ? k_pose_opt<true> : k_pose_opt<false>;
+    kern<<<(P + per - 1) / per, kPoseThreads, 0, ctx->stream>>>(
         reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags, reinterpret_cast<PoseOut*>(d + ctx->pose_o_out),
         P, delta);
     timer_end(ctx, "pose");
@@ -708,6 +819,18 @@ extern "C" int orbx_pose_optimization_batch(orbx_ctx* ctx, int P, orbx_pose_fram
     if (r != ORBX_OK) return r;
     if ((r = orbx_pose_run(ctx)) != ORBX_OK) return r;
     return orbx_pose_fetch(ctx, frames, n_inliers, stats);
+}
+
+extern "C" int orbx_pose_set_exact(orbx_ctx* ctx, int exact)
+{
+    if (!ctx || exact < 0 || exact > 1) return ORBX_ERR_ARG;
+    ctx->pose_exact = exact != 0;
+    return ORBX_OK;
+}
+
+extern "C" int orbx_pose_get_exact(const orbx_ctx* ctx)
+{
+    return ctx ? (ctx->pose_exact ? 1 : 0) : ORBX_ERR_ARG;
 }
 
 extern "C" int orbx_pose_optimization(orbx_ctx* ctx, orbx_pose_frame* f, int* n_inliers, orbx_pose_stats* stats)

@@ -64,6 +64,8 @@ def test_context_setters_refuse_null_context():
         ("orbx_set_launch_mode", (None, 1)),
         ("orbx_lba_set_workgroups", (None, 4)),
         ("orbx_lba_get_workgroups", (None,)),
+        ("orbx_pose_set_exact", (None, 1)),
+        ("orbx_pose_get_exact", (None,)),
         ("orbx_get_launch_mode", (None,)),
         ("orbx_dev_upload_async", (None, 0, 1, None, 640, 480, 640)),
         ("orbx_dev_download_async", (None, 0, 1, None, None, None, None, None)),

@@ -13,6 +13,11 @@ no reimplementation with another order (the GPU sums lane-strided partials
 through a DPP tree; g2o sums sequentially) reproduces them.  Such steps move
 the pose by far less than the tolerance; where the counts differ the test
 requires the two poses to agree to 1e-6.
+
+With orbx_pose_set_exact(ctx, 1) every sum runs sequentially in g2o's
+active-edge order: then the whole trajectory must match the restatement --
+iterations, trials and outliers of every round, the final chi2 of each round
+and the pose bit for bit (test_pose_exact_trajectory, no 1e-6 rule).
 """
 import ctypes
 
@@ -113,3 +118,51 @@ def test_pose_rejects_bad_octave(ctx):
     p, arrs = sp.to_ctypes(fr)
     n = ctypes.c_int()
     assert ox.lib().orbx_pose_optimization(ctx.handle, ctypes.byref(p), ctypes.byref(n), None) == -1
+
+
+@pytest.fixture()
+def exact_ctx(ctx):
+    assert ox.lib().orbx_pose_set_exact(ctx.handle, 1) == 0
+    assert ox.lib().orbx_pose_get_exact(ctx.handle) == 1
+    yield ctx
+    assert ox.lib().orbx_pose_set_exact(ctx.handle, 0) == 0
+
+
+EXACT_CASES = CASES + [dict(n_kp=1000, seed=s, outlier_frac=0.1) for s in range(20, 36)]
+
+
+@pytest.mark.parametrize("case", EXACT_CASES, ids=[f"n{c['n_kp']}_s{c['seed']}" for c in EXACT_CASES])
+def test_pose_exact_trajectory(exact_ctx, case):
+    """Sequential sums in g2o's edge order: the LM trajectory of every round
+    equals the restatement's -- counts, outliers, per-round chi2 and pose."""
+    fr = sp.make_frame(**case)
+    rT, rout, rn, rst = ref_pose(fr)
+    gT, gout, gn, gst = gpu_pose(exact_ctx, [fr])[0]
+    assert gst.rounds == rst.rounds
+    assert list(gst.iterations) == list(rst.iterations)
+    assert list(gst.levenberg_trials) == list(rst.levenberg_trials)
+    assert list(gst.n_bad) == list(rst.n_bad)
+    assert gst.not_posdef == rst.not_posdef
+    assert list(gst.chi2_final) == list(rst.chi2_final)
+    assert np.array_equal(gout, rout) and gn == rn
+    assert np.array_equal(gT, rT), np.abs(gT - rT).max()
+
+
+def test_pose_exact_batch_mixed_sizes(exact_ctx):
+    rng = np.random.default_rng(1)
+    frames = [sp.make_frame(n_kp=int(rng.integers(5, 1500)), seed=300 + k, outlier_frac=float(rng.uniform(0, 0.3)))
+              for k in range(23)]
+    for fr, (gT, gout, gn, gst) in zip(frames, gpu_pose(exact_ctx, frames)):
+        rT, rout, rn, rst = ref_pose(fr)
+        assert list(gst.iterations) == list(rst.iterations)
+        assert list(gst.levenberg_trials) == list(rst.levenberg_trials)
+        assert np.array_equal(gT, rT) and np.array_equal(gout, rout) and gn == rn
+
+
+def test_pose_exact_setter_validates():
+    assert ox.lib().orbx_pose_set_exact(None, 1) == -1
+    c = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1)
+    assert ox.lib().orbx_pose_get_exact(c.handle) == 0
+    assert ox.lib().orbx_pose_set_exact(c.handle, 2) == -1
+    assert ox.lib().orbx_pose_set_exact(c.handle, -1) == -1
+    c.close()
