@@ -54,6 +54,37 @@
 
 namespace orbx {
 
+// Race / call-boundary checks (diagnostic builds, tools/lba_race_check.py):
+//  -DORBX_LBA_NOINLINE: every device function of this file is a real call
+//   (the form in which round 4's dropped pose-pair Schur went wrong);
+//  -DORBX_LBA_PERTURB: after every workgroup barrier each wave sleeps a
+//   pseudo-random 0..~2k cycles (wave, workgroup and clock hashed), so the
+//   phases between barriers run in other interleavings.  A missing barrier or
+//   an LDS overlap between phases then changes bits; the product build and
+//   both variants must give the same bits.
+#ifdef ORBX_LBA_NOINLINE
+#define LBA_FN __device__ __noinline__
+#else
+#define LBA_FN __device__ __forceinline__
+#endif
+#ifdef ORBX_LBA_PERTURB
+__device__ __forceinline__ void lba_perturb()
+{
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    unsigned h = (unsigned)t * 2654435761u ^ (threadIdx.x >> 6) * 40503u ^ blockIdx.x * 9973u;
+    h ^= h >> 13;
+    for (unsigned k = h & 31; k > 0; k--) __builtin_amdgcn_s_sleep(1);
+}
+#define LBA_SYNC()      \
+    do {                \
+        __syncthreads(); \
+        lba_perturb();  \
+    } while (0)
+#else
+#define LBA_SYNC() __syncthreads()
+#endif
+
 // Active edge, point-major.  pose: index into the problem's poses; ph: its
 // pose block (free poses in g2o id order) or -1 for a fixed pose.
 struct EdgeRecF {
@@ -114,7 +145,7 @@ enum { kRunning = 0, kTerminated = 1 };
 // Phase timing of block 0 (diagnostic build only: -DORBX_LBA_PROFILE).
 #ifdef ORBX_LBA_PROFILE
 __device__ unsigned long long g_lba_prof[32];
-__device__ __forceinline__ unsigned long long lba_stamp()
+LBA_FN unsigned long long lba_stamp()
 {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -137,7 +168,7 @@ __device__ unsigned long long g_llt_wave[8][4];
 #define LBA_T0() unsigned long long _t = lba_stamp()
 #define LBA_MARK(k)                                                         \
     do {                                                                    \
-        __syncthreads();                                                    \
+        LBA_SYNC();                                                    \
         const unsigned long long _n = lba_stamp();                          \
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_lba_prof[k], _n - _t); \
         _t = _n;                                                            \
@@ -162,37 +193,37 @@ struct DScratch {
     double w[kLbaWaves];
 };
 
-__device__ __forceinline__ double wave_sum_d(double v)
+LBA_FN double wave_sum_d(double v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-__device__ __forceinline__ double wave_max_d(double v)
+LBA_FN double wave_max_d(double v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
 
-__device__ __forceinline__ double block_sum_d(double v, DScratch& s)
+LBA_FN double block_sum_d(double v, DScratch& s)
 {
     v = wave_sum_d(v);
-    __syncthreads();
+    LBA_SYNC();
     if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
-    __syncthreads();
+    LBA_SYNC();
     double t = 0;
     for (int i = 0; i < kLbaWaves; i++) t += s.w[i];
     return t;
 }
 
-__device__ __forceinline__ double block_max_d(double v, DScratch& s)
+LBA_FN double block_max_d(double v, DScratch& s)
 {
     v = wave_max_d(v);
-    __syncthreads();
+    LBA_SYNC();
     if ((threadIdx.x & 63) == 0) s.w[threadIdx.x >> 6] = v;
-    __syncthreads();
+    LBA_SYNC();
     double t = s.w[0];
     for (int i = 1; i < kLbaWaves; i++) t = fmax(t, s.w[i]);
     return t;
@@ -202,7 +233,7 @@ __device__ __forceinline__ double block_max_d(double v, DScratch& s)
 // Edge algebra (pose z in the LDS layout: q at z[0..3], t at z[4..6], the
 // rotation matrix at z[7..15], fx fy cx cy at z[16..19])
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void huber(double e2, double delta, double* rho0, double* rho1)
+LBA_FN void huber(double e2, double delta, double* rho0, double* rho1)
 {
     const double dsqr = delta * delta;
     if (e2 <= dsqr) {
@@ -217,7 +248,7 @@ __device__ __forceinline__ void huber(double e2, double delta, double* rho0, dou
 
 // EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) with
 // cam_project (.cpp:422-428): e = obs - (fx X / Z + cx, fy Y / Z + cy)
-__device__ __forceinline__ void residual(const double* c, const double (&pc)[3], double ox, double oy, double& e0, double& e1)
+LBA_FN void residual(const double* c, const double (&pc)[3], double ox, double oy, double& e0, double& e1)
 {
     e0 = ox - (pc[0] / pc[2] * c[0] + c[2]);
     e1 = oy - (pc[1] / pc[2] * c[1] + c[3]);
@@ -227,7 +258,7 @@ __device__ __forceinline__ void residual(const double* c, const double (&pc)[3],
 // camera-frame point pc: A = d e / d point (2x3) with the pose's rotation R,
 // the reference's divisions by z and z^2 as products with 1/z (one division
 // per edge; the values differ from g2o's in rounding only).
-__device__ __forceinline__ void jac_point(const double* c, const double* R, const double (&pc)[3], double (&A)[6])
+LBA_FN void jac_point(const double* c, const double* R, const double (&pc)[3], double (&A)[6])
 {
     const double iz = 1. / pc[2];
     const double fx = c[0], fy = c[1];
@@ -241,7 +272,7 @@ __device__ __forceinline__ void jac_point(const double* c, const double* R, cons
 }
 
 // B = d e / d pose (2x6), update order [omega(3), upsilon(3)]
-__device__ __forceinline__ void jac_pose(const double* c, const double (&pc)[3], double (&B)[12])
+LBA_FN void jac_pose(const double* c, const double (&pc)[3], double (&B)[12])
 {
     const double x = pc[0], y = pc[1];
     const double iz = 1. / pc[2], iz2 = iz * iz;
@@ -261,19 +292,19 @@ __device__ __forceinline__ void jac_pose(const double* c, const double (&pc)[3],
 }
 
 template <class Rec>
-__device__ __forceinline__ Rec load_rec(const LbaDev& P, int j)
+LBA_FN Rec load_rec(const LbaDev& P, int j)
 {
     return reinterpret_cast<const Rec*>(P.rec)[j];
 }
 
-__device__ __forceinline__ void load_point(const double* p, double (&v)[3])
+LBA_FN void load_point(const double* p, double (&v)[3])
 {
     v[0] = p[0];
     v[1] = p[1];
     v[2] = p[2];
 }
 
-__device__ __forceinline__ void map_point(const double* z, const double (&p)[3], double (&pc)[3])
+LBA_FN void map_point(const double* z, const double (&p)[3], double (&pc)[3])
 {
     se3_map(z, p, pc);   // SE3Quat::map: q p + t
 }
@@ -282,7 +313,7 @@ __device__ __forceinline__ void map_point(const double* z, const double (&p)[3],
 // pt; writes P.err, returns the summed robust chi2 (computeActiveErrors +
 // activeRobustChi2 of these edges)
 template <class Rec>
-__device__ __forceinline__ double point_errors(LbaDev& P, const double* pz, int l, const double (&pt)[3])
+LBA_FN double point_errors(LbaDev& P, const double* pz, int l, const double (&pt)[3])
 {
     double part = 0;
     for (int j = P.le_ptr[l]; j < P.le_ptr[l + 1]; j++) {
@@ -307,7 +338,7 @@ __device__ __forceinline__ double point_errors(LbaDev& P, const double* pz, int 
 // every run (the count-sorted order of the Schur pass is not fixed within a
 // count).
 template <class Rec>
-__device__ __forceinline__ double compute_errors(LbaDev& P, const double* pz, DScratch& sc)
+LBA_FN double compute_errors(LbaDev& P, const double* pz, DScratch& sc)
 {
     double part = 0;
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) {
@@ -318,10 +349,10 @@ __device__ __forceinline__ double compute_errors(LbaDev& P, const double* pz, DS
     return block_sum_d(part, sc);
 }
 
-__device__ __forceinline__ int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
-__device__ __forceinline__ int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
+LBA_FN int up6(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }   // i <= j
+LBA_FN int up3(int i, int j) { return i * 3 - (i * (i - 1)) / 2 + (j - i); }
 // packed lower triangle: element (i, j), j <= i
-__device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
+LBA_FN int pk(int i, int j) { return i * (i + 1) / 2 + j; }
 
 // constructQuadraticForm (base_binary_edge.hpp:55-120) split by owner:
 //  - per point (one thread, its edges in edge order): Hll += A^T W A,
@@ -335,7 +366,7 @@ __device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
 // One point's share (thread per point, its edges in edge order): Hll, bl
 // into P.hl, the robust weights into P.ew; returns max |bl|.
 template <class Rec>
-__device__ __forceinline__ double point_linearize(LbaDev& P, const double* pz, int l, double (&acc)[9])
+LBA_FN double point_linearize(LbaDev& P, const double* pz, int l, double (&acc)[9])
 {
     double pt[3];
     load_point(P.point + 3 * P.iv_point[l], pt);
@@ -370,7 +401,7 @@ __device__ __forceinline__ double point_linearize(LbaDev& P, const double* pz, i
 // order, fixed butterfly reduction): Hpp, bp into P.hp.  hm / bm take the
 // largest |diagonal| and |bp|; every lane ends with the same values.
 template <class Rec>
-__device__ __forceinline__ void pose_linearize(LbaDev& P, const double* pz, int p, double& hm, double& bm)
+LBA_FN void pose_linearize(LbaDev& P, const double* pz, int p, double& hm, double& bm)
 {
     const int lane = threadIdx.x & 63;
     const double* z = pz + kPz * P.iv_pose[p];
@@ -418,7 +449,7 @@ __device__ __forceinline__ void pose_linearize(LbaDev& P, const double* pz, int 
 // in P.err, bit for bit).  Also the largest |Hpp| diagonal and |b| entry
 // (the fixed-point scales of the trials).
 template <class Rec>
-__device__ __forceinline__ void linearize(LbaDev& P, const double* pz, DScratch& sc)
+LBA_FN void linearize(LbaDev& P, const double* pz, DScratch& sc)
 {
     const int wv = threadIdx.x >> 6;
     double hm = 0, bm = 0;
@@ -434,7 +465,7 @@ __device__ __forceinline__ void linearize(LbaDev& P, const double* pz, DScratch&
         P.hmax = hm;
         P.bmax = bm;
     }
-    __syncthreads();
+    LBA_SYNC();
 }
 
 // Fixed-point accumulation of the reduced camera system.  Every value v is
@@ -469,7 +500,7 @@ constexpr double kFxMagic = 6755399441055744.0;            // 1.5 * 2^52
 typedef unsigned long long fx_t;
 
 // (t = x * 2^11, already scaled)
-__device__ __forceinline__ void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
+LBA_FN void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
 {
     bad |= !(fabs(t) < kFxMax);
     const double th = t + kFxMagic;                 // round(t) in the low mantissa bits
@@ -485,7 +516,7 @@ __device__ __forceinline__ void fx_split_scaled(double t, fx_t& hi, fx_t& lo, in
 // pointer the compiler tests the address space at run time, and that test
 // has tripped its instruction selection here
 template <bool kLds>
-__device__ __forceinline__ void fx_atomic(fx_t* p, fx_t v)
+LBA_FN void fx_atomic(fx_t* p, fx_t v)
 {
     if constexpr (kLds) {
         atomicAdd(p, v);
@@ -496,7 +527,7 @@ __device__ __forceinline__ void fx_atomic(fx_t* p, fx_t v)
 }
 
 template <bool kLds>
-__device__ __forceinline__ void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int& bad)
+LBA_FN void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, double t, int& bad)
 {
     fx_t h, l;
     fx_split_scaled(t, h, l, bad);
@@ -504,7 +535,7 @@ __device__ __forceinline__ void fx_add_scaled(fx_t* hi, fx_t* lo, int idx, doubl
     fx_atomic<kLds>(lo + idx, l);
 }
 
-__device__ __forceinline__ double fx_value(fx_t hi, fx_t lo)
+LBA_FN double fx_value(fx_t hi, fx_t lo)
 {
     return (double)(long long)hi * kFxInvHi + (double)(long long)lo * kFxInvLo;
 }
@@ -517,7 +548,7 @@ __host__ __device__ constexpr long long lba_sys_doubles(long long n) { return n 
 
 // Dinv = (Hll + lambda I)^-1 of a point (Eigen's 3x3 cofactor inverse:
 // d[i*3+j] = cof(j, i) / det)
-__device__ __forceinline__ void point_dinv(const double* h, double lambda, double (&d)[9])
+LBA_FN void point_dinv(const double* h, double lambda, double (&d)[9])
 {
     double m[9];
 #pragma unroll
@@ -544,7 +575,7 @@ __device__ __forceinline__ void point_dinv(const double* h, double lambda, doubl
 // form's zero product adds only a signed zero, so the value is the same (a
 // non-finite a0 / a1 still reaches the other columns, which reject the
 // trial as before).
-__device__ __forceinline__ double wb_dot(const double (&wB)[12], int k, double a0, double a1)
+LBA_FN double wb_dot(const double (&wB)[12], int k, double a0, double a1)
 {
     if (k == 3) return wB[3] * a0;
     if (k == 4) return wB[10] * a1;
@@ -552,7 +583,7 @@ __device__ __forceinline__ double wb_dot(const double (&wB)[12], int k, double a
 }
 
 template <bool kLds>
-__device__ __forceinline__ void schur_block(const double (&AD)[6], const double (&wBu)[12], const double (&Av)[6],
+LBA_FN void schur_block(const double (&AD)[6], const double (&wBu)[12], const double (&Av)[6],
                                    const double (&wBv)[12], int pu, int pv, bool diag, double kS, fx_t* hi, fx_t* lo,
                                    int& bad)
 {
@@ -600,7 +631,7 @@ __device__ __forceinline__ void schur_block(const double (&AD)[6], const double 
 }
 
 // the edge's A (2x3) and w B (2x6) at point pt (pose z in LDS)
-__device__ __forceinline__ void edge_aw(const LbaDev& P, const double* z, int j, const double (&pt)[3], double (&A)[6],
+LBA_FN void edge_aw(const LbaDev& P, const double* z, int j, const double (&pt)[3], double (&A)[6],
                                double (&wB)[12])
 {
     double pc[3], B[12];
@@ -613,7 +644,7 @@ __device__ __forceinline__ void edge_aw(const LbaDev& P, const double* z, int j,
 }
 
 template <class Rec, bool kLds>
-__device__ __forceinline__ void schur_point(LbaDev& P, const double* pz, int l, double lambda, double kS, double kB, fx_t* hi,
+LBA_FN void schur_point(LbaDev& P, const double* pz, int l, double lambda, double kS, double kB, fx_t* hi,
                                    fx_t* lo, fx_t* bhi, fx_t* blo, int& bad)
 {
     double* dlo = P.dl + 12 * l;
@@ -666,7 +697,7 @@ __device__ __forceinline__ void schur_point(LbaDev& P, const double* pz, int l, 
 // Newton steps, r <- r (3/2 - x/2 r^2), to within a few ulps.  The LLT below
 // scales by it instead of dividing by sqrt(x): a dependent double sqrt and
 // division cost several times its latency on the pivot chain.
-__device__ __forceinline__ double rsqrt_nr(double x)
+LBA_FN double rsqrt_nr(double x)
 {
     double r = __builtin_amdgcn_rsq(x);
     const double h = 0.5 * x;
@@ -680,7 +711,7 @@ __device__ __forceinline__ double rsqrt_nr(double x)
 // into xp; every thread of the workgroup takes part.  Returns false when S
 // is not positive definite (uniform).  The reciprocals 1 / L_jj live at
 // S + M + n (the free half of the limb region).
-__device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
+LBA_FN bool llt_solve(double* S, double* xp, const int n)
 {
     __shared__ int s_fail;
     LBA_T0();
@@ -731,7 +762,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
     };
     if (nb > 0) {
         if (threadIdx.x == 0) factor_diag(0);
-        __syncthreads();
+        LBA_SYNC();
         if (s_fail) return false;   // not positive definite (uniform)
     }
     LLT_W0();
@@ -754,7 +785,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
             for (int j = 0; j < 6; j++) Sr[j] = x[j];
         }
         LLT_W(0);
-        __syncthreads();
+        LBA_SYNC();
         LLT_W(1);
         LBA_MARK(26);
         const bool ahead = kb + 1 < nb;
@@ -795,7 +826,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
             }
         }
         LLT_W(2);
-        __syncthreads();
+        LBA_SYNC();
         LLT_W(3);
         LBA_MARK(27);
         if (s_fail) return false;
@@ -847,7 +878,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
             wave_fence();
         }
     }
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(4);
     return true;
 }
@@ -858,7 +889,7 @@ __device__ __forceinline__ bool llt_solve(double* S, double* xp, const int n)
 // kLds: the reduced system lives in the dynamic LDS block (its accesses then
 // compile to ds_* instructions instead of flat ones), else in P.S.
 template <class Rec, bool kLds>
-__device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double* pz, double* xp, double lambda)
+LBA_FN bool trial_solve(LbaDev& P, double* lds, const double* pz, double* xp, double lambda)
 {
     __shared__ int s_bad;
     LBA_T0();
@@ -889,7 +920,7 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
             lo[k] = 0;
         }
         if (threadIdx.x == 0) s_bad = 0;
-        __syncthreads();
+        LBA_SYNC();
         for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
             const int p = item / 21, u = item - p * 21;
             int r = 0;
@@ -900,7 +931,7 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
         }
         for (int i = threadIdx.x; i < n; i += kLbaThreads)
             fx_split_scaled(P.hp[27 * (i / 6) + 21 + (i % 6)] * kB, bhi[i], blo[i], bad);
-        __syncthreads();
+        LBA_SYNC();
         LBA_MARK(1);
         // points in the order of their edge counts: the lanes of a wave run
         // loops of similar length; with order-independent sums this changes
@@ -908,35 +939,35 @@ __device__ __forceinline__ bool trial_solve(LbaDev& P, double* lds, const double
         for (int t = threadIdx.x; t < P.nL; t += kLbaThreads)
             schur_point<Rec, kLds>(P, pz, order[t], lambda, kS, kB, hi, lo, bhi, blo, bad);
         if (bad) s_bad = 1;
-        __syncthreads();
+        LBA_SYNC();
         if (!s_bad) break;                  // uniform
         if (attempt == 1) return false;     // still out of range (or non-finite): rejected
         sS *= 0x1p-24;                      // a contribution reached 2^40: once more at a smaller scale
         sB *= 0x1p-24;
-        __syncthreads();                    // every thread has read s_bad before it is reset
+        LBA_SYNC();                    // every thread has read s_bad before it is reset
     }
     // limbs -> doubles in place (element k's double overwrites its own hi),
     // scaled back (exact)
     const double iS = 1.0 / sS, iB = 1.0 / sB;
     for (int k = threadIdx.x; k < M; k += kLbaThreads) S[k] = fx_value(hi[k], lo[k]) * iS;
-    __syncthreads();   // the lo limbs are read before row n overwrites them
+    LBA_SYNC();   // the lo limbs are read before row n overwrites them
     for (int i = threadIdx.x; i < n; i += kLbaThreads) bs[i] = fx_value(bhi[i], blo[i]) * iB;
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(2);
     return llt_solve(S, xp, n);
 }
 
 // The points of a pass by decreasing count of edges (counting sort; the
 // order within a count is arbitrary and does not matter) into P.ce.
-__device__ __forceinline__ void point_order(LbaDev& P)
+LBA_FN void point_order(LbaDev& P)
 {
     __shared__ int hist[64], off[64];
     int* order = P.ce;
     for (int b = threadIdx.x; b < 64; b += kLbaThreads) hist[b] = 0;
-    __syncthreads();
+    LBA_SYNC();
     auto bucket = [&](int l) { return 63 - min(P.le_ptr[l + 1] - P.le_ptr[l], 63); };
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) atomicAdd(&hist[bucket(l)], 1);
-    __syncthreads();
+    LBA_SYNC();
     if (threadIdx.x == 0) {
         int acc = 0;
         for (int b = 0; b < 64; b++) {
@@ -944,20 +975,20 @@ __device__ __forceinline__ void point_order(LbaDev& P)
             acc += hist[b];
         }
     }
-    __syncthreads();
+    LBA_SYNC();
     for (int l = threadIdx.x; l < P.nL; l += kLbaThreads) order[atomicAdd(&off[bucket(l)], 1)] = l;
-    __syncthreads();
+    LBA_SYNC();
 }
 
 // rotation matrix of pose z (q at z[0..3]) into z[7..15] (Eigen's
 // toRotationMatrix, the R of linearizeOplus)
-__device__ __forceinline__ void pz_rot(double* z) { qmat(Q{z[0], z[1], z[2], z[3]}, z + 7); }
+LBA_FN void pz_rot(double* z) { qmat(Q{z[0], z[1], z[2], z[3]}, z + 7); }
 
 // Back-substitution of point l with the W_i of the linearisation state (the
 // saved poses pbk, the point before its update pt): xl = Dinv (bl - sum_i
 // W_i^T xp_i) (block_solver.hpp:461-486)
 template <class Rec>
-__device__ __forceinline__ void point_backsub(const LbaDev& P, const double* pz, const double* pbk, const double* xp, int l,
+LBA_FN void point_backsub(const LbaDev& P, const double* pz, const double* pbk, const double* xp, int l,
                                      const double (&pt)[3], double (&xl)[3])
 {
     const double* h = P.hl + 9 * l;
@@ -1024,10 +1055,10 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         const int p = i / 11, k = i - 11 * p;
         pz[kPz * p + (k < 7 ? k : 9 + k)] = k < 7 ? P.pose[7 * p + k] : P.cam[4 * p + (k - 7)];
     }
-    __syncthreads();
+    LBA_SYNC();
     for (int p = threadIdx.x; p < P.nposes_all; p += kLbaThreads) pz_rot(pz + kPz * p);
     if (iteration == 0) point_order(P);
-    __syncthreads();
+    LBA_SYNC();
     // the LM state carried from iteration to iteration of this launch, in
     // LDS: kept in registers across the iteration loop it spilled the Schur
     // pass (every thread computes the same values; thread 0 stores them)
@@ -1042,7 +1073,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         s_it[2] = 0;
         s_it[3] = 0;
     }
-    __syncthreads();
+    LBA_SYNC();
     for (int it = iteration; it < iteration + iters && s_it[1] == kRunning; it++) {
     double lambda = s_lm[0], ni = s_lm[1], currentChi = s_lm[2];
     int nBad = s_it[0];
@@ -1076,7 +1107,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
             const int p = i / kPbk, k = i - kPbk * p;
             pbk[i] = pz[kPz * P.iv_pose[p] + k];
         }
-        __syncthreads();
+        LBA_SYNC();
         const bool ok2 = trial_solve<Rec, kLds>(P, lds, pz, xp, lambda);
         if (ok2)
             for (int p = threadIdx.x; p < P.nP; p += kLbaThreads) {
@@ -1084,7 +1115,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
                 se3_oplus(z, xp + 6 * p);
                 pz_rot(z);
             }
-        __syncthreads();
+        LBA_SYNC();
         LBA_T0();
         // per point: back-substitution, the update (VertexSBAPointXYZ::
         // oplusImpl) and the errors of its edges at the new state;
@@ -1146,7 +1177,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
                 }
             }
         }
-        __syncthreads();
+        LBA_SYNC();
         qmax++;
     } while (rho < 0 && qmax < 10 && !P.abort);
     int status = kRunning;
@@ -1166,7 +1197,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_iteration(LbaDev* probs, in
         s_it[2]++;
         s_it[3] += qmax;
     }
-    __syncthreads();
+    LBA_SYNC();
     }
     // the free poses back to global memory (the next launch and the outlier
     // pass read them there)
@@ -1235,7 +1266,7 @@ constexpr int kSEd = 24;   // doubles per slot: A (6), w B (12), A Dinv (6)
 __host__ __device__ constexpr int lba_staged_bytes() { return kSE * kSEd * 8 + kSP * 12 * 8 + (3 * kSE + 3 * kSP + 2) * 4; }
 
 template <class Rec>
-__device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const int g, const int G, const double lambda,
+LBA_FN void schur_staged(LbaDev& P, const double* pz, const int g, const int G, const double lambda,
                                              const double kS, const double kB, fx_t* hi, fx_t* lo, fx_t* bhi,
                                              fx_t* blo, int& bad, double* eA, double* pD, int* tab)
 {
@@ -1257,7 +1288,7 @@ __device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const 
             }
             f[t] = c;
         }
-        __syncthreads();
+        LBA_SYNC();
         if (t < 64) {
             const int c = f[t];
             const int inc = wave_inclusive_scan(c), pinc = wave_inclusive_scan(c * (c + 1) / 2);
@@ -1273,7 +1304,7 @@ __device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const 
                 s_np = pinc;
             }
         }
-        __syncthreads();
+        LBA_SYNC();
         const int m = s_m;
         if (m == 0) {   // a point with more than kSE edges: the host does not split such problems
             bad = 1;
@@ -1302,7 +1333,7 @@ __device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const 
                 sl++;
             }
         }
-        __syncthreads();
+        LBA_SYNC();
         for (int e = t; e < ne; e += kLbaThreads) {
             const int j = erec[e], i = epnt[e];
             const int l = g + G * (k0 + i);
@@ -1331,7 +1362,7 @@ __device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const 
 #pragma unroll
             for (int k = 0; k < 12; k++) o[6 + k] = wBu[k];
         }
-        __syncthreads();
+        LBA_SYNC();
         for (int q = t; q < np; q += kLbaThreads) {
             int i = 0;
             while (pb[i + 1] <= q) i++;          // the chunk point of pair q
@@ -1357,7 +1388,7 @@ __device__ __forceinline__ void schur_staged(LbaDev& P, const double* pz, const 
             }
             schur_block<true>(ADu, wBu, Av, wBv, eph[eu], eph[ev], eu == ev, kS, hi, lo, bad);
         }
-        __syncthreads();
+        LBA_SYNC();
         k0 += m;
     }
 }
@@ -1373,12 +1404,12 @@ struct LbaSplit {
     int G, limbs;     // limbs = lba_sys_doubles(dim_p): hi M | lo M | bhi n | blo n
 };
 
-__device__ __forceinline__ bool grid_sync(const LbaSplit& X, unsigned& epoch)
+LBA_FN bool grid_sync(const LbaSplit& X, unsigned& epoch)
 {
     __shared__ int s_ok;
     epoch++;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores drained
-    __syncthreads();
+    LBA_SYNC();
     if (threadIdx.x == 0) {
         auto* bar = (__attribute__((address_space(1))) unsigned*)X.bar;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1399,13 +1430,13 @@ __device__ __forceinline__ bool grid_sync(const LbaSplit& X, unsigned& epoch)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         s_ok = ok;
     }
-    __syncthreads();
+    LBA_SYNC();
     return s_ok != 0;
 }
 
 // sum over l of v[l] in k_lba_iteration's order (thread t: l = t, t + 512,
 // ... sequentially, then the block sum); every workgroup gets the same bits
-__device__ __forceinline__ double canon_sum(const double* v, int nL, DScratch& sc)
+LBA_FN double canon_sum(const double* v, int nL, DScratch& sc)
 {
     double part = 0;
     for (int l = threadIdx.x; l < nL; l += kLbaThreads) part += v[l];
@@ -1469,9 +1500,9 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
         st.done = st.trials = st.not_posdef = 0;
         st.ok = 1;
     }
-    __syncthreads();
+    LBA_SYNC();
     for (int p = threadIdx.x; p < P.nposes_all; p += kLbaThreads) pz_rot(pz + kPz * p);
-    __syncthreads();
+    LBA_SYNC();
     for (int it = iteration; it < iteration + iters && st.status == kRunning && st.ok; it++) {
         LBA_T0();
         {   // linearisation (and, in a pass's first iteration, computeActiveErrors)
@@ -1529,7 +1560,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                 st.rho = 0;
                 st.qmax = 0;
             }
-            __syncthreads();
+            LBA_SYNC();
         }
         LBA_MARK(17);
         do {
@@ -1548,7 +1579,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                 int bad = 0;
                 for (int k = threadIdx.x; k < X.limbs; k += kLbaThreads) hi[k] = 0;
                 if (threadIdx.x == 0) s_bad = 0;
-                __syncthreads();
+                LBA_SYNC();
                 const double lambda = st.lambda, kS = st.sS * kFxHi, kB = st.sB * kFxHi;
                 if (g == 0) {
                     for (int item = threadIdx.x; item < P.nP * 21; item += kLbaThreads) {
@@ -1562,10 +1593,10 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                     for (int i = threadIdx.x; i < n; i += kLbaThreads)
                         fx_split_scaled(P.hp[27 * (i / 6) + 21 + (i % 6)] * kB, bhi[i], blo[i], bad);
                 }
-                __syncthreads();
+                LBA_SYNC();
                 schur_staged<Rec>(P, pz, g, G, lambda, kS, kB, hi, lo, bhi, blo, bad, eA, pD, etab);
                 if (bad) s_bad = 1;
-                __syncthreads();
+                LBA_SYNC();
                 LBA_MARK(18);
                 fx_t* slab = X.slabs + (size_t)g * X.limbs;
                 for (int k = threadIdx.x; k < X.limbs; k += kLbaThreads) slab[k] = hi[k];
@@ -1577,13 +1608,13 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                 anyb = __syncthreads_or(anyb);
                 if (threadIdx.x == 0) st.ok = st.ok && oka;
                 if (anyb) {
-                    __syncthreads();   // every thread has read st before thread 0 updates it
+                    LBA_SYNC();   // every thread has read st before thread 0 updates it
                     if (threadIdx.x == 0) {
                         if (attempt == 1) st.ok2 = 0;   // still out of range (or non-finite): rejected
                         st.sS *= 0x1p-24;
                         st.sB *= 0x1p-24;
                     }
-                    __syncthreads();
+                    LBA_SYNC();
                     if (attempt == 1) break;
                     continue;
                 }
@@ -1620,7 +1651,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                             part[2 * t] = a;
                             part[2 * t + 1] = b;
                         }
-                        __syncthreads();
+                        LBA_SYNC();
                         for (int k = t; k < nu; k += kLbaThreads) {
                             fx_t a = 0, b = 0;
                             for (int q = 0; q < ngrp; q++) {
@@ -1639,7 +1670,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                 for (int i = threadIdx.x; i < n; i += kLbaThreads)
                     bs[i] = fx_value(T[2 * M + i], T[2 * M + n + i]) * iB;
                 if (threadIdx.x == 0) st.ok = st.ok && okb;
-                __syncthreads();
+                LBA_SYNC();
                 break;
             }
             LBA_MARK(21);
@@ -1652,7 +1683,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                         se3_oplus(z, xp + 6 * p);
                         pz_rot(z);
                     }
-                __syncthreads();
+                LBA_SYNC();
                 if (threadIdx.x == 0) st.ok2 = ok2;
             }
             {   // --- back-substitution, point update, errors of this workgroup's points
@@ -1716,7 +1747,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                         for (int k = 0; k < 3; k++) P.point[3 * P.iv_point[l] + k] = P.point_bk[3 * l + k];
                     }
                 }
-                __syncthreads();   // every thread has read st
+                LBA_SYNC();   // every thread has read st
                 if (threadIdx.x == 0) {
                     if (accept) {
                         double alpha = 1. - pow((2 * rho - 1), 3);
@@ -1733,11 +1764,11 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
                     st.qmax++;
                     st.ok = st.ok && ok3;
                 }
-                __syncthreads();
+                LBA_SYNC();
             }
             LBA_MARK(25);
         } while (st.rho < 0 && st.qmax < 10 && !P.abort && st.ok);
-        __syncthreads();   // every thread has evaluated the loop condition
+        LBA_SYNC();   // every thread has evaluated the loop condition
         if (threadIdx.x == 0) {
             if (st.qmax == 10 || st.rho == 0) {
                 st.status = kTerminated;
@@ -1749,7 +1780,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
             st.done++;
             st.trials += st.qmax;
         }
-        __syncthreads();
+        LBA_SYNC();
     }
     // every workgroup is past its last read of P and of the shared buffers
     const bool okf = grid_sync(X, epoch);
@@ -1790,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     uint8_t* st = status_all + eo;
     uint8_t* bad = bad_all + po;
     if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
+    LBA_SYNC();
     int cnt = 0;
     // points spread over gridDim.y workgroups (a single problem's call:
     // several; a batch: one per problem)
@@ -1815,7 +1846,7 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
         }
     }
     atomicAdd(&s_cnt, cnt);
-    __syncthreads();
+    LBA_SYNC();
     if (threadIdx.x == 0) atomicAdd(&n_out[blockIdx.x], s_cnt);   // zeroed before the solve
 }
 
@@ -1830,14 +1861,14 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
 // from a scan when the ids are already increasing (the caller's usual order)
 // and from pairwise counts otherwise.  One workgroup per problem; the maps
 // live in the ce scratch.
-__device__ __forceinline__ void lba_rank(const long long* id, const int* act, int n, int* rank, int* count,
+LBA_FN void lba_rank(const long long* id, const int* act, int n, int* rank, int* count,
                                 BlockScratchN<kLbaWaves>& bs)
 {
     const int tid = threadIdx.x;
     int unsorted = 0;
     for (int i = tid; i + 1 < n; i += kLbaThreads) unsorted |= !(id[i] < id[i + 1]);
     unsorted = block_sum<kLbaWaves>(unsorted, bs, 0);
-    __syncthreads();
+    LBA_SYNC();
     int total = 0;
     if (!unsorted) {
         int base = 0;
@@ -1865,12 +1896,12 @@ __device__ __forceinline__ void lba_rank(const long long* id, const int* act, in
         }
         total = block_sum<kLbaWaves>(cnt, bs, 1);
     }
-    __syncthreads();
+    LBA_SYNC();
     *count = total;
 }
 
 // counts in ptr[1 .. n] -> offsets (block scans); ptr[0] = 0
-__device__ __forceinline__ void lba_offsets(int* ptr, int n, BlockScratchN<kLbaWaves>& bs)
+LBA_FN void lba_offsets(int* ptr, int n, BlockScratchN<kLbaWaves>& bs)
 {
     const int tid = threadIdx.x;
     int base = 0;
@@ -1879,13 +1910,13 @@ __device__ __forceinline__ void lba_offsets(int* ptr, int n, BlockScratchN<kLbaW
         const int v = i < n ? ptr[i + 1] : 0;
         int tot;
         const int inc = block_exclusive_scan<kLbaWaves>(v, &tot, bs, (c / kLbaThreads) & 1) + v;
-        __syncthreads();
+        LBA_SYNC();
         if (i < n) ptr[i + 1] = base + inc;
         base += tot;
-        __syncthreads();
+        LBA_SYNC();
     }
     if (tid == 0) ptr[0] = 0;
-    __syncthreads();
+    LBA_SYNC();
 }
 
 // The edges of each free pose in edge order, as a stable counting scatter:
@@ -1898,7 +1929,7 @@ __device__ __forceinline__ void lba_offsets(int* ptr, int n, BlockScratchN<kLbaW
 constexpr int kBuildPoses = 128;   // free poses the LDS tables hold (else the per-pose scan)
 constexpr int kBuildPoints = 8192; // active points whose counts / cursors k_lba_build keeps in LDS
 
-__device__ __forceinline__ void pose_chunks(const LbaDev& A, const int* ph, int nP, int (*wcnt)[kBuildPoses],
+LBA_FN void pose_chunks(const LbaDev& A, const int* ph, int nP, int (*wcnt)[kBuildPoses],
                                             int* base, int* ptr, const int* pos, int2* pe_idx)
 {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, E = A.nedges_all;
@@ -1907,7 +1938,7 @@ __device__ __forceinline__ void pose_chunks(const LbaDev& A, const int* ph, int 
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (int a0 = 0; a0 < E; a0 += kLbaThreads) {
         for (int q = lane; q < nP; q += 64) wcnt[wv][q] = 0;
-        __syncthreads();
+        LBA_SYNC();
         const int a = a0 + tid;
         const int q = a < E ? ph[A.r_edge_pose[a]] : -1;
         int rank = 0;
@@ -1920,7 +1951,7 @@ __device__ __forceinline__ void pose_chunks(const LbaDev& A, const int* ph, int 
             if (lane == lead) wcnt[wv][qq] = (int)__popcll(m);
             act &= ~m;
         }
-        __syncthreads();
+        LBA_SYNC();
         for (int qq = tid; qq < nP; qq += kLbaThreads) {   // wave-order prefix per pose
             int sum = base[qq];
 #pragma unroll
@@ -1931,13 +1962,13 @@ __device__ __forceinline__ void pose_chunks(const LbaDev& A, const int* ph, int 
             }
             base[qq] = sum;
         }
-        __syncthreads();
+        LBA_SYNC();
         if (!count_only && q >= 0) pe_idx[ptr[q] + wcnt[wv][q] + rank] = make_int2(pos[a], A.r_edge_point[a]);
     }
-    __syncthreads();
+    LBA_SYNC();
     if (count_only)
         for (int qq = tid; qq < nP; qq += kLbaThreads) ptr[qq] = base[qq];
-    __syncthreads();
+    LBA_SYNC();
 }
 
 template <class Rec>
@@ -1958,13 +1989,13 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     LBA_T0();
     for (int i = tid; i < NP; i += kLbaThreads) pflag[i] = 0;
     for (int i = tid; i < NL; i += kLbaThreads) lflag[i] = 0;
-    __syncthreads();
+    LBA_SYNC();
     for (int a = tid; a < E; a += kLbaThreads) {
         const int p = A.r_edge_pose[a];
         if (!A.r_pose_fixed[p]) pflag[p] = 1;
         lflag[A.r_edge_point[a]] = 1;
     }
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(9);
     int nP, nL;
     lba_rank(A.r_pose_id, pflag, NP, ph, &nP, bs);
@@ -1980,7 +2011,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     int* le_ptr = const_cast<int*>(A.le_ptr);
     for (int i = tid; i <= nP; i += kLbaThreads) pe_ptr[i] = 0;
     for (int i = tid; i <= nL; i += kLbaThreads) le_ptr[i] = 0;
-    __syncthreads();
+    LBA_SYNC();
     // the free poses' edge counts come from the chunked pass below when the
     // batch's free poses fit its LDS tables (kBuildPoses), else from atomics
     const bool chunked = nP <= kBuildPoses;
@@ -1989,7 +2020,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     const bool pts_lds = nL <= kBuildPoints;
     if (pts_lds) {
         for (int l = tid; l < nL; l += kLbaThreads) s_pt[l] = 0;
-        __syncthreads();
+        LBA_SYNC();
     }
     for (int a = tid; a < E; a += kLbaThreads) {
         if (!chunked) {
@@ -2000,10 +2031,10 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         if (pts_lds) atomicAdd(&s_pt[l], 1);
         else atomicAdd(&le_ptr[l + 1], 1);
     }
-    __syncthreads();
+    LBA_SYNC();
     if (pts_lds)
         for (int l = tid; l < nL; l += kLbaThreads) le_ptr[l + 1] = s_pt[l];
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(11);
     lba_offsets(pe_ptr, nP, bs);
     lba_offsets(le_ptr, nL, bs);
@@ -2011,9 +2042,9 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     int* e_orig = const_cast<int*>(A.e_orig);
     int* cursor = pts_lds ? s_pt : cur;
     for (int l = tid; l < nL; l += kLbaThreads) cursor[l] = le_ptr[l];
-    __syncthreads();
+    LBA_SYNC();
     for (int a = tid; a < E; a += kLbaThreads) e_orig[atomicAdd(&cursor[lh[A.r_edge_point[a]]], 1)] = a;
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(12);
     for (int l = tid; l < nL; l += kLbaThreads) {
         const int q0 = le_ptr[l], q1 = le_ptr[l + 1];
@@ -2027,7 +2058,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
             e_orig[j + 1] = x;
         }
     }
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(13);
     // the records (float fields only when the host found every value exact)
     Rec* rec = reinterpret_cast<Rec*>(const_cast<void*>(A.rec));
@@ -2043,7 +2074,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
         rec[j] = r;
         pos[a] = j;
     }
-    __syncthreads();
+    LBA_SYNC();
     LBA_MARK(14);
     // per free pose, its edges in edge order: the chunked stable scatter, or
     // (more free poses than its tables) a wave per pose with ballot compaction
@@ -2107,7 +2138,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
         base += tot;
     }
     const int nE1 = base;
-    __syncthreads();
+    LBA_SYNC();
     // 2. kept edges per pose (wave per pose) and per point (thread per point)
     for (int p = wv; p < nP0; p += kLbaWaves) {
         int cnt = 0;
@@ -2120,7 +2151,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
         for (int j = A.le_ptr[l]; j < A.le_ptr[l + 1]; j++) c1 += nj[j] >= 0;
         cl[l] = c1;
     }
-    __syncthreads();
+    LBA_SYNC();
     // 3. new pose / point indices and list offsets: scans over the active ones
     int nP1 = 0, pe_base = 0;
     for (int c = 0; c < nP0; c += kLbaThreads) {
@@ -2139,7 +2170,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
         }
         nP1 += tot;
         pe_base += tot2;
-        __syncthreads();   // bs reads done before the next round's scans
+        LBA_SYNC();   // bs reads done before the next round's scans
     }
     int nL1 = 0, le_base = 0;
     for (int c = 0; c < nL0; c += kLbaThreads) {
@@ -2158,13 +2189,13 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_rebuild(const LbaDev* d0s, 
         }
         nL1 += tot;
         le_base += tot2;
-        __syncthreads();   // bs reads done before the next round's scans
+        LBA_SYNC();   // bs reads done before the next round's scans
     }
     if (tid == 0) {
         const_cast<int*>(B.pe_ptr)[nP1] = pe_base;
         const_cast<int*>(B.le_ptr)[nL1] = le_base;
     }
-    __syncthreads();
+    LBA_SYNC();
     // 4. the kept records, pose blocks remapped
     const Rec* ra = reinterpret_cast<const Rec*>(A.rec);
     Rec* rb = reinterpret_cast<Rec*>(const_cast<void*>(B.rec));
@@ -2824,11 +2855,11 @@ __global__ void __launch_bounds__(kLbaThreads) k_llt_bench(const double* Sin, in
         if (mode == 5 || mode == 6) {   // 1000 workgroup barriers (5); 1000 dependent LDS loads (6)
             int* q = reinterpret_cast<int*>(lds);
             for (int k = threadIdx.x; k < 1024; k += kLbaThreads) q[k] = (k + 1) & 1023;
-            __syncthreads();
+            LBA_SYNC();
             int j = threadIdx.x & 63;
             const unsigned long long t0 = lba_stamp();
             if (mode == 5)
-                for (int i = 0; i < 1000; i++) __syncthreads();
+                for (int i = 0; i < 1000; i++) LBA_SYNC();
             else
                 for (int i = 0; i < 1000; i++) j = q[j];
             const unsigned long long t1 = lba_stamp();
@@ -2852,7 +2883,7 @@ __global__ void __launch_bounds__(kLbaThreads) k_llt_bench(const double* Sin, in
     }
     for (int r = 0; r < reps; r++) {
         for (int k = threadIdx.x; k < M + n; k += kLbaThreads) S[k] = Sin[k];
-        __syncthreads();
+        LBA_SYNC();
         const unsigned long long t0 = lba_stamp();
         const bool ok = llt_solve(S, xp, n);
         const unsigned long long t1 = lba_stamp();
