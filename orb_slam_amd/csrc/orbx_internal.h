@@ -318,7 +318,6 @@ struct orbx_ctx {
     int lba_workgroups = 0;
     void* lba_split = nullptr;
     size_t lba_split_bytes = 0;
-    const unsigned* lba_split_failed = nullptr;
     void* pose_dev = nullptr;
     size_t pose_dev_bytes = 0;
     void* pose_host = nullptr;

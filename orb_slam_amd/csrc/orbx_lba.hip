@@ -142,6 +142,14 @@ struct LbaDev {
 
 enum { kRunning = 0, kTerminated = 1 };
 
+// One optimize() pass's statistics of one problem, written by k_lba_outliers
+// after the pass into the readback block (one copy brings back the results,
+// the flags and these).
+struct LbaStatRec {
+    int iterations, trials, not_posdef, pad;
+    double chi2_initial, last_chi;
+};
+
 // Phase timing of block 0 (diagnostic build only: -DORBX_LBA_PROFILE).
 #ifdef ORBX_LBA_PROFILE
 __device__ unsigned long long g_lba_prof[32];
@@ -1812,7 +1820,8 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
 template <class Rec>
 __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_all, uint8_t* status_all,
                                                       uint8_t* bad_all, int pass, double thr, int* n_out,
-                                                      const long long* offs)
+                                                      const long long* offs, LbaStatRec* stat, unsigned* split_bar,
+                                                      int* split_failed)
 {
     __shared__ int s_cnt;
     LbaDev& P = probs[blockIdx.x];
@@ -1847,7 +1856,22 @@ __global__ __launch_bounds__(256) void k_lba_outliers(LbaDev* probs, int* nobs_a
     }
     atomicAdd(&s_cnt, cnt);
     LBA_SYNC();
-    if (threadIdx.x == 0) atomicAdd(&n_out[blockIdx.x], s_cnt);   // zeroed before the solve
+    if (threadIdx.x == 0) atomicAdd(&n_out[blockIdx.x], s_cnt);   // zeroed by k_lba_build
+    if (threadIdx.x == 0 && blockIdx.y == 0) {
+        LbaStatRec& o = stat[blockIdx.x];
+        o.iterations = P.iterations;
+        o.trials = P.trials;
+        o.not_posdef = P.not_posdef;
+        o.pad = 0;
+        o.chi2_initial = P.chi2_initial;
+        o.last_chi = P.last_chi;
+        // k_lba_split's barrier words (one problem): note a timed-out barrier,
+        // re-arm the arrival counter for the next pass's launch
+        if (split_bar && blockIdx.x == 0) {
+            if (split_bar[1]) *split_failed = 1;
+            split_bar[0] = 0;
+        }
+    }
 }
 
 // Structures of the first optimize() built on the device from the caller's
@@ -1972,7 +1996,8 @@ LBA_FN void pose_chunks(const LbaDev& A, const int* ph, int nP, int (*wcnt)[kBui
 }
 
 template <class Rec>
-__global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
+__global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs, int* n_out, int P_all, unsigned* split_bar,
+                                                           int* split_failed)
 {
     __shared__ BlockScratchN<kLbaWaves> bs;
     __shared__ int s_wcnt[kLbaWaves][kBuildPoses], s_base[kBuildPoses];
@@ -1987,6 +2012,12 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_build(LbaDev* probs)
     int* cur = lh + NL;          // [NL] list cursors
     int* pos = cur + NL;         // [E] point-major position of each edge
     LBA_T0();
+    // the solve's zero state: per-edge errors, both passes' outlier counts,
+    // k_lba_split's barrier words and failed flag
+    for (int i = tid; i < 2 * E; i += kLbaThreads) A.err[i] = 0.0;
+    if (tid < 2) n_out[tid * P_all + blockIdx.x] = 0;
+    if (blockIdx.x == 0 && split_bar && tid < 16) split_bar[tid] = 0;
+    if (blockIdx.x == 0 && tid == 0) *split_failed = 0;
     for (int i = tid; i < NP; i += kLbaThreads) pflag[i] = 0;
     for (int i = tid; i < NL; i += kLbaThreads) lflag[i] = 0;
     LBA_SYNC();
@@ -2295,6 +2326,7 @@ struct LbaPlan {
     std::vector<int> n_poses, n_points, n_edges;
     long long eacc = 0, pacc = 0;
     size_t result_bytes = 0, base_bytes = 0, o_all_nobs = 0, o_all_st = 0, o_all_bad = 0, o_offs = 0, o_nout = 0;
+    size_t o_stats = 0, o_failed = 0;   // LbaStatRec [2][P], k_lba_split's failed flag: the end of the readback block
     size_t o_devs = 0, o_devs1 = 0, staged_end = 0, o_err = 0, err_bytes = 0, dev_end = 0;
     double chi2_threshold = 0;
 };
@@ -2312,7 +2344,12 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
         // pose index in 16 bits and its block in 15
         if (p.n_points >= (1 << 22) || p.n_poses > 32767) return ORBX_ERR_UNSUPPORTED;
     }
+    // the sizes-only call before this one (lba_run: plan, allocate, stage)
+    // checked the same batch: reuse its verdicts
+    const bool checked = d && L.P == P && L.d == nullptr && L.n_edges.size() == (size_t)P;
+    const bool prev_float = L.float_rec;
     std::vector<uint8_t> bad_edge(P, 0), not_float(P, 0);
+    if (!checked)
     host_parallel(P, [&](int i) {
         const orbx_ba_problem& p = probs[i];
         for (int e = 0; e < p.n_edges; e++) {
@@ -2324,8 +2361,8 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
             for (double x : v) not_float[i] |= (double)(float)x != x;
         }
     });
-    bool float_rec = true;
-    for (int i = 0; i < P; i++) {
+    bool float_rec = checked ? prev_float : true;
+    for (int i = 0; i < P && !checked; i++) {
         if (bad_edge[i]) return ORBX_ERR_ARG;
         float_rec = float_rec && !not_float[i];
     }
@@ -2363,7 +2400,9 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     L.o_all_st = at;   at += align256((size_t)L.eacc);
     L.o_all_bad = at;  at += align256((size_t)L.pacc);
     L.o_offs = at;     at += align256(L.offs.size() * 8);
-    L.o_nout = at;     at += align256(8 * (size_t)P);   // outliers per problem, per pass
+    L.o_nout = at;     at += 8 * (size_t)P;             // outliers per problem, per pass
+    L.o_stats = at;    at += sizeof(LbaStatRec) * 2 * (size_t)P;
+    L.o_failed = at;   at += align256(8);
     L.base_bytes = at;
     // Both optimize() calls' structures are built on the device: the first
     // from the caller's arrays (k_lba_build), the second from the first's
@@ -2445,7 +2484,7 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
     L.lay.stage_off = L.lay.bp_off + 6 * nf_max + 1;
     L.lds_split_bytes = (size_t)L.lay.stage_off * 8 + lba_staged_bytes();
     L.nfree0 = P > 0 ? nfree[0] : 0;
-    if (P == 1) {
+    if (P == 1 && d) {
         std::vector<int> obs(probs[0].n_points, 0);
         for (int e = 0; e < probs[0].n_edges; e++) L.max_obs0 = std::max(L.max_obs0, ++obs[probs[0].edge_point[e]]);
     }
@@ -2530,6 +2569,7 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
         fill(devs1[i], &so1[kArr * i]);   // counts and contents: k_lba_rebuild
     });
     std::memcpy(hb + L.o_offs, L.offs.data(), L.offs.size() * 8);
+    std::memset(hb + L.o_nout, 0, L.base_bytes - L.o_nout);   // counts, statistics, flag (k_lba_build zeroes them too)
     std::memcpy(hb + L.o_devs, devs.data(), sizeof(LbaDev) * P);
     std::memcpy(hb + L.o_devs1, devs1.data(), sizeof(LbaDev) * P);
     ORBX_HIP_CHECK(hipMemcpyAsync(d, hb, L.staged_end, hipMemcpyHostToDevice, ctx->stream));
@@ -2565,19 +2605,7 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
 {
     const int P = L.P;
     uint8_t* d = L.d;
-    ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_err, 0, L.err_bytes, ctx->stream));
-    ORBX_HIP_CHECK(hipMemsetAsync(d + L.o_nout, 0, 8 * (size_t)P, ctx->stream));   // outlier counts (atomic adds)
-    timer_begin(ctx, "lba_build");
-    hipLaunchKernelGGL(k_lba_build<Rec>, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
-                       reinterpret_cast<LbaDev*>(d + L.o_devs));
-    timer_end(ctx, "lba_build");
-    ORBX_HIP_CHECK(hipGetLastError());
-    // one layout for both passes: the second pass's systems are no larger
-    const size_t lds = L.lds_bytes;
-    // the reduced systems in LDS (when the batch's largest fits) or in global memory
-    auto kern = L.lay.s_doubles > 0 ? k_lba_iteration<Rec, true> : k_lba_iteration<Rec, false>;
-    // a single problem runs over G workgroups (k_lba_split) when its reduced
-    // system fits LDS and it has enough points to share out
+    // k_lba_split's buffers (a batch of one problem over G workgroups)
     LbaSplit X{};
     const int G = lba_split_workgroups(ctx, L);
     if (G > 1) {
@@ -2608,12 +2636,20 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
         X.slabs = reinterpret_cast<fx_t*>(b + o_slabs);
         X.G = G;
         X.limbs = (int)limbs;
-        // the failed flag (bar[1]) once per solve, the arrival counter per launch
-        ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 64, ctx->stream));
-        ctx->lba_split_failed = reinterpret_cast<const unsigned*>(X.bar + 1);
-    } else {
-        ctx->lba_split_failed = nullptr;
     }
+    // k_lba_build also zeroes the errors, the outlier counts and (G > 1) the
+    // barrier words; k_lba_outliers re-arms the arrival counter after a pass
+    int* n_out = reinterpret_cast<int*>(d + L.o_nout);
+    int* failed = reinterpret_cast<int*>(d + L.o_failed);
+    timer_begin(ctx, "lba_build");
+    hipLaunchKernelGGL(k_lba_build<Rec>, dim3(P), dim3(kLbaThreads), 0, ctx->stream,
+                       reinterpret_cast<LbaDev*>(d + L.o_devs), n_out, P, X.bar, failed);
+    timer_end(ctx, "lba_build");
+    ORBX_HIP_CHECK(hipGetLastError());
+    // one layout for both passes: the second pass's systems are no larger
+    const size_t lds = L.lds_bytes;
+    // the reduced systems in LDS (when the batch's largest fits) or in global memory
+    auto kern = L.lay.s_doubles > 0 ? k_lba_iteration<Rec, true> : k_lba_iteration<Rec, false>;
     bool polled = false;
     for (int i = 0; aborts && i < P; i++) polled |= aborts[i] != nullptr;
     std::vector<LbaDev> hv(polled ? P : 0);
@@ -2652,7 +2688,8 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             // without abort flags a pass's iterations run in one launch
             const int n_it = polled ? 1 : iters;
             if (G > 1) {
-                ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 4, ctx->stream));
+                if (polled && it > 0)   // a launch per iteration: re-arm the arrival counter
+                    ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 4, ctx->stream));
                 hipLaunchKernelGGL(k_lba_split<Rec>, dim3(G), dim3(kLbaThreads), L.lds_split_bytes, ctx->stream, dd, it,
                                    n_it, L.lay, X);
             } else {
@@ -2675,8 +2712,8 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
         timer_begin(ctx, "lba_outliers");
         hipLaunchKernelGGL(k_lba_outliers<Rec>, dim3(P, G > 1 ? 16 : 1), dim3(256), 0, ctx->stream, dd,
                            reinterpret_cast<int*>(d + L.o_all_nobs), d + L.o_all_st, d + L.o_all_bad, pass + 1,
-                           L.chi2_threshold, reinterpret_cast<int*>(d + L.o_nout) + pass * P,
-                           reinterpret_cast<const long long*>(d + L.o_offs));
+                           L.chi2_threshold, n_out + pass * P, reinterpret_cast<const long long*>(d + L.o_offs),
+                           reinterpret_cast<LbaStatRec*>(d + L.o_stats) + pass * P, X.bar, failed);
         timer_end(ctx, "lba_outliers");
         ORBX_HIP_CHECK(hipGetLastError());
     }
@@ -2697,38 +2734,27 @@ static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs,
     const int P = L.P;
     uint8_t* d = L.d;
     int r;
-    if ((r = ensure_pinned(ctx, std::max(L.result_bytes, L.o_all_bad + (size_t)L.pacc))) != ORBX_OK) return r;
+    if ((r = ensure_pinned(ctx, L.base_bytes)) != ORBX_OK) return r;
     uint8_t* hb = static_cast<uint8_t*>(ctx->host_pinned);
-    std::vector<LbaDev> devs(P), devs1(P);
-    std::vector<uint8_t> all_st((size_t)L.eacc, 0);
-    std::vector<int> nout(2 * (size_t)P);
-    ORBX_HIP_CHECK(hipMemcpyAsync(devs.data(), d + L.o_devs, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(devs1.data(), d + L.o_devs1, sizeof(LbaDev) * P, hipMemcpyDeviceToHost, ctx->stream));
-    if (L.eacc)
-        ORBX_HIP_CHECK(hipMemcpyAsync(all_st.data(), d + L.o_all_st, all_st.size(), hipMemcpyDeviceToHost, ctx->stream));
-    ORBX_HIP_CHECK(hipMemcpyAsync(nout.data(), d + L.o_nout, 8 * (size_t)P, hipMemcpyDeviceToHost, ctx->stream));
-    unsigned split_failed = 0;
-    if (ctx->lba_split_failed)
-        ORBX_HIP_CHECK(hipMemcpyAsync(&split_failed, ctx->lba_split_failed, 4, hipMemcpyDeviceToHost, ctx->stream));
-    // results: poses and points in one copy, scattered on host threads below
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, L.result_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    if (L.pacc)
-        ORBX_HIP_CHECK(hipMemcpyAsync(hb + L.o_all_bad, d + L.o_all_bad, (size_t)L.pacc, hipMemcpyDeviceToHost,
-                                      ctx->stream));
+    // one copy: poses, points, cameras, observation counts, edge status,
+    // point flags, offsets, outlier counts, per-pass statistics, failed flag
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, L.base_bytes, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (split_failed) return ORBX_ERR_HIP;   // a k_lba_split barrier timed out (workgroups not co-resident)
+    if (*reinterpret_cast<const int*>(hb + L.o_failed)) return ORBX_ERR_HIP;   // a k_lba_split barrier timed out
+    const int* nout = reinterpret_cast<const int*>(hb + L.o_nout);
+    const LbaStatRec* sr = reinterpret_cast<const LbaStatRec*>(hb + L.o_stats);
+    const uint8_t* all_st = hb + L.o_all_st;
     if (stats)
-        for (int pass = 0; pass < 2; pass++) {
-            const std::vector<LbaDev>& hv = pass == 0 ? devs : devs1;
+        for (int pass = 0; pass < 2; pass++)
             for (int i = 0; i < P; i++) {
-                stats[i].iterations[pass] = hv[i].iterations;
-                stats[i].levenberg_trials[pass] = hv[i].trials;
-                stats[i].chi2_initial[pass] = hv[i].chi2_initial;
-                stats[i].chi2_final[pass] = hv[i].last_chi;
+                const LbaStatRec& o = sr[pass * (size_t)P + i];
+                stats[i].iterations[pass] = o.iterations;
+                stats[i].levenberg_trials[pass] = o.trials;
+                stats[i].chi2_initial[pass] = o.chi2_initial;
+                stats[i].chi2_final[pass] = o.last_chi;
                 stats[i].n_outliers[pass] = nout[pass * (size_t)P + i];
-                stats[i].not_posdef += hv[i].not_posdef;
+                stats[i].not_posdef += o.not_posdef;
             }
-        }
     host_parallel(P, [&](int i) {
         orbx_ba_problem& p = probs[i];
         const double* pose = reinterpret_cast<const double*>(hb + L.pl[i].pose);
@@ -2737,7 +2763,7 @@ static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs,
             for (int j = 0; j < 3; j++) p.pose_t[3 * k + j] = pose[7 * k + 4 + j];
         }
         std::memcpy(p.points, hb + L.pl[i].point, 3 * (size_t)p.n_points * 8);
-        if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st.data() + L.offs[3 * i], p.n_edges);
+        if (edge_status && edge_status[i]) std::memcpy(edge_status[i], all_st + L.offs[3 * i], p.n_edges);
         if (point_bad && point_bad[i]) std::memcpy(point_bad[i], hb + L.o_all_bad + L.offs[3 * i + 1], p.n_points);
     });
     return ORBX_OK;
