@@ -519,21 +519,42 @@ struct Uploader {
     uint8_t* base() const { return static_cast<uint8_t*>(ctx->scratch); }
 };
 
-int put(orbx_ctx* ctx, size_t off, const void* src, size_t bytes)
-{
-    if (bytes == 0 || !src) return ORBX_OK;
-    ORBX_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(ctx->scratch) + off, src, bytes, hipMemcpyHostToDevice,
-                                  ctx->stream));
-    return ORBX_OK;
-}
-
-int get(orbx_ctx* ctx, void* dst, size_t off, size_t bytes)
-{
-    if (bytes == 0 || !dst) return ORBX_OK;
-    ORBX_HIP_CHECK(hipMemcpyAsync(dst, static_cast<uint8_t*>(ctx->scratch) + off, bytes, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-    return ORBX_OK;
-}
+// One call's device block staged through the context's page-locked buffer:
+// inputs (and initialised outputs) are written at their device offsets into
+// the pinned copy and go over in ONE copy, the outputs come back in ONE copy
+// from out_begin -- instead of a copy per array, each of which costs a
+// DMA setup (and, from pageable memory, a staging kernel).
+struct Pinned {
+    orbx_ctx* ctx;
+    uint8_t* h = nullptr;
+    int open(size_t total)
+    {
+        const int r = ensure_pinned(ctx, total);
+        h = static_cast<uint8_t*>(ctx->host_pinned);
+        return r;
+    }
+    void put(size_t off, const void* src, size_t bytes)
+    {
+        if (bytes && src) std::memcpy(h + off, src, bytes);
+    }
+    void fill(size_t off, int v, size_t bytes) { std::memset(h + off, v, bytes); }
+    int upload(size_t bytes)
+    {
+        ORBX_HIP_CHECK(hipMemcpyAsync(ctx->scratch, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+        return ORBX_OK;
+    }
+    int download(size_t begin, size_t end)
+    {
+        ORBX_HIP_CHECK(hipMemcpyAsync(h + begin, static_cast<uint8_t*>(ctx->scratch) + begin, end - begin,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+        ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        return ORBX_OK;
+    }
+    void get(void* dst, size_t off, size_t bytes) const
+    {
+        if (bytes && dst) std::memcpy(dst, h + off, bytes);
+    }
+};
 
 bool valid_view(const orbx_frame_view* v)
 {
@@ -574,11 +595,10 @@ FrameOffs reserve_frame(Uploader& u, const orbx_frame_view* v)
     return o;
 }
 
-int put_frame(orbx_ctx* ctx, const FrameOffs& o, const orbx_frame_view* v)
+void put_frame(Pinned& pin, const FrameOffs& o, const orbx_frame_view* v)
 {
-    int r = put(ctx, o.kp, v->keys_un, (size_t)v->n * sizeof(orbx_keypoint));
-    if (r == ORBX_OK) r = put(ctx, o.desc, v->desc, (size_t)v->n * 32);
-    return r;
+    pin.put(o.kp, v->keys_un, (size_t)v->n * sizeof(orbx_keypoint));
+    pin.put(o.desc, v->desc, (size_t)v->n * 32);
 }
 
 size_t tab_lds(int n) { return (size_t)n * 16 + ((n + 15) & ~15) + (size_t)n * 4 + 32 * 4 + 64; }
@@ -597,25 +617,11 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     if (!ctx || !valid_view(F1) || !valid_view(F2) || !prev_matched || !matches12 || !n_matches || window < 0)
         return ORBX_ERR_ARG;
     ctx_enter(ctx);
+    // inputs, then the outputs (prev_out starts as a copy of prev_matched)
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
-    const size_t op = u.reserve((size_t)F1->n * 8), oo = u.reserve((size_t)F1->n * 4 + 4), on = u.reserve(4);
-    const size_t opo = u.reserve((size_t)F1->n * 8);
-    int r = ensure_scratch(ctx, u.total);
-    if (r != ORBX_OK) return r;
-    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, op, prev_matched, (size_t)F1->n * 8)) ||
-        (r = put(ctx, opo, prev_matched, (size_t)F1->n * 8)))
-        return r;
-    SearchArgs a{};
-    a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
-    a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
-    a.prev_xy = reinterpret_cast<const float*>(u.base() + op);
-    a.prev_out = reinterpret_cast<float*>(u.base() + opo);
-    a.window = window;
-    a.nnratio = nnratio;
-    a.check_ori = check_ori;
-    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
-    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
+    const size_t op = u.reserve((size_t)F1->n * 8);
+    const size_t opo = u.reserve((size_t)F1->n * 8), oo = u.reserve((size_t)F1->n * 4 + 4), on = u.reserve(4);
     // candidate slots = F2 keypoints of octave 0
     int cap_c = 0;
     for (int i = 0; i < F2->n; i++) cap_c += F2->keys_un[i].octave == 0;
@@ -626,12 +632,31 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     const int cap_keys = std::max<int>(cap_c, (int)((kInitLdsBudget - std::min(fixed, kInitLdsBudget)) / 4));
     const size_t lds = init_lds_bytes(cap_c, cap1, cap_keys);
     if (lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
+    int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r != ORBX_OK) return r;
+    put_frame(pin, o1, F1);
+    put_frame(pin, o2, F2);
+    pin.put(op, prev_matched, (size_t)F1->n * 8);
+    pin.put(opo, prev_matched, (size_t)F1->n * 8);
+    if ((r = pin.upload(oo)) != ORBX_OK) return r;
+    SearchArgs a{};
+    a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
+    a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
+    a.prev_xy = reinterpret_cast<const float*>(u.base() + op);
+    a.prev_out = reinterpret_cast<float*>(u.base() + opo);
+    a.window = window;
+    a.nnratio = nnratio;
+    a.check_ori = check_ori;
+    a.out = reinterpret_cast<int32_t*>(u.base() + oo);
+    a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
     hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(256), lds, ctx->stream, a, cap_c, cap_keys, ctx->error_flags);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, matches12, oo, (size_t)F1->n * 4)) || (r = get(ctx, n_matches, on, 4)) ||
-        (r = get(ctx, prev_matched, opo, (size_t)F1->n * 8)))
-        return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(opo, u.total)) != ORBX_OK) return r;
+    pin.get(matches12, oo, (size_t)F1->n * 4);
+    pin.get(n_matches, on, 4);
+    pin.get(prev_matched, opo, (size_t)F1->n * 8);
     return *n_matches < 0 ? *n_matches : ORBX_OK;
 }
 
@@ -646,9 +671,14 @@ int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_fram
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t ov = u.reserve(F1->n), oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
     int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
     if (r != ORBX_OK) return r;
-    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, ov, f1_mp, F1->n))) return r;
-    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F2->n * 4 + 4, ctx->stream));
+    put_frame(pin, o1, F1);
+    put_frame(pin, o2, F2);
+    pin.put(ov, f1_mp, F1->n);
+    pin.fill(oo, 0xFF, (size_t)F2->n * 4 + 4);
+    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
     a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
@@ -662,8 +692,9 @@ int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_fram
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
     hipLaunchKernelGGL(k_window_search, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, matches21, oo, (size_t)F2->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.get(matches21, oo, (size_t)F2->n * 4);
+    pin.get(n_matches, on, 4);
     return ORBX_OK;
 }
 
@@ -681,11 +712,16 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     const size_t ox = u.reserve((size_t)F1->n * 12), ov = u.reserve(F1->n), oa = u.reserve(F2->n);
     const size_t oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
     int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
     if (r != ORBX_OK) return r;
-    if ((r = put_frame(ctx, o1, F1)) || (r = put_frame(ctx, o2, F2)) || (r = put(ctx, ox, f1_mp_xyz, (size_t)F1->n * 12)) ||
-        (r = put(ctx, ov, f1_mp_valid, F1->n)) || (r = put(ctx, oa, f2_assigned, F2->n)))
-        return r;
-    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F2->n * 4 + 4, ctx->stream));
+    put_frame(pin, o1, F1);
+    put_frame(pin, o2, F2);
+    pin.put(ox, f1_mp_xyz, (size_t)F1->n * 12);
+    pin.put(ov, f1_mp_valid, F1->n);
+    pin.put(oa, f2_assigned, F2->n);
+    pin.fill(oo, 0xFF, (size_t)F2->n * 4 + 4);
+    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
     a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
@@ -700,8 +736,9 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
     hipLaunchKernelGGL(k_proj_pair, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, matches21, oo, (size_t)F2->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.get(matches21, oo, (size_t)F2->n * 4);
+    pin.get(n_matches, on, 4);
     return ORBX_OK;
 }
 
@@ -719,12 +756,16 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     const size_t ox = u.reserve((size_t)Last->n * 12), ov = u.reserve(Last->n), oa = u.reserve(Cur->n);
     const size_t oo = u.reserve((size_t)Cur->n * 4 + 4), on = u.reserve(4);
     int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
     if (r != ORBX_OK) return r;
-    if ((r = put_frame(ctx, oL, Last)) || (r = put_frame(ctx, oC, Cur)) ||
-        (r = put(ctx, ox, last_mp_xyz, (size_t)Last->n * 12)) || (r = put(ctx, ov, last_mp_valid, Last->n)) ||
-        (r = put(ctx, oa, cur_assigned, Cur->n)))
-        return r;
-    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)Cur->n * 4 + 4, ctx->stream));
+    put_frame(pin, oL, Last);
+    put_frame(pin, oC, Cur);
+    pin.put(ox, last_mp_xyz, (size_t)Last->n * 12);
+    pin.put(ov, last_mp_valid, Last->n);
+    pin.put(oa, cur_assigned, Cur->n);
+    pin.fill(oo, 0xFF, (size_t)Cur->n * 4 + 4);
+    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(Last, u.base(), oL.kp, oL.desc);
     a.F2 = dev_frame(Cur, u.base(), oC.kp, oC.desc);
@@ -740,8 +781,9 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
     hipLaunchKernelGGL(k_proj_motion, dim3(1), dim3(64), tab_lds(std::max(Cur->n, 1)), ctx->stream, a);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, matches_cur, oo, (size_t)Cur->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.get(matches_cur, oo, (size_t)Cur->n * 4);
+    pin.get(n_matches, on, 4);
     return ORBX_OK;
 }
 
@@ -762,12 +804,18 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     const size_t oc = u.reserve((size_t)n_mp * 4), od = u.reserve((size_t)n_mp * 32), oa = u.reserve(F->n);
     const size_t oo = u.reserve((size_t)F->n * 4 + 4), on = u.reserve(4);
     int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
     if (r != ORBX_OK) return r;
-    if ((r = put_frame(ctx, oF, F)) || (r = put(ctx, ov, in_view, n_mp)) || (r = put(ctx, op, proj_xy, (size_t)n_mp * 8)) ||
-        (r = put(ctx, ol, pred_level, (size_t)n_mp * 4)) || (r = put(ctx, oc, view_cos, (size_t)n_mp * 4)) ||
-        (r = put(ctx, od, mp_desc, (size_t)n_mp * 32)) || (r = put(ctx, oa, f_assigned, F->n)))
-        return r;
-    ORBX_HIP_CHECK(hipMemsetAsync(u.base() + oo, 0xFF, (size_t)F->n * 4 + 4, ctx->stream));
+    put_frame(pin, oF, F);
+    pin.put(ov, in_view, n_mp);
+    pin.put(op, proj_xy, (size_t)n_mp * 8);
+    pin.put(ol, pred_level, (size_t)n_mp * 4);
+    pin.put(oc, view_cos, (size_t)n_mp * 4);
+    pin.put(od, mp_desc, (size_t)n_mp * 32);
+    pin.put(oa, f_assigned, F->n);
+    pin.fill(oo, 0xFF, (size_t)F->n * 4 + 4);
+    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F2 = dev_frame(F, u.base(), oF.kp, oF.desc);
     a.nq = n_mp;
@@ -784,8 +832,9 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
     hipLaunchKernelGGL(k_proj_local, dim3(1), dim3(64), tab_lds(std::max(F->n, 1)), ctx->stream, a);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, matches_f, oo, (size_t)F->n * 4)) || (r = get(ctx, n_matches, on, 4))) return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.get(matches_f, oo, (size_t)F->n * 4);
+    pin.get(n_matches, on, 4);
     return ORBX_OK;
 }
 
@@ -935,18 +984,23 @@ static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8
     const size_t oi = u.reserve((size_t)nA * 4), o1 = u.reserve((size_t)nA * 4), o2 = u.reserve((size_t)nA * 4);
     const size_t om = u.reserve((size_t)nA * 4);
     int r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(u.total);
     if (r != ORBX_OK) return r;
-    if ((r = put(ctx, oa, dA, (size_t)nA * 32)) || (r = put(ctx, ob, dB, (size_t)nB * 32))) return r;
+    pin.put(oa, dA, (size_t)nA * 32);
+    pin.put(ob, dB, (size_t)nB * 32);
+    if ((r = pin.upload(oi)) != ORBX_OK) return r;
     uint8_t* base = u.base();
     hipLaunchKernelGGL(k_hamming_bf, dim3((nA + 255) / 256), dim3(256), 0, ctx->stream, base + oa, nA, base + ob, nB,
                        reinterpret_cast<int32_t*>(base + oi), reinterpret_cast<int32_t*>(base + o1),
                        reinterpret_cast<int32_t*>(base + o2), m12 ? reinterpret_cast<int32_t*>(base + om) : nullptr,
                        th_low, nnratio);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = get(ctx, best_idx, oi, (size_t)nA * 4)) || (r = get(ctx, best, o1, (size_t)nA * 4)) ||
-        (r = get(ctx, second, o2, (size_t)nA * 4)) || (r = get(ctx, m12, om, (size_t)nA * 4)))
-        return r;
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if ((r = pin.download(oi, u.total)) != ORBX_OK) return r;
+    pin.get(best_idx, oi, (size_t)nA * 4);
+    pin.get(best, o1, (size_t)nA * 4);
+    pin.get(second, o2, (size_t)nA * 4);
+    pin.get(m12, om, (size_t)nA * 4);
     return ORBX_OK;
 }
 
