@@ -904,12 +904,13 @@ def run_lba(args, wl, rank, local, world, dist):
     st = (sb.BAStats * P)()
     check_rc(L.orbx_lba_fetch(ctx.handle, arr, esp, pbp, st), "orbx_lba_fetch")
     cpu_leg = rank == 0 and not args.no_cpu_baseline
-    # the last timed run's results against the oracle, before the host-array
-    # leg below reuses these arrays
-    parity = parity_lba(uniq, work, es, pb, st) if cpu_leg else None
     stats = np.array([elapsed, P * args.steps, st[0].iterations[0] + st[0].iterations[1], st[0].n_outliers[0]],
                      dtype=np.float64)
     allst = odist.gather_stats(stats, dist, device=args.gather_device)   # before rank 0's CPU legs
+    # the last timed run's results against the oracle, before the host-array
+    # leg below reuses these arrays (after the gather: the other ranks do
+    # not wait in the collective while rank 0 runs the oracle)
+    parity = parity_lba(uniq, work, es, pb, st) if cpu_leg else None
     # the host-array boundary (orbx_lba_solve_batch: packing, H2D upload,
     # both passes, D2H readback and unpacking), timed beside it on rank 0;
     # reported in `check`, never as `value`

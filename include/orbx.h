@@ -700,7 +700,13 @@ typedef struct {
  * the graph), optimize(iters1) and the second outlier pass.  edge_status
  * (out, n_edges): 0 inlier, 1 erased in pass 1, 2 erased in pass 2.
  * point_bad (out, n_points): MapPoint became bad through EraseObservation.
- * abort: polled between LM iterations (mbAbortBA; may be NULL). */
+ * abort: polled between LM iterations (mbAbortBA; may be NULL).  g2o also
+ * tests its stop flag between the trials of an iteration (levenberg.cpp:149);
+ * here an iteration that has started runs its trials to the end, so a flag
+ * raised mid-iteration stops the solve at the same iteration boundary but
+ * possibly after more trials.
+ * One problem runs over several workgroups when it qualifies
+ * (orbx_lba_set_workgroups), with the same result bits. */
 int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
                    const volatile uint8_t* abort, uint8_t* edge_status,
                    uint8_t* point_bad, orbx_ba_stats* stats);

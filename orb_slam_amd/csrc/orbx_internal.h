@@ -323,6 +323,7 @@ struct orbx_ctx {
     void* pose_host = nullptr;
     size_t pose_host_bytes = 0;
     bool pose_exact = false;   // orbx_pose_set_exact: sequential sums in g2o's edge order
+    int pose_wide_max = 1;     // batches up to this size run a workgroup per frame (k_pose_opt kW > 1)
     int pose_P = 0;
     long long pose_E = 0;
     size_t pose_o_flags = 0, pose_o_out = 0, pose_out_bytes = 0;

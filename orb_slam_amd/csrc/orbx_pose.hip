@@ -68,6 +68,9 @@ constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
 // instead of re-fetching the frame from HBM; edges past the first 800 are
 // read from global memory.
 constexpr int kPoseLdsEdges = 800;
+// edges a one-frame workgroup (the kW > 1 instances) keeps in LDS: 75 KB
+constexpr int kPoseLdsEdgesWide = 3072;
+constexpr int kPoseWideWaves = 4;    // wavefronts per frame of the one-call kernel
 static_assert((kPoseThreads / 64) * kPoseLdsEdges * (6 * sizeof(float) + 1) <= 80 * 1024,
               "two pose workgroups per CU need <= 80 KB of LDS each (gfx950: 160 KB per CU)");
 
@@ -314,14 +317,26 @@ __device__ inline void pose_edge_terms(const double* pose, const Cam& cam, doubl
 // +0.0: the sum starts at +0.0 and round-to-nearest never yields -0.0 from
 // it, so adding +0.0 leaves every bit as skipping the edge would.  The term
 // rows (57 KB per workgroup) sit beside the edge cache: one workgroup per CU.
-template <bool kExact>
-__global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __restrict__ hdrs, PoseEdgeArrays ed,
-                                                          uint8_t* __restrict__ eflag, PoseOut* __restrict__ outs,
-                                                          int P, double delta)
+//
+// kW > 1 (a single frame or a few, orbx_pose_optimization's one call): a
+// workgroup of kW wavefronts per frame, the edges strided over all of its
+// threads, each sum formed per wave (the DPP tree) and then over the waves in
+// wave order through LDS -- deterministic, and the same LM logic on the
+// same uniform data, but another summation order than the one-wave kernel.
+template <bool kExact, int kW = 1>
+__global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(const PoseHdr* __restrict__ hdrs,
+                                                                              PoseEdgeArrays ed,
+                                                                              uint8_t* __restrict__ eflag,
+                                                                              PoseOut* __restrict__ outs, int P,
+                                                                              double delta)
 {
-    const int prob = blockIdx.x * (kPoseThreads / 64) + (threadIdx.x >> 6);
-    if (prob >= P) return;   // whole wavefront
-    const int lane = threadIdx.x & 63;
+    static_assert(kW == 1 || !kExact, "the exact sums run one wave per frame");
+    constexpr int kT = 64 * kW;                          // threads striding one frame's edges
+    constexpr int kFrames = kW == 1 ? kPoseThreads / 64 : 1;
+    constexpr int kCache = kW == 1 ? kPoseLdsEdges : kPoseLdsEdgesWide;
+    const int prob = kW == 1 ? blockIdx.x * (kPoseThreads / 64) + (threadIdx.x >> 6) : blockIdx.x;
+    if (prob >= P) return;   // whole wavefront (kW > 1: whole workgroup)
+    const int lane = kW == 1 ? threadIdx.x & 63 : threadIdx.x;   // position among the frame's threads
     const PoseHdr& H = hdrs[prob];
     const long long e0 = H.e0;
     const int nE = H.nE;
@@ -349,11 +364,45 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
     const float* py = ed.py + e0;
     const float* pz = ed.pz + e0;
     uint8_t* flag = eflag + e0;
-    __shared__ float s_e[kPoseThreads / 64][6][kPoseLdsEdges];
-    __shared__ uint8_t s_f[kPoseThreads / 64][kPoseLdsEdges];
+    __shared__ float s_e[kFrames][6][kCache];
+    __shared__ uint8_t s_f[kFrames][kCache];
     __shared__ double s_rows[kExact ? kPoseThreads / 64 : 1][kExact ? 64 : 1][28];   // per-edge terms
-    const int wq = threadIdx.x >> 6;
-    const int nL = min(nE, kPoseLdsEdges);
+    __shared__ double s_red[kW][28];                                                 // kW > 1: per-wave sums
+    const int wq = kW == 1 ? threadIdx.x >> 6 : 0;
+    const int nL = min(nE, kCache);
+    // sums over the frame's threads, the same double on every thread: the
+    // wave's DPP tree, then (kW > 1) the waves' sums in wave order
+    auto frame_sums = [&](double* v, const int n) {
+#pragma unroll
+        for (int k = 0; k < n; k++) v[k] = wave_sum_uniform(v[k]);
+        if constexpr (kW > 1) {
+            if ((threadIdx.x & 63) == 0)
+#pragma unroll
+                for (int k = 0; k < n; k++) s_red[threadIdx.x >> 6][k] = v[k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < n; k++) {
+                double t = s_red[0][k];
+#pragma unroll
+                for (int w = 1; w < kW; w++) t += s_red[w][k];
+                v[k] = t;
+            }
+            __syncthreads();
+        }
+    };
+    auto frame_sum_int = [&](int v) {
+        v = wave_sum_int(v);
+        if constexpr (kW > 1) {
+            if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6][0] = (double)v;
+            __syncthreads();
+            int t = 0;
+#pragma unroll
+            for (int w = 0; w < kW; w++) t += (int)s_red[w][0];
+            __syncthreads();
+            return t;
+        }
+        return v;
+    };
     float* lox = s_e[wq][0];
     float* loy = s_e[wq][1];
     float* lis = s_e[wq][2];
@@ -362,7 +411,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
     float* lpz = s_e[wq][5];
     uint8_t* lfl = s_f[wq];
 #pragma unroll 1
-    for (int a = lane; a < nL; a += 64) {
+    for (int a = lane; a < nL; a += kT) {
         const float v0 = ox[a], v1 = oy[a], v2 = isg[a], v3 = px[a], v4 = py[a], v5 = pz[a];
         lox[a] = v0;
         loy[a] = v1;
@@ -372,17 +421,22 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
         lpz[a] = v5;
         lfl[a] = 0;
     }
-    for (int a = nL + lane; a < nE; a += 64) flag[a] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the frame's edges: LDS part [0, nL), global part [nL, nE)
+    for (int a = nL + lane; a < nE; a += kT) flag[a] = 0;
+    if constexpr (kW == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+    // the frame's edges: LDS part [0, nL), global part [nL, nE); an edge
+    // stays on one thread for the whole run, so its flag is thread-private
     auto for_edges = [&](auto&& body) {
 #pragma unroll 1
-        for (int a = lane; a < nL; a += 64)
+        for (int a = lane; a < nL; a += kT)
             if (!lfl[a]) body(lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a]);
 #pragma unroll 1
-        for (int a = nL + lane; a < nE; a += 64)
+        for (int a = nL + lane; a < nE; a += kT)
             if (!flag[a]) body(ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
     };
 
@@ -492,11 +546,10 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
 #pragma unroll
                         for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
                 });
-                currentChi = wave_sum_uniform(chi);
-#pragma unroll
-                for (int k = 0; k < 21; k++) h[k] = wave_sum_uniform(h[k]);
-#pragma unroll
-                for (int k = 0; k < 6; k++) bv[k] = wave_sum_uniform(bv[k]);
+                frame_sums(&chi, 1);
+                frame_sums(h, 21);
+                frame_sums(bv, 6);
+                currentChi = chi;
                 }
                 const double iniChi = currentChi;
                 if (iter == 0) {   // computeLambdaInit (levenberg.cpp:166-180)
@@ -511,20 +564,41 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                 int qmax = 0;
                 do {
                     double m[21], xs[6], tp[7];
+                    bool ok2 = false;
+                    // kW > 1: wave 0 alone solves and steps (the other waves
+                    // would only compete for the SIMDs), then shares the result
+                    if (kW == 1 || threadIdx.x < 64) {
 #pragma unroll
-                    for (int k = 0; k < 21; k++) m[k] = h[k];
+                        for (int k = 0; k < 21; k++) m[k] = h[k];
 #pragma unroll
-                    for (int j = 0; j < 6; j++) m[LT(j, j)] += lambda;
-                    const bool ok2 = ldlt6_solve(m, bv, xs);
+                        for (int j = 0; j < 6; j++) m[LT(j, j)] += lambda;
+                        ok2 = ldlt6_solve(m, bv, xs);
 #pragma unroll
-                    for (int i = 0; i < 7; i++) tp[i] = pose[i];
-                    if (ok2) {
-                        se3_oplus(tp, xs);
-                    } else {
-                        not_posdef++;
+                        for (int i = 0; i < 7; i++) tp[i] = pose[i];
+                        if (ok2) {
+                            se3_oplus(tp, xs);
+                        } else {
 #pragma unroll
-                        for (int i = 0; i < 6; i++) xs[i] = 0.0;
+                            for (int i = 0; i < 6; i++) xs[i] = 0.0;
+                        }
                     }
+                    if constexpr (kW > 1) {
+                        if (threadIdx.x == 0) {
+#pragma unroll
+                            for (int i = 0; i < 6; i++) s_red[0][i] = xs[i];
+#pragma unroll
+                            for (int i = 0; i < 7; i++) s_red[0][6 + i] = tp[i];
+                            s_red[0][13] = ok2 ? 1.0 : 0.0;
+                        }
+                        __syncthreads();
+#pragma unroll
+                        for (int i = 0; i < 6; i++) xs[i] = s_red[0][i];
+#pragma unroll
+                        for (int i = 0; i < 7; i++) tp[i] = s_red[0][6 + i];
+                        ok2 = s_red[0][13] != 0.0;
+                        __syncthreads();
+                    }
+                    if (!ok2) not_posdef++;
                     // computeActiveErrors at the trial estimate
                     auto trial_chi = [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
                         const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
@@ -547,7 +621,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
                         for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
                             tchi += trial_chi(fo0, fo1, fis, fx_, fy_, fz_);
                         });
-                        tempChi = wave_sum_uniform(tchi);
+                        frame_sums(&tchi, 1);
+                        tempChi = tchi;
                     }
 #pragma unroll
                     for (int i = 0; i < 7; i++) errpose[i] = tp[i];
@@ -600,11 +675,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
             return nf;
         };
 #pragma unroll 1
-        for (int a = lane; a < nL; a += 64) lfl[a] = classify(lfl[a], lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a]);
+        for (int a = lane; a < nL; a += kT) lfl[a] = classify(lfl[a], lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a]);
 #pragma unroll 1
-        for (int a = nL + lane; a < nE; a += 64) flag[a] = classify(flag[a], ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
-        nBadOut = wave_sum_int(bad);
-        n_active = wave_sum_int(act);
+        for (int a = nL + lane; a < nE; a += kT) flag[a] = classify(flag[a], ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
+        nBadOut = frame_sum_int(bad);
+        n_active = frame_sum_int(act);
         if (lane == 0) {
             out.iterations[it] = r_iters;
             out.trials[it] = r_trials;
@@ -613,7 +688,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(const PoseHdr* __rest
         }
         if (nE < 10) break;
     }
-    for (int a = lane; a < nL; a += 64) flag[a] = lfl[a];   // mvbOutlier of the LDS part
+    for (int a = lane; a < nL; a += kT) flag[a] = lfl[a];   // mvbOutlier of the LDS part
     if (lane == 0) {
         double R[9];
         qmat(Q{pose[0], pose[1], pose[2], pose[3]}, R);
@@ -659,7 +734,11 @@ void pose_parallel(int n, Fn fn)
 
 using namespace orbx;
 
-extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames)
+// sync: wait for the upload (orbx_pose_stage: the caller may stage again
+// before running; the one-call batch below runs and fetches on the same
+// stream, which orders the copies, and its host threads touch the buffer
+// only after the fetch's synchronisation)
+static int pose_stage_impl(orbx_ctx* ctx, int P, const orbx_pose_frame* frames, bool sync)
 {
     if (!ctx || P < 0 || (P > 0 && !frames)) return ORBX_ERR_ARG;
     std::vector<long long> e0(P + 1, 0);
@@ -687,7 +766,7 @@ extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* fram
     const size_t out_bytes = sizeof(PoseOut) * (size_t)std::max(P, 1);
     const size_t total = o_out + align256(out_bytes);
     const size_t staged = o_flags;                                  // copied H2D
-    const size_t host_need = std::max(staged, out_bytes + (size_t)std::max<long long>(E, 1));
+    const size_t host_need = std::max(staged, o_out - o_flags + out_bytes);   // fetch: flags | outputs, one copy
     if (total > ctx->pose_dev_bytes) {
         if (ctx->pose_dev) (void)hipFree(ctx->pose_dev);
         ctx->pose_dev = nullptr;
@@ -730,7 +809,7 @@ extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* fram
         }
     });
     ORBX_HIP_CHECK(hipMemcpyAsync(ctx->pose_dev, hb, staged, hipMemcpyHostToDevice, ctx->stream));
-    ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));   // the pinned buffer is reused by fetch
+    if (sync) ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));   // the pinned buffer is reused by fetch
     ctx->pose_P = P;
     ctx->pose_E = E;
     ctx->pose_o_flags = o_flags;
@@ -739,6 +818,11 @@ extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* fram
     ctx->pose_e0 = e0;
     ctx->pose_ran = false;
     return ORBX_OK;
+}
+
+extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames)
+{
+    return pose_stage_impl(ctx, P, frames, true);
 }
 
 extern "C" int orbx_pose_run(orbx_ctx* ctx)
@@ -761,10 +845,13 @@ extern "C" int orbx_pose_run(orbx_ctx* ctx)
     const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
     const int per = kPoseThreads / 64;
     timer_begin(ctx, "pose");
-    auto kern = ctx->pose_exact ? k_pose_opt<true> : k_pose_opt<false>;
-    kern<<<(P + per - 1) / per, kPoseThreads, 0, ctx->stream>>>(
-        reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags, reinterpret_cast<PoseOut*>(d + ctx->pose_o_out),
-        P, delta);
+    // a lone frame (the reference's one call per frame) gets a workgroup of
+    // kPoseWideWaves wavefronts; batches a wavefront per frame
+    const bool wide = !ctx->pose_exact && P <= ctx->pose_wide_max;
+    auto kern = ctx->pose_exact ? k_pose_opt<true> : (wide ? k_pose_opt<false, kPoseWideWaves> : k_pose_opt<false>);
+    const int blocks = wide ? P : (P + per - 1) / per, threads = wide ? 64 * kPoseWideWaves : kPoseThreads;
+    kern<<<blocks, threads, 0, ctx->stream>>>(reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags,
+                                              reinterpret_cast<PoseOut*>(d + ctx->pose_o_out), P, delta);
     timer_end(ctx, "pose");
     ORBX_HIP_CHECK(hipGetLastError());
     return ORBX_OK;
@@ -776,16 +863,14 @@ extern "C" int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* 
     ctx_enter(ctx);
     const int P = ctx->pose_P;
     if (P == 0) return ORBX_OK;
-    const long long E = ctx->pose_E;
     uint8_t* hb = static_cast<uint8_t*>(ctx->pose_host);
     uint8_t* d = static_cast<uint8_t*>(ctx->pose_dev);
-    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d + ctx->pose_o_out, ctx->pose_out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    if (E > 0)
-        ORBX_HIP_CHECK(hipMemcpyAsync(hb + ctx->pose_out_bytes, d + ctx->pose_o_flags, (size_t)E,
-                                      hipMemcpyDeviceToHost, ctx->stream));
+    // flags and outputs are adjacent on the device: one copy
+    const size_t span = ctx->pose_o_out - ctx->pose_o_flags + ctx->pose_out_bytes;
+    ORBX_HIP_CHECK(hipMemcpyAsync(hb, d + ctx->pose_o_flags, span, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    const PoseOut* outs = reinterpret_cast<const PoseOut*>(hb);
-    const uint8_t* flags = hb + ctx->pose_out_bytes;
+    const PoseOut* outs = reinterpret_cast<const PoseOut*>(hb + (ctx->pose_o_out - ctx->pose_o_flags));
+    const uint8_t* flags = hb;
     pose_parallel(P, [&](int i) {
         orbx_pose_frame& f = frames[i];
         const PoseOut& o = outs[i];
@@ -815,7 +900,7 @@ extern "C" int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* 
 extern "C" int orbx_pose_optimization_batch(orbx_ctx* ctx, int P, orbx_pose_frame* frames, int32_t* n_inliers,
                                             orbx_pose_stats* stats)
 {
-    int r = orbx_pose_stage(ctx, P, frames);
+    int r = pose_stage_impl(ctx, P, frames, false);
     if (r != ORBX_OK) return r;
     if ((r = orbx_pose_run(ctx)) != ORBX_OK) return r;
     return orbx_pose_fetch(ctx, frames, n_inliers, stats);
