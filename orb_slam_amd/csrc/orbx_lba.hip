@@ -526,6 +526,17 @@ LBA_FN void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
 template <bool kLds>
 LBA_FN void fx_atomic(fx_t* p, fx_t v)
 {
+#if defined(ORBX_LBA_DIAG_NOATOMIC)   // timing diagnostics only (wrong sums): a plain LDS add
+    if constexpr (kLds) {
+        *p += v;
+        return;
+    }
+#elif defined(ORBX_LBA_DIAG_NOSTORE)  // timing diagnostics only: the contribution is computed, not stored
+    if constexpr (kLds) {
+        asm volatile("" ::"v"(v));
+        return;
+    }
+#endif
     if constexpr (kLds) {
         atomicAdd(p, v);
     } else {
