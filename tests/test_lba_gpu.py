@@ -170,6 +170,51 @@ def test_lba_batch_per_problem_abort(ctx):
                 assert np.array_equal(es[k], s[1]) and np.array_equal(pb[k], s[2])
 
 
+def test_lba_abort_raised_during_the_run(ctx):
+    """A flag raised by another host thread while the batch runs (mbAbortBA set
+    by LocalMapping's caller mid-optimisation): the flagged problem stops at
+    an iteration boundary of whichever pass it is in and skips the rest of
+    that pass and the next one; its result equals an unflagged solve with
+    exactly the iteration counts it reports, whenever the flag landed.  The
+    other problems equal their single solves."""
+    import threading
+    import time
+    probs = [sb.make_problem(n_kf=12, n_points=900 + 100 * k, seed=80 + k) for k in range(3)]
+    singles = [run_gpu(ctx, pr) for pr in probs]
+    L = ox.lib()
+    for delay in (0.002, 0.006):
+        flag = ctypes.c_uint8(0)
+        ab = (ctypes.c_void_p * 3)(None, ctypes.addressof(flag), None)
+        cps = [sb.to_ctypes(pr) for pr in probs]
+        arr = (sb.BAProblem * 3)(*[c[0] for c in cps])
+        es = [np.zeros(c[0].n_edges, np.uint8) for c in cps]
+        pb = [np.zeros(c[0].n_points, np.uint8) for c in cps]
+        esp = (ctypes.c_void_p * 3)(*[e.ctypes.data for e in es])
+        pbp = (ctypes.c_void_p * 3)(*[b.ctypes.data for b in pb])
+        st = (sb.BAStats * 3)()
+
+        def raise_flag():
+            time.sleep(delay)
+            flag.value = 1
+
+        th = threading.Thread(target=raise_flag)
+        th.start()
+        assert L.orbx_lba_solve_batch(ctx.handle, 3, arr, 5, 10, ab, esp, pbp, st) == 0
+        th.join()
+        for k in (0, 2):
+            s = singles[k]
+            assert list(st[k].iterations) == list(s[3].iterations)
+            assert np.array_equal(cps[k][1]["pose_q"], s[0]["pose_q"]) and np.array_equal(cps[k][1]["points"], s[0]["points"])
+        k0, k1 = st[1].iterations
+        n0, n1 = singles[1][3].iterations
+        assert k0 <= n0 and k1 <= n1
+        ref = run_gpu(ctx, probs[1], k0, k1)
+        got = cps[1][1]
+        for key in ("pose_q", "pose_t", "points"):
+            assert np.array_equal(got[key], ref[0][key]), (delay, k0, k1, key)
+        assert np.array_equal(es[1], ref[1]) and np.array_equal(pb[1], ref[2])
+
+
 def test_lba_resident_equals_batch(ctx):
     """orbx_lba_stage / _run / _fetch (problems resident in HBM, every run
     restarting from the staged state) against orbx_lba_solve_batch on the
