@@ -40,6 +40,17 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+# A context drives up to six HIP streams (the extraction parts, the match
+# stream, the upload stream) besides the null stream.  With HIP's default of
+# four hardware queues per process they share queues, and extraction kernels
+# queued behind an upload's completion marker wait for the copy: the
+# host-inclusive step (tools/host_leg.py, 1024 frames) runs upload + extract
+# in 9.97 ms at 4 queues and 5.78 ms at 8 (the copy alone 5.6 ms).  Set before
+# anything initialises HIP; rank processes inherit it.
+HW_QUEUES = 8
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) < HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+
 import orb_slam_amd as ox  # noqa: E402
 from orb_slam_amd import dist as odist, synth  # noqa: E402
 
@@ -1231,6 +1242,7 @@ def main():
             "dtype": "f64" if args.workload in ("c5", "pose") else "u8",
             "data": "synthetic (orb_slam_amd/synth.py / synth_ba.py / synth_pose.py, seeded per rank)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu, "check": check,
+            "hip_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
         }
         if world > 1:
             # what `value` is made of: every rank's units and timed seconds
