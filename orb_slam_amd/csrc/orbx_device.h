@@ -199,7 +199,8 @@ __device__ inline int block_sum(int v, BlockScratchN<kW>& s, int buf)
     return t;
 }
 
-__device__ inline int block_max(int v, BlockScratch& s, int buf)
+template <int kW>
+__device__ inline int block_max(int v, BlockScratchN<kW>& s, int buf)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     v = wave_max(v);
@@ -207,7 +208,7 @@ __device__ inline int block_max(int v, BlockScratch& s, int buf)
     __syncthreads();
     int t = s.wave[buf][0];
 #pragma unroll
-    for (int i = 1; i < kWaves; i++) t = max(t, s.wave[buf][i]);
+    for (int i = 1; i < kW; i++) t = max(t, s.wave[buf][i]);
     return t;
 }
 

@@ -172,9 +172,12 @@ __device__ inline void load_desc(const uint8_t* d, uint4& a, uint4& b)
 //     dist (9 bits) << 23 | grid cell (12 bits) << 11 | candidate slot.
 //     Keys order candidates by (distance, GetFeaturesInArea order), so the
 //     minimum key is the reference's first strict minimum.
+//     In the single-pair kernel a list of at most 64 keys is then sorted
+//     (each lane's rank).
 //  2. (wave 0, sequential in i1 order) the greedy replay: admissible keys
-//     (vMatchedDistance[i2] > dist) -> best key and second-best distance by
-//     wave reductions, then the accept / steal update in LDS.
+//     (vMatchedDistance[i2] > dist) -> best key and second-best distance:
+//     on a sorted list the first two admissible lanes of one ballot, else
+//     wave reductions; then the accept / steal update in LDS.
 //
 // Descriptors of the candidates are staged in LDS.  The rotation histogram
 // (with the reference's stale entries of stolen matches) is built with LDS
@@ -193,7 +196,7 @@ __device__ inline bool in_area_rec(const AreaQuery& q, const float4& rc, float q
 }
 
 #ifdef ORBX_MATCH_PROFILE
-__device__ unsigned long long g_match_prof[8];
+__device__ unsigned long long g_match_prof[12];   // 0-7 cycles, 8-10 replay counts
 __device__ inline unsigned long long match_stamp()
 {
     unsigned long long t;
@@ -201,6 +204,10 @@ __device__ inline unsigned long long match_stamp()
     return t;
 }
 #define MP_T0() unsigned long long _mt = match_stamp()
+#define MP_COUNT(k, v)                                                           \
+    do {                                                                         \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_match_prof[k] += (v);         \
+    } while (0)
 #define MP_MARK(k)                                                               \
     do {                                                                         \
         const unsigned long long _n = match_stamp();                             \
@@ -209,6 +216,7 @@ __device__ inline unsigned long long match_stamp()
     } while (0)
 #else
 #define MP_T0()
+#define MP_COUNT(k, v)
 #define MP_MARK(k)
 #endif
 // LDS of a SearchForInitialization block: its fixed tables (~40 KB at 1000
@@ -274,16 +282,29 @@ __device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap
     return s;
 }
 
+//
+// kT threads (a multiple of 64, >= kBlock): the batch kernel runs 256 per
+// pair; the single-pair call 1024, so the count and fill passes (one wave per
+// query) have 16 waves instead of 4.  Queries are staged in groups of kBlock
+// whatever kT is.
+template <int kT = kBlock>
 __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev& F2, const float* prev_xy,
                                              int window, float nnratio, bool check_ori, int32_t* out_m12,
-                                             int32_t* out_n, float* out_prev_xy, InitLDS s, BlockScratch& bs,
-                                             int32_t* error_flags)
+                                             int32_t* out_n, float* out_prev_xy, InitLDS s,
+                                             BlockScratchN<kT / 64>& bs, int32_t* error_flags)
 {
+    static_assert(kT % 64 == 0 && kT >= kBlock, "whole waves, at least one query group");
+    constexpr int kW = kT / 64;
+    // sorted candidate lists and the ballot replay for the single-pair
+    // kernel (latency: one pair on the chip); the batch kernel keeps the
+    // unsorted lists and the reduction replay (throughput: its extra fill
+    // work cost c2 1.2 % while matching overlaps extraction)
+    constexpr bool kSortLists = kT > kBlock;
     const int tid = threadIdx.x, lane = tid & 63;
     MP_T0();
     // F2 octave-0 keypoints in index order -> candidate slots
     int nc = 0;
-    for (int base = 0; base < F2.n; base += kBlock) {
+    for (int base = 0; base < F2.n; base += kT) {
         const int i2 = base + tid;
         orbx_keypoint k;
         bool ok = false;
@@ -292,7 +313,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
             ok = (k.octave == 0);
         }
         int tot;
-        const int pos = nc + block_exclusive_scan(ok ? 1 : 0, &tot, bs, (base / kBlock) & 1);
+        const int pos = nc + block_exclusive_scan(ok ? 1 : 0, &tot, bs, (base / kT) & 1);
         if (ok && pos < s.cap_c) {
             s.x[pos] = k.x;
             s.y[pos] = k.y;
@@ -320,7 +341,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     // queries are the F1 octave-0 keypoints: the groups below stop after the
     // last one (extractor output is level-major, so they are a prefix)
     int last0 = -1;
-    for (int i = tid; i < F1.n; i += kBlock) {
+    for (int i = tid; i < F1.n; i += kT) {
         const orbx_keypoint k1 = F1.kps[i];
         s.m12[i] = -1;
         s.pushed[i] = -1;
@@ -343,7 +364,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
             const int i1 = g0 + tid;
             int4 qa = make_int4(1, 0, 1, 0);
             float2 qp = make_float2(0.f, 0.f);
-            if (tid < gn) {
+            if (tid < gn) {   // gn <= kBlock
                 const orbx_keypoint k1 = F1.kps[i1];
                 if (k1.octave == 0) {
                     qp = make_float2(prev_xy ? prev_xy[2 * i1] : k1.x, prev_xy ? prev_xy[2 * i1 + 1] : k1.y);
@@ -352,13 +373,15 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
                     load_desc(F1.desc + (size_t)i1 * 32, s.qdesc[2 * tid], s.qdesc[2 * tid + 1]);
                 }
             }
-            s.qarea[tid] = qa;
-            s.qxy[tid] = qp;
+            if (tid < kBlock) {
+                s.qarea[tid] = qa;
+                s.qxy[tid] = qp;
+            }
         }
         __syncthreads();
         // count pass, one wave per query (lanes over the candidates): balanced
         // whatever the window population of individual queries
-        for (int t = wv; t < gn; t += kWaves) {
+        for (int t = wv; t < gn; t += kW) {
             const int4 qa = s.qarea[t];
             int cnt = 0;
             if (qa.x <= qa.y) {
@@ -376,16 +399,16 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
         if (g0 == 0) MP_MARK(5);
         int total;
         const int off = block_exclusive_scan(cnt, &total, bs, 0);
-        s.offs[tid] = off;
+        if (tid < kBlock) s.offs[tid] = off;
         if (tid == kBlock - 1) s.offs[kBlock] = total;
         __syncthreads();
         for (int lo = 0; lo < kBlock;) {
             // largest hi with offs[hi] - offs[lo] <= cap_keys (one list always fits: cnt <= nc <= cap)
             const int base_off = s.offs[lo];
-            const int fits = (tid >= lo && s.offs[tid + 1] - base_off <= s.cap_keys) ? 1 : 0;
+            const int fits = (tid >= lo && tid < kBlock && s.offs[tid + 1] - base_off <= s.cap_keys) ? 1 : 0;
             const int hi = lo + block_sum(fits, bs, 1);
             // fill pass, one wave per query: keys of the in-area candidates
-            for (int t = lo + wv; t < hi; t += kWaves) {
+            for (int t = lo + wv; t < hi; t += kW) {
                 const int n = s.offs[t + 1] - s.offs[t];
                 if (n == 0) continue;
                 const int4 qa = s.qarea[t];
@@ -407,16 +430,107 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
                     const unsigned long long bal = __ballot(ok);
                     if (ok) {
                         const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
-                        out[w + __popcll(bal & lt_mask)] =
-                            ((uint32_t)dist << 23) | ((uint32_t)__float_as_int(rc.w) << 11) | (uint32_t)j;
+                        const uint32_t key = ((uint32_t)dist << 23) | ((uint32_t)__float_as_int(rc.w) << 11) | (uint32_t)j;
+                        out[w + __popcll(bal & lt_mask)] = key;
                     }
                     w += __popcll(bal);
+                }
+                // a list that fits one wave is left in ascending key order
+                // (rank of each key among the list; keys are distinct)
+                if (kSortLists && w <= 64) {
+                    const uint32_t mine = lane < w ? out[lane] : 0xFFFFFFFFu;
+                    int rank = 0;
+                    for (int i = 0; i < w; i++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mine, i) < mine;
+                    if (lane < w) out[rank] = mine;
                 }
             }
             if (g0 == 0) MP_MARK(6);
             __syncthreads();
             MP_MARK(1);
-            if (tid < 64) {
+            if (kSortLists && tid < 64) {
+                // nnratio in a register for the whole replay (not re-read
+                // from the kernel arguments per accepted query)
+                float nr = nnratio;
+                asm volatile("" : "+v"(nr));
+                for (int w0 = lo; w0 < hi; w0 += 64) {
+                    // a window of up to 64 queries, one per lane: list offset
+                    // and length, read per query with readlane instead of
+                    // dependent LDS loads
+                    const int wn = min(64, hi - w0);
+                    const int tq = w0 + lane;
+                    const int q_b = lane < wn ? s.offs[tq] - base_off : 0;
+                    const int q_n = lane < wn ? s.offs[tq + 1] - s.offs[tq] : 0;
+                    // keys of query i+1 are loaded while i is decided: only the
+                    // mdist reads depend on the previous query's outcome
+                    int b = __builtin_amdgcn_readlane(q_b, 0), n = __builtin_amdgcn_readlane(q_n, 0);
+                    uint32_t kn = lane < n ? s.keys[b + lane] : 0xFFFFFFFFu;
+                    for (int i = 0; i < wn; i++) {
+                        const int t = w0 + i;
+                        const int bc = b, nc1 = n;
+                        const uint32_t k0 = kn;
+                        if (i + 1 < wn) {
+                            b = __builtin_amdgcn_readlane(q_b, i + 1);
+                            n = __builtin_amdgcn_readlane(q_n, i + 1);
+                            kn = lane < n ? s.keys[b + lane] : 0xFFFFFFFFu;
+                        }
+                        if (nc1 == 0) continue;   // vIndices2.empty(), or not an octave-0 query
+                        const int d0 = (int)(k0 >> 23);
+                        const bool adm0 = lane < nc1 && s.mdist[k0 & 0x7FF] > d0;   // vMatchedDistance[i2] > dist
+                        uint32_t m1;
+                        int m2;
+                        if (nc1 <= 64) {
+                            // the list is in key order: the best admissible
+                            // key is the first admissible lane, the second-best
+                            // distance the next one's
+                            const unsigned long long am = __ballot(adm0);
+                            if (am == 0) continue;
+                            const unsigned long long am2 = am & (am - 1);
+                            m1 = (uint32_t)__builtin_amdgcn_readlane((int)k0, __builtin_ctzll(am));
+                            m2 = am2 ? (int)((uint32_t)__builtin_amdgcn_readlane((int)k0, __builtin_ctzll(am2)) >> 23)
+                                     : 511;
+                        } else {
+                            // one pass over the admissible candidates, as the
+                            // reference's loop
+                            m1 = adm0 ? k0 : 0xFFFFFFFFu;
+                            m2 = 511;   // "none" (> any Hamming distance)
+                            for (int e = lane + 64; e < nc1; e += 64) {   // lists longer than a wave
+                                const uint32_t key = s.keys[bc + e];
+                                const int dist = (int)(key >> 23);
+                                if (s.mdist[key & 0x7FF] > dist) {
+                                    if (key < m1) {
+                                        m2 = min(m2, (int)(m1 >> 23));
+                                        m1 = key;
+                                    } else {
+                                        m2 = min(m2, dist);
+                                    }
+                                }
+                            }
+                            best_second_reduce(m1, m2);
+                        }
+                        if (m1 == 0xFFFFFFFFu) continue;
+                        const int bestDist = (int)(m1 >> 23);
+                        const int second = m2 >= 511 ? 0x7fffffff : m2;
+                        if (bestDist <= kTHLow && (float)bestDist < __fmul_rn((float)second, nr)) {
+                            // accept: the slot now belongs to ii1.  A steal needs no
+                            // read-modify-write here: m12 is rebuilt at the end from
+                            // "ii1 still owns the slot it took" (m21[slot] == ii1),
+                            // and the rotation bin from the slot ii1 took.
+                            if (lane == 0) {
+                                const int slot = (int)(m1 & 0x7FF);
+                                s.m12[g0 + t] = slot;
+                                s.m21[slot] = g0 + t;
+                                s.mdist[slot] = bestDist;
+                            }
+                            // LDS operations of one wave complete in order: the next
+                            // query's mdist reads see these writes; only keep the
+                            // compiler from moving memory operations across
+                            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                    }
+                }
+            }
+            if (!kSortLists && tid < 64) {
                 // keys of query t+1 are loaded while t is decided: only the
                 // mdist reads depend on the previous query's outcome
                 int oa = s.offs[lo], ob = s.offs[lo + 1];
@@ -481,20 +595,20 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     __syncthreads();
     // m12[i] held the slot i took; keep it only if i still owns that slot
     // (rotHist keeps the entries of stolen matches too: src/ORBmatcher.cc:675, 688-703)
-    for (int i = tid; i < F1.n; i += kBlock) {
+    for (int i = tid; i < F1.n; i += kT) {
         const int sl = s.m12[i];
         if (check_ori && sl >= 0) s.pushed[i] = (signed char)rot_bin(s.ang1[i], s.ang[sl]);
         s.m12[i] = (sl >= 0 && s.m21[sl] == i) ? s.idx[sl] : -1;
     }
     __syncthreads();
     if (check_ori) {
-        for (int i = tid; i < F1.n; i += kBlock)
+        for (int i = tid; i < F1.n; i += kT)
             if (s.pushed[i] >= 0) atomicAdd(&s.hist[s.pushed[i]], 1);
         __syncthreads();
         if (tid == 0) three_maxima(s.hist, s.hist[32], s.hist[33], s.hist[34]);
         __syncthreads();
         const int ind1 = s.hist[32], ind2 = s.hist[33], ind3 = s.hist[34];
-        for (int i = tid; i < F1.n; i += kBlock) {
+        for (int i = tid; i < F1.n; i += kT) {
             const int b = s.pushed[i];
             if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
             s.m12[i] = -1;
@@ -502,7 +616,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
         __syncthreads();
     }
     int nm = 0;
-    for (int i = tid; i < F1.n; i += kBlock) {
+    for (int i = tid; i < F1.n; i += kT) {
         const int m = s.m12[i];
         out_m12[i] = m;
         nm += m >= 0;

@@ -451,13 +451,17 @@ __global__ __launch_bounds__(64) void k_proj_local_jobs(const SearchArgs* jobs)
     proj_local_wave(a, smem);
 }
 
-// SearchForInitialization with host inputs (prev_xy in/out).
-__global__ __launch_bounds__(256) void k_search_init_one(SearchArgs a, int cap_c, int cap_keys, int32_t* error_flags)
+// SearchForInitialization with host inputs (prev_xy in/out): one pair, one
+// workgroup of kInitOneThreads (the replay is one wave; the parallel passes
+// around it use all 16).
+constexpr int kInitOneThreads = 1024;
+__global__ __launch_bounds__(kInitOneThreads) void k_search_init_one(SearchArgs a, int cap_c, int cap_keys,
+                                                                      int32_t* error_flags)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ BlockScratch bs;
+    __shared__ BlockScratchN<kInitOneThreads / 64> bs;
     const InitLDS L = carve_init(smem, cap_c, max(a.F1.n, 1), cap_keys);
-    search_for_init_block(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n, a.prev_out,
+    search_for_init_block<kInitOneThreads>(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n, a.prev_out,
                           L, bs, error_flags);
 }
 
@@ -651,7 +655,7 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     a.check_ori = check_ori;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(256), lds, ctx->stream, a, cap_c, cap_keys, ctx->error_flags);
+    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(kInitOneThreads), lds, ctx->stream, a, cap_c, cap_keys, ctx->error_flags);
     ORBX_HIP_CHECK(hipGetLastError());
     if ((r = pin.download(opo, u.total)) != ORBX_OK) return r;
     pin.get(matches12, oo, (size_t)F1->n * 4);
@@ -1035,3 +1039,16 @@ int orbx_match_bf(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8_t* dB, i
 }
 
 }  // extern "C"
+
+#ifdef ORBX_MATCH_PROFILE
+// this file's copy of the stamp sums (k_search_init_one's block 0, wave 0)
+extern "C" int orbx_debug_search_prof(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_match_prof), sizeof(unsigned long long) * 12) != hipSuccess) return -2;
+    if (reset) {
+        const unsigned long long z[12] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_match_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
