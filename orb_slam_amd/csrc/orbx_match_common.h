@@ -283,15 +283,72 @@ __device__ inline InitLDS carve_init(uint8_t* base, int cap_c, int cap1, int cap
 }
 
 //
+// One query's candidate count and keys (one wave, lanes over the nc
+// candidate records): the count pass and the fill pass of the routine
+// below, shared with k_sfi_lists.
+__device__ inline AreaQuery area_of(const int4 qa)
+{
+    AreaQuery q;
+    q.min_cx = qa.x; q.max_cx = qa.y; q.min_cy = qa.z; q.max_cy = qa.w; q.empty = false;
+    return q;
+}
+
+__device__ inline int sfi_query_count(const InitLDS& s, int nc, int4 qa, float2 qp, float r, int lane)
+{
+    if (qa.x > qa.y) return 0;
+    const AreaQuery q = area_of(qa);
+    int cnt = 0;
+    for (int j = lane; j < nc; j += 64) cnt += in_area_rec(q, s.rec[j], qp.x, qp.y, r);
+    return wave_sum(cnt);
+}
+
+// keys of the in-area candidates, compacted in candidate order into out[]
+__device__ inline void sfi_query_fill(const InitLDS& s, int nc, int4 qa, float2 qp, uint4 d1a, uint4 d1b, float r,
+                                      uint32_t* out, int lane)
+{
+    const AreaQuery q = area_of(qa);
+    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int w = 0;
+    for (int j0 = 0; j0 < nc; j0 += 64) {
+        const int j = j0 + lane;
+        bool ok = false;
+        float4 rc;
+        if (j < nc) {
+            rc = s.rec[j];
+            ok = in_area_rec(q, rc, qp.x, qp.y, r);
+        }
+        const unsigned long long bal = __ballot(ok);
+        if (ok) {
+            const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
+            out[w + __popcll(bal & lt_mask)] = ((uint32_t)dist << 23) | ((uint32_t)__float_as_int(rc.w) << 11) | (uint32_t)j;
+        }
+        w += __popcll(bal);
+    }
+}
+
+// a list of w <= 64 distinct keys into ascending order (each lane's rank),
+// from src to dst (may be the same array)
+__device__ inline void sfi_sort_short(const uint32_t* src, uint32_t* dst, int w, int lane)
+{
+    const uint32_t mine = lane < w ? src[lane] : 0xFFFFFFFFu;
+    int rank = 0;
+    for (int i = 0; i < w; i++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mine, i) < mine;
+    if (lane < w) dst[rank] = mine;
+}
+
 // kT threads (a multiple of 64, >= kBlock): the batch kernel runs 256 per
 // pair; the single-pair call 1024, so the count and fill passes (one wave per
 // query) have 16 waves instead of 4.  Queries are staged in groups of kBlock
 // whatever kT is.
-template <int kT = kBlock>
+// kPre: the candidate lists were built by k_sfi_lists (pre_cnt[i1] keys at
+// pre_keys + i1 * cap_c, sorted when <= 64): the count and fill passes
+// become a copy into LDS.
+template <int kT = kBlock, bool kPre = false>
 __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev& F2, const float* prev_xy,
                                              int window, float nnratio, bool check_ori, int32_t* out_m12,
                                              int32_t* out_n, float* out_prev_xy, InitLDS s,
-                                             BlockScratchN<kT / 64>& bs, int32_t* error_flags)
+                                             BlockScratchN<kT / 64>& bs, int32_t* error_flags,
+                                             const uint32_t* pre_keys = nullptr, const int32_t* pre_cnt = nullptr)
 {
     static_assert(kT % 64 == 0 && kT >= kBlock, "whole waves, at least one query group");
     constexpr int kW = kT / 64;
@@ -355,12 +412,11 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
     MP_MARK(0);
     const float r = (float)window;
     const int wv = tid >> 6;
-    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int g0 = 0; g0 < n1q; g0 += kBlock) {
         const int gn = min(kBlock, n1q - g0);
         // stage the group's queries (one thread each): position, cell range,
         // descriptor; inactive (octave > 0 or empty area) get an empty range
-        {
+        if (!kPre) {
             const int i1 = g0 + tid;
             int4 qa = make_int4(1, 0, 1, 0);
             float2 qp = make_float2(0.f, 0.f);
@@ -382,15 +438,7 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
         // count pass, one wave per query (lanes over the candidates): balanced
         // whatever the window population of individual queries
         for (int t = wv; t < gn; t += kW) {
-            const int4 qa = s.qarea[t];
-            int cnt = 0;
-            if (qa.x <= qa.y) {
-                const float2 qp = s.qxy[t];
-                AreaQuery q;
-                q.min_cx = qa.x; q.max_cx = qa.y; q.min_cy = qa.z; q.max_cy = qa.w; q.empty = false;
-                for (int j = lane; j < nc; j += 64) cnt += in_area_rec(q, s.rec[j], qp.x, qp.y, r);
-                cnt = wave_sum(cnt);
-            }
+            const int cnt = kPre ? pre_cnt[g0 + t] : sfi_query_count(s, nc, s.qarea[t], s.qxy[t], r, lane);
             if (lane == 0) s.offs[t] = cnt;
         }
         if (g0 == 0) MP_MARK(4);
@@ -408,41 +456,28 @@ __device__ inline void search_for_init_block(const FrameDev& F1, const FrameDev&
             const int fits = (tid >= lo && tid < kBlock && s.offs[tid + 1] - base_off <= s.cap_keys) ? 1 : 0;
             const int hi = lo + block_sum(fits, bs, 1);
             // fill pass, one wave per query: keys of the in-area candidates
-            for (int t = lo + wv; t < hi; t += kW) {
+            if (kPre) {
+                // flat copy of the chunk's keys: key e belongs to the last
+                // query t with offs[t] - base_off <= e
+                const int tot = s.offs[hi] - base_off;
+                for (int e = tid; e < tot; e += kT) {
+                    int qa = lo, qb = hi - 1;
+                    while (qa < qb) {
+                        const int m = (qa + qb + 1) >> 1;
+                        if (s.offs[m] - base_off <= e) qa = m;
+                        else qb = m - 1;
+                    }
+                    s.keys[e] = pre_keys[(size_t)(g0 + qa) * s.cap_c + (e - (s.offs[qa] - base_off))];
+                }
+            }
+            for (int t = lo + wv; !kPre && t < hi; t += kW) {
                 const int n = s.offs[t + 1] - s.offs[t];
                 if (n == 0) continue;
-                const int4 qa = s.qarea[t];
-                const float2 qp = s.qxy[t];
-                const float qx = qp.x, qy = qp.y;
-                AreaQuery q;
-                q.min_cx = qa.x; q.max_cx = qa.y; q.min_cy = qa.z; q.max_cy = qa.w; q.empty = false;
-                const uint4 d1a = s.qdesc[2 * t], d1b = s.qdesc[2 * t + 1];
                 uint32_t* out = s.keys + (s.offs[t] - base_off);
-                int w = 0;
-                for (int j0 = 0; j0 < nc; j0 += 64) {
-                    const int j = j0 + lane;
-                    bool ok = false;
-                    float4 rc;
-                    if (j < nc) {
-                        rc = s.rec[j];
-                        ok = in_area_rec(q, rc, qx, qy, r);
-                    }
-                    const unsigned long long bal = __ballot(ok);
-                    if (ok) {
-                        const int dist = hamming256(d1a, d1b, s.desc[2 * j], s.desc[2 * j + 1]);
-                        const uint32_t key = ((uint32_t)dist << 23) | ((uint32_t)__float_as_int(rc.w) << 11) | (uint32_t)j;
-                        out[w + __popcll(bal & lt_mask)] = key;
-                    }
-                    w += __popcll(bal);
-                }
+                sfi_query_fill(s, nc, s.qarea[t], s.qxy[t], s.qdesc[2 * t], s.qdesc[2 * t + 1], r, out, lane);
                 // a list that fits one wave is left in ascending key order
                 // (rank of each key among the list; keys are distinct)
-                if (kSortLists && w <= 64) {
-                    const uint32_t mine = lane < w ? out[lane] : 0xFFFFFFFFu;
-                    int rank = 0;
-                    for (int i = 0; i < w; i++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mine, i) < mine;
-                    if (lane < w) out[rank] = mine;
-                }
+                if (kSortLists && n <= 64) sfi_sort_short(out, out, n, lane);
             }
             if (g0 == 0) MP_MARK(6);
             __syncthreads();

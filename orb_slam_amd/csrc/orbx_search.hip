@@ -451,18 +451,92 @@ __global__ __launch_bounds__(64) void k_proj_local_jobs(const SearchArgs* jobs)
     proj_local_wave(a, smem);
 }
 
-// SearchForInitialization with host inputs (prev_xy in/out): one pair, one
-// workgroup of kInitOneThreads (the replay is one wave; the parallel passes
-// around it use all 16).
+// SearchForInitialization with host inputs (prev_xy in/out), one pair, in
+// two launches: k_sfi_lists builds every query's candidate list across the
+// chip (one wave per F1 octave-0 keypoint, 16 per workgroup), then one
+// workgroup of kInitOneThreads copies them into LDS and replays the greedy
+// assignment (one wave; the rest stage and finish).
 constexpr int kInitOneThreads = 1024;
+constexpr int kListWaves = 16;
+
+// LDS of k_sfi_lists: candidate records and descriptors (cap_c each) and a
+// 64-key sort buffer per wave
+__host__ __device__ inline size_t sfi_lists_lds(int cap_c) { return (size_t)cap_c * 48 + kListWaves * 64 * 4; }
+
+__global__ __launch_bounds__(kListWaves * 64) void k_sfi_lists(SearchArgs a, int cap_c, int n1q, uint32_t* keys,
+                                                               int32_t* cnt)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ BlockScratchN<kListWaves> bs;
+    InitLDS s{};
+    s.desc = reinterpret_cast<uint4*>(smem);
+    s.rec = reinterpret_cast<float4*>(s.desc + 2 * cap_c);
+    uint32_t* sortbuf = reinterpret_cast<uint32_t*>(s.rec + cap_c);
+    s.cap_c = cap_c;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const FrameDev& F2 = a.F2;
+    // F2 octave-0 keypoints in index order -> candidate slots (as
+    // search_for_init_block stages them)
+    int nc = 0;
+    for (int base = 0; base < F2.n; base += kListWaves * 64) {
+        const int i2 = base + tid;
+        orbx_keypoint k;
+        bool ok = false;
+        if (i2 < F2.n) {
+            k = F2.kps[i2];
+            ok = (k.octave == 0);
+        }
+        int tot;
+        const int pos = nc + block_exclusive_scan(ok ? 1 : 0, &tot, bs, (base / (kListWaves * 64)) & 1);
+        if (ok && pos < cap_c) {
+            const int cell = grid_cell(F2, k.x, k.y);
+            s.rec[pos] = make_float4(k.x, k.y, __int_as_float(cell < 0 ? -1 : ((cell / kGridRows) | ((cell % kGridRows) << 8))),
+                                     __int_as_float(cell));
+            const uint4* d = reinterpret_cast<const uint4*>(F2.desc + (size_t)i2 * 32);
+            s.desc[2 * pos] = d[0];
+            s.desc[2 * pos + 1] = d[1];
+        }
+        nc += tot;
+    }
+    __syncthreads();
+    nc = min(nc, cap_c);   // the replay kernel reports an overflow
+    const int i1 = blockIdx.x * kListWaves + wv;
+    if (i1 >= n1q) return;   // whole waves; no barrier below
+    const orbx_keypoint k1 = a.F1.kps[i1];
+    int n = 0;
+    int4 qa = make_int4(1, 0, 1, 0);
+    float2 qp = make_float2(0.f, 0.f);
+    const float r = (float)a.window;
+    if (k1.octave == 0) {
+        qp = make_float2(a.prev_xy[2 * i1], a.prev_xy[2 * i1 + 1]);
+        const AreaQuery q = area_cells(F2, qp.x, qp.y, r);
+        if (!q.empty) qa = make_int4(q.min_cx, q.max_cx, q.min_cy, q.max_cy);
+        n = sfi_query_count(s, nc, qa, qp, r, lane);
+    }
+    if (n > 0) {
+        uint4 d1a, d1b;
+        load_desc(a.F1.desc + (size_t)i1 * 32, d1a, d1b);
+        uint32_t* out = keys + (size_t)i1 * cap_c;
+        if (n <= 64) {   // sorted through this wave's LDS buffer
+            uint32_t* sb = sortbuf + 64 * wv;
+            sfi_query_fill(s, nc, qa, qp, d1a, d1b, r, sb, lane);
+            sfi_sort_short(sb, out, n, lane);
+        } else {
+            sfi_query_fill(s, nc, qa, qp, d1a, d1b, r, out, lane);
+        }
+    }
+    if (lane == 0) cnt[i1] = n;
+}
+
 __global__ __launch_bounds__(kInitOneThreads) void k_search_init_one(SearchArgs a, int cap_c, int cap_keys,
-                                                                      int32_t* error_flags)
+                                                                      int32_t* error_flags, const uint32_t* keys,
+                                                                      const int32_t* cnt)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ BlockScratchN<kInitOneThreads / 64> bs;
     const InitLDS L = carve_init(smem, cap_c, max(a.F1.n, 1), cap_keys);
-    search_for_init_block<kInitOneThreads>(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0, a.out, a.out_n, a.prev_out,
-                          L, bs, error_flags);
+    search_for_init_block<kInitOneThreads, true>(a.F1, a.F2, a.prev_xy, a.window, a.nnratio, a.check_ori != 0,
+                                                 a.out, a.out_n, a.prev_out, L, bs, error_flags, keys, cnt);
 }
 
 // ---------------------------------------------------------------------------
@@ -626,11 +700,17 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t op = u.reserve((size_t)F1->n * 8);
     const size_t opo = u.reserve((size_t)F1->n * 8), oo = u.reserve((size_t)F1->n * 4 + 4), on = u.reserve(4);
-    // candidate slots = F2 keypoints of octave 0
-    int cap_c = 0;
+    // candidate slots = F2 keypoints of octave 0; queries = F1's up to its
+    // last octave-0 keypoint
+    int cap_c = 0, n1q = 0;
     for (int i = 0; i < F2->n; i++) cap_c += F2->keys_un[i].octave == 0;
+    for (int i = 0; i < F1->n; i++)
+        if (F1->keys_un[i].octave == 0) n1q = i + 1;
     cap_c = std::max(cap_c, 1);
     if (cap_c > kInitMaxCand) return ORBX_ERR_UNSUPPORTED;
+    // k_sfi_lists' output (device only, after the read-back range)
+    const size_t out_end = on + 4;
+    const size_t okeys = u.reserve((size_t)std::max(n1q, 1) * cap_c * 4), ocnt = u.reserve((size_t)std::max(n1q, 1) * 4);
     const int cap1 = std::max(F1->n, 1);
     const size_t fixed = init_lds_bytes(cap_c, cap1, 0);
     const int cap_keys = std::max<int>(cap_c, (int)((kInitLdsBudget - std::min(fixed, kInitLdsBudget)) / 4));
@@ -638,7 +718,7 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     if (lds > 160 * 1024) return ORBX_ERR_UNSUPPORTED;
     int r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
-    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r == ORBX_OK) r = pin.open(out_end);
     if (r != ORBX_OK) return r;
     put_frame(pin, o1, F1);
     put_frame(pin, o2, F2);
@@ -655,9 +735,15 @@ int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, con
     a.check_ori = check_ori;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(kInitOneThreads), lds, ctx->stream, a, cap_c, cap_keys, ctx->error_flags);
+    uint32_t* dkeys = reinterpret_cast<uint32_t*>(u.base() + okeys);
+    int32_t* dcnt = reinterpret_cast<int32_t*>(u.base() + ocnt);
+    if (n1q > 0)
+        hipLaunchKernelGGL(k_sfi_lists, dim3((n1q + kListWaves - 1) / kListWaves), dim3(kListWaves * 64),
+                           sfi_lists_lds(cap_c), ctx->stream, a, cap_c, n1q, dkeys, dcnt);
+    hipLaunchKernelGGL(k_search_init_one, dim3(1), dim3(kInitOneThreads), lds, ctx->stream, a, cap_c, cap_keys,
+                       ctx->error_flags, dkeys, dcnt);
     ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = pin.download(opo, u.total)) != ORBX_OK) return r;
+    if ((r = pin.download(opo, out_end)) != ORBX_OK) return r;
     pin.get(matches12, oo, (size_t)F1->n * 4);
     pin.get(n_matches, on, 4);
     pin.get(prev_matched, opo, (size_t)F1->n * 8);

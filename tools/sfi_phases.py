@@ -30,7 +30,9 @@ def main():
     feats = [rex(np.ascontiguousarray(f)) for f in frames]
     views = [ox.frame_view(k, d, w, h) for k, d in feats]
     L = ox.lib()
-    L.orbx_debug_search_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    prof_fn = getattr(L, "orbx_debug_search_prof", None)   # absent from the product build: timing only
+    if prof_fn is not None:
+        prof_fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=1)
     m12 = np.zeros(nf, np.int32)
     pm = np.zeros((nf, 2), np.float32)
@@ -41,16 +43,20 @@ def main():
         i = c % 7
         k = feats[i][0]
         pm[:len(k)] = np.stack([k["x"], k["y"]], 1)
-        if c == 20:
-            L.orbx_debug_search_prof(prof.ctypes.data, 1)
+        if c == 20 and prof_fn is not None:
+            prof_fn(prof.ctypes.data, 1)
         t0 = time.perf_counter()
         r = L.orbx_search_for_initialization(ctx.handle, ctypes.byref(views[i]), ctypes.byref(views[i + 1]),
                                              pm.ctypes.data, m12.ctypes.data, 100, 0.9, 1, ctypes.byref(nm))
         ts.append(time.perf_counter() - t0)
         assert r == 0, r
-    L.orbx_debug_search_prof(prof.ctypes.data, 0)
+    print(f"median call {1e3 * np.median(ts[20:]):.3f} ms ({ox.LIB_PATH})")
+    if prof_fn is None:
+        ctx.close()
+        return
+    prof_fn(prof.ctypes.data, 0)
     tot = int(prof[:8].sum())
-    print(f"median call {1e3 * np.median(ts[20:]):.3f} ms; per call:")
+    print("per call:")
     for k in (0, 4, 5, 6, 1, 7, 2, 3):
         v = int(prof[k]) / calls
         print(f"  {NAMES[k]:28s} {v:10.0f} cycles ({100 * int(prof[k]) / max(tot, 1):5.1f} %)")
