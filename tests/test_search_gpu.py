@@ -71,6 +71,47 @@ def test_search_for_initialization(ctx, frames_feats, check_ori, window):
     assert np.array_equal(pg, pr)
 
 
+def _sfi_both(ctx, k1, d1, k2, d2, prev0, window, ratio, ori):
+    F1, F2 = views(k1, d1, k2, d2)
+    L = load()
+    pr, pg = prev0.copy(), prev0.copy()
+    mr, mg = np.zeros(len(k1), np.int32), np.zeros(len(k1), np.int32)
+    nr, ng = ctypes.c_int(), ctypes.c_int()
+    assert L.orbx_ref_search_for_initialization(ctypes.byref(F1), ctypes.byref(F2), ptr(pr), ptr(mr), window, ratio,
+                                                int(ori), ctypes.byref(nr)) == 0
+    assert ox.lib().orbx_search_for_initialization(ctx.handle, ctypes.byref(F1), ctypes.byref(F2), ox._ptr(pg),
+                                                   ox._ptr(mg), window, ratio, int(ori), ctypes.byref(ng)) == 0
+    assert ng.value == nr.value
+    assert np.array_equal(mg, mr)
+    assert np.array_equal(pg, pr)
+    return nr.value
+
+
+# the single-pair path (k_sfi_lists + k_search_init_one): lists longer than a
+# wave (window 400: unsorted, reduction replay), short windows, ratios, moved
+# search centres, and pairs without queries or without candidates
+@pytest.mark.parametrize("pair,window,ratio,ori,jitter", [((0, 2), 400, 0.9, True, 0), ((1, 2), 20, 0.6, False, 0),
+                                                          ((0, 1), 100, 1.0, True, 15), ((2, 0), 250, 0.8, True, 40),
+                                                          ((1, 0), 0, 0.9, False, 0)])
+def test_search_for_initialization_cases(ctx, frames_feats, pair, window, ratio, ori, jitter):
+    (k1, d1), (k2, d2) = frames_feats[pair[0]], frames_feats[pair[1]]
+    rng = np.random.default_rng(window + jitter)
+    prev0 = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    prev0 += rng.uniform(-jitter, jitter, prev0.shape).astype(np.float32)
+    n = _sfi_both(ctx, k1, d1, k2, d2, prev0, window, ratio, ori)
+    if window >= 100:
+        assert n > 0
+
+
+@pytest.mark.parametrize("which", ["no_queries", "no_candidates"])
+def test_search_for_initialization_empty(ctx, frames_feats, which):
+    (k1, d1), (k2, d2) = frames_feats[0], frames_feats[1]
+    k1, k2 = k1.copy(), k2.copy()
+    (k1 if which == "no_queries" else k2)["octave"] = np.maximum((k1 if which == "no_queries" else k2)["octave"], 1)
+    prev0 = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    assert _sfi_both(ctx, k1, d1, k2, d2, prev0, 100, 0.9, True) == 0
+
+
 @pytest.mark.parametrize("window,minl,maxl,ratio,ori", [(100, 0, -1, 0.9, True), (200, 1, 5, 0.7, False),
                                                          (30, 0, 2, 1.0, True)])
 def test_window_search(ctx, frames_feats, window, minl, maxl, ratio, ori):
