@@ -444,15 +444,89 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
 #ifndef ORBX_CASCADE_SINGLE_THREADS
 #define ORBX_CASCADE_SINGLE_THREADS 1024
 #endif
-template <int T>
-__global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* plan, int buf_x)
+#ifdef ORBX_CASC_PROFILE
+// diagnostic: band 0's cycles per (level, phase): 0 resize or level-0 load,
+// 1 first barrier, 2 border pass + second barrier, 3 pyramid stores
+__device__ unsigned long long g_casc_prof[kMaxLevels][4];
+#define CASC_T0() unsigned long long _ct = __builtin_readcyclecounter()
+#define CASC_MARK(l, k)                                                          \
+    do {                                                                         \
+        const unsigned long long _n = __builtin_readcyclecounter();              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_casc_prof[l][k] += _n - _ct;  \
+        _ct = _n;                                                                \
+    } while (0)
+extern "C" int orbx_debug_casc_prof(unsigned long long* out)
 {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_casc_prof), sizeof(g_casc_prof)) == hipSuccess ? 0 : -2;
+}
+#else
+#define CASC_T0()
+#define CASC_MARK(l, k)
+#endif
+// kTab (the single-frame instance): every level's column table and the
+// band's row-table slices are staged in LDS at tab_off (tab_cols entries,
+// then the rows) with the level-0 loads, so no level's row loop waits on a
+// global table load per row (band 0's stamps: 4-5 dependent ~2 k-cycle
+// loads per group at levels 1-3 before).
+template <int T>
+__global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* plan, int buf_x, int tab_off,
+                                                   int tab_cols)
+{
+    CASC_T0();
+    const bool kTab = T >= 1024 && tab_off > 0;   // tab_off 0: tables too large for LDS, read from HBM
     extern __shared__ uint4 s_dyn[];
     uint8_t* const lds = reinterpret_cast<uint8_t*>(s_dyn);   // buffers: [0, buf_x) even levels, then odd
     const int band = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
     uint8_t* pyr = a.pyr_raw + (size_t)f * a.frame_pyr_bytes;
     const uint8_t* img = a.frames + (size_t)(a.first_slot + f) * a.w * a.h;
+    ResizeCol* const t_cols = reinterpret_cast<ResizeCol*>(lds + tab_off);
+    ResizeRow* const t_rows = reinterpret_cast<ResizeRow*>(t_cols + tab_cols);
+    if (kTab) {
+        // flat index over the levels' column tables, then the band's row
+        // slices; four loads in flight per thread before the stores
+        int ncol = 0, nrow = 0;
+        for (int l = 1; l < a.nlevels; l++) {
+            const int4 pl = plan[band * a.nlevels + l];
+            ncol += cget(a.levels, l).w;
+            nrow += max(0, pl.w - pl.z + 1);
+        }
+        const int n = ncol + nrow;
+        for (int u0 = 0; u0 < n; u0 += 4 * T) {
+            uint2 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                int e = u0 + k * T + tid;
+                v[k] = make_uint2(0, 0);
+                if (e >= n) continue;
+                if (e < ncol) {
+                    int l = 1, w;
+                    while (e >= (w = cget(a.levels, l).w)) {
+                        e -= w;
+                        l++;
+                    }
+                    v[k] = *reinterpret_cast<const uint2*>(a.res_cols + cget(a.levels, l).res_col_off + e);
+                } else {
+                    e -= ncol;
+                    int l = 1, m;
+                    int4 pl = plan[band * a.nlevels + 1];
+                    while (e >= (m = max(0, pl.w - pl.z + 1))) {
+                        e -= m;
+                        l++;
+                        pl = plan[band * a.nlevels + l];
+                    }
+                    v[k] = *reinterpret_cast<const uint2*>(a.res_rows + cget(a.levels, l).res_row_off + pl.z + e);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int e = u0 + k * T + tid;
+                if (e < ncol) reinterpret_cast<uint2*>(t_cols)[e] = v[k];
+                else if (e < n) reinterpret_cast<uint2*>(t_rows)[e - ncol] = v[k];
+            }
+        }
+    }
     int sc0 = 0, sstride = 0;   // the previous level's first computed ROI row and row pitch
+    int tcol = 0, trow = 0;     // this level's offsets in the staged tables (kTab)
     for (int l = 0; l < a.nlevels; l++) {
         const int4 pl = plan[band * a.nlevels + l];
         const LevelGeom L = cget(a.levels, l);
@@ -489,7 +563,7 @@ __global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* pl
 #pragma unroll
                 for (int b = 0; b < 4; b++) {
                     const bool on = px0 + b < L.w;
-                    const ResizeCol c = a.res_cols[L.res_col_off + (on ? px0 + b : 0)];
+                    const ResizeCol c = kTab ? t_cols[tcol + (on ? px0 + b : 0)] : a.res_cols[L.res_col_off + (on ? px0 + b : 0)];
                     ca[b] = kEdge + c.sx0;
                     a0[b] = on ? c.a0 : 0;
                     a1[b] = on ? c.a1 : 0;
@@ -503,7 +577,7 @@ __global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* pl
                 };
                 int H0[4], H1[4], cs0 = -1, cs1 = -1;
                 for (int r = r_lo; r < r_hi; r++) {
-                    const ResizeRow rw = a.res_rows[L.res_row_off + c0 + r];
+                    const ResizeRow rw = kTab ? t_rows[trow + r] : a.res_rows[L.res_row_off + c0 + r];
                     const int sy0 = rw.sy0, sy1 = rw.sy1, b0 = rw.b0, b1 = rw.b1;
                     int A[4], B[4];
                     if (sy0 == cs1) {
@@ -556,7 +630,9 @@ __global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* pl
                 }
             }
         }
+        CASC_MARK(l, 0);
         __syncthreads();
+        CASC_MARK(l, 1);
         // 2. border columns (REFLECT_101 of the row's own pixels) and the zero
         //    tail past the padded width, per computed row
         const int tail = stride - L.pw;
@@ -571,6 +647,7 @@ __global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* pl
             }
         }
         __syncthreads();
+        CASC_MARK(l, 2);
         // 3. the band's rows to the pyramid, 16-byte stores: its owned ROI
         //    rows, then the border rows whose reflection it owns
         {
@@ -589,6 +666,11 @@ __global__ __launch_bounds__(T) void k_pyr_cascade(ExtractArgs a, const int4* pl
                     *reinterpret_cast<uint4*>(out + (size_t)py * stride + 16 * q) =
                         *reinterpret_cast<const uint4*>(dst + (r - c0) * stride + 16 * q);
             }
+        }
+        CASC_MARK(l, 3);
+        if (l > 0) {
+            tcol += L.w;
+            trow += max(0, nrows);
         }
         // the next level reads dst's ROI bytes (final since the first barrier)
         // and writes the other buffer, which nobody reads any more
@@ -1974,13 +2056,20 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         if ((ctx->pyr_mode == 2 || (ctx->single_frame && ctx->pyr_mode == 0)) && g.cascade_bands > 0) {
             timer_begin(ctx, "resize", st);
             for (int rep = 0; rep < kDiagRepeat[0]; rep++) {
-                if (ctx->single_frame)
+                if (ctx->single_frame) {
+                    int tab_off = (g.cascade_lds + 15) & ~15;
+                    size_t lds = (size_t)tab_off + 8 * (size_t)(g.cascade_tab_cols + g.cascade_tab_rows);
+                    if (lds > 160 * 1024) {   // very wide frames: the tables stay in HBM
+                        tab_off = 0;
+                        lds = g.cascade_lds;
+                    }
                     hipLaunchKernelGGL(k_pyr_cascade<ORBX_CASCADE_SINGLE_THREADS>, dim3(g.cascade_bands, nb),
-                                       dim3(ORBX_CASCADE_SINGLE_THREADS), g.cascade_lds, st, x, ctx->cascade,
-                                       g.cascade_buf_x);
-                else
+                                       dim3(ORBX_CASCADE_SINGLE_THREADS), lds, st, x, ctx->cascade, g.cascade_buf_x,
+                                       tab_off, g.cascade_tab_cols);
+                } else {
                     hipLaunchKernelGGL(k_pyr_cascade<256>, dim3(g.cascade_bands, nb), dim3(256), g.cascade_lds, st, x,
-                                       ctx->cascade, g.cascade_buf_x);
+                                       ctx->cascade, g.cascade_buf_x, 0, 0);
+                }
             }
             timer_end(ctx, "resize", st);
             return;

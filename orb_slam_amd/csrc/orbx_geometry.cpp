@@ -302,6 +302,7 @@ void plan_cascade(Geometry& g, int lds_target)
 {
     g.cascade.clear();
     g.cascade_bands = g.cascade_buf_x = g.cascade_lds = 0;
+    g.cascade_tab_cols = g.cascade_tab_rows = 0;
     const int nl = g.nlevels;
     if (g.w % 16 != 0 || nl < 1) return;
     std::vector<int4> tab;
@@ -343,6 +344,12 @@ void plan_cascade(Geometry& g, int lds_target)
             g.cascade_bands = B;
             g.cascade_buf_x = bx;
             g.cascade_lds = bx + by;
+            for (int l = 1; l < nl; l++) g.cascade_tab_cols += g.levels[l].w;
+            for (int j = 0; j < B; j++) {
+                int rows = 0;
+                for (int l = 1; l < nl; l++) rows += std::max(0, tab[(size_t)j * nl + l].w - tab[(size_t)j * nl + l].z + 1);
+                g.cascade_tab_rows = std::max(g.cascade_tab_rows, rows);
+            }
             return;
         }
     }

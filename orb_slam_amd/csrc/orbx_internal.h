@@ -146,6 +146,10 @@ struct Geometry {
     // the geometry does not take it (the staged launches run instead)
     std::vector<int4> cascade;
     int cascade_bands = 0, cascade_buf_x = 0, cascade_lds = 0;
+    // the single-frame cascade (1024 threads) stages every level's resize
+    // column table and its band's row-table slices in LDS after the buffers:
+    // cascade_tab_cols entries, then cascade_tab_rows (the most any band needs)
+    int cascade_tab_cols = 0, cascade_tab_rows = 0;
 };
 
 // ORBextractor constructor tables (src/ORBextractor.cc:457-511).
