@@ -659,10 +659,11 @@ int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
             cr = ORBX_ERR_HIP;
         ctx->frames_src = ctx->launch_mode == 2 ? static_cast<const uint8_t*>(ctx->one_in) : nullptr;
         ctx->single_frame = true;
+        ctx->single_out = out_host;   // k_describe writes the read-back block (no pack launch)
         if (cr == ORBX_OK) cr = launch_extract(ctx, 0, 1);
         ctx->frames_src = nullptr;
         ctx->single_frame = false;
-        if (cr == ORBX_OK) cr = launch_pack_single(ctx, out_host, ctx->stream);
+        ctx->single_out = nullptr;
         return cr;
     };
     if (ctx->launch_mode != 3 && (!ctx->one_exec || ctx->one_key != key)) {

@@ -77,6 +77,10 @@ struct ExtractArgs {
     uint8_t* out_desc;
     int32_t* out_n;
     int32_t* error_flags;
+    // orbx_extract's single frame: k_describe also writes the page-locked
+    // read-back block (count and flags at 0, records at 64, descriptors
+    // after nfeatures records), in place of a pack launch; else null
+    uint8_t* host_out;
     int32_t* retain_scratch;        // slots x (list_entries + 4 ncells): global nth_element scratch
     const int4* blur_tiles;         // k_blur work blocks (also the blur tail of k_fast_cells<..., true>)
     uint64_t* cell_keys64;          // HARRIS_SCORE: Harris-keyed cell lists (as cell_lists)
@@ -1792,7 +1796,13 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
         }
         total += c;
     }
-    if (k == 0 && lane == 0) a.out_n[a.first_slot + f] = total;
+    if (k == 0 && lane == 0) {
+        a.out_n[a.first_slot + f] = total;
+        if (a.host_out) {   // every earlier kernel's error flags are final here
+            reinterpret_cast<int32_t*>(a.host_out)[0] = total;
+            reinterpret_cast<int32_t*>(a.host_out)[1] = *a.error_flags;
+        }
+    }
     // a wave keeps running while either half has a keypoint (DPP/ballot need
     // the whole wave); an empty half works on level 0 / key 0 and stores nothing
     const bool valid = level >= 0;
@@ -1919,7 +1929,12 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
         const int t1 = lds_bytes[a2];
         const unsigned long long bits = __ballot(t0 < t1);
         // this half's 32 bits are descriptor bits 32r .. 32r+31 (bytes 4r .. 4r+3)
-        if (valid && hl == r) reinterpret_cast<uint32_t*>(desc)[r] = (uint32_t)(bits >> (32 * half));
+        if (valid && hl == r) {
+            reinterpret_cast<uint32_t*>(desc)[r] = (uint32_t)(bits >> (32 * half));
+            if (a.host_out)
+                reinterpret_cast<uint32_t*>(a.host_out + 64 + (size_t)a.nfeatures * sizeof(orbx_keypoint) +
+                                            (size_t)k * 32)[r] = (uint32_t)(bits >> (32 * half));
+        }
     }
     if (valid && hl == 0) {
         orbx_keypoint kp;
@@ -1935,6 +1950,7 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a, int nframes)
         kp.octave = level;
         kp.class_id = -1;
         a.out_kps[(size_t)(a.first_slot + f) * a.nfeatures + k] = kp;
+        if (a.host_out) reinterpret_cast<orbx_keypoint*>(a.host_out + 64)[k] = kp;
     }
 }
 
@@ -2019,6 +2035,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.out_desc = ctx->out_desc;
     a.out_n = ctx->out_n;
     a.error_flags = ctx->error_flags;
+    a.host_out = ctx->single_frame ? ctx->single_out : nullptr;
     a.retain_scratch = ctx->retain_scratch + (size_t)first * (g.list_entries + 4 * g.cells.size());
     a.blur_tiles = ctx->blur_tiles;
     a.harris = ctx->harris;
@@ -2395,32 +2412,5 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     return ORBX_OK;
 }
 
-// Single-frame read-back (orbx_extract's graph): slot 0's keypoint count,
-// the device error flags, then its keypoint records and descriptors, stored
-// straight into the page-locked host buffer (header 64 bytes; records at 64;
-// descriptors at 64 + nfeatures * 28).  One launch in place of four copies.
-__global__ __launch_bounds__(1024) void k_pack_single(const int32_t* out_n, const int32_t* flags,
-                                                     const orbx_keypoint* kps, const uint8_t* desc, int nf,
-                                                     uint8_t* host)
-{
-    const int n = min(max(out_n[0], 0), nf);
-    if (threadIdx.x == 0) {
-        reinterpret_cast<int32_t*>(host)[0] = out_n[0];
-        reinterpret_cast<int32_t*>(host)[1] = flags[0];
-    }
-    const uint32_t* ks = reinterpret_cast<const uint32_t*>(kps);
-    uint32_t* kd = reinterpret_cast<uint32_t*>(host + 64);
-    for (int i = threadIdx.x; i < n * 7; i += blockDim.x) kd[i] = ks[i];
-    const uint4* ds = reinterpret_cast<const uint4*>(desc);
-    uint4* dd = reinterpret_cast<uint4*>(host + 64 + (size_t)nf * sizeof(orbx_keypoint));
-    for (int i = threadIdx.x; i < n * 2; i += blockDim.x) dd[i] = ds[i];
-}
-
-int launch_pack_single(orbx_ctx* ctx, uint8_t* host, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_pack_single, dim3(1), dim3(1024), 0, st, ctx->out_n, ctx->error_flags, ctx->out_kps,
-                       ctx->out_desc, ctx->geom.nfeatures, host);
-    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_ERR_HIP;
-}
 
 }  // namespace orbx

@@ -250,6 +250,7 @@ struct orbx_ctx {
     int launch_mode = 1;                       // 0: stream launches, 1: graph, 2: graph reading the staged frame in place
     const uint8_t* frames_src = nullptr;       // launch_extract's frame source override (graph capture of mode 2)
     bool single_frame = false;                // launch_extract: one frame, latency-first launches (graph capture)
+    uint8_t* single_out = nullptr;            // its page-locked read-back block (k_describe writes it)
     void* one_in = nullptr;
     size_t one_in_bytes = 0;
     void* one_out = nullptr;
@@ -364,7 +365,6 @@ struct MatchSpec {
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nullptr);
 // orbx_extract's read-back kernel: slot 0's count, error flags, keypoints and
 // descriptors into the page-locked buffer `host` (layout in orbx_extract.hip)
-int launch_pack_single(orbx_ctx* ctx, uint8_t* host, hipStream_t st);
 // orbx_pyramid.hip: plan of the fused pyramid + blur kernel for geometry g
 // (plan.ok false when it does not apply: tiny levels, LDS or job overflow),
 // its upload, and its launch over nb frames (frame f reads slot first_slot + f
