@@ -367,7 +367,12 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     __shared__ float s_e[kFrames][6][kCache];
     __shared__ uint8_t s_f[kFrames][kCache];
     __shared__ double s_rows[kExact ? kPoseThreads / 64 : 1][kExact ? 64 : 1][28];   // per-edge terms
-    __shared__ double s_red[kW][28];                                                 // kW > 1: per-wave sums
+    // kW > 1: per-wave sums and the solver's broadcast, in two buffers used
+    // in turn, so each exchange needs one barrier (a buffer is written again
+    // only after the barrier of the exchange that used the other one, which
+    // every thread passes after its reads of this one)
+    __shared__ double s_red[2][kW][28];
+    int rb = 0;
     const int wq = kW == 1 ? threadIdx.x >> 6 : 0;
     const int nL = min(nE, kCache);
     // sums over the frame's threads, the same double on every thread: the
@@ -378,27 +383,27 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
         if constexpr (kW > 1) {
             if ((threadIdx.x & 63) == 0)
 #pragma unroll
-                for (int k = 0; k < n; k++) s_red[threadIdx.x >> 6][k] = v[k];
+                for (int k = 0; k < n; k++) s_red[rb][threadIdx.x >> 6][k] = v[k];
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < n; k++) {
-                double t = s_red[0][k];
+                double t = s_red[rb][0][k];
 #pragma unroll
-                for (int w = 1; w < kW; w++) t += s_red[w][k];
+                for (int w = 1; w < kW; w++) t += s_red[rb][w][k];
                 v[k] = t;
             }
-            __syncthreads();
+            rb ^= 1;
         }
     };
     auto frame_sum_int = [&](int v) {
         v = wave_sum_int(v);
         if constexpr (kW > 1) {
-            if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6][0] = (double)v;
+            if ((threadIdx.x & 63) == 0) s_red[rb][threadIdx.x >> 6][0] = (double)v;
             __syncthreads();
             int t = 0;
 #pragma unroll
-            for (int w = 0; w < kW; w++) t += (int)s_red[w][0];
-            __syncthreads();
+            for (int w = 0; w < kW; w++) t += (int)s_red[rb][w][0];
+            rb ^= 1;
             return t;
         }
         return v;
@@ -546,9 +551,20 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
 #pragma unroll
                         for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
                 });
-                frame_sums(&chi, 1);
-                frame_sums(h, 21);
-                frame_sums(bv, 6);
+                {   // chi, H and b in one exchange (each sum in the same order as alone)
+                    double v[28];
+                    v[0] = chi;
+#pragma unroll
+                    for (int k = 0; k < 21; k++) v[1 + k] = h[k];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) v[22 + k] = bv[k];
+                    frame_sums(v, 28);
+                    chi = v[0];
+#pragma unroll
+                    for (int k = 0; k < 21; k++) h[k] = v[1 + k];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) bv[k] = v[22 + k];
+                }
                 currentChi = chi;
                 }
                 const double iniChi = currentChi;
@@ -585,18 +601,18 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
                     if constexpr (kW > 1) {
                         if (threadIdx.x == 0) {
 #pragma unroll
-                            for (int i = 0; i < 6; i++) s_red[0][i] = xs[i];
+                            for (int i = 0; i < 6; i++) s_red[rb][0][i] = xs[i];
 #pragma unroll
-                            for (int i = 0; i < 7; i++) s_red[0][6 + i] = tp[i];
-                            s_red[0][13] = ok2 ? 1.0 : 0.0;
+                            for (int i = 0; i < 7; i++) s_red[rb][0][6 + i] = tp[i];
+                            s_red[rb][0][13] = ok2 ? 1.0 : 0.0;
                         }
                         __syncthreads();
 #pragma unroll
-                        for (int i = 0; i < 6; i++) xs[i] = s_red[0][i];
+                        for (int i = 0; i < 6; i++) xs[i] = s_red[rb][0][i];
 #pragma unroll
-                        for (int i = 0; i < 7; i++) tp[i] = s_red[0][6 + i];
-                        ok2 = s_red[0][13] != 0.0;
-                        __syncthreads();
+                        for (int i = 0; i < 7; i++) tp[i] = s_red[rb][0][6 + i];
+                        ok2 = s_red[rb][0][13] != 0.0;
+                        rb ^= 1;
                     }
                     if (!ok2) not_posdef++;
                     // computeActiveErrors at the trial estimate
