@@ -70,7 +70,10 @@ constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
 constexpr int kPoseLdsEdges = 800;
 // edges a one-frame workgroup (the kW > 1 instances) keeps in LDS: 75 KB
 constexpr int kPoseLdsEdgesWide = 3072;
-constexpr int kPoseWideWaves = 4;    // wavefronts per frame of the one-call kernel
+#ifndef ORBX_POSE_WIDE
+#define ORBX_POSE_WIDE 4
+#endif
+constexpr int kPoseWideWaves = ORBX_POSE_WIDE;    // wavefronts per frame of the one-call kernel
 static_assert((kPoseThreads / 64) * kPoseLdsEdges * (6 * sizeof(float) + 1) <= 80 * 1024,
               "two pose workgroups per CU need <= 80 KB of LDS each (gfx950: 160 KB per CU)");
 
