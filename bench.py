@@ -512,7 +512,7 @@ def single_call_legs(args, frames, nf, w, h):
                                 ctypes.byref(n)), "orbx_extract")
 
     ex = {}
-    for mode, name in ((1, "graph"), (2, "graph_frame_in_place"), (0, "stream_launches")):
+    for mode, name in ((1, "graph"), (0, "stream_launches")):
         ctx1.set_launch_mode(mode)
         ex[name] = time_calls(ext, len(imgs), proto)
     ctx1.set_launch_mode(1)
@@ -768,10 +768,6 @@ def run_frames(args, wl, rank, local, world, dist):
     ctx.upload(frames, first=B)
     if args.split_ways:
         ctx.set_split(args.split_ways)
-    if args.pyramid_mode:
-        ctx.set_pyramid_mode(args.pyramid_mode)
-    if args.fast_chunk:
-        ctx.set_fast_chunk(args.fast_chunk)
     pipelined = not (args.sync_match or args.serial)
 
     def configure(serial):
@@ -1131,10 +1127,6 @@ def main():
                          "order) -- the form the headline roofline's PMC profile is collected from")
     ap.add_argument("--split-ways", type=int, default=0, choices=[0, 2, 3, 4],
                     help="extraction pipeline parts (orbx_dev_set_split; 0 = library default, 3)")
-    ap.add_argument("--pyramid-mode", type=int, default=0, choices=[0, 1, 2],
-                    help="orbx_dev_set_pyramid_mode: 0 staged launches (default), 1 fused pyramid + blur, 2 band cascade")
-    ap.add_argument("--fast-chunk", type=int, default=0,
-                    help="orbx_dev_set_fast_chunk: cells per FAST workgroup (0 = library default)")
     ap.add_argument("--pose-exact", action="store_true",
                     help="pose workload: sums in g2o's sequential edge order (orbx_pose_set_exact)")
     ap.add_argument("--no-single-call", action="store_true",

@@ -39,8 +39,11 @@ extern "C" {
  *      image bounds of device-resident frames (orbx_dev_set_image_bounds),
  *      multi-workgroup single local-BA problems (orbx_lba_set_workgroups);
  *      additions only.
- *   4: orbx_pose_set_exact / orbx_pose_get_exact; additions only. */
-#define ORBX_ABI_VERSION 4
+ *   4: orbx_pose_set_exact / orbx_pose_get_exact; additions only.
+ *   5: the measured-slower opt-in modes removed (orbx_dev_set_pyramid_mode,
+ *      orbx_dev_pyramid_fused / _kind, orbx_dev_set_fast_chunk / get, launch
+ *      modes 2 and 3); orbx_lba_last_workgroups, orbx_debug_lba_split. */
+#define ORBX_ABI_VERSION 5
 int orbx_abi_version(void);
 
 #define ORBX_OK               0
@@ -115,15 +118,14 @@ int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
  *     blur on a branch beside FAST and retainBest), then one kernel that
  *     stores the count, error flags, keypoints and descriptors into a
  *     page-locked buffer -- and one synchronisation.  The graph is captured
- *     on the first call of a configuration (frame size, launch mode,
- *     fp-contract mode, nth_element era, pyramid mode, FAST chunking) and
- *     replayed after that.
- *   2: as 1, but the pyramid kernels read the frame from the page-locked
- *     staging buffer directly (no copy).
+ *     on the first call of a configuration (frame size, fp-contract mode,
+ *     nth_element era) and replayed after that.
  *   0: the kernels launched one by one on the context stream, with pageable
  *     copies (rounds 1-4).
  * Both produce identical outputs; kernel timing (orbx_dev_kernel_time_enable)
- * takes the stream launches. */
+ * takes the stream launches.  (Modes 2 -- the pyramid reading the staging
+ * buffer in place -- and 3 -- the single-frame launches without a graph --
+ * measured within noise of 1 and were removed in ABI 5.) */
 int orbx_set_launch_mode(orbx_ctx* ctx, int mode);
 int orbx_get_launch_mode(const orbx_ctx* ctx);
 
@@ -194,34 +196,11 @@ int orbx_dev_extract_match(orbx_ctx* ctx, int first, int count, int seq_len, int
  * consecutive batches concurrent).  Any other call on the context, or an
  * extraction into slots the pending match reads, waits for it first. */
 int orbx_dev_set_async_match(orbx_ctx* ctx, int enable);
-/* Pyramid construction mode (all produce identical buffers):
- * 0 = default: staged launches (level-0 copy, one resize per level, blur);
- * 2 = the raw pyramid as a band cascade in one launch (one workgroup per row
- *     band and frame derives every level from the previous level's rows in
- *     LDS), then the blur; frames whose width is not a multiple of 16 take the
- *     staged launches.  Slower than the staged launches at C2 (1.77 vs 1.03 ms
- *     serialised per 1024 frames), kept for parity
- *     coverage and experiments;
- * 1 = one fused launch per batch (orbx_pyramid.hip) that streams each frame
- *     once and builds every level and its blur from LDS rings, used when the
- *     frame size fits its plan (otherwise the staged launches run).  It
- *     holds one 1024-thread workgroup per frame on a CU for the whole frame,
- *     which the two-stream extraction pipeline cannot overlap: slower at C2
- *     (DESIGN.md section 3), kept for parity coverage and experiments.
- * orbx_dev_pyramid_fused reports whether the fused launch applies to the
- * current frame size and mode (1) or not (0). */
-int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode);
-int orbx_dev_pyramid_fused(orbx_ctx* ctx);
-/* The construction the current frame size and mode run: 0 staged launches,
- * 1 fused, 2 band cascade. */
-int orbx_dev_pyramid_kind(orbx_ctx* ctx);
-/* Cells per FAST workgroup (k_fast_cells, src/ORBextractor.cc:599-614 per
- * cell): 1 = one workgroup per cell; n > 1 = each workgroup scores n
- * consecutive cells of a frame and copies the next cell's tile into a second
- * LDS buffer while it scores the current one.  Outputs are identical; cells
- * too wide for two buffers take one per workgroup.  Range 1..64. */
-int orbx_dev_set_fast_chunk(orbx_ctx* ctx, int cells);
-int orbx_dev_get_fast_chunk(const orbx_ctx* ctx);
+/* (ABI 5 removed the opt-in pyramid modes -- one fused pyramid + blur
+ * launch per batch, and the band-cascade raw pyramid for batches -- and
+ * chunked FAST workgroups: each measured slower than the default at every
+ * frame size.  The band cascade remains the pyramid of
+ * orbx_extract's single-frame graph, where it is the fastest.) */
 /* SearchForInitialization (B3) for slots [first, first+count): slot s is
  * matched against slot s-1 unless s % seq_len == 0 (sequence start).  Frame
  * s-1 plays F1 (initial frame), s plays F2; vbPrevMatched = F1 keypoints. */
@@ -716,9 +695,23 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
  * system fits a workgroup's LDS); 1 = one workgroup, as in a batch; n > 1 =
  * n workgroups.  Every setting gives the same bits (k_lba_split sums in the
  * single-workgroup kernel's order); more workgroups cut the latency of the
- * call LocalMapping makes once per keyframe (src/LocalMapping.cc:83). */
+ * call LocalMapping makes once per keyframe (src/LocalMapping.cc:83).
+ * The workgroups of one problem meet at grid barriers, so they must all be
+ * resident at once: the count is capped at what the device holds of that
+ * kernel (occupancy x CUs: a partitioned device, or a setting of 256, gets
+ * fewer), the launch is cooperative where the device supports it, and a
+ * solve whose barrier still times out (another context's kernels holding
+ * the CUs) is run again on one workgroup -- same bits, longer call. */
 int orbx_lba_set_workgroups(orbx_ctx* ctx, int n);
 int orbx_lba_get_workgroups(const orbx_ctx* ctx);
+/* Workgroups the last local-BA launch of ctx ran with (after the cap and any
+ * one-workgroup re-run). */
+int orbx_lba_last_workgroups(const orbx_ctx* ctx);
+/* Test hooks of that residency handling (fail: the next n split launches
+ * see a barrier timeout; fallback 0: no re-run, ORBX_ERR_HIP with the
+ * caller's arrays untouched; cap > 0: capacity capped; coop -1 / 0 / 1:
+ * device choice / plain / cooperative launch; negative = unchanged). */
+int orbx_debug_lba_split(orbx_ctx* ctx, int fail, int fallback, int cap, int coop);
 
 /* Batched throughput form: P independent problems, one workgroup each.
  * aborts: NULL, or P flags (entries may be NULL), each polled between LM

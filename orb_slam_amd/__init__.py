@@ -77,11 +77,6 @@ def _declare(L):
         "orbx_get_fp_contract": ([vp], i),
         "orbx_set_nth_pivot": ([vp, i], i),
         "orbx_get_nth_pivot": ([vp], i),
-        "orbx_dev_set_pyramid_mode": ([vp, i], i),
-        "orbx_dev_pyramid_fused": ([vp], i),
-        "orbx_dev_pyramid_kind": ([vp], i),
-        "orbx_dev_set_fast_chunk": ([vp, i], i),
-        "orbx_dev_get_fast_chunk": ([vp], i),
         "orbx_dev_extract_match": ([vp, i, i, i, i, i, i, f, i], i),
         "orbx_dev_read_features": ([vp, i, vp, vp, i, ip], i),
         "orbx_dev_read_matches": ([vp, i, vp, i, ip, ip], i),
@@ -140,6 +135,8 @@ def _declare(L):
         "orbx_abi_version": ([], i),
         "orbx_lba_set_workgroups": ([vp, i], i),
         "orbx_lba_get_workgroups": ([vp], i),
+        "orbx_lba_last_workgroups": ([vp], i),
+        "orbx_debug_lba_split": ([vp, i, i, i, i], i),
         "orbx_pose_set_exact": ([vp, i], i),
         "orbx_pose_get_exact": ([vp], i),
         "orbx_dev_set_image_bounds": ([vp, vp], i),
@@ -295,30 +292,6 @@ class Context:
         """Queue extract_match's matching behind the extraction on an internal
         stream; later extract_match calls on other slots overlap it."""
         _check(lib().orbx_dev_set_async_match(self._h, int(enable)), "orbx_dev_set_async_match")
-
-    def set_pyramid_mode(self, mode):
-        """0: the staged launches (level-0 copy, per-level resize, blur; the
-        default), 1: one fused pyramid + blur launch where its plan fits the
-        frame size, 2: the raw pyramid as one band-cascade launch, then the
-        blur (staged launches where the cascade does not fit)."""
-        _check(lib().orbx_dev_set_pyramid_mode(self._h, int(mode)), "orbx_dev_set_pyramid_mode")
-
-    def pyramid_fused(self):
-        """True when extraction of the current frame size uses the fused pyramid."""
-        return bool(lib().orbx_dev_pyramid_fused(self._h))
-
-    def pyramid_kind(self):
-        """The construction extraction runs: 0 staged, 1 fused, 2 cascade."""
-        return lib().orbx_dev_pyramid_kind(self._h)
-
-    def set_fast_chunk(self, cells):
-        """Cells per FAST workgroup: 1 = one per workgroup, n > 1 = n cells with
-        the next cell's tile prefetched into a second LDS buffer (identical
-        outputs)."""
-        _check(lib().orbx_dev_set_fast_chunk(self._h, int(cells)), "orbx_dev_set_fast_chunk")
-
-    def fast_chunk(self):
-        return lib().orbx_dev_get_fast_chunk(self._h)
 
     def match_bf_prev(self, first, count, seq_len, th_low=50, nnratio=0.9):
         _check(lib().orbx_dev_match_bf_prev(self._h, first, count, seq_len, th_low, nnratio),

@@ -80,7 +80,7 @@ static void free_buffers(orbx_ctx* ctx)
                     ctx->level_keys, ctx->cell_keys64, ctx->level_keys64, ctx->level_count, ctx->out_kps, ctx->out_desc, ctx->out_n,
                     ctx->match12, ctx->match_n, ctx->error_flags, ctx->dgeom.levels, ctx->dgeom.cells,
                     ctx->dgeom.res_cols, ctx->dgeom.res_rows, ctx->dgeom.umax, ctx->blur_tiles, ctx->cascade,
-                    ctx->scratch, ctx->pose_dev, ctx->bow_dev, ctx->d_pyr_levels, ctx->d_pyr_sched, ctx->d_pyr_waves};
+                    ctx->scratch, ctx->pose_dev, ctx->bow_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
@@ -163,12 +163,36 @@ static int set_geometry(orbx_ctx* ctx, int w, int h)
         ORBX_HIP_CHECK(hipMemcpy(ctx->cascade, g.cascade.data(), g.cascade.size() * sizeof(int4), hipMemcpyHostToDevice));
     // The retain kernel keeps per-cell state for up to 256 cells per level.
     if (g.max_cells_per_level > 256) return ORBX_ERR_UNSUPPORTED;
-    // the fused-pyramid plan is optional: planned on first use (pyramid mode 1)
-    ctx->pyr = PyrPlan{};
-    ctx->pyr_planned = false;
     ctx->geom_w = w;
     ctx->geom_h = h;
     ctx->geom_gen++;   // a captured single-frame graph holds the old tables and buffers
+    return ORBX_OK;
+}
+
+// The streams of the batch pipeline (stream2, the part streams, the match
+// stream), created on first use.  HIP maps each new stream of a process onto
+// its hardware queues in turn (GPU_MAX_HW_QUEUES, 4 by default): a context
+// that only ever serves single calls -- the Tracking, LocalMapping and
+// LoopClosing threads of the reference each hold one -- then keeps one
+// stream, and three such contexts get a hardware queue each instead of
+// sharing them with idle pipeline streams (a call queued behind another
+// context's 3 ms local BA on a shared queue waits for it).
+int ensure_aux_streams(orbx_ctx* ctx)
+{
+    if (ctx->mstream) return ORBX_OK;
+    hipStream_t s2 = nullptr, ms = nullptr, xs[orbx_ctx::kMaxWays - 2] = {};
+    bool ok = hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&ms, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < orbx_ctx::kMaxWays - 2; i++)
+        ok = hipStreamCreateWithFlags(&xs[i], hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
+        for (hipStream_t s : {s2, ms, xs[0], xs[1]})
+            if (s) (void)hipStreamDestroy(s);
+        return ORBX_ERR_HIP;
+    }
+    ctx->stream2 = s2;
+    for (int i = 0; i < orbx_ctx::kMaxWays - 2; i++) ctx->xstreams[i] = xs[i];
+    ctx->mstream = ms;   // last: its presence marks the set complete
     return ORBX_OK;
 }
 
@@ -191,7 +215,7 @@ static void drop_single_graph(orbx_ctx* ctx)
     if (ctx->one_graph) (void)hipGraphDestroy(ctx->one_graph);
     ctx->one_exec = nullptr;
     ctx->one_graph = nullptr;
-    ctx->one_key = 0;
+    ctx->one_key = orbx_ctx::GraphKey{};
 }
 
 static int check_errors(orbx_ctx* ctx)
@@ -274,17 +298,15 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
     int r = ORBX_OK;
     const int S = max_batch;
+    // one stream up front; the batch pipeline's part and match streams are
+    // created on first use (ensure_aux_streams)
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
-    if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
-    if (r == ORBX_OK && hipStreamCreateWithFlags(&ctx->mstream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     if (r == ORBX_OK && (hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->ev_extracted, hipEventDisableTiming) != hipSuccess))
         r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxPending; i++)
         if (hipEventCreateWithFlags(&ctx->ev_match[i], hipEventDisableTiming) != hipSuccess) r = ORBX_ERR_HIP;
-    for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays - 2; i++)
-        if (hipStreamCreateWithFlags(&ctx->xstreams[i], hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
     for (int i = 0; r == ORBX_OK && i < orbx_ctx::kMaxWays; i++)
         if (hipEventCreateWithFlags(&ctx->ev_part_fast[i], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ctx->ev_part_done[i], hipEventDisableTiming) != hipSuccess ||
@@ -463,38 +485,6 @@ int orbx_dev_set_async_match(orbx_ctx* ctx, int enable)
     return ORBX_OK;
 }
 
-int orbx_dev_set_pyramid_mode(orbx_ctx* ctx, int mode)
-{
-    if (!ctx || mode < 0 || mode > 2) return ORBX_ERR_ARG;
-    ctx_enter(ctx);
-    ctx->pyr_mode = mode;
-    return ORBX_OK;
-}
-
-int orbx_dev_set_fast_chunk(orbx_ctx* ctx, int cells)
-{
-    if (!ctx || cells < 1 || cells > 64) return ORBX_ERR_ARG;
-    ctx_enter(ctx);
-    ctx->fast_chunk = cells;
-    return ORBX_OK;
-}
-
-int orbx_dev_get_fast_chunk(const orbx_ctx* ctx) { return ctx ? ctx->fast_chunk : ORBX_ERR_ARG; }
-
-int orbx_dev_pyramid_fused(orbx_ctx* ctx)
-{
-    if (!ctx) return ORBX_ERR_ARG;
-    return ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx) ? 1 : 0;
-}
-
-int orbx_dev_pyramid_kind(orbx_ctx* ctx)
-{
-    if (!ctx) return ORBX_ERR_ARG;
-    if (ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx)) return 1;
-    if (ctx->pyr_mode == 2 && ctx->geom.cascade_bands > 0) return 2;
-    return 0;
-}
-
 int orbx_dev_match_bf_prev(orbx_ctx* ctx, int first, int count, int seq_len, int th_low, float nnratio)
 {
     if (!ctx || count <= 0 || first < 0 || first + count > ctx->slots || seq_len <= 0) return ORBX_ERR_ARG;
@@ -643,32 +633,26 @@ int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
         if (hipHostMalloc(&ctx->one_out, out_bytes, hipHostMallocDefault) != hipSuccess) return ORBX_ERR_NOMEM;
         ctx->one_out_bytes = out_bytes;
     }
-    // everything a captured launch sequence depends on
-    const unsigned long long key = (unsigned long long)ctx->launch_mode | (unsigned long long)ctx->geom_gen << 2 |
-                                   (unsigned long long)ctx->fp_contract << 33 |
-                                   (unsigned long long)ctx->nth_pivot << 34 | (unsigned long long)ctx->pyr_mode << 35 |
-                                   (unsigned long long)ctx->fast_chunk << 37;
-    // the call's device work on the context stream: the frame into slot 0
-    // (modes 1 and 3; mode 2 reads the staging buffer in place), the
-    // single-frame extraction launches, the read-back kernel
+    // everything a captured launch sequence depends on (each setting in a
+    // field of its own)
+    const orbx_ctx::GraphKey key{ctx->geom_gen, ctx->fp_contract, ctx->nth_pivot, true};
+    // the call's device work on the context stream: the frame into slot 0,
+    // the single-frame extraction launches (k_describe also writes the
+    // read-back block)
     uint8_t* out_host = static_cast<uint8_t*>(ctx->one_out);
     auto enqueue = [&]() -> int {
         int cr = ORBX_OK;
-        if (ctx->launch_mode != 2 &&
-            hipMemcpyAsync(ctx->frames, ctx->one_in, in_bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        if (hipMemcpyAsync(ctx->frames, ctx->one_in, in_bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             cr = ORBX_ERR_HIP;
-        ctx->frames_src = ctx->launch_mode == 2 ? static_cast<const uint8_t*>(ctx->one_in) : nullptr;
         ctx->single_frame = true;
         ctx->single_out = out_host;   // k_describe writes the read-back block (no pack launch)
         if (cr == ORBX_OK) cr = launch_extract(ctx, 0, 1);
-        ctx->frames_src = nullptr;
         ctx->single_frame = false;
         ctx->single_out = nullptr;
         return cr;
     };
-    if (ctx->launch_mode != 3 && (!ctx->one_exec || ctx->one_key != key)) {
+    if (!ctx->one_exec || !(ctx->one_key == key)) {
         drop_single_graph(ctx);
-        if (ctx->pyr_mode == 1) ensure_pyramid_plan(ctx);   // plans and uploads synchronously: not inside a capture
         ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
         ORBX_HIP_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
         const int cr = enqueue();
@@ -692,16 +676,11 @@ int orbx_extract(orbx_ctx* ctx, const uint8_t* img, int w, int h, size_t stride,
     } else {
         for (int y = 0; y < h; y++) std::memcpy(in + (size_t)y * w, img + (size_t)y * stride, (size_t)w);
     }
-    if (ctx->launch_mode == 3) {
-        const int cr = enqueue();
-        if (cr != ORBX_OK) return cr;
-    } else {
-        // host-side effects of launch_extract that a graph replay does not repeat
-        if (!ctx->bow_ready.empty()) ctx->bow_ready[0] = 0;
-        ctx->last_first = 0;
-        ctx->last_count = 1;
-        ORBX_HIP_CHECK(hipGraphLaunch(ctx->one_exec, ctx->stream));
-    }
+    // host-side effects of launch_extract that a graph replay does not repeat
+    if (!ctx->bow_ready.empty()) ctx->bow_ready[0] = 0;
+    ctx->last_first = 0;
+    ctx->last_count = 1;
+    ORBX_HIP_CHECK(hipGraphLaunch(ctx->one_exec, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     const uint8_t* out = static_cast<const uint8_t*>(ctx->one_out);
     int32_t n = 0, flags = 0;
@@ -730,7 +709,7 @@ int orbx_dev_set_image_bounds(orbx_ctx* ctx, const float* bounds)
 
 int orbx_set_launch_mode(orbx_ctx* ctx, int mode)
 {
-    if (!ctx || mode < 0 || mode > 3) return ORBX_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 1) return ORBX_ERR_ARG;
     ctx_enter(ctx);
     ctx->launch_mode = mode;
     return ORBX_OK;
@@ -792,7 +771,9 @@ int orbx_dev_download_async(orbx_ctx* ctx, int first, int count, orbx_keypoint* 
     (void)hipSetDevice(ctx->device);
     // after the extraction of the slots (every stream it may run on) and, mstream
     // being in order, after their queued match
-    int r = order_after_extraction(ctx, ctx->mstream);
+    int r = ensure_aux_streams(ctx);
+    if (r != ORBX_OK) return r;
+    r = order_after_extraction(ctx, ctx->mstream);
     if (r != ORBX_OK) return r;
     const size_t nf = ctx->geom.nfeatures, s0 = first, n = count;
     const hipStream_t st = ctx->mstream;

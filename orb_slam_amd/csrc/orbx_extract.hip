@@ -819,24 +819,16 @@ constexpr int kDiagRepeat[4] = {ORBX_DIAG_REPEAT};
 // kThreads: 256 for cells up to 208-byte rows; the wide tiles of large
 // frames (1920x1080: 336-byte rows, 75 KB of LDS, two workgroups per CU)
 // get more waves per workgroup instead.
-// kChunk (whole-cell instances only; orbx_dev_set_fast_chunk, measured
-// slower than one cell per workgroup): each workgroup
-// takes `chunk` consecutive cells of its frame with two tile buffers; the
-// next cell's tile is copied HBM -> LDS by global_load_lds (no VGPR staging)
-// before the current cell is scored.  The compiler waits for that copy at the
-// scoring's first LDS atomic (the `nz` bits), so the copy overlaps only the
-// compass work before the first survivor batch.
 __device__ __forceinline__ void blur_block(const ExtractArgs& a, const int4* tiles, int bx, int f);
 
 // kBlurTail (orbx_extract's single-frame graph): the grid carries the blur's
 // work blocks after the cells (blockIdx.x >= ncells), so FAST and the blur,
 // which both read only the raw pyramid, are one launch.
-template <int kP, int kThreads = 256, bool kBanded = false, bool kChunk = false, bool kBlurTail = false>
+template <int kP, int kThreads = 256, bool kBanded = false, bool kBlurTail = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThreads > 256 ? 6 : 4))) void k_fast_cells(
-    ExtractArgs a, int tile_bytes, int band_rows, int chunk)
+    ExtractArgs a, int tile_bytes, int band_rows)
 {
-    static_assert(!kChunk || (kP > 0 && !kBanded), "chunked FAST takes whole cells at a template pitch");
-    static_assert(!kBlurTail || (!kChunk && kThreads == kBlurItems), "the blur tail runs 256-thread blur blocks");
+    static_assert(!kBlurTail || kThreads == kBlurItems, "the blur tail runs 256-thread blur blocks");
     if constexpr (kBlurTail) {
         if ((int)blockIdx.x >= a.ncells) {
             blur_block(a, a.blur_tiles, (int)blockIdx.x - a.ncells, (int)blockIdx.y);
@@ -864,10 +856,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     auto clear_maps_at = [&](uint8_t* sm) {
         for (int i = tid; i < clear16; i += kBlock) reinterpret_cast<uint4*>(sm)[i] = make_uint4(0, 0, 0, 0);
     };
-    // One cell.  tile / sm: its tile buffer and the S' map (nz follows sm);
-    // ready: the tile already holds the cell's rows and S' / nz are clear
-    // (chunked instances), so the first band neither loads nor clears.
-    auto process = [&](const int cell, uint8_t* const tile, uint8_t* const sm, const bool ready) {
+    // One cell.  tile / sm: its tile buffer and the S' map (nz follows sm).
+    auto process = [&](const int cell, uint8_t* const tile, uint8_t* const sm) {
     const CellGeom C = cget(a.cells, cell);
     int32_t* count_out = a.cell_count + (size_t)f * a.ncells + cell;
     if (!C.valid) {
@@ -1234,7 +1224,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
         }
     } else if (hy > 6) {   // the whole cell as one band (the host sends band_rows = 0)
         int tmin_final = a.fast_th;
-        n1 = band(3, hy - 3, a.fast_th, ready);
+        n1 = band(3, hy - 3, a.fast_th);
         FP_MARK(2);
         if (a.fast_th > a.fast_th_low && n1 <= 3) {   // uniform over the block
             if (threadIdx.x == 0) FP_ADD(8, 1);
@@ -1252,54 +1242,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     FP_MARK(4);
     if (tid == 0) FP_ADD(9, 1);
     };
-    if constexpr (!kChunk) {
-        process(blockIdx.x, smem, smem + tile_bytes, false);
-    } else {
-        // LDS: tile buffers 0 and 1, then S' and nz
-        uint8_t* const sm = smem + 2 * tile_bytes;
-        constexpr int kW = kP >> 4;   // 16-byte words per tile row
-        // Copy a whole cell (rows 0 .. hy - 1, kW words each) into dst with
-        // global_load_lds: lane-linear LDS destinations, so every word of
-        // a row is loaded (columns past the ROI repeat its last word and are
-        // never read as pixels).  Cells process() does not score get none.
-        auto prefetch = [&](const int cell, uint8_t* dst) {
-            const CellGeom C = cget(a.cells, cell);
-            if (!C.valid || C.hy <= 6) return;
-            const LevelGeom L = cget(a.levels, C.level);
-            const int roi_x = kEdge + C.ini_x, x_al = roi_x & ~15;
-            const int last = ((roi_x - x_al + C.hx + 15) >> 4) - 1;
-            const uint8_t* src =
-                a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)(kEdge + C.ini_y) * L.stride + x_al;
-            const int n = C.hy * kW;
-            for (int base = wv * 64; base < n; base += kBlock) {
-                const int i = base + lane;
-                if (i < n) {
-                    const int r = i / kW, c = min(i - r * kW, last);
-                    __builtin_amdgcn_global_load_lds(src + (uint32_t)(r * L.stride + 16 * c),
-                                                     (__attribute__((address_space(3))) void*)(dst + 16 * base), 16, 0,
-                                                     0);
-                }
-            }
-        };
-        const int c0 = blockIdx.x * chunk, c1 = min(c0 + chunk, a.ncells);
-        clear_maps_at(sm);
-        prefetch(c0, smem);
-        for (int cell = c0; cell < c1; cell++) {
-            const int k = cell - c0;
-            // this cell's tile landed, S' and nz are clear, and the previous
-            // cell is done with the other buffer; the next cell's copy is
-            // issued before this cell's scoring.  A workgroup barrier does not
-            // wait for vector-memory counters: each wave drains its own
-            // global_load_lds copies (vmcnt) first, then the barrier makes
-            // every wave's part of the tile visible to all.
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (cell + 1 < c1) prefetch(cell + 1, smem + ((k + 1) & 1) * tile_bytes);
-            process(cell, smem + (k & 1) * tile_bytes, sm, true);
-            __syncthreads();
-            clear_maps_at(sm);
-        }
-    }
+    process(blockIdx.x, smem, smem + tile_bytes);
 }
 
 // ---------------------------------------------------------------------------
@@ -2010,6 +1953,10 @@ namespace orbx {
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
 {
     const Geometry& g = ctx->geom;
+    if (count > 1 || (m && m->kind != 0 && ctx->async_match)) {   // the batch pipeline's streams
+        const int r = ensure_aux_streams(ctx);
+        if (r != ORBX_OK) return r;
+    }
     for (int sl = first; sl < first + count && sl < (int)ctx->bow_ready.size(); sl++) ctx->bow_ready[sl] = 0;
     // frames still being uploaded (orbx_dev_upload_async): every part and
     // half below starts on, or is released from, the context stream
@@ -2020,9 +1967,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.res_cols = ctx->dgeom.res_cols;
     a.res_rows = ctx->dgeom.res_rows;
     a.umax = ctx->dgeom.umax;
-    // the single-frame graph may read its frame where the host staged it
-    // (page-locked, device-mapped: orbx_extract's zero-copy launch mode)
-    a.frames = ctx->frames_src ? ctx->frames_src : ctx->frames;
+    a.frames = ctx->frames;
     // work buffers are per slot (frame f of this pass uses slot first + f):
     // batches on disjoint slots can be in flight at the same time
     a.pyr_raw = ctx->pyr_raw + (size_t)first * g.frame_pyr_bytes;
@@ -2059,21 +2004,14 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     a.max_level_cap = g.max_level_cap;
 
     // The pyramid stages over nb frames on stream st.
-    // fused pyramid + blur (orbx_pyramid.hip) when the plan fits this geometry
-    const bool fused = ctx->pyr_mode == 1 && ensure_pyramid_plan(ctx);
     auto run_pyramid = [&](const ExtractArgs& x, int nb, hipStream_t st) {
-        if (fused) {
-            timer_begin(ctx, "pyramid", st);
-            launch_pyramid(ctx, x.first_slot, x.pyr_raw, x.pyr_blur, nb, st);
-            timer_end(ctx, "pyramid", st);
-            return;
-        }
-        // the whole raw pyramid in one launch: pyramid mode 2, and the
-        // default of orbx_extract's single-frame graph (its lowest latency)
-        if ((ctx->pyr_mode == 2 || (ctx->single_frame && ctx->pyr_mode == 0)) && g.cascade_bands > 0) {
+        // orbx_extract's single-frame graph: the whole raw pyramid in one
+        // launch (its lowest latency; batches fill the chip with the staged
+        // per-level launches below, which measured faster there)
+        if (ctx->single_frame && g.cascade_bands > 0) {
             timer_begin(ctx, "resize", st);
             for (int rep = 0; rep < kDiagRepeat[0]; rep++) {
-                if (ctx->single_frame) {
+                {
                     int tab_off = (g.cascade_lds + 15) & ~15;
                     size_t lds = (size_t)tab_off + 8 * (size_t)(g.cascade_tab_cols + g.cascade_tab_rows);
                     if (lds > 160 * 1024) {   // very wide frames: the tables stay in HBM
@@ -2083,9 +2021,6 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                     hipLaunchKernelGGL(k_pyr_cascade<ORBX_CASCADE_SINGLE_THREADS>, dim3(g.cascade_bands, nb),
                                        dim3(ORBX_CASCADE_SINGLE_THREADS), lds, st, x, ctx->cascade, g.cascade_buf_x,
                                        tab_off, g.cascade_tab_cols);
-                } else {
-                    hipLaunchKernelGGL(k_pyr_cascade<256>, dim3(g.cascade_bands, nb), dim3(256), g.cascade_lds, st, x,
-                                       ctx->cascade, g.cascade_buf_x, 0, 0);
                 }
             }
             timer_end(ctx, "resize", st);
@@ -2130,7 +2065,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
     // 16 = FAST with the blur's blocks in the same launch where the FAST
     // instance takes them (whole cells at a template pitch), else FAST then blur
     auto run_rest = [&](const ExtractArgs& x, int nb, hipStream_t st, int parts) {
-        const bool tail = (parts & 16) && !fused;
+        const bool tail = (parts & 16) != 0;
         bool tail_done = false;
         if (parts & (1 | 16)) {
         timer_begin(ctx, "fast", st);
@@ -2160,21 +2095,13 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             };
             auto fast = [&](auto kern, int bytes, int band_rows, int threads) {
                 const int lds = fast_lds_bytes(bytes);
-                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows, 1);
+                hipLaunchKernelGGL(kern, grid, dim3(threads), lds, st, x, bytes, band_rows);
             };
             auto fast_tail = [&](auto kern, int bytes) {
                 const int lds = fast_lds_bytes(bytes);
                 hipLaunchKernelGGL(kern, dim3((int)g.cells.size() + ctx->blur_tiles_n, nb), dim3(256), lds, st, x, bytes,
-                                   0, 1);
+                                   0);
                 tail_done = true;
-            };
-            // whole cells, `chunk` per workgroup, next tile prefetched (a
-            // second tile buffer)
-            int chunk = ctx->fast_chunk;
-            auto fast_chunked = [&](auto kern, int bytes) {
-                const int lds = fast_lds_bytes(bytes) + bytes;
-                const dim3 cgrid(((int)g.cells.size() + chunk - 1) / chunk, nb);
-                hipLaunchKernelGGL(kern, cgrid, dim3(256), lds, st, x, bytes, 0, chunk);
             };
             // the templated instances queue u16 tile positions: windows of up
             // to 64 KB (larger ones take the runtime-pitch instance)
@@ -2192,22 +2119,15 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
                 bytes = plan(P, fast_static_lds(false), br);
                 return bytes <= 65536;
             };
-            // two tile buffers must fit the CU's LDS with the static queues
-            auto chunk_fits = [&](int b) { return fast_lds_bytes(b) + b + fast_static_lds(false) <= 160 * 1024; };
             if (fits(96)) {
-                if (tail) fast_tail(k_fast_cells<96, 256, false, false, true>, bytes);
-                else if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<96, 256, false, true>, bytes);
+                if (tail) fast_tail(k_fast_cells<96, 256, false, true>, bytes);
                 else fast(k_fast_cells<96>, bytes, 0, 256);
             } else if (fits(144)) {
-                if (tail) fast_tail(k_fast_cells<144, 256, false, false, true>, bytes);
+                if (tail) fast_tail(k_fast_cells<144, 256, false, true>, bytes);
                 else
-                for (int rep = 0; rep < kDiagRepeat[3]; rep++) {
-                    if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<144, 256, false, true>, bytes);
-                    else fast(k_fast_cells<144>, bytes, 0, 256);
-                }
+                for (int rep = 0; rep < kDiagRepeat[3]; rep++) fast(k_fast_cells<144>, bytes, 0, 256);
             } else if (fits(208)) {
-                if (tail) fast_tail(k_fast_cells<208, 256, false, false, true>, bytes);
-                else if (chunk > 1 && chunk_fits(bytes)) fast_chunked(k_fast_cells<208, 256, false, true>, bytes);
+                if (tail) fast_tail(k_fast_cells<208, 256, false, true>, bytes);
                 else fast(k_fast_cells<208>, bytes, 0, 256);
             }
             else if (fits_banded(336)) fast(k_fast_cells<336, kFastWideThreads, true>, bytes, br, kFastWideThreads);
@@ -2244,7 +2164,7 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
         }
         timer_end(ctx, "retain", st);
         }
-        if ((parts & 4 || (tail && !tail_done)) && !fused) {
+        if (parts & 4 || (tail && !tail_done)) {
             timer_begin(ctx, "blur", st);
             for (int rep = 0; rep < kDiagRepeat[1]; rep++)
                 hipLaunchKernelGGL(k_blur, dim3(ctx->blur_tiles_n, nb), dim3(kBlurItems), 0, st, x, ctx->blur_tiles);

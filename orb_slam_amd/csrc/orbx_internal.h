@@ -93,34 +93,6 @@ struct CellGeom {
 struct ResizeCol { int16_t sx0, sx1, a0, a1; };
 struct ResizeRow { int16_t sy0, sy1, b0, b1; };
 
-// Fused pyramid + blur (k_pyramid, orbx_pyramid.hip): one 1024-thread
-// workgroup per frame streams the frame's rows top to bottom; each level keeps
-// its most recent rows in an LDS ring.  Per level: ring placement and the
-// multiply-shift constant of (row mod ring).
-constexpr int kPyrThreads = 1024;
-constexpr int kPyrWaves = kPyrThreads / 64;
-struct PyrLevel {
-    int ring_off;   // LDS byte offset of the ring
-    int ring;       // rows in the ring
-    int rp;         // ring row pitch (padded row rounded up to 16 bytes)
-    uint32_t mul;   // ceil(2^20 / ring): row mod ring = r - ring * ((r * mul) >> 20)
-};
-// Jobs of one wave (-1: none): the blur of 64 dword columns of a level, the
-// resize of 64 dword columns of a level >= 1, 64 level-0 load items.
-struct PyrWave {
-    int16_t blur_level, blur_q0, res_level, res_q0, l0_base, pad;
-};
-struct PyrPlan {
-    bool ok = false;
-    int T = 0, S = 0;             // level-0 rows per step, steps
-    int l0_items = 0, nq16 = 0;   // level-0 load items per step (rows x 16-byte columns)
-    int rows_first = 0, rows_count = 0;   // res_rows entries staged in LDS (levels >= 1)
-    int rows_lds = 0, sched_lds = 0, lds_bytes = 0;
-    std::vector<PyrLevel> levels;
-    std::vector<int32_t> sched;   // S x nlevels: rows produced | rows blurred << 16, by the end of each step
-    PyrWave waves[kPyrWaves];
-};
-
 // Extractor configuration and per-image-size geometry (host computed, the
 // way OpenCV computes its tables per call).
 struct Geometry {
@@ -247,8 +219,7 @@ struct orbx_ctx {
     // image and the outputs, and the whole call (upload, extraction launches,
     // read-back) captured once per configuration as a hipGraph
     // (orbx_set_launch_mode).
-    int launch_mode = 1;                       // 0: stream launches, 1: graph, 2: graph reading the staged frame in place
-    const uint8_t* frames_src = nullptr;       // launch_extract's frame source override (graph capture of mode 2)
+    int launch_mode = 1;                       // 0: stream launches, 1: one captured graph per call
     bool single_frame = false;                // launch_extract: one frame, latency-first launches (graph capture)
     uint8_t* single_out = nullptr;            // its page-locked read-back block (k_describe writes it)
     void* one_in = nullptr;
@@ -257,7 +228,17 @@ struct orbx_ctx {
     size_t one_out_bytes = 0;
     hipGraph_t one_graph = nullptr;
     hipGraphExec_t one_exec = nullptr;
-    unsigned long long one_key = 0;            // configuration the graph was captured for
+    struct GraphKey {                          // configuration the graph was captured for
+        unsigned geom_gen = 0;
+        int fp_contract = 0, nth_pivot = 0;
+        bool valid = false;
+        bool operator==(const GraphKey& o) const
+        {
+            return valid && o.valid && geom_gen == o.geom_gen && fp_contract == o.fp_contract &&
+                   nth_pivot == o.nth_pivot;
+        }
+    };
+    GraphKey one_key;
     unsigned geom_gen = 0;                     // bumped whenever set_geometry changes the buffers
     bool stream_dirty = true;   // the context stream got work outside the async pipeline
     orbx::Geometry geom;
@@ -296,15 +277,6 @@ struct orbx_ctx {
     int4* cascade = nullptr;           // k_pyr_cascade band plan (Geometry::cascade)
     int cap_cascade = 0;
     int blur_tiles_n = 0;
-    // fused pyramid + blur plan for the current geometry (orbx_pyramid.hip)
-    orbx::PyrPlan pyr;
-    int pyr_mode = 0;                  // 0: staged launches, 1: fused, 2: band cascade (staged when it does not fit)
-    int fast_chunk = 1;                // cells per FAST workgroup (> 1: next tile prefetched by global_load_lds)
-    bool pyr_planned = false;          // pyr holds the plan of the current geometry
-    orbx::PyrLevel* d_pyr_levels = nullptr;
-    int32_t* d_pyr_sched = nullptr;
-    orbx::PyrWave* d_pyr_waves = nullptr;
-    int cap_pyr_sched = 0;
     int last_first = 0, last_count = 0;   // batch of the most recent extract
     // Frame::ComputeImageBounds of the slots' keypoints (orbx_dev_set_image_bounds;
     // has_bounds 0: 0..w x 0..h, the undistorted case) for the device matchers
@@ -323,6 +295,21 @@ struct orbx_ctx {
     int lba_workgroups = 0;
     void* lba_split = nullptr;
     size_t lba_split_bytes = 0;
+    // k_lba_split's grid barrier needs all G workgroups resident at once:
+    // G is clamped to the device's capacity for the kernel (occupancy query
+    // x CUs, cached per record type and LDS size), the launch is cooperative
+    // where the device supports it, and a solve whose barrier timed out
+    // (bar[1]) is run again on one workgroup (lba_split_fallback)
+    int lba_split_cap[2] = {0, 0};
+    size_t lba_split_cap_lds[2] = {0, 0};
+    int lba_last_workgroups = 0;        // G of the last launch (after clamping and fallback)
+    bool lba_force_single = false;      // the fallback re-run in progress
+    bool lba_split_timed_out = false;   // set by lba_readback
+    bool lba_split_fallback = true;     // orbx_debug_lba_split: off = return ORBX_ERR_HIP instead
+    int lba_split_coop = -1;            // -1: the device attribute decides; 0 / 1 forced
+    int lba_dbg_fail = 0;               // test hook: split launches whose barrier is made to time out
+    int lba_dbg_cap = 0;                // test hook: > 0 caps the residency capacity
+    int lba_res_iters[2] = {0, 0};      // the resident batch's last run (the fallback re-runs it)
     void* pose_dev = nullptr;
     size_t pose_dev_bytes = 0;
     void* pose_host = nullptr;
@@ -363,22 +350,11 @@ struct MatchSpec {
     float nnratio;
 };
 int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m = nullptr);
-// orbx_extract's read-back kernel: slot 0's count, error flags, keypoints and
-// descriptors into the page-locked buffer `host` (layout in orbx_extract.hip)
-// orbx_pyramid.hip: plan of the fused pyramid + blur kernel for geometry g
-// (plan.ok false when it does not apply: tiny levels, LDS or job overflow),
-// its upload, and its launch over nb frames (frame f reads slot first_slot + f
-// and writes the pyramid buffers at f * frame_pyr_bytes).
-void plan_pyramid(const Geometry& g, int T, PyrPlan& p);
-int upload_pyramid_plan(orbx_ctx* ctx);
-// plan + upload the fused pyramid for the current geometry on first use;
-// true when the fused path can run
-bool ensure_pyramid_plan(orbx_ctx* ctx);
-int launch_pyramid(orbx_ctx* ctx, int first_slot, uint8_t* pyr_raw, uint8_t* pyr_blur, int nb, hipStream_t st);
 // timing helpers (orbx_api.cpp)
 void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 int ensure_scratch(orbx_ctx* ctx, size_t bytes);
+int ensure_aux_streams(orbx_ctx* ctx);   // stream2, the part streams and mstream (first batch use)
 void lba_resident_free(orbx_ctx* ctx);
 int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 }  // namespace orbx

@@ -2595,12 +2595,45 @@ static int lba_plan_stage(orbx_ctx* ctx, int P, const orbx_ba_problem* probs, ui
 // costs less than the solve every workgroup repeats).
 static int lba_split_workgroups(const orbx_ctx* ctx, const LbaPlan& L)
 {
-    if (L.P != 1 || L.lay.s_doubles == 0 || ctx->lba_workgroups == 1) return 1;
+    if (L.P != 1 || L.lay.s_doubles == 0 || ctx->lba_workgroups == 1 || ctx->lba_force_single) return 1;
     if (L.lds_split_bytes + 2048 > 160 * 1024 || L.max_obs0 > kSE) return 1;
     const int nL = L.n_points[0];
     if (ctx->lba_workgroups > 1) return std::min(ctx->lba_workgroups, 256);
     if (nL < 128) return 1;
     return std::min(64, (nL + 31) / 32);
+}
+
+// How many k_lba_split<Rec> workgroups of `lds` dynamic LDS bytes the device
+// holds at once (occupancy per CU x CUs): the grid barrier waits for all G,
+// so G above this would spin until the barrier's bound.  Cached per record
+// type and LDS size; 0 when the query fails.
+template <class Rec>
+static int lba_split_capacity(orbx_ctx* ctx, size_t lds)
+{
+    const int k = std::is_same<Rec, EdgeRecF>::value ? 1 : 0;
+    if (ctx->lba_split_cap_lds[k] != lds || ctx->lba_split_cap[k] == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lba_split<Rec>, kLbaThreads, lds) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+            return 0;
+        ctx->lba_split_cap[k] = per_cu * cus;
+        ctx->lba_split_cap_lds[k] = lds;
+    }
+    int cap = ctx->lba_split_cap[k];
+    if (ctx->lba_dbg_cap > 0) cap = std::min(cap, ctx->lba_dbg_cap);
+    return cap;
+}
+
+// Cooperative launches where the device offers them (the runtime then
+// refuses a grid that cannot be co-resident instead of starting it).
+static bool lba_split_coop(orbx_ctx* ctx)
+{
+    if (ctx->lba_split_coop < 0) {
+        int v = 0;
+        ctx->lba_split_coop =
+            hipDeviceGetAttribute(&v, hipDeviceAttributeCooperativeLaunch, ctx->device) == hipSuccess && v ? 1 : 0;
+    }
+    return ctx->lba_split_coop != 0;
 }
 
 // Queues both optimize() passes of a staged batch on the context stream:
@@ -2618,7 +2651,15 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
     uint8_t* d = L.d;
     // k_lba_split's buffers (a batch of one problem over G workgroups)
     LbaSplit X{};
-    const int G = lba_split_workgroups(ctx, L);
+    int G = lba_split_workgroups(ctx, L);
+    if (G > 1) {
+        // no more workgroups than the device holds at once (a partitioned
+        // device, a large setting): fewer give the same bits
+        const int cap = lba_split_capacity<Rec>(ctx, L.lds_split_bytes);
+        G = std::min(G, cap);
+        if (G < 2) G = 1;
+    }
+    ctx->lba_last_workgroups = G;
     if (G > 1) {
         const long long nL = L.n_points[0], limbs = lba_sys_doubles(6LL * L.nfree0);
         size_t o = 0;
@@ -2657,6 +2698,11 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
                        reinterpret_cast<LbaDev*>(d + L.o_devs), n_out, P, X.bar, failed);
     timer_end(ctx, "lba_build");
     ORBX_HIP_CHECK(hipGetLastError());
+    if (G > 1 && ctx->lba_dbg_fail > 0) {   // test hook: every barrier of this solve reports a timeout
+        ORBX_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(X.bar + 1), 1, 1, ctx->stream));
+        ctx->lba_dbg_fail--;
+    }
+    const bool coop = G > 1 && lba_split_coop(ctx);
     // one layout for both passes: the second pass's systems are no larger
     const size_t lds = L.lds_bytes;
     // the reduced systems in LDS (when the batch's largest fits) or in global memory
@@ -2701,8 +2747,16 @@ static int lba_launch_t(orbx_ctx* ctx, const LbaPlan& L, int iters0, int iters1,
             if (G > 1) {
                 if (polled && it > 0)   // a launch per iteration: re-arm the arrival counter
                     ORBX_HIP_CHECK(hipMemsetAsync(X.bar, 0, 4, ctx->stream));
-                hipLaunchKernelGGL(k_lba_split<Rec>, dim3(G), dim3(kLbaThreads), L.lds_split_bytes, ctx->stream, dd, it,
-                                   n_it, L.lay, X);
+                if (coop) {
+                    int it_arg = it, n_arg = n_it;
+                    LbaLds lay = L.lay;
+                    void* args[] = {&dd, &it_arg, &n_arg, &lay, &X};
+                    ORBX_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lba_split<Rec>), dim3(G),
+                                                              dim3(kLbaThreads), args, L.lds_split_bytes, ctx->stream));
+                } else {
+                    hipLaunchKernelGGL(k_lba_split<Rec>, dim3(G), dim3(kLbaThreads), L.lds_split_bytes, ctx->stream,
+                                       dd, it, n_it, L.lay, X);
+                }
             } else {
                 hipLaunchKernelGGL(kern, dim3(P), dim3(kLbaThreads), lds, ctx->stream, dd, it, n_it, L.lay);
             }
@@ -2751,7 +2805,10 @@ static int lba_readback(orbx_ctx* ctx, const LbaPlan& L, orbx_ba_problem* probs,
     // point flags, offsets, outlier counts, per-pass statistics, failed flag
     ORBX_HIP_CHECK(hipMemcpyAsync(hb, d, L.base_bytes, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (*reinterpret_cast<const int*>(hb + L.o_failed)) return ORBX_ERR_HIP;   // a k_lba_split barrier timed out
+    // a k_lba_split barrier timed out: nothing is written back (the caller's
+    // arrays keep their input) and the callers below re-run on one workgroup
+    ctx->lba_split_timed_out = *reinterpret_cast<const int*>(hb + L.o_failed) != 0;
+    if (ctx->lba_split_timed_out) return ORBX_ERR_HIP;
     const int* nout = reinterpret_cast<const int*>(hb + L.o_nout);
     const LbaStatRec* sr = reinterpret_cast<const LbaStatRec*>(hb + L.o_stats);
     const uint8_t* all_st = hb + L.o_all_st;
@@ -2795,7 +2852,16 @@ static int lba_run(orbx_ctx* ctx, int P, orbx_ba_problem* probs, int iters0, int
     if (L.dev_end > ctx->scratch_bytes && (r = ensure_scratch(ctx, L.dev_end)) != ORBX_OK) return r;
     if ((r = lba_plan_stage(ctx, P, probs, static_cast<uint8_t*>(ctx->scratch), L)) != ORBX_OK) return r;
     if ((r = lba_launch(ctx, L, iters0, iters1, aborts)) != ORBX_OK) return r;
-    return lba_readback(ctx, L, probs, edge_status, point_bad, stats);
+    r = lba_readback(ctx, L, probs, edge_status, point_bad, stats);
+    if (r == ORBX_ERR_HIP && ctx->lba_split_timed_out && ctx->lba_split_fallback && !ctx->lba_force_single) {
+        // the split kernel's workgroups were not all resident (another
+        // context's kernels held the CUs): the same solve on one workgroup,
+        // restaged from the untouched input; same bits
+        ctx->lba_force_single = true;
+        r = lba_run(ctx, P, probs, iters0, iters1, aborts, edge_status, point_bad, stats);
+        ctx->lba_force_single = false;
+    }
+    return r;
 }
 
 // Device-resident form (orbx_lba_stage / _run / _fetch): the batch lives in
@@ -2859,6 +2925,8 @@ static int lba_run_resident(orbx_ctx* ctx, int iters0, int iters1, const volatil
 {
     if (!ctx->lba_res || ctx->lba_res->plan.P == 0) return ORBX_ERR_ARG;
     ctx_enter(ctx);
+    ctx->lba_res_iters[0] = iters0;
+    ctx->lba_res_iters[1] = iters1;
     LbaResident& R = *ctx->lba_res;
     const LbaPlan& L = R.plan;
     uint8_t* d = static_cast<uint8_t*>(R.dev);
@@ -3020,7 +3088,34 @@ int orbx_lba_fetch(orbx_ctx* ctx, orbx_ba_problem* problems, uint8_t* const* edg
             return ORBX_ERR_ARG;
     if (stats) std::memset(stats, 0, sizeof(*stats) * L.P);
     ctx_enter(ctx);
-    return orbx::lba_readback(ctx, L, problems, edge_status, point_bad, stats);
+    int r = orbx::lba_readback(ctx, L, problems, edge_status, point_bad, stats);
+    if (r == ORBX_ERR_HIP && ctx->lba_split_timed_out && ctx->lba_split_fallback) {
+        // a timed-out split run (orbx::lba_run's fallback): the staged batch
+        // again from its image on one workgroup, without abort polling
+        ctx->lba_force_single = true;
+        r = orbx::lba_run_resident(ctx, ctx->lba_res_iters[0], ctx->lba_res_iters[1], nullptr);
+        ctx->lba_force_single = false;
+        if (r == ORBX_OK) r = orbx::lba_readback(ctx, L, problems, edge_status, point_bad, stats);
+    }
+    return r;
 }
+
+/* Test hooks of the split kernel's residency handling: fail > 0 makes the
+ * barriers of the next `fail` split launches report a timeout; fallback 0
+ * turns the one-workgroup re-run off (the call then returns ORBX_ERR_HIP with
+ * the caller's arrays untouched); cap > 0 caps the residency capacity; coop
+ * -1 leaves the cooperative-launch choice to the device, 0 / 1 force it.
+ * Every argument < 0 (coop < -1) leaves that setting unchanged. */
+int orbx_debug_lba_split(orbx_ctx* ctx, int fail, int fallback, int cap, int coop)
+{
+    if (!ctx) return ORBX_ERR_ARG;
+    if (fail >= 0) ctx->lba_dbg_fail = fail;
+    if (fallback >= 0) ctx->lba_split_fallback = fallback != 0;
+    if (cap >= 0) ctx->lba_dbg_cap = cap;
+    if (coop >= -1) ctx->lba_split_coop = coop;
+    return ORBX_OK;
+}
+
+int orbx_lba_last_workgroups(const orbx_ctx* ctx) { return ctx ? ctx->lba_last_workgroups : ORBX_ERR_ARG; }
 
 }  // extern "C"

@@ -64,9 +64,6 @@ class StubContext:
     def set_async_match(self, enable):
         pass
 
-    def set_pyramid_mode(self, mode):
-        pass
-
     def nth_pivot(self):
         return self.ex.nth_pivot
 

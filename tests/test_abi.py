@@ -51,11 +51,6 @@ def test_context_setters_refuse_null_context():
     lib = ox.lib()
     err_arg = -1
     calls = [
-        ("orbx_dev_set_pyramid_mode", (None, 0)),
-        ("orbx_dev_pyramid_kind", (None,)),
-        ("orbx_dev_pyramid_fused", (None,)),
-        ("orbx_dev_set_fast_chunk", (None, 2)),
-        ("orbx_dev_get_fast_chunk", (None,)),
         ("orbx_set_nth_pivot", (None, 1)),
         ("orbx_get_nth_pivot", (None,)),
         ("orbx_dev_set_split", (None, 3)),
@@ -64,6 +59,8 @@ def test_context_setters_refuse_null_context():
         ("orbx_set_launch_mode", (None, 1)),
         ("orbx_lba_set_workgroups", (None, 4)),
         ("orbx_lba_get_workgroups", (None,)),
+        ("orbx_lba_last_workgroups", (None,)),
+        ("orbx_debug_lba_split", (None, 1, 0, 0, -1)),
         ("orbx_pose_set_exact", (None, 1)),
         ("orbx_pose_get_exact", (None,)),
         ("orbx_get_launch_mode", (None,)),

@@ -127,68 +127,31 @@ def test_large_batch_paths_match_oracle():
 
 
 @pytest.mark.parametrize("kind,w,h,n,seed", CASES)
-def test_pyramid_modes_identical(kind, w, h, n, seed):
-    """The staged launches (default), the fused pyramid + blur launch
-    (orbx_pyramid.hip) and the band-cascade pyramid give byte-identical padded
-    levels, keypoints and descriptors, on a two-frame batch (frame 1 flipped,
-    so the workgroups differ)."""
+def test_single_frame_cascade_pyramid_identical(kind, w, h, n, seed):
+    """orbx_extract's single-frame graph builds the raw pyramid as one
+    band-cascade launch (k_pyr_cascade, with FAST and the blur in one grid);
+    the batch path uses the staged per-level launches.  Both leave
+    byte-identical padded levels (raw and blurred) in slot 0 and the same
+    keypoints and descriptors."""
     img = make(kind, w, h, seed)
-    frames = np.stack([img, img[::-1].copy()])
     res = []
-    for mode in (0, 2, 1):
-        ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=2)
-        ctx.set_pyramid_mode(mode)
-        ctx.upload(frames)
-        ctx.extract(0, 2)
-        ctx.sync()
-        if mode == 1 and (w, h) in ((640, 480), (96, 80), (333, 251)):
-            assert ctx.pyramid_fused(), "fused pyramid plan expected for this size"
-        if mode != 1:
-            assert not ctx.pyramid_fused()
-        if mode == 2 and w % 16 == 0 and w <= 640:
-            assert ctx.pyramid_kind() == 2, "band cascade expected for this size"
-        if mode == 0:
-            assert ctx.pyramid_kind() == 0
-        res.append([(ctx.level(s, l), ctx.level(s, l, blurred=True)) for s in range(2) for l in range(8)]
-                   + [ctx.features(s) for s in range(2)])
+    for path in ("graph", "staged"):
+        ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=1)
+        if path == "graph":
+            feats = ctx(img)
+        else:
+            ctx.upload(img[None])
+            ctx.extract(0, 1)
+            ctx.sync()
+            feats = ctx.features(0)
+        res.append([(ctx.level(0, lv), ctx.level(0, lv, blurred=True)) for lv in range(8)] + [feats])
         ctx.close()
-    a = res[0]
-    for b in res[1:]:
-        for i in range(16):
-            assert np.array_equal(a[i][0], b[i][0]), f"raw slot {i // 8} level {i % 8}"
-            assert np.array_equal(a[i][1], b[i][1]), f"blurred slot {i // 8} level {i % 8}"
-        for i in (16, 17):
-            assert_kps_equal(a[i][0], b[i][0])
-            assert np.array_equal(a[i][1], b[i][1])
-
-
-@pytest.mark.parametrize("kind,w,h,n,seed", CASES)
-def test_fast_chunk_identical(kind, w, h, n, seed):
-    """Chunked FAST workgroups (orbx_dev_set_fast_chunk: several cells per
-    workgroup, the next tile prefetched with global_load_lds) give the same
-    keypoints and descriptors as one cell per workgroup, and both match the
-    oracle; a three-frame batch so the chunks cross cell rows and levels."""
-    img = make(kind, w, h, seed)
-    frames = np.stack([img, img[::-1].copy(), img[:, ::-1].copy()])
-    res = []
-    for chunk in (1, 2, 3, 8):
-        ctx = ox.Context(nfeatures=n, max_w=w, max_h=h, slots=3)
-        ctx.set_fast_chunk(chunk)
-        assert ctx.fast_chunk() == chunk
-        ctx.upload(frames)
-        ctx.extract(0, 3)
-        ctx.sync()
-        res.append([ctx.features(s) for s in range(3)])
-        ctx.close()
-    ref = RefExtractor(n)
-    for s in range(3):
-        kps, desc = ref(frames[s])
-        assert_kps_equal(res[0][s][0], kps)
-        assert np.array_equal(res[0][s][1], desc)
-    for r in res[1:]:
-        for s in range(3):
-            assert_kps_equal(r[s][0], res[0][s][0])
-            assert np.array_equal(r[s][1], res[0][s][1])
+    a, b = res
+    for lv in range(8):
+        assert np.array_equal(a[lv][0], b[lv][0]), f"raw level {lv}"
+        assert np.array_equal(a[lv][1], b[lv][1]), f"blurred level {lv}"
+    assert_kps_equal(a[8][0], b[8][0])
+    assert np.array_equal(a[8][1], b[8][1])
 
 
 @pytest.mark.parametrize("kind,w,h,n,seed", CASES)

@@ -21,10 +21,10 @@ pytestmark = pytest.mark.gpu
 
 
 def extract_both(ctx, img, stride=None):
-    """(keypoints, descriptors) of one call in each launch mode: graph with the
-    frame copied, graph reading the staged frame in place, stream launches."""
+    """(keypoints, descriptors) of one call in each launch mode: the captured
+    graph, the stream launches."""
     out = []
-    for mode in (1, 2, 3, 0):
+    for mode in (1, 0):
         ctx.set_launch_mode(mode)
         out.append(ctx(img) if stride is None else call_strided(ctx, img, stride))
     ctx.set_launch_mode(1)
@@ -81,8 +81,9 @@ def test_graph_call_after_size_change_and_with_stride():
 
 
 def test_graph_call_follows_configuration_switches():
-    """fp-contract mode, nth_element era and pyramid mode changes re-capture:
-    each result equals the oracle of the same configuration."""
+    """fp-contract mode and nth_element era changes re-capture: each result
+    equals the oracle of the same configuration; launch modes outside 0..1
+    are refused."""
     img = synth.noise_frame(640, 480, 21)
     ctx = ox.Context(nfeatures=1000, max_w=640, max_h=480, slots=1)
     assert same(ctx(img), RefExtractor(1000)(img))
@@ -92,11 +93,12 @@ def test_graph_call_follows_configuration_switches():
     ctx.set_fp_contract(1)
     assert same(ctx(img), RefExtractor(1000, variant="contract")(img))
     ctx.set_fp_contract(0)
-    for mode in (1, 2, 0):
-        ctx.set_pyramid_mode(mode)
-        for lm in (1, 2, 3):
-            ctx.set_launch_mode(lm)
-            assert same(ctx(img), RefExtractor(1000)(img)), (mode, lm)
+    for lm in (1, 0, 1):
+        ctx.set_launch_mode(lm)
+        assert same(ctx(img), RefExtractor(1000)(img)), lm
+    for bad in (2, 3, -1):
+        assert ox.lib().orbx_set_launch_mode(ctx.handle, bad) == -1
+    assert ctx.launch_mode() == 1
     ctx.close()
 
 
@@ -109,7 +111,7 @@ def test_graph_call_empty_and_capacity():
     L = ox.lib()
     n = ctypes.c_int(-1)
     assert L.orbx_extract(ctx.handle, None, 0, 0, 0, None, None, 0, ctypes.byref(n)) == 0 and n.value == 0
-    for mode in (1, 2, 3, 0):
+    for mode in (1, 0):
         ctx.set_launch_mode(mode)
         kps = np.zeros(10, ox.KEYPOINT)
         desc = np.zeros((10, 32), np.uint8)

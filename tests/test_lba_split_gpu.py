@@ -96,3 +96,112 @@ def test_workgroup_setting_validates():
     assert ox.lib().orbx_lba_set_workgroups(c.handle, 16) == 0
     assert ox.lib().orbx_lba_get_workgroups(c.handle) == 16
     c.close()
+
+
+def _hooks(ctx, fail=0, fallback=1, cap=0, coop=-1):
+    assert ox.lib().orbx_debug_lba_split(ctx.handle, fail, fallback, cap, coop) == 0
+
+
+def test_split_capped_at_device_capacity(ctx):
+    """The grid barrier needs every workgroup resident: the count is capped
+    at the kernel's capacity (occupancy x CUs, here capped by the test hook
+    as on a partitioned device), with the same bits."""
+    prob = sb.make_problem(n_kf=12, n_points=900, seed=43)
+    one = solve(ctx, prob, 1)
+    assert ox.lib().orbx_lba_last_workgroups(ctx.handle) == 1
+    try:
+        _hooks(ctx, cap=5)
+        same_bits(solve(ctx, prob, 64), one)
+        assert ox.lib().orbx_lba_last_workgroups(ctx.handle) == 5
+        _hooks(ctx, cap=1)   # nothing co-resident beyond one: the one-workgroup kernel
+        same_bits(solve(ctx, prob, 64), one)
+        assert ox.lib().orbx_lba_last_workgroups(ctx.handle) == 1
+        _hooks(ctx, cap=0)   # the device's own capacity: the largest setting fits or is capped
+        same_bits(solve(ctx, prob, 256), one)
+        g = ox.lib().orbx_lba_last_workgroups(ctx.handle)
+        assert 2 <= g <= 256
+    finally:
+        _hooks(ctx, cap=0)
+
+
+@pytest.mark.parametrize("coop", [0, 1])
+def test_split_plain_and_cooperative_launch(ctx, coop):
+    prob = sb.make_problem(n_kf=10, n_points=600, seed=44, outlier_frac=0.03)
+    one = solve(ctx, prob, 1)
+    try:
+        _hooks(ctx, coop=coop)
+        same_bits(solve(ctx, prob, 0), one)
+        assert ox.lib().orbx_lba_last_workgroups(ctx.handle) > 1
+    finally:
+        _hooks(ctx, coop=-1)
+
+
+def test_split_barrier_timeout_falls_back_to_one_workgroup(ctx):
+    """A barrier that times out (workgroups not all resident) makes the call
+    run the same solve again on one workgroup: the result equals the
+    one-workgroup solve bit for bit."""
+    prob = sb.make_problem(n_kf=12, n_points=900, seed=45)
+    one = solve(ctx, prob, 1)
+    try:
+        _hooks(ctx, fail=1)
+        same_bits(solve(ctx, prob, 0), one)
+        assert ox.lib().orbx_lba_last_workgroups(ctx.handle) == 1
+        # the hook is spent: the next solve splits again
+        same_bits(solve(ctx, prob, 0), one)
+        assert ox.lib().orbx_lba_last_workgroups(ctx.handle) > 1
+    finally:
+        _hooks(ctx, fail=0)
+
+
+def test_split_barrier_timeout_without_fallback_leaves_problem_untouched(ctx):
+    """With the re-run off the timed-out call returns ORBX_ERR_HIP and
+    writes nothing back: poses, points and the output flags keep their
+    input values."""
+    prob = sb.make_problem(n_kf=12, n_points=900, seed=46)
+    assert ox.lib().orbx_lba_set_workgroups(ctx.handle, 0) == 0
+    p, arrs = sb.to_ctypes(prob)
+    es = np.full(p.n_edges, 7, np.uint8)
+    pb = np.full(p.n_points, 7, np.uint8)
+    st = sb.BAStats()
+    try:
+        _hooks(ctx, fail=1, fallback=0)
+        r = ox.lib().orbx_lba_solve(ctx.handle, ctypes.byref(p), 5, 10, None, es.ctypes.data, pb.ctypes.data,
+                                    ctypes.byref(st))
+        assert r == -2
+    finally:
+        _hooks(ctx, fail=0, fallback=1)
+    for key in ("pose_q", "pose_t", "points"):
+        assert np.array_equal(arrs[key], np.asarray(prob[key])), key
+    assert (es == 7).all() and (pb == 7).all()
+    # the context is usable afterwards
+    same_bits(solve(ctx, prob, 0), solve(ctx, prob, 1))
+
+
+def test_split_resident_timeout_falls_back(ctx):
+    """orbx_lba_stage / _run / _fetch of one problem (the split kernel) with
+    a timed-out barrier: the fetch re-runs the staged problem on one
+    workgroup."""
+    prob = sb.make_problem(n_kf=12, n_points=900, seed=47)
+    one = solve(ctx, prob, 1)
+    L = ox.lib()
+    assert L.orbx_lba_set_workgroups(ctx.handle, 0) == 0
+    p, arrs = sb.to_ctypes(prob)
+    arr = (sb.BAProblem * 1)(p)
+    es = np.zeros(p.n_edges, np.uint8)
+    pb = np.zeros(p.n_points, np.uint8)
+    esp = (ctypes.c_void_p * 1)(es.ctypes.data)
+    pbp = (ctypes.c_void_p * 1)(pb.ctypes.data)
+    st = (sb.BAStats * 1)()
+    try:
+        _hooks(ctx, fail=1)
+        assert L.orbx_lba_stage(ctx.handle, 1, arr) == 0
+        assert L.orbx_lba_run(ctx.handle, 5, 10, None) == 0
+        assert L.orbx_lba_fetch(ctx.handle, arr, esp, pbp, st) == 0
+    finally:
+        _hooks(ctx, fail=0)
+    same_bits((arrs, es, pb, st[0]), one)
+
+
+def test_debug_split_hook_validates():
+    assert ox.lib().orbx_debug_lba_split(None, 1, 0, 0, -1) == -1
+    assert ox.lib().orbx_lba_last_workgroups(None) == -1

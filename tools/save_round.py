@@ -44,6 +44,8 @@ for wl in ("c2", "c3"):   # `bench.py --serial` profiles (tools/collect_round.sh
     sq = one(f"{wl}_serial_prof/sq/**/*counter_collection.csv")
     with open(dst / f"{tag}_{wl}_serial_pmc_hbm.json", "w") as f:
         subprocess.run([sys.executable, str(ROOT / "tools/pmc_summary.py"), fetch, write, sq], stdout=f, check=True)
-    with open(dst / f"{tag}_{wl}_serial_pmc_sq.txt", "w") as f:
-        subprocess.run([sys.executable, str(ROOT / "tools/pmc_table.py"), sq], stdout=f, check=True)
+    with open(dst / f"{tag}_{wl}_serial_pmc_sq.txt", "w") as f:   # per dispatch and per frame
+        frames = "1024" if wl == "c2" else "128"
+        subprocess.run([sys.executable, str(ROOT / "tools/pmc_table.py"), sq, "--frames", frames], stdout=f,
+                       check=True)
 print("saved", tag)

@@ -8,7 +8,7 @@ repo root on the GPU box, under `rocprofv3 --kernel-trace --memory-copy-trace
   pose      orbx_pose_optimization on one frame
   lba       orbx_lba_solve on one 20 KF x 2000 MP problem
 
-usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N] [--pyr m,...] [--lbawg g,...]
+usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N] [--lbawg g,...] [--coop c,...]
 """
 import ctypes
 import sys
@@ -26,8 +26,9 @@ from orb_slam_amd import synth  # noqa: E402
 args = sys.argv[1:]
 n = int(args[args.index("--n") + 1]) if "--n" in args else 100
 what = [a for a in args if a in ("extract", "sfi", "pose", "lba")] or ["extract"]
-pyr = [int(v) for v in args[args.index("--pyr") + 1].split(",")] if "--pyr" in args else [0]
 lbawg = [int(v) for v in args[args.index("--lbawg") + 1].split(",")] if "--lbawg" in args else [0]
+# k_lba_split launch: -1 the device's choice, 0 plain, 1 cooperative (orbx_debug_lba_split)
+coop = [int(v) for v in args[args.index("--coop") + 1].split(",")] if "--coop" in args else [-1]
 L = ox.lib()
 
 
@@ -52,12 +53,9 @@ if "extract" in what or "sfi" in what:
                               desc.ctypes.data, 1000, ctypes.byref(nk)) == 0
 
     if "extract" in what:
-        for pm in pyr:
-            ctx.set_pyramid_mode(pm)
-            for mode in (1, 2, 3, 0):
-                ctx.set_launch_mode(mode)
-                print(f"extract pyramid mode {pm} launch mode {mode}: {med(ext, n):.4f} ms median", flush=True)
-        ctx.set_pyramid_mode(0)
+        for mode in (1, 0):
+            ctx.set_launch_mode(mode)
+            print(f"extract launch mode {mode}: {med(ext, n):.4f} ms median", flush=True)
         ctx.set_launch_mode(1)
     if "sfi" in what:
         feats = [ctx(frames[i]) for i in range(2)]
@@ -106,8 +104,12 @@ if "lba" in what:
         assert L.orbx_lba_solve(ctx.handle, ctypes.byref(p), 5, 10, None, es.ctypes.data, pb.ctypes.data,
                                 ctypes.byref(st)) == 0
 
-    for wg in lbawg:
-        assert L.orbx_lba_set_workgroups(ctx.handle, wg) == 0
-        print(f"lba workgroups {wg}: {med(lba, max(5, n // 10)):.4f} ms median", flush=True)
+    for cp in coop:
+        assert L.orbx_debug_lba_split(ctx.handle, -1, -1, -1, cp) == 0
+        for wg in lbawg:
+            assert L.orbx_lba_set_workgroups(ctx.handle, wg) == 0
+            t = med(lba, max(5, n // 10))
+            print(f"lba coop {cp} workgroups {wg} (ran {L.orbx_lba_last_workgroups(ctx.handle)}): {t:.4f} ms median",
+                  flush=True)
     ctx.close()
 print("ok")
