@@ -699,9 +699,11 @@ int orbx_lba_solve(orbx_ctx* ctx, orbx_ba_problem* p, int iters0, int iters1,
  * The workgroups of one problem meet at grid barriers, so they must all be
  * resident at once: the count is capped at what the device holds of that
  * kernel (occupancy x CUs: a partitioned device, or a setting of 256, gets
- * fewer), the launch is cooperative where the device supports it, and a
- * solve whose barrier still times out (another context's kernels holding
- * the CUs) is run again on one workgroup -- same bits, longer call. */
+ * fewer), and a solve whose barrier still times out (another context's
+ * kernels holding the CUs) is run again on one workgroup -- same bits,
+ * longer call.  (A cooperative launch, available through
+ * orbx_debug_lba_split, gives the same bits but measured to delay other
+ * contexts' calls beside it.) */
 int orbx_lba_set_workgroups(orbx_ctx* ctx, int n);
 int orbx_lba_get_workgroups(const orbx_ctx* ctx);
 /* Workgroups the last local-BA launch of ctx ran with (after the cap and any
@@ -710,7 +712,8 @@ int orbx_lba_last_workgroups(const orbx_ctx* ctx);
 /* Test hooks of that residency handling (fail: the next n split launches
  * see a barrier timeout; fallback 0: no re-run, ORBX_ERR_HIP with the
  * caller's arrays untouched; cap > 0: capacity capped; coop -1 / 0 / 1:
- * device choice / plain / cooperative launch; negative = unchanged). */
+ * the device's choice / plain (default) / cooperative launch; arguments
+ * below those ranges leave the setting unchanged). */
 int orbx_debug_lba_split(orbx_ctx* ctx, int fail, int fallback, int cap, int coop);
 
 /* Batched throughput form: P independent problems, one workgroup each.

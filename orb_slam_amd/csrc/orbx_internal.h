@@ -297,16 +297,18 @@ struct orbx_ctx {
     size_t lba_split_bytes = 0;
     // k_lba_split's grid barrier needs all G workgroups resident at once:
     // G is clamped to the device's capacity for the kernel (occupancy query
-    // x CUs, cached per record type and LDS size), the launch is cooperative
-    // where the device supports it, and a solve whose barrier timed out
-    // (bar[1]) is run again on one workgroup (lba_split_fallback)
+    // x CUs, cached per record type and LDS size), and a solve whose barrier
+    // timed out (bar[1]) is run again on one workgroup (lba_split_fallback).
+    // Plain launches by default: a cooperative launch gave the same bits but
+    // delayed the other threads' contexts (LoopClosing's calls 0.22 -> 0.51
+    // ms beside a local BA, tests/test_threads_gpu.py)
     int lba_split_cap[2] = {0, 0};
     size_t lba_split_cap_lds[2] = {0, 0};
     int lba_last_workgroups = 0;        // G of the last launch (after clamping and fallback)
     bool lba_force_single = false;      // the fallback re-run in progress
     bool lba_split_timed_out = false;   // set by lba_readback
     bool lba_split_fallback = true;     // orbx_debug_lba_split: off = return ORBX_ERR_HIP instead
-    int lba_split_coop = -1;            // -1: the device attribute decides; 0 / 1 forced
+    int lba_split_coop = 0;             // 1: cooperative launch (-1: where the device offers it)
     int lba_dbg_fail = 0;               // test hook: split launches whose barrier is made to time out
     int lba_dbg_cap = 0;                // test hook: > 0 caps the residency capacity
     int lba_res_iters[2] = {0, 0};      // the resident batch's last run (the fallback re-runs it)

@@ -191,134 +191,6 @@ struct SearchArgs {
     int32_t* fr_count;            // points in view
 };
 
-// ORBmatcher::WindowSearch (src/ORBmatcher.cc:409-516)
-__global__ __launch_bounds__(64) void k_window_search(SearchArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    CandTab t;
-    carve_tab(smem, a.F2.n, t);
-    signed char* bins = reinterpret_cast<signed char*>(t.taken + a.F2.n);
-    int* keys = reinterpret_cast<int*>(bins + ((a.F2.n + 15) & ~15));
-    int* hist = keys + a.F2.n;
-    fill_tab(a.F2, nullptr, t);
-    const bool bMin = a.min_level > 0, bMax = a.max_level < 0x7fffffff;
-    int nmatches = 0, npushed = 0;
-    for (int i1 = 0; i1 < a.F1.n; i1++) {
-        if (!a.q_valid[i1]) continue;
-        const orbx_keypoint k1 = a.F1.kps[i1];
-        const int level1 = k1.octave;
-        if (bMin && level1 < a.min_level) continue;
-        if (bMax && level1 > a.max_level) continue;
-        const float r = (float)a.window;
-        const AreaQuery q = area_cells(a.F2, k1.x, k1.y, r);
-        if (q.empty) continue;
-        uint4 d1a, d1b;
-        load_desc(a.F1.desc + (size_t)i1 * 32, d1a, d1b);
-        const Best2 b = eval_query(t, a.F2.n, q, k1.x, k1.y, r, level_filter(level1, level1), d1a, d1b, a.F2.desc);
-        if (!b.any) continue;
-        const int bestDist = key_dist(b.best), bestDist2 = key_dist(b.second), bestIdx2 = key_idx(b.best);
-        if ((float)bestDist <= __fmul_rn((float)bestDist2, a.nnratio) && bestDist <= kTHHigh) {
-            if (threadIdx.x == 0) {
-                t.taken[bestIdx2] = i1;
-                a.out[bestIdx2] = i1;
-                bins[npushed] = (signed char)rot_bin(k1.angle, a.F2.kps[bestIdx2].angle);
-                keys[npushed] = bestIdx2;
-            }
-            npushed++;
-            nmatches++;
-            wave_sync();
-        }
-    }
-    wave_sync();
-    if (threadIdx.x == 0) {
-        if (a.check_ori) nmatches -= rotation_filter(bins, keys, npushed, a.out, hist);
-        *a.out_n = nmatches;
-    }
-}
-
-// ORBmatcher::SearchByProjection(Frame&, Frame&, int, vector<MapPoint*>&)
-// (src/ORBmatcher.cc:519-594)
-__global__ __launch_bounds__(64) void k_proj_pair(SearchArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    CandTab t;
-    carve_tab(smem, a.F2.n, t);
-    fill_tab(a.F2, a.f2_assigned, t);
-    int nmatches = 0;
-    for (int i1 = 0; i1 < a.F1.n; i1++) {
-        if (!a.q_valid[i1]) continue;
-        const int level1 = a.F1.kps[i1].octave;
-        float u, v, zc;
-        project(a.T, a.cam, a.q_xyz + 3 * i1, &u, &v, &zc);
-        const float r = (float)a.window;
-        const AreaQuery q = area_cells(a.F2, u, v, r);
-        if (q.empty) continue;
-        uint4 d1a, d1b;
-        load_desc(a.F1.desc + (size_t)i1 * 32, d1a, d1b);
-        const Best2 b = eval_query(t, a.F2.n, q, u, v, r, level_filter(level1, level1), d1a, d1b, a.F2.desc);
-        if (!b.any) continue;
-        const int bestDist = key_dist(b.best), bestDist2 = key_dist(b.second), bestIdx2 = key_idx(b.best);
-        if ((float)bestDist <= __fmul_rn((float)bestDist2, a.nnratio) && bestDist <= kTHHigh) {
-            if (threadIdx.x == 0) {
-                t.taken[bestIdx2] = i1;
-                a.out[bestIdx2] = i1;
-            }
-            nmatches++;
-            wave_sync();
-        }
-    }
-    if (threadIdx.x == 0) *a.out_n = nmatches;
-}
-
-// ORBmatcher::SearchByProjection(Frame& Current, const Frame& Last, float th)
-// (src/ORBmatcher.cc:1507-1620).  F1 = LastFrame, F2 = CurrentFrame.
-__global__ __launch_bounds__(64) void k_proj_motion(SearchArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    CandTab t;
-    carve_tab(smem, a.F2.n, t);
-    signed char* bins = reinterpret_cast<signed char*>(t.taken + a.F2.n);
-    int* keys = reinterpret_cast<int*>(bins + ((a.F2.n + 15) & ~15));
-    int* hist = keys + a.F2.n;
-    fill_tab(a.F2, a.f2_assigned, t);
-    int nmatches = 0, npushed = 0;
-    for (int i = 0; i < a.F1.n; i++) {
-        if (!a.q_valid[i]) continue;
-        float u, v, zc;
-        project(a.T, a.cam, a.q_xyz + 3 * i, &u, &v, &zc);
-        if (u < a.F2.min_x || u > a.F2.max_x) continue;
-        if (v < a.F2.min_y || v > a.F2.max_y) continue;
-        const orbx_keypoint kl = a.F1.kps[i];
-        const int oct = kl.octave;
-        const float radius = __fmul_rn(a.th, a.scale[oct]);
-        const AreaQuery q = area_cells(a.F2, u, v, radius);
-        if (q.empty) continue;
-        uint4 d1a, d1b;
-        load_desc(a.F1.desc + (size_t)i * 32, d1a, d1b);
-        const Best2 b = eval_query(t, a.F2.n, q, u, v, radius, level_filter(oct - 1, oct + 1), d1a, d1b, a.F2.desc);
-        if (!b.any) continue;
-        const int bestDist = key_dist(b.best), bestIdx2 = key_idx(b.best);
-        if (bestDist <= kTHHigh) {
-            if (threadIdx.x == 0) {
-                t.taken[bestIdx2] = i;
-                a.out[bestIdx2] = i;
-                if (a.check_ori) {
-                    bins[npushed] = (signed char)rot_bin(kl.angle, a.F2.kps[bestIdx2].angle);
-                    keys[npushed] = bestIdx2;
-                }
-            }
-            if (a.check_ori) npushed++;
-            nmatches++;
-            wave_sync();
-        }
-    }
-    wave_sync();
-    if (threadIdx.x == 0) {
-        if (a.check_ori) nmatches -= rotation_filter(bins, keys, npushed, a.out, hist);
-        *a.out_n = nmatches;
-    }
-}
-
 // ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, float)
 // (src/ORBmatcher.cc:49-125) with RadiusByViewingCos (:127-133).
 __device__ inline void proj_local_wave(const SearchArgs& a, uint8_t* smem)
@@ -358,10 +230,505 @@ __device__ inline void proj_local_wave(const SearchArgs& a, uint8_t* smem)
     if (threadIdx.x == 0) *a.out_n = nmatches;
 }
 
-__global__ __launch_bounds__(64) void k_proj_local(SearchArgs a)
+// ---------------------------------------------------------------------------
+// Two-phase form of the greedy window / projection searches (the calls
+// Tracking makes per frame: WindowSearch :409-516, SearchByProjection
+// :1507-1620 (motion), :519-594 (pair), :49-125 (local map)).
+//
+// The one-wave kernels above scan every candidate of the searched frame for
+// every query, twice, in the reference's sequential order: ~5 us per query.
+// But the only state a query reads from the earlier ones is which candidates
+// are taken (`if(F.mvpMapPoints[i2]) continue`).  So:
+//  1. k_area_lists (state-free, one wave per query across the chip): the
+//     query's area, level filter and candidate keys (distance, then
+//     GetFeaturesInArea order: cell x, cell y, index) -- the list sorted
+//     when it holds <= 64 keys, else in index order;
+//  2. k_area_replay (one wave, sequential): per query the first two
+//     admissible (untaken) keys of the sorted list -- one LDS lookup and
+//     one ballot -- or wave minima over a longer list; a list that
+//     overflowed its slot is evaluated in full as before.  Then each
+//     search's own acceptance rule, the `taken` update and the rotation
+//     filter, exactly as the one-wave kernels.
+// Best and second are the same keys eval_query finds (the minimum key, and
+// the minimum over the others), so the results are identical.
+// ---------------------------------------------------------------------------
+enum QueryKind { kQWindow = 0, kQPair = 1, kQMotion = 2, kQLocal = 3 };
+constexpr int kAreaListWaves = 16;
+constexpr int kAreaCap = 128;   // list entries per query (dist << 16 | index)
+
+struct QuerySetup {
+    bool active;
+    float qx, qy, r;
+    AreaQuery q;
+    LevelFilter lf;
+    const uint8_t* desc;
+};
+
+// The reference's per-query preamble of each search, up to
+// GetFeaturesInArea.  nq: queries of the search.
+template <int K>
+__device__ inline int query_count(const SearchArgs& a)
+{
+    return K == kQLocal ? a.nq : a.F1.n;
+}
+
+template <int K>
+__device__ inline QuerySetup query_setup(const SearchArgs& a, int i)
+{
+    QuerySetup s;
+    s.active = false;
+    s.qx = s.qy = s.r = 0.f;
+    s.desc = nullptr;
+    if (!a.q_valid[i]) return s;
+    if constexpr (K == kQWindow) {
+        const orbx_keypoint k1 = a.F1.kps[i];
+        const int level1 = k1.octave;
+        if (a.min_level > 0 && level1 < a.min_level) return s;
+        if (a.max_level < 0x7fffffff && level1 > a.max_level) return s;
+        s.qx = k1.x;
+        s.qy = k1.y;
+        s.r = (float)a.window;
+        s.lf = level_filter(level1, level1);
+        s.desc = a.F1.desc + (size_t)i * 32;
+    } else if constexpr (K == kQPair) {
+        const int level1 = a.F1.kps[i].octave;
+        float zc;
+        project(a.T, a.cam, a.q_xyz + 3 * i, &s.qx, &s.qy, &zc);
+        s.r = (float)a.window;
+        s.lf = level_filter(level1, level1);
+        s.desc = a.F1.desc + (size_t)i * 32;
+    } else if constexpr (K == kQMotion) {
+        float zc;
+        project(a.T, a.cam, a.q_xyz + 3 * i, &s.qx, &s.qy, &zc);
+        if (s.qx < a.F2.min_x || s.qx > a.F2.max_x) return s;
+        if (s.qy < a.F2.min_y || s.qy > a.F2.max_y) return s;
+        const int oct = a.F1.kps[i].octave;
+        s.r = __fmul_rn(a.th, a.scale[oct]);
+        s.lf = level_filter(oct - 1, oct + 1);
+        s.desc = a.F1.desc + (size_t)i * 32;
+    } else {
+        const int pred = a.pred_level[i];
+        float r = ((double)a.view_cos[i] > 0.998) ? 2.5f : 4.0f;
+        if (a.th != 1.0f) r = __fmul_rn(r, a.th);
+        s.r = __fmul_rn(r, a.scale[pred]);
+        s.qx = a.proj_xy[2 * i];
+        s.qy = a.proj_xy[2 * i + 1];
+        s.lf = level_filter(pred - 1, pred);
+        s.desc = a.q_desc + (size_t)i * 32;
+    }
+    s.q = area_cells(a.F2, s.qx, s.qy, s.r);
+    s.active = !s.q.empty;
+    return s;
+}
+
+// LDS of k_area_lists: per searched keypoint x, y and code (cx | cy << 8 |
+// octave << 16, -1 outside the grid), then a 64-key sort buffer per wave
+__host__ __device__ inline size_t area_lists_lds(int n2) { return (size_t)((n2 * 12 + 15) & ~15) + kAreaListWaves * 64 * 8; }
+
+// grid.x: groups of kAreaListWaves queries; grid.y: job.  cnt[i]: -1 for a
+// query the preamble skips, else its candidate count (admissible before
+// `taken`; 0 = GetFeaturesInArea empty).
+template <int K>
+__global__ __launch_bounds__(kAreaListWaves * 64) void k_area_lists(const SearchArgs* jobs, int cap_q,
+                                                                    uint32_t* lists_all, int32_t* cnt_all)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    proj_local_wave(a, smem);
+    const SearchArgs& a = jobs[blockIdx.y];
+    const int nq = query_count<K>(a);
+    if ((int)blockIdx.x * kAreaListWaves >= nq) return;   // uniform
+    if constexpr (K == kQLocal) {   // after k_frustum (fr_count set): no point in view, the replay skips the job
+        if (a.fr_count && *a.fr_count == 0) return;
+    }
+    const FrameDev& F2 = a.F2;
+    const int n2 = F2.n;
+    float* sx = reinterpret_cast<float*>(smem);
+    float* sy = sx + n2;
+    int* scode = reinterpret_cast<int*>(sy + n2);
+    unsigned long long* sortbuf = reinterpret_cast<unsigned long long*>(smem + ((n2 * 12 + 15) & ~15));
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int j = tid; j < n2; j += kAreaListWaves * 64) {
+        const orbx_keypoint k = F2.kps[j];
+        const int cell = grid_cell(F2, k.x, k.y);
+        sx[j] = k.x;
+        sy[j] = k.y;
+        scode[j] = cell < 0 ? -1 : ((cell / kGridRows) | ((cell % kGridRows) << 8) | (k.octave << 16));
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kAreaListWaves + wv;
+    if (i >= nq) return;   // whole waves; no barrier below
+    uint32_t* lists = lists_all + (size_t)blockIdx.y * cap_q * kAreaCap;
+    int32_t* cnt = cnt_all + (size_t)blockIdx.y * cap_q;
+    const QuerySetup s = query_setup<K>(a, i);
+    int n = -1;
+    if (s.active) {
+        uint4 d1a, d1b;
+        load_desc(s.desc, d1a, d1b);
+        unsigned long long* sb = sortbuf + 64 * wv;
+        uint32_t* out = lists + (size_t)i * kAreaCap;
+        const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        n = 0;
+        for (int j0 = 0; j0 < n2; j0 += 64) {
+            const int j = j0 + lane;
+            bool ok = false;
+            int cx = 0, cy = 0;
+            if (j < n2) {
+                const int code = scode[j];
+                cx = code & 0xFF;
+                cy = (code >> 8) & 0xFF;
+                ok = code >= 0 && level_ok(s.lf, code >> 16) && cx >= s.q.min_cx && cx <= s.q.max_cx &&
+                     cy >= s.q.min_cy && cy <= s.q.max_cy && !(fabsf(__fsub_rn(sx[j], s.qx)) > s.r) &&
+                     !(fabsf(__fsub_rn(sy[j], s.qy)) > s.r);
+            }
+            const unsigned long long bal = __ballot(ok);
+            if (ok) {
+                uint4 a2, b2;
+                load_desc(F2.desc + (size_t)j * 32, a2, b2);
+                const uint32_t dist = (uint32_t)hamming256(d1a, d1b, a2, b2);
+                const int pos = n + __popcll(bal & lt_mask);
+                if (pos < 64)
+                    sb[pos] = ((unsigned long long)dist << 32) |
+                              ((unsigned long long)(cx * kGridRows + cy) << 12) | (unsigned long long)j;
+                if (pos < kAreaCap) out[pos] = dist << 16 | (uint32_t)j;   // index order
+            }
+            n += __popcll(bal);
+        }
+        if (n > 1 && n <= 64) {   // sorted by key: each lane's rank
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const unsigned long long mine = lane < n ? sb[lane] : ~0ull;
+            int rank = 0;
+            for (int k = 0; k < n; k++) {
+                const unsigned long long o =
+                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(mine >> 32), k) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, k);
+                rank += o < mine;
+            }
+            if (lane < n) out[rank] = (uint32_t)(mine >> 32) << 16 | (uint32_t)(mine & 0xFFF);
+        }
+    }
+    if (lane == 0) cnt[i] = n;
+}
+
+// The greedy resolution, in parallel rounds.  A query's result depends on
+// the earlier queries only through the candidates they took, so with
+//   R_t(i) = query i decided with the candidates that queries k < i took
+//            in round t - 1 excluded (claim_{t-1}[j] < i),
+//   claim_t[j] = the smallest query that takes j in round t,
+// round t reproduces the sequential result for every query whose earlier
+// queries were already right in round t - 1 (query 0 always is), and the
+// rounds reach the sequential result -- its unique fixed point -- when no
+// query changes.  Conflicts (two queries wanting one candidate) are rare, so
+// that takes a few rounds of all queries at once instead of nq dependent
+// steps of one wave; after kMaxRounds the sequential replay takes over.
+//
+// One workgroup per job (16 waves): the candidate table, the searched
+// keypoints' angles, every query's count / short list (<= 64 keys, up to an
+// LDS budget; the rest stay in global memory) and angle are staged first.
+constexpr int kReplayThreads = 1024;
+constexpr int kReplayWaves = kReplayThreads / 64;
+constexpr int kReplayEntries = 8192;   // short-list entries staged in LDS (32 KB), at most
+constexpr int kMaxRounds = 24;
+// rounds used and sequential fallbacks, summed over replays (orbx_debug_area_rounds)
+__device__ unsigned long long g_area_rounds[2];
+// LDS: table (x, y, cell_oct, taken), bins, keys, hist, angles, two claim
+// arrays; per query count, offset, angle, state (nq_lds of them: 0 when the
+// per-query arrays live in global memory); ent_cap short-list entries
+__host__ __device__ inline size_t area_replay_lds(int n2, int nq_lds, int ent_cap)
+{
+    return (size_t)n2 * 16 + ((n2 + 15) & ~15) + (size_t)n2 * 4 + 48 * 4 + (size_t)n2 * 4 + (size_t)n2 * 8 +
+           (size_t)nq_lds * 20 + (size_t)ent_cap * 4;
+}
+
+// qglob: per job 5 cap_q ints (count, offset, angle, state, long-list
+// queries) when the per-query arrays do not fit LDS (q_lds 0), else unused
+template <int K>
+__global__ __launch_bounds__(kReplayThreads) void k_area_replay(const SearchArgs* jobs, int cap_q,
+                                                                const uint32_t* lists_all, const int32_t* cnt_all,
+                                                                int q_lds, int ent_cap, int* qglob)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ BlockScratchN<kReplayWaves> bs, bs2;
+    __shared__ int s_changed[2], s_removed;
+    const SearchArgs& a = jobs[blockIdx.x];
+    if constexpr (K == kQLocal) {
+        if (a.fr_count && *a.fr_count == 0) {
+            if (threadIdx.x == 0) *a.out_n = 0;
+            return;
+        }
+    }
+    const int n2 = a.F2.n, nq = query_count<K>(a), tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    CandTab t;
+    carve_tab(smem, n2, t);
+    signed char* bins = reinterpret_cast<signed char*>(t.taken + n2);
+    int* keys = reinterpret_cast<int*>(bins + ((n2 + 15) & ~15));
+    int* hist = keys + n2;
+    float* ang2 = reinterpret_cast<float*>(hist + 48);
+    int* claim0 = reinterpret_cast<int*>(ang2 + n2);
+    int* claim1 = claim0 + n2;
+    int* qbase = q_lds ? claim1 + n2 : qglob + (size_t)blockIdx.x * 5 * cap_q;
+    int* q_cnt = qbase;
+    int* q_off = q_cnt + cap_q;                                // entry offset of the short list, -1: global
+    float* q_ang = reinterpret_cast<float*>(q_off + cap_q);
+    int* q_state = reinterpret_cast<int*>(q_ang + cap_q);      // accepted candidate, or -1
+    int* q_long = q_state + cap_q;                             // the queries with more than 64 candidates
+    uint32_t* ent = reinterpret_cast<uint32_t*>(claim1 + n2 + (q_lds ? 5 * cap_q : 0));
+    const uint32_t* lists = lists_all + (size_t)blockIdx.x * cap_q * kAreaCap;
+    const int32_t* cnt = cnt_all + (size_t)blockIdx.x * cap_q;
+    constexpr bool kRot = K == kQWindow || K == kQMotion;
+    constexpr int kBig = 0x7fffffff;
+    for (int i = tid; i < n2; i += kReplayThreads) {
+        const orbx_keypoint k = a.F2.kps[i];
+        ang2[i] = k.angle;
+        t.x[i] = k.x;
+        t.y[i] = k.y;
+        const int cell = grid_cell(a.F2, k.x, k.y);
+        t.cell_oct[i] = (cell & 0xFFFF) | (k.octave << 16);
+        t.taken[i] = (a.f2_assigned && a.f2_assigned[i]) ? -2 : -1;
+        claim0[i] = kBig;
+    }
+    // short lists into LDS: block prefix over the queries (in chunks of the
+    // block), while the budget lasts
+    int used = 0, nlong = 0;
+    for (int q0 = 0; q0 < nq; q0 += kReplayThreads) {
+        const int i = q0 + tid;
+        const int c = i < nq ? cnt[i] : -1;
+        const int w = (c > 0 && c <= 64) ? c : 0;
+        int total, tl;
+        const int off = used + block_exclusive_scan(w, &total, bs, (q0 / kReplayThreads) & 1);
+        const int pl = nlong + block_exclusive_scan(c > 64 ? 1 : 0, &tl, bs2, (q0 / kReplayThreads) & 1);
+        if (c > 64) q_long[pl] = i;
+        nlong += tl;
+        if (i < nq) {
+            const bool fits = w > 0 && off + w <= ent_cap;
+            q_cnt[i] = c;
+            q_off[i] = fits ? off : -1;
+            q_state[i] = -2;
+            if (kRot) q_ang[i] = a.F1.kps[i].angle;
+            if (fits) {
+                const uint32_t* L = lists + (size_t)i * kAreaCap;
+                for (int e = 0; e < w; e++) ent[off + e] = L[e];
+            }
+        }
+        used = min(used + total, ent_cap);
+    }
+    __syncthreads();
+
+    // best and second keys of query i (one wave) among the candidates with
+    // is_free(j)
+    auto best2 = [&](const int i, auto is_free, unsigned long long& best, unsigned long long& second) {
+        best = ~0ull;
+        second = ~0ull;
+        const int c = q_cnt[i];
+        if (c <= 64) {
+            const int off = q_off[i];
+            const uint32_t e = lane < c ? (off >= 0 ? ent[off + lane] : lists[(size_t)i * kAreaCap + lane]) : 0u;
+            const int j = lane < c ? (int)(e & 0xFFFF) : 0;
+            const bool adm = lane < c && is_free(j);
+            const unsigned long long bal = __ballot(adm);
+            if (bal) {
+                const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)e, __builtin_ctzll(bal));
+                best = ((unsigned long long)(e1 >> 16) << 32) | (e1 & 0xFFFF);
+                const unsigned long long bal2 = bal & (bal - 1);
+                if (bal2) {
+                    const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)e, __builtin_ctzll(bal2));
+                    second = ((unsigned long long)(e2 >> 16) << 32) | (e2 & 0xFFFF);
+                }
+            }
+            return;
+        }
+        // longer lists: minima over full keys (distance, cell, index)
+        unsigned long long b = ~0ull;
+        if (c <= kAreaCap) {
+            const uint32_t* L = lists + (size_t)i * kAreaCap;
+            for (int k = lane; k < c; k += 64) {
+                const uint32_t ek = L[k];
+                const int j = (int)(ek & 0xFFFF);
+                if (!is_free(j)) continue;
+                const unsigned long long kk = ((unsigned long long)(ek >> 16) << 32) |
+                                              ((unsigned long long)(t.cell_oct[j] & 0xFFFF) << 12) | (unsigned long long)j;
+                b = kk < b ? kk : b;
+            }
+            best = wave_min_u64(b);
+            if (best == ~0ull) return;
+            b = ~0ull;
+            for (int k = lane; k < c; k += 64) {
+                const uint32_t ek = L[k];
+                const int j = (int)(ek & 0xFFFF);
+                if (j == key_idx(best) || !is_free(j)) continue;
+                const unsigned long long kk = ((unsigned long long)(ek >> 16) << 32) |
+                                              ((unsigned long long)(t.cell_oct[j] & 0xFFFF) << 12) | (unsigned long long)j;
+                b = kk < b ? kk : b;
+            }
+            second = wave_min_u64(b);
+            return;
+        }
+        // more candidates than the slot holds: every keypoint of the frame
+        const QuerySetup s = query_setup<K>(a, i);
+        uint4 d1a, d1b;
+        load_desc(s.desc, d1a, d1b);
+        for (int pass = 0; pass < 2; pass++) {
+            b = ~0ull;
+            for (int j = lane; j < n2; j += 64) {
+                const int co = t.cell_oct[j];
+                const int cell = (co & 0xFFFF) == 0xFFFF ? -1 : (co & 0xFFFF);
+                if (!level_ok(s.lf, co >> 16)) continue;
+                if (!in_area(s.q, cell, t.x[j], t.y[j], s.qx, s.qy, s.r)) continue;
+                if (!is_free(j) || (pass == 1 && j == key_idx(best))) continue;
+                uint4 a2, b2;
+                load_desc(a.F2.desc + (size_t)j * 32, a2, b2);
+                const unsigned long long kk = ((unsigned long long)hamming256(d1a, d1b, a2, b2) << 32) |
+                                              ((unsigned long long)cell << 12) | (unsigned long long)j;
+                b = kk < b ? kk : b;
+            }
+            b = wave_min_u64(b);
+            if (pass == 0) {
+                best = b;
+                if (best == ~0ull) return;
+            } else {
+                second = b;
+            }
+        }
+    };
+    // each search's acceptance rule; returns the candidate taken, or -1
+    auto decide = [&](const unsigned long long best, const unsigned long long second) {
+        const int bestDist = key_dist(best), bestDist2 = key_dist(second), bestIdx = key_idx(best);
+        bool accept;
+        if constexpr (K == kQWindow || K == kQPair) {
+            accept = (float)bestDist <= __fmul_rn((float)bestDist2, a.nnratio) && bestDist <= kTHHigh;
+        } else if constexpr (K == kQMotion) {
+            accept = bestDist <= kTHHigh;
+        } else {
+            accept = bestDist <= kTHHigh;
+            if (accept) {
+                const int bestLevel = (t.cell_oct[bestIdx] >> 16);
+                const int j2 = key_idx(second);
+                const int bestLevel2 = j2 >= 0 ? (t.cell_oct[j2] >> 16) : -1;
+                if (bestLevel == bestLevel2 && (float)bestDist > __fmul_rn(a.nnratio, (float)bestDist2)) accept = false;
+            }
+        }
+        return accept ? bestIdx : -1;
+    };
+
+    // parallel rounds: a thread per query with a short sorted list (the first
+    // two free keys of the list), a wave per query with a longer one
+    int* claim_prev = claim0;
+    int* claim_next = claim1;
+    bool converged = false;
+    for (int round = 0; round < kMaxRounds; round++) {
+        for (int j = tid; j < n2; j += kReplayThreads) claim_next[j] = kBig;
+        // a flag per round parity: a thread still reading the last round's
+        // flag must not see this round's reset
+        if (tid == 0) s_changed[round & 1] = 0;
+        __syncthreads();
+        int changed = 0;
+        for (int i = tid; i < nq; i += kReplayThreads) {
+            const int c = q_cnt[i];
+            if (c > 64) continue;
+            int st = -1;
+            if (c > 0) {
+                const int off = q_off[i];
+                const uint32_t* L = off >= 0 ? ent + off : lists + (size_t)i * kAreaCap;
+                unsigned long long best = ~0ull, second = ~0ull;
+                for (int k = 0; k < c; k++) {
+                    const uint32_t e = L[k];
+                    const int j = (int)(e & 0xFFFF);
+                    if (t.taken[j] != -1 || claim_prev[j] < i) continue;
+                    const unsigned long long kk = ((unsigned long long)(e >> 16) << 32) | (unsigned long long)j;
+                    if (best == ~0ull) {
+                        best = kk;
+                    } else {
+                        second = kk;
+                        break;
+                    }
+                }
+                st = decide(best, second);
+            }
+            changed |= st != q_state[i];
+            q_state[i] = st;
+            if (st >= 0) atomicMin(&claim_next[st], i);
+        }
+        for (int l = wv; l < nlong; l += kReplayWaves) {
+            const int i = q_long[l];
+            unsigned long long best, second;
+            best2(i, [&](int j) { return t.taken[j] == -1 && claim_prev[j] >= i; }, best, second);
+            const int st = decide(best, second);
+            if (lane == 0) {
+                changed |= st != q_state[i];
+                q_state[i] = st;
+                if (st >= 0) atomicMin(&claim_next[st], i);
+            }
+        }
+        if (__any(changed) && lane == 0) s_changed[round & 1] = 1;
+        __syncthreads();
+        if (!s_changed[round & 1]) {
+            if (tid == 0) atomicAdd(&g_area_rounds[0], (unsigned long long)(round + 1));
+            converged = true;
+            break;
+        }
+        int* tmp = claim_prev;
+        claim_prev = claim_next;
+        claim_next = tmp;
+    }
+    if (!converged && tid == 0) atomicAdd(&g_area_rounds[1], 1ull);
+    if (!converged && tid < 64) {   // the sequential replay (taken: -1 free, >= 0 / -2 not)
+        for (int i = 0; i < nq; i++) {
+            int st = -1;
+            if (q_cnt[i] > 0) {
+                unsigned long long best, second;
+                best2(i, [&](int j) { return t.taken[j] == -1; }, best, second);
+                st = decide(best, second);
+                if (st >= 0 && lane == 0) t.taken[st] = i;
+            }
+            if (lane == 0) q_state[i] = st;
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    // matches, rotation histogram (the reference pushes every match of
+    // WindowSearch, and of the motion search with its check on; the filter
+    // runs with the check on)
+    const bool filter = kRot && a.check_ori;
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) s_removed = 0;
+    for (int j = tid; j < n2; j += kReplayThreads) keys[j] = -1;   // out of the searched keypoint
+    __syncthreads();
+    int acc = 0;
+    for (int i = tid; i < nq; i += kReplayThreads) {
+        const int st = q_state[i];
+        if (st < 0) continue;
+        acc++;
+        keys[st] = i;
+        if (filter) {
+            const int b = rot_bin(q_ang[i], ang2[st]);
+            bins[st] = (signed char)b;
+            atomicAdd(&hist[b], 1);
+        }
+    }
+    const int nacc = block_sum(acc, bs, 0);
+    __syncthreads();
+    if (filter && tid == 0) {
+        int ind1, ind2, ind3;
+        three_maxima(hist, ind1, ind2, ind3);
+        hist[32] = ind1;
+        hist[33] = ind2;
+        hist[34] = ind3;
+    }
+    __syncthreads();
+    int removed = 0;
+    for (int j = tid; j < n2; j += kReplayThreads) {
+        int m = keys[j];
+        if (m >= 0 && filter) {
+            const int b = bins[j];
+            if (b != hist[32] && b != hist[33] && b != hist[34]) {
+                m = -1;
+                removed++;
+            }
+        }
+        a.out[j] = m;
+    }
+    const int nrem = block_sum(removed, bs, 1);
+    if (tid == 0) *a.out_n = nacc - nrem;
 }
 
 // Frame::isInFrustum (src/Frame.cc:136-197) for map point m of job a:
@@ -681,12 +1048,62 @@ void put_frame(Pinned& pin, const FrameOffs& o, const orbx_frame_view* v)
 
 size_t tab_lds(int n) { return (size_t)n * 16 + ((n + 15) & ~15) + (size_t)n * 4 + 32 * 4 + 64; }
 
+// Device space of the two-phase searches' candidate lists: B jobs of up to
+// nq queries (reserved after the read-back range; never copied).
+struct AreaBufs {
+    size_t lists, cnt, qglob;
+};
+AreaBufs reserve_area(Uploader& u, int B, int nq)
+{
+    AreaBufs o;
+    o.lists = u.reserve((size_t)B * std::max(nq, 1) * kAreaCap * 4);
+    o.cnt = u.reserve((size_t)B * std::max(nq, 1) * 4);
+    o.qglob = u.reserve((size_t)B * std::max(nq, 1) * 16);
+    return o;
+}
+
+// The two launches of a search of kind K over B jobs whose SearchArgs are
+// in device memory at dj (nq_max queries, n2_max searched keypoints at most).
+template <int K>
+int launch_area_search(orbx_ctx* ctx, const SearchArgs* dj, int B, int nq_max, int n2_max, const Uploader& u,
+                       const AreaBufs& o)
+{
+    uint32_t* lists = reinterpret_cast<uint32_t*>(u.base() + o.lists);
+    int32_t* cnt = reinterpret_cast<int32_t*>(u.base() + o.cnt);
+    const int cap_q = std::max(nq_max, 1);
+    n2_max = std::max(n2_max, 1);
+    // the replay's per-query arrays in LDS when they fit beside the table
+    // and a full entry budget, else in global memory; the entry budget
+    // shrinks to what is left
+    constexpr size_t kLds = 160 * 1024 - 1024;   // static LDS of the kernel aside
+    int q_lds = area_replay_lds(n2_max, cap_q, kReplayEntries) <= kLds;
+    const size_t fixed = area_replay_lds(n2_max, q_lds ? cap_q : 0, 0);
+    if (fixed > kLds) return ORBX_ERR_UNSUPPORTED;
+    const int ent_cap = (int)std::min<size_t>(kReplayEntries, (kLds - fixed) / 4);
+    if (nq_max > 0)
+        hipLaunchKernelGGL(k_area_lists<K>, dim3((nq_max + kAreaListWaves - 1) / kAreaListWaves, B),
+                           dim3(kAreaListWaves * 64), area_lists_lds(n2_max), ctx->stream, dj, cap_q, lists, cnt);
+    hipLaunchKernelGGL(k_area_replay<K>, dim3(B), dim3(kReplayThreads), area_replay_lds(n2_max, q_lds ? cap_q : 0, ent_cap),
+                       ctx->stream, dj, cap_q, lists, cnt, q_lds, ent_cap, reinterpret_cast<int*>(u.base() + o.qglob));
+    ORBX_HIP_CHECK(hipGetLastError());
+    return ORBX_OK;
+}
+
 }  // namespace
 }  // namespace orbx
 
 using namespace orbx;
 
 extern "C" {
+
+// Diagnostics: rounds of the two-phase searches' parallel replay summed over
+// calls, and how many fell back to the sequential replay.
+int orbx_debug_area_rounds(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_area_rounds), sizeof(unsigned long long) * 2) == hipSuccess
+               ? ORBX_OK
+               : ORBX_ERR_HIP;
+}
 
 int orbx_search_for_initialization(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_frame_view* F2,
                                    float* prev_matched, int32_t* matches12, int window, float nnratio,
@@ -759,16 +1176,17 @@ int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_fram
     ctx_enter(ctx);
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
-    const size_t ov = u.reserve(F1->n), oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
+    const size_t ov = u.reserve(F1->n), oarg = u.reserve(sizeof(SearchArgs));
+    const size_t oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4), io_end = on + 4;
+    const AreaBufs ol = reserve_area(u, 1, F1->n);
     int r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
-    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r == ORBX_OK) r = pin.open(io_end);
     if (r != ORBX_OK) return r;
     put_frame(pin, o1, F1);
     put_frame(pin, o2, F2);
     pin.put(ov, f1_mp, F1->n);
     pin.fill(oo, 0xFF, (size_t)F2->n * 4 + 4);
-    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
     a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
@@ -780,9 +1198,11 @@ int orbx_window_search(orbx_ctx* ctx, const orbx_frame_view* F1, const orbx_fram
     a.check_ori = check_ori;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_window_search, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
-    ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.put(oarg, &a, sizeof(a));
+    if ((r = pin.upload(io_end)) != ORBX_OK) return r;
+    const SearchArgs* da = reinterpret_cast<const SearchArgs*>(u.base() + oarg);
+    if ((r = launch_area_search<kQWindow>(ctx, da, 1, F1->n, F2->n, u, ol)) != ORBX_OK) return r;
+    if ((r = pin.download(oo, io_end)) != ORBX_OK) return r;
     pin.get(matches21, oo, (size_t)F2->n * 4);
     pin.get(n_matches, on, 4);
     return ORBX_OK;
@@ -800,10 +1220,12 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     Uploader u{ctx};
     const FrameOffs o1 = reserve_frame(u, F1), o2 = reserve_frame(u, F2);
     const size_t ox = u.reserve((size_t)F1->n * 12), ov = u.reserve(F1->n), oa = u.reserve(F2->n);
-    const size_t oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4);
+    const size_t oarg = u.reserve(sizeof(SearchArgs));
+    const size_t oo = u.reserve((size_t)F2->n * 4 + 4), on = u.reserve(4), io_end = on + 4;
+    const AreaBufs ol = reserve_area(u, 1, F1->n);
     int r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
-    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r == ORBX_OK) r = pin.open(io_end);
     if (r != ORBX_OK) return r;
     put_frame(pin, o1, F1);
     put_frame(pin, o2, F2);
@@ -811,7 +1233,6 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     pin.put(ov, f1_mp_valid, F1->n);
     pin.put(oa, f2_assigned, F2->n);
     pin.fill(oo, 0xFF, (size_t)F2->n * 4 + 4);
-    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(F1, u.base(), o1.kp, o1.desc);
     a.F2 = dev_frame(F2, u.base(), o2.kp, o2.desc);
@@ -824,9 +1245,11 @@ int orbx_search_by_projection_pair(orbx_ctx* ctx, const orbx_frame_view* F1, con
     a.nnratio = nnratio;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_proj_pair, dim3(1), dim3(64), tab_lds(std::max(F2->n, 1)), ctx->stream, a);
-    ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.put(oarg, &a, sizeof(a));
+    if ((r = pin.upload(io_end)) != ORBX_OK) return r;
+    const SearchArgs* da = reinterpret_cast<const SearchArgs*>(u.base() + oarg);
+    if ((r = launch_area_search<kQPair>(ctx, da, 1, F1->n, F2->n, u, ol)) != ORBX_OK) return r;
+    if ((r = pin.download(oo, io_end)) != ORBX_OK) return r;
     pin.get(matches21, oo, (size_t)F2->n * 4);
     pin.get(n_matches, on, 4);
     return ORBX_OK;
@@ -844,10 +1267,12 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     Uploader u{ctx};
     const FrameOffs oL = reserve_frame(u, Last), oC = reserve_frame(u, Cur);
     const size_t ox = u.reserve((size_t)Last->n * 12), ov = u.reserve(Last->n), oa = u.reserve(Cur->n);
-    const size_t oo = u.reserve((size_t)Cur->n * 4 + 4), on = u.reserve(4);
+    const size_t oarg = u.reserve(sizeof(SearchArgs));
+    const size_t oo = u.reserve((size_t)Cur->n * 4 + 4), on = u.reserve(4), io_end = on + 4;
+    const AreaBufs ol = reserve_area(u, 1, Last->n);
     int r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
-    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r == ORBX_OK) r = pin.open(io_end);
     if (r != ORBX_OK) return r;
     put_frame(pin, oL, Last);
     put_frame(pin, oC, Cur);
@@ -855,7 +1280,6 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     pin.put(ov, last_mp_valid, Last->n);
     pin.put(oa, cur_assigned, Cur->n);
     pin.fill(oo, 0xFF, (size_t)Cur->n * 4 + 4);
-    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F1 = dev_frame(Last, u.base(), oL.kp, oL.desc);
     a.F2 = dev_frame(Cur, u.base(), oC.kp, oC.desc);
@@ -869,9 +1293,11 @@ int orbx_search_by_projection_motion(orbx_ctx* ctx, const orbx_frame_view* Cur, 
     a.check_ori = check_ori;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_proj_motion, dim3(1), dim3(64), tab_lds(std::max(Cur->n, 1)), ctx->stream, a);
-    ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.put(oarg, &a, sizeof(a));
+    if ((r = pin.upload(io_end)) != ORBX_OK) return r;
+    const SearchArgs* da = reinterpret_cast<const SearchArgs*>(u.base() + oarg);
+    if ((r = launch_area_search<kQMotion>(ctx, da, 1, Last->n, Cur->n, u, ol)) != ORBX_OK) return r;
+    if ((r = pin.download(oo, io_end)) != ORBX_OK) return r;
     pin.get(matches_cur, oo, (size_t)Cur->n * 4);
     pin.get(n_matches, on, 4);
     return ORBX_OK;
@@ -892,10 +1318,12 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     const FrameOffs oF = reserve_frame(u, F);
     const size_t ov = u.reserve(n_mp), op = u.reserve((size_t)n_mp * 8), ol = u.reserve((size_t)n_mp * 4);
     const size_t oc = u.reserve((size_t)n_mp * 4), od = u.reserve((size_t)n_mp * 32), oa = u.reserve(F->n);
-    const size_t oo = u.reserve((size_t)F->n * 4 + 4), on = u.reserve(4);
+    const size_t oarg = u.reserve(sizeof(SearchArgs));
+    const size_t oo = u.reserve((size_t)F->n * 4 + 4), on = u.reserve(4), io_end = on + 4;
+    const AreaBufs oli = reserve_area(u, 1, n_mp);
     int r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
-    if (r == ORBX_OK) r = pin.open(u.total);
+    if (r == ORBX_OK) r = pin.open(io_end);
     if (r != ORBX_OK) return r;
     put_frame(pin, oF, F);
     pin.put(ov, in_view, n_mp);
@@ -905,7 +1333,6 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     pin.put(od, mp_desc, (size_t)n_mp * 32);
     pin.put(oa, f_assigned, F->n);
     pin.fill(oo, 0xFF, (size_t)F->n * 4 + 4);
-    if ((r = pin.upload(u.total)) != ORBX_OK) return r;
     SearchArgs a{};
     a.F2 = dev_frame(F, u.base(), oF.kp, oF.desc);
     a.nq = n_mp;
@@ -920,9 +1347,11 @@ int orbx_search_by_projection_local(orbx_ctx* ctx, const orbx_frame_view* F, int
     a.nnratio = nnratio;
     a.out = reinterpret_cast<int32_t*>(u.base() + oo);
     a.out_n = reinterpret_cast<int32_t*>(u.base() + on);
-    hipLaunchKernelGGL(k_proj_local, dim3(1), dim3(64), tab_lds(std::max(F->n, 1)), ctx->stream, a);
-    ORBX_HIP_CHECK(hipGetLastError());
-    if ((r = pin.download(oo, u.total)) != ORBX_OK) return r;
+    pin.put(oarg, &a, sizeof(a));
+    if ((r = pin.upload(io_end)) != ORBX_OK) return r;
+    const SearchArgs* da = reinterpret_cast<const SearchArgs*>(u.base() + oarg);
+    if ((r = launch_area_search<kQLocal>(ctx, da, 1, n_mp, F->n, u, oli)) != ORBX_OK) return r;
+    if ((r = pin.download(oo, io_end)) != ORBX_OK) return r;
     pin.get(matches_f, oo, (size_t)F->n * 4);
     pin.get(n_matches, on, 4);
     return ORBX_OK;
@@ -966,6 +1395,7 @@ static int search_local_map_impl(orbx_ctx* ctx, int B, orbx_local_map_query* qs)
     }
     const size_t o_jobs = u.reserve((size_t)B * sizeof(SearchArgs));
     const size_t o_outputs = u.total;
+    size_t o_end = 0;
     for (int b = 0; b < B; b++) {
         const orbx_local_map_query& q = qs[b];
         const size_t n = q.frame->n, m = q.n_mp;
@@ -977,8 +1407,12 @@ static int search_local_map_impl(orbx_ctx* ctx, int B, orbx_local_map_query* qs)
         o[b].pred = u.reserve(m * 4);
         o[b].cos = u.reserve(m * 4);
     }
+    o_end = u.total;
+    // one frame (Tracking's per-frame call): the two-phase search; batches of
+    // frames keep one wave per frame (k_proj_local_jobs)
+    const AreaBufs oa = reserve_area(u, 1, B == 1 ? max_mp : 0);
     int r = ensure_scratch(ctx, u.total);
-    if (r == ORBX_OK) r = ensure_pinned(ctx, u.total);
+    if (r == ORBX_OK) r = ensure_pinned(ctx, o_end);
     if (r != ORBX_OK) return r;
     uint8_t* h = static_cast<uint8_t*>(ctx->host_pinned);
     uint8_t* d = u.base();
@@ -1045,9 +1479,13 @@ static int search_local_map_impl(orbx_ctx* ctx, int B, orbx_local_map_query* qs)
     const SearchArgs* dj = reinterpret_cast<const SearchArgs*>(d + o_jobs);
     if (max_mp > 0)
         hipLaunchKernelGGL(k_frustum, dim3((max_mp + 255) / 256, B), dim3(256), 0, ctx->stream, dj);
-    hipLaunchKernelGGL(k_proj_local_jobs, dim3(B), dim3(64), tab_lds(max_n), ctx->stream, dj);
+    if (B == 1) {
+        if ((r = launch_area_search<kQLocal>(ctx, dj, 1, max_mp, max_n, u, oa)) != ORBX_OK) return r;
+    } else {
+        hipLaunchKernelGGL(k_proj_local_jobs, dim3(B), dim3(64), tab_lds(max_n), ctx->stream, dj);
+    }
     ORBX_HIP_CHECK(hipGetLastError());
-    ORBX_HIP_CHECK(hipMemcpyAsync(h + o_outputs, d + o_outputs, u.total - o_outputs, hipMemcpyDeviceToHost, ctx->stream));
+    ORBX_HIP_CHECK(hipMemcpyAsync(h + o_outputs, d + o_outputs, o_end - o_outputs, hipMemcpyDeviceToHost, ctx->stream));
     ORBX_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     for (int b = 0; b < B; b++) {
         orbx_local_map_query& q = qs[b];

@@ -98,7 +98,7 @@ def test_workgroup_setting_validates():
     c.close()
 
 
-def _hooks(ctx, fail=0, fallback=1, cap=0, coop=-1):
+def _hooks(ctx, fail=0, fallback=1, cap=0, coop=-2):   # coop -2: unchanged
     assert ox.lib().orbx_debug_lba_split(ctx.handle, fail, fallback, cap, coop) == 0
 
 
@@ -133,7 +133,7 @@ def test_split_plain_and_cooperative_launch(ctx, coop):
         same_bits(solve(ctx, prob, 0), one)
         assert ox.lib().orbx_lba_last_workgroups(ctx.handle) > 1
     finally:
-        _hooks(ctx, coop=-1)
+        _hooks(ctx, coop=0)
 
 
 def test_split_barrier_timeout_falls_back_to_one_workgroup(ctx):

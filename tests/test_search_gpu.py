@@ -112,8 +112,12 @@ def test_search_for_initialization_empty(ctx, frames_feats, which):
     assert _sfi_both(ctx, k1, d1, k2, d2, prev0, 100, 0.9, True) == 0
 
 
+# the two-phase searches (k_area_lists + k_area_replay): short sorted lists,
+# lists of 65..128 candidates in index order, and longer ones that the replay
+# evaluates in full (windows of 100 .. 400 pixels)
 @pytest.mark.parametrize("window,minl,maxl,ratio,ori", [(100, 0, -1, 0.9, True), (200, 1, 5, 0.7, False),
-                                                         (30, 0, 2, 1.0, True)])
+                                                         (30, 0, 2, 1.0, True), (400, 0, -1, 0.8, True),
+                                                         (60, 0, -1, 0.9, False)])
 def test_window_search(ctx, frames_feats, window, minl, maxl, ratio, ori):
     (k1, d1), (k2, d2) = frames_feats[0], frames_feats[1]
     F1, F2 = views(k1, d1, k2, d2)
@@ -129,7 +133,7 @@ def test_window_search(ctx, frames_feats, window, minl, maxl, ratio, ori):
     assert np.array_equal(mg, mr)
 
 
-@pytest.mark.parametrize("window", [15, 50])
+@pytest.mark.parametrize("window", [15, 50, 150, 300])
 def test_search_by_projection_pair(ctx, frames_feats, window):
     (k1, d1), (k2, d2) = frames_feats[0], frames_feats[1]
     F1, F2 = views(k1, d1, k2, d2)
@@ -150,7 +154,7 @@ def test_search_by_projection_pair(ctx, frames_feats, window):
     assert np.array_equal(mg, mr)
 
 
-@pytest.mark.parametrize("th,ori", [(15.0, True), (7.0, False)])
+@pytest.mark.parametrize("th,ori", [(15.0, True), (7.0, False), (40.0, True), (120.0, False), (2.0, True)])
 def test_search_by_projection_motion(ctx, frames_feats, th, ori):
     (kl, dl), (kc, dc) = frames_feats[1], frames_feats[2]
     C, Lv = views(kc, dc, kl, dl)
@@ -171,7 +175,7 @@ def test_search_by_projection_motion(ctx, frames_feats, th, ori):
     assert np.array_equal(mg, mr)
 
 
-@pytest.mark.parametrize("th", [1.0, 5.0])
+@pytest.mark.parametrize("th", [1.0, 5.0, 12.0, 30.0])
 def test_search_by_projection_local(ctx, frames_feats, th):
     (km, dm), (kf, df) = frames_feats[0], frames_feats[1]
     F = ox.frame_view(kf, df, W, H)

@@ -25,7 +25,7 @@ from orb_slam_amd import synth  # noqa: E402
 
 args = sys.argv[1:]
 n = int(args[args.index("--n") + 1]) if "--n" in args else 100
-what = [a for a in args if a in ("extract", "sfi", "pose", "lba")] or ["extract"]
+what = [a for a in args if a in ("extract", "sfi", "pose", "lba", "search")] or ["extract"]
 lbawg = [int(v) for v in args[args.index("--lbawg") + 1].split(",")] if "--lbawg" in args else [0]
 # k_lba_split launch: -1 the device's choice, 0 plain, 1 cooperative (orbx_debug_lba_split)
 coop = [int(v) for v in args[args.index("--coop") + 1].split(",")] if "--coop" in args else [-1]
@@ -72,6 +72,57 @@ if "extract" in what or "sfi" in what:
                                                     m.ctypes.data, 100, 0.9, 1, ctypes.byref(nm)) == 0
 
         print(f"sfi: {med(sfi, n):.4f} ms median", flush=True)
+    ctx.close()
+
+if "search" in what:
+    # the per-frame Tracking searches (host-pointer calls) against the CPU port
+    from oracle_lib import RefExtractor, load, ptr
+    W, H = 640, 480
+    CAM = np.array([500.0, 500.0, 320.0, 240.0], np.float32)
+    fr = synth.sequence(W, H, 3, seed=77)
+    ex = RefExtractor(1000)
+    (kl, dl), (kc, dc) = ex(fr[1]), ex(fr[2])
+    C, Lv = ox.frame_view(kc, dc, W, H), ox.frame_view(kl, dl, W, H)
+    rng = np.random.default_rng(15)
+    z = rng.uniform(2, 6, len(kl)).astype(np.float32)
+    xyz = np.ascontiguousarray(np.stack([(kl["x"] - CAM[2]) / CAM[0] * z, (kl["y"] - CAM[3]) / CAM[1] * z, z],
+                                        1).astype(np.float32))
+    valid = (rng.random(len(kl)) < 0.85).astype(np.uint8)
+    asg = np.zeros(len(kc), np.uint8)
+    c_, s_ = np.cos(0.002), np.sin(0.002)
+    T = np.array([[c_, 0, s_, -0.008], [0, 1, 0, -0.004], [-s_, 0, c_, 0]], np.float32).reshape(-1).copy()
+    m = np.zeros(len(kc), np.int32)
+    nm = ctypes.c_int()
+    R = load()
+    ctx = ox.Context(nfeatures=1000, max_w=W, max_h=H, slots=1)
+    calls = {
+        "motion th15": (lambda i: L.orbx_search_by_projection_motion(ctx.handle, ctypes.byref(C), ctypes.byref(Lv),
+                                                                    ptr(xyz), ptr(valid), ptr(asg), ptr(T), ptr(CAM),
+                                                                    15.0, 1, ptr(m), ctypes.byref(nm)),
+                        lambda i: R.orbx_ref_search_by_projection_motion(ctypes.byref(C), ctypes.byref(Lv), ptr(xyz),
+                                                                        ptr(valid), ptr(asg), ptr(T), ptr(CAM), 15.0, 1,
+                                                                        ptr(m), ctypes.byref(nm))),
+        "window 200": (lambda i: L.orbx_window_search(ctx.handle, ctypes.byref(Lv), ctypes.byref(C), ptr(valid), 200,
+                                                      0, -1, 0.9, 1, ptr(m), ctypes.byref(nm)),
+                       lambda i: R.orbx_ref_window_search(ctypes.byref(Lv), ctypes.byref(C), ptr(valid), 200, 0, -1,
+                                                          0.9, 1, ptr(m), ctypes.byref(nm))),
+        "pair 15": (lambda i: L.orbx_search_by_projection_pair(ctx.handle, ctypes.byref(Lv), ctypes.byref(C),
+                                                               ptr(xyz), ptr(valid), ptr(asg), ptr(T), ptr(CAM), 15,
+                                                               0.9, ptr(m), ctypes.byref(nm)),
+                    lambda i: R.orbx_ref_search_by_projection_pair(ctypes.byref(Lv), ctypes.byref(C), ptr(xyz),
+                                                                   ptr(valid), ptr(asg), ptr(T), ptr(CAM), 15, 0.9,
+                                                                   ptr(m), ctypes.byref(nm))),
+    }
+    dbg = (ctypes.c_ulonglong * 2)()
+    L.orbx_debug_area_rounds.argtypes = [ctypes.c_void_p]
+    for name, (g, c) in calls.items():
+        L.orbx_debug_area_rounds(dbg)
+        r0 = list(dbg)
+        tg = med(g, n)
+        L.orbx_debug_area_rounds(dbg)
+        print(f"search {name}: gpu {tg:.4f} ms, cpu port {med(c, max(5, n // 4)):.4f} ms median; "
+              f"replay rounds {(dbg[0] - r0[0]) / n:.2f} per call, sequential fallbacks {dbg[1] - r0[1]} of {n}",
+              flush=True)
     ctx.close()
 
 if "pose" in what:
