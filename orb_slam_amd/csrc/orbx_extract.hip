@@ -308,6 +308,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize(ExtractArgs a, int level)
 struct ResizeLevel {
     long long off, poff;                 // level / parent offsets in a frame's pyramid
     int stride, pstride, w, h, pw, ph, ph_parent_h, nvec, span, strip_off, row_off, col_off;
+    int packed;                          // every interior word's taps lie within 8 bytes (the packed form applies)
 };
 
 __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLevel L, int pitch)
@@ -327,54 +328,84 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
     const int nsrc = min(L.span, L.ph_parent_h - lo);
     const uint8_t* pbase = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.poff + (size_t)(lo + kEdge) * L.pstride;
 #ifndef RES_NO_STAGE
-    stage_to_lds<8>(s_dyn, nsrc * nch, tid, (int)blockDim.x, [&](int u) {
-        const int r = u / nch, c = u - r * nch;
-        return *reinterpret_cast<const uint4*>(pbase + (size_t)r * L.pstride + 16 * c);
-    });
+    {
+        // u / nch as a float product: (u + 1/2) / nch lies at least 1/(2 nch)
+        // from an integer and the product errs by < 2^-21 (u + 1) for
+        // u < 2^16 (no integer division per item)
+        const float inv = 1.0f / (float)nch;
+        stage_to_lds<8>(s_dyn, nsrc * nch, tid, (int)blockDim.x, [&](int u) {
+            const int r = (int)(((float)u + 0.5f) * inv), c = u - r * nch;
+            return *reinterpret_cast<const uint4*>(pbase + (size_t)r * L.pstride + 16 * c);
+        });
+    }
 #endif
     __syncthreads();
     uint8_t* dst = a.pyr_raw + (size_t)f * a.frame_pyr_bytes + L.off + (size_t)py0 * L.stride;
-    // One thread per 4-pixel output word, sliding down the strip's rows.
-    // Its four columns' LDS offsets and weights are fixed; the horizontal
-    // sums of a source row are computed once and reused by the next output
-    // row when it shares the row (rows are uniform across the block).
-    // sx1 is sx0 + 1, or sx0 with a1 = 0 (HResizeLinear tail), so the
-    // second tap is always read at offset +1.
 #ifdef RES_NO_COMPUTE
     if (tid < 64) reinterpret_cast<uint32_t*>(dst)[tid] = s_src[tid * 7];
     return;
 #endif
-    for (int q = tid; q < (L.stride >> 2); q += blockDim.x) {
-        const int px0 = 4 * q;
-        int ca[4], a0[4], a1[4];
-        bool vb[4], vec = true;
+    // Output words split by form (no wave runs both):
+    //  * interior words [q_lo, q_hi) whose four columns are on the SSE2 path
+    //    (x < nvec): the packed form below, one thread per word sliding
+    //    down the strip's rows;
+    //  * the rest -- the reflected border words, the scalar-tail columns
+    //    x >= nvec and the row padding -- one (row, word) item per thread,
+    //    in the general form.
+    // sx1 is sx0 + 1, or sx0 with a1 = 0 (HResizeLinear tail), so the
+    // second tap is always read at offset +1.
+    const int nq = L.stride >> 2;
+    const int q_lo = (kEdge + 3) >> 2, q_hi = L.packed ? max(q_lo, (kEdge + min(L.w, L.nvec)) >> 2) : q_lo;
+    const int nfast = q_hi - q_lo;
+    // Packed form: a word's four source taps lie in 8 bytes (source step
+    // < 2, so sx0(x + 3) - sx0(x) <= 6); three dword reads aligned to the
+    // word's first tap (alignbyte) hold them, each column's (p0, p1) pair is
+    // one v_perm into 16-bit halves and its 2-tap sum one v_dot2_u32_u16 with
+    // weights (16 a0, 16 a1) -- 16 S, whose bits 8..23 are (S >> 4) << 8 --
+    // and VResizeLinearVec_32s8u's (S >> 4) * b >> 16 is one
+    // v_mul_hi_u32_u24 of that with b << 8.  S >> 4 <= 32640 and the
+    // weights are <= 2048, so none of its 16-bit saturations can trigger.
+    typedef unsigned short orbx_us2 __attribute__((ext_vector_type(2)));
+    auto mh = [](uint32_t x, uint32_t y) {   // bits 32..47 of the 24 x 24-bit product
+        return (uint32_t)(((unsigned long long)(x & 0xFFFFFFu) * (unsigned long long)(y & 0xFFFFFFu)) >> 32);
+    };
+    for (int t = tid; t < nfast; t += blockDim.x) {
+        const int q = q_lo + t, x0 = 4 * q - kEdge;
+        int ca[4];
+        uint32_t sel[4], wgt[4];
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-            const bool on = px0 + b < L.pw;
-            const int x = on ? reflect101(px0 + b - kEdge, L.w) : 0;
-            const ResizeCol c = s_cols[x];
+            const ResizeCol c = s_cols[x0 + b];
             ca[b] = kEdge + c.sx0;
-            a0[b] = on ? c.a0 : 0;
-            a1[b] = on ? c.a1 : 0;
-            vb[b] = x < L.nvec;
-            vec = vec && (!on || vb[b]);
+            wgt[b] = (uint32_t)(16 * c.a0) | (uint32_t)(16 * c.a1) << 16;
         }
-        auto hrow = [&](int sy, int (&S)[4]) {
-            const uint8_t* base = s_src + (sy - lo) * pitch;
+        const int qa = ca[0] & ~3, sh = ca[0] & 3;
 #pragma unroll
-            for (int b = 0; b < 4; b++) S[b] = base[ca[b]] * a0[b] + base[ca[b] + 1] * a1[b];
+        for (int b = 0; b < 4; b++) {
+            const uint32_t r = (uint32_t)(ca[b] - ca[0]);   // tap bytes r, r + 1 of the aligned 8 (L.packed)
+            sel[b] = r | 0x0C00u | (r + 1) << 16 | 0x0C000000u;
+        }
+        auto hrow = [&](int sy, uint32_t (&S)[4]) {
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(s_src + (sy - lo) * pitch + qa);
+            const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                S[b] = __builtin_amdgcn_udot2(__builtin_bit_cast(orbx_us2, __builtin_amdgcn_perm(w1, w0, sel[b])),
+                                              __builtin_bit_cast(orbx_us2, wgt[b]), 0u, false) &
+                       0x00FFFF00u;
         };
-        int H0[4], H1[4], c0 = -1, c1 = -1;
+        uint32_t H0[4], H1[4];
+        int c0 = -1, c1 = -1;
         // the next row's table entry is read while this row is computed
-        // (its LDS round trip then overlaps the source reads of this row)
         uint2 nxt = reinterpret_cast<const uint2*>(s_rows)[0];
         for (int rr = 0; rr < nrows; rr++) {
             const uint2 cur = nxt;
             if (rr + 1 < nrows) nxt = reinterpret_cast<const uint2*>(s_rows)[rr + 1];
             const uint32_t w0 = __builtin_amdgcn_readfirstlane(cur.x), w1 = __builtin_amdgcn_readfirstlane(cur.y);
             const int sy0 = (int)(int16_t)(w0 & 0xFFFF), sy1 = (int)(int16_t)(w0 >> 16);
-            const int b0 = (int)(int16_t)(w1 & 0xFFFF), b1 = (int)(int16_t)(w1 >> 16);
-            int A[4], B[4];
+            const uint32_t B0 = (w1 & 0xFFFFu) << 8, B1 = (w1 >> 16) << 8;
+            uint32_t A[4], B[4];
             if (sy0 == c1) {
 #pragma unroll
                 for (int b = 0; b < 4; b++) A[b] = H1[b];
@@ -401,27 +432,34 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
             c0 = sy0;
             c1 = sy1;
             uint32_t word = 0;
-            if (vec) {
-                // VResizeLinearVec_32s8u; S >> 4 <= 32640 and the weights are
-                // <= 2048, so none of its 16-bit saturations can trigger
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
-                    word |= (uint32_t)min(v, 255) << (8 * b);
-                }
-            } else {
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    int v;
-                    if (vb[b])
-                        v = (((A[b] >> 4) * b0 >> 16) + ((B[b] >> 4) * b1 >> 16) + 2) >> 2;
-                    else   // FixedPtCast<int, uchar, 22>
-                        v = (A[b] * b0 + B[b] * b1 + (1 << 21)) >> 22;
-                    word |= (uint32_t)sat_u8(v) << (8 * b);
-                }
-            }
-            *reinterpret_cast<uint32_t*>(dst + (size_t)rr * L.stride + px0) = word;
+            for (int b = 0; b < 4; b++) word |= min((mh(A[b], B0) + mh(B[b], B1) + 2) >> 2, 255u) << (8 * b);
+            *reinterpret_cast<uint32_t*>(dst + (size_t)rr * L.stride + 4 * q) = word;
         }
+    }
+    // the other words, one (row, word) each
+    const int nslow = nq - nfast;
+    for (int item = tid; item < nrows * nslow; item += blockDim.x) {
+        const int rr = item / nslow, k = item - rr * nslow;
+        const int q = k < q_lo ? k : k + nfast, px0 = 4 * q;
+        const ResizeRow R = s_rows[rr];
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (px0 + b >= L.pw) continue;   // row padding: zero
+            const int x = reflect101(px0 + b - kEdge, L.w);
+            const ResizeCol c = s_cols[x];
+            const uint8_t* r0 = s_src + (R.sy0 - lo) * pitch + kEdge + c.sx0;
+            const uint8_t* r1 = s_src + (R.sy1 - lo) * pitch + kEdge + c.sx0;
+            const int S0 = r0[0] * c.a0 + r0[1] * c.a1, S1 = r1[0] * c.a0 + r1[1] * c.a1;
+            int v;
+            if (x < L.nvec)
+                v = (((S0 >> 4) * R.b0 >> 16) + ((S1 >> 4) * R.b1 >> 16) + 2) >> 2;
+            else   // FixedPtCast<int, uchar, 22>
+                v = (S0 * R.b0 + S1 * R.b1 + (1 << 21)) >> 22;
+            word |= (uint32_t)sat_u8(v) << (8 * b);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (size_t)rr * L.stride + px0) = word;
     }
 }
 
@@ -2048,8 +2086,14 @@ int launch_extract(orbx_ctx* ctx, int first, int count, const MatchSpec* m)
             timer_begin(ctx, "resize", st);
             if (lds <= kResizeLds) {
                 const int threads = std::min(256, ((L.stride / 4) + 63) & ~63);
+                // the packed form needs each interior word's taps within 8
+                // bytes (source step < 2 keeps them within 7; a level just
+                // over 2x, e.g. 333 -> 166, may not)
+                int packed = 1;
+                for (int x0 = 0; x0 + 3 < L.w; x0 += 4)
+                    if (g.res_cols[L.res_col_off + x0 + 3].sx0 - g.res_cols[L.res_col_off + x0].sx0 > 6) packed = 0;
                 const ResizeLevel rl{L.off, P.off, L.stride, P.stride, L.w, L.h, L.pw, L.ph, P.h, L.nvec_resize,
-                                     L.res_span, L.res_strip_off, L.res_row_off, L.res_col_off};
+                                     L.res_span, L.res_strip_off, L.res_row_off, L.res_col_off, packed};
                 for (int rep = 0; rep < kDiagRepeat[0]; rep++)
                     hipLaunchKernelGGL(k_pyr_resize_lds, dim3((L.ph + kResRows - 1) / kResRows, nb), dim3(threads), lds,
                                        st, x, rl, pitch);
