@@ -563,6 +563,79 @@ def single_call_legs(args, frames, nf, w, h):
     mt["call"] = ("orbx_search_for_initialization: two host frame views (1000 keypoints each), window 100, nnratio "
                   "0.9, orientation check (ORBmatcher::SearchForInitialization, src/ORBmatcher.cc:598-713)")
     out["search_for_initialization"] = mt
+
+    # --- Tracking's per-frame window / projection searches (host views) ------
+    # TrackWithMotionModel's SearchByProjection (src/Tracking.cc:584, th 15),
+    # TrackPreviousFrame's WindowSearch (:510, window 200) and pair search
+    # (:544, window 15), SearchReferencePointsInFrustum's local-map search
+    # (:745-750, th 1): the two-phase kernels (k_area_lists + k_area_replay)
+    cam = np.array([500.0, 500.0, 320.0, 240.0], np.float32)
+    (kl, dl), (kc, dc) = feats[0], feats[1]
+    Lv, Cv = views[0][0], views[1][0]
+    rng = np.random.default_rng(31)
+    z = rng.uniform(2.0, 6.0, len(kl)).astype(np.float32)
+    xyz = np.ascontiguousarray(np.stack([(kl["x"] - cam[2]) / cam[0] * z, (kl["y"] - cam[3]) / cam[1] * z, z],
+                                        1).astype(np.float32))
+    valid = (rng.random(len(kl)) < 0.85).astype(np.uint8)
+    asg = np.zeros(len(kc), np.uint8)
+    c_, s_ = np.cos(0.002), np.sin(0.002)
+    T = np.array([[c_, 0, s_, -0.008], [0, 1, 0, -0.004], [-s_, 0, c_, 0.0]], np.float32).reshape(-1).copy()
+    proj = np.ascontiguousarray(np.stack([kl["x"] + 2.0, kl["y"] + 1.0], 1).astype(np.float32))
+    pred = np.ascontiguousarray(kl["octave"].astype(np.int32))
+    vcos = rng.uniform(0.99, 1.0, len(kl)).astype(np.float32)
+    mpd = np.ascontiguousarray(dl)
+    m_out = np.zeros(nf, np.int32)
+    P = oracle_lib.load()   # the parity oracle (R, the native build, is the timed one)
+    searches = {
+        "motion_th15": (
+            lambda lib_: lib_.orbx_ref_search_by_projection_motion(ctypes.byref(Cv), ctypes.byref(Lv), xyz.ctypes.data,
+                                                                   valid.ctypes.data, asg.ctypes.data, T.ctypes.data,
+                                                                   cam.ctypes.data, ctypes.c_float(15.0), 1,
+                                                                   m_out.ctypes.data, ctypes.byref(nm)),
+            lambda: L.orbx_search_by_projection_motion(ctx1.handle, ctypes.byref(Cv), ctypes.byref(Lv), xyz.ctypes.data,
+                                                       valid.ctypes.data, asg.ctypes.data, T.ctypes.data,
+                                                       cam.ctypes.data, 15.0, 1, m_out.ctypes.data, ctypes.byref(nm)),
+            "SearchByProjection(Frame&, const Frame&, th 15) (src/ORBmatcher.cc:1507-1620)"),
+        "window_200": (
+            lambda lib_: lib_.orbx_ref_window_search(ctypes.byref(Lv), ctypes.byref(Cv), valid.ctypes.data, 200, 0, -1,
+                                                     ctypes.c_float(0.9), 1, m_out.ctypes.data, ctypes.byref(nm)),
+            lambda: L.orbx_window_search(ctx1.handle, ctypes.byref(Lv), ctypes.byref(Cv), valid.ctypes.data, 200, 0,
+                                         -1, 0.9, 1, m_out.ctypes.data, ctypes.byref(nm)),
+            "WindowSearch(window 200) (src/ORBmatcher.cc:409-516)"),
+        "pair_15": (
+            lambda lib_: lib_.orbx_ref_search_by_projection_pair(ctypes.byref(Lv), ctypes.byref(Cv), xyz.ctypes.data,
+                                                                 valid.ctypes.data, asg.ctypes.data, T.ctypes.data,
+                                                                 cam.ctypes.data, 15, ctypes.c_float(0.9),
+                                                                 m_out.ctypes.data, ctypes.byref(nm)),
+            lambda: L.orbx_search_by_projection_pair(ctx1.handle, ctypes.byref(Lv), ctypes.byref(Cv), xyz.ctypes.data,
+                                                     valid.ctypes.data, asg.ctypes.data, T.ctypes.data,
+                                                     cam.ctypes.data, 15, 0.9, m_out.ctypes.data, ctypes.byref(nm)),
+            "SearchByProjection(Frame&, Frame&, window 15) (src/ORBmatcher.cc:519-594)"),
+        "local_map_th1": (
+            lambda lib_: lib_.orbx_ref_search_by_projection_local(ctypes.byref(Cv), len(kl), valid.ctypes.data,
+                                                                  proj.ctypes.data, pred.ctypes.data, vcos.ctypes.data,
+                                                                  mpd.ctypes.data, asg.ctypes.data, ctypes.c_float(1.0),
+                                                                  ctypes.c_float(0.8), m_out.ctypes.data,
+                                                                  ctypes.byref(nm)),
+            lambda: L.orbx_search_by_projection_local(ctx1.handle, ctypes.byref(Cv), len(kl), valid.ctypes.data,
+                                                      proj.ctypes.data, pred.ctypes.data, vcos.ctypes.data,
+                                                      mpd.ctypes.data, asg.ctypes.data, 1.0, 0.8, m_out.ctypes.data,
+                                                      ctypes.byref(nm)),
+            "SearchByProjection(Frame&, local map, th 1) (src/ORBmatcher.cc:49-125)"),
+    }
+    ts = {}
+    for name, (cpu_fn, gpu_fn, what) in searches.items():
+        cpu_fn(P)
+        ref = (m_out.copy(), nm.value)
+        check_rc(gpu_fn(), name)
+        leg = {"bit_exact": bool(np.array_equal(m_out, ref[0]) and nm.value == ref[1]), "matches": ref[1],
+               "gpu": time_calls(lambda i: check_rc(gpu_fn(), name), 1, proto),
+               "cpu": time_calls(lambda i: cpu_fn(R), 1, proto), "call": what}
+        leg["speedup_vs_cpu"] = round(leg["cpu"]["median_ms"] / leg["gpu"]["median_ms"], 2)
+        ts[name] = leg
+    ts["note"] = ("host frame views of two consecutive extracted frames (1000 keypoints); candidate lists per query "
+                  "across the chip, greedy assignment resolved in parallel fixed-point rounds (k_area_replay)")
+    out["tracking_searches"] = ts
     ctx1.close()
 
     # --- Optimizer::PoseOptimization on one frame ------------------------
@@ -641,6 +714,35 @@ def single_call_legs(args, frames, nf, w, h):
                   "outlier pass (Optimizer::LocalBundleAdjustment, src/Optimizer.cc:287-536)")
     out["lba_solve"] = ba
     ctxb.close()
+
+    # --- ORB-SLAM's three threads at once on this GPU ----------------------
+    # Tracking (extract -> motion search -> pose), LocalMapping (local BA over
+    # several workgroups -> triangulation search) and LoopClosing (BoW search
+    # -> Sim3 search), each on its own context and host thread
+    # (src/main.cc:122-133; tests/test_threads_gpu.py): per-call medians one
+    # thread at a time and under contention, outputs compared bit for bit
+    import threads_work as tw
+    tin = tw.make_inputs()
+    tcs = tw.make_contexts()
+    rounds = 40
+    alone_o = {k: [] for k in tw.WORK}
+    alone_t = {k: [] for k in tw.WORK}
+    for k in tw.WORK:
+        for r in range(rounds):
+            o, t = tw.WORK[k](tcs[k], tin, r)
+            alone_o[k].append(o)
+            alone_t[k].append(t)
+    res, conc_t, errs = tw.run_threads(tcs, tin, rounds)
+    same = not errs and all(tw.same(o, alone_o[k][r]) for k in tw.WORK for r, o in enumerate(res[k]))
+    lba_wg = L.orbx_lba_last_workgroups(tcs["local_mapping"].handle)
+    for c in tcs.values():
+        c.close()
+    out["three_threads"] = {
+        "median_ms_alone": tw._medians(alone_t), "median_ms_concurrent": tw._medians(conc_t),
+        "rounds_per_thread": rounds, "outputs_identical_to_alone": bool(same), "errors": errs,
+        "lba_workgroups": lba_wg,
+        "note": "Tracking / LocalMapping / LoopClosing calls from three host threads, one context each "
+                "(src/main.cc:122-133); local BA on the multi-workgroup kernel (plain launch, residency cap)"}
     return out
 
 
