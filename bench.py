@@ -638,6 +638,54 @@ def single_call_legs(args, frames, nf, w, h):
     out["tracking_searches"] = ts
     ctx1.close()
 
+    # --- one whole Tracking frame on the device (orbx_track_frame) ----------
+    # TrackWithMotionModel + TrackLocalMap (src/Tracking.cc:572-627,
+    # 701-752): image in, extraction, motion search, PoseOptimization,
+    # frustum + local-map search, PoseOptimization, one read-back; cpu = the
+    # same chain over the oracle (tests/track_data.py ref_chain)
+    import track_data as td
+    ctxt = ox.Context(nfeatures=nf, max_w=w, max_h=h, slots=3, device=args.device)
+    last_img, cur_img = td.images(w, h, 6, 11)
+    ctxt.upload(last_img, 0)
+    ctxt.extract(0, 1)
+    ctxt.sync()
+    tkl, tdl = ctxt.features(0)
+    tscene = td.make_scene(tkl, tdl, 11)
+    tpred = td.pose_x(7.5 * td.DEPTH / float(td.CAM[0]))
+    tq_img, tkeep_img = td.query(tscene, tpred, slot=1, image=cur_img, last_slot=0, cap=nf)
+    tq_slot, tkeep_slot = td.query(tscene, tpred, slot=1, last_slot=0, cap=nf)
+    check_rc(L.orbx_track_frame(ctxt.handle, ctypes.byref(tq_img)), "orbx_track_frame")
+    tkc, tdc = ctxt.features(1)
+    texp = td.ref_chain(P, tkl, tdl, tkc, tdc, tscene, tpred)
+    tr = {}
+    for exact, key in ((1, "gpu_exact_sums"), (0, "gpu")):
+        check_rc(L.orbx_pose_set_exact(ctxt.handle, exact), "orbx_pose_set_exact")
+        leg = {"with_extraction": time_calls(lambda i: check_rc(L.orbx_track_frame(ctxt.handle, ctypes.byref(tq_img)),
+                                                                "orbx_track_frame"), 1, proto),
+               "chain_only": time_calls(lambda i: check_rc(L.orbx_track_frame(ctxt.handle, ctypes.byref(tq_slot)),
+                                                           "orbx_track_frame"), 1, proto)}
+        got = td.result(tq_slot, tkeep_slot)
+        same = all(got[k] == texp[k] for k in ("status", "n_cur", "n_motion", "n_after_pose", "n_in_view", "n_local",
+                                               "n_inliers"))
+        same = same and np.array_equal(got["cur_mp"], texp["cur_mp"]) and np.array_equal(got["cur_outlier"],
+                                                                                         texp["cur_outlier"])
+        leg["matches_identical"] = bool(same)
+        leg["max_abs_tcw_diff_vs_oracle"] = float(np.abs(got["Tcw"] - texp["Tcw"]).max())
+        tr[key] = leg
+    check_rc(L.orbx_pose_set_exact(ctxt.handle, 0), "orbx_pose_set_exact")
+    ctxt.close()
+    tr["cpu"] = {"with_extraction": time_calls(lambda i: (rex(cur_img), td.ref_chain(R, tkl, tdl, tkc, tdc, tscene,
+                                                                                   tpred)), 1, proto),
+                 "chain_only": time_calls(lambda i: td.ref_chain(R, tkl, tdl, tkc, tdc, tscene, tpred), 1, proto)}
+    for k in ("with_extraction", "chain_only"):
+        tr["speedup_vs_cpu_" + k] = round(tr["cpu"][k]["median_ms"] / tr["gpu"][k]["median_ms"], 2)
+    tr["status"] = texp["status"]
+    tr["counts"] = {k: int(texp[k]) for k in ("n_motion", "n_after_pose", "n_in_view", "n_local", "n_inliers")}
+    tr["call"] = ("orbx_track_frame: one 640x480 image in (or the slot already extracted: chain_only), last frame in "
+                  "its slot, local map of %d points; one upload, one read-back (cpu: the oracle's extractor, "
+                  "matchers and PoseOptimization in the same order, numpy glue)" % len(tscene["pos"]))
+    out["tracking_frame"] = tr
+
     # --- Optimizer::PoseOptimization on one frame ------------------------
     ctxp = ox.Context(nfeatures=100, max_w=64, max_h=64, slots=1, device=args.device)
     pframes = [sp.make_frame(n_kp=1000, seed=7000 * 1000 + i) for i in range(16)]

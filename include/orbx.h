@@ -390,6 +390,66 @@ typedef struct {
 } orbx_local_map_query;
 
 int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q);
+
+/* One Tracking frame on the device (Tracking::TrackWithMotionModel then
+ * Tracking::TrackLocalMap, src/Tracking.cc:573-600, 604-627): the current
+ * frame's keypoints are read where extraction left them (slot `slot`; with
+ * `image` set, the image is uploaded and extracted into that slot first),
+ * and the chain
+ *   SearchByProjection(current, last, 15)            (src/ORBmatcher.cc:1507)
+ *   -> < 20 matches: status 1 (the reference then tries TrackPreviousFrame)
+ *   -> PoseOptimization, outliers discarded          (src/Optimizer.cc:154)
+ *   -> < 10 matches left: status 2
+ *   -> SearchReferencePointsInFrustum: isInFrustum of the local map points
+ *      not already matched, SearchByProjection(F, local map, th)
+ *   -> PoseOptimization on all matches
+ * runs without a host round trip: one upload (last frame, local map, pose
+ * prediction, image) and one read-back.  The last frame's map points are
+ * named by their index in the local map.  The camera centre for the frustum
+ * test is Frame::UpdatePoseMatrices' mOw = -Rcw^T tcw evaluated in float
+ * left to right (the adapter's host glue does the same).  The undistorted
+ * keypoints of the slot are its extracted keypoints (k1 = 0) or those
+ * orbx_dev_undistort wrote; the frame bounds those of
+ * orbx_dev_set_image_bounds (default 0..w, 0..h). */
+typedef struct {
+    int slot;                       /* current frame's slot                                */
+    const uint8_t* image;           /* NULL (slot already extracted) or the mono8 image    */
+    int w, h;                       /* image size (also the default bounds)                */
+    size_t stride;
+    int last_slot;                  /* >= 0: LastFrame is that slot's extraction (the previous
+                                       call's slot; `last` unused), else -1              */
+    int last_cap;                   /* last_slot >= 0: entries of last_mp / last_outlier (at
+                                       least that frame's n_cur, at most nfeatures)       */
+    const orbx_frame_view* last;    /* last_slot < 0: LastFrame's mvKeysUn, mDescriptors,
+                                       bounds, pyramid                                    */
+    const int32_t* last_mp;         /* local-map index of LastFrame.mvpMapPoints[i], or -1 */
+    const uint8_t* last_outlier;    /* LastFrame.mvbOutlier                                */
+    int n_mp;                       /* local map (mvpLocalMapPoints)                       */
+    const float* mp_pos;            /* n_mp x 3                                            */
+    const float* mp_normal;         /* n_mp x 3                                            */
+    const float* mp_dist;           /* n_mp x 2: min, max distance invariance              */
+    const uint8_t* mp_desc;         /* n_mp x 32                                           */
+    const uint8_t* mp_skip;         /* n_mp or NULL: isBad()                               */
+    const float* Tcw_pred;          /* 12 (rows 0..2 of mVelocity * LastFrame.mTcw)        */
+    const float* cam;               /* fx, fy, cx, cy                                      */
+    const float* inv_level_sigma2;  /* nlevels (mvInvLevelSigma2)                          */
+    int nlevels;
+    float th_local;                 /* 1, or 5 just after relocalisation                   */
+    /* outputs */
+    float Tcw[12];                  /* final pose (rows 0..2): after the last PoseOptimization
+                                       that ran (the prediction for status 1)              */
+    int32_t* cur_mp;                /* cap: local-map index per current keypoint, or -1     */
+    uint8_t* cur_outlier;           /* cap: mvbOutlier after the last PoseOptimization      */
+    int cap;                        /* capacity of cur_mp / cur_outlier                    */
+    int n_cur;                      /* current frame's keypoints                           */
+    int status;                     /* 0 tracked (TrackLocalMap ran), 1 / 2 see above      */
+    int n_motion;                   /* SearchByProjection(current, last) matches           */
+    int n_after_pose;               /* matches left after the first PoseOptimization       */
+    int n_in_view;                  /* local map points in view (nToMatch)                  */
+    int n_local;                    /* SearchByProjection(F, local map) matches            */
+    int n_inliers;                  /* the last PoseOptimization's return value            */
+} orbx_track_query;
+int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q);
 /* B independent frames (each with its own local map) in one upload, two
  * launches (all frustum tests, then one search wavefront per frame) and one
  * readback. */

@@ -94,6 +94,7 @@ def _declare(L):
         "orbx_search_by_projection_local": ([vp, vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, ip], i),
         "orbx_search_local_map": ([vp, vp], i),
         "orbx_search_local_map_batch": ([vp, i, vp], i),
+        "orbx_track_frame": ([vp, vp], i),
         "orbx_lba_solve": ([vp, vp, i, i, vp, vp, vp, vp], i),
         "orbx_lba_solve_batch": ([vp, i, vp, i, i, vp, vp, vp, vp], i),
         "orbx_lba_stage": ([vp, i, vp], i),

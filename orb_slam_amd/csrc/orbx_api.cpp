@@ -196,6 +196,8 @@ int ensure_aux_streams(orbx_ctx* ctx)
     return ORBX_OK;
 }
 
+int ensure_geometry(orbx_ctx* ctx, int w, int h) { return set_geometry(ctx, w, h); }
+
 // Make stream dst wait for everything queued so far on the extraction streams
 // (the context stream, stream2 and the pipeline part streams).
 static int order_after_extraction(orbx_ctx* ctx, hipStream_t dst)

@@ -357,6 +357,7 @@ void timer_begin(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 void timer_end(orbx_ctx* ctx, const char* name, hipStream_t st = nullptr);
 int ensure_scratch(orbx_ctx* ctx, size_t bytes);
 int ensure_aux_streams(orbx_ctx* ctx);   // stream2, the part streams and mstream (first batch use)
+int ensure_geometry(orbx_ctx* ctx, int w, int h);   // device tables and buffers for frames of w x h
 void lba_resident_free(orbx_ctx* ctx);
 int ensure_pinned(orbx_ctx* ctx, size_t bytes);
 }  // namespace orbx

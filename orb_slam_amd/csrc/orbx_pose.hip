@@ -36,29 +36,11 @@
 
 #include "orbx_device.h"
 #include "orbx_internal.h"
+#include "orbx_pose_dev.h"
 #include "orbx_se3.h"
 
 namespace orbx {
 
-struct PoseHdr {
-    long long e0;        // first edge in the SoA arrays
-    int nE;              // edges (keypoints with a map point)
-    int pad;
-    float T[12];         // initial Tcw rows 0..2
-    float cam[4];        // fx fy cx cy
-};
-
-struct PoseOut {
-    float T[12];
-    int n_inliers;
-    int rounds;
-    int iterations[4];
-    int trials[4];
-    int n_bad[4];
-    int not_posdef;
-    int pad;
-    double chi2_final[4];
-};
 
 constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
 // Edges per frame kept in LDS (6 floats + the outlier flag, 25 B each):
@@ -231,14 +213,6 @@ __device__ inline bool ldlt6_solve(double m[21], const double b[6], double x[6])
     return sign == 1 || sign == 0;
 }
 
-struct PoseEdgeArrays {
-    const float* ox;
-    const float* oy;
-    const float* isig;
-    const float* px;
-    const float* py;
-    const float* pz;
-};
 
 struct Cam {
     double fx, fy, cx, cy;
@@ -843,6 +817,24 @@ extern "C" int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* fram
 {
     return pose_stage_impl(ctx, P, frames, true);
 }
+
+namespace orbx {
+// P frames whose headers, edges, flags and outputs are already in device
+// memory (the tracking chain builds them on the device): the launch
+// orbx_pose_run makes (the same kernel selection).
+int launch_pose_device(orbx_ctx* ctx, const PoseHdr* hdrs, const PoseEdgeArrays& ed, uint8_t* flags, PoseOut* outs,
+                       int P)
+{
+    const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
+    const int per = kPoseThreads / 64;
+    const bool wide = !ctx->pose_exact && P <= ctx->pose_wide_max;
+    auto kern = ctx->pose_exact ? k_pose_opt<true> : (wide ? k_pose_opt<false, kPoseWideWaves> : k_pose_opt<false>);
+    const int blocks = wide ? P : (P + per - 1) / per, threads = wide ? 64 * kPoseWideWaves : kPoseThreads;
+    kern<<<blocks, threads, 0, ctx->stream>>>(hdrs, ed, flags, outs, P, delta);
+    ORBX_HIP_CHECK(hipGetLastError());
+    return ORBX_OK;
+}
+}  // namespace orbx
 
 extern "C" int orbx_pose_run(orbx_ctx* ctx)
 {

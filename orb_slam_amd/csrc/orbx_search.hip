@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "orbx_match_common.h"
+#include "orbx_pose_dev.h"
 
 namespace orbx {
 
@@ -189,6 +190,10 @@ struct SearchArgs {
     int32_t* fr_pred;             // n
     float* fr_cos;                // n
     int32_t* fr_count;            // points in view
+    // frames resident in slots (orbx_track_frame): keypoint counts on the
+    // device (F1.n / F2.n are then capacities)
+    const int32_t* F1_cnt;
+    const int32_t* F2_cnt;
 };
 
 // ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, float)
@@ -269,7 +274,7 @@ struct QuerySetup {
 template <int K>
 __device__ inline int query_count(const SearchArgs& a)
 {
-    return K == kQLocal ? a.nq : a.F1.n;
+    return K == kQLocal ? a.nq : (a.F1_cnt ? *a.F1_cnt : a.F1.n);
 }
 
 template <int K>
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(kAreaListWaves * 64) void k_area_lists(const Search
         if (a.fr_count && *a.fr_count == 0) return;
     }
     const FrameDev& F2 = a.F2;
-    const int n2 = F2.n;
+    const int n2 = a.F2_cnt ? *a.F2_cnt : F2.n;
     float* sx = reinterpret_cast<float*>(smem);
     float* sy = sx + n2;
     int* scode = reinterpret_cast<int*>(sy + n2);
@@ -457,7 +462,8 @@ __global__ __launch_bounds__(kReplayThreads) void k_area_replay(const SearchArgs
             return;
         }
     }
-    const int n2 = a.F2.n, nq = query_count<K>(a), tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n2 = a.F2_cnt ? *a.F2_cnt : a.F2.n, nq = query_count<K>(a), tid = threadIdx.x, lane = tid & 63,
+              wv = tid >> 6;
     CandTab t;
     carve_tab(smem, n2, t);
     signed char* bins = reinterpret_cast<signed char*>(t.taken + n2);
@@ -943,6 +949,240 @@ __global__ __launch_bounds__(256) void k_hamming_bf(const uint8_t* dA, int nA, c
         second[a] = b2;
         // C3 acceptance: best <= TH_LOW and best < nnratio * second
         if (m12) m12[a] = (b1 <= th_low && (float)b1 < __fmul_rn((float)b2, nnratio)) ? bi : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The tracking chain's glue (orbx_track_frame): one 1024-thread workgroup
+// between the searches and the PoseOptimization launches, reading and writing
+// the chain's state in device memory (no host round trip).
+// ---------------------------------------------------------------------------
+struct TrackOut {
+    float T[12];
+    int n_cur, status, n_motion, n_after_pose, n_in_view, n_local, n_inliers, err;
+};
+
+struct TrackDev {
+    const orbx_keypoint* cur_kps;   // the current frame's slot
+    const int32_t* cur_cnt;
+    const int32_t* last_mp;
+    const uint8_t* last_outlier;
+    int n_last, n_mp, cap;          // n_last: entries of last_mp / last_outlier
+    const int32_t* last_cnt;        // LastFrame in a slot: its keypoint count (else null)
+    const int32_t* err;             // the context's error flags (read back with the outputs)
+    const float* mp_pos;
+    const uint8_t* mp_skip_in;      // or null
+    const float* isig;
+    float Tpred[12], cam[4];
+    float* q_xyz;                   // motion search queries (last frame's points)
+    uint8_t* q_valid;
+    const int32_t* motion_out;      // k_area_replay<kQMotion>: last-frame index per current keypoint
+    const int32_t* motion_n;
+    int32_t* motion_out_w;          // the same, initialised by stage 0
+    int32_t* motion_n_w;
+    int32_t* local_out_w;           // the local search's, initialised by stage 2
+    int32_t* local_n_w;
+    const int32_t* local_out;       // k_area_replay<kQLocal>: local-map index per current keypoint
+    const int32_t* local_n;
+    int32_t* cur_mp;
+    uint8_t* f_assigned;
+    uint8_t* mp_skip;
+    SearchArgs* local_job;
+    PoseHdr* hdr;                   // 2 problems
+    float* edges;                   // 6 arrays x 2 cap
+    int32_t* edge_kp;               // 2 cap
+    const uint8_t* flags;           // 2 cap (k_pose_opt's outlier flags)
+    const PoseOut* pout;            // 2
+    int32_t* st;                    // status, n_motion, n_after_pose
+    TrackOut* out;                  // read-back block: TrackOut, cur_mp[cap], cur_outlier[cap]
+};
+
+constexpr int kTrackThreads = 1024;
+
+// PoseOptimization problem p from the current matches (edges in keypoint
+// order: g2o's insertion order, src/Optimizer.cc:187-231), initial pose T
+template <int kT>
+__device__ inline void track_build_pose(const TrackDev& d, int p, const float* T, bool run, int n,
+                                        BlockScratchN<kT / 64>& bs)
+{
+    const int tid = threadIdx.x;
+    float* ox = d.edges;
+    const size_t arr = (size_t)2 * d.cap;
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += kT) {
+        const int i = c0 + tid;
+        const int m = (run && i < n) ? d.cur_mp[i] : -1;
+        int tot;
+        const int pos = base + block_exclusive_scan(m >= 0 ? 1 : 0, &tot, bs, (c0 / kT) & 1);
+        if (m >= 0) {
+            const size_t e = (size_t)p * d.cap + pos;
+            const orbx_keypoint k = d.cur_kps[i];
+            ox[e] = k.x;
+            ox[arr + e] = k.y;
+            ox[2 * arr + e] = d.isig[k.octave];
+            ox[3 * arr + e] = d.mp_pos[3 * m];
+            ox[4 * arr + e] = d.mp_pos[3 * m + 1];
+            ox[5 * arr + e] = d.mp_pos[3 * m + 2];
+            d.edge_kp[e] = i;
+        }
+        base += tot;
+    }
+    if (tid == 0) {
+        PoseHdr& h = d.hdr[p];
+        h.e0 = (long long)p * d.cap;
+        h.nE = base;
+        h.pad = 0;
+        for (int k = 0; k < 12; k++) h.T[k] = T[k];
+        for (int k = 0; k < 4; k++) h.cam[k] = d.cam[k];
+    }
+}
+
+// stage 0: motion queries; 1: after the motion search; 2: after the first
+// PoseOptimization; 3: after the local-map search; 4: outputs
+__global__ __launch_bounds__(kTrackThreads) void k_track_stage(TrackDev d, int stage)
+{
+    __shared__ BlockScratchN<kTrackThreads / 64> bs;
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x;
+    const int n = *d.cur_cnt;
+    if (stage == 0) {
+        const int nl = d.last_cnt ? min(*d.last_cnt, d.n_last) : d.n_last;
+        for (int i = tid; i < d.n_last; i += kTrackThreads) {
+            const int m = i < nl ? d.last_mp[i] : -1;
+            const bool v = m >= 0 && m < d.n_mp && !d.last_outlier[i];
+            d.q_valid[i] = v;
+            d.q_xyz[3 * i] = v ? d.mp_pos[3 * m] : 0.f;
+            d.q_xyz[3 * i + 1] = v ? d.mp_pos[3 * m + 1] : 0.f;
+            d.q_xyz[3 * i + 2] = v ? d.mp_pos[3 * m + 2] : 0.f;
+        }
+        // SearchByProjection's outputs; the current frame's mvpMapPoints are
+        // cleared (src/Tracking.cc:581), nothing is assigned yet
+        for (int i = tid; i < d.cap; i += kTrackThreads) {
+            d.motion_out_w[i] = -1;
+            d.f_assigned[i] = 0;
+        }
+        if (tid == 0) {
+            d.st[0] = d.st[1] = d.st[2] = 0;
+            *d.motion_n_w = 0;
+        }
+        return;
+    }
+    const int status = d.st[0];
+    if (stage == 1) {
+        // mvpMapPoints of the current frame = the last frame's points found
+        // (src/ORBmatcher.cc:1575); < 20 matches: TrackWithMotionModel fails
+        for (int i = tid; i < n; i += kTrackThreads) {
+            const int m = d.motion_out[i];
+            d.cur_mp[i] = m >= 0 ? d.last_mp[m] : -1;
+        }
+        const int nm = *d.motion_n;
+        const bool run = nm >= 20;
+        __syncthreads();
+        track_build_pose<kTrackThreads>(d, 0, d.Tpred, run, n, bs);
+        if (tid == 0) {
+            d.st[0] = run ? 0 : 1;
+            d.st[1] = nm;
+        }
+        return;
+    }
+    if (stage == 2) {
+        // discard the outliers (src/Tracking.cc:592-603); < 10 left: fail
+        if (tid == 0) s_cnt = 0;
+        __syncthreads();
+        int nout = 0;
+        if (status == 0) {
+            const int nE = d.hdr[0].nE;
+            for (int e = tid; e < nE; e += kTrackThreads)
+                if (d.flags[e]) {
+                    d.cur_mp[d.edge_kp[e]] = -1;
+                    nout++;
+                }
+            if (nout) atomicAdd(&s_cnt, nout);
+        }
+        __syncthreads();
+        const int left = d.st[1] - s_cnt;
+        const bool ok = status == 0 && left >= 10;
+        // SearchReferencePointsInFrustum (src/Tracking.cc:701-752) with the
+        // pose just found: points matched already are not projected
+        for (int m = tid; m < d.n_mp; m += kTrackThreads) d.mp_skip[m] = d.mp_skip_in ? d.mp_skip_in[m] : 0;
+        for (int i = tid; i < d.cap; i += kTrackThreads) {
+            d.f_assigned[i] = 0;
+            d.local_out_w[i] = -1;
+        }
+        __syncthreads();
+        // matched points: bad ones are dropped, the others marked seen
+        // (mnLastFrameSeen, src/Tracking.cc:704-718)
+        if (ok)
+            for (int i = tid; i < n; i += kTrackThreads) {
+                const int m = d.cur_mp[i];
+                if (m < 0) continue;
+                if (d.mp_skip_in && d.mp_skip_in[m]) {
+                    d.cur_mp[i] = -1;
+                } else {
+                    d.f_assigned[i] = 1;
+                    d.mp_skip[m] = 1;
+                }
+            }
+        if (tid == 0) {
+            *d.local_n_w = 0;
+            SearchArgs& j = *d.local_job;
+            *j.fr_count = 0;
+            j.nq = ok ? d.n_mp : 0;
+            if (ok) {
+                // Frame::UpdatePoseMatrices (src/Frame.cc:129-134): Rcw, tcw,
+                // Ow = -Rcw^T tcw (float, left to right)
+                const float* T = d.pout[0].T;
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) j.Rcw[3 * r + c] = T[4 * r + c];
+                    j.tcw[r] = T[4 * r + 3];
+                }
+                for (int c = 0; c < 3; c++)
+                    j.Ow[c] = -__fadd_rn(__fadd_rn(__fmul_rn(T[c], T[3]), __fmul_rn(T[4 + c], T[7])),
+                                         __fmul_rn(T[8 + c], T[11]));
+            }
+            d.st[0] = status != 0 ? status : (ok ? 0 : 2);
+            d.st[2] = left;
+        }
+        return;
+    }
+    if (stage == 3) {
+        // the local-map matches join the frame's (SearchByProjection writes
+        // F.mvpMapPoints, src/ORBmatcher.cc:115); PoseOptimization again from
+        // the pose found (src/Tracking.cc:627)
+        const bool ok = status == 0;
+        if (ok && *d.local_job->fr_count > 0)
+            for (int i = tid; i < n; i += kTrackThreads) {
+                const int m = d.local_out[i];
+                if (m >= 0) d.cur_mp[i] = m;
+            }
+        __syncthreads();
+        track_build_pose<kTrackThreads>(d, 1, d.pout[0].T, ok, n, bs);
+        return;
+    }
+    // stage 4: outputs of the last PoseOptimization that ran
+    int32_t* cur_mp_out = reinterpret_cast<int32_t*>(d.out + 1);
+    uint8_t* cur_out = reinterpret_cast<uint8_t*>(cur_mp_out + d.cap);
+    for (int i = tid; i < d.cap; i += kTrackThreads) {
+        cur_mp_out[i] = i < n ? d.cur_mp[i] : -1;
+        cur_out[i] = 0;
+    }
+    __syncthreads();
+    if (status == 0) {
+        const int nE = d.hdr[1].nE;
+        for (int e = tid; e < nE; e += kTrackThreads) cur_out[d.edge_kp[(size_t)d.cap + e]] = d.flags[(size_t)d.cap + e];
+    }
+    if (tid == 0) {
+        TrackOut& o = *d.out;
+        const float* T = status == 0 ? d.pout[1].T : status == 2 ? d.pout[0].T : d.Tpred;
+        for (int k = 0; k < 12; k++) o.T[k] = T[k];
+        o.n_cur = n;
+        o.status = status;
+        o.n_motion = d.st[1];
+        o.n_after_pose = status == 1 ? 0 : d.st[2];
+        o.n_in_view = status == 0 ? *d.local_job->fr_count : 0;
+        o.n_local = (status == 0 && *d.local_job->fr_count > 0) ? *d.local_n : 0;
+        o.n_inliers = status == 0 ? d.pout[1].n_inliers : status == 2 ? d.pout[0].n_inliers : 0;
+        o.err = *d.err;
     }
 }
 
@@ -1530,6 +1770,232 @@ static int hamming_bf_impl(orbx_ctx* ctx, const uint8_t* dA, int nA, const uint8
     pin.get(second, o2, (size_t)nA * 4);
     pin.get(m12, om, (size_t)nA * 4);
     return ORBX_OK;
+}
+
+// Tracking::TrackWithMotionModel + TrackLocalMap on the device (see
+// include/orbx.h): one upload, the extraction of the slot, nine launches
+// (glue, two-phase motion search, glue, PoseOptimization, glue, frustum,
+// two-phase local search, glue, PoseOptimization, glue), one read-back.
+int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
+{
+    if (!ctx || !q) return ORBX_ERR_ARG;
+    const bool from_slot = q->last_slot >= 0;
+    if (q->slot < 0 || q->slot >= ctx->slots || q->last_slot >= ctx->slots || q->last_slot == q->slot ||
+        (!from_slot && !valid_view(q->last)) || (from_slot && q->last_cap < 0) || q->n_mp < 0 ||
+        (q->n_mp > 0 && (!q->mp_pos || !q->mp_normal || !q->mp_dist || !q->mp_desc)) || !q->Tcw_pred || !q->cam ||
+        !q->inv_level_sigma2 || !q->cur_mp || !q->cur_outlier || q->cap < 0 || q->nlevels <= 0 ||
+        q->nlevels > kMaxLevels)
+        return ORBX_ERR_ARG;
+    const int n1 = from_slot ? q->last_cap : q->last->n;
+    if (from_slot && n1 > ctx->geom.nfeatures) return ORBX_ERR_ARG;
+    if (n1 > 0 && (!q->last_mp || !q->last_outlier)) return ORBX_ERR_ARG;
+    if (q->image && (q->w <= 0 || q->h <= 0 || q->stride < (size_t)q->w)) return ORBX_ERR_ARG;
+    ctx_enter(ctx);
+    int r = ORBX_OK;
+    if (q->image && (r = ensure_geometry(ctx, q->w, q->h)) != ORBX_OK) return r;
+    if (ctx->geom_w <= 0 || q->nlevels != ctx->geom.nlevels) return ORBX_ERR_ARG;
+    for (int i = 0; i < n1; i++)
+        if (q->last_mp[i] >= q->n_mp) return ORBX_ERR_ARG;
+    const Geometry& g = ctx->geom;
+    const int nf = g.nfeatures, m = q->n_mp, cap = std::max(nf, 1);
+    const size_t img_bytes = q->image ? (size_t)q->w * q->h : 0;
+    // [inputs | SearchArgs x2 | read-back block | device-only state]
+    Uploader u{ctx};
+    FrameOffs oL{};
+    if (!from_slot) oL = reserve_frame(u, q->last);
+    const size_t o_lmp = u.reserve((size_t)n1 * 4), o_lout = u.reserve(n1);
+    const size_t o_pos = u.reserve((size_t)m * 12), o_nrm = u.reserve((size_t)m * 12), o_dist = u.reserve((size_t)m * 8);
+    const size_t o_desc = u.reserve((size_t)m * 32), o_skin = u.reserve(m), o_isig = u.reserve(4 * kMaxLevels);
+    const size_t o_img = u.reserve(img_bytes);
+    const size_t o_jm = u.reserve(sizeof(SearchArgs)), o_jl = u.reserve(sizeof(SearchArgs)), in_end = u.total;
+    const size_t o_out = u.reserve(sizeof(TrackOut) + (size_t)cap * 5), out_end = u.total;
+    const size_t o_qxyz = u.reserve((size_t)n1 * 12), o_qv = u.reserve(n1);
+    const size_t o_mout = u.reserve((size_t)cap * 4 + 4), o_mn = u.reserve(4);
+    const size_t o_lo = u.reserve((size_t)cap * 4 + 4), o_ln = u.reserve(4), o_cnt = u.reserve(4);
+    const size_t o_fiv = u.reserve(m), o_fpr = u.reserve((size_t)m * 8), o_fpl = u.reserve((size_t)m * 4);
+    const size_t o_fcos = u.reserve((size_t)m * 4), o_cmp = u.reserve((size_t)cap * 4), o_fas = u.reserve(cap);
+    const size_t o_skip = u.reserve(m), o_hdr = u.reserve(2 * sizeof(PoseHdr)), o_edg = u.reserve((size_t)cap * 48);
+    const size_t o_ekp = u.reserve((size_t)cap * 8), o_flg = u.reserve((size_t)cap * 2);
+    const size_t o_pout = u.reserve(2 * sizeof(PoseOut)), o_st = u.reserve(16);
+    const AreaBufs am = reserve_area(u, 1, n1), al = reserve_area(u, 1, m);
+    r = ensure_scratch(ctx, u.total);
+    Pinned pin{ctx};
+    if (r == ORBX_OK) r = pin.open(out_end);
+    if (r != ORBX_OK) return r;
+    uint8_t* d = u.base();
+    if (!from_slot) put_frame(pin, oL, q->last);
+    pin.put(o_lmp, q->last_mp, (size_t)n1 * 4);
+    pin.put(o_lout, q->last_outlier, n1);
+    pin.put(o_pos, q->mp_pos, (size_t)m * 12);
+    pin.put(o_nrm, q->mp_normal, (size_t)m * 12);
+    pin.put(o_dist, q->mp_dist, (size_t)m * 8);
+    pin.put(o_desc, q->mp_desc, (size_t)m * 32);
+    if (q->mp_skip) pin.put(o_skin, q->mp_skip, m);
+    pin.put(o_isig, q->inv_level_sigma2, (size_t)q->nlevels * 4);
+    if (q->image) {
+        if (q->stride == (size_t)q->w) {
+            pin.put(o_img, q->image, img_bytes);
+        } else {
+            for (int y = 0; y < q->h; y++) pin.put(o_img + (size_t)y * q->w, q->image + (size_t)y * q->stride, q->w);
+        }
+    }
+    // the slots' frames: keypoints where extraction left them, the count on
+    // the device, bounds of orbx_dev_set_image_bounds (default the image)
+    auto slot_frame = [&](int slot) {
+        FrameDev F;
+        F.kps = ctx->out_kps + (size_t)slot * nf;
+        F.desc = ctx->out_desc + (size_t)slot * nf * 32;
+        F.n = nf;
+        F.min_x = ctx->has_bounds ? ctx->bounds[0] : 0.f;
+        F.max_x = ctx->has_bounds ? ctx->bounds[1] : (float)g.w;
+        F.min_y = ctx->has_bounds ? ctx->bounds[2] : 0.f;
+        F.max_y = ctx->has_bounds ? ctx->bounds[3] : (float)g.h;
+        F.grid_w_inv = static_cast<float>(kGridCols) / (F.max_x - F.min_x);
+        F.grid_h_inv = static_cast<float>(kGridRows) / (F.max_y - F.min_y);
+        return F;
+    };
+    float scale[kMaxLevels] = {};
+    scale[0] = 1.0f;
+    for (int i = 1; i < g.nlevels; i++) scale[i] = scale[i - 1] * g.scale_factor;   // src/Frame.cc:98-102
+    // SearchByProjection(mCurrentFrame, mLastFrame, 15), ORBmatcher(0.9, true)
+    // (src/Tracking.cc:574-584): queries = the last frame's keypoints
+    SearchArgs jm{};
+    jm.F1 = from_slot ? slot_frame(q->last_slot) : dev_frame(q->last, d, oL.kp, oL.desc);
+    jm.F2 = slot_frame(q->slot);
+    jm.F2_cnt = ctx->out_n + q->slot;
+    if (from_slot) jm.F1.n = n1;   // queries past the slot's count are not valid (k_track_stage 0)
+    jm.q_xyz = reinterpret_cast<const float*>(d + o_qxyz);
+    jm.q_valid = d + o_qv;
+    jm.f2_assigned = d + o_fas;
+    for (int i = 0; i < 12; i++) jm.T[i] = q->Tcw_pred[i];
+    for (int i = 0; i < 4; i++) jm.cam[i] = q->cam[i];
+    std::memcpy(jm.scale, scale, sizeof(scale));
+    jm.th = 15.f;
+    jm.check_ori = 1;
+    jm.out = reinterpret_cast<int32_t*>(d + o_mout);
+    jm.out_n = reinterpret_cast<int32_t*>(d + o_mn);
+    // SearchReferencePointsInFrustum (src/Tracking.cc:701-752): the pose and
+    // the query count are filled in on the device (k_track_stage 2)
+    SearchArgs jl{};
+    jl.F2 = slot_frame(q->slot);
+    jl.F2_cnt = ctx->out_n + q->slot;
+    jl.nq = 0;
+    jl.q_xyz = reinterpret_cast<const float*>(d + o_pos);
+    jl.mp_normal = reinterpret_cast<const float*>(d + o_nrm);
+    jl.mp_dist = reinterpret_cast<const float*>(d + o_dist);
+    jl.mp_skip = d + o_skip;
+    jl.q_desc = d + o_desc;
+    jl.f2_assigned = d + o_fas;
+    for (int i = 0; i < 4; i++) jl.cam[i] = q->cam[i];
+    std::memcpy(jl.scale, scale, sizeof(scale));
+    jl.nlevels = g.nlevels;
+    jl.view_cos_limit = 0.5f;
+    jl.th = q->th_local;
+    jl.nnratio = 0.8f;
+    jl.fr_in_view = d + o_fiv;
+    jl.fr_proj = reinterpret_cast<float*>(d + o_fpr);
+    jl.fr_pred = reinterpret_cast<int32_t*>(d + o_fpl);
+    jl.fr_cos = reinterpret_cast<float*>(d + o_fcos);
+    jl.fr_count = reinterpret_cast<int32_t*>(d + o_cnt);
+    jl.q_valid = jl.fr_in_view;
+    jl.proj_xy = jl.fr_proj;
+    jl.pred_level = jl.fr_pred;
+    jl.view_cos = jl.fr_cos;
+    jl.out = reinterpret_cast<int32_t*>(d + o_lo);
+    jl.out_n = reinterpret_cast<int32_t*>(d + o_ln);
+    pin.put(o_jm, &jm, sizeof(jm));
+    pin.put(o_jl, &jl, sizeof(jl));
+    TrackDev td{};
+    td.cur_kps = jm.F2.kps;
+    td.cur_cnt = jm.F2_cnt;
+    td.last_mp = reinterpret_cast<const int32_t*>(d + o_lmp);
+    td.last_outlier = d + o_lout;
+    td.n_last = n1;
+    td.last_cnt = from_slot ? ctx->out_n + q->last_slot : nullptr;
+    td.err = ctx->error_flags;
+    td.n_mp = m;
+    td.cap = cap;
+    td.mp_pos = jl.q_xyz;
+    td.mp_skip_in = q->mp_skip ? d + o_skin : nullptr;
+    td.isig = reinterpret_cast<const float*>(d + o_isig);
+    for (int i = 0; i < 12; i++) td.Tpred[i] = q->Tcw_pred[i];
+    for (int i = 0; i < 4; i++) td.cam[i] = q->cam[i];
+    td.q_xyz = reinterpret_cast<float*>(d + o_qxyz);
+    td.q_valid = d + o_qv;
+    td.motion_out = jm.out;
+    td.motion_n = jm.out_n;
+    td.local_out = jl.out;
+    td.local_n = jl.out_n;
+    td.motion_out_w = jm.out;
+    td.motion_n_w = jm.out_n;
+    td.local_out_w = jl.out;
+    td.local_n_w = jl.out_n;
+    td.cur_mp = reinterpret_cast<int32_t*>(d + o_cmp);
+    td.f_assigned = d + o_fas;
+    td.mp_skip = d + o_skip;
+    td.local_job = reinterpret_cast<SearchArgs*>(d + o_jl);
+    td.hdr = reinterpret_cast<PoseHdr*>(d + o_hdr);
+    td.edges = reinterpret_cast<float*>(d + o_edg);
+    td.edge_kp = reinterpret_cast<int32_t*>(d + o_ekp);
+    td.flags = d + o_flg;
+    td.pout = reinterpret_cast<const PoseOut*>(d + o_pout);
+    td.st = reinterpret_cast<int32_t*>(d + o_st);
+    td.out = reinterpret_cast<TrackOut*>(d + o_out);
+    // one upload; the image into its slot and the slot's extraction
+    if ((r = pin.upload(in_end)) != ORBX_OK) return r;
+    if (q->image) {
+        ORBX_HIP_CHECK(hipMemcpyAsync(ctx->frames + (size_t)q->slot * img_bytes, d + o_img, img_bytes,
+                                      hipMemcpyDeviceToDevice, ctx->stream));
+        ctx->last_first = q->slot;
+        ctx->last_count = 1;
+        ctx->single_frame = true;   // the latency-first single-frame launches
+        r = launch_extract(ctx, q->slot, 1);
+        ctx->single_frame = false;
+        if (r != ORBX_OK) return r;
+    }
+    PoseEdgeArrays ed;
+    const size_t arr = (size_t)2 * cap;
+    ed.ox = td.edges;
+    ed.oy = td.edges + arr;
+    ed.isig = td.edges + 2 * arr;
+    ed.px = td.edges + 3 * arr;
+    ed.py = td.edges + 4 * arr;
+    ed.pz = td.edges + 5 * arr;
+    uint8_t* flags = d + o_flg;
+    PoseOut* pout = reinterpret_cast<PoseOut*>(d + o_pout);
+    const SearchArgs* dm = reinterpret_cast<const SearchArgs*>(d + o_jm);
+    const SearchArgs* dl = reinterpret_cast<const SearchArgs*>(d + o_jl);
+    auto stage = [&](int s) { hipLaunchKernelGGL(k_track_stage, dim3(1), dim3(kTrackThreads), 0, ctx->stream, td, s); };
+    stage(0);
+    if ((r = launch_area_search<kQMotion>(ctx, dm, 1, n1, nf, u, am)) != ORBX_OK) return r;
+    stage(1);
+    if ((r = launch_pose_device(ctx, td.hdr, ed, flags, pout, 1)) != ORBX_OK) return r;
+    stage(2);
+    if (m > 0) hipLaunchKernelGGL(k_frustum, dim3((m + 255) / 256, 1), dim3(256), 0, ctx->stream, dl);
+    if ((r = launch_area_search<kQLocal>(ctx, dl, 1, m, nf, u, al)) != ORBX_OK) return r;
+    stage(3);
+    if ((r = launch_pose_device(ctx, td.hdr + 1, ed, flags, pout + 1, 1)) != ORBX_OK) return r;
+    stage(4);
+    ORBX_HIP_CHECK(hipGetLastError());
+    if ((r = pin.download(o_out, out_end)) != ORBX_OK) return r;
+    TrackOut o;
+    pin.get(&o, o_out, sizeof(o));
+    for (int i = 0; i < 12; i++) q->Tcw[i] = o.T[i];
+    q->n_cur = o.n_cur;
+    q->status = o.status;
+    q->n_motion = o.n_motion;
+    q->n_after_pose = o.n_after_pose;
+    q->n_in_view = o.n_in_view;
+    q->n_local = o.n_local;
+    q->n_inliers = o.n_inliers;
+    const int nc = std::min(o.n_cur, q->cap);
+    pin.get(q->cur_mp, o_out + sizeof(TrackOut), (size_t)nc * 4);
+    pin.get(q->cur_outlier, o_out + sizeof(TrackOut) + (size_t)cap * 4, nc);
+    if (o.err) {   // an extraction overflow (k_track_stage read the flags)
+        ORBX_HIP_CHECK(hipMemsetAsync(ctx->error_flags, 0, sizeof(int32_t), ctx->stream));
+        return ORBX_ERR_CAPACITY;
+    }
+    return o.n_cur > q->cap ? ORBX_ERR_CAPACITY : ORBX_OK;
 }
 
 int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q)

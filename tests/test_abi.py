@@ -66,6 +66,7 @@ def test_context_setters_refuse_null_context():
         ("orbx_get_launch_mode", (None,)),
         ("orbx_dev_upload_async", (None, 0, 1, None, 640, 480, 640)),
         ("orbx_dev_download_async", (None, 0, 1, None, None, None, None, None)),
+        ("orbx_track_frame", (None, None)),
     ]
     for name, args in calls:
         assert getattr(lib, name)(*args) == err_arg, name

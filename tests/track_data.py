@@ -1,0 +1,223 @@
+"""One Tracking frame (Tracking::TrackWithMotionModel + TrackLocalMap,
+src/Tracking.cc:572-627, 701-752): the ctypes view of orbx_track_query, a
+synthetic two-frame scene, and the chain restated over the oracle's
+matchers and PoseOptimization (test data and checker only).
+
+Scene: a textured plane 4 m in front of the last camera (identity pose);
+the current camera is translated so the image moves by `shift` pixels, the
+motion-model prediction misses by `pred_err` pixels.  The local map is the
+last frame's keypoints back-projected onto the plane (descriptors, normals,
+the distance range MapPoint::UpdateNormalAndDepth derives from the
+observing octave) plus random points; the last frame observes a subset.
+"""
+import ctypes
+
+import numpy as np
+
+import orb_slam_amd as ox
+from orb_slam_amd import synth_pose as sp
+
+CAM = np.array([500.0, 500.0, 320.0, 240.0], np.float32)
+DEPTH = 4.0
+vp = ctypes.c_void_p
+
+
+class TrackQuery(ctypes.Structure):
+    _fields_ = [("slot", ctypes.c_int), ("image", vp), ("w", ctypes.c_int), ("h", ctypes.c_int),
+                ("stride", ctypes.c_size_t), ("last_slot", ctypes.c_int), ("last_cap", ctypes.c_int),
+                ("last", vp), ("last_mp", vp), ("last_outlier", vp), ("n_mp", ctypes.c_int),
+                ("mp_pos", vp), ("mp_normal", vp), ("mp_dist", vp), ("mp_desc", vp), ("mp_skip", vp),
+                ("Tcw_pred", vp), ("cam", vp), ("inv_level_sigma2", vp), ("nlevels", ctypes.c_int),
+                ("th_local", ctypes.c_float), ("Tcw", ctypes.c_float * 12), ("cur_mp", vp),
+                ("cur_outlier", vp), ("cap", ctypes.c_int), ("n_cur", ctypes.c_int), ("status", ctypes.c_int),
+                ("n_motion", ctypes.c_int), ("n_after_pose", ctypes.c_int), ("n_in_view", ctypes.c_int),
+                ("n_local", ctypes.c_int), ("n_inliers", ctypes.c_int)]
+
+
+def texture(w, h, seed):
+    """Blob texture with corners at several scales (FAST finds them on every
+    pyramid level)."""
+    from scipy.ndimage import gaussian_filter
+    r = np.random.default_rng(seed)
+    img = np.zeros((h, w), np.float64)
+    for sigma, amp in ((1.2, 1.0), (3.0, 1.5), (8.0, 2.0)):
+        img += amp * gaussian_filter(r.normal(size=(h, w)), sigma) * sigma
+    img = (img - img.min()) / (img.max() - img.min())
+    return np.ascontiguousarray((img * 255).astype(np.uint8))
+
+
+def images(w, h, shift, seed):
+    """(last, current): crops of one texture `shift` pixels apart
+    (current(x) = last(x + shift))."""
+    tex = texture(w + 64, h, seed)
+    return (np.ascontiguousarray(tex[:, 32:32 + w]), np.ascontiguousarray(tex[:, 32 + shift:32 + shift + w]))
+
+
+def pose_x(cx):
+    """Tcw (3 x 4 rows, float) of a camera at (cx, 0, 0) looking down +z."""
+    T = np.zeros(12, np.float32)
+    T[0] = T[5] = T[10] = 1.0
+    T[3] = -cx
+    return T
+
+
+def inv_sigma2(nlevels=8, scale=1.2):
+    s = np.float32(1.0)
+    out = []
+    for _ in range(nlevels):   # Frame: mvLevelSigma2 = scale^(2l), float products
+        out.append(np.float32(1.0) / (s * s))
+        s = np.float32(s * np.float32(scale))
+    return np.array(out, np.float32)
+
+
+def make_scene(kl, dl, seed, n_extra=400, observed=0.8, outlier=0.05, bad=0.02, nlevels=8, scale=1.2):
+    """Local map around the last frame's keypoints (kl, dl): arrays dict."""
+    r = np.random.default_rng(seed)
+    nl = len(kl)
+    u = kl["x"].astype(np.float64)
+    v = kl["y"].astype(np.float64)
+    P0 = np.stack([(u - CAM[2]) / CAM[0] * DEPTH, (v - CAM[3]) / CAM[1] * DEPTH, np.full(nl, DEPTH)], 1)
+    P1 = np.stack([r.uniform(-3, 3, n_extra), r.uniform(-2.5, 2.5, n_extra), r.uniform(2.0, 7.0, n_extra)], 1)
+    P = np.concatenate([P0, P1]).astype(np.float32)
+    n = len(P)
+    dist = np.linalg.norm(P.astype(np.float64), axis=1)
+    normal = (P / dist[:, None]).astype(np.float32)
+    level = np.concatenate([kl["octave"], r.integers(0, nlevels, n_extra)]).astype(np.int64)
+    sf = scale ** np.arange(nlevels)
+    dmax = dist * sf[level]
+    dmin = dmax / sf[-1]
+    desc = np.concatenate([dl, r.integers(0, 256, (n_extra, 32), dtype=np.uint8)])
+    last_mp = np.where(r.random(nl) < observed, np.arange(nl), -1).astype(np.int32)
+    last_out = ((r.random(nl) < outlier) & (last_mp >= 0)).astype(np.uint8)
+    skip = (r.random(n) < bad).astype(np.uint8)
+    return dict(pos=np.ascontiguousarray(P), normal=np.ascontiguousarray(normal),
+                dist=np.ascontiguousarray(np.stack([dmin, dmax], 1).astype(np.float32)),
+                desc=np.ascontiguousarray(desc), skip=skip, last_mp=last_mp, last_outlier=last_out,
+                isig=inv_sigma2(nlevels, scale), cam=CAM.copy())
+
+
+def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h=480, cap=1000, th_local=1.0):
+    """orbx_track_query over the scene's arrays; returns (query, keep-alive
+    dict with the output arrays cur_mp / cur_outlier)."""
+    keep = dict(scene)
+    keep["Tpred"] = np.ascontiguousarray(Tpred, np.float32)
+    keep["cur_mp"] = np.full(cap, -7, np.int32)
+    keep["cur_outlier"] = np.full(cap, 7, np.uint8)
+    q = TrackQuery()
+    q.slot = slot
+    if image is not None:
+        keep["image"] = np.ascontiguousarray(image, np.uint8)
+        q.image = keep["image"].ctypes.data
+        q.h, q.w = image.shape
+        q.stride = q.w
+    else:
+        q.w, q.h, q.stride = w, h, w
+    q.last_slot = last_slot
+    q.last_cap = len(scene["last_mp"])
+    if last_view is not None:
+        keep["last_view"] = last_view
+        q.last = ctypes.addressof(last_view)
+    q.last_mp = scene["last_mp"].ctypes.data
+    q.last_outlier = scene["last_outlier"].ctypes.data
+    q.n_mp = len(scene["pos"])
+    for f, k in (("mp_pos", "pos"), ("mp_normal", "normal"), ("mp_dist", "dist"), ("mp_desc", "desc"),
+                 ("mp_skip", "skip"), ("cam", "cam"), ("inv_level_sigma2", "isig")):
+        setattr(q, f, keep[k].ctypes.data)
+    q.Tcw_pred = keep["Tpred"].ctypes.data
+    q.nlevels = len(scene["isig"])
+    q.th_local = th_local
+    q.cur_mp = keep["cur_mp"].ctypes.data
+    q.cur_outlier = keep["cur_outlier"].ctypes.data
+    q.cap = cap
+    return q, keep
+
+
+def result(q, keep):
+    n = q.n_cur
+    return dict(Tcw=np.frombuffer(bytes(q.Tcw), np.float32).copy(), status=q.status, n_cur=n,
+                n_motion=q.n_motion, n_after_pose=q.n_after_pose, n_in_view=q.n_in_view, n_local=q.n_local,
+                n_inliers=q.n_inliers, cur_mp=keep["cur_mp"][:n].copy(), cur_outlier=keep["cur_outlier"][:n].copy())
+
+
+def _ref_pose(L, kc, cur_mp, scene, T12):
+    n = len(kc)
+    has = (cur_mp >= 0).astype(np.uint8)
+    xyz = np.zeros((n, 3), np.float32)
+    xyz[has.astype(bool)] = scene["pos"][cur_mp[has.astype(bool)]]
+    T = np.eye(4, dtype=np.float32)
+    T[:3] = np.asarray(T12, np.float32).reshape(3, 4)
+    fr = dict(kp_un=np.stack([kc["x"], kc["y"]], 1).astype(np.float32), octave=kc["octave"].astype(np.int32),
+              inv_level_sigma2=scene["isig"], has_mp=has, mp_xyz=xyz, cam=scene["cam"], Tcw=T,
+              outlier=np.zeros(n, np.uint8))
+    p, arrs = sp.to_ctypes(fr)
+    ni = ctypes.c_int()
+    L.orbx_ref_pose_optimization.argtypes = [vp, vp, vp]
+    assert L.orbx_ref_pose_optimization(ctypes.byref(p), ctypes.byref(ni), None) == 0
+    return sp.pose_of(p)[:3].reshape(-1).copy(), arrs["outlier"].copy(), ni.value
+
+
+def ref_chain(L, kl, dl, kc, dc, scene, Tpred, w=640, h=480, th_local=1.0, nlevels=8, scale=1.2):
+    """The chain of include/orbx.h's orbx_track_frame over the oracle:
+    SearchByProjection(cur, last, 15) -> PoseOptimization -> discard ->
+    SearchReferencePointsInFrustum -> PoseOptimization."""
+    from local_map_data import LocalMapQuery
+    nl, nc = len(kl), len(kc)
+    Lv = ox.frame_view(kl, dl, w, h, nlevels, scale)
+    Cv = ox.frame_view(kc, dc, w, h, nlevels, scale)
+    lmp = scene["last_mp"]
+    valid = ((lmp >= 0) & (scene["last_outlier"] == 0)).astype(np.uint8)
+    xyz = np.zeros((nl, 3), np.float32)
+    xyz[valid.astype(bool)] = scene["pos"][lmp[valid.astype(bool)]]
+    Tp = np.ascontiguousarray(Tpred, np.float32)
+    mc = np.zeros(nc, np.int32)
+    nm = ctypes.c_int()
+    assert L.orbx_ref_search_by_projection_motion(ctypes.addressof(Cv), ctypes.addressof(Lv), xyz.ctypes.data,
+                                                  valid.ctypes.data, np.zeros(nc, np.uint8).ctypes.data,
+                                                  Tp.ctypes.data, scene["cam"].ctypes.data, 15.0, 1,
+                                                  mc.ctypes.data, ctypes.byref(nm)) == 0
+    cur_mp = np.where(mc >= 0, lmp[np.maximum(mc, 0)], -1).astype(np.int32)
+    out = dict(n_cur=nc, n_motion=nm.value, n_after_pose=0, n_in_view=0, n_local=0, n_inliers=0,
+               cur_outlier=np.zeros(nc, np.uint8))
+    if nm.value < 20:
+        out.update(status=1, Tcw=Tp.copy(), cur_mp=cur_mp)
+        return out
+    T0, fl0, ni0 = _ref_pose(L, kc, cur_mp, scene, Tp)
+    left = nm.value - int(np.count_nonzero(fl0 & (cur_mp >= 0)))
+    cur_mp = np.where(fl0.astype(bool), -1, cur_mp).astype(np.int32)
+    out["n_after_pose"] = left
+    if left < 10:
+        out.update(status=2, Tcw=T0, cur_mp=cur_mp, n_inliers=ni0)
+        return out
+    # SearchReferencePointsInFrustum: bad matched points dropped, the rest
+    # not projected again; Ow = -Rcw^T tcw in float, left to right
+    skip_in = scene["skip"]
+    bad = (cur_mp >= 0) & (skip_in[np.maximum(cur_mp, 0)] != 0)
+    cur_mp = np.where(bad, -1, cur_mp).astype(np.int32)
+    skip = skip_in.copy()
+    skip[cur_mp[cur_mp >= 0]] = 1
+    assigned = (cur_mp >= 0).astype(np.uint8)
+    T = T0.reshape(3, 4)
+    Rcw = np.ascontiguousarray(T[:, :3])
+    tcw = np.ascontiguousarray(T[:, 3])
+    f32 = np.float32
+    Ow = np.array([-((f32(T[0, c]) * T[0, 3] + f32(T[1, c]) * T[1, 3]) + f32(T[2, c]) * T[2, 3]) for c in range(3)],
+                  np.float32)
+    n = len(scene["pos"])
+    matches = np.zeros(nc, np.int32)
+    q = LocalMapQuery()
+    q.frame = ctypes.addressof(Cv)
+    keep = [Rcw, tcw, Ow, skip, assigned, matches]
+    q.Rcw, q.tcw, q.Ow, q.cam = Rcw.ctypes.data, tcw.ctypes.data, Ow.ctypes.data, scene["cam"].ctypes.data
+    q.n_mp = n
+    q.mp_pos, q.mp_normal, q.mp_dist = scene["pos"].ctypes.data, scene["normal"].ctypes.data, scene["dist"].ctypes.data
+    q.mp_skip, q.mp_desc, q.f_assigned = skip.ctypes.data, scene["desc"].ctypes.data, assigned.ctypes.data
+    q.view_cos_limit, q.th, q.nnratio = 0.5, th_local, 0.8
+    q.matches_f = matches.ctypes.data
+    L.orbx_ref_search_local_map.argtypes = [vp]
+    assert L.orbx_ref_search_local_map(ctypes.byref(q)) == 0
+    del keep
+    cur_mp = np.where(matches >= 0, matches, cur_mp).astype(np.int32)
+    T1, fl1, ni1 = _ref_pose(L, kc, cur_mp, scene, T0)
+    out.update(status=0, Tcw=T1, cur_mp=cur_mp, cur_outlier=np.where(cur_mp >= 0, fl1, 0).astype(np.uint8),
+               n_in_view=q.n_in_view, n_local=q.n_matches if q.n_in_view > 0 else 0, n_inliers=ni1)
+    return out

@@ -7,8 +7,11 @@ repo root on the GPU box, under `rocprofv3 --kernel-trace --memory-copy-trace
   sfi       orbx_search_for_initialization on two host frame views
   pose      orbx_pose_optimization on one frame
   lba       orbx_lba_solve on one 20 KF x 2000 MP problem
+  search    the Tracking searches on host frame views
+  track     orbx_track_frame: one whole Tracking frame (image in), then the
+            chain alone (slot already extracted)
 
-usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [--n N] [--lbawg g,...] [--coop c,...]
+usage: python tools/single_call.py [extract] [sfi] [pose] [lba] [search] [track] [--n N] [--lbawg g,...] [--coop c,...]
 """
 import ctypes
 import sys
@@ -25,7 +28,7 @@ from orb_slam_amd import synth  # noqa: E402
 
 args = sys.argv[1:]
 n = int(args[args.index("--n") + 1]) if "--n" in args else 100
-what = [a for a in args if a in ("extract", "sfi", "pose", "lba", "search")] or ["extract"]
+what = [a for a in args if a in ("extract", "sfi", "pose", "lba", "search", "track")] or ["extract"]
 lbawg = [int(v) for v in args[args.index("--lbawg") + 1].split(",")] if "--lbawg" in args else [0]
 # k_lba_split launch: -1 the device's choice, 0 plain, 1 cooperative (orbx_debug_lba_split)
 coop = [int(v) for v in args[args.index("--coop") + 1].split(",")] if "--coop" in args else [-1]
@@ -123,6 +126,29 @@ if "search" in what:
         print(f"search {name}: gpu {tg:.4f} ms, cpu port {med(c, max(5, n // 4)):.4f} ms median; "
               f"replay rounds {(dbg[0] - r0[0]) / n:.2f} per call, sequential fallbacks {dbg[1] - r0[1]} of {n}",
               flush=True)
+    ctx.close()
+
+if "track" in what:
+    import track_data as td
+    W, H = 640, 480
+    ctx = ox.Context(nfeatures=1000, max_w=W, max_h=H, slots=3)
+    last_img, cur_img = td.images(W, H, 6, 11)
+    ctx.upload(last_img, 0)
+    ctx.extract(0, 1)
+    ctx.sync()
+    kl, dl = ctx.features(0)
+    scene = td.make_scene(kl, dl, 11)
+    Tp = td.pose_x(7.5 * td.DEPTH / float(td.CAM[0]))
+    qi, ki = td.query(scene, Tp, slot=1, image=cur_img, last_slot=0)
+    qs, ks = td.query(scene, Tp, slot=1, last_slot=0)
+    for exact in (0, 1):
+        assert L.orbx_pose_set_exact(ctx.handle, exact) == 0
+        ti = med(lambda i: L.orbx_track_frame(ctx.handle, ctypes.byref(qi)), n)
+        tc = med(lambda i: L.orbx_track_frame(ctx.handle, ctypes.byref(qs)), n)
+        r = td.result(qs, ks)
+        print(f"track (exact sums {exact}): image in {ti:.4f} ms, chain only {tc:.4f} ms median; status "
+              f"{r['status']} motion {r['n_motion']} in view {r['n_in_view']} local {r['n_local']} "
+              f"inliers {r['n_inliers']}", flush=True)
     ctx.close()
 
 if "pose" in what:
