@@ -42,7 +42,9 @@ extern "C" {
  *   4: orbx_pose_set_exact / orbx_pose_get_exact; additions only.
  *   5: the measured-slower opt-in modes removed (orbx_dev_set_pyramid_mode,
  *      orbx_dev_pyramid_fused / _kind, orbx_dev_set_fast_chunk / get, launch
- *      modes 2 and 3); orbx_lba_last_workgroups, orbx_debug_lba_split. */
+ *      modes 2 and 3); orbx_lba_last_workgroups, orbx_debug_lba_split;
+ *      orbx_track_frame (one Tracking frame on the device); PoseOptimization
+ *      sums sequentially in g2o's order by default (orbx_pose_set_exact). */
 #define ORBX_ABI_VERSION 5
 int orbx_abi_version(void);
 
@@ -851,17 +853,20 @@ int orbx_pose_stage(orbx_ctx* ctx, int P, const orbx_pose_frame* frames);
 int orbx_pose_run(orbx_ctx* ctx);
 int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* n_inliers,
                     orbx_pose_stats* stats);
-/* Summation mode of the pose optimisation (default 0).  0: each wavefront
- * sums its edges' chi2 / H / b terms lane-strided and then through a fixed
- * DPP tree -- deterministic, but in another order than g2o, so LM steps
- * decided on rounding noise (a converged pose restarted in a later robust
- * round) may count differently.  1: every sum runs sequentially in g2o's
- * active-edge order (the edge terms are computed in parallel, accumulated
- * edge by edge), so the whole LM trajectory -- accept / reject of every
- * trial, lambda, iterations -- follows the sequential reference; about 2x the
- * kernel time (the dependent chain of additions).  Takes effect at the next
- * orbx_pose_run.  Returns ORBX_ERR_ARG for a null context or a mode outside
- * 0..1; orbx_pose_get_exact returns the mode (ORBX_ERR_ARG for NULL). */
+/* Summation mode of the pose optimisation (default 1).  1: every chi2 / H /
+ * b sum runs sequentially in g2o's active-edge order (the edge terms are
+ * computed in parallel, accumulated edge by edge), so the whole LM
+ * trajectory -- accept / reject of every trial, lambda, iterations -- and
+ * the returned pose are the sequential reference's bit for bit, for every
+ * batch size.  0 (opt-in, faster: ~1.25x one call, ~1.6x a batch): each
+ * wavefront sums its edges' terms lane-strided and then through a fixed DPP
+ * tree -- deterministic, but in another order than g2o, so LM steps decided
+ * on rounding noise (a converged pose restarted in a later robust round) may
+ * count differently: poses within 1e-5, and the result of a frame may differ
+ * between a lone call (a workgroup per frame) and a batch (a wavefront per
+ * frame).  Takes effect at the next orbx_pose_run.  Returns ORBX_ERR_ARG for
+ * a null context or a mode outside 0..1; orbx_pose_get_exact returns the
+ * mode (ORBX_ERR_ARG for NULL). */
 int orbx_pose_set_exact(orbx_ctx* ctx, int exact);
 int orbx_pose_get_exact(const orbx_ctx* ctx);
 

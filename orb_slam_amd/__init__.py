@@ -159,6 +159,25 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _async_array(a, dtype, min_items, name):
+    """An asynchronous copy's host array: a HostArray or numpy array of
+    `dtype`, C-contiguous (the copy goes through its raw pointer), holding at
+    least min_items elements (None: no size requirement); None passes."""
+    if a is None:
+        return None
+    if isinstance(a, HostArray):
+        a = a.array
+    if not isinstance(a, np.ndarray):
+        raise TypeError(f"{name}: expected a numpy array or HostArray, got {type(a).__name__}")
+    if a.dtype != np.dtype(dtype):
+        raise TypeError(f"{name}: dtype {a.dtype}, expected {np.dtype(dtype)}")
+    if not a.flags.c_contiguous:
+        raise ValueError(f"{name}: must be C-contiguous")
+    if min_items is not None and a.size < min_items:
+        raise ValueError(f"{name}: {a.size} elements, the copy writes {min_items}")
+    return a
+
+
 def _check(code, where):
     if code != ORBX_OK:
         raise OrbxError(code, where)
@@ -241,15 +260,27 @@ class Context:
         _check(lib().orbx_dev_upload(self._h, first, cnt, _ptr(frames), w, h, w), "orbx_dev_upload")
 
     def upload_async(self, frames, first=0):
-        """orbx_dev_upload_async: `frames` should be page-locked (HostArray)
-        for the copy to overlap device work."""
+        """orbx_dev_upload_async: `frames` (count, h, w) u8, C-contiguous --
+        a HostArray (or its .array) for the copy to overlap device work.  The
+        memory must stay untouched until the extraction of those slots."""
+        frames = _async_array(frames, np.uint8, None, "frames")
+        if frames.ndim != 3:
+            raise ValueError(f"frames: expected (count, h, w), got shape {frames.shape}")
         cnt, h, w = frames.shape
         _check(lib().orbx_dev_upload_async(self._h, first, cnt, _ptr(frames), w, h, w), "orbx_dev_upload_async")
 
     def download_async(self, first, count, kps=None, desc=None, n_kps=None, m12=None, n_m=None):
-        """orbx_dev_download_async into (preferably page-locked) arrays:
-        kps count*nfeatures KEYPOINT, desc (count*nfeatures, 32) u8, n_kps
-        count i32, m12 count*nfeatures i32, n_m count i32."""
+        """orbx_dev_download_async into (preferably page-locked: HostArray)
+        arrays: kps count*nfeatures KEYPOINT, desc count*nfeatures*32 u8,
+        n_kps count i32, m12 count*nfeatures i32, n_m count i32 (each may be
+        None).  The arrays are written when the copy completes (after the
+        next call that orders after it, e.g. sync)."""
+        nf = self.nfeatures
+        kps = _async_array(kps, KEYPOINT, count * nf, "kps")
+        desc = _async_array(desc, np.uint8, count * nf * 32, "desc")
+        n_kps = _async_array(n_kps, np.int32, count, "n_kps")
+        m12 = _async_array(m12, np.int32, count * nf, "m12")
+        n_m = _async_array(n_m, np.int32, count, "n_m")
         _check(lib().orbx_dev_download_async(self._h, first, count, _ptr(kps), _ptr(desc), _ptr(n_kps), _ptr(m12),
                                              _ptr(n_m)), "orbx_dev_download_async")
 

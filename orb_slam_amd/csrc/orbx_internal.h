@@ -316,7 +316,7 @@ struct orbx_ctx {
     size_t pose_dev_bytes = 0;
     void* pose_host = nullptr;
     size_t pose_host_bytes = 0;
-    bool pose_exact = false;   // orbx_pose_set_exact: sequential sums in g2o's edge order
+    bool pose_exact = true;    // orbx_pose_set_exact: sequential sums in g2o's edge order (default)
     int pose_wide_max = 1;     // batches up to this size run a workgroup per frame (k_pose_opt kW > 1)
     int pose_P = 0;
     long long pose_E = 0;

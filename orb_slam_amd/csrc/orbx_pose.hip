@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "orbx_device.h"
@@ -310,7 +311,9 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     static_assert(kW == 1 || !kExact, "the exact sums run one wave per frame");
     constexpr int kT = 64 * kW;                          // threads striding one frame's edges
     constexpr int kFrames = kW == 1 ? kPoseThreads / 64 : 1;
-    constexpr int kCache = kW == 1 ? kPoseLdsEdges : kPoseLdsEdgesWide;
+    // kExact keeps no edges in LDS: the term rows (57 KB) alone let two
+    // workgroups share a CU, so a wave's add chain overlaps another's terms
+    constexpr int kCache = kExact ? 1 : (kW == 1 ? kPoseLdsEdges : kPoseLdsEdgesWide);
     const int prob = kW == 1 ? blockIdx.x * (kPoseThreads / 64) + (threadIdx.x >> 6) : blockIdx.x;
     if (prob >= P) return;   // whole wavefront (kW > 1: whole workgroup)
     const int lane = kW == 1 ? threadIdx.x & 63 : threadIdx.x;   // position among the frame's threads
@@ -444,9 +447,25 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (lane < Q) {
-                const int ne = min(64, nE - g);
-#pragma unroll 8
-                for (int e = 0; e < ne; e++) acc += rows[e][lane];
+                // blocks of 8 rows (rows past the last edge are +0.0), the
+                // next block's loads issued before this block's adds
+                const int nb = (min(64, nE - g) + 7) >> 3;
+                double cur[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) cur[k] = rows[k][lane];
+#pragma unroll
+                for (int bk = 1; bk < 8; bk++) {
+                    if (bk >= nb) break;
+                    double nxt[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) nxt[k] = rows[8 * bk + k][lane];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) acc += cur[k];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc += cur[k];
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -470,6 +489,12 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
         if (n_active > 0) {
             double lambda = 0, ni = 2;
             int nBadLM = 0;
+            // kExact: a trial pass sums the whole system at the trial pose
+            // (lane q holds sum q), which the next iteration takes when the
+            // trial is accepted -- the sums computeActiveErrors + buildSystem
+            // would form there, in the same order
+            double sys_sum = 0;
+            bool have_sys = false;
 #pragma unroll 1
             for (int iter = 0; iter < its; iter++) {
                 // computeActiveErrors + activeRobustChi2 + buildSystem (fused)
@@ -480,15 +505,17 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
                 for (int k = 0; k < 6; k++) bv[k] = 0;
                 double currentChi;
                 if constexpr (kExact) {
-                    const double sum = seq_sums(28, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
-                                                        double (&c)[28]) {
-                        pose_edge_terms(pose, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
-                    });
-                    currentChi = lane_f64(sum, 0);
+                    if (!have_sys)
+                        sys_sum = seq_sums(28, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
+                                                   double (&c)[28]) {
+                            pose_edge_terms(pose, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                        });
+                    have_sys = false;
+                    currentChi = lane_f64(sys_sum, 0);
 #pragma unroll
-                    for (int k = 0; k < 21; k++) h[k] = lane_f64(sum, 1 + k);
+                    for (int k = 0; k < 21; k++) h[k] = lane_f64(sys_sum, 1 + k);
 #pragma unroll
-                    for (int k = 0; k < 6; k++) bv[k] = lane_f64(sum, 22 + k);
+                    for (int k = 0; k < 6; k++) bv[k] = lane_f64(sys_sum, 22 + k);
                 } else {
                 for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
                     const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
@@ -602,13 +629,13 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
                         huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
                         return rho0;
                     };
-                    double tempChi;
+                    double tempChi, tsum = 0;
                     if constexpr (kExact) {
-                        tempChi = lane_f64(seq_sums(1, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
-                                                           double (&c)[28]) {
-                                               c[0] = trial_chi(fo0, fo1, fis, fx_, fy_, fz_);
-                                           }),
-                                           0);
+                        tsum = seq_sums(28, [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_,
+                                                double (&c)[28]) {
+                            pose_edge_terms(tp, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                        });
+                        tempChi = lane_f64(tsum, 0);
                     } else {
                         double tchi = 0;
                         for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
@@ -633,6 +660,10 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
                         currentChi = tempChi;
 #pragma unroll
                         for (int i = 0; i < 7; i++) pose[i] = tp[i];
+                        if constexpr (kExact) {
+                            sys_sum = tsum;
+                            have_sys = true;
+                        }
                     } else {
                         lambda *= ni;
                         ni *= 2;
@@ -701,6 +732,392 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
         }
         out.not_posdef = not_posdef;
     }
+}
+
+// The exact sums (g2o's sequential edge order, bit for bit the restatement)
+// for one frame per workgroup, fast.  Every sum of a pass is a chain of
+// dependent FP64 adds in edge order -- the part no reassociation may
+// shorten -- so the kernel keeps that chain busy and hides everything else
+// behind it.  Wave 0 adds; waves 1..7 compute the per-edge terms (28
+// doubles per edge: chi2, the 21 lower entries of J^T W J, b) of groups of
+// 64 edges, group g on worker g % 7, into a ring of kPxSlots LDS slots
+// (column-major, one column per sum, padded so lanes 0..27 of wave 0 read
+// 28 different bank pairs).  Producer and consumer meet through LDS
+// counters, not workgroup barriers: a worker waits until its slot's
+// previous group was consumed, wave 0 until its next group is ready -- so
+// seven groups are in flight while the chain runs.  A trial pass computes
+// the full system at the trial pose (the next iteration's build when the
+// trial is accepted).  The LM control runs on uniform values broadcast
+// through LDS, the 6x6 LDLT and the exp-map step on wave 0 alone
+// (orbx_pose_set_exact; see k_pose_opt for the g2o semantics every line
+// below follows).
+#ifdef ORBX_POSE_PROFILE
+// phase stamps of k_pose_exact_wide (block 0, thread 0; wall clock, 100 MHz):
+// 0 round-start builds, 1 solves, 2 trial passes, 3 classification, 4 the
+// whole kernel, 5 builds, 6 trials
+__device__ unsigned long long g_pose_prof[8];
+// (accumulated in registers, written once at the kernel's end: a global
+// read-modify-write per stamp would stall the wave it measures)
+#define PX_T0() const unsigned long long _px_t0 = wall_clock64()
+#define PX_ACC(k, t0) (px_acc[k] += wall_clock64() - (t0))
+#define PX_CNT(k) (px_acc[k] += 1)
+#else
+#define PX_T0() (void)0
+#define PX_ACC(k, t0) (void)0
+#define PX_CNT(k) (void)0
+#endif
+constexpr int kPxWaves = 8;                   // two per SIMD (255 VGPRs)
+constexpr int kPxThreads = 64 * kPxWaves;
+constexpr int kPxWorkers = kPxWaves - 1;
+constexpr int kPxCache = 1024;                // edges kept in LDS (25 KB)
+constexpr int kPxStride = 65;                 // doubles per column of a slot (64 edges + 1 pad)
+constexpr int kPxSlot = 28 * kPxStride;       // doubles per slot
+constexpr int kPxSlots = 8;                   // ring depth (114 KB)
+
+__global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* __restrict__ hdrs, PoseEdgeArrays ed,
+                                                               uint8_t* __restrict__ eflag,
+                                                               PoseOut* __restrict__ outs, int P, double delta)
+{
+    const int prob = blockIdx.x;
+    if (prob >= P) return;   // whole workgroup
+#ifdef ORBX_POSE_PROFILE
+    const unsigned long long t_kernel = wall_clock64();
+    unsigned long long px_acc[8] = {};
+#endif
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const PoseHdr& H = hdrs[prob];
+    const long long e0 = H.e0;
+    const int nE = H.nE;
+    const Cam cam{(double)H.cam[0], (double)H.cam[1], (double)H.cam[2], (double)H.cam[3]};
+    double pose[7], errpose[7];
+    {
+        double R[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) R[i * 3 + j] = (double)H.T[i * 4 + j];
+        Q q = qfrom(R);
+        qnormalize(q);
+        pose[0] = q.x; pose[1] = q.y; pose[2] = q.z; pose[3] = q.w;
+#pragma unroll
+        for (int i = 0; i < 3; i++) pose[4 + i] = (double)H.T[i * 4 + 3];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) errpose[i] = pose[i];
+    const float* ox = ed.ox + e0;
+    const float* oy = ed.oy + e0;
+    const float* isg = ed.isig + e0;
+    const float* px = ed.px + e0;
+    const float* py = ed.py + e0;
+    const float* pz = ed.pz + e0;
+    uint8_t* flag = eflag + e0;
+    __shared__ float s_e[6][kPxCache];
+    __shared__ uint8_t s_f[kPxCache];
+    __shared__ double s_ring[kPxSlots * kPxSlot];
+    __shared__ int s_ready[kPxSlots];   // ticket + 1 of the group a slot holds
+    __shared__ int s_done;              // tickets consumed so far (all passes)
+    __shared__ double s_sum[28];        // the pass's sums (written by wave 0 after the chain)
+    __shared__ double s_sol[14];        // wave 0's step: xs, trial pose, ok
+    __shared__ int s_cnt[kPxWaves][2];
+    const int nL = min(nE, kPxCache);
+    for (int a = tid; a < nL; a += kPxThreads) {
+        s_e[0][a] = ox[a];
+        s_e[1][a] = oy[a];
+        s_e[2][a] = isg[a];
+        s_e[3][a] = px[a];
+        s_e[4][a] = py[a];
+        s_e[5][a] = pz[a];
+        s_f[a] = 0;
+    }
+    for (int a = nL + tid; a < nE; a += kPxThreads) flag[a] = 0;
+    if (tid < kPxSlots) s_ready[tid] = 0;
+    if (tid == 0) s_done = 0;
+    __syncthreads();
+    int ticket = 0;   // groups of all passes so far (uniform: every wave counts every pass)
+    // the edge's inputs and whether it is active (not an outlier)
+    auto edge = [&](int a, float& o0, float& o1, float& is, float& X, float& Y, float& Z) -> bool {
+        if (a < nL) {
+            o0 = s_e[0][a]; o1 = s_e[1][a]; is = s_e[2][a]; X = s_e[3][a]; Y = s_e[4][a]; Z = s_e[5][a];
+            return !s_f[a];
+        }
+        o0 = ox[a]; o1 = oy[a]; is = isg[a]; X = px[a]; Y = py[a]; Z = pz[a];
+        return !flag[a];
+    };
+    // Q sequential sums over the active edges in edge order (an inactive
+    // edge adds +0.0, which leaves every bit: the sums start at +0.0 and
+    // round-to-nearest never yields -0.0 from there); the results land in
+    // s_sum[0, Q) for every thread
+    auto seq_sums = [&](auto Qc, auto&& terms) {
+        constexpr int Qn = decltype(Qc)::value;
+        const int G = (nE + 63) >> 6;   // groups of 64 edges (the last padded with +0.0 rows)
+        if (wave > 0) {
+#pragma unroll 1
+            for (int g = wave - 1; g < G; g += kPxWorkers) {
+                const int tk = ticket + g, slot = tk % kPxSlots;
+                // the slot's previous group (ticket tk - kPxSlots) is consumed
+                // (bounded: a wait that never ends would hang the device;
+                // after ~0.1 s the pass goes on with wrong sums instead)
+                for (int spin = 0; *(volatile int*)&s_done < tk - kPxSlots + 1 && spin < (1 << 22); spin++)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                double* buf = s_ring + slot * kPxSlot;
+                const int a = g * 64 + lane;
+                double t[Qn];
+                float o0, o1, is, X, Y, Z;
+                const bool act = a < nE && edge(a, o0, o1, is, X, Y, Z);
+                if (act) terms(o0, o1, is, X, Y, Z, t);
+#pragma unroll
+                for (int q = 0; q < Qn; q++) buf[q * kPxStride + lane] = act ? t[q] : 0.0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) *(volatile int*)&s_ready[slot] = tk + 1;
+            }
+        } else {
+            double acc = 0.0;
+#pragma unroll 1
+            for (int g = 0; g < G; g++) {
+                const int tk = ticket + g, slot = tk % kPxSlots;
+                for (int spin = 0; *(volatile int*)&s_ready[slot] != tk + 1 && spin < (1 << 22); spin++)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (lane < Qn) {
+                    // the chain: blocks of 8 (the group's last edge rounded
+                    // up), the next block's loads issued before this block's adds
+                    const double* col = s_ring + slot * kPxSlot + lane * kPxStride;
+                    const int nb = min(8, (nE - g * 64 + 7) >> 3);
+                    double cur[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) cur[k] = col[k];
+#pragma unroll
+                    for (int bk = 1; bk < 8; bk++) {
+                        if (bk >= nb) break;
+                        double nxt[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) nxt[k] = col[8 * bk + k];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) acc += cur[k];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; k++) acc += cur[k];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the slot's reads are done
+                if (lane == 0) *(volatile int*)&s_done = tk + 1;
+            }
+            if (lane < Qn) s_sum[lane] = acc;
+        }
+        ticket += G;
+        __syncthreads();
+    };
+    auto block_counts = [&](int a0, int a1, int& r0, int& r1) {
+        a0 = wave_sum_int(a0);
+        a1 = wave_sum_int(a1);
+        if (lane == 0) {
+            s_cnt[wave][0] = a0;
+            s_cnt[wave][1] = a1;
+        }
+        __syncthreads();
+        r0 = r1 = 0;
+#pragma unroll
+        for (int w = 0; w < kPxWaves; w++) {
+            r0 += s_cnt[w][0];
+            r1 += s_cnt[w][1];
+        }
+        __syncthreads();   // s_cnt is written again by the next round
+    };
+
+    PoseOut& out = outs[prob];
+    int not_posdef = 0, rounds = 0;
+    int n_active = nE;
+    int nBadOut = 0;
+#pragma unroll 1
+    for (int it = 0; it < 4; it++) {
+        const float chi2th = it == 0 ? 9.210f : (it == 1 ? 7.378f : 5.991f);
+        const int its = it < 2 ? 10 : (it == 2 ? 7 : 5);
+        int r_iters = 0, r_trials = 0;
+        double r_chi = 0;
+        rounds = it + 1;
+        if (n_active > 0) {
+            double lambda = 0, ni = 2;
+            int nBadLM = 0;
+            // the system at `pose` (chi2, H, b): built at the round's start; a
+            // trial pass builds it at the trial pose too, which the next
+            // iteration uses when the trial is accepted -- the same sums in
+            // the same order as computeActiveErrors + buildSystem there
+            double h[21], bv[6], currentChi = 0;
+            bool have_sys = false;
+#pragma unroll 1
+            for (int iter = 0; iter < its; iter++) {
+                if (!have_sys) {
+                    PX_T0();
+                    PX_CNT(5);
+                    seq_sums(std::integral_constant<int, 28>{},
+                             [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_, double(&c)[28]) {
+                                 pose_edge_terms(pose, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                             });
+                    currentChi = s_sum[0];
+#pragma unroll
+                    for (int k = 0; k < 21; k++) h[k] = s_sum[1 + k];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) bv[k] = s_sum[22 + k];
+                    PX_ACC(0, _px_t0);
+                }
+                have_sys = false;
+                const double iniChi = currentChi;
+                if (iter == 0) {   // computeLambdaInit (levenberg.cpp:166-180)
+                    double mx = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) mx = fmax(fabs(h[LT(j, j)]), mx);
+                    lambda = 1e-5 * mx;
+                    ni = 2;
+                    nBadLM = 0;
+                }
+                double rho = 0;
+                int qmax = 0;
+                do {
+                    double xs[6], tp[7];
+#ifdef ORBX_POSE_PROFILE
+                    const unsigned long long t_solve = wall_clock64();
+#endif
+                    if (wave == 0) {
+                        double m[21];
+#pragma unroll
+                        for (int k = 0; k < 21; k++) m[k] = h[k];
+#pragma unroll
+                        for (int j = 0; j < 6; j++) m[LT(j, j)] += lambda;
+                        const bool ok = ldlt6_solve(m, bv, xs);
+#pragma unroll
+                        for (int i = 0; i < 7; i++) tp[i] = pose[i];
+                        if (ok) {
+                            se3_oplus(tp, xs);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 6; i++) xs[i] = 0.0;
+                        }
+                        if (lane == 0) {
+#pragma unroll
+                            for (int i = 0; i < 6; i++) s_sol[i] = xs[i];
+#pragma unroll
+                            for (int i = 0; i < 7; i++) s_sol[6 + i] = tp[i];
+                            s_sol[13] = ok ? 1.0 : 0.0;
+                        }
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int i = 0; i < 6; i++) xs[i] = s_sol[i];
+#pragma unroll
+                    for (int i = 0; i < 7; i++) tp[i] = s_sol[6 + i];
+                    const bool ok2 = s_sol[13] != 0.0;
+                    PX_ACC(1, t_solve);
+                    PX_T0();
+                    PX_CNT(6);
+                    if (!ok2) not_posdef++;
+                    // computeActiveErrors at the trial estimate, with the
+                    // system there (s_sol is written again only after this
+                    // pass's barriers)
+                    seq_sums(std::integral_constant<int, 28>{},
+                             [&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_, double(&c)[28]) {
+                                 pose_edge_terms(tp, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                             });
+                    double tempChi = s_sum[0];
+                    PX_ACC(2, _px_t0);
+#pragma unroll
+                    for (int i = 0; i < 7; i++) errpose[i] = tp[i];
+                    if (!ok2) tempChi = 1.79769313486231570815e+308;
+                    double scale = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) scale += xs[j] * (lambda * xs[j] + bv[j]);
+                    scale += 1e-3;
+                    rho = (currentChi - tempChi) / scale;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - pow((2 * rho - 1), 3);
+                        alpha = fmin(alpha, 2. / 3.);
+                        lambda *= fmax(1. / 3., alpha);
+                        ni = 2;
+                        currentChi = tempChi;
+#pragma unroll
+                        for (int i = 0; i < 7; i++) pose[i] = tp[i];
+                        // the trial pass's system (s_sum stays until the
+                        // next pass's last barrier)
+#pragma unroll
+                        for (int k = 0; k < 21; k++) h[k] = s_sum[1 + k];
+#pragma unroll
+                        for (int k = 0; k < 6; k++) bv[k] = s_sum[22 + k];
+                        have_sys = true;
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                    }
+                    qmax++;
+                } while (rho < 0 && qmax < 10);
+                r_iters++;
+                r_trials += qmax;
+                r_chi = currentChi;
+                if (qmax == 10 || rho == 0) break;
+                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                else nBadLM = 0;
+                if (nBadLM >= 3) break;
+            }
+        }
+        // outlier classification (src/Optimizer.cc:243-265)
+        PX_T0();
+        int bad = 0, act = 0;
+        const double th = (double)chi2th;
+#pragma unroll 1
+        for (int a = tid; a < nE; a += kPxThreads) {
+            float o0, o1, is, X, Y, Z;
+            const uint8_t f = edge(a, o0, o1, is, X, Y, Z) ? 0 : 1;
+            const double Xw[3] = {(double)X, (double)Y, (double)Z};
+            const double sg = (double)is;
+            double pc[3], er0, er1;
+            pose_edge_error(f ? pose : errpose, Xw, (double)o0, (double)o1, cam, pc, er0, er1);
+            const double c2 = er0 * (sg * er0) + er1 * (sg * er1);
+            uint8_t nf = f;
+            if (c2 > th) {
+                nf = 1;
+                bad++;
+            } else if (c2 <= th) {
+                nf = 0;
+            }
+            act += nf == 0;
+            if (a < nL) s_f[a] = nf;
+            else flag[a] = nf;
+        }
+        block_counts(bad, act, nBadOut, n_active);
+        PX_ACC(3, _px_t0);
+        if (tid == 0) {
+            out.iterations[it] = r_iters;
+            out.trials[it] = r_trials;
+            out.chi2_final[it] = r_chi;
+            out.n_bad[it] = nBadOut;
+        }
+        if (nE < 10) break;
+    }
+    for (int a = tid; a < nL; a += kPxThreads) flag[a] = s_f[a];   // mvbOutlier of the LDS part
+    if (tid == 0) {
+        double R[9];
+        qmat(Q{pose[0], pose[1], pose[2], pose[3]}, R);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) out.T[i * 4 + j] = (float)R[i * 3 + j];
+            out.T[i * 4 + 3] = (float)pose[4 + i];
+        }
+        out.n_inliers = nE - nBadOut;
+        out.rounds = rounds;
+        for (int r = rounds; r < 4; r++) {
+            out.iterations[r] = 0;
+            out.trials[r] = 0;
+            out.chi2_final[r] = 0;
+            out.n_bad[r] = 0;
+        }
+        out.not_posdef = not_posdef;
+    }
+#ifdef ORBX_POSE_PROFILE
+    PX_ACC(4, t_kernel);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int k = 0; k < 8; k++) g_pose_prof[k] += px_acc[k];
+#endif
 }
 
 namespace {
@@ -827,14 +1244,32 @@ int launch_pose_device(orbx_ctx* ctx, const PoseHdr* hdrs, const PoseEdgeArrays&
 {
     const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
     const int per = kPoseThreads / 64;
-    const bool wide = !ctx->pose_exact && P <= ctx->pose_wide_max;
-    auto kern = ctx->pose_exact ? k_pose_opt<true> : (wide ? k_pose_opt<false, kPoseWideWaves> : k_pose_opt<false>);
-    const int blocks = wide ? P : (P + per - 1) / per, threads = wide ? 64 * kPoseWideWaves : kPoseThreads;
-    kern<<<blocks, threads, 0, ctx->stream>>>(hdrs, ed, flags, outs, P, delta);
+    const bool wide = P <= ctx->pose_wide_max;
+    if (ctx->pose_exact && wide) {
+        k_pose_exact_wide<<<P, kPxThreads, 0, ctx->stream>>>(hdrs, ed, flags, outs, P, delta);
+    } else {
+        auto kern = ctx->pose_exact ? k_pose_opt<true>
+                                    : (wide ? k_pose_opt<false, kPoseWideWaves> : k_pose_opt<false>);
+        const int blocks = wide && !ctx->pose_exact ? P : (P + per - 1) / per;
+        const int threads = wide && !ctx->pose_exact ? 64 * kPoseWideWaves : kPoseThreads;
+        kern<<<blocks, threads, 0, ctx->stream>>>(hdrs, ed, flags, outs, P, delta);
+    }
     ORBX_HIP_CHECK(hipGetLastError());
     return ORBX_OK;
 }
 }  // namespace orbx
+
+#ifdef ORBX_POSE_PROFILE
+extern "C" int orbx_debug_pose_prof(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pose_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+    if (reset) {
+        const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
 
 extern "C" int orbx_pose_run(orbx_ctx* ctx)
 {
@@ -853,16 +1288,12 @@ extern "C" int orbx_pose_run(orbx_ctx* ctx)
     ed.px = reinterpret_cast<const float*>(d + o_edges + 3 * arr);
     ed.py = reinterpret_cast<const float*>(d + o_edges + 4 * arr);
     ed.pz = reinterpret_cast<const float*>(d + o_edges + 5 * arr);
-    const double delta = (double)(float)std::sqrt(5.991);   // const float delta = sqrt(5.991) (:188)
-    const int per = kPoseThreads / 64;
     timer_begin(ctx, "pose");
     // a lone frame (the reference's one call per frame) gets a workgroup of
-    // kPoseWideWaves wavefronts; batches a wavefront per frame
-    const bool wide = !ctx->pose_exact && P <= ctx->pose_wide_max;
-    auto kern = ctx->pose_exact ? k_pose_opt<true> : (wide ? k_pose_opt<false, kPoseWideWaves> : k_pose_opt<false>);
-    const int blocks = wide ? P : (P + per - 1) / per, threads = wide ? 64 * kPoseWideWaves : kPoseThreads;
-    kern<<<blocks, threads, 0, ctx->stream>>>(reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags,
-                                              reinterpret_cast<PoseOut*>(d + ctx->pose_o_out), P, delta);
+    // several wavefronts; batches a wavefront per frame
+    const int lr = launch_pose_device(ctx, reinterpret_cast<const PoseHdr*>(d), ed, d + ctx->pose_o_flags,
+                                      reinterpret_cast<PoseOut*>(d + ctx->pose_o_out), P);
+    if (lr != ORBX_OK) return lr;
     timer_end(ctx, "pose");
     ORBX_HIP_CHECK(hipGetLastError());
     return ORBX_OK;

@@ -28,7 +28,7 @@ from oracle_lib import load
 from test_bow_oracle import run_ref as bow_ref
 from test_lba_gpu import compare as lba_compare
 from test_lba_gpu import run_ref as lba_ref
-from test_pose_gpu import compare as pose_compare
+from test_pose_gpu import compare_exact as pose_compare
 from test_pose_oracle import ref_pose
 from threads_work import WORK, _medians, _motion, _sim3, make_contexts, make_inputs, run_threads, same
 

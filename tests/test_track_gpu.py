@@ -4,11 +4,12 @@ restated over the oracle's matchers and PoseOptimization
 (tests/track_data.py: ref_chain).
 
 The GPU extraction's keypoints are the chain's input on both sides (the
-extraction's own parity is tests/test_extract_gpu.py).  With
-orbx_pose_set_exact(ctx, 1) the whole chain -- matches, statuses, counts,
-outlier flags and the final pose -- must equal the restatement bit for bit.
-In the default PoseOptimization mode (parallel sums) the pose must agree to
-1e-5 (north_star's tolerance for the pose) and everything else exactly.
+extraction's own parity is tests/test_extract_gpu.py).  In the default
+PoseOptimization mode (sums in g2o's order) the whole chain -- matches,
+statuses, counts, outlier flags and the final pose -- must equal the
+restatement bit for bit.  With the opt-in fast sums
+(orbx_pose_set_exact(ctx, 0)) the pose must agree to 1e-5 (north_star's
+tolerance for the pose) and everything else exactly.
 """
 import ctypes
 
@@ -73,7 +74,7 @@ def compare(got, exp, exact):
 @pytest.fixture
 def pose_mode(ctx):
     yield lambda exact: ox.lib().orbx_pose_set_exact(ctx.handle, int(exact))
-    ox.lib().orbx_pose_set_exact(ctx.handle, 0)
+    ox.lib().orbx_pose_set_exact(ctx.handle, 1)
 
 
 @pytest.mark.parametrize("exact", [1, 0])
