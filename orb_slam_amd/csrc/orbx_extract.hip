@@ -364,7 +364,10 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
     // weights (16 a0, 16 a1) -- 16 S, whose bits 8..23 are (S >> 4) << 8 --
     // and VResizeLinearVec_32s8u's (S >> 4) * b >> 16 is one
     // v_mul_hi_u32_u24 of that with b << 8.  S >> 4 <= 32640 and the
-    // weights are <= 2048, so none of its 16-bit saturations can trigger.
+    // weights are <= 2048, so none of its 16-bit saturations can trigger;
+    // the rounded row weights sum to 2048 +- 1 (cvRound of complementary
+    // values), so the two terms sum to <= 32640 * 2049 / 2^16 < 1021, the
+    // final (t + 2) >> 2 is <= 255 and its u8 saturation is a no-op.
     typedef unsigned short orbx_us2 __attribute__((ext_vector_type(2)));
     auto mh = [](uint32_t x, uint32_t y) {   // bits 32..47 of the 24 x 24-bit product
         return (uint32_t)(((unsigned long long)(x & 0xFFFFFFu) * (unsigned long long)(y & 0xFFFFFFu)) >> 32);
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(256) void k_pyr_resize_lds(ExtractArgs a, ResizeLev
             c1 = sy1;
             uint32_t word = 0;
 #pragma unroll
-            for (int b = 0; b < 4; b++) word |= min((mh(A[b], B0) + mh(B[b], B1) + 2) >> 2, 255u) << (8 * b);
+            for (int b = 0; b < 4; b++) word |= ((mh(A[b], B0) + mh(B[b], B1) + 2) >> 2) << (8 * b);
             *reinterpret_cast<uint32_t*>(dst + (size_t)rr * L.stride + 4 * q) = word;
         }
     }
@@ -885,6 +888,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
     constexpr int kQueueWords = kWaves * kQueue * (int)sizeof(QEntry) / 4;
     constexpr int kUnitCap = 2 * kQueueWords;   // u16 NMS unit list aliasing the queues
     __shared__ __attribute__((aligned(16))) uint32_t qbuf[kQueueWords];
+    __shared__ int s_left[kWaves];   // each wave's queue length at the end of a score pass
     uint16_t* ulist = reinterpret_cast<uint16_t*>(qbuf);
     const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     QEntry* cand = reinterpret_cast<QEntry*>(qbuf) + wv * kQueue;
@@ -1080,9 +1084,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kThrea
             // rest lies below it), and the queue is read only after the
             // fence above
         }
-        if (qt > 0)   // the last < 128
-            score_pair(lane < qt ? (int)cand[lane] : 0, lane + 64 < qt ? (int)cand[lane + 64] : 0, lane < qt,
-                       lane + 64 < qt);
+        // the waves' leftovers (< 128 each) scored together, in full batches
+        // of 128 where they add up (one partly filled batch per wave would
+        // run the whole scoring code for a few pixels)
+        if (lane == 0) s_left[wv] = qt;
+        __syncthreads();
+        int pre[kWaves + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) pre[w + 1] = pre[w] + s_left[w];
+        const int T = pre[kWaves];
+        auto entry = [&](int g) {
+            int w = 0;
+#pragma unroll
+            for (int k = 1; k < kWaves; k++) w += g >= pre[k];
+            return (int)(reinterpret_cast<const QEntry*>(qbuf) + w * kQueue)[g - pre[w]];
+        };
+        for (int b0 = wv * 128; b0 < T; b0 += kWaves * 128) {
+            const int ga = b0 + lane, gb = b0 + 64 + lane;
+            score_pair(ga < T ? entry(ga) : 0, gb < T ? entry(gb) : 0, ga < T, gb < T);
+        }
     };
     // non-max suppression over the S' map: a pixel is kept if its S' beats
     // all 8 neighbours' S'.  Only dwords whose `nz` bit is set can keep

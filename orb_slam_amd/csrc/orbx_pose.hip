@@ -754,7 +754,7 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
 #ifdef ORBX_POSE_PROFILE
 // phase stamps of k_pose_exact_wide (block 0, thread 0; wall clock, 100 MHz):
 // 0 round-start builds, 1 solves, 2 trial passes, 3 classification, 4 the
-// whole kernel, 5 builds, 6 trials
+// whole kernel, 5 builds, 6 trials, 7 the LDLT part of the solves
 __device__ unsigned long long g_pose_prof[8];
 // (accumulated in registers, written once at the kernel's end: a global
 // read-modify-write per stamp would stall the wave it measures)
@@ -985,9 +985,15 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
                         for (int k = 0; k < 21; k++) m[k] = h[k];
 #pragma unroll
                         for (int j = 0; j < 6; j++) m[LT(j, j)] += lambda;
+#ifdef ORBX_POSE_PROFILE
+                        const unsigned long long t_l0 = wall_clock64();
+#endif
                         const bool ok = ldlt6_solve(m, bv, xs);
 #pragma unroll
                         for (int i = 0; i < 7; i++) tp[i] = pose[i];
+#ifdef ORBX_POSE_PROFILE
+                        PX_ACC(7, t_l0);
+#endif
                         if (ok) {
                             se3_oplus(tp, xs);
                         } else {
