@@ -40,6 +40,7 @@ for i in range(n + 5):
 L.orbx_debug_pose_prof(buf, 0)
 v = np.array(list(buf), np.float64)
 us = v[:5] / 100.0 / n          # 100 MHz ticks -> us per call
+print(f"ldlt part of solves: {v[7] / 100.0 / n:.1f} us per call")
 print(f"edges {int(np.count_nonzero(arrs['has_mp']))} iterations {list(st.iterations)} trials {list(st.levenberg_trials)}")
 print(f"per call: kernel {us[4]:.1f} us = builds {us[0]:.1f} ({v[5] / n:.1f}x) + solves {us[1]:.1f} + trials "
       f"{us[2]:.1f} ({v[6] / n:.1f}x) + classify {us[3]:.1f} + rest {us[4] - us[:4].sum():.1f}")
