@@ -407,7 +407,13 @@ int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q);
  *   -> PoseOptimization on all matches
  * runs without a host round trip: one upload (last frame, local map, pose
  * prediction, image) and one read-back.  The last frame's map points are
- * named by their index in the local map.  The camera centre for the frustum
+ * named by their index in the map-point arrays.  The local map is an input:
+ * the reference rebuilds it (UpdateReference, src/Tracking.cc:754-790) from
+ * the keyframes that observe the motion search's matches, between the two
+ * searches; a caller passes the one it holds (the previous frame's), which
+ * is the reference's whenever those keyframes are unchanged, or runs the two
+ * halves with the host-array calls (orbx_search_by_projection_motion,
+ * orbx_pose_optimization, orbx_search_local_map).  The camera centre for the frustum
  * test is Frame::UpdatePoseMatrices' mOw = -Rcw^T tcw evaluated in float
  * left to right (the adapter's host glue does the same).  The undistorted
  * keypoints of the slot are its extracted keypoints (k1 = 0) or those
@@ -426,7 +432,9 @@ typedef struct {
                                        bounds, pyramid                                    */
     const int32_t* last_mp;         /* local-map index of LastFrame.mvpMapPoints[i], or -1 */
     const uint8_t* last_outlier;    /* LastFrame.mvbOutlier                                */
-    int n_mp;                       /* local map (mvpLocalMapPoints)                       */
+    int n_mp;                       /* map points of the arrays below                      */
+    int n_local_mp;                 /* the first n_local_mp of them are mvpLocalMapPoints (the
+                                       frustum search's); the rest only LastFrame's. <= 0: all */
     const float* mp_pos;            /* n_mp x 3                                            */
     const float* mp_normal;         /* n_mp x 3                                            */
     const float* mp_dist;           /* n_mp x 2: min, max distance invariance              */

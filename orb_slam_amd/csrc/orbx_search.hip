@@ -967,7 +967,7 @@ struct TrackDev {
     const int32_t* cur_cnt;
     const int32_t* last_mp;
     const uint8_t* last_outlier;
-    int n_last, n_mp, cap;          // n_last: entries of last_mp / last_outlier
+    int n_last, n_mp, n_local, cap; // n_last: entries of last_mp / last_outlier; n_local: frustum search's points
     const int32_t* last_cnt;        // LastFrame in a slot: its keypoint count (else null)
     const int32_t* err;             // the context's error flags (read back with the outputs)
     const float* mp_pos;
@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(kTrackThreads) void k_track_stage(TrackDev d, int s
             *d.local_n_w = 0;
             SearchArgs& j = *d.local_job;
             *j.fr_count = 0;
-            j.nq = ok ? d.n_mp : 0;
+            j.nq = ok ? d.n_local : 0;
             if (ok) {
                 // Frame::UpdatePoseMatrices (src/Frame.cc:129-134): Rcw, tcw,
                 // Ow = -Rcw^T tcw (float, left to right)
@@ -1798,6 +1798,7 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
         if (q->last_mp[i] >= q->n_mp) return ORBX_ERR_ARG;
     const Geometry& g = ctx->geom;
     const int nf = g.nfeatures, m = q->n_mp, cap = std::max(nf, 1);
+    const int m_local = q->n_local_mp > 0 ? std::min(q->n_local_mp, m) : m;   // the frustum search's points
     const size_t img_bytes = q->image ? (size_t)q->w * q->h : 0;
     // [inputs | SearchArgs x2 | read-back block | device-only state]
     Uploader u{ctx};
@@ -1817,7 +1818,7 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     const size_t o_skip = u.reserve(m), o_hdr = u.reserve(2 * sizeof(PoseHdr)), o_edg = u.reserve((size_t)cap * 48);
     const size_t o_ekp = u.reserve((size_t)cap * 8), o_flg = u.reserve((size_t)cap * 2);
     const size_t o_pout = u.reserve(2 * sizeof(PoseOut)), o_st = u.reserve(16);
-    const AreaBufs am = reserve_area(u, 1, n1), al = reserve_area(u, 1, m);
+    const AreaBufs am = reserve_area(u, 1, n1), al = reserve_area(u, 1, m_local);
     r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
     if (r == ORBX_OK) r = pin.open(out_end);
@@ -1914,6 +1915,7 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     td.last_cnt = from_slot ? ctx->out_n + q->last_slot : nullptr;
     td.err = ctx->error_flags;
     td.n_mp = m;
+    td.n_local = m_local;
     td.cap = cap;
     td.mp_pos = jl.q_xyz;
     td.mp_skip_in = q->mp_skip ? d + o_skin : nullptr;
@@ -1971,8 +1973,8 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     stage(1);
     if ((r = launch_pose_device(ctx, td.hdr, ed, flags, pout, 1)) != ORBX_OK) return r;
     stage(2);
-    if (m > 0) hipLaunchKernelGGL(k_frustum, dim3((m + 255) / 256, 1), dim3(256), 0, ctx->stream, dl);
-    if ((r = launch_area_search<kQLocal>(ctx, dl, 1, m, nf, u, al)) != ORBX_OK) return r;
+    if (m_local > 0) hipLaunchKernelGGL(k_frustum, dim3((m_local + 255) / 256, 1), dim3(256), 0, ctx->stream, dl);
+    if ((r = launch_area_search<kQLocal>(ctx, dl, 1, m_local, nf, u, al)) != ORBX_OK) return r;
     stage(3);
     if ((r = launch_pose_device(ctx, td.hdr + 1, ed, flags, pout + 1, 1)) != ORBX_OK) return r;
     stage(4);

@@ -152,6 +152,20 @@ def test_track_sequence_chains_slots(ctx, ref, pose_mode):
         kl, dl, slot_last, T_last = kc, dc, slot, got["Tcw"]
 
 
+def test_track_frame_last_frame_points_outside_local_map(ctx, ref, pose_mode):
+    """n_local_mp: only the first points are the local map searched in the
+    frustum step; the last frame's other points still feed the motion
+    search."""
+    pose_mode(1)
+    _, _, kl, dl, kc, dc, scene, Tpred = setup(ctx, 10, 7, 1.0)
+    scene["n_local"] = len(kl) // 2
+    got = run(ctx, scene, Tpred, slot=1, last_view=ox.frame_view(kl, dl, W, H))
+    exp = td.ref_chain(ref, kl, dl, kc, dc, scene, Tpred)
+    assert exp["status"] == 0
+    compare(got, exp, True)
+    assert (got["cur_mp"] >= len(kl) // 2).any()   # motion-only points were matched
+
+
 def test_track_frame_rejects_bad_queries(ctx):
     _, _, kl, dl, kc, dc, scene, Tpred = setup(ctx, 9, 6, 1.0)
     L = ox.lib()

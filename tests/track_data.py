@@ -26,7 +26,7 @@ class TrackQuery(ctypes.Structure):
     _fields_ = [("slot", ctypes.c_int), ("image", vp), ("w", ctypes.c_int), ("h", ctypes.c_int),
                 ("stride", ctypes.c_size_t), ("last_slot", ctypes.c_int), ("last_cap", ctypes.c_int),
                 ("last", vp), ("last_mp", vp), ("last_outlier", vp), ("n_mp", ctypes.c_int),
-                ("mp_pos", vp), ("mp_normal", vp), ("mp_dist", vp), ("mp_desc", vp), ("mp_skip", vp),
+                ("n_local_mp", ctypes.c_int), ("mp_pos", vp), ("mp_normal", vp), ("mp_dist", vp), ("mp_desc", vp), ("mp_skip", vp),
                 ("Tcw_pred", vp), ("cam", vp), ("inv_level_sigma2", vp), ("nlevels", ctypes.c_int),
                 ("th_local", ctypes.c_float), ("Tcw", ctypes.c_float * 12), ("cur_mp", vp),
                 ("cur_outlier", vp), ("cap", ctypes.c_int), ("n_cur", ctypes.c_int), ("status", ctypes.c_int),
@@ -120,6 +120,7 @@ def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h
     q.last_mp = scene["last_mp"].ctypes.data
     q.last_outlier = scene["last_outlier"].ctypes.data
     q.n_mp = len(scene["pos"])
+    q.n_local_mp = scene.get("n_local", 0)
     for f, k in (("mp_pos", "pos"), ("mp_normal", "normal"), ("mp_dist", "dist"), ("mp_desc", "desc"),
                  ("mp_skip", "skip"), ("cam", "cam"), ("inv_level_sigma2", "isig")):
         setattr(q, f, keep[k].ctypes.data)
@@ -202,7 +203,7 @@ def ref_chain(L, kl, dl, kc, dc, scene, Tpred, w=640, h=480, th_local=1.0, nleve
     f32 = np.float32
     Ow = np.array([-((f32(T[0, c]) * T[0, 3] + f32(T[1, c]) * T[1, 3]) + f32(T[2, c]) * T[2, 3]) for c in range(3)],
                   np.float32)
-    n = len(scene["pos"])
+    n = scene.get("n_local", 0) or len(scene["pos"])   # the frustum search's points (the first n)
     matches = np.zeros(nc, np.int32)
     q = LocalMapQuery()
     q.frame = ctypes.addressof(Cv)
