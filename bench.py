@@ -672,6 +672,16 @@ def single_call_legs(args, frames, nf, w, h):
         leg["matches_identical"] = bool(same)
         leg["max_abs_tcw_diff_vs_oracle"] = float(np.abs(got["Tcw"] - texp["Tcw"]).max())
         tr[key] = leg
+    # mode 1: TrackPreviousFrame then TrackLocalMap (the reference's fallback
+    # after a failed motion model), on the same frames
+    tq_prev, tkeep_prev = td.query(tscene, td.pose_x(0.0), slot=1, last_slot=0, cap=nf, mode=1)
+    tr["previous_frame_chain_only"] = time_calls(
+        lambda i: check_rc(L.orbx_track_frame(ctxt.handle, ctypes.byref(tq_prev)), "orbx_track_frame"), 1, proto)
+    pgot = td.result(tq_prev, tkeep_prev)
+    pexp = td.ref_chain_prev(P, tkl, tdl, tkc, tdc, tscene, td.pose_x(0.0))
+    tr["previous_frame_chain_only"]["identical_to_oracle"] = bool(
+        all(pgot[k] == pexp[k] for k in ("status", "n_motion", "n_pair", "n_after_pose", "n_local", "n_inliers"))
+        and np.array_equal(pgot["cur_mp"], pexp["cur_mp"]) and np.array_equal(pgot["Tcw"], pexp["Tcw"]))
     ctxt.close()
     tr["cpu"] = {"with_extraction": time_calls(lambda i: (rex(cur_img), td.ref_chain(R, tkl, tdl, tkc, tdc, tscene,
                                                                                    tpred)), 1, proto),

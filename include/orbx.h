@@ -405,6 +405,12 @@ int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q);
  *   -> SearchReferencePointsInFrustum: isInFrustum of the local map points
  *      not already matched, SearchByProjection(F, local map, th)
  *   -> PoseOptimization on all matches
+ * (mode 0) or, mode 1, TrackPreviousFrame's
+ *   WindowSearch(last, current, 200, minOctave), < 10: WindowSearch(100)
+ *   -> >= 10: PoseOptimization from mLastFrame.mTcw, outliers discarded,
+ *      SearchByProjection(last, current, 15); else SearchByProjection(.., 50)
+ *   -> < 10 matches: status 3; PoseOptimization, outliers discarded; < 10: 4
+ * followed by the same local-map search and PoseOptimization,
  * runs without a host round trip: one upload (last frame, local map, pose
  * prediction, image) and one read-back.  The last frame's map points are
  * named by their index in the map-point arrays.  The local map is an input:
@@ -420,6 +426,11 @@ int orbx_search_local_map(orbx_ctx* ctx, orbx_local_map_query* q);
  * orbx_dev_undistort wrote; the frame bounds those of
  * orbx_dev_set_image_bounds (default 0..w, 0..h). */
 typedef struct {
+    int mode;                       /* 0: TrackWithMotionModel (src/Tracking.cc:572-611);
+                                       1: TrackPreviousFrame (:497-569, the reference's
+                                       fallback after status 1); both then TrackLocalMap  */
+    int min_octave;                 /* mode 1: WindowSearch's minOctave (maxOctave / 2 + 1
+                                       when KeyFramesInMap() > 5, else 0, :505-507)        */
     int slot;                       /* current frame's slot                                */
     const uint8_t* image;           /* NULL (slot already extracted) or the mono8 image    */
     int w, h;                       /* image size (also the default bounds)                */
@@ -440,7 +451,8 @@ typedef struct {
     const float* mp_dist;           /* n_mp x 2: min, max distance invariance              */
     const uint8_t* mp_desc;         /* n_mp x 32                                           */
     const uint8_t* mp_skip;         /* n_mp or NULL: isBad()                               */
-    const float* Tcw_pred;          /* 12 (rows 0..2 of mVelocity * LastFrame.mTcw)        */
+    const float* Tcw_pred;          /* 12: mode 0 rows 0..2 of mVelocity * mLastFrame.mTcw,
+                                       mode 1 of mLastFrame.mTcw                          */
     const float* cam;               /* fx, fy, cx, cy                                      */
     const float* inv_level_sigma2;  /* nlevels (mvInvLevelSigma2)                          */
     int nlevels;
@@ -452,9 +464,14 @@ typedef struct {
     uint8_t* cur_outlier;           /* cap: mvbOutlier after the last PoseOptimization      */
     int cap;                        /* capacity of cur_mp / cur_outlier                    */
     int n_cur;                      /* current frame's keypoints                           */
-    int status;                     /* 0 tracked (TrackLocalMap ran), 1 / 2 see above      */
-    int n_motion;                   /* SearchByProjection(current, last) matches           */
-    int n_after_pose;               /* matches left after the first PoseOptimization       */
+    int status;                     /* 0 tracked (TrackLocalMap ran); mode 0: 1 / 2 above;
+                                       mode 1: 3 < 10 matches after the window and pair
+                                       searches, 4 < 10 left after their PoseOptimization */
+    int n_motion;                   /* mode 0: SearchByProjection(current, last) matches;
+                                       mode 1: the WindowSearch's (200, else 100)         */
+    int n_pair;                     /* mode 1: SearchByProjection(last, current, 15 / 50)  */
+    int n_after_pose;               /* matches left after the PoseOptimization before the
+                                       local-map search                                   */
     int n_in_view;                  /* local map points in view (nToMatch)                  */
     int n_local;                    /* SearchByProjection(F, local map) matches            */
     int n_inliers;                  /* the last PoseOptimization's return value            */

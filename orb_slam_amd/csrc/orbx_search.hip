@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256) void k_hamming_bf(const uint8_t* dA, int nA, c
 // ---------------------------------------------------------------------------
 struct TrackOut {
     float T[12];
-    int n_cur, status, n_motion, n_after_pose, n_in_view, n_local, n_inliers, err;
+    int n_cur, status, n_motion, n_pair, n_after_pose, n_in_view, n_local, n_inliers, err, pad[3];
 };
 
 struct TrackDev {
@@ -988,12 +988,23 @@ struct TrackDev {
     uint8_t* f_assigned;
     uint8_t* mp_skip;
     SearchArgs* local_job;
-    PoseHdr* hdr;                   // 2 problems
-    float* edges;                   // 6 arrays x 2 cap
-    int32_t* edge_kp;               // 2 cap
-    const uint8_t* flags;           // 2 cap (k_pose_opt's outlier flags)
-    const PoseOut* pout;            // 2
-    int32_t* st;                    // status, n_motion, n_after_pose
+    PoseHdr* hdr;                   // 3 problems: before the local map, after it, TrackPreviousFrame's first
+    float* edges;                   // 6 arrays x 3 cap
+    int32_t* edge_kp;               // 3 cap
+    const uint8_t* flags;           // 3 cap (k_pose_opt's outlier flags)
+    const PoseOut* pout;            // 3
+    int32_t* st;                    // status, matches before pose 0, left after it, first search's, pair's
+    // TrackPreviousFrame (mode 1): the two WindowSearch jobs and the pair
+    // search's, their outputs, the window and pair queries' validity
+    int mode, min_octave;
+    SearchArgs* win_job[2];
+    SearchArgs* pair_job;
+    int32_t* win_out[2];
+    int32_t* win_n[2];
+    int32_t* pair_out;
+    int32_t* pair_n;
+    uint8_t* w_valid;
+    uint8_t* p_valid;
     TrackOut* out;                  // read-back block: TrackOut, cur_mp[cap], cur_outlier[cap]
 };
 
@@ -1007,7 +1018,7 @@ __device__ inline void track_build_pose(const TrackDev& d, int p, const float* T
 {
     const int tid = threadIdx.x;
     float* ox = d.edges;
-    const size_t arr = (size_t)2 * d.cap;
+    const size_t arr = (size_t)3 * d.cap;
     int base = 0;
     for (int c0 = 0; c0 < n; c0 += kT) {
         const int i = c0 + tid;
@@ -1068,6 +1079,111 @@ __global__ __launch_bounds__(kTrackThreads) void k_track_stage(TrackDev d, int s
         return;
     }
     const int status = d.st[0];
+    if (stage == 10) {
+        // TrackPreviousFrame (src/Tracking.cc:497-569): WindowSearch queries
+        // are the last frame's points that are not bad (no outlier test,
+        // src/ORBmatcher.cc:424-430); all outputs cleared
+        const int nl = d.last_cnt ? min(*d.last_cnt, d.n_last) : d.n_last;
+        for (int i = tid; i < d.n_last; i += kTrackThreads) {
+            const int m = i < nl ? d.last_mp[i] : -1;
+            d.w_valid[i] = m >= 0 && m < d.n_mp && !(d.mp_skip_in && d.mp_skip_in[m]);
+        }
+        for (int i = tid; i < d.cap; i += kTrackThreads) {
+            d.win_out[0][i] = d.win_out[1][i] = d.pair_out[i] = -1;
+            d.f_assigned[i] = 0;
+        }
+        if (tid == 0) {
+            for (int k = 0; k < 5; k++) d.st[k] = 0;
+            *d.win_n[0] = *d.win_n[1] = *d.pair_n = 0;
+        }
+        return;
+    }
+    if (stage == 11) {   // < 10: WindowSearch(100) without the scale constraint (:514-517)
+        // (F1.n is the window kind's query count: 0 makes the launch a no-op)
+        if (tid == 0 && *d.win_n[0] >= 10) d.win_job[1]->F1.n = 0;
+        return;
+    }
+    if (stage == 12) {
+        // the window matches taken (< 10 after both: none, :518-522);
+        // mCurrentFrame.mTcw = mLastFrame.mTcw; >= 10: PoseOptimization
+        const int n0 = *d.win_n[0], n1 = *d.win_n[1];
+        const int src = n0 >= 10 ? 0 : (n1 >= 10 ? 1 : -1);
+        const int nm = src < 0 ? 0 : (src == 0 ? n0 : n1);
+        for (int i = tid; i < n; i += kTrackThreads) {
+            const int m = src < 0 ? -1 : d.win_out[src][i];
+            d.cur_mp[i] = m >= 0 ? d.last_mp[m] : -1;
+        }
+        __syncthreads();
+        track_build_pose<kTrackThreads>(d, 2, d.Tpred, nm >= 10, n, bs);
+        if (tid == 0) {
+            d.st[1] = nm;
+            d.st[3] = nm;
+        }
+        return;
+    }
+    if (stage == 13) {
+        // >= 10: outliers discarded, SearchByProjection(last, current, 15) at
+        // the optimised pose; else (none kept) at mLastFrame.mTcw with 50
+        // (:531-547).  Its queries: the last frame's points that are not bad
+        // and not already among the current frame's (:530-534); candidates:
+        // the current keypoints without a point
+        const int nm = d.st[1];
+        const bool posed = nm >= 10;
+        if (tid == 0) s_cnt = 0;
+        for (int m = tid; m < d.n_mp; m += kTrackThreads) d.mp_skip[m] = 0;   // "already found" set
+        __syncthreads();
+        int nout = 0;
+        if (posed) {
+            const int nE = d.hdr[2].nE;
+            for (int e = tid; e < nE; e += kTrackThreads)
+                if (d.flags[(size_t)2 * d.cap + e]) {
+                    d.cur_mp[d.edge_kp[(size_t)2 * d.cap + e]] = -1;
+                    nout++;
+                }
+            if (nout) atomicAdd(&s_cnt, nout);
+        }
+        __syncthreads();
+        for (int i = tid; i < d.cap; i += kTrackThreads) {
+            const int m = i < n ? d.cur_mp[i] : -1;
+            d.f_assigned[i] = m >= 0;
+            if (m >= 0) d.mp_skip[m] = 1;
+        }
+        __syncthreads();
+        const int nl = d.last_cnt ? min(*d.last_cnt, d.n_last) : d.n_last;
+        for (int i = tid; i < d.n_last; i += kTrackThreads) {
+            const int m = i < nl ? d.last_mp[i] : -1;
+            const bool v = d.w_valid[i] && !d.mp_skip[m];
+            d.p_valid[i] = v;
+            d.q_xyz[3 * i] = v ? d.mp_pos[3 * m] : 0.f;
+            d.q_xyz[3 * i + 1] = v ? d.mp_pos[3 * m + 1] : 0.f;
+            d.q_xyz[3 * i + 2] = v ? d.mp_pos[3 * m + 2] : 0.f;
+        }
+        if (tid == 0) {
+            SearchArgs& j = *d.pair_job;
+            const float* T = posed ? d.pout[2].T : d.Tpred;
+            for (int k = 0; k < 12; k++) j.T[k] = T[k];
+            j.window = posed ? 15 : 50;
+            d.st[1] = posed ? nm - s_cnt : 0;   // nmatches before the pair search
+        }
+        return;
+    }
+    if (stage == 14) {
+        // the pair search's matches added (vpMapPointMatches, :548); < 10:
+        // fail; else PoseOptimization from the pose the search used (:553-556)
+        for (int i = tid; i < n; i += kTrackThreads) {
+            const int m = d.pair_out[i];
+            if (m >= 0) d.cur_mp[i] = d.last_mp[m];
+        }
+        const int np = *d.pair_n, total = d.st[1] + np;
+        __syncthreads();
+        track_build_pose<kTrackThreads>(d, 0, d.pair_job->T, total >= 10, n, bs);
+        if (tid == 0) {
+            d.st[4] = np;
+            d.st[1] = total;
+            d.st[0] = total >= 10 ? 0 : 3;
+        }
+        return;
+    }
     if (stage == 1) {
         // mvpMapPoints of the current frame = the last frame's points found
         // (src/ORBmatcher.cc:1575); < 20 matches: TrackWithMotionModel fails
@@ -1140,7 +1256,7 @@ __global__ __launch_bounds__(kTrackThreads) void k_track_stage(TrackDev d, int s
                     j.Ow[c] = -__fadd_rn(__fadd_rn(__fmul_rn(T[c], T[3]), __fmul_rn(T[4 + c], T[7])),
                                          __fmul_rn(T[8 + c], T[11]));
             }
-            d.st[0] = status != 0 ? status : (ok ? 0 : 2);
+            d.st[0] = status != 0 ? status : (ok ? 0 : (d.mode ? 4 : 2));
             d.st[2] = left;
         }
         return;
@@ -1173,15 +1289,21 @@ __global__ __launch_bounds__(kTrackThreads) void k_track_stage(TrackDev d, int s
     }
     if (tid == 0) {
         TrackOut& o = *d.out;
-        const float* T = status == 0 ? d.pout[1].T : status == 2 ? d.pout[0].T : d.Tpred;
+        // the pose of the last PoseOptimization that ran (status 3: the pair
+        // search's pose, i.e. the first one's or mLastFrame.mTcw)
+        const float* T = status == 0 ? d.pout[1].T
+                         : (status == 2 || status == 4) ? d.pout[0].T
+                         : status == 3 ? d.pair_job->T : d.Tpred;
         for (int k = 0; k < 12; k++) o.T[k] = T[k];
         o.n_cur = n;
         o.status = status;
-        o.n_motion = d.st[1];
-        o.n_after_pose = status == 1 ? 0 : d.st[2];
+        o.n_motion = d.mode ? d.st[3] : d.st[1];
+        o.n_pair = d.mode ? d.st[4] : 0;
+        o.n_after_pose = (status == 0 || status == 2 || status == 4) ? d.st[2] : 0;
         o.n_in_view = status == 0 ? *d.local_job->fr_count : 0;
         o.n_local = (status == 0 && *d.local_job->fr_count > 0) ? *d.local_n : 0;
-        o.n_inliers = status == 0 ? d.pout[1].n_inliers : status == 2 ? d.pout[0].n_inliers : 0;
+        o.n_inliers = status == 0 ? d.pout[1].n_inliers : (status == 2 || status == 4) ? d.pout[0].n_inliers : 0;
+        o.pad[0] = o.pad[1] = o.pad[2] = 0;
         o.err = *d.err;
     }
 }
@@ -1784,8 +1906,9 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
         (!from_slot && !valid_view(q->last)) || (from_slot && q->last_cap < 0) || q->n_mp < 0 ||
         (q->n_mp > 0 && (!q->mp_pos || !q->mp_normal || !q->mp_dist || !q->mp_desc)) || !q->Tcw_pred || !q->cam ||
         !q->inv_level_sigma2 || !q->cur_mp || !q->cur_outlier || q->cap < 0 || q->nlevels <= 0 ||
-        q->nlevels > kMaxLevels)
+        q->nlevels > kMaxLevels || q->mode < 0 || q->mode > 1 || q->min_octave < 0)
         return ORBX_ERR_ARG;
+    const bool prev = q->mode == 1;   // TrackPreviousFrame
     const int n1 = from_slot ? q->last_cap : q->last->n;
     if (from_slot && n1 > ctx->geom.nfeatures) return ORBX_ERR_ARG;
     if (n1 > 0 && (!q->last_mp || !q->last_outlier)) return ORBX_ERR_ARG;
@@ -1808,16 +1931,30 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     const size_t o_pos = u.reserve((size_t)m * 12), o_nrm = u.reserve((size_t)m * 12), o_dist = u.reserve((size_t)m * 8);
     const size_t o_desc = u.reserve((size_t)m * 32), o_skin = u.reserve(m), o_isig = u.reserve(4 * kMaxLevels);
     const size_t o_img = u.reserve(img_bytes);
-    const size_t o_jm = u.reserve(sizeof(SearchArgs)), o_jl = u.reserve(sizeof(SearchArgs)), in_end = u.total;
+    const size_t o_jm = u.reserve(sizeof(SearchArgs)), o_jl = u.reserve(sizeof(SearchArgs));
+    // mode 1: the two WindowSearch jobs and the pair search's
+    const size_t o_jw = u.reserve(prev ? 2 * sizeof(SearchArgs) : 0), o_jp = u.reserve(prev ? sizeof(SearchArgs) : 0);
+    const size_t in_end = u.total;
     const size_t o_out = u.reserve(sizeof(TrackOut) + (size_t)cap * 5), out_end = u.total;
     const size_t o_qxyz = u.reserve((size_t)n1 * 12), o_qv = u.reserve(n1);
     const size_t o_mout = u.reserve((size_t)cap * 4 + 4), o_mn = u.reserve(4);
     const size_t o_lo = u.reserve((size_t)cap * 4 + 4), o_ln = u.reserve(4), o_cnt = u.reserve(4);
     const size_t o_fiv = u.reserve(m), o_fpr = u.reserve((size_t)m * 8), o_fpl = u.reserve((size_t)m * 4);
     const size_t o_fcos = u.reserve((size_t)m * 4), o_cmp = u.reserve((size_t)cap * 4), o_fas = u.reserve(cap);
-    const size_t o_skip = u.reserve(m), o_hdr = u.reserve(2 * sizeof(PoseHdr)), o_edg = u.reserve((size_t)cap * 48);
-    const size_t o_ekp = u.reserve((size_t)cap * 8), o_flg = u.reserve((size_t)cap * 2);
-    const size_t o_pout = u.reserve(2 * sizeof(PoseOut)), o_st = u.reserve(16);
+    const size_t o_skip = u.reserve(m), o_hdr = u.reserve(3 * sizeof(PoseHdr)), o_edg = u.reserve((size_t)cap * 72);
+    const size_t o_ekp = u.reserve((size_t)cap * 12), o_flg = u.reserve((size_t)cap * 3);
+    const size_t o_pout = u.reserve(3 * sizeof(PoseOut)), o_st = u.reserve(32);
+    size_t o_wout[2] = {0, 0}, o_wn[2] = {0, 0}, o_pout2 = 0, o_pn = 0, o_wv = 0, o_pv = 0;
+    if (prev) {
+        for (int k = 0; k < 2; k++) {
+            o_wout[k] = u.reserve((size_t)cap * 4 + 4);
+            o_wn[k] = u.reserve(4);
+        }
+        o_pout2 = u.reserve((size_t)cap * 4 + 4);
+        o_pn = u.reserve(4);
+        o_wv = u.reserve(n1);
+        o_pv = u.reserve(n1);
+    }
     const AreaBufs am = reserve_area(u, 1, n1), al = reserve_area(u, 1, m_local);
     r = ensure_scratch(ctx, u.total);
     Pinned pin{ctx};
@@ -1906,6 +2043,39 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     jl.out_n = reinterpret_cast<int32_t*>(d + o_ln);
     pin.put(o_jm, &jm, sizeof(jm));
     pin.put(o_jl, &jl, sizeof(jl));
+    if (prev) {
+        // WindowSearch(mLastFrame, mCurrentFrame, 200, minOctave) and (100, 0),
+        // ORBmatcher(0.9, true) (src/Tracking.cc:500-517)
+        for (int k = 0; k < 2; k++) {
+            SearchArgs jw{};
+            jw.F1 = jm.F1;
+            jw.F2 = jm.F2;
+            jw.F2_cnt = jm.F2_cnt;
+            jw.q_valid = d + o_wv;
+            jw.window = k == 0 ? 200 : 100;
+            jw.min_level = k == 0 ? q->min_octave : 0;
+            jw.max_level = 0x7fffffff;
+            jw.nnratio = 0.9f;
+            jw.check_ori = 1;
+            jw.out = reinterpret_cast<int32_t*>(d + o_wout[k]);
+            jw.out_n = reinterpret_cast<int32_t*>(d + o_wn[k]);
+            pin.put(o_jw + k * sizeof(SearchArgs), &jw, sizeof(jw));
+        }
+        // SearchByProjection(mLastFrame, mCurrentFrame, 15 or 50) (:544, :547):
+        // pose and window set on the device
+        SearchArgs jp{};
+        jp.F1 = jm.F1;
+        jp.F2 = jm.F2;
+        jp.F2_cnt = jm.F2_cnt;
+        jp.q_xyz = jm.q_xyz;
+        jp.q_valid = d + o_pv;
+        jp.f2_assigned = d + o_fas;
+        for (int i = 0; i < 4; i++) jp.cam[i] = q->cam[i];
+        jp.nnratio = 0.9f;
+        jp.out = reinterpret_cast<int32_t*>(d + o_pout2);
+        jp.out_n = reinterpret_cast<int32_t*>(d + o_pn);
+        pin.put(o_jp, &jp, sizeof(jp));
+    }
     TrackDev td{};
     td.cur_kps = jm.F2.kps;
     td.cur_cnt = jm.F2_cnt;
@@ -1943,6 +2113,22 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     td.pout = reinterpret_cast<const PoseOut*>(d + o_pout);
     td.st = reinterpret_cast<int32_t*>(d + o_st);
     td.out = reinterpret_cast<TrackOut*>(d + o_out);
+    td.mode = q->mode;
+    td.min_octave = q->min_octave;
+    if (prev) {
+        for (int k = 0; k < 2; k++) {
+            td.win_job[k] = reinterpret_cast<SearchArgs*>(d + o_jw + k * sizeof(SearchArgs));
+            td.win_out[k] = reinterpret_cast<int32_t*>(d + o_wout[k]);
+            td.win_n[k] = reinterpret_cast<int32_t*>(d + o_wn[k]);
+        }
+        td.pair_job = reinterpret_cast<SearchArgs*>(d + o_jp);
+        td.pair_out = reinterpret_cast<int32_t*>(d + o_pout2);
+        td.pair_n = reinterpret_cast<int32_t*>(d + o_pn);
+        td.w_valid = d + o_wv;
+        td.p_valid = d + o_pv;
+    } else {
+        td.pair_job = reinterpret_cast<SearchArgs*>(d + o_jm);   // stage 4 reads its T only for status 3
+    }
     // one upload; the image into its slot and the slot's extraction
     if ((r = pin.upload(in_end)) != ORBX_OK) return r;
     if (q->image) {
@@ -1956,7 +2142,7 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
         if (r != ORBX_OK) return r;
     }
     PoseEdgeArrays ed;
-    const size_t arr = (size_t)2 * cap;
+    const size_t arr = (size_t)3 * cap;
     ed.ox = td.edges;
     ed.oy = td.edges + arr;
     ed.isig = td.edges + 2 * arr;
@@ -1968,9 +2154,24 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     const SearchArgs* dm = reinterpret_cast<const SearchArgs*>(d + o_jm);
     const SearchArgs* dl = reinterpret_cast<const SearchArgs*>(d + o_jl);
     auto stage = [&](int s) { hipLaunchKernelGGL(k_track_stage, dim3(1), dim3(kTrackThreads), 0, ctx->stream, td, s); };
-    stage(0);
-    if ((r = launch_area_search<kQMotion>(ctx, dm, 1, n1, nf, u, am)) != ORBX_OK) return r;
-    stage(1);
+    if (!prev) {
+        stage(0);
+        if ((r = launch_area_search<kQMotion>(ctx, dm, 1, n1, nf, u, am)) != ORBX_OK) return r;
+        stage(1);
+    } else {
+        const SearchArgs* dw = reinterpret_cast<const SearchArgs*>(d + o_jw);
+        stage(10);
+        if ((r = launch_area_search<kQWindow>(ctx, dw, 1, n1, nf, u, am)) != ORBX_OK) return r;
+        stage(11);
+        if ((r = launch_area_search<kQWindow>(ctx, dw + 1, 1, n1, nf, u, am)) != ORBX_OK) return r;
+        stage(12);
+        if ((r = launch_pose_device(ctx, td.hdr + 2, ed, flags, pout + 2, 1)) != ORBX_OK) return r;
+        stage(13);
+        if ((r = launch_area_search<kQPair>(ctx, reinterpret_cast<const SearchArgs*>(d + o_jp), 1, n1, nf, u, am)) !=
+            ORBX_OK)
+            return r;
+        stage(14);
+    }
     if ((r = launch_pose_device(ctx, td.hdr, ed, flags, pout, 1)) != ORBX_OK) return r;
     stage(2);
     if (m_local > 0) hipLaunchKernelGGL(k_frustum, dim3((m_local + 255) / 256, 1), dim3(256), 0, ctx->stream, dl);
@@ -1986,6 +2187,7 @@ int orbx_track_frame(orbx_ctx* ctx, orbx_track_query* q)
     q->n_cur = o.n_cur;
     q->status = o.status;
     q->n_motion = o.n_motion;
+    q->n_pair = o.n_pair;
     q->n_after_pose = o.n_after_pose;
     q->n_in_view = o.n_in_view;
     q->n_local = o.n_local;

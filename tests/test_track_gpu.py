@@ -60,7 +60,7 @@ def run(ctx, scene, Tpred, **kw):
 
 
 def compare(got, exp, exact):
-    for k in ("status", "n_cur", "n_motion", "n_after_pose", "n_in_view", "n_local", "n_inliers"):
+    for k in ("status", "n_cur", "n_motion", "n_pair", "n_after_pose", "n_in_view", "n_local", "n_inliers"):
         assert got[k] == exp[k], (k, got[k], exp[k])
     assert np.array_equal(got["cur_mp"], exp["cur_mp"]), np.count_nonzero(got["cur_mp"] != exp["cur_mp"])
     assert np.array_equal(got["cur_outlier"], exp["cur_outlier"])
@@ -166,15 +166,50 @@ def test_track_frame_last_frame_points_outside_local_map(ctx, ref, pose_mode):
     assert (got["cur_mp"] >= len(kl) // 2).any()   # motion-only points were matched
 
 
+@pytest.mark.parametrize("seed,shift,min_octave,observed", [(1, 6, 0, 0.8), (2, 10, 4, 0.8), (3, 3, 0, 0.02),
+                                                            (5, 40, 0, 0.8), (6, 6, 0, 0.05)])
+def test_track_previous_frame_matches_oracle_chain(ctx, ref, pose_mode, seed, shift, min_octave, observed):
+    """mode 1 (TrackPreviousFrame then TrackLocalMap): the window searches,
+    the pose from mLastFrame.mTcw, the pair search at 15 (or 50 with too few
+    window matches), the pose, the local map -- bit for bit."""
+    pose_mode(1)
+    last, cur = td.images(W, H, shift, seed)
+    kl, dl = features(ctx, last, 0)
+    kc, dc = features(ctx, cur, 1)
+    scene = td.make_scene(kl, dl, seed, observed=observed)
+    Tl = td.pose_x(0.0)
+    got = run(ctx, scene, Tl, slot=1, last_view=ox.frame_view(kl, dl, W, H), mode=1, min_octave=min_octave)
+    exp = td.ref_chain_prev(ref, kl, dl, kc, dc, scene, Tl, min_octave=min_octave)
+    assert exp["status"] == 0
+    compare(got, exp, True)
+    assert got["n_pair"] == exp["n_pair"]
+
+
+def test_track_previous_frame_failure(ctx, ref, pose_mode):
+    """Almost no map points in the last frame: < 10 window matches, the
+    pair search at 50 from mLastFrame.mTcw finds too few: status 3."""
+    pose_mode(1)
+    last, cur = td.images(W, H, 6, 11)
+    kl, dl = features(ctx, last, 0)
+    kc, dc = features(ctx, cur, 1)
+    scene = td.make_scene(kl, dl, 11, observed=0.004)
+    Tl = td.pose_x(0.0)
+    got = run(ctx, scene, Tl, slot=1, last_slot=0, mode=1)
+    exp = td.ref_chain_prev(ref, kl, dl, kc, dc, scene, Tl)
+    assert exp["status"] == 3
+    compare(got, exp, True)
+
+
 def test_track_frame_rejects_bad_queries(ctx):
     _, _, kl, dl, kc, dc, scene, Tpred = setup(ctx, 9, 6, 1.0)
     L = ox.lib()
     for bad in (dict(slot=7), dict(slot=1, last_slot=1), dict(slot=1, last_slot=0, cap=-1),
-                dict(slot=1, last_slot=0, nlevels=7)):
+                dict(slot=1, last_slot=0, nlevels=7), dict(slot=1, last_slot=0, mode=2),
+                dict(slot=1, last_slot=0, min_octave=-1)):
         kw = dict(last_view=None if "last_slot" in bad else ox.frame_view(kl, dl, W, H))
         kw.update({k: v for k, v in bad.items() if k in ("slot", "last_slot")})
         q, keep = td.query(scene, Tpred, **kw)
-        for k in ("cap", "nlevels"):
+        for k in ("cap", "nlevels", "mode", "min_octave"):
             if k in bad:
                 setattr(q, k, bad[k])
         assert L.orbx_track_frame(ctx.handle, ctypes.byref(q)) == -1, bad

@@ -23,14 +23,14 @@ vp = ctypes.c_void_p
 
 
 class TrackQuery(ctypes.Structure):
-    _fields_ = [("slot", ctypes.c_int), ("image", vp), ("w", ctypes.c_int), ("h", ctypes.c_int),
+    _fields_ = [("mode", ctypes.c_int), ("min_octave", ctypes.c_int), ("slot", ctypes.c_int), ("image", vp), ("w", ctypes.c_int), ("h", ctypes.c_int),
                 ("stride", ctypes.c_size_t), ("last_slot", ctypes.c_int), ("last_cap", ctypes.c_int),
                 ("last", vp), ("last_mp", vp), ("last_outlier", vp), ("n_mp", ctypes.c_int),
                 ("n_local_mp", ctypes.c_int), ("mp_pos", vp), ("mp_normal", vp), ("mp_dist", vp), ("mp_desc", vp), ("mp_skip", vp),
                 ("Tcw_pred", vp), ("cam", vp), ("inv_level_sigma2", vp), ("nlevels", ctypes.c_int),
                 ("th_local", ctypes.c_float), ("Tcw", ctypes.c_float * 12), ("cur_mp", vp),
                 ("cur_outlier", vp), ("cap", ctypes.c_int), ("n_cur", ctypes.c_int), ("status", ctypes.c_int),
-                ("n_motion", ctypes.c_int), ("n_after_pose", ctypes.c_int), ("n_in_view", ctypes.c_int),
+                ("n_motion", ctypes.c_int), ("n_pair", ctypes.c_int), ("n_after_pose", ctypes.c_int), ("n_in_view", ctypes.c_int),
                 ("n_local", ctypes.c_int), ("n_inliers", ctypes.c_int)]
 
 
@@ -49,7 +49,8 @@ def texture(w, h, seed):
 def images(w, h, shift, seed):
     """(last, current): crops of one texture `shift` pixels apart
     (current(x) = last(x + shift))."""
-    tex = texture(w + 64, h, seed)
+    assert 0 <= shift <= 96, shift
+    tex = texture(w + 128, h, seed)
     return (np.ascontiguousarray(tex[:, 32:32 + w]), np.ascontiguousarray(tex[:, 32 + shift:32 + shift + w]))
 
 
@@ -96,7 +97,8 @@ def make_scene(kl, dl, seed, n_extra=400, observed=0.8, outlier=0.05, bad=0.02, 
                 isig=inv_sigma2(nlevels, scale), cam=CAM.copy())
 
 
-def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h=480, cap=1000, th_local=1.0):
+def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h=480, cap=1000, th_local=1.0,
+          mode=0, min_octave=0):
     """orbx_track_query over the scene's arrays; returns (query, keep-alive
     dict with the output arrays cur_mp / cur_outlier)."""
     keep = dict(scene)
@@ -104,6 +106,8 @@ def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h
     keep["cur_mp"] = np.full(cap, -7, np.int32)
     keep["cur_outlier"] = np.full(cap, 7, np.uint8)
     q = TrackQuery()
+    q.mode = mode
+    q.min_octave = min_octave
     q.slot = slot
     if image is not None:
         keep["image"] = np.ascontiguousarray(image, np.uint8)
@@ -136,7 +140,7 @@ def query(scene, Tpred, slot, last_view=None, last_slot=-1, image=None, w=640, h
 def result(q, keep):
     n = q.n_cur
     return dict(Tcw=np.frombuffer(bytes(q.Tcw), np.float32).copy(), status=q.status, n_cur=n,
-                n_motion=q.n_motion, n_after_pose=q.n_after_pose, n_in_view=q.n_in_view, n_local=q.n_local,
+                n_motion=q.n_motion, n_pair=q.n_pair, n_after_pose=q.n_after_pose, n_in_view=q.n_in_view, n_local=q.n_local,
                 n_inliers=q.n_inliers, cur_mp=keep["cur_mp"][:n].copy(), cur_outlier=keep["cur_outlier"][:n].copy())
 
 
@@ -157,47 +161,20 @@ def _ref_pose(L, kc, cur_mp, scene, T12):
     return sp.pose_of(p)[:3].reshape(-1).copy(), arrs["outlier"].copy(), ni.value
 
 
-def ref_chain(L, kl, dl, kc, dc, scene, Tpred, w=640, h=480, th_local=1.0, nlevels=8, scale=1.2):
-    """The chain of include/orbx.h's orbx_track_frame over the oracle:
-    SearchByProjection(cur, last, 15) -> PoseOptimization -> discard ->
-    SearchReferencePointsInFrustum -> PoseOptimization."""
+def _local_tail(L, kc, Cv, scene, cur_mp, T0, out, th_local):
+    """TrackLocalMap after a tracked pose T0: SearchReferencePointsInFrustum
+    (bad matched points dropped, the rest not projected again; Ow = -Rcw^T
+    tcw in float, left to right) and the last PoseOptimization."""
     from local_map_data import LocalMapQuery
-    nl, nc = len(kl), len(kc)
-    Lv = ox.frame_view(kl, dl, w, h, nlevels, scale)
-    Cv = ox.frame_view(kc, dc, w, h, nlevels, scale)
-    lmp = scene["last_mp"]
-    valid = ((lmp >= 0) & (scene["last_outlier"] == 0)).astype(np.uint8)
-    xyz = np.zeros((nl, 3), np.float32)
-    xyz[valid.astype(bool)] = scene["pos"][lmp[valid.astype(bool)]]
-    Tp = np.ascontiguousarray(Tpred, np.float32)
-    mc = np.zeros(nc, np.int32)
-    nm = ctypes.c_int()
-    assert L.orbx_ref_search_by_projection_motion(ctypes.addressof(Cv), ctypes.addressof(Lv), xyz.ctypes.data,
-                                                  valid.ctypes.data, np.zeros(nc, np.uint8).ctypes.data,
-                                                  Tp.ctypes.data, scene["cam"].ctypes.data, 15.0, 1,
-                                                  mc.ctypes.data, ctypes.byref(nm)) == 0
-    cur_mp = np.where(mc >= 0, lmp[np.maximum(mc, 0)], -1).astype(np.int32)
-    out = dict(n_cur=nc, n_motion=nm.value, n_after_pose=0, n_in_view=0, n_local=0, n_inliers=0,
-               cur_outlier=np.zeros(nc, np.uint8))
-    if nm.value < 20:
-        out.update(status=1, Tcw=Tp.copy(), cur_mp=cur_mp)
-        return out
-    T0, fl0, ni0 = _ref_pose(L, kc, cur_mp, scene, Tp)
-    left = nm.value - int(np.count_nonzero(fl0 & (cur_mp >= 0)))
-    cur_mp = np.where(fl0.astype(bool), -1, cur_mp).astype(np.int32)
-    out["n_after_pose"] = left
-    if left < 10:
-        out.update(status=2, Tcw=T0, cur_mp=cur_mp, n_inliers=ni0)
-        return out
-    # SearchReferencePointsInFrustum: bad matched points dropped, the rest
-    # not projected again; Ow = -Rcw^T tcw in float, left to right
+    nc = len(kc)
     skip_in = scene["skip"]
     bad = (cur_mp >= 0) & (skip_in[np.maximum(cur_mp, 0)] != 0)
     cur_mp = np.where(bad, -1, cur_mp).astype(np.int32)
+    out["T_frustum"] = np.asarray(T0, np.float32).reshape(-1).copy()   # (diagnostics)
     skip = skip_in.copy()
     skip[cur_mp[cur_mp >= 0]] = 1
     assigned = (cur_mp >= 0).astype(np.uint8)
-    T = T0.reshape(3, 4)
+    T = np.asarray(T0, np.float32).reshape(3, 4)
     Rcw = np.ascontiguousarray(T[:, :3])
     tcw = np.ascontiguousarray(T[:, 3])
     f32 = np.float32
@@ -222,3 +199,107 @@ def ref_chain(L, kl, dl, kc, dc, scene, Tpred, w=640, h=480, th_local=1.0, nleve
     out.update(status=0, Tcw=T1, cur_mp=cur_mp, cur_outlier=np.where(cur_mp >= 0, fl1, 0).astype(np.uint8),
                n_in_view=q.n_in_view, n_local=q.n_matches if q.n_in_view > 0 else 0, n_inliers=ni1)
     return out
+
+
+def ref_chain(L, kl, dl, kc, dc, scene, Tpred, w=640, h=480, th_local=1.0, nlevels=8, scale=1.2):
+    """The chain of include/orbx.h's orbx_track_frame (mode 0) over the
+    oracle: SearchByProjection(cur, last, 15) -> PoseOptimization -> discard
+    -> SearchReferencePointsInFrustum -> PoseOptimization."""
+    nl, nc = len(kl), len(kc)
+    Lv = ox.frame_view(kl, dl, w, h, nlevels, scale)
+    Cv = ox.frame_view(kc, dc, w, h, nlevels, scale)
+    lmp = scene["last_mp"]
+    valid = ((lmp >= 0) & (scene["last_outlier"] == 0)).astype(np.uint8)
+    xyz = np.zeros((nl, 3), np.float32)
+    xyz[valid.astype(bool)] = scene["pos"][lmp[valid.astype(bool)]]
+    Tp = np.ascontiguousarray(Tpred, np.float32)
+    mc = np.zeros(nc, np.int32)
+    nm = ctypes.c_int()
+    assert L.orbx_ref_search_by_projection_motion(ctypes.addressof(Cv), ctypes.addressof(Lv), xyz.ctypes.data,
+                                                  valid.ctypes.data, np.zeros(nc, np.uint8).ctypes.data,
+                                                  Tp.ctypes.data, scene["cam"].ctypes.data, 15.0, 1,
+                                                  mc.ctypes.data, ctypes.byref(nm)) == 0
+    cur_mp = np.where(mc >= 0, lmp[np.maximum(mc, 0)], -1).astype(np.int32)
+    out = dict(n_cur=nc, n_motion=nm.value, n_pair=0, n_after_pose=0, n_in_view=0, n_local=0, n_inliers=0,
+               cur_outlier=np.zeros(nc, np.uint8))
+    if nm.value < 20:
+        out.update(status=1, Tcw=Tp.copy(), cur_mp=cur_mp)
+        return out
+    T0, fl0, ni0 = _ref_pose(L, kc, cur_mp, scene, Tp)
+    left = nm.value - int(np.count_nonzero(fl0 & (cur_mp >= 0)))
+    cur_mp = np.where(fl0.astype(bool), -1, cur_mp).astype(np.int32)
+    out["n_after_pose"] = left
+    if left < 10:
+        out.update(status=2, Tcw=T0, cur_mp=cur_mp, n_inliers=ni0)
+        return out
+    return _local_tail(L, kc, Cv, scene, cur_mp, T0, out, th_local)
+
+
+def ref_chain_prev(L, kl, dl, kc, dc, scene, Tlast, min_octave=0, w=640, h=480, th_local=1.0, nlevels=8,
+                   scale=1.2):
+    """orbx_track_frame mode 1 over the oracle: TrackPreviousFrame
+    (src/Tracking.cc:497-569) -- WindowSearch(200, minOctave), < 10:
+    WindowSearch(100); >= 10: PoseOptimization from mLastFrame.mTcw, outliers
+    discarded, SearchByProjection(last, current, 15), else (.., 50); < 10:
+    fail; PoseOptimization, outliers discarded, < 10: fail -- then
+    TrackLocalMap."""
+    nl, nc = len(kl), len(kc)
+    Lv = ox.frame_view(kl, dl, w, h, nlevels, scale)
+    Cv = ox.frame_view(kc, dc, w, h, nlevels, scale)
+    lmp = scene["last_mp"]
+    skip_in = scene["skip"]
+    wvalid = ((lmp >= 0) & (skip_in[np.maximum(lmp, 0)] == 0)).astype(np.uint8)
+    Tl = np.ascontiguousarray(Tlast, np.float32)
+    out = dict(n_cur=nc, n_motion=0, n_pair=0, n_after_pose=0, n_in_view=0, n_local=0, n_inliers=0,
+               cur_outlier=np.zeros(nc, np.uint8))
+
+    def window(size, min_level):
+        m = np.zeros(nc, np.int32)
+        n = ctypes.c_int()
+        assert L.orbx_ref_window_search(ctypes.addressof(Lv), ctypes.addressof(Cv), wvalid.ctypes.data, size,
+                                        min_level, -1, 0.9, 1, m.ctypes.data, ctypes.byref(n)) == 0
+        return m, n.value
+
+    m, nm = window(200, min_octave)
+    if nm < 10:
+        m, nm = window(100, 0)
+        if nm < 10:
+            m, nm = np.full(nc, -1, np.int32), 0
+    cur_mp = np.where(m >= 0, lmp[np.maximum(m, 0)], -1).astype(np.int32)
+    out["n_motion"] = nm
+    T = Tl
+    if nm >= 10:
+        T, fl, _ = _ref_pose(L, kc, cur_mp, scene, Tl)
+        nm -= int(np.count_nonzero(fl & (cur_mp >= 0)))
+        cur_mp = np.where(fl.astype(bool), -1, cur_mp).astype(np.int32)
+        size = 15
+    else:
+        cur_mp[:] = -1
+        nm, size = 0, 50
+    found = np.zeros(len(scene["pos"]), bool)
+    found[cur_mp[cur_mp >= 0]] = True
+    pvalid = (wvalid.astype(bool) & ~found[np.maximum(lmp, 0)]).astype(np.uint8)
+    xyz = np.zeros((nl, 3), np.float32)
+    xyz[pvalid.astype(bool)] = scene["pos"][lmp[pvalid.astype(bool)]]
+    assigned = (cur_mp >= 0).astype(np.uint8)
+    T = np.ascontiguousarray(T, np.float32)
+    mp = np.zeros(nc, np.int32)
+    npair = ctypes.c_int()
+    assert L.orbx_ref_search_by_projection_pair(ctypes.addressof(Lv), ctypes.addressof(Cv), xyz.ctypes.data,
+                                                pvalid.ctypes.data, assigned.ctypes.data, T.ctypes.data,
+                                                scene["cam"].ctypes.data, size, 0.9, mp.ctypes.data,
+                                                ctypes.byref(npair)) == 0
+    cur_mp = np.where(mp >= 0, lmp[np.maximum(mp, 0)], cur_mp).astype(np.int32)
+    total = nm + npair.value
+    out["n_pair"] = npair.value
+    if total < 10:
+        out.update(status=3, Tcw=T.copy(), cur_mp=cur_mp)
+        return out
+    T0, fl0, ni0 = _ref_pose(L, kc, cur_mp, scene, T)
+    left = total - int(np.count_nonzero(fl0 & (cur_mp >= 0)))
+    cur_mp = np.where(fl0.astype(bool), -1, cur_mp).astype(np.int32)
+    out["n_after_pose"] = left
+    if left < 10:
+        out.update(status=4, Tcw=T0, cur_mp=cur_mp, n_inliers=ni0)
+        return out
+    return _local_tail(L, kc, Cv, scene, cur_mp, T0, out, th_local)

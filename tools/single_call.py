@@ -149,6 +149,12 @@ if "track" in what:
         print(f"track (exact sums {exact}): image in {ti:.4f} ms, chain only {tc:.4f} ms median; status "
               f"{r['status']} motion {r['n_motion']} in view {r['n_in_view']} local {r['n_local']} "
               f"inliers {r['n_inliers']}", flush=True)
+    assert L.orbx_pose_set_exact(ctx.handle, 1) == 0
+    qp, kp = td.query(scene, td.pose_x(0.0), slot=1, last_slot=0, mode=1)
+    tp = med(lambda i: L.orbx_track_frame(ctx.handle, ctypes.byref(qp)), n)
+    r = td.result(qp, kp)
+    print(f"track previous frame (mode 1): chain only {tp:.4f} ms median; status {r['status']} window "
+          f"{r['n_motion']} pair {r['n_pair']} local {r['n_local']} inliers {r['n_inliers']}", flush=True)
     ctx.close()
 
 if "pose" in what:
