@@ -300,9 +300,17 @@ int orbx_create(orbx_ctx** out, int device, int nfeatures, float scale_factor, i
     init_extractor_tables(ctx->geom, nfeatures, scale_factor, nlevels, fast_th);
     int r = ORBX_OK;
     const int S = max_batch;
-    // one stream up front; the batch pipeline's part and match streams are
-    // created on first use (ensure_aux_streams)
+    // the context stream; a batch context (several slots) also creates the
+    // pipeline's part and match streams now, right after it -- HIP maps the
+    // streams of a process onto its hardware queues in creation order, and
+    // created together they take neighbouring queues (created later, between
+    // other contexts' streams, they were measured to share queues: c2
+    // 249 k -> 226-230 k frames/s on one box).  A one-slot context (the
+    // reference's per-thread extractor / matcher / optimizer) keeps one
+    // stream and creates the others only if a batch call needs them
+    // (ensure_aux_streams), so several such contexts get a queue each.
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) r = ORBX_ERR_HIP;
+    if (r == ORBX_OK && max_batch > 1) r = ensure_aux_streams(ctx);
     if (r == ORBX_OK && (hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
                          hipEventCreateWithFlags(&ctx->ev_extracted, hipEventDisableTiming) != hipSuccess))
