@@ -53,6 +53,9 @@ constexpr int kPoseThreads = 256;   // 4 frames (wavefronts) per workgroup
 constexpr int kPoseLdsEdges = 800;
 // edges a one-frame workgroup (the kW > 1 instances) keeps in LDS: 75 KB
 constexpr int kPoseLdsEdgesWide = 3072;
+// active-edge list capacity of the exact-sum batch kernel (u16 indices, 4 KB
+// per frame); frames with more edges walk all of them every pass
+constexpr int kPoseActCap = 2048;
 #ifndef ORBX_POSE_WIDE
 #define ORBX_POSE_WIDE 4
 #endif
@@ -221,12 +224,22 @@ struct Cam {
 
 // EdgeSE3ProjectXYZ::computeError (types_six_dof_expmap.h:172-177) at pose
 // (q x y z w, t): e = obs - (fx X/Z + cx, fy Y/Z + cy), Xc = q Xw + t.
+__device__ inline bool div_safe(double x, double y, double z);
+__device__ inline double div_rcp(double d);
+__device__ inline double div_by(double n, double d, double y);
 __device__ inline void pose_edge_error(const double* pose, const double X[3], double o0, double o1, const Cam& c,
                                        double pc[3], double& e0, double& e1)
 {
     se3_map(pose, X, pc);
-    const double u = pc[0] / pc[2] * c.fx + c.cx;
-    const double v = pc[1] / pc[2] * c.fy + c.cy;
+    double u, v;
+    if (div_safe(pc[0], pc[1], pc[2])) {   // the two quotients by z through one reciprocal (below)
+        const double y = div_rcp(pc[2]);
+        u = div_by(pc[0], pc[2], y) * c.fx + c.cx;
+        v = div_by(pc[1], pc[2], y) * c.fy + c.cy;
+    } else {
+        u = pc[0] / pc[2] * c.fx + c.cx;
+        v = pc[1] / pc[2] * c.fy + c.cy;
+    }
     e0 = o0 - u;
     e1 = o1 - v;
 }
@@ -245,16 +258,104 @@ __device__ inline void huber2(double e2, double delta, double& rho0, double& rho
     }
 }
 
+// Double division with the reciprocal shared between quotients of one
+// denominator.  The compiler's f64 division is v_div_scale (operands
+// rescaled only near the exponent range's ends), y = v_rcp_f64 refined by two
+// Newton steps fma(y, fma(-d, y, 1), y), then q = n y, r = fma(-d, q, n),
+// v_div_fmas = fma(r, y, q) and v_div_fixup (special values only) -- the
+// correctly rounded n / d.  y depends on d alone, so where v_div_scale leaves
+// both operands alone (div_safe below) div_by returns the same bits as n / d
+// (up to the sign of a zero quotient, which only ever reaches sums and
+// products here, where it changes nothing) for 3 instructions instead of 11.
+__device__ inline double div_rcp(double d)
+{
+    double y = __builtin_amdgcn_rcp(d);
+    y = __fma_rn(y, __fma_rn(-d, y, 1.0), y);
+    return __fma_rn(y, __fma_rn(-d, y, 1.0), y);
+}
+__device__ inline double div_by(double n, double d, double y)
+{
+    const double q = n * y;
+    return __fma_rn(__fma_rn(-d, q, n), y, q);
+}
+// The camera-frame point (x, y, z) of an edge keeps every division of
+// computeError and linearizeOplus away from v_div_scale's rescaling: |x|, |y|
+// zero or in [2^-150, 2^150], |z| in [2^-150, 2^150] bound every numerator
+// (x, y, 1, x y, x^2, y^2) by 2^+-300, every denominator (z, z^2) likewise,
+// so the exponent gap stays below 768 and no operand, reciprocal or quotient
+// is denormal or tiny.  NaN and infinity fail the comparisons.
+__device__ inline bool div_safe(double x, double y, double z)
+{
+    constexpr double lo = 0x1p-150, hi = 0x1p150;
+    const double ax = fabs(x), ay = fabs(y), az = fabs(z);
+    return (ax <= hi) & ((ax >= lo) | (ax == 0.0)) & (ay <= hi) & ((ay >= lo) | (ay == 0.0)) & (az <= hi) &
+           (az >= lo);
+}
+
 // The per-edge terms of one LM linearisation (computeActiveErrors +
 // buildSystem): c[0] the robust chi2, c[1..21] the lower entries of
 // J^T W J, c[22..27] b -- each the value g2o adds for this edge.
+// Fast form (div_safe): the quotients of computeError and linearizeOplus by
+// z and z^2 through two shared reciprocals, and the structural zeros
+// B(0, 4) = B(1, 3) = 0 of the pose Jacobian left out of the products: a
+// left-out product is +-0, and x + (+-0) = x for every x the sums can hold
+// (they start at +0.0, and round-to-nearest never makes -0.0 of it), so each
+// term adds the same value to every sum as g2o's.  Elsewhere the original
+// expressions, division by division.
 __device__ inline void pose_edge_terms(const double* pose, const Cam& cam, double delta, float fo0, float fo1, float fis,
                                        float fx_, float fy_, float fz_, double (&c)[28])
 {
     const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
     const double s = (double)fis;
     double pc[3], er0, er1;
-    pose_edge_error(pose, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
+    se3_map(pose, X, pc);
+    if (div_safe(pc[0], pc[1], pc[2])) {
+        const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
+        const double yz = div_rcp(z), yz2 = div_rcp(z_2);
+        const double x_z = div_by(x, z, yz), y_z = div_by(y, z, yz);
+        const double i_z = __fma_rn(__fma_rn(-z, yz, 1.0), yz, yz);   // div_by(1, z, yz)
+        er0 = (double)fo0 - (x_z * cam.fx + cam.cx);
+        er1 = (double)fo1 - (y_z * cam.fy + cam.cy);
+        double rho0, rho1;
+        huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
+        c[0] = rho0;
+        const double fx = cam.fx, fy = cam.fy;
+        const double xy_z2 = div_by(x * y, z_2, yz2);
+        double B[12];
+        B[0] = xy_z2 * fx;
+        B[1] = -(1 + div_by(x * x, z_2, yz2)) * fx;
+        B[2] = y_z * fx;
+        B[3] = -i_z * fx;    // -1. / z = -(1 / z)
+        B[4] = 0;
+        B[5] = div_by(x, z_2, yz2) * fx;
+        B[6] = (1 + div_by(y * y, z_2, yz2)) * fy;
+        B[7] = -xy_z2 * fy;  // -x * y / z_2 = -(x y / z_2)
+        B[8] = -x_z * fy;
+        B[9] = 0;
+        B[10] = -i_z * fy;
+        B[11] = div_by(y, z_2, yz2) * fy;
+        const double w = rho1 * s;
+        const double om0 = -(s * er0) * rho1, om1 = -(s * er1) * rho1;
+        int k = 1;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = 0; j <= i; j++, k++) {
+                const bool p0 = i == 4 || j == 4, q0 = i == 3 || j == 3;   // B(0, 4), B(1, 3) factors
+                const double P = (B[i] * w) * B[j], Q = (B[6 + i] * w) * B[6 + j];
+                c[k] = p0 ? (q0 ? 0.0 : Q) : (q0 ? P : P + Q);
+            }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            c[22 + i] = i == 3 ? B[3] * om0 : (i == 4 ? B[10] * om1 : B[i] * om0 + B[6 + i] * om1);
+        return;
+    }
+    {
+        const double u = pc[0] / pc[2] * cam.fx + cam.cx;
+        const double v = pc[1] / pc[2] * cam.fy + cam.cy;
+        er0 = (double)fo0 - u;
+        er1 = (double)fo1 - v;
+    }
     double rho0, rho1;
     huber2(er0 * (s * er0) + er1 * (s * er1), delta, rho0, rho1);
     c[0] = rho0;
@@ -291,7 +392,8 @@ __device__ inline void pose_edge_terms(const double* pose, const Cam& cam, doubl
 // edge order.  The sums -- and so every accept / reject decision and the
 // whole LM trajectory -- are then those of the sequential restatement
 // (oracle/ref_pose.cpp), at the cost of a 64-step dependent chain per group
-// (orbx_pose_set_exact; off by default).  An inactive edge contributes
+// (the default; orbx_pose_set_exact(ctx, 0) selects the reassociated sums).
+// An inactive edge contributes
 // +0.0: the sum starts at +0.0 and round-to-nearest never yields -0.0 from
 // it, so adding +0.0 leaves every bit as skipping the edge would.  The term
 // rows (57 KB per workgroup) sit beside the edge cache: one workgroup per CU.
@@ -311,8 +413,9 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     static_assert(kW == 1 || !kExact, "the exact sums run one wave per frame");
     constexpr int kT = 64 * kW;                          // threads striding one frame's edges
     constexpr int kFrames = kW == 1 ? kPoseThreads / 64 : 1;
-    // kExact keeps no edges in LDS: the term rows (57 KB) alone let two
-    // workgroups share a CU, so a wave's add chain overlaps another's terms
+    // kExact keeps no edges in LDS: the term rows (57 KB) and the active-edge
+    // lists (16 KB) let two workgroups share a CU, so a wave's add chain
+    // overlaps another's terms
     constexpr int kCache = kExact ? 1 : (kW == 1 ? kPoseLdsEdges : kPoseLdsEdgesWide);
     const int prob = kW == 1 ? blockIdx.x * (kPoseThreads / 64) + (threadIdx.x >> 6) : blockIdx.x;
     if (prob >= P) return;   // whole wavefront (kW > 1: whole workgroup)
@@ -347,6 +450,11 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     __shared__ float s_e[kFrames][6][kCache];
     __shared__ uint8_t s_f[kFrames][kCache];
     __shared__ double s_rows[kExact ? kPoseThreads / 64 : 1][kExact ? 64 : 1][28];   // per-edge terms
+    // kExact, robust rounds 2-4: the active edges (flag 0) in edge order, so
+    // the passes walk only them; an outlier adds +0.0 to every sum, so
+    // leaving it out changes no bit, and ~16 % fewer groups run
+    __shared__ uint16_t s_act[kExact ? kPoseThreads / 64 : 1][kExact ? kPoseActCap : 1];
+    int n_list = -1;   // -1: walk every edge (round 1, or a frame over kPoseActCap edges)
     // kW > 1: per-wave sums and the solver's broadcast, in two buffers used
     // in turn, so each exchange needs one barrier (a buffer is written again
     // only after the barrier of the exchange that used the other one, which
@@ -354,7 +462,7 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     __shared__ double s_red[2][kW][28];
     int rb = 0;
     const int wq = kW == 1 ? threadIdx.x >> 6 : 0;
-    const int nL = min(nE, kCache);
+    const int nL = kExact ? 0 : min(nE, kCache);
     // sums over the frame's threads, the same double on every thread: the
     // wave's DPP tree, then (kW > 1) the waves' sums in wave order
     auto frame_sums = [&](double* v, const int n) {
@@ -430,42 +538,64 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
     auto seq_sums = [&](int Q, auto&& terms) -> double {
         double acc = 0;
         double(*rows)[28] = s_rows[kExact ? wq : 0];
+        const int cnt = n_list >= 0 ? n_list : nE;
 #pragma unroll 1
-        for (int g = 0; g < nE; g += 64) {
-            const int a = g + lane;
+        for (int g = 0; g < cnt; g += 64) {
+            const int i = g + lane;
             double c[28];
-            bool act = false;
-            if (a < nL) {
-                act = !lfl[a];
-                if (act) terms(lox[a], loy[a], lis[a], lpx[a], lpy[a], lpz[a], c);
-            } else if (a < nE) {
-                act = !flag[a];
-                if (act) terms(ox[a], oy[a], isg[a], px[a], py[a], pz[a], c);
+            bool act;
+            int a;
+            if (n_list >= 0) {   // uniform
+                act = i < cnt;
+                a = act ? (int)s_act[kExact ? wq : 0][i] : 0;
+            } else {
+                a = i;
+                act = a < nE && !flag[a];
             }
-            for (int q = 0; q < Q; q++) rows[lane][q] = act ? c[q] : 0.0;
+            if (act) terms(ox[a], oy[a], isg[a], px[a], py[a], pz[a], c);
+            // stores in two branches, not 56 selects on every lane (the
+            // empty asm keeps the compiler from merging them back into
+            // selects); the zero branch runs only when some lane is idle
+            if (act) {
+                for (int q = 0; q < Q; q++) rows[lane][q] = c[q];
+            } else {
+                asm volatile("" ::: "memory");
+                for (int q = 0; q < Q; q++) rows[lane][q] = 0.0;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (lane < Q) {
-                // blocks of 8 rows (rows past the last edge are +0.0), the
-                // next block's loads issued before this block's adds
-                const int nb = (min(64, nE - g) + 7) >> 3;
-                double cur[8];
+                // all 64 rows in two register buffers of 16, each refilled
+                // right after its adds, so 16 loads are in flight while 16
+                // adds run (no copies between buffers; a third buffer would
+                // take the kernel past 256 VGPRs).  Rows past the frame's
+                // last edge hold +0.0, which leaves the sum's bits as they
+                // are (a frame's last group is nearly always full).  The
+                // sched_barriers keep the compiler's scheduler from sinking
+                // each load next to its add.
+                double A[16], Bf[16];
 #pragma unroll
-                for (int k = 0; k < 8; k++) cur[k] = rows[k][lane];
+                for (int k = 0; k < 16; k++) A[k] = rows[k][lane];
 #pragma unroll
-                for (int bk = 1; bk < 8; bk++) {
-                    if (bk >= nb) break;
-                    double nxt[8];
+                for (int k = 0; k < 16; k++) Bf[k] = rows[16 + k][lane];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int k = 0; k < 8; k++) nxt[k] = rows[8 * bk + k][lane];
+                for (int k = 0; k < 16; k++) acc += A[k];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int k = 0; k < 8; k++) acc += cur[k];
+                for (int k = 0; k < 16; k++) A[k] = rows[32 + k][lane];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int k = 0; k < 8; k++) cur[k] = nxt[k];
-                }
+                for (int k = 0; k < 16; k++) acc += Bf[k];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int k = 0; k < 8; k++) acc += cur[k];
+                for (int k = 0; k < 16; k++) Bf[k] = rows[48 + k][lane];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc += A[k];
+#pragma unroll
+                for (int k = 0; k < 16; k++) acc += Bf[k];
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -518,42 +648,17 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
                     for (int k = 0; k < 6; k++) bv[k] = lane_f64(sys_sum, 22 + k);
                 } else {
                 for_edges([&](float fo0, float fo1, float fis, float fx_, float fy_, float fz_) {
-                    const double X[3] = {(double)fx_, (double)fy_, (double)fz_};
-                    const double s = (double)fis;
-                    double pc[3], er0, er1;
-                    pose_edge_error(pose, X, (double)fo0, (double)fo1, cam, pc, er0, er1);
-                    const double c2 = er0 * (s * er0) + er1 * (s * er1);
-                    double rho0, rho1;
-                    huber2(c2, delta, rho0, rho1);
-                    chi += rho0;
-                    // EdgeSE3ProjectXYZ::linearizeOplus, pose block
-                    // (types_six_dof_expmap.cpp:384-420)
-                    const double x = pc[0], y = pc[1], z = pc[2], z_2 = z * z;
-                    const double fx = cam.fx, fy = cam.fy;
-                    double B[12];
-                    B[0] = x * y / z_2 * fx;
-                    B[1] = -(1 + (x * x / z_2)) * fx;
-                    B[2] = y / z * fx;
-                    B[3] = -1. / z * fx;
-                    B[4] = 0;
-                    B[5] = x / z_2 * fx;
-                    B[6] = (1 + y * y / z_2) * fy;
-                    B[7] = -x * y / z_2 * fy;
-                    B[8] = -x / z * fy;
-                    B[9] = 0;
-                    B[10] = -1. / z * fy;
-                    B[11] = y / z_2 * fy;
-                    // constructQuadraticForm, toNotFixed branch
-                    // (base_binary_edge.hpp:96-113)
-                    const double w = rho1 * s;
-                    const double om0 = -(s * er0) * rho1, om1 = -(s * er1) * rho1;
+                    // computeError, the Huber kernel, linearizeOplus's pose
+                    // block (types_six_dof_expmap.cpp:384-420) and
+                    // constructQuadraticForm's toNotFixed branch
+                    // (base_binary_edge.hpp:96-113): the edge's terms, added
+                    double c[28];
+                    pose_edge_terms(pose, cam, delta, fo0, fo1, fis, fx_, fy_, fz_, c);
+                    chi += c[0];
 #pragma unroll
-                    for (int i = 0; i < 6; i++) bv[i] += B[i] * om0 + B[6 + i] * om1;
-                    int k = 0;
+                    for (int k = 0; k < 21; k++) h[k] += c[1 + k];
 #pragma unroll
-                    for (int i = 0; i < 6; i++)
-#pragma unroll
-                        for (int j = 0; j <= i; j++, k++) h[k] += (B[i] * w) * B[j] + (B[6 + i] * w) * B[6 + j];
+                    for (int i = 0; i < 6; i++) bv[i] += c[22 + i];
                 });
                 {   // chi, H and b in one exchange (each sum in the same order as alone)
                     double v[28];
@@ -704,6 +809,27 @@ __global__ __launch_bounds__(kW == 1 ? kPoseThreads : 64 * kW) void k_pose_opt(c
         for (int a = nL + lane; a < nE; a += kT) flag[a] = classify(flag[a], ox[a], oy[a], isg[a], px[a], py[a], pz[a]);
         nBadOut = frame_sum_int(bad);
         n_active = frame_sum_int(act);
+        if constexpr (kExact) {
+            // the next round's active edges, in edge order (each lane reads
+            // the flags it has just written)
+            if (nE <= kPoseActCap) {
+                int base = 0;
+#pragma unroll 1
+                for (int c0 = 0; c0 < nE; c0 += 64) {
+                    const int a = c0 + lane;
+                    const bool on = a < nE && flag[a] == 0;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(on);
+                    const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (on) s_act[wq][base + r] = (uint16_t)a;
+                    base += __popcll(m);
+                }
+                n_list = base;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
         if (lane == 0) {
             out.iterations[it] = r_iters;
             out.trials[it] = r_trials;

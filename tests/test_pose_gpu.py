@@ -119,6 +119,23 @@ def test_pose_batch_mixed_sizes(ctx):
     assert np.array_equal(alone[0], batch[0][0]) and np.array_equal(alone[1], batch[0][1])
 
 
+def test_pose_batch_active_lists(ctx):
+    """The batch kernel walks each later robust round's active edges from a
+    list of at most 2048 (kPoseActCap) and every edge above that: frames
+    around and over the cap, mostly-outlier and outlier-free frames, bit for
+    bit the restatement."""
+    cases = [dict(n_kp=3000, seed=400, mp_frac=0.9, outlier_frac=0.2),   # ~2700 edges: no list
+             dict(n_kp=2200, seed=401, mp_frac=0.93, outlier_frac=0.1),  # ~2050 edges: at the cap
+             dict(n_kp=2000, seed=402, mp_frac=0.9, outlier_frac=0.15),
+             dict(n_kp=500, seed=403, outlier_frac=0.9),
+             dict(n_kp=700, seed=404, pix_noise=0.0, outlier_frac=0.0),
+             dict(n_kp=65, seed=405, outlier_frac=0.5)]
+    frames = [sp.make_frame(**c) for c in cases]
+    assert any(int(fr["has_mp"].sum()) > 2048 for fr in frames)
+    for fr, g in zip(frames, gpu_pose(ctx, frames)):
+        compare_exact(ref_pose(fr), g)
+
+
 def test_pose_fast_sums_batch_mixed_sizes(fast_ctx):
     rng = np.random.default_rng(0)
     frames = [sp.make_frame(n_kp=int(rng.integers(5, 1500)), seed=100 + k, outlier_frac=float(rng.uniform(0, 0.3)))
