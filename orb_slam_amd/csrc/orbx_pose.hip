@@ -945,6 +945,10 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
     __shared__ double s_sum[28];        // the pass's sums (written by wave 0 after the chain)
     __shared__ double s_sol[14];        // wave 0's step: xs, trial pose, ok
     __shared__ int s_cnt[kPxWaves][2];
+    // robust rounds 2-4: the active edges in edge order (an outlier adds
+    // +0.0 to every sum, so the chain skips it without changing a bit)
+    __shared__ uint16_t s_act[kPoseActCap];
+    int n_list = -1;   // -1: every edge (round 1, or over kPoseActCap edges)
     const int nL = min(nE, kPxCache);
     for (int a = tid; a < nL; a += kPxThreads) {
         s_e[0][a] = ox[a];
@@ -975,7 +979,8 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
     // s_sum[0, Q) for every thread
     auto seq_sums = [&](auto Qc, auto&& terms) {
         constexpr int Qn = decltype(Qc)::value;
-        const int G = (nE + 63) >> 6;   // groups of 64 edges (the last padded with +0.0 rows)
+        const int cnt = n_list >= 0 ? n_list : nE;
+        const int G = (cnt + 63) >> 6;   // groups of 64 edges (the last padded with +0.0 rows)
         if (wave > 0) {
 #pragma unroll 1
             for (int g = wave - 1; g < G; g += kPxWorkers) {
@@ -987,10 +992,16 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
                     __builtin_amdgcn_s_sleep(1);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 double* buf = s_ring + slot * kPxSlot;
-                const int a = g * 64 + lane;
+                const int i = g * 64 + lane;
                 double t[Qn];
                 float o0, o1, is, X, Y, Z;
-                const bool act = a < nE && edge(a, o0, o1, is, X, Y, Z);
+                bool act;
+                if (n_list >= 0) {   // uniform
+                    act = i < cnt;
+                    if (act) edge((int)s_act[i], o0, o1, is, X, Y, Z);
+                } else {
+                    act = i < nE && edge(i, o0, o1, is, X, Y, Z);
+                }
                 if (act) terms(o0, o1, is, X, Y, Z, t);
 #pragma unroll
                 for (int q = 0; q < Qn; q++) buf[q * kPxStride + lane] = act ? t[q] : 0.0;
@@ -1009,7 +1020,7 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
                     // the chain: blocks of 8 (the group's last edge rounded
                     // up), the next block's loads issued before this block's adds
                     const double* col = s_ring + slot * kPxSlot + lane * kPxStride;
-                    const int nb = min(8, (nE - g * 64 + 7) >> 3);
+                    const int nb = min(8, (cnt - g * 64 + 7) >> 3);
                     double cur[8];
 #pragma unroll
                     for (int k = 0; k < 8; k++) cur[k] = col[k];
@@ -1216,6 +1227,23 @@ __global__ __launch_bounds__(kPxThreads) void k_pose_exact_wide(const PoseHdr* _
             else flag[a] = nf;
         }
         block_counts(bad, act, nBadOut, n_active);
+        if (nE <= kPoseActCap) {   // uniform: the next round's list, by wave 0
+            if (wave == 0) {
+                int base = 0;
+#pragma unroll 1
+                for (int c0 = 0; c0 < nE; c0 += 64) {
+                    const int a = c0 + lane;
+                    const bool on = a < nE && (a < nL ? s_f[a] : flag[a]) == 0;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(on);
+                    const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (on) s_act[base + r] = (uint16_t)a;
+                    base += __popcll(m);
+                }
+            }
+            n_list = n_active;   // the same count (block_counts)
+            __syncthreads();
+        }
         PX_ACC(3, _px_t0);
         if (tid == 0) {
             out.iterations[it] = r_iters;
