@@ -513,7 +513,10 @@ LBA_FN void fx_split_scaled(double t, fx_t& hi, fx_t& lo, int& bad)
     bad |= !(fabs(t) < kFxMax);
     const double th = t + kFxMagic;                 // round(t) in the low mantissa bits
     const double r = t - (th - kFxMagic);           // exact, |r| <= 1/2
-    const double tl = __fma_rn(r, kFxLo, kFxMagic); // round(r * 2^40) likewise
+    // round(r * 2^40) likewise: the product is exact (a power of two), so the
+    // multiply-then-add rounds exactly as fma(r, 2^40, M) -- in two
+    // instructions, where the fma's accumulator needs M copied in first
+    const double tl = r * kFxLo + kFxMagic;
     const long long m = __double_as_longlong(kFxMagic);
     hi = (fx_t)(__double_as_longlong(th) - m);
     lo = (fx_t)(__double_as_longlong(tl) - m);
@@ -626,26 +629,47 @@ LBA_FN void schur_block(const double (&AD)[6], const double (&wBu)[12], const do
     const int ihi = upper ? pv : pu, ilo = upper ? pu : pv;
     const int base = pk(6 * ihi, 0) + 6 * ilo;
     if (pu != pv) {
+        // Storage element (s, t) of the lower block is the block's (s, t)
+        // when pu > pv and its (t, s) when pu < pv.  Both are
+        // fma(P1[s], W1[t], P0[s] W0[t]) with (P, W) = (Q, w B_v) for the
+        // first and (w B_v, Q) for the second -- wb_dot's value either way
+        // (products commute; its structural zeros w B(0, 4) = w B(1, 3) = 0
+        // enter here as +-0 terms, whose limbs are 0 all the same) -- so the
+        // operands are swapped once per block, each storage row is one base
+        // address and its six columns are immediate offsets (the per-element
+        // index arithmetic cost more than the element's own arithmetic).
+        double P0[6], P1[6], W0[6], W1[6];
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+        for (int k = 0; k < 6; k++) {
+            P0[k] = upper ? wBv[k] : Q0[k];
+            P1[k] = upper ? wBv[6 + k] : Q1[k];
+            W0[k] = upper ? Q0[k] : wBv[k];
+            W1[k] = upper ? Q1[k] : wBv[6 + k];
+        }
 #pragma unroll
-            for (int c = 0; c < 6; c++) {
-                const double t = wb_dot(wBv, c, Q0[r], Q1[r]);
-                const int rr = upper ? c : r, cc = upper ? r : c;
-                fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * rr + rr * (rr + 1) / 2 + cc, t, bad);
-            }
+        for (int s = 0; s < 6; s++) {
+            const int row = base + 6 * ihi * s + s * (s + 1) / 2;
+            fx_t* hr = hi + row;
+            fx_t* lr = lo + row;
+#pragma unroll
+            for (int t = 0; t < 6; t++) fx_add_scaled<kLds>(hr, lr, t, __fma_rn(P1[s], W1[t], P0[s] * W0[t]), bad);
+        }
     } else {
         // one edge (diag): the lower triangle of its own block; two edges of
         // one point on the same pose (not made by LocalBundleAdjustment,
         // handled for completeness): the block plus its transpose
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+        for (int r = 0; r < 6; r++) {
+            const int row = base + 6 * ihi * r + r * (r + 1) / 2;   // one base per row, immediate columns
+            fx_t* hr = hi + row;
+            fx_t* lr = lo + row;
 #pragma unroll
             for (int c = 0; c <= r; c++) {
                 double t = wb_dot(wBv, c, Q0[r], Q1[r]);
                 if (!diag) t += wb_dot(wBv, r, Q0[c], Q1[c]);
-                fx_add_scaled<kLds>(hi, lo, base + 6 * ihi * r + r * (r + 1) / 2 + c, t, bad);
+                fx_add_scaled<kLds>(hr, lr, c, t, bad);
             }
+        }
     }
 }
 
