@@ -1477,6 +1477,135 @@ LBA_FN bool grid_sync(const LbaSplit& X, unsigned& epoch)
     return s_ok != 0;
 }
 
+// k_lba_split's back-substitution, point update and errors with the per-edge
+// work spread over the workgroup's threads.  Per point (one thread, as
+// k_lba_iteration does it) the workgroup's longest point -- up to ~20 edges of
+// Jacobians in a row -- set the phase's length.  Here, in four steps:
+//  1. per free edge (a thread each) its W^T x term (point_backsub's loop body),
+//  2. per point (a thread each) the terms subtracted in edge order, Dinv, the
+//     update,
+//  3. per edge the error at the updated point (point_errors' loop body),
+//  4. per point the robust chi2 summed in edge order.
+// Every value and every sum is formed as point_backsub / point_errors form
+// it, so the bits are those of the per-point loop (and of k_lba_iteration).
+// The scratch is the staged Schur's LDS (free here): returns false, having
+// done nothing, when the workgroup's points or edges exceed it.
+constexpr int kBsPoints = 64;                                    // one wave's prefix
+constexpr int kBsEdges = (kSE * kSEd - 3 * kBsPoints) / 3;       // 3 doubles per edge
+template <class Rec>
+LBA_FN bool backsub_edgewise(LbaDev& P, const double* pz, const double* pbk, const double* xp, const int g, const int G,
+                             const bool ok2, const double lambda, const LbaSplit& X, double* es, int* pre)
+{
+    __shared__ int s_ne;
+    const int t = threadIdx.x;
+    const int np = g < P.nL ? (P.nL - g + G - 1) / G : 0;
+    if (np > kBsPoints) return false;   // uniform
+    double* npt = es + 3 * kBsEdges;    // the updated points
+    if (t < 64) {
+        const int c = t < np ? P.le_ptr[g + G * t + 1] - P.le_ptr[g + G * t] : 0;
+        const int inc = wave_inclusive_scan(c);
+        pre[t + 1] = inc;
+        if (t == 0) pre[0] = 0;
+        if (t == 63) s_ne = inc;
+    }
+    LBA_SYNC();
+    const int ne = s_ne;
+    if (ne > kBsEdges) return false;    // uniform
+    // the workgroup point of edge slot e: the last t with pre[t] <= e
+    auto point_of = [&](int e) {
+        int a = 0, b = np - 1;
+        while (a < b) {
+            const int m = (a + b + 1) >> 1;
+            if (pre[m] <= e) a = m;
+            else b = m - 1;
+        }
+        return a;
+    };
+    if (ok2)
+        for (int e = t; e < ne; e += kLbaThreads) {
+            const int tp = point_of(e), l = g + G * tp, j = P.le_ptr[l] + (e - pre[tp]);
+            const Rec r = load_rec<Rec>(P, j);
+            if (r.ph < 0) continue;
+            double pt[3];
+            load_point(P.point + 3 * P.iv_point[l], pt);
+            const double* zo = pbk + kPbk * r.ph;
+            const double* cam = pz + kPz * r.pose + 16;
+            double pc[3], A[6], B[12];
+            map_point(zo, pt, pc);
+            jac_point(cam, zo + 7, pc, A);
+            jac_pose(cam, pc, B);
+            const double w = P.ew[j];
+            const double* x6 = xp + 6 * r.ph;
+            double bx0 = 0, bx1 = 0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                bx0 += B[k] * x6[k];
+                bx1 += B[6 + k] * x6[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 3; k++) es[3 * e + k] = w * (A[k] * bx0 + A[3 + k] * bx1);
+        }
+    LBA_SYNC();
+    if (t < np) {
+        const int l = g + G * t;
+        double* pw = P.point + 3 * P.iv_point[l];
+        double pt[3];
+        load_point(pw, pt);
+        double s3[3] = {0.0, 0.0, 0.0};
+        if (ok2) {
+            const double* h = P.hl + 9 * l;
+            double cl[3] = {h[6], h[7], h[8]};
+            const int j0 = P.le_ptr[l] - pre[t];
+            for (int e = pre[t]; e < pre[t + 1]; e++) {
+                if (load_rec<Rec>(P, j0 + e).ph < 0) continue;
+#pragma unroll
+                for (int k = 0; k < 3; k++) cl[k] -= es[3 * e + k];
+            }
+            const double* d = P.dl + 12 * l;
+            double xl[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) xl[i] = d[3 * i] * cl[0] + d[3 * i + 1] * cl[1] + d[3 * i + 2] * cl[2];
+            double* bk = P.point_bk + 3 * l;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                bk[i] = pt[i];
+                s3[i] = xl[i] * (lambda * xl[i] + h[6 + i]);
+                pt[i] += xl[i];
+                pw[i] = pt[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            npt[3 * t + i] = pt[i];
+            X.sc_pt[3 * l + i] = s3[i];
+        }
+    }
+    LBA_SYNC();
+    for (int e = t; e < ne; e += kLbaThreads) {
+        const int tp = point_of(e), l = g + G * tp, j = P.le_ptr[l] + (e - pre[tp]);
+        const Rec r = load_rec<Rec>(P, j);
+        const double* z = pz + kPz * r.pose;
+        const double pt[3] = {npt[3 * tp], npt[3 * tp + 1], npt[3 * tp + 2]};
+        double pc[3], e0, e1;
+        map_point(z, pt, pc);
+        residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+        const int eo = P.e_orig[j];
+        P.err[2 * eo] = e0;
+        P.err[2 * eo + 1] = e1;
+        const double s = (double)r.isig;
+        double r0, r1;
+        huber(e0 * (s * e0) + e1 * (s * e1), P.huber_delta, &r0, &r1);
+        es[e] = r0;   // the terms of step 1 are dead: step 2 is behind the barrier
+    }
+    LBA_SYNC();
+    if (t < np) {
+        double part = 0;
+        for (int e = pre[t]; e < pre[t + 1]; e++) part += es[e];
+        X.chi_pt[g + G * t] = part;
+    }
+    return true;
+}
+
 // sum over l of v[l] in k_lba_iteration's order (thread t: l = t, t + 512,
 // ... sequentially, then the block sum); every workgroup gets the same bits
 LBA_FN double canon_sum(const double* v, int nL, DScratch& sc)
@@ -1732,7 +1861,10 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
             {   // --- back-substitution, point update, errors of this workgroup's points
                 const bool ok2 = st.ok2;
                 const double lambda = st.lambda;
-                for (int t = threadIdx.x;; t += kLbaThreads) {
+                // edge-parallel when the workgroup's points fit the scratch,
+                // else a thread per point (the same bits either way)
+                const bool edgewise = backsub_edgewise<Rec>(P, pz, pbk, xp, g, G, ok2, lambda, X, eA, etab);
+                for (int t = threadIdx.x; !edgewise; t += kLbaThreads) {
                     const int l = g + G * t;
                     if (l >= P.nL) break;
                     double* pw = P.point + 3 * P.iv_point[l];
