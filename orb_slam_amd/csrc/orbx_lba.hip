@@ -1606,6 +1606,89 @@ LBA_FN bool backsub_edgewise(LbaDev& P, const double* pz, const double* pbk, con
     return true;
 }
 
+// k_lba_split's linearisation of the workgroup's points (point_linearize) and,
+// in a pass's first iteration, their errors (point_errors), edge-parallel the
+// same way: per edge (a thread each) its 9 Hll / bl terms, its robust weight
+// and chi2 term -- computeError's values are the same in both functions, so
+// one residual serves both; per point (a thread each) the sums in edge order.
+// Returns false, having done nothing, when the workgroup's points or edges
+// exceed the staged Schur's LDS (10 doubles per edge).
+constexpr int kLinEdges = (kSE * kSEd) / 10;
+template <class Rec>
+LBA_FN bool linearize_edgewise(LbaDev& P, const double* pz, const int g, const int G, const bool errors,
+                               const LbaSplit& X, double* es, int* pre, double& bm, double& hlm)
+{
+    __shared__ int s_ne;
+    const int t = threadIdx.x;
+    const int np = g < P.nL ? (P.nL - g + G - 1) / G : 0;
+    if (np > kBsPoints) return false;   // uniform
+    if (t < 64) {
+        const int c = t < np ? P.le_ptr[g + G * t + 1] - P.le_ptr[g + G * t] : 0;
+        const int inc = wave_inclusive_scan(c);
+        pre[t + 1] = inc;
+        if (t == 0) pre[0] = 0;
+        if (t == 63) s_ne = inc;
+    }
+    LBA_SYNC();
+    const int ne = s_ne;
+    if (ne > kLinEdges) return false;   // uniform
+    double* chi = es + 9 * ne;          // per-edge robust chi2 terms
+    for (int e = t; e < ne; e += kLbaThreads) {
+        int a = 0, b = np - 1;   // the workgroup point of edge slot e
+        while (a < b) {
+            const int m = (a + b + 1) >> 1;
+            if (pre[m] <= e) a = m;
+            else b = m - 1;
+        }
+        const int l = g + G * a, j = P.le_ptr[l] + (e - pre[a]);
+        double pt[3];
+        load_point(P.point + 3 * P.iv_point[l], pt);
+        const Rec r = load_rec<Rec>(P, j);
+        const double* z = pz + kPz * r.pose;
+        double pc[3], e0, e1, A[6];
+        map_point(z, pt, pc);
+        residual(z + 16, pc, (double)r.ox, (double)r.oy, e0, e1);
+        if (errors) {
+            const int eo = P.e_orig[j];
+            P.err[2 * eo] = e0;
+            P.err[2 * eo + 1] = e1;
+        }
+        jac_point(z + 16, z + 7, pc, A);
+        const double sg = (double)r.isig;
+        double r0, r1;
+        huber(e0 * (sg * e0) + e1 * (sg * e1), P.huber_delta, &r0, &r1);
+        const double w = r1 * sg, om0 = -(sg * e0) * r1, om1 = -(sg * e1) * r1;
+        P.ew[j] = w;
+        double* o = es + 9 * e;
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int c = i; c < 3; c++) o[k++] = (A[i] * w) * A[c] + (A[3 + i] * w) * A[3 + c];
+#pragma unroll
+        for (int i = 0; i < 3; i++) o[6 + i] = A[i] * om0 + A[3 + i] * om1;
+        chi[e] = r0;
+    }
+    LBA_SYNC();
+    if (t < np) {
+        const int l = g + G * t;
+        double acc[9], part = 0;
+#pragma unroll
+        for (int v = 0; v < 9; v++) acc[v] = 0.0;
+        for (int e = pre[t]; e < pre[t + 1]; e++) {
+#pragma unroll
+            for (int v = 0; v < 9; v++) acc[v] += es[9 * e + v];
+            part += chi[e];
+        }
+#pragma unroll
+        for (int v = 0; v < 9; v++) P.hl[9 * l + v] = acc[v];
+        if (errors) X.chi_pt[l] = part;
+        bm = fmax(bm, fmax(fabs(acc[6]), fmax(fabs(acc[7]), fabs(acc[8]))));
+        hlm = fmax(hlm, fmax(fabs(acc[0]), fmax(fabs(acc[3]), fabs(acc[5]))));
+    }
+    return true;
+}
+
 // sum over l of v[l] in k_lba_iteration's order (thread t: l = t, t + 512,
 // ... sequentially, then the block sum); every workgroup gets the same bits
 LBA_FN double canon_sum(const double* v, int nL, DScratch& sc)
@@ -1679,7 +1762,10 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_split(LbaDev* probs, int it
         LBA_T0();
         {   // linearisation (and, in a pass's first iteration, computeActiveErrors)
             double hm = 0, bm = 0, hlm = 0;
-            for (int t = threadIdx.x;; t += kLbaThreads) {
+            // edge-parallel when the workgroup's points fit the scratch, else
+            // a thread per point (the same bits either way)
+            const bool edgewise = linearize_edgewise<Rec>(P, pz, g, G, it == 0, X, eA, etab, bm, hlm);
+            for (int t = threadIdx.x; !edgewise; t += kLbaThreads) {
                 const int l = g + G * t;
                 if (l >= P.nL) break;
                 if (it == 0) {
