@@ -883,7 +883,7 @@ int orbx_pose_fetch(orbx_ctx* ctx, orbx_pose_frame* frames, int32_t* n_inliers,
  * computed in parallel, accumulated edge by edge), so the whole LM
  * trajectory -- accept / reject of every trial, lambda, iterations -- and
  * the returned pose are the sequential reference's bit for bit, for every
- * batch size.  0 (opt-in, faster: ~1.25x one call, ~1.6x a batch): each
+ * batch size.  0 (opt-in, faster: about 1.03x one call, 1.4x a batch): each
  * wavefront sums its edges' terms lane-strided and then through a fixed DPP
  * tree -- deterministic, but in another order than g2o, so LM steps decided
  * on rounding noise (a converged pose restarted in a later robust round) may
