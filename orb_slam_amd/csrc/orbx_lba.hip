@@ -646,13 +646,21 @@ LBA_FN void schur_block(const double (&AD)[6], const double (&wBu)[12], const do
             W0[k] = upper ? Q0[k] : wBv[k];
             W1[k] = upper ? Q1[k] : wBv[6 + k];
         }
+        // odd lanes take the storage rows in the order 3, 4, 5, 0, 1, 2: lanes
+        // of a wave that land on the same block then add to different rows
+        // at the same instruction (fewer LDS address conflicts); the integer
+        // limb sums do not depend on the order
+        const bool rot = threadIdx.x & 1;
 #pragma unroll
-        for (int s = 0; s < 6; s++) {
-            const int row = base + 6 * ihi * s + s * (s + 1) / 2;
+        for (int k = 0; k < 6; k++) {
+            const int sa = k, sb = (k + 3) % 6;
+            const int s = rot ? sb : sa;
+            const double p0 = rot ? P0[sb] : P0[sa], p1 = rot ? P1[sb] : P1[sa];
+            const int row = base + 6 * ihi * s + (rot ? sb * (sb + 1) / 2 : sa * (sa + 1) / 2);
             fx_t* hr = hi + row;
             fx_t* lr = lo + row;
 #pragma unroll
-            for (int t = 0; t < 6; t++) fx_add_scaled<kLds>(hr, lr, t, __fma_rn(P1[s], W1[t], P0[s] * W0[t]), bad);
+            for (int t = 0; t < 6; t++) fx_add_scaled<kLds>(hr, lr, t, __fma_rn(p1, W1[t], p0 * W0[t]), bad);
         }
     } else {
         // one edge (diag): the lower triangle of its own block; two edges of
