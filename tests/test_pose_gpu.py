@@ -136,6 +136,32 @@ def test_pose_batch_active_lists(ctx):
         compare_exact(ref_pose(fr), g)
 
 
+def test_pose_degenerate_edge_takes_the_division_path(ctx):
+    """The per-edge terms divide through shared reciprocals only where the
+    camera-frame point keeps v_div_scale from rescaling (orbx_pose.hip
+    div_safe); a point on the camera plane (z = 0) takes the original
+    divisions, on one lane of a wave whose other lanes take the fast path.
+    Its infinite error makes every chi2 NaN, as in the restatement, so every
+    trial is rejected there too: the same counts, outliers and pose (chi2
+    compared NaN-aware), alone and in a batch."""
+    fr = sp.make_frame(n_kp=300, seed=500)
+    fr["Tcw"] = np.eye(4, dtype=np.float32)           # pc = X exactly (identity quaternion, t = 0)
+    k = int(np.nonzero(fr["has_mp"])[0][5])
+    fr["mp_xyz"][k] = [0.5, -0.25, 0.0]               # z = 0: outside div_safe
+    other = sp.make_frame(n_kp=400, seed=501)
+    ref = ref_pose(fr)
+    for got in (gpu_pose(ctx, [fr])[0], gpu_pose(ctx, [fr, other])[0]):
+        rT, rout, rn, rst = ref
+        gT, gout, gn, gst = got
+        assert gst.rounds == rst.rounds
+        assert list(gst.iterations) == list(rst.iterations)
+        assert list(gst.levenberg_trials) == list(rst.levenberg_trials)
+        assert list(gst.n_bad) == list(rst.n_bad)
+        assert np.array_equal(np.array(gst.chi2_final), np.array(rst.chi2_final), equal_nan=True)
+        assert np.array_equal(gout, rout) and gn == rn
+        assert np.array_equal(gT, rT, equal_nan=True)
+
+
 def test_pose_fast_sums_batch_mixed_sizes(fast_ctx):
     rng = np.random.default_rng(0)
     frames = [sp.make_frame(n_kp=int(rng.integers(5, 1500)), seed=100 + k, outlier_frac=float(rng.uniform(0, 0.3)))
